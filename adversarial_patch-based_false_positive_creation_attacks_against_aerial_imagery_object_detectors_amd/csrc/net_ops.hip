@@ -1,0 +1,218 @@
+// Data-movement ops of the Darknet graph (route / upsample / maxpool / layout),
+// forward and backward, NHWC fp32 with padded channel strides.
+// Reference: darknet_v3.py:61-113 (maxpool, upsample), 202-207 (route, shortcut).
+#include "common.h"
+
+namespace {
+__global__ __launch_bounds__(256) void slice_accum_k(const float* __restrict__ src, int ss, int so,
+                                                     float* __restrict__ dst, int ds, int doff,
+                                                     int64_t M, int C, int acc,
+                                                     const float* __restrict__ my, int ms) {
+  const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (t >= M * C) return;
+  const int64_t m = t / C;
+  const int c = (int)(t - m * C);
+  float v = src[m * ss + so + c];
+  float* d = dst + m * ds + doff + c;
+  if (acc) v += *d;
+  if (my) v *= po::leaky_grad(my[m * ms + c]);
+  *d = v;
+}
+
+__global__ __launch_bounds__(256) void up2_fwd_k(const float* __restrict__ src, int B, int H, int W,
+                                                 int C, int ss, float* __restrict__ dst, int ds,
+                                                 int doff) {
+  const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const int64_t tot = (int64_t)B * 2 * H * 2 * W * C;
+  if (t >= tot) return;
+  const int c = (int)(t % C);
+  int64_t p = t / C;                       // output pixel (b, y, x) at 2H x 2W
+  const int x = (int)(p % (2 * W));
+  p /= 2 * W;
+  const int y = (int)(p % (2 * H));
+  const int b = (int)(p / (2 * H));
+  const float v = src[(((int64_t)b * H + y / 2) * W + x / 2) * ss + c];   // nearest: floor(dst/2)
+  dst[(((int64_t)b * 2 * H + y) * 2 * W + x) * ds + doff + c] = v;
+}
+
+__global__ __launch_bounds__(256) void up2_bwd_k(const float* __restrict__ src, int ss, int so, int B,
+                                                 int H, int W, int C, float* __restrict__ dst, int ds,
+                                                 int acc, const float* __restrict__ my, int ms) {
+  const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const int64_t tot = (int64_t)B * H * W * C;
+  if (t >= tot) return;
+  const int c = (int)(t % C);
+  const int64_t p = t / C;
+  const int x = (int)(p % W);
+  const int y = (int)((p / W) % H);
+  const int b = (int)(p / ((int64_t)W * H));
+  const float* s0 = src + (((int64_t)b * 2 * H + 2 * y) * 2 * W + 2 * x) * ss + so + c;
+  const int64_t rs = (int64_t)2 * W * ss;
+  float v = (s0[0] + s0[ss]) + (s0[rs] + s0[rs + ss]);
+  float* d = dst + p * ds + c;
+  if (acc) v += *d;
+  if (my) v *= po::leaky_grad(my[p * ms + c]);
+  *d = v;
+}
+
+// k=2 max pool; stride 2 (no padding) or stride 1 over ZeroPad2d((0,1,0,1))
+__global__ __launch_bounds__(256) void maxpool2_fwd_k(const float* __restrict__ src, int B, int H, int W,
+                                                      int C, int Cp, int stride, int Ho, int Wo,
+                                                      float* __restrict__ dst, int8_t* __restrict__ am) {
+  const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const int64_t tot = (int64_t)B * Ho * Wo * Cp;
+  if (t >= tot) return;
+  const int c = (int)(t % Cp);
+  const int64_t p = t / Cp;
+  const int x = (int)(p % Wo);
+  const int y = (int)((p / Wo) % Ho);
+  const int b = (int)(p / ((int64_t)Wo * Ho));
+  if (c >= C) { dst[t] = 0.f; am[t] = 0; return; }
+  float best = 0.f;
+  int arg = -1;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const int yy = y * stride + (k >> 1), xx = x * stride + (k & 1);
+    // outside the source = the zero padding of ZeroPad2d (stride-1 case)
+    const float v = (yy < H && xx < W) ? src[(((int64_t)b * H + yy) * W + xx) * Cp + c] : 0.f;
+    if (arg < 0 || v > best || isnan(v)) { best = v; arg = k; }
+  }
+  dst[t] = best;
+  am[t] = (int8_t)arg;
+}
+
+// gather form: each source pixel sums the outputs whose argmax selected it
+__global__ __launch_bounds__(256) void maxpool2_bwd_k(const float* __restrict__ dd,
+                                                      const int8_t* __restrict__ am, int B, int H, int W,
+                                                      int C, int Cp, int stride, int Ho, int Wo,
+                                                      float* __restrict__ ds, int acc,
+                                                      const float* __restrict__ my) {
+  const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const int64_t tot = (int64_t)B * H * W * Cp;
+  if (t >= tot) return;
+  const int c = (int)(t % Cp);
+  const int64_t p = t / Cp;
+  const int x = (int)(p % W);
+  const int y = (int)((p / W) % H);
+  const int b = (int)(p / ((int64_t)W * H));
+  float v = 0.f;
+  if (c < C) {
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int dy = k >> 1, dx = k & 1;
+      const int ty = y - dy, tx = x - dx;
+      if (ty < 0 || tx < 0 || ty % stride || tx % stride) continue;
+      const int oy = ty / stride, ox = tx / stride;
+      if (oy >= Ho || ox >= Wo) continue;
+      const int64_t o = (((int64_t)b * Ho + oy) * Wo + ox) * Cp + c;
+      if (am[o] == k) v += dd[o];
+    }
+  }
+  if (acc) v += ds[t];
+  if (my) v *= po::leaky_grad(my[t]);
+  ds[t] = v;
+}
+
+__global__ __launch_bounds__(256) void nhwc2nchw_k(const float* __restrict__ s, int B, int H, int W, int C,
+                                                   int Cp, float* __restrict__ d) {
+  const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const int64_t tot = (int64_t)B * C * H * W;
+  if (t >= tot) return;
+  const int x = (int)(t % W);
+  const int y = (int)((t / W) % H);
+  const int c = (int)((t / ((int64_t)W * H)) % C);
+  const int b = (int)(t / ((int64_t)W * H * C));
+  d[t] = s[(((int64_t)b * H + y) * W + x) * Cp + c];
+}
+
+__global__ __launch_bounds__(256) void nchw2nhwc_k(const float* __restrict__ s, int B, int H, int W, int C,
+                                                   int Cp, float* __restrict__ d) {
+  const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const int64_t tot = (int64_t)B * H * W * Cp;
+  if (t >= tot) return;
+  const int c = (int)(t % Cp);
+  const int64_t p = t / Cp;
+  const int x = (int)(p % W);
+  const int y = (int)((p / W) % H);
+  const int b = (int)(p / ((int64_t)W * H));
+  d[t] = c < C ? s[(((int64_t)b * C + c) * H + y) * W + x] : 0.f;
+}
+}  // namespace
+
+extern "C" int po_slice_accum(const float* src, int src_stride, int src_off, float* dst, int dst_stride,
+                              int dst_off, int64_t M, int C, int accumulate, const float* mask_y,
+                              int mask_stride, po_stream_t s) {
+  PO_REQUIRE(src && dst && M >= 0 && C >= 0, "po_slice_accum: bad argument");
+  PO_REQUIRE(src_off + C <= src_stride && dst_off + C <= dst_stride, "po_slice_accum: slice exceeds stride");
+  if (M * C == 0) return PO_OK;
+  hipLaunchKernelGGL(slice_accum_k, dim3(po::ceil_div(M * C, 256)), dim3(256), 0, po::stream_of(s), src,
+                     src_stride, src_off, dst, dst_stride, dst_off, M, C, accumulate, mask_y, mask_stride);
+  return po::check_launch("po_slice_accum");
+}
+
+extern "C" int po_upsample2_fwd(const float* src, int B, int H, int W, int C, int src_stride, float* dst,
+                                int dst_stride, int dst_off, po_stream_t s) {
+  PO_REQUIRE(src && dst && C <= src_stride && dst_off + C <= dst_stride, "po_upsample2_fwd: bad argument");
+  const int64_t tot = (int64_t)B * 4 * H * W * C;
+  hipLaunchKernelGGL(up2_fwd_k, dim3(po::ceil_div(tot, 256)), dim3(256), 0, po::stream_of(s), src, B, H, W,
+                     C, src_stride, dst, dst_stride, dst_off);
+  return po::check_launch("po_upsample2_fwd");
+}
+
+extern "C" int po_upsample2_bwd(const float* src, int src_stride, int src_off, int B, int H, int W, int C,
+                                float* dst, int dst_stride, int accumulate, const float* mask_y,
+                                int mask_stride, po_stream_t s) {
+  PO_REQUIRE(src && dst && src_off + C <= src_stride && C <= dst_stride, "po_upsample2_bwd: bad argument");
+  const int64_t tot = (int64_t)B * H * W * C;
+  hipLaunchKernelGGL(up2_bwd_k, dim3(po::ceil_div(tot, 256)), dim3(256), 0, po::stream_of(s), src,
+                     src_stride, src_off, B, H, W, C, dst, dst_stride, accumulate, mask_y, mask_stride);
+  return po::check_launch("po_upsample2_bwd");
+}
+
+static inline void pool_out(int H, int W, int stride, int& Ho, int& Wo) {
+  if (stride == 2) { Ho = H / 2; Wo = W / 2; }       // MaxPool2d(2,2,padding=0)
+  else { Ho = H; Wo = W; }                            // ZeroPad2d((0,1,0,1)) + MaxPool2d(2,1)
+}
+
+extern "C" int po_maxpool2_fwd(const float* src, int B, int H, int W, int C, int Cp, int stride, float* dst,
+                               int8_t* argmax, po_stream_t s) {
+  PO_REQUIRE(src && dst && argmax && (stride == 1 || stride == 2) && C <= Cp, "po_maxpool2_fwd: bad argument");
+  int Ho, Wo;
+  pool_out(H, W, stride, Ho, Wo);
+  const int64_t tot = (int64_t)B * Ho * Wo * Cp;
+  hipLaunchKernelGGL(maxpool2_fwd_k, dim3(po::ceil_div(tot, 256)), dim3(256), 0, po::stream_of(s), src, B, H,
+                     W, C, Cp, stride, Ho, Wo, dst, argmax);
+  return po::check_launch("po_maxpool2_fwd");
+}
+
+extern "C" int po_maxpool2_bwd(const float* d_dst, const int8_t* argmax, int B, int H, int W, int C, int Cp,
+                               int stride, float* d_src, int accumulate, const float* mask_y,
+                               po_stream_t s) {
+  PO_REQUIRE(d_dst && argmax && d_src && (stride == 1 || stride == 2), "po_maxpool2_bwd: bad argument");
+  int Ho, Wo;
+  pool_out(H, W, stride, Ho, Wo);
+  const int64_t tot = (int64_t)B * H * W * Cp;
+  hipLaunchKernelGGL(maxpool2_bwd_k, dim3(po::ceil_div(tot, 256)), dim3(256), 0, po::stream_of(s), d_dst,
+                     argmax, B, H, W, C, Cp, stride, Ho, Wo, d_src, accumulate, mask_y);
+  return po::check_launch("po_maxpool2_bwd");
+}
+
+extern "C" int po_nhwc_to_nchw(const float* src, int B, int H, int W, int C, int Cp, float* dst,
+                               po_stream_t s) {
+  PO_REQUIRE(src && dst && C <= Cp, "po_nhwc_to_nchw: bad argument");
+  const int64_t tot = (int64_t)B * C * H * W;
+  if (!tot) return PO_OK;
+  hipLaunchKernelGGL(nhwc2nchw_k, dim3(po::ceil_div(tot, 256)), dim3(256), 0, po::stream_of(s), src, B, H, W,
+                     C, Cp, dst);
+  return po::check_launch("po_nhwc_to_nchw");
+}
+
+extern "C" int po_nchw_to_nhwc(const float* src, int B, int H, int W, int C, int Cp, float* dst,
+                               po_stream_t s) {
+  PO_REQUIRE(src && dst && C <= Cp, "po_nchw_to_nhwc: bad argument");
+  const int64_t tot = (int64_t)B * H * W * Cp;
+  if (!tot) return PO_OK;
+  hipLaunchKernelGGL(nchw2nhwc_k, dim3(po::ceil_div(tot, 256)), dim3(256), 0, po::stream_of(s), src, B, H, W,
+                     C, Cp, dst);
+  return po::check_launch("po_nchw_to_nhwc");
+}

@@ -1,0 +1,637 @@
+// Patch-side kernels for gfx950: median pool, placement parameters, the fused
+// augment + affine-warp + composite (forward and deterministic gather-form
+// backward), PatchApplier, and the NPS/TV/colour regularisers.
+//
+// Float operation order follows the reference's PyTorch ops (no FMA
+// contraction in this file) so the exact-zero composite test and the clamp
+// masks route gradients like the reference.
+#pragma clang fp contract(off)
+#include "common.h"
+#include <math.h>
+#include <string.h>
+
+namespace po {
+static thread_local char g_err[512] = {0};
+void set_error(const char* fmt, ...) {
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(g_err, sizeof(g_err), fmt, ap);
+  va_end(ap);
+}
+}  // namespace po
+
+extern "C" int po_abi_version(void) { return PO_ABI_VERSION; }
+extern "C" const char* po_last_error(void) { return po::g_err; }
+
+extern "C" int po_device_check(int device) {
+  hipError_t e = hipSetDevice(device);
+  if (e != hipSuccess) {
+    po::set_error("hipSetDevice(%d): %s", device, hipGetErrorString(e));
+    return PO_EHIP;
+  }
+  hipDeviceProp_t p;
+  e = hipGetDeviceProperties(&p, device);
+  if (e != hipSuccess) {
+    po::set_error("hipGetDeviceProperties: %s", hipGetErrorString(e));
+    return PO_EHIP;
+  }
+  if (strncmp(p.gcnArchName, "gfx950", 6) != 0) {
+    po::set_error("device %d is %s, this library is built for gfx950 only", device, p.gcnArchName);
+    return PO_EDEVICE;
+  }
+  return PO_OK;
+}
+
+// ------------------------------------------------------------------------
+// Median pool 7x7, reflect padding (median_pool.py:26-52)
+// ------------------------------------------------------------------------
+namespace {
+constexpr int MT = 16;             // output tile
+constexpr int MH = MT + 6;         // input tile with halo
+
+__device__ __forceinline__ int reflect_idx(int k, int n) {
+  return k < 0 ? -k : (k >= n ? 2 * (n - 1) - k : k);
+}
+
+__global__ __launch_bounds__(256) void median7_fwd_k(const float* __restrict__ x, int H, int W,
+                                                     float* __restrict__ y, int32_t* __restrict__ arg) {
+  __shared__ float tile[MH][MH + 1];
+  const int c = blockIdx.z, i0 = blockIdx.y * MT, j0 = blockIdx.x * MT;
+  const float* xc = x + (size_t)c * H * W;
+  for (int t = threadIdx.x; t < MH * MH; t += 256) {
+    int ti = t / MH, tj = t % MH;
+    int r = reflect_idx(min(max(i0 + ti - 3, -3), H + 2), H);
+    int q = reflect_idx(min(max(j0 + tj - 3, -3), W + 2), W);
+    tile[ti][tj] = xc[(size_t)r * W + q];
+  }
+  __syncthreads();
+  const int ty = threadIdx.x / MT, tx = threadIdx.x % MT;
+  const int i = i0 + ty, j = j0 + tx;
+  if (i >= H || j >= W) return;
+  float v[49];
+#pragma unroll
+  for (int a = 0; a < 49; ++a) v[a] = tile[ty + a / 7][tx + a % 7];
+  // rank selection: the 25th smallest (index 24) of 49; first window
+  // position (row-major) holding the median value is the argument.
+  int found = 48;
+#pragma unroll
+  for (int a = 48; a >= 0; --a) {
+    int less = 0, leq = 0;
+#pragma unroll
+    for (int b = 0; b < 49; ++b) {
+      less += v[b] < v[a];
+      leq += v[b] <= v[a];
+    }
+    if (less <= 24 && leq > 24) found = a;
+  }
+  float med = v[0];
+#pragma unroll
+  for (int a = 0; a < 49; ++a) med = (a == found) ? v[a] : med;
+  const int di = found / 7, dj = found % 7;
+  const int r = reflect_idx(i + di - 3, H), q = reflect_idx(j + dj - 3, W);
+  y[(size_t)c * H * W + (size_t)i * W + j] = med;
+  arg[(size_t)c * H * W + (size_t)i * W + j] = (int32_t)((size_t)c * H * W + (size_t)r * W + q);
+}
+
+// dx[p] = sum over outputs o within the 7x7 neighbourhood of p with
+// argidx[o] == p (reflection images of p fall inside that neighbourhood).
+__global__ __launch_bounds__(256) void median7_bwd_k(const float* __restrict__ dy,
+                                                     const int32_t* __restrict__ arg, int C, int H,
+                                                     int W, float* __restrict__ dx) {
+  const int64_t n = (int64_t)C * H * W;
+  int64_t p = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (p >= n) return;
+  const int c = (int)(p / ((int64_t)H * W));
+  const int rem = (int)(p - (int64_t)c * H * W);
+  const int r = rem / W, q = rem % W;
+  const size_t base = (size_t)c * H * W;
+  float acc = 0.f;
+  for (int i = max(0, r - 3); i <= min(H - 1, r + 3); ++i)
+    for (int j = max(0, q - 3); j <= min(W - 1, q + 3); ++j) {
+      size_t o = base + (size_t)i * W + j;
+      if (arg[o] == (int32_t)p) acc += dy[o];
+    }
+  dx[p] = acc;
+}
+}  // namespace
+
+extern "C" int po_median7_fwd(const float* x, int C, int H, int W, float* y, int32_t* argidx,
+                              po_stream_t s) {
+  PO_REQUIRE(x && y && argidx, "po_median7_fwd: null pointer");
+  PO_REQUIRE(C > 0 && H > 3 && W > 3, "po_median7_fwd: need C>0, H>3, W>3 (reflect pad 3), got %d %d %d", C, H, W);
+  dim3 grid(po::ceil_div(W, MT), po::ceil_div(H, MT), C);
+  hipLaunchKernelGGL(median7_fwd_k, grid, dim3(256), 0, po::stream_of(s), x, H, W, y, argidx);
+  return po::check_launch("po_median7_fwd");
+}
+
+extern "C" int po_median7_bwd(const float* dy, const int32_t* argidx, int C, int H, int W, float* dx,
+                              po_stream_t s) {
+  PO_REQUIRE(dy && argidx && dx, "po_median7_bwd: null pointer");
+  PO_REQUIRE(C > 0 && H > 3 && W > 3, "po_median7_bwd: bad shape");
+  int64_t n = (int64_t)C * H * W;
+  hipLaunchKernelGGL(median7_bwd_k, dim3(po::ceil_div(n, 256)), dim3(256), 0, po::stream_of(s), dy,
+                     argidx, C, H, W, dx);
+  return po::check_launch("po_median7_bwd");
+}
+
+// ------------------------------------------------------------------------
+// Placement parameters (load_data.py:453-509, 654-743)
+// ------------------------------------------------------------------------
+namespace {
+__global__ void patch_params_k(const float* __restrict__ lab, int B, int L,
+                               const float* __restrict__ angle, const float* __restrict__ ux,
+                               const float* __restrict__ uy, int do_rotate, int S, int P,
+                               float* __restrict__ theta, float* __restrict__ center,
+                               float* __restrict__ tsize) {
+  int b = blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= B) return;
+  const float* lb = lab + (size_t)b * L * 5;
+  // lab_transform: area = lab[:,:,3]*lab[:,:,4]; torch.max / torch.min over
+  // rows, first index on ties (load_data.py:464-467)
+  float vmax = lb[3] * lb[4], vmin = vmax;
+  int imax = 0, imin = 0;
+  for (int l = 1; l < L; ++l) {
+    float a = lb[l * 5 + 3] * lb[l * 5 + 4];
+    if (a > vmax) { vmax = a; imax = l; }
+    if (a < vmin) { vmin = a; imin = l; }
+  }
+  float sel2, sel3;
+  if (vmax > 0.99f) {                       // load_data.py:471-473
+    sel2 = 0.25f; sel3 = 0.25f;
+  } else {                                  // load_data.py:474-477
+    sel2 = (lb[imax * 5 + 2] + lb[imin * 5 + 2]) / 2.f;
+    sel3 = (lb[imax * 5 + 3] + lb[imin * 5 + 3]) / 2.f;
+  }
+  const float fS = (float)S;
+  float l2 = sel2 * fS, l3 = sel3 * fS;      // load_data.py:651-655
+  float h2 = l2 * 0.5f, h3 = l3 * 0.5f;      // .mul(1/pre_scale), SCALE_FACTOR=2
+  float ts = sqrtf(h2 * h2 + h3 * h3);       // load_data.py:662-663
+  float tx_ = fmaxf(ux[b], 0.2f);            // load_data.py:703
+  float ty_ = fminf(uy[b], 0.8f);            // load_data.py:706
+  center[2 * b + 0] = tx_ * fS;              // load_data.py:712-715
+  center[2 * b + 1] = ty_ * fS;
+  float scale = ts / (float)P;               // load_data.py:717
+  float tx = (-tx_ + 0.5f) * 2.f;            // load_data.py:726
+  float ty = (-ty_ + 0.5f) * 2.f;            // load_data.py:727
+  float a = do_rotate ? angle[b] : 0.f;
+  float sn = sinf(a), cs = cosf(a);
+  float* th = theta + 6 * b;                 // load_data.py:738-743
+  th[0] = cs / scale;
+  th[1] = sn / scale;
+  th[2] = tx * cs / scale + ty * sn / scale;
+  th[3] = -sn / scale;
+  th[4] = cs / scale;
+  th[5] = -tx * sn / scale + ty * cs / scale;
+  if (tsize) tsize[b] = ts;
+}
+}  // namespace
+
+extern "C" int po_patch_params(const float* lab, int B, int L, const float* angle, const float* ux,
+                               const float* uy, int do_rotate, int S, int P, float* theta,
+                               float* center, float* target_size, po_stream_t s) {
+  PO_REQUIRE(lab && ux && uy && theta && center, "po_patch_params: null pointer");
+  PO_REQUIRE(!do_rotate || angle, "po_patch_params: angle required when do_rotate");
+  PO_REQUIRE(B > 0 && L > 0 && S > 0 && P > 0, "po_patch_params: bad shape");
+  hipLaunchKernelGGL(patch_params_k, dim3(po::ceil_div(B, 64)), dim3(64), 0, po::stream_of(s), lab,
+                     B, L, angle, ux, uy, do_rotate, S, P, theta, center, target_size);
+  return po::check_launch("po_patch_params");
+}
+
+// ------------------------------------------------------------------------
+// Augment + affine warp + clamp*mask (+ composite)  (load_data.py:548-792, 820)
+// ------------------------------------------------------------------------
+namespace {
+struct WarpGeom {
+  int S, P, padL, padT;
+};
+
+// torch.linspace(-1,1,S) (scalar / CUDA formula) * (S-1) / S  (affine_grid base, align_corners=False)
+__device__ __forceinline__ float grid_base(int j, int S) {
+  const float step = 2.0f / (float)(S - 1);
+  float v = (j < S / 2) ? (-1.0f + step * (float)j) : (1.0f - step * (float)(S - 1 - j));
+  v = v * (float)(S - 1);
+  return v / (float)S;
+}
+
+// source coordinate (ix: column, iy: row) for output pixel (i, j)
+__device__ __forceinline__ void sample_coord(const float* th, int i, int j, int S, float& ix, float& iy) {
+  const float x = grid_base(j, S), y = grid_base(i, S);
+  const float gx = th[0] * x + th[1] * y + th[2];
+  const float gy = th[3] * x + th[4] * y + th[5];
+  const float fS = (float)S;
+  ix = ((gx + 1.f) * fS - 1.f) / 2.f;   // grid_sampler_unnormalize, align_corners=False
+  iy = ((gy + 1.f) * fS - 1.f) / 2.f;
+}
+
+__device__ __forceinline__ float aug_value(const float* __restrict__ mp, const float* __restrict__ nz,
+                                           float contrast, float bright, int ch, int pr, int pc, int P) {
+  const size_t o = ((size_t)ch * P + pr) * P + pc;
+  float v = mp[o] * contrast + bright + nz[o] * 0.1f;    // load_data.py:566-571
+  return fminf(fmaxf(v, 0.f), 1.f);                      // load_data.py:574
+}
+
+// Forward of one output pixel: adv_t[3] (clamped) and msk_t.  Returns false
+// if no neighbour lies inside the padded patch region (output exactly 0).
+__device__ __forceinline__ bool warp_pixel(const float* th, const WarpGeom& g, const float* mp,
+                                           const float* nz, float contrast, float bright, int i, int j,
+                                           float adv[3], float& msk, bool raw_in_range[3]) {
+  float ix, iy;
+  sample_coord(th, i, j, g.S, ix, iy);
+  const float fx = floorf(ix), fy = floorf(iy);
+  if (!(fx >= (float)(g.padL - 1) && fx <= (float)(g.padL + g.P - 1) &&
+        fy >= (float)(g.padT - 1) && fy <= (float)(g.padT + g.P - 1)))
+    return false;
+  const int x0 = (int)fx, y0 = (int)fy;
+  const float xs = (float)(x0 + 1), ys = (float)(y0 + 1);
+  const float w_nw = (xs - ix) * (ys - iy);
+  const float w_ne = (ix - (float)x0) * (ys - iy);
+  const float w_sw = (xs - ix) * (iy - (float)y0);
+  const float w_se = (ix - (float)x0) * (iy - (float)y0);
+  const int cx[4] = {x0, x0 + 1, x0, x0 + 1};
+  const int cy[4] = {y0, y0, y0 + 1, y0 + 1};
+  const float w[4] = {w_nw, w_ne, w_sw, w_se};
+  float a0 = 0.f, a1 = 0.f, a2 = 0.f, m = 0.f;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const int pr = cy[k] - g.padT, pc = cx[k] - g.padL;
+    if (pr >= 0 && pr < g.P && pc >= 0 && pc < g.P) {
+      a0 += aug_value(mp, nz, contrast, bright, 0, pr, pc, g.P) * w[k];
+      a1 += aug_value(mp, nz, contrast, bright, 1, pr, pc, g.P) * w[k];
+      a2 += aug_value(mp, nz, contrast, bright, 2, pr, pc, g.P) * w[k];
+      m += 1.f * w[k];
+    }
+  }
+  raw_in_range[0] = a0 >= 0.f && a0 <= 1.f;
+  raw_in_range[1] = a1 >= 0.f && a1 <= 1.f;
+  raw_in_range[2] = a2 >= 0.f && a2 <= 1.f;
+  adv[0] = fminf(fmaxf(a0, 0.f), 1.f);
+  adv[1] = fminf(fmaxf(a1, 0.f), 1.f);
+  adv[2] = fminf(fmaxf(a2, 0.f), 1.f);
+  msk = m;
+  return true;
+}
+
+__global__ __launch_bounds__(256) void warp_fwd_k(const float* __restrict__ img,
+                                                  const float* __restrict__ mp,
+                                                  const float* __restrict__ noise,
+                                                  const float* __restrict__ contrast,
+                                                  const float* __restrict__ bright,
+                                                  const float* __restrict__ theta, WarpGeom g, int mode,
+                                                  float* __restrict__ out) {
+  const int b = blockIdx.z;
+  const int i = blockIdx.y, j = blockIdx.x * 256 + threadIdx.x;
+  if (j >= g.S) return;
+  const size_t plane = (size_t)g.S * g.S;
+  const size_t o = (size_t)b * 3 * plane + (size_t)i * g.S + j;
+  float adv[3], msk;
+  bool rng[3];
+  const bool hit = warp_pixel(theta + 6 * b, g, mp, noise + (size_t)b * 3 * g.P * g.P, contrast[b],
+                              bright[b], i, j, adv, msk, rng);
+#pragma unroll
+  for (int ch = 0; ch < 3; ++ch) {
+    float v = hit ? adv[ch] * msk : 0.f;          // load_data.py:791-792
+    if (mode == 1) v = (v == 0.f) ? img[o + ch * plane] : v;   // load_data.py:820
+    out[o + ch * plane] = v;
+  }
+}
+
+// Backward phase A: per output pixel of the footprint,
+// gfac = d_out * [out != 0 (mode 1)] * msk_t * [0 <= adv_t <= 1]
+__global__ __launch_bounds__(256) void warp_bwd_a_k(const float* __restrict__ d_out,
+                                                    const float* __restrict__ mp,
+                                                    const float* __restrict__ noise,
+                                                    const float* __restrict__ contrast,
+                                                    const float* __restrict__ bright,
+                                                    const float* __restrict__ theta, WarpGeom g,
+                                                    int mode, float* __restrict__ gfac) {
+  const int b = blockIdx.z;
+  const int i = blockIdx.y, j = blockIdx.x * 256 + threadIdx.x;
+  if (j >= g.S) return;
+  const size_t plane = (size_t)g.S * g.S;
+  const size_t o = (size_t)b * 3 * plane + (size_t)i * g.S + j;
+  float adv[3], msk;
+  bool rng[3];
+  if (!warp_pixel(theta + 6 * b, g, mp, noise + (size_t)b * 3 * g.P * g.P, contrast[b], bright[b],
+                  i, j, adv, msk, rng))
+    return;   // never read by phase B
+#pragma unroll
+  for (int ch = 0; ch < 3; ++ch) {
+    const float out = adv[ch] * msk;
+    float gv = d_out[o + ch * plane];
+    if (mode == 1 && out == 0.f) gv = 0.f;
+    gv = gv * msk;                                 // d(clamp(adv)*msk)/d clamp(adv)
+    if (!rng[ch]) gv = 0.f;                        // clamp backward (inclusive bounds)
+    gfac[o + ch * plane] = gv;
+  }
+}
+
+// Backward phase B: per patch element (pr, pc), gather over images and over the
+// output pixels whose bilinear footprint covers padded-input pixel (pr+padT, pc+padL).
+__global__ __launch_bounds__(256) void warp_bwd_b_k(const float* __restrict__ gfac,
+                                                    const float* __restrict__ mp,
+                                                    const float* __restrict__ noise,
+                                                    const float* __restrict__ contrast,
+                                                    const float* __restrict__ bright,
+                                                    const float* __restrict__ theta, WarpGeom g,
+                                                    int B, float* __restrict__ d_mp) {
+  const int e = blockIdx.x * 256 + threadIdx.x;
+  if (e >= g.P * g.P) return;
+  const int pr = e / g.P, pc = e % g.P;
+  const int r = pr + g.padT, c = pc + g.padL;
+  const size_t plane = (size_t)g.S * g.S;
+  const float fS = (float)g.S, half = 0.5f - 0.5f * fS;
+  float d0 = 0.f, d1 = 0.f, d2 = 0.f;
+  for (int b = 0; b < B; ++b) {
+    const float* th = theta + 6 * b;
+    // pixel-space affine: ix = A00 j + A01 i + A02, iy = A10 j + A11 i + A12
+    const float A00 = th[0], A01 = th[1], A10 = th[3], A11 = th[4];
+    const float A02 = (th[0] + th[1]) * half + 0.5f * fS * th[2] + 0.5f * (fS - 1.f);
+    const float A12 = (th[3] + th[4]) * half + 0.5f * fS * th[5] + 0.5f * (fS - 1.f);
+    const float det = A00 * A11 - A01 * A10;
+    float jlo = 1e30f, jhi = -1e30f, ilo = 1e30f, ihi = -1e30f;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const float X = (float)c + ((k & 1) ? 1.f : -1.f) - A02;
+      const float Y = (float)r + ((k & 2) ? 1.f : -1.f) - A12;
+      const float jj = (A11 * X - A01 * Y) / det;
+      const float ii = (-A10 * X + A00 * Y) / det;
+      jlo = fminf(jlo, jj); jhi = fmaxf(jhi, jj);
+      ilo = fminf(ilo, ii); ihi = fmaxf(ihi, ii);
+    }
+    if (!(jhi >= -1.f && jlo <= fS && ihi >= -1.f && ilo <= fS)) continue;
+    const int j0 = max(0, (int)floorf(jlo) - 1), j1 = min(g.S - 1, (int)ceilf(jhi) + 1);
+    const int i0 = max(0, (int)floorf(ilo) - 1), i1 = min(g.S - 1, (int)ceilf(ihi) + 1);
+    float a0 = 0.f, a1 = 0.f, a2 = 0.f;
+    const float* gb = gfac + (size_t)b * 3 * plane;
+    for (int i = i0; i <= i1; ++i)
+      for (int j = j0; j <= j1; ++j) {
+        float ix, iy;
+        sample_coord(th, i, j, g.S, ix, iy);
+        const float fx = floorf(ix), fy = floorf(iy);
+        const int x0 = (int)fx, y0 = (int)fy;
+        const int dx = c - x0, dy = r - y0;
+        if (dx < 0 || dx > 1 || dy < 0 || dy > 1) continue;
+        const float xs = (float)(x0 + 1), ys = (float)(y0 + 1);
+        const float wx = dx ? (ix - (float)x0) : (xs - ix);
+        const float wy = dy ? (iy - (float)y0) : (ys - iy);
+        const float w = wx * wy;
+        const size_t o = (size_t)i * g.S + j;
+        a0 += w * gb[o];
+        a1 += w * gb[o + plane];
+        a2 += w * gb[o + 2 * plane];
+      }
+    // through clamp(adv*contrast + bright + noise) and * contrast, summed over images
+    const float cb = contrast[b], bb = bright[b];
+    const float* nz = noise + (size_t)b * 3 * g.P * g.P;
+    const float av[3] = {a0, a1, a2};
+    float dd[3];
+#pragma unroll
+    for (int ch = 0; ch < 3; ++ch) {
+      const size_t po_ = ((size_t)ch * g.P + pr) * g.P + pc;
+      const float pre = mp[po_] * cb + bb + nz[po_] * 0.1f;
+      dd[ch] = (pre >= 0.f && pre <= 1.f) ? av[ch] * cb : 0.f;
+    }
+    d0 += dd[0]; d1 += dd[1]; d2 += dd[2];
+  }
+  const size_t pp = (size_t)g.P * g.P;
+  d_mp[e] = d0;
+  d_mp[e + pp] = d1;
+  d_mp[e + 2 * pp] = d2;
+}
+
+WarpGeom make_geom(int S, int P) {
+  WarpGeom g;
+  g.S = S;
+  g.P = P;
+  const double pad = (S - P) / 2.0;      // load_data.py:534
+  g.padL = (int)(pad + 0.5);            // ConstantPad2d((int(pad+.5), int(pad), int(pad+.5), int(pad)))
+  g.padT = (int)(pad + 0.5);
+  return g;
+}
+}  // namespace
+
+extern "C" int po_warp_fwd(const float* img, const float* patch_mp, const float* noise,
+                           const float* contrast, const float* bright, const float* theta, int B,
+                           int S, int P, int mode, float* out, po_stream_t s) {
+  PO_REQUIRE(patch_mp && noise && contrast && bright && theta && out, "po_warp_fwd: null pointer");
+  PO_REQUIRE(mode == 0 || (mode == 1 && img), "po_warp_fwd: mode must be 0 or 1 (1 needs img)");
+  PO_REQUIRE(B > 0 && S > 1 && P > 0 && P <= S, "po_warp_fwd: bad shape B=%d S=%d P=%d", B, S, P);
+  dim3 grid(po::ceil_div(S, 256), S, B);
+  hipLaunchKernelGGL(warp_fwd_k, grid, dim3(256), 0, po::stream_of(s), img, patch_mp, noise, contrast,
+                     bright, theta, make_geom(S, P), mode, out);
+  return po::check_launch("po_warp_fwd");
+}
+
+extern "C" int po_warp_bwd(const float* d_out, const float* patch_mp, const float* noise,
+                           const float* contrast, const float* bright, const float* theta, int B,
+                           int S, int P, int mode, float* work, float* d_patch_mp, po_stream_t s) {
+  PO_REQUIRE(d_out && patch_mp && noise && contrast && bright && theta && work && d_patch_mp,
+             "po_warp_bwd: null pointer");
+  PO_REQUIRE(mode == 0 || mode == 1, "po_warp_bwd: mode must be 0 or 1");
+  PO_REQUIRE(B > 0 && S > 1 && P > 0 && P <= S, "po_warp_bwd: bad shape");
+  WarpGeom g = make_geom(S, P);
+  dim3 grid(po::ceil_div(S, 256), S, B);
+  hipLaunchKernelGGL(warp_bwd_a_k, grid, dim3(256), 0, po::stream_of(s), d_out, patch_mp, noise,
+                     contrast, bright, theta, g, mode, work);
+  int rc = po::check_launch("po_warp_bwd(a)");
+  if (rc) return rc;
+  hipLaunchKernelGGL(warp_bwd_b_k, dim3(po::ceil_div(P * P, 256)), dim3(256), 0, po::stream_of(s),
+                     work, patch_mp, noise, contrast, bright, theta, g, B, d_patch_mp);
+  return po::check_launch("po_warp_bwd(b)");
+}
+
+// ------------------------------------------------------------------------
+// PatchApplier on an explicit adv tensor (load_data.py:808-833)
+// ------------------------------------------------------------------------
+namespace {
+__global__ void apply_fwd_k(const float* __restrict__ img, const float* __restrict__ adv, int64_t n,
+                            float* __restrict__ out) {
+  int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i < n) {
+    float a = adv[i];
+    out[i] = (a == 0.f) ? img[i] : a;
+  }
+}
+__global__ void apply_bwd_k(const float* __restrict__ dout, const float* __restrict__ adv, int64_t n,
+                            float* __restrict__ dimg, float* __restrict__ dadv) {
+  int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i < n) {
+    float a = adv[i], g = dout[i];
+    if (dimg) dimg[i] = (a == 0.f) ? g : 0.f;
+    if (dadv) dadv[i] = (a == 0.f) ? 0.f : g;
+  }
+}
+}  // namespace
+
+extern "C" int po_apply_fwd(const float* img, const float* adv, int64_t n, float* out, po_stream_t s) {
+  PO_REQUIRE(img && adv && out && n >= 0, "po_apply_fwd: bad argument");
+  if (n == 0) return PO_OK;
+  hipLaunchKernelGGL(apply_fwd_k, dim3(po::ceil_div(n, 256)), dim3(256), 0, po::stream_of(s), img, adv,
+                     n, out);
+  return po::check_launch("po_apply_fwd");
+}
+
+extern "C" int po_apply_bwd(const float* d_out, const float* adv, int64_t n, float* d_img, float* d_adv,
+                            po_stream_t s) {
+  PO_REQUIRE(d_out && adv && n >= 0, "po_apply_bwd: bad argument");
+  if (n == 0 || (!d_img && !d_adv)) return PO_OK;
+  hipLaunchKernelGGL(apply_bwd_k, dim3(po::ceil_div(n, 256)), dim3(256), 0, po::stream_of(s), d_out,
+                     adv, n, d_img, d_adv);
+  return po::check_launch("po_apply_bwd");
+}
+
+// ------------------------------------------------------------------------
+// Regularisers: NPS (load_data.py:357-367), TV (404-411), colour (1729-1754)
+// ------------------------------------------------------------------------
+namespace {
+constexpr int RB = 256;        // threads per block
+constexpr int RMAXB = 1024;    // max partial blocks
+constexpr int NPART = 7;       // nps, tv1, tv2, s_rg, s_yb, s_rg2, s_yb2
+
+__device__ __forceinline__ void nps_pixel(const float* col, int ncol, float r, float g, float b,
+                                          float& dmin, int& kmin) {
+  dmin = 0.f;
+  kmin = -1;
+  for (int k = 0; k < ncol; ++k) {
+    float d0 = r - col[3 * k + 0] + 0.000001f;
+    float d1 = g - col[3 * k + 1] + 0.000001f;
+    float d2 = b - col[3 * k + 2] + 0.000001f;
+    float d = sqrtf(d0 * d0 + d1 * d1 + d2 * d2 + 0.000001f);
+    if (kmin < 0 || d < dmin) { dmin = d; kmin = k; }
+  }
+}
+
+__device__ __forceinline__ double block_sum(double v, double* sh) {
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+  const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
+  __syncthreads();
+  if (l == 0) sh[w] = v;
+  __syncthreads();
+  double t = 0.0;
+  if (threadIdx.x == 0)
+    for (int k = 0; k < RB / 64; ++k) t += sh[k];
+  return t;   // valid in thread 0
+}
+
+__global__ __launch_bounds__(RB) void reg_partial_k(const float* __restrict__ p, int P,
+                                                    const float* __restrict__ col, int ncol,
+                                                    double* __restrict__ part) {
+  __shared__ double sh[RB / 64];
+  const int n = P * P;
+  double acc[NPART] = {0, 0, 0, 0, 0, 0, 0};
+  const size_t pp = (size_t)n;
+  for (int e = blockIdx.x * RB + threadIdx.x; e < n; e += gridDim.x * RB) {
+    const int i = e / P, q = e % P;
+    const float r = p[e], g = p[e + pp], b = p[e + 2 * pp];
+    float dmin;
+    int kmin;
+    nps_pixel(col, ncol, r, g, b, dmin, kmin);
+    acc[0] += dmin;
+    for (int ch = 0; ch < 3; ++ch) {
+      const float* pc = p + ch * pp;
+      if (q + 1 < P) acc[1] += fabsf(pc[e + 1] - pc[e] + 0.000001f);
+      if (i + 1 < P) acc[2] += fabsf(pc[e + P] - pc[e] + 0.000001f);
+    }
+    const float rg = r - g, yb = 0.5f * (r + g) - b;
+    acc[3] += rg;
+    acc[4] += yb;
+    acc[5] += (double)rg * rg;
+    acc[6] += (double)yb * yb;
+  }
+  for (int k = 0; k < NPART; ++k) {
+    double t = block_sum(acc[k], sh);
+    if (threadIdx.x == 0) part[(size_t)k * RMAXB + blockIdx.x] = t;
+  }
+}
+
+// coef layout: [0]=g_nps/numel [1]=g_tv/numel [2]=g_col [3]=mu_rg [4]=mu_yb
+// [5]=d sigma/d x factor [6]=d mu term / d rg_i [7]=d mu term / d yb_i
+__global__ __launch_bounds__(RB) void reg_final_k(const double* __restrict__ part, int nblk, int P,
+                                                  const float* __restrict__ g3,
+                                                  float* __restrict__ out3, float* __restrict__ coef) {
+  __shared__ double sh[RB / 64];
+  __shared__ double tot[NPART];
+  for (int k = 0; k < NPART; ++k) {
+    double v = 0.0;
+    for (int bI = threadIdx.x; bI < nblk; bI += RB) v += part[(size_t)k * RMAXB + bI];
+    double t = block_sum(v, sh);
+    if (threadIdx.x == 0) tot[k] = t;
+  }
+  __syncthreads();
+  if (threadIdx.x != 0) return;
+  const double numel = 3.0 * P * P, N = (double)P * P;
+  const float nps = (float)(tot[0] / numel);
+  const float tv = (float)((tot[1] + tot[2]) / numel);
+  const double mu_rg = tot[3] / N, mu_yb = tot[4] / N;
+  const double var_rg = (tot[5] - tot[3] * mu_rg) / (N - 1.0);   // torch.var: unbiased
+  const double var_yb = (tot[6] - tot[4] * mu_yb) / (N - 1.0);
+  const float sigma = sqrtf((float)var_rg + (float)var_yb);
+  const float mu = sqrtf((float)(mu_rg * mu_rg) + (float)(mu_yb * mu_yb));
+  out3[0] = nps;
+  out3[1] = tv;
+  out3[2] = sigma + 0.3f * mu;
+  const float g_nps = g3 ? g3[0] : 0.f, g_tv = g3 ? g3[1] : 0.f, g_col = g3 ? g3[2] : 0.f;
+  coef[0] = g_nps / (float)numel;
+  coef[1] = g_tv / (float)numel;
+  coef[2] = g_col;
+  coef[3] = (float)mu_rg;
+  coef[4] = (float)mu_yb;
+  coef[5] = 0.5f / sigma * (2.f / (float)(N - 1.0));       // d sqrt(var_rg+var_yb) / d x_i = coef5*(x_i-mu)
+  coef[6] = 0.3f * (float)mu_rg / mu / (float)N;            // d 0.3*sqrt(mu_rg^2+mu_yb^2) / d rg_i
+  coef[7] = 0.3f * (float)mu_yb / mu / (float)N;
+}
+
+__device__ __forceinline__ float sgnf(float x) { return x > 0.f ? 1.f : (x < 0.f ? -1.f : 0.f); }
+
+__global__ __launch_bounds__(RB) void reg_grad_k(const float* __restrict__ p, int P,
+                                                 const float* __restrict__ col, int ncol,
+                                                 const float* __restrict__ coef,
+                                                 float* __restrict__ d) {
+  const int n = P * P;
+  const int e = blockIdx.x * RB + threadIdx.x;
+  if (e >= n) return;
+  const size_t pp = (size_t)n;
+  const int i = e / P, q = e % P;
+  const float r = p[e], g = p[e + pp], b = p[e + 2 * pp];
+  float dmin;
+  int k;
+  nps_pixel(col, ncol, r, g, b, dmin, k);
+  const float cn = coef[0], ct = coef[1], wc = coef[2];
+  const float rg = r - g, yb = 0.5f * (r + g) - b;
+  const float drg = coef[5] * (rg - coef[3]) + coef[6];
+  const float dyb = coef[5] * (yb - coef[4]) + coef[7];
+  const float dcol[3] = {wc * (drg + 0.5f * dyb), wc * (-drg + 0.5f * dyb), wc * (-dyb)};
+  const float pv[3] = {r, g, b};
+  for (int ch = 0; ch < 3; ++ch) {
+    const float* pc = p + ch * pp;
+    float gn = cn * (pv[ch] - col[3 * k + ch] + 0.000001f) / dmin;
+    float tvs = 0.f;
+    if (q + 1 < P) tvs -= sgnf(pc[e + 1] - pc[e] + 0.000001f);
+    if (q > 0) tvs += sgnf(pc[e] - pc[e - 1] + 0.000001f);
+    if (i + 1 < P) tvs -= sgnf(pc[e + P] - pc[e] + 0.000001f);
+    if (i > 0) tvs += sgnf(pc[e] - pc[e - P] + 0.000001f);
+    d[e + ch * pp] = gn + ct * tvs + dcol[ch];
+  }
+}
+}  // namespace
+
+extern "C" int po_regularisers(const float* patch, int P, const float* colors, int ncol, const float* g3,
+                               float* out3, float* d_patch, float* workspace, po_stream_t s) {
+  PO_REQUIRE(patch && colors && out3 && workspace, "po_regularisers: null pointer");
+  PO_REQUIRE(P > 1 && ncol > 0, "po_regularisers: bad shape");
+  PO_REQUIRE(!d_patch || g3, "po_regularisers: g3 required with d_patch");
+  const int n = P * P;
+  const int nblk = po::ceil_div(n, RB) < RMAXB ? po::ceil_div(n, RB) : RMAXB;
+  double* part = reinterpret_cast<double*>(workspace);                   // 7*1024 doubles
+  float* coef = workspace + 2 * NPART * RMAXB;                            // 8 floats
+  hipStream_t st = po::stream_of(s);
+  hipLaunchKernelGGL(reg_partial_k, dim3(nblk), dim3(RB), 0, st, patch, P, colors, ncol, part);
+  int rc = po::check_launch("po_regularisers(partial)");
+  if (rc) return rc;
+  hipLaunchKernelGGL(reg_final_k, dim3(1), dim3(RB), 0, st, part, nblk, P, g3, out3, coef);
+  rc = po::check_launch("po_regularisers(final)");
+  if (rc || !d_patch) return rc;
+  hipLaunchKernelGGL(reg_grad_k, dim3(po::ceil_div(n, RB)), dim3(RB), 0, st, patch, P, colors, ncol,
+                     coef, d_patch);
+  return po::check_launch("po_regularisers(grad)");
+}

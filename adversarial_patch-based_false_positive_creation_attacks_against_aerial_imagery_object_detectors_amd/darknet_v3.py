@@ -1,0 +1,687 @@
+"""Darknet (YOLOv3 family) — drop-in for reference ``darknet_v3.py`` whose
+forward and input-gradient run as HIP kernels on gfx950.
+
+Surface kept from the reference: ``create_modules`` (darknet_v3.py:9-100),
+``Upsample``, ``Mish``, ``YOLOLayer`` (identity on the training path,
+darknet_v3.py:144-169), ``Darknet`` with ``.blocks``, ``.module_list``,
+``.width``, ``.height``, ``.hyperparams``, ``.yolo_layers``,
+``load_darknet_weights`` (darknet_v3.py:223-281) and ``forward(x)`` returning
+the raw head tensors [B, 3*(5+C), h, w] (darknet_v3.py:195-220).
+
+Execution (``NetPlan``): one plan per (batch, height, width, device) holds
+every activation and gradient buffer in HBM (NHWC, channel stride padded to a
+multiple of 16).  Forward = per block one launch: ``po_conv`` implicit-GEMM
+on fp32 MFMA with BN folded into W/bias, LeakyReLU and the following
+``shortcut`` add fused into its epilogue; ``route`` of one layer is an alias,
+of several layers a channel-slice copy; ``upsample`` and ``maxpool`` are
+data-movement kernels.  Backward computes the input gradient only (dgrad, no
+weight gradients: the patch is the only trainable tensor): each conv's dgrad
+is the same implicit GEMM with transposed/flipped weights (stride 2 split into
+its 4 parity classes), and the LeakyReLU derivative of the producing layer is
+applied in the epilogue of the last gradient contribution to it.
+"""
+from itertools import chain
+
+import numpy as np
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+from . import _native as nat
+from .cfg import parse_model_config
+
+
+# ---------------------------------------------------------------------------
+# Module construction (parameter containers, as in the reference)
+# ---------------------------------------------------------------------------
+def create_modules(module_defs):
+    """Constructs module list of layer blocks from module configuration in
+    module_defs (pops the [net] block, darknet_v3.py:13-29)."""
+    hyperparams = module_defs.pop(0)
+    hyperparams.update({
+        "batch": int(hyperparams["batch"]),
+        "subdivisions": int(hyperparams["subdivisions"]),
+        "width": int(hyperparams["width"]),
+        "height": int(hyperparams["height"]),
+        "channels": int(hyperparams["channels"]),
+        "optimizer": hyperparams.get("optimizer"),
+        "momentum": float(hyperparams["momentum"]),
+        "decay": float(hyperparams["decay"]),
+        "learning_rate": float(hyperparams["learning_rate"]),
+        "burn_in": int(hyperparams["burn_in"]),
+        "max_batches": int(hyperparams["max_batches"]),
+        "policy": hyperparams["policy"],
+        "lr_steps": list(zip(map(int, hyperparams["steps"].split(",")),
+                             map(float, hyperparams["scales"].split(",")))),
+    })
+    assert hyperparams["height"] == hyperparams["width"], \
+        "Height and width should be equal! Non square images are padded with zeros."
+    output_filters = [hyperparams["channels"]]
+    module_list = nn.ModuleList()
+    for module_i, module_def in enumerate(module_defs):
+        modules = nn.Sequential()
+        t = module_def["type"]
+        if t == "convolutional":
+            bn = int(module_def["batch_normalize"])
+            filters = int(module_def["filters"])
+            k = int(module_def["size"])
+            conv = torch.nn.utils.skip_init(nn.Conv2d, output_filters[-1], filters, k,
+                                            stride=int(module_def["stride"]), padding=(k - 1) // 2,
+                                            bias=not bn)
+            with torch.no_grad():
+                conv.weight.zero_()
+                if conv.bias is not None:
+                    conv.bias.zero_()
+            modules.add_module(f"conv_{module_i}", conv)
+            if bn:
+                modules.add_module(f"batch_norm_{module_i}", nn.BatchNorm2d(filters, momentum=0.9, eps=1e-5))
+            if module_def["activation"] == "leaky":
+                modules.add_module(f"leaky_{module_i}", nn.LeakyReLU(0.1))
+            if module_def["activation"] == "mish":
+                modules.add_module(f"mish_{module_i}", Mish())
+        elif t == "maxpool":
+            k, s = int(module_def["size"]), int(module_def["stride"])
+            if k == 2 and s == 1:
+                modules.add_module(f"_debug_padding_{module_i}", nn.ZeroPad2d((0, 1, 0, 1)))
+            modules.add_module(f"maxpool_{module_i}", nn.MaxPool2d(kernel_size=k, stride=s, padding=int((k - 1) // 2)))
+            filters = output_filters[-1]
+        elif t == "upsample":
+            modules.add_module(f"upsample_{module_i}", Upsample(scale_factor=int(module_def["stride"]), mode="nearest"))
+            filters = output_filters[-1]
+        elif t == "route":
+            layers = [int(x) for x in module_def["layers"].split(",")]
+            filters = sum([output_filters[1:][i] for i in layers])
+            modules.add_module(f"route_{module_i}", nn.Sequential())
+        elif t == "shortcut":
+            filters = output_filters[1:][int(module_def["from"])]
+            modules.add_module(f"shortcut_{module_i}", nn.Sequential())
+        elif t == "yolo":
+            anchor_idxs = [int(x) for x in module_def["mask"].split(",")]
+            anchors = [int(x) for x in module_def["anchors"].split(",")]
+            anchors = [(anchors[i], anchors[i + 1]) for i in range(0, len(anchors), 2)]
+            anchors = [anchors[i] for i in anchor_idxs]
+            modules.add_module(f"yolo_{module_i}", YOLOLayer(anchors, int(module_def["classes"])))
+            filters = output_filters[-1]
+        else:
+            raise ValueError("unsupported darknet block type %r" % t)
+        module_list.append(modules)
+        output_filters.append(filters)
+    return hyperparams, module_list
+
+
+class Upsample(nn.Module):
+    """nearest upsample (darknet_v3.py:103-113)"""
+
+    def __init__(self, scale_factor, mode="nearest"):
+        super().__init__()
+        self.scale_factor = scale_factor
+        self.mode = mode
+
+    def forward(self, x):
+        return F.interpolate(x, scale_factor=self.scale_factor, mode=self.mode)
+
+
+class Mish(nn.Module):
+    """Mish activation (darknet_v3.py:116-123; unused by the yolov3 cfgs)."""
+
+    def forward(self, x):
+        return x * torch.tanh(F.softplus(x))
+
+
+class YOLOLayer(nn.Module):
+    """Detection layer: identity on the training path (darknet_v3.py:144-169)."""
+
+    def __init__(self, anchors, num_classes):
+        super().__init__()
+        self.num_anchors = len(anchors)
+        self.num_classes = num_classes
+        self.no = num_classes + 5
+        self.grid = torch.zeros(1)
+        anchors = torch.tensor(list(chain(*anchors))).float().view(-1, 2)
+        self.register_buffer("anchors", anchors)
+        self.register_buffer("anchor_grid", anchors.clone().view(1, -1, 1, 1, 2))
+        self.stride = None
+
+    def forward(self, x, img_size):
+        return x
+
+
+def _cp(c):
+    return (c + 15) // 16 * 16
+
+
+# ---------------------------------------------------------------------------
+# Execution plan
+# ---------------------------------------------------------------------------
+INPUT = -1
+
+
+class NetPlan:
+    """All buffers and launch lists of one (B, H, W, device) configuration."""
+
+    def __init__(self, net, B, H, W, device):
+        self.net, self.B, self.H, self.W, self.device = net, B, H, W, device
+        self.gen = 0
+        blocks = net.blocks
+        n = len(blocks)
+        self.n = n
+        self.lib = nat.load()
+        # ---- shapes, roots
+        shp = []                     # (H, W, C) per block
+        root = list(range(n))
+        srcs = [[] for _ in range(n)]
+        h, w, c = H, W, net.hyperparams["channels"]
+        prev = INPUT
+        self.heads = []              # block indices of yolo layers
+        fused = set()                # shortcut blocks fused into the previous conv
+        for i, d in enumerate(blocks):
+            t = d["type"]
+            if t == "convolutional":
+                p = net._conv_meta[i]
+                h = (h + 2 * p["pad"] - p["k"]) // p["stride"] + 1
+                w = (w + 2 * p["pad"] - p["k"]) // p["stride"] + 1
+                c = p["cout"]
+                srcs[i] = [prev]
+            elif t == "maxpool":
+                k, s = int(d["size"]), int(d["stride"])
+                if k != 2:
+                    raise NotImplementedError("maxpool size %d (only 2 on the yolov3 paths)" % k)
+                if s == 2:
+                    h, w = h // 2, w // 2
+                srcs[i] = [prev]
+            elif t == "upsample":
+                if int(d["stride"]) != 2:
+                    raise NotImplementedError("upsample stride %s" % d["stride"])
+                h, w = 2 * h, 2 * w
+                srcs[i] = [prev]
+            elif t == "route":
+                ls = [int(x) for x in d["layers"].split(",")]
+                ls = [l if l >= 0 else i + l for l in ls]
+                srcs[i] = [root[l] for l in ls]
+                h, w = shp[ls[0]][0], shp[ls[0]][1]
+                c = sum(shp[l][2] for l in ls)
+                for l in ls:
+                    assert shp[l][:2] == (h, w), "route of mismatched spatial sizes"
+                if len(ls) == 1:
+                    root[i] = root[ls[0]]
+            elif t == "shortcut":
+                f = int(d["from"])
+                f = f if f >= 0 else i + f
+                srcs[i] = [prev, root[f]]
+                if i > 0 and blocks[i - 1]["type"] == "convolutional" and root[i - 1] == i - 1:
+                    fused.add(i)
+            elif t == "yolo":
+                root[i] = root[i - 1]
+                srcs[i] = [prev]
+                self.heads.append(i)
+            shp.append((h, w, c))
+            prev = root[i]
+        self.shp, self.root, self.srcs, self.fused = shp, root, srcs, fused
+        self.cp = [_cp(s[2]) for s in shp]
+        dev = device
+        z = lambda i: torch.zeros(B, shp[i][0], shp[i][1], self.cp[i], device=dev)
+        self.act = [z(i) if root[i] == i else None for i in range(n)]
+        for i in range(n):
+            if self.act[i] is None:
+                self.act[i] = self.act[root[i]]
+        self.argmax = {i: torch.zeros(B, shp[i][0], shp[i][1], self.cp[i], dtype=torch.int8, device=dev)
+                       for i, d in enumerate(blocks) if d["type"] == "maxpool"}
+        first = blocks[0]
+        self.first_direct = (first["type"] == "convolutional" and net._conv_meta[0]["k"] == 3
+                             and net._conv_meta[0]["cin"] == 3 and net._conv_meta[0]["cout"] <= 64)
+        self.in_nhwc = None if self.first_direct else torch.zeros(B, H, W, 16, device=dev)
+        self._build_grad_plan()
+        self._build_ops()
+
+    # ---------------- gradient bookkeeping ----------------
+    def _build_grad_plan(self):
+        n, blocks, root = self.n, self.net.blocks, self.root
+        has = [False] * n
+        for j in range(n - 1, -1, -1):
+            t = blocks[j]["type"]
+            if t == "yolo":
+                has[root[j]] = True
+            elif root[j] == j and has[j]:
+                for s in self.srcs[j]:
+                    if s != INPUT:
+                        has[s] = True
+        self.has_grad = has
+        ncons = [0] * n
+        ext = [0] * n
+        for j in range(n):
+            t = blocks[j]["type"]
+            if t == "yolo":
+                ext[root[j]] += 1
+            elif t == "route" and len(self.srcs[j]) == 1:
+                continue
+            elif root[j] == j and has[j]:
+                for s in self.srcs[j]:
+                    if s != INPUT:
+                        ncons[s] += 1
+        self.ncons, self.ext = ncons, ext
+        dev, B = self.device, self.B
+        self.grad = [None] * n
+        for i in range(n):
+            if root[i] == i and has[i]:
+                self.grad[i] = torch.zeros(B, self.shp[i][0], self.shp[i][1], self.cp[i], device=dev)
+
+    def _leaky(self, r):
+        return (self.net.blocks[r]["type"] == "convolutional" and self.net._conv_meta[r]["act"] == "leaky")
+
+    # ---------------- launch lists ----------------
+    def _build_ops(self):
+        net, blocks, B = self.net, self.net.blocks, self.B
+        lib = self.lib
+        P = lambda t: nat.c_void_p(t.data_ptr()) if t is not None else None
+        fwd = []
+        for i, d in enumerate(blocks):
+            t = d["type"]
+            if t == "convolutional":
+                m = net._conv_meta[i]
+                wts = net._dev[i]
+                src = self.srcs[i][0]
+                y = self.act[i] if i not in self.fused else None
+                fuse_next = (i + 1) in self.fused
+                y_out = self.act[i]
+                if i == 0 and self.first_direct:
+                    args = (None, B, self.H, self.W, m["stride"], P(wts["w27"]), P(wts["bias"]), m["cout"],
+                            self.cp[i], 1 if m["act"] == "leaky" else 0, P(y_out))
+                    fwd.append(("po_conv_first_fwd", args, "img0"))
+                    assert not fuse_next
+                    continue
+                Hin, Win = (self.H, self.W) if src == INPUT else self.shp[src][:2]
+                cin_p = 16 if src == INPUT else self.cp[src]
+                desc = nat.po_conv_desc()
+                desc.B, desc.Hin, desc.Win, desc.Cin_p = B, Hin, Win, cin_p
+                desc.Hout, desc.Wout, desc.Cout_p = self.shp[i][0], self.shp[i][1], self.cp[i]
+                desc.Hg, desc.Wg = self.shp[i][0], self.shp[i][1]
+                desc.in_step, desc.out_step, desc.out_oy, desc.out_ox = m["stride"], 1, 0, 0
+                k, pad = m["k"], m["pad"]
+                desc.ntaps = k * k
+                for kh in range(k):
+                    for kw in range(k):
+                        desc.dh[kh * k + kw] = kh - pad
+                        desc.dw[kh * k + kw] = kw - pad
+                desc.N = self.cp[i]
+                desc.act = 1 if m["act"] == "leaky" else 0
+                desc.accumulate = 0
+                inp = self.in_nhwc if src == INPUT else self.act[src]
+                res = sum_out = None
+                if fuse_next:
+                    sc = blocks[i + 1]
+                    f = int(sc["from"])
+                    f = f if f >= 0 else (i + 1) + f
+                    res, sum_out = self.act[self.root[f]], self.act[i + 1]
+                args = (nat.ctypes.byref(desc), P(inp), P(wts["w"]), P(wts["bias"]), P(y_out), P(res),
+                        P(sum_out), None)
+                fwd.append(("po_conv", args, desc))
+            elif t == "shortcut":
+                if i in self.fused:
+                    continue
+                a, b = self.srcs[i]
+                M = B * self.shp[i][0] * self.shp[i][1]
+                C = self.shp[i][2]
+                fwd.append(("po_slice_accum", (P(self.act[a]), self.cp[a], 0, P(self.act[i]), self.cp[i], 0, M, C, 0,
+                                               None, 0), None))
+                fwd.append(("po_slice_accum", (P(self.act[b]), self.cp[b], 0, P(self.act[i]), self.cp[i], 0, M, C, 1,
+                                               None, 0), None))
+            elif t == "route":
+                if len(self.srcs[i]) == 1:
+                    continue
+                off = 0
+                M = B * self.shp[i][0] * self.shp[i][1]
+                for s in self.srcs[i]:
+                    C = self.shp[s][2]
+                    fwd.append(("po_slice_accum", (P(self.act[s]), self.cp[s], 0, P(self.act[i]), self.cp[i], off, M, C,
+                                                   0, None, 0), None))
+                    off += C
+            elif t == "upsample":
+                s = self.srcs[i][0]
+                hs, ws_, cs = self.shp[s]
+                fwd.append(("po_upsample2_fwd", (P(self.act[s]), B, hs, ws_, cs, self.cp[s], P(self.act[i]),
+                                                 self.cp[i], 0), None))
+            elif t == "maxpool":
+                s = self.srcs[i][0]
+                hs, ws_, cs = self.shp[s]
+                fwd.append(("po_maxpool2_fwd", (P(self.act[s]), B, hs, ws_, cs, self.cp[s], int(d["stride"]),
+                                                P(self.act[i]), P(self.argmax[i])), None))
+        self.fwd_ops = fwd
+
+        # backward
+        bwd = []
+        done = [0] * self.n
+        pre = []
+        root = self.root
+        for r in range(self.n):
+            if self.ext[r] and root[r] == r and self.has_grad[r]:
+                done[r] += 1        # the head gradient is copied in first (run_backward)
+
+        def contrib(r):
+            acc = 1 if done[r] > 0 else 0
+            final = (done[r] + 1 - (1 if self.ext[r] else 0)) == self.ncons[r]
+            mask = self.act[r] if (final and self._leaky(r)) else None
+            done[r] += 1
+            return acc, mask
+
+        for j in range(self.n - 1, -1, -1):
+            d = blocks[j]
+            t = d["type"]
+            if root[j] != j or not self.has_grad[j] or t == "yolo":
+                continue
+            G = self.grad[j]
+            if t == "convolutional":
+                m = net._conv_meta[j]
+                wts = net._dev[j]
+                src = self.srcs[j][0]
+                if src == INPUT:
+                    if self.first_direct:
+                        bwd.append(("po_conv_first_dgrad", (P(G), B, self.H, self.W, m["stride"], P(wts["w27"]),
+                                                            m["cout"], self.cp[j], "dimg"), None))
+                    else:
+                        for desc, wd in self._dgrad_descs(j, INPUT, 0):
+                            bwd.append(("po_conv", (nat.ctypes.byref(desc), P(G), P(wd), None, P(self.in_nhwc), None,
+                                                    None, None), desc))
+                        bwd.append(("po_nhwc_to_nchw", (P(self.in_nhwc), B, self.H, self.W, 3, 16, "dimg"), None))
+                    continue
+                acc, mask = contrib(src)
+                for desc, wd in self._dgrad_descs(j, src, acc):
+                    bwd.append(("po_conv", (nat.ctypes.byref(desc), P(G), P(wd), None, P(self.grad[src]), None, None,
+                                            P(mask)), desc))
+            elif t == "shortcut":
+                M = self.B * self.shp[j][0] * self.shp[j][1]
+                C = self.shp[j][2]
+                for s in self.srcs[j]:
+                    acc, mask = contrib(s)
+                    bwd.append(("po_slice_accum", (P(G), self.cp[j], 0, P(self.grad[s]), self.cp[s], 0, M, C, acc,
+                                                   P(mask), self.cp[s]), None))
+            elif t == "route":
+                off = 0
+                M = self.B * self.shp[j][0] * self.shp[j][1]
+                for s in self.srcs[j]:
+                    C = self.shp[s][2]
+                    acc, mask = contrib(s)
+                    bwd.append(("po_slice_accum", (P(G), self.cp[j], off, P(self.grad[s]), self.cp[s], 0, M, C, acc,
+                                                   P(mask), self.cp[s]), None))
+                    off += C
+            elif t == "upsample":
+                s = self.srcs[j][0]
+                acc, mask = contrib(s)
+                hs, ws_, cs = self.shp[s]
+                bwd.append(("po_upsample2_bwd", (P(G), self.cp[j], 0, B, hs, ws_, cs, P(self.grad[s]), self.cp[s],
+                                                 acc, P(mask), self.cp[s]), None))
+            elif t == "maxpool":
+                s = self.srcs[j][0]
+                acc, mask = contrib(s)
+                hs, ws_, cs = self.shp[s]
+                bwd.append(("po_maxpool2_bwd", (P(G), P(self.argmax[j]), B, hs, ws_, cs, self.cp[s], int(d["stride"]),
+                                                P(self.grad[s]), acc, P(mask)), None))
+        self.bwd_ops = bwd
+
+    def _dgrad_descs(self, j, src, acc):
+        """po_conv launches computing d(input of conv j) (one per stride parity class)."""
+        m = self.net._conv_meta[j]
+        s, k, pad = m["stride"], m["k"], m["pad"]
+        Hin, Win = (self.H, self.W) if src == INPUT else self.shp[src][:2]
+        cin_p = 16 if src == INPUT else self.cp[src]
+        out = []
+        for py in range(s):
+            for px in range(s):
+                Hg = (Hin - py + s - 1) // s
+                Wg = (Win - px + s - 1) // s
+                if Hg <= 0 or Wg <= 0:
+                    continue
+                taps = [(kh, kw) for kh in range(k) for kw in range(k)
+                        if (py + pad - kh) % s == 0 and (px + pad - kw) % s == 0]
+                wd = self.net._dgrad_weight(j, taps, cin_p, self.device)
+                desc = nat.po_conv_desc()
+                desc.B, desc.Hin, desc.Win, desc.Cin_p = self.B, self.shp[j][0], self.shp[j][1], self.cp[j]
+                desc.Hout, desc.Wout, desc.Cout_p = Hin, Win, cin_p
+                desc.Hg, desc.Wg = Hg, Wg
+                desc.in_step, desc.out_step, desc.out_oy, desc.out_ox = 1, s, py, px
+                desc.ntaps = len(taps)
+                for ti, (kh, kw) in enumerate(taps):
+                    desc.dh[ti] = (py + pad - kh) // s
+                    desc.dw[ti] = (px + pad - kw) // s
+                desc.N = cin_p
+                desc.act = 0
+                desc.accumulate = acc
+                out.append((desc, wd))
+        return out
+
+    # ---------------- execution ----------------
+    def run_forward(self, x):
+        """x: [B,3,H,W] contiguous CUDA float32 (NCHW).  Returns NHWC head buffers."""
+        self.gen += 1
+        st = nat.stream()
+        lib = self.lib
+        xp = nat.c_void_p(x.data_ptr())
+        if not self.first_direct:
+            nat.call("po_nchw_to_nhwc", xp, self.B, self.H, self.W, 3, 16, nat.c_void_p(self.in_nhwc.data_ptr()), st)
+        for name, args, _ in self.fwd_ops:
+            if name == "po_conv_first_fwd":
+                args = (xp,) + args[1:]
+            rc = getattr(lib, name)(*args, st)
+            if rc:
+                raise RuntimeError("%s failed: %s" % (name, nat.last_error()))
+        return [self.act[h] for h in self.heads]
+
+    def run_backward(self, d_heads, d_x):
+        """d_heads: NHWC gradient tensors of the head buffers (list, in head order);
+        d_x: [B,3,H,W] output buffer for the input gradient."""
+        st = nat.stream()
+        lib = self.lib
+        for hi, h in enumerate(self.heads):
+            r = self.root[h]
+            g = d_heads[hi].contiguous()
+            M = self.B * self.shp[r][0] * self.shp[r][1]
+            mask = self.act[r] if (self.ncons[r] == 0 and self._leaky(r)) else None
+            nat.call("po_slice_accum", nat.c_void_p(g.data_ptr()), self.cp[r], 0,
+                     nat.c_void_p(self.grad[r].data_ptr()), self.cp[r], 0, M, self.cp[r], 0,
+                     nat.c_void_p(mask.data_ptr()) if mask is not None else None, self.cp[r], st)
+        dxp = nat.c_void_p(d_x.data_ptr())
+        for name, args, _ in self.bwd_ops:
+            if args and args[-1] == "dimg":
+                args = args[:-1] + (dxp,)
+            rc = getattr(lib, name)(*args, st)
+            if rc:
+                raise RuntimeError("%s failed: %s" % (name, nat.last_error()))
+
+
+
+class _DarknetFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, plan, nchw):
+        heads = plan.run_forward(x.contiguous())
+        ctx.plan, ctx.gen, ctx.nchw = plan, plan.gen, nchw
+        if not nchw:
+            return tuple(h.clone() if plan.net.clone_heads else h.detach() for h in heads)
+        outs = []
+        for hb, h in zip(heads, plan.heads):
+            hh, ww, c = plan.shp[h]
+            o = torch.empty(plan.B, c, hh, ww, device=x.device)
+            nat.call("po_nhwc_to_nchw", nat.c_void_p(hb.data_ptr()), plan.B, hh, ww, c, plan.cp[h],
+                     nat.c_void_p(o.data_ptr()), nat.stream())
+            outs.append(o)
+        return tuple(outs)
+
+    @staticmethod
+    def backward(ctx, *grads):
+        plan = ctx.plan
+        if plan.gen != ctx.gen:
+            raise RuntimeError("Darknet activations were overwritten by a later forward of the same "
+                               "plan before backward (one forward per backward per batch shape)")
+        d_heads = []
+        for g, h in zip(grads, plan.heads):
+            hh, ww, c = plan.shp[h]
+            if g is None:
+                g = torch.zeros(plan.B, hh, ww, plan.cp[h], device=plan.device)
+            elif ctx.nchw:
+                gn = torch.empty(plan.B, hh, ww, plan.cp[h], device=plan.device)
+                nat.call("po_nchw_to_nhwc", nat.c_void_p(g.contiguous().data_ptr()), plan.B, hh, ww, c, plan.cp[h],
+                         nat.c_void_p(gn.data_ptr()), nat.stream())
+                g = gn
+            d_heads.append(g.contiguous())
+        d_x = torch.empty(plan.B, 3, plan.H, plan.W, device=plan.device)
+        plan.run_backward(d_heads, d_x)
+        return d_x, None, None
+
+
+class Darknet(nn.Module):
+    """YOLOv3 object detection model (darknet_v3.py:179-309), HIP execution."""
+
+    def __init__(self, config_path):
+        super().__init__()
+        self.blocks = parse_model_config(config_path)
+        self.width = int(self.blocks[0]["width"])
+        self.height = int(self.blocks[0]["height"])
+        self.hyperparams, self.module_list = create_modules(self.blocks)
+        self.yolo_layers = [layer[0] for layer in self.module_list if isinstance(layer[0], YOLOLayer)]
+        self.seen = 0
+        self.header_info = np.array([0, 0, 0, self.seen, 0], dtype=np.int32)
+        self.clone_heads = False
+        self._conv_meta = {}
+        cin = [int(self.hyperparams["channels"])]
+        for i, (d, mod) in enumerate(zip(self.blocks, self.module_list)):
+            if d["type"] == "convolutional":
+                conv = mod[0]
+                self._conv_meta[i] = {"cin": conv.in_channels, "cout": conv.out_channels,
+                                      "k": conv.kernel_size[0], "stride": conv.stride[0],
+                                      "pad": conv.padding[0], "bn": int(d["batch_normalize"]),
+                                      "act": d["activation"]}
+                if d["activation"] not in ("leaky", "linear"):
+                    self._conv_meta[i]["unsupported"] = d["activation"]
+        self._dev = None
+        self._dev_device = None
+        self._dgrad_cache = {}
+        self._plans = {}
+
+    # ---------------- weights ----------------
+    def load_darknet_weights(self, weights_path):
+        """Parses and loads the weights stored in 'weights_path' (darknet_v3.py:223-281)."""
+        with open(weights_path, "rb") as f:
+            header = np.fromfile(f, dtype=np.int32, count=5)
+            self.header_info = header
+            self.seen = header[3]
+            weights = np.fromfile(f, dtype=np.float32)
+        cutoff = 75 if "darknet53.conv.74" in weights_path else None
+        ptr = 0
+        for i, (module_def, module) in enumerate(zip(self.blocks, self.module_list)):
+            if i == cutoff:
+                break
+            if module_def["type"] != "convolutional":
+                continue
+            conv_layer = module[0]
+            with torch.no_grad():
+                if module_def["batch_normalize"]:
+                    bn = module[1]
+                    nb = bn.bias.numel()
+                    for t in (bn.bias, bn.weight, bn.running_mean, bn.running_var):
+                        t.copy_(torch.from_numpy(weights[ptr:ptr + nb]).view_as(t))
+                        ptr += nb
+                else:
+                    nb = conv_layer.bias.numel()
+                    conv_layer.bias.copy_(torch.from_numpy(weights[ptr:ptr + nb]).view_as(conv_layer.bias))
+                    ptr += nb
+                nw = conv_layer.weight.numel()
+                conv_layer.weight.copy_(torch.from_numpy(weights[ptr:ptr + nw]).view_as(conv_layer.weight))
+                ptr += nw
+        self.invalidate()
+        return ptr
+
+    def save_darknet_weights(self, path, cutoff=-1):
+        """Write the darknet .weights layout (the reference's version refers to an
+        undefined attribute, darknet_v3.py:293; this one works)."""
+        with open(path, "wb") as fp:
+            self.header_info[3] = self.seen
+            np.asarray(self.header_info, dtype=np.int32).tofile(fp)
+            pairs = list(zip(self.blocks, self.module_list))
+            if cutoff != -1:
+                pairs = pairs[:cutoff]
+            for module_def, module in pairs:
+                if module_def["type"] != "convolutional":
+                    continue
+                conv_layer = module[0]
+                if module_def["batch_normalize"]:
+                    bn = module[1]
+                    for t in (bn.bias, bn.weight, bn.running_mean, bn.running_var):
+                        t.detach().cpu().numpy().astype(np.float32).tofile(fp)
+                else:
+                    conv_layer.bias.detach().cpu().numpy().astype(np.float32).tofile(fp)
+                conv_layer.weight.detach().cpu().numpy().astype(np.float32).tofile(fp)
+
+    def invalidate(self):
+        """Drop device-side folded weights and plans (after a weight change)."""
+        self._dev = None
+        self._dgrad_cache = {}
+        self._plans = {}
+
+    def _folded(self, i):
+        """(W [Cout,Cin,k,k], bias [Cout]) with eval BN folded (float64 fold)."""
+        mod = self.module_list[i]
+        conv = mod[0]
+        W = conv.weight.detach().double().cpu()
+        if self._conv_meta[i]["bn"]:
+            bn = mod[1]
+            scale = bn.weight.detach().double().cpu() / torch.sqrt(bn.running_var.detach().double().cpu() + bn.eps)
+            bias = bn.bias.detach().double().cpu() - bn.running_mean.detach().double().cpu() * scale
+            W = W * scale.view(-1, 1, 1, 1)
+        else:
+            bias = conv.bias.detach().double().cpu()
+        return W, bias
+
+    def _prepare(self, device):
+        if self._dev is not None and self._dev_device == device:
+            return
+        for i, m in self._conv_meta.items():
+            if "unsupported" in m:
+                raise NotImplementedError("activation %r (block %d) is not on the HIP path" % (m["unsupported"], i))
+        self._dev, self._dgrad_cache, self._plans = {}, {}, {}
+        self._folded_cache = {}
+        for i, m in self._conv_meta.items():
+            W, bias = self._folded(i)
+            self._folded_cache[i] = W
+            cout, cin, k = m["cout"], m["cin"], m["k"]
+            cop, cip = _cp(cout), _cp(cin)
+            Wn = torch.zeros(cop, k * k, cip, dtype=torch.float64)
+            Wn[:cout, :, :cin] = W.permute(0, 2, 3, 1).reshape(cout, k * k, cin)
+            b = torch.zeros(cop, dtype=torch.float64)
+            b[:cout] = bias
+            ent = {"w": Wn.float().contiguous().to(device), "bias": b.float().to(device)}
+            if i == 0 and cin == 3 and k == 3:
+                ent["w27"] = W.reshape(cout, 27).float().contiguous().to(device)
+            self._dev[i] = ent
+        self._dev_device = device
+
+    def _dgrad_weight(self, j, taps, cin_p, device):
+        """[Cin_p][len(taps)][Cout_p] weights of one dgrad launch of conv j."""
+        key = (j, tuple(taps), cin_p)
+        if key not in self._dgrad_cache:
+            W = self._folded_cache[j]
+            m = self._conv_meta[j]
+            cout, cin = m["cout"], m["cin"]
+            Wd = torch.zeros(cin_p, len(taps), _cp(cout), dtype=torch.float64)
+            for ti, (kh, kw) in enumerate(taps):
+                Wd[:cin, ti, :cout] = W[:, :, kh, kw].t()
+            self._dgrad_cache[key] = Wd.float().contiguous().to(device)
+        return self._dgrad_cache[key]
+
+    def plan(self, B, H, W, device):
+        self._prepare(device)
+        key = (B, H, W, str(device))
+        if key not in self._plans:
+            self._plans[key] = NetPlan(self, B, H, W, device)
+        return self._plans[key]
+
+    # ---------------- forward ----------------
+    def forward(self, x):
+        """x [B,3,H,W] -> list of raw head tensors [B, 3*(5+C), h, w] (NCHW)."""
+        nat.ensure_device(x)
+        p = self.plan(x.size(0), x.size(2), x.size(3), x.device)
+        return list(_DarknetFn.apply(x, p, True))
+
+    def forward_nhwc(self, x):
+        """Training-path forward: returns the NHWC head buffers [B, h, w, Cp]
+        (Cp = padded channel stride, channel = anchor*(5+C) + field)."""
+        nat.ensure_device(x)
+        p = self.plan(x.size(0), x.size(2), x.size(3), x.device)
+        return list(_DarknetFn.apply(x, p, False)), p

@@ -1,0 +1,340 @@
+"""Patch transform / composite / regularisers — drop-in for the training-path
+classes of reference ``load_data.py`` backed by the HIP library.
+
+=====================  ==========================================  =========================
+class                  reference                                   HIP entry points
+=====================  ==========================================  =========================
+NPSCalculator          load_data.py:340-389                        po_regularisers
+TotalVariation         load_data.py:392-411                        po_regularisers
+PatchTransformer       load_data.py:414-794 (training placement)   po_median7_*, po_patch_params,
+                                                                   po_warp_fwd / po_warp_bwd
+PatchApplier           load_data.py:797-833                        po_apply_fwd / po_apply_bwd
+HasSusRGB              load_data.py:1724-1754                      po_regularisers
+DotaDataset            load_data.py:859-978 (host data loader)     (PIL / numpy, no GPU)
+=====================  ==========================================  =========================
+
+Randomness: the reference draws contrast/brightness/noise/angle from the CUDA
+RNG and target_x/target_y from the CPU RNG (load_data.py:548-707).  Here all
+draws are made on the device (``synthetic.draws_torch``) unless passed in
+explicitly with ``draws=`` (parity tests), so a step has no host<->device sync.
+"""
+import fnmatch
+import math
+import os
+
+import numpy as np
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+from . import _native as nat
+from .median_pool import MedianPool2d
+from .printability import PRINTABLE_RGB_30
+from . import synthetic
+
+SCALE_FACTOR = 2.          # load_data.py:32
+NOISE_FACTOR = 0.10        # load_data.py:436
+
+
+def read_image(path):
+    """PNG/JPG -> [3,H,W] float in [0,1] (load_data.py:35-47; ToTensor)."""
+    from PIL import Image
+    img = Image.open(path).convert("RGB")
+    return torch.from_numpy(np.asarray(img, dtype=np.uint8).copy()).permute(2, 0, 1).float().div_(255.0)
+
+
+def load_printability_colors(printability_file):
+    """[ncol,3] float32 colours from a reference-format file ('r,g,b' per
+    line; load_data.py:369-389 converts the decimal strings with np.float32)
+    or from ``builtin:30values``."""
+    if printability_file in (None, "builtin:30values"):
+        rows = PRINTABLE_RGB_30
+    else:
+        rows = []
+        with open(printability_file) as f:
+            for line in f:
+                line = line.strip()
+                if line and not line.startswith("#"):
+                    rows.append(tuple(line.split(",")))
+    return torch.tensor(np.asarray([[np.float32(float(v)) for v in r] for r in rows], dtype=np.float32))
+
+
+# ---------------------------------------------------------------------------
+# Regularisers (NPS / TV / colourfulness) as one autograd function
+# ---------------------------------------------------------------------------
+class _Regularisers(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, patch, colors):
+        nat.ensure_device(patch)
+        patch = patch.contiguous()
+        P = patch.size(-1)
+        out3 = torch.empty(3, device=patch.device)
+        ws = torch.empty(16384, device=patch.device)
+        nat.call("po_regularisers", nat.ptr(patch), P, nat.ptr(colors), colors.size(0), None,
+                 nat.ptr(out3), None, nat.ptr(ws), nat.stream())
+        ctx.save_for_backward(patch, colors)
+        return out3
+
+    @staticmethod
+    def backward(ctx, g3):
+        patch, colors = ctx.saved_tensors
+        g3 = g3.contiguous().float()
+        out3 = torch.empty(3, device=patch.device)
+        ws = torch.empty(16384, device=patch.device)
+        d = torch.empty_like(patch)
+        nat.call("po_regularisers", nat.ptr(patch), patch.size(-1), nat.ptr(colors), colors.size(0),
+                 nat.ptr(g3), nat.ptr(out3), nat.ptr(d), nat.ptr(ws), nat.stream())
+        return d, None
+
+
+def regularisers(patch, colors):
+    """(nps, tv, colour) of the raw [3,P,P] patch as a [3] tensor."""
+    return _Regularisers.apply(patch, colors)
+
+
+class NPSCalculator(nn.Module):
+    """Non-printability score (load_data.py:340-389)."""
+
+    def __init__(self, printability_file, patch_side):
+        super().__init__()
+        self.patch_side = patch_side
+        self.register_buffer("colors", load_printability_colors(printability_file))
+
+    @property
+    def printability_array(self):
+        """The reference's [ncol,3,side,side] array (expanded view)."""
+        s = self.patch_side
+        return self.colors.view(-1, 3, 1, 1).expand(-1, 3, s, s)
+
+    def get_printability_array(self, printability_file, side):
+        return load_printability_colors(printability_file).view(-1, 3, 1, 1).expand(-1, 3, side, side).contiguous()
+
+    def forward(self, adv_patch):
+        return regularisers(adv_patch, self.colors.to(adv_patch.device))[0]
+
+
+class TotalVariation(nn.Module):
+    """Total variation of the patch (load_data.py:392-411)."""
+
+    def __init__(self):
+        super().__init__()
+        self.register_buffer("colors", torch.tensor([[0.5, 0.5, 0.5]]))
+
+    def forward(self, adv_patch):
+        return regularisers(adv_patch, self.colors.to(adv_patch.device))[1]
+
+
+class HasSusRGB(nn.Module):
+    """Colourfulness loss sigma + 0.3*mu of (R-G, (R+G)/2-B) (load_data.py:1724-1754)."""
+
+    def __init__(self):
+        super().__init__()
+        self.register_buffer("colors", torch.tensor([[0.5, 0.5, 0.5]]))
+
+    def forward(self, RGB_img):
+        return regularisers(RGB_img, self.colors.to(RGB_img.device))[2]
+
+
+# ---------------------------------------------------------------------------
+# Patch placement and warp
+# ---------------------------------------------------------------------------
+def patch_params(lab_batch, img_size, P, draws, do_rotate=True):
+    """(theta [B,6], patch_center [B,2], target_size [B]) on the device."""
+    nat.ensure_device(lab_batch)
+    lab = lab_batch.contiguous().float()
+    B, L = lab.size(0), lab.size(1)
+    dev = lab.device
+    theta = torch.empty(B, 6, device=dev)
+    center = torch.empty(B, 2, device=dev)
+    tsize = torch.empty(B, device=dev)
+    angle = draws["angle"].contiguous().float() if do_rotate else None
+    nat.call("po_patch_params", nat.ptr(lab), B, L, nat.ptr(angle), nat.ptr(draws["ux"].contiguous().float()),
+             nat.ptr(draws["uy"].contiguous().float()), int(bool(do_rotate)), int(img_size), int(P),
+             nat.ptr(theta), nat.ptr(center), nat.ptr(tsize), nat.stream())
+    return theta, center, tsize
+
+
+class _Warp(torch.autograd.Function):
+    """Augment + warp + clamp*mask (mode 0) or + composite onto img (mode 1)."""
+
+    @staticmethod
+    def forward(ctx, mp, noise, contrast, bright, theta, img, S, mode):
+        mp = mp.contiguous()
+        B = theta.size(0)
+        P = mp.size(-1)
+        out = torch.empty(B, 3, S, S, device=mp.device)
+        nat.call("po_warp_fwd", nat.ptr(img.contiguous() if img is not None else None), nat.ptr(mp),
+                 nat.ptr(noise), nat.ptr(contrast), nat.ptr(bright), nat.ptr(theta), B, S, P, mode,
+                 nat.ptr(out), nat.stream())
+        ctx.save_for_backward(mp, noise, contrast, bright, theta)
+        ctx.S, ctx.mode = S, mode
+        return out
+
+    @staticmethod
+    def backward(ctx, d_out):
+        mp, noise, contrast, bright, theta = ctx.saved_tensors
+        d_out = d_out.contiguous()
+        work = torch.empty_like(d_out)
+        d_mp = torch.empty_like(mp)
+        nat.call("po_warp_bwd", nat.ptr(d_out), nat.ptr(mp), nat.ptr(noise), nat.ptr(contrast),
+                 nat.ptr(bright), nat.ptr(theta), theta.size(0), ctx.S, mp.size(-1), ctx.mode,
+                 nat.ptr(work), nat.ptr(d_mp), nat.stream())
+        return d_mp, None, None, None, None, None, None, None
+
+
+class PatchTransformer(nn.Module):
+    """Training-time patch transformer (load_data.py:414-794): median pool,
+    contrast U(0.8,1.2), brightness U(-0.1,0.1), noise 0.1*U(-1,1), clamp,
+    random rotation U(-pi,pi), scale from the selected label (cols 2,3 — Q2),
+    random centre (max(U,0.2), min(U,0.8) — Q4), bilinear affine warp,
+    clamp * mask."""
+
+    def __init__(self):
+        super().__init__()
+        self.min_contrast = 0.8
+        self.max_contrast = 1.2
+        self.min_brightness = -0.1
+        self.max_brightness = 0.1
+        self.noise_factor = NOISE_FACTOR
+        self.minangle = -180 / 180 * math.pi
+        self.maxangle = 180 / 180 * math.pi
+        self.medianpooler = MedianPool2d(7, same=True)
+        self.generator = None
+
+    def lab_transform(self, lab_batch_origin):
+        """[B,L,5] -> [B,1,5] (load_data.py:453-478): (max-area row + min-area row)/2,
+        or 0.25 everywhere when the max area exceeds 0.99."""
+        area = lab_batch_origin[:, :, 3] * lab_batch_origin[:, :, 4]
+        imax = torch.argmax(area, 1)
+        imin = torch.argmin(area, 1)
+        ar = torch.arange(lab_batch_origin.size(0), device=lab_batch_origin.device)
+        sel = (lab_batch_origin[ar, imax, :] + lab_batch_origin[ar, imin, :]) / 2.
+        empty = area.max(1).values > 0.99
+        sel = torch.where(empty[:, None], torch.full_like(sel, 0.25), sel)
+        return sel.unsqueeze(1)
+
+    def make_draws(self, B, P, device):
+        return synthetic.draws_torch(B, P, device, self.generator)
+
+    def _prep(self, adv_patch, lab_batch, img_size, do_rotate, draws):
+        nat.ensure_device(adv_patch)
+        mp = self.medianpooler(adv_patch.unsqueeze(0))[0]               # load_data.py:531-532
+        B, P = lab_batch.size(0), mp.size(-1)
+        if draws is None:
+            draws = self.make_draws(B, P, adv_patch.device)
+        theta, center, _ = patch_params(lab_batch, img_size, P, draws, do_rotate)
+        return mp, draws, theta, center
+
+    def forward(self, adv_patch, lab_batch, img_size, do_rotate=True, rand_loc=False, draws=None):
+        """-> (adv_batch_t [B,1,3,S,S], patch_center [B,2] = (x*S, y*S))."""
+        mp, d, theta, center = self._prep(adv_patch, lab_batch, img_size, do_rotate, draws)
+        out = _Warp.apply(mp, d["noise"].contiguous(), d["contrast"].contiguous(),
+                          d["bright"].contiguous(), theta, None, int(img_size), 0)
+        return out.unsqueeze(1), center
+
+    def forward_composite(self, adv_patch, lab_batch, img_batch, img_size, do_rotate=True, draws=None):
+        """Fused PatchTransformer + PatchApplier (the training step's path):
+        -> (p_img_batch [B,3,S,S], patch_center [B,2]) without materialising
+        adv_batch_t."""
+        mp, d, theta, center = self._prep(adv_patch, lab_batch, img_size, do_rotate, draws)
+        out = _Warp.apply(mp, d["noise"].contiguous(), d["contrast"].contiguous(),
+                          d["bright"].contiguous(), theta, img_batch.contiguous(), int(img_size), 1)
+        return out, center
+
+
+class _Apply(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, img, adv):
+        nat.ensure_device(adv)
+        img, adv = img.contiguous(), adv.contiguous()
+        out = torch.empty_like(adv)
+        nat.call("po_apply_fwd", nat.ptr(img), nat.ptr(adv), adv.numel(), nat.ptr(out), nat.stream())
+        ctx.save_for_backward(adv)
+        return out
+
+    @staticmethod
+    def backward(ctx, d_out):
+        (adv,) = ctx.saved_tensors
+        d_out = d_out.contiguous()
+        d_img = torch.empty_like(d_out) if ctx.needs_input_grad[0] else None
+        d_adv = torch.empty_like(d_out) if ctx.needs_input_grad[1] else None
+        nat.call("po_apply_bwd", nat.ptr(d_out), nat.ptr(adv), adv.numel(), nat.ptr(d_img),
+                 nat.ptr(d_adv), nat.stream())
+        return d_img, d_adv
+
+
+class PatchApplier(nn.Module):
+    """img = where(adv == 0, img, adv) for every patch slot (load_data.py:808-833)."""
+
+    def forward(self, img_batch, adv_batch):
+        for adv in torch.unbind(adv_batch, 1):
+            if img_batch.shape != adv.shape:
+                img_batch = img_batch.expand_as(adv)
+            img_batch = _Apply.apply(img_batch, adv)
+        return img_batch
+
+
+# ---------------------------------------------------------------------------
+# Host data path (load_data.py:859-978)
+# ---------------------------------------------------------------------------
+class DotaDataset(torch.utils.data.Dataset):
+    """DOTA-style image/label folder: square grey-127 pad, bilinear resize to
+    ``imgsize``, labels ``cls x y w h`` normalised and padded to ``max_lab``
+    rows with 1e-6; an empty label file becomes one row of ones(5)."""
+
+    def __init__(self, img_dir, lab_dir, max_lab, imgsize, shuffle=True):
+        names = fnmatch.filter(os.listdir(img_dir), "*.png") + fnmatch.filter(os.listdir(img_dir), "*.jpg")
+        n_labels = len(fnmatch.filter(os.listdir(lab_dir), "*.txt"))
+        assert len(names) == n_labels, "Number of images and number of labels does't match"
+        self.len = len(names)
+        self.img_dir, self.lab_dir, self.imgsize = img_dir, lab_dir, imgsize
+        self.img_names = names
+        self.shuffle = shuffle
+        self.img_paths = [os.path.join(img_dir, n) for n in names]
+        self.lab_paths = [os.path.join(lab_dir, n).replace(".jpg", ".txt").replace(".png", ".txt") for n in names]
+        self.max_n_labels = max_lab
+
+    def __len__(self):
+        return self.len
+
+    def __getitem__(self, idx):
+        from PIL import Image
+        assert idx <= len(self), "index range error"
+        image = Image.open(self.img_paths[idx]).convert("RGB")
+        lab_path = self.lab_paths[idx]
+        if os.path.getsize(lab_path):
+            label = np.loadtxt(lab_path)
+        else:
+            label = np.ones([5])
+        label = torch.from_numpy(label).float()
+        if label.dim() == 1:
+            label = label.unsqueeze(0)
+        image, label = self.pad_and_scale(image, label)
+        image = torch.from_numpy(np.asarray(image, dtype=np.uint8).copy()).permute(2, 0, 1).float().div_(255.0)
+        return image, self.pad_lab(label)
+
+    def pad_and_scale(self, img, lab):
+        from PIL import Image
+        w, h = img.size
+        if w == h:
+            padded = img
+        elif w < h:
+            padding = (h - w) / 2
+            padded = Image.new("RGB", (h, h), color=(127, 127, 127))
+            padded.paste(img, (int(padding), 0))
+            lab[:, [1]] = (lab[:, [1]] * w + padding) / h
+            lab[:, [3]] = (lab[:, [3]] * w / h)
+        else:
+            padding = (w - h) / 2
+            padded = Image.new("RGB", (w, w), color=(127, 127, 127))
+            padded.paste(img, (0, int(padding)))
+            lab[:, [2]] = (lab[:, [2]] * h + padding) / w
+            lab[:, [4]] = (lab[:, [4]] * h / w)
+        padded = padded.resize((self.imgsize, self.imgsize), Image.BILINEAR)
+        return padded, lab
+
+    def pad_lab(self, lab):
+        pad_size = self.max_n_labels - lab.shape[0]
+        if pad_size > 0:
+            return F.pad(lab, (0, 0, 0, pad_size), value=1e-6)
+        return lab

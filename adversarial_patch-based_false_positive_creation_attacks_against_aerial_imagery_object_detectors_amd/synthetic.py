@@ -1,0 +1,90 @@
+"""Seeded synthetic inputs of the reference's training shapes.
+
+There is no dataset and no pretrained checkpoint in this environment, so
+benches and parity tests run on synthetic data of the DOTA loader's shapes:
+
+* frames  [B,3,S,S] float32 = uint8 U{0..255}/255 (PNG quantisation)   seed 0
+* labels  [B,L,5]   rows [cls,x,y,w,h] normalised, padded to L=252 with 1e-6
+  (reference load_data.py:968-978); every 8th frame is an empty-label file,
+  i.e. one row of ones(5) (load_data.py:918-923)                      seed 1
+* patch   [3,P,P]   U[0,1) (train_patch.py:404-406)                    seed 2
+* draws   the PatchTransformer random draws (load_data.py:548-707)      seed 3
+
+All generators use numpy's PCG64 so the oracle and the HIP path see the
+same bytes.  ``draws_torch`` is the on-device generator the training loop
+uses (torch's Philox, seeded per step).
+"""
+import math
+
+import numpy as np
+import torch
+
+MAX_LAB = 252  # train_patch.py:116
+
+
+def _rng(seed):
+    return np.random.Generator(np.random.PCG64(seed))
+
+
+def frames(B, S, seed=0):
+    g = _rng(seed)
+    u8 = g.integers(0, 256, size=(B, 3, S, S), dtype=np.uint8)
+    return torch.from_numpy(u8.astype(np.float32) / np.float32(255.0))
+
+
+def labels(B, L=MAX_LAB, seed=1, n_classes=15):
+    g = _rng(seed)
+    out = np.full((B, L, 5), 1e-6, dtype=np.float32)
+    for b in range(B):
+        if b % 8 == 7:
+            out[b, 0, :] = 1.0          # empty label file -> np.ones([5])
+            continue
+        n = int(min(max(g.poisson(9.0), 1), 50))
+        out[b, :n, 0] = g.integers(0, n_classes, size=n)
+        out[b, :n, 1] = g.uniform(0.05, 0.95, size=n)
+        out[b, :n, 2] = g.uniform(0.05, 0.95, size=n)
+        out[b, :n, 3] = g.uniform(0.01, 0.20, size=n)
+        out[b, :n, 4] = g.uniform(0.01, 0.20, size=n)
+    return torch.from_numpy(out)
+
+
+def patch(P, seed=2):
+    return torch.from_numpy(_rng(seed).random((3, P, P), dtype=np.float32))
+
+
+def draws(B, P, seed=3):
+    g = _rng(seed)
+    f32 = np.float32
+    return {
+        "contrast": torch.from_numpy(g.uniform(0.8, 1.2, B).astype(f32)),
+        "bright": torch.from_numpy(g.uniform(-0.1, 0.1, B).astype(f32)),
+        "noise": torch.from_numpy(g.uniform(-1.0, 1.0, (B, 3, P, P)).astype(f32)),
+        "angle": torch.from_numpy(g.uniform(-math.pi, math.pi, B).astype(f32)),
+        "ux": torch.from_numpy(g.random(B, dtype=f32)),
+        "uy": torch.from_numpy(g.random(B, dtype=f32)),
+    }
+
+
+def draws_torch(B, P, device, generator=None):
+    """On-device draws with the reference's distributions (load_data.py:548-707)."""
+    kw = {"device": device, "generator": generator, "dtype": torch.float32}
+    return {
+        "contrast": torch.empty(B, device=device).uniform_(0.8, 1.2, generator=generator),
+        "bright": torch.empty(B, device=device).uniform_(-0.1, 0.1, generator=generator),
+        "noise": torch.empty(B, 3, P, P, device=device).uniform_(-1.0, 1.0, generator=generator),
+        "angle": torch.empty(B, device=device).uniform_(-math.pi, math.pi, generator=generator),
+        "ux": torch.rand(B, **kw),
+        "uy": torch.rand(B, **kw),
+    }
+
+
+def shard(t, rank, world):
+    """Contiguous equal shard of the global batch."""
+    n = t.size(0)
+    assert n % world == 0, "global batch %d not divisible by world size %d" % (n, world)
+    per = n // world
+    return t[rank * per:(rank + 1) * per]
+
+
+def shard_draws(d, rank, world):
+    return {k: shard(v, rank, world) for k, v in d.items()}

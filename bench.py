@@ -1,0 +1,228 @@
+"""Patch-optimisation images/s on synthetic DOTA-shaped batches (BASELINE.json metric).
+
+One step = one iteration of the reference's batch loop (train_patch.py:164-330):
+on-device draws -> median pool -> placement -> fused augment/warp/composite ->
+YOLOv3-DOTA forward -> cell loss + NPS/TV/colour -> backward (dgrad) ->
+[all-reduce of the patch gradient over RCCL when N > 1] -> Adam(amsgrad) + clamp.
+Inputs (frames, labels, patch) are resident in HBM before the timed region.
+
+    python bench.py [--gpus N --steps K --warmup W --batch B --config yolov3|tiny]
+
+N > 1 is launched by torchrun (one process per GPU, RCCL over xGMI); the
+global batch is N*B (weak scaling).
+"""
+import argparse
+import json
+import os
+import platform
+import sys
+import time
+
+import torch
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+import __graft_entry__ as ge  # noqa: E402
+
+PEAK_FP32_MFMA_TFLOPS = 157.3   # MI355X dense fp32 matrix peak (MI355X_MICROARCH.md)
+PEAK_HBM_GBS = 8000.0
+
+CONFIGS = {
+    # name: (cfg, S, P, default per-GPU batch)
+    "yolov3": ("builtin:yolov3-dota", 608, 224, 16),
+    "tiny": ("builtin:yolov3-tiny-dota", 416, 224, 256),
+}
+
+
+def conv_macs(net):
+    """Algorithmic MACs per image of the forward convolutions (logical channels)."""
+    plan_shapes = {}
+    h = w = net.height
+    total = 0
+    shp = []
+    for i, d in enumerate(net.blocks):
+        t = d["type"]
+        if t == "convolutional":
+            m = net._conv_meta[i]
+            h = (h + 2 * m["pad"] - m["k"]) // m["stride"] + 1
+            w = (w + 2 * m["pad"] - m["k"]) // m["stride"] + 1
+            total += h * w * m["cout"] * m["cin"] * m["k"] * m["k"]
+        elif t == "maxpool" and int(d["stride"]) == 2:
+            h, w = h // 2, w // 2
+        elif t == "upsample":
+            h, w = 2 * h, 2 * w
+        elif t == "route":
+            ls = [int(x) for x in d["layers"].split(",")]
+            l0 = ls[0] if ls[0] >= 0 else i + ls[0]
+            h, w = shp[l0]
+        shp.append((h, w))
+    return total
+
+
+def cpu_baseline(cfg, S, P, seconds_budget=25.0):
+    """The oracle (PyTorch-CPU restatement, weight grads on as in the
+    reference, no detect_anomaly) on the host cores: 1 warm-up + timed
+    iterations of a 1-image batch until ~seconds_budget."""
+    import oracle
+    sy, W, G, ld = ge._pkg("synthetic"), ge._pkg("weights"), ge._pkg("cfg_gen"), ge._pkg("load_data")
+    cores = min(16, os.cpu_count() or 1)
+    torch.set_num_threads(cores)
+    stream = W.synthesize(cfg, seed=4)
+    net = oracle.OracleDarknet(G.cfg_text(cfg), None, requires_grad=True)
+    import numpy as np
+    net.load_darknet_weights(stream)
+    for p in net.parameters():
+        pass
+    for p in net.params:
+        if p is not None:
+            for k in ("W", "b", "bn_b", "bn_w"):
+                if k in p:
+                    p[k].requires_grad_(True)
+    colors = ld.load_printability_colors("builtin:30values")
+    B = 1
+    img, lab, patch, dr = sy.frames(B, S, seed=100), sy.labels(B, seed=101), sy.patch(P, seed=102), sy.draws(B, P, seed=103)
+    oracle.train_step(patch, img, lab, dr, net, colors)           # warm-up
+    n, t0 = 0, time.time()
+    while True:
+        oracle.train_step(patch, img, lab, dr, net, colors)
+        n += 1
+        if time.time() - t0 > seconds_budget or n >= 8:
+            break
+    el = time.time() - t0
+    cpu = platform.processor() or platform.machine()
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    cpu = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    return {"value": n * B / el, "unit": "images/s", "cores": cores, "kind": "port",
+            "sample": "oracle train_step (PyTorch-CPU fp32, weight grads on), batch 1 @%d, %d timed iters "
+                      "after 1 warm-up, %.1fs, %d threads of %s" % (S, n, el, cores, cpu)}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--batch", type=int, default=None, help="per-GPU batch")
+    ap.add_argument("--config", default="yolov3", choices=sorted(CONFIGS))
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local)
+        torch.distributed.init_process_group("nccl", device_id=torch.device("cuda", local))
+    dev = torch.device("cuda", local)
+    cfg, S, P, Bdef = CONFIGS[args.config]
+    B = args.batch or Bdef
+
+    tp, pc, sy, W = ge._pkg("train_patch"), ge._pkg("patch_config"), ge._pkg("synthetic"), ge._pkg("weights")
+    wpath = pc.synthetic_weights_path(cfg.split(":")[-1])
+    if rank == 0:
+        W.ensure_synthetic(cfg, wpath)
+    if world > 1:
+        torch.distributed.barrier()
+
+    class _Cfg(pc.ReproducePaperObj):
+        def __init__(self):
+            super().__init__()
+            self.cfgfile = cfg
+            self.weightfile = wpath
+            self.batch_size = B
+
+    pc.patch_configs["_bench"] = _Cfg
+    tr = tp.PatchTrainer("_bench", device=dev, verbose=False, distributed=world > 1)
+
+    img = sy.frames(B, S, seed=1000 + rank).to(dev)
+    lab = sy.labels(B, seed=2000 + rank).to(dev)
+    patch = sy.patch(P, seed=2).to(dev).requires_grad_(True)
+    opt = tr.make_optimizer(patch)
+    gen = torch.Generator(device=dev)
+    gen.manual_seed(3 + rank)
+    tr.patch_transformer.generator = gen
+
+    net = tr.darknet_model
+    flops_per_img = 4.0 * conv_macs(net)      # fwd + dgrad
+    plan = net.plan(B, S, S, dev)
+
+    # per-step HIP events around the Darknet forward and backward (the conv stack)
+    ev = []
+    orig_f, orig_b = plan.run_forward, plan.run_backward
+
+    def rf(x):
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        r = orig_f(x)
+        e1.record()
+        ev.append((e0, e1))
+        return r
+
+    def rb(dh, dx):
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        orig_b(dh, dx)
+        e1.record()
+        ev.append((e0, e1))
+
+    plan.run_forward, plan.run_backward = rf, rb
+
+    for _ in range(args.warmup):
+        tr.step(patch, opt, img, lab)
+    torch.cuda.synchronize()
+    ev.clear()
+    if world > 1:
+        torch.distributed.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        terms = tr.step(patch, opt, img, lab)
+    torch.cuda.synchronize()
+    if world > 1:
+        torch.distributed.barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], device=dev)
+        torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
+        elapsed = float(t)
+    net_ms = sum(a.elapsed_time(b) for a, b in ev) / args.steps
+    ms_per_step = elapsed * 1000.0 / args.steps
+    value = world * B * args.steps / elapsed
+    achieved = flops_per_img * B / (net_ms * 1e-3) / 1e12
+
+    if rank == 0:
+        traffic = None
+        tfile = os.path.join(ROOT, "profiles", "traffic_%s_b%d.json" % (args.config, B))
+        if os.path.exists(tfile):
+            with open(tfile) as f:
+                traffic = json.load(f).get("hbm_bytes_per_step")
+        line = {
+            "metric": "patch-opt images/sec (608x608, YOLOv3-DOTA) at 1/2/4/8 MI355X" if args.config == "yolov3"
+            else "patch-opt images/sec (416x416, YOLOv3-tiny-15)",
+            "value": value, "unit": "images/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+            "ms_per_step": ms_per_step, "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+            "dtype": "fp32", "data": "synthetic (seeded DOTA-shaped frames/labels, synthetic calibrated weights)",
+            "config": {"workload": "%s S=%d P=%d batch=%d per GPU, global %d" % (cfg, S, P, B, B * world),
+                       "global_batch": B * world, "per_gpu_batch": B, "image_size": S, "patch_size": P,
+                       "parallelism": "dp%d" % world},
+            "roofline": {"bound": "mfma", "kernel": "po_conv implicit-GEMM (Darknet fwd + dgrad, all launches of a step)",
+                         "achieved": achieved, "peak": PEAK_FP32_MFMA_TFLOPS, "unit": "TFLOP/s",
+                         "frac": achieved / PEAK_FP32_MFMA_TFLOPS, "traffic": traffic,
+                         "algorithmic_flops_per_step": flops_per_img * B, "net_ms_per_step": net_ms},
+            "loss": float(terms["loss"]),
+        }
+        if world == 1 and not args.no_cpu_baseline:
+            line["cpu_baseline"] = cpu_baseline(cfg, S, P)
+        print(json.dumps(line))
+    if world > 1:
+        torch.distributed.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

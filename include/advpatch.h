@@ -1,0 +1,184 @@
+/*
+ * advpatch.h — C ABI of libadvpatch_hip.so, the MI355X (gfx950) hot path of the
+ * adversarial-patch training loop (reference: train_patch.py batch body,
+ * train_patch.py:157-330).
+ *
+ * The reference is pure Python over PyTorch (no FFI of its own);
+ * each entry below replaces the ATen kernels that one reference Python op
+ * invokes, and is bound from Python with ctypes.
+ *
+ * Conventions
+ *  - All tensor pointers are DEVICE pointers owned by the caller; the library
+ *    never allocates on the hot path.  float = IEEE fp32.
+ *  - Every entry is stream-ordered on the caller's hipStream_t (passed as
+ *    po_stream_t, an opaque pointer so this header needs no HIP headers) and
+ *    returns 0 on success or a negative PO_E* code; po_last_error() returns a
+ *    thread-local message for the last failure.
+ *  - Activations inside the network are NHWC with the channel stride padded
+ *    to a multiple of 16 ("Cp"); patch/image tensors are NCHW as in the
+ *    reference.
+ */
+#ifndef ADVPATCH_H
+#define ADVPATCH_H
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef void* po_stream_t;
+
+#define PO_OK 0
+#define PO_EINVAL -1   /* bad argument (shape, null pointer, unsupported config) */
+#define PO_EHIP -2     /* HIP runtime error */
+#define PO_EDEVICE -3  /* device is not gfx950 */
+
+#define PO_ABI_VERSION 1
+
+int po_abi_version(void);
+const char* po_last_error(void);
+/* Select the device and verify it is gfx950.  Returns PO_EDEVICE otherwise. */
+int po_device_check(int device);
+
+/* ---------------- patch-side ops (reference load_data.py / median_pool.py) ---------------- */
+
+/* MedianPool2d(7, same=True).forward: reflect pad 3, 7x7 window median.
+ * Replaces median_pool.py:46-52.  x,y [C,H,W]; argidx [C,H,W] = flat source
+ * index (c*H*W + r*W + q, reflection resolved) of the selected element:
+ * the first window position (row-major) holding the median value. */
+int po_median7_fwd(const float* x, int C, int H, int W, float* y, int32_t* argidx, po_stream_t s);
+/* dx = scatter-add of dy through argidx (deterministic gather form). */
+int po_median7_bwd(const float* dy, const int32_t* argidx, int C, int H, int W, float* dx, po_stream_t s);
+
+/* Per-image patch placement (load_data.py:453-509 lab_transform,
+ * 654-743 target_size/scale/theta, 693-715 target_x/y and patch_center).
+ * lab [B,L,5]; angle,ux,uy [B]; theta out [B,6]; center out [B,2]
+ * (column,row) pixels; target_size out [B] (may be NULL). */
+int po_patch_params(const float* lab, int B, int L, const float* angle, const float* ux,
+                    const float* uy, int do_rotate, int S, int P, float* theta, float* center,
+                    float* target_size, po_stream_t s);
+
+/* Augment (contrast/brightness/noise/clamp, load_data.py:548-574) + affine
+ * bilinear warp of patch and mask (affine_grid + grid_sample, align_corners
+ * False, zeros, load_data.py:745-749) + clamp*mask (791-792).
+ * mode 0: write adv_t [B,3,S,S] (PatchTransformer output, dim 1 squeezed).
+ * mode 1: also composite, out = where(adv_t==0, img, adv_t) (PatchApplier,
+ *         load_data.py:820) into `out` [B,3,S,S]; `img` required.
+ * patch_mp [3,P,P] (median-pooled patch), noise [B,3,P,P] U(-1,1) (x0.1 inside),
+ * contrast/bright [B], theta [B,6]. */
+int po_warp_fwd(const float* img, const float* patch_mp, const float* noise, const float* contrast,
+                const float* bright, const float* theta, int B, int S, int P, int mode,
+                float* out, po_stream_t s);
+/* Backward of po_warp_fwd w.r.t. patch_mp: d_patch_mp [3,P,P] (overwritten).
+ * d_out [B,3,S,S] is dL/d(out).  mode as in fwd (mode 1 applies the where()
+ * routing).  Deterministic: one thread per patch element gathers over images
+ * and over the output pixels whose bilinear footprint covers it. */
+int po_warp_bwd(const float* d_out, const float* patch_mp, const float* noise, const float* contrast,
+                const float* bright, const float* theta, int B, int S, int P, int mode,
+                float* work /* [B,3,S,S] scratch, may alias d_out */, float* d_patch_mp,
+                po_stream_t s);
+
+/* PatchApplier for an explicit adv tensor: out = where(adv==0, img, adv)
+ * (load_data.py:820); n elements. bwd: d_img = d_out*(adv==0), d_adv = d_out*(adv!=0). */
+int po_apply_fwd(const float* img, const float* adv, int64_t n, float* out, po_stream_t s);
+int po_apply_bwd(const float* d_out, const float* adv, int64_t n, float* d_img, float* d_adv,
+                 po_stream_t s);
+
+/* NPS (load_data.py:357-367), TV (404-411) and HasSusRGB colourfulness
+ * (1729-1754) of the raw patch [3,P,P], and the gradient
+ *   d_patch = g3[0] * dNPS/dp + g3[1] * dTV/dp + g3[2] * dCOL/dp
+ * g3 = DEVICE pointer to the upstream gradients of the three terms (so no
+ * host sync is needed; the train_patch.py:280-314 weights and
+ * torch.max(tv_loss, 0.1) are applied by the caller's autograd).
+ * colors [ncol,3].  out3 [3] = {nps, tv, colour};
+ * d_patch [3,P,P] is OVERWRITTEN (may be NULL: forward only). */
+int po_regularisers(const float* patch, int P, const float* colors, int ncol, const float* g3,
+                    float* out3, float* d_patch,
+                    float* workspace /* >= 16384 floats */, po_stream_t s);
+
+/* Loss head (train_patch.py:428-548 + 230-253):
+ * for each head h (NHWC [B,hw_h,hw_h,Cp], Cp>=60, channel a*20+f), each image b:
+ *   cell = floor(center/ (S/hw)) ; index = ix*hw + iy  (transposed)
+ *   obj[b, h*3+a] = sigmoid(head[b, index, a*20+4]); cls[b,h*3+a,c] = sigmoid(.. a*20+5+c)
+ * no_obj = 4*(1 - mean_b max_k obj)          (max: first index on ties)
+ * no_cls = objective 0: mean_b mean_k CE(cls[b,k,:], target)  (CE on probabilities)
+ *          objective 1: sum_b mean_k (max_c cls - cls[target])  (noCLS_loss_targeted,
+ *                       train_patch.py:550-577; max: first index on ties)
+ *          objective 2: 0 (untargeted)
+ * out2 [2] = {no_obj, no_cls}; obj_out [B,3*nheads], cls_out [B,3*nheads,15], cells [nheads,B]
+ * (each may be NULL).  d_heads (may be NULL): gradient of g2[0]*no_obj + g2[1]*no_cls
+ * (g2: DEVICE pointer, 2 floats)
+ * written at the selected cells only (other elements untouched — caller zeroes).
+ * flags: bit0 set if any cell index was out of range (clamped). */
+int po_cell_loss(const float* const* heads, const int* hw, int nheads, int Cp, int B, int S,
+                 const float* center, int target, int objective, const float* g2,
+                 float* const* d_heads, float* out2, float* obj_out, float* cls_out,
+                 int32_t* cells, int32_t* flags, po_stream_t s);
+
+/* ---------------- network ops (reference darknet_v3.py:37-100, 195-220) ---------------- */
+
+/* Tap list of an implicit-GEMM convolution launch.  For output pixel (b,i,j)
+ * of the launch grid and tap t the source pixel is
+ *   (b, i*in_step + dh[t], j*in_step + dw[t])  (zero outside [0,Hin)x[0,Win))
+ * and the destination is (b, i*out_step + out_oy, j*out_step + out_ox). */
+typedef struct po_conv_desc {
+  int B;
+  int Hin, Win, Cin_p;        /* source tensor (NHWC, channel stride Cin_p) */
+  int Hout, Wout, Cout_p;     /* destination tensor (NHWC, channel stride Cout_p) */
+  int Hg, Wg;                 /* launch grid (output pixels computed per image) */
+  int in_step, out_step, out_oy, out_ox;
+  int ntaps;
+  int dh[9], dw[9];
+  int N;                      /* output channels computed (<= Cout_p, multiple of 16) */
+  int act;                    /* 0 linear, 1 leaky(0.1) */
+  int accumulate;             /* 1: out = acc + out_prev (dst read) */
+} po_conv_desc;
+
+/* out[m][n] = act(sum_k A[m][k] * W[n][k] + bias[n]) (+ residual[m][n]);
+ * W [N][ntaps][Cin_p] (BN folded on the host).  y_out: pre-shortcut
+ * activation (may be NULL when no residual); res/sum_out: fused shortcut
+ * (darknet_v3.py:205-207) — both NULL or both set.  mask_y (may be NULL):
+ * multiply the result by leaky'(mask_y) (dgrad epilogue). */
+int po_conv(const po_conv_desc* d, const float* in, const float* W, const float* bias,
+            float* y_out, const float* res, float* sum_out, const float* mask_y,
+            po_stream_t s);
+
+/* First layer, 3 input channels NCHW image -> NHWC Cout_p (VALU direct conv):
+ * y = leaky(conv3x3(img, W[Cout][27]) + bias). */
+int po_conv_first_fwd(const float* img, int B, int H, int W, int stride, const float* Wt,
+                      const float* bias, int Cout, int Cout_p, int act, float* y, po_stream_t s);
+/* Its input gradient: d_img[b,c,h,w] (NCHW) from D [B,Ho,Wo,Cout_p] (already
+ * multiplied by leaky'), W [Cout][27]. */
+int po_conv_first_dgrad(const float* D, int B, int H, int W, int stride, const float* Wt,
+                        int Cout, int Cout_p, float* d_img, po_stream_t s);
+
+/* dst[m, 0:C] (=|+=) src[m, off:off+C] (optionally * leaky'(y[m,0:C])).
+ * strides are channel strides; M pixels. */
+int po_slice_accum(const float* src, int src_stride, int src_off, float* dst, int dst_stride,
+                   int dst_off, int64_t M, int C, int accumulate, const float* mask_y,
+                   int mask_stride, po_stream_t s);
+/* nearest 2x upsample fwd (darknet_v3.py:103-113): dst[b,2h+y,2w+x, off+c] = src[b,h,w,c]. */
+int po_upsample2_fwd(const float* src, int B, int H, int W, int C, int src_stride, float* dst,
+                     int dst_stride, int dst_off, po_stream_t s);
+/* its backward: dst[b,h,w,c] (=|+=) sum of the 4 src pixels (src at 2H x 2W,
+ * channel offset src_off), optionally * leaky'(mask_y). */
+int po_upsample2_bwd(const float* src, int src_stride, int src_off, int B, int H, int W, int C,
+                     float* dst, int dst_stride, int accumulate, const float* mask_y,
+                     int mask_stride, po_stream_t s);
+/* max pool k=2 (stride 2, or stride 1 after ZeroPad2d((0,1,0,1)), darknet_v3.py:61-69);
+ * argmax [B,Ho,Wo,C] int8 window position. */
+int po_maxpool2_fwd(const float* src, int B, int H, int W, int C, int Cp, int stride, float* dst,
+                    int8_t* argmax, po_stream_t s);
+int po_maxpool2_bwd(const float* d_dst, const int8_t* argmax, int B, int H, int W, int C, int Cp,
+                    int stride, float* d_src, int accumulate, const float* mask_y,
+                    po_stream_t s);
+
+/* NCHW [B,C,H,W] <-> NHWC [B,H,W,Cp] layout conversion (heads in and out of
+ * the drop-in Darknet.forward API). */
+int po_nhwc_to_nchw(const float* src, int B, int H, int W, int C, int Cp, float* dst, po_stream_t s);
+int po_nchw_to_nhwc(const float* src, int B, int H, int W, int C, int Cp, float* dst, po_stream_t s);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* ADVPATCH_H */

@@ -1,0 +1,150 @@
+"""CPU tests of the boundary and the host-side plan: the C-ABI library loads
+and exports every entry point include/advpatch.h declares; builtin cfgs
+reproduce the reference networks; synthetic weights have the reference
+.weights layout; the Darknet execution plan is well formed.  No kernel is
+launched (no GPU here)."""
+import os
+import re
+
+import pytest
+import torch
+
+from conftest import ROOT, pkg_mod
+
+HEADER = os.path.join(ROOT, "include", "advpatch.h")
+REF_CFG = "/root/reference/cfg"
+
+
+def _lib():
+    nat = pkg_mod("_native")
+    if not os.path.exists(nat.LIB_PATH):
+        import __graft_entry__
+        __graft_entry__.build()
+    return nat, nat.load()
+
+
+def test_library_exports_every_header_symbol():
+    text = open(HEADER).read()
+    declared = set(re.findall(r"^\s*(?:int|const char\*)\s+(po_\w+)\s*\(", text, re.M))
+    assert len(declared) >= 20
+    nat, lib = _lib()
+    for name in sorted(declared):
+        assert hasattr(lib, name), "libadvpatch_hip.so does not export %s" % name
+    assert declared == set(nat.symbols()), declared ^ set(nat.symbols())
+    assert lib.po_abi_version() == 1
+
+
+def test_conv_desc_struct_matches_header():
+    text = open(HEADER).read()
+    body = text[text.index("typedef struct po_conv_desc"):text.index("} po_conv_desc;")]
+    fields = re.findall(r"int\s+([^;]+);", body)
+    names = []
+    for f in fields:
+        for part in f.split(","):
+            names.append(re.sub(r"\[.*\]", "", part).strip())
+    nat = pkg_mod("_native")
+    assert names == [f[0] for f in nat.po_conv_desc._fields_]
+
+
+def test_errors_are_reported_not_silent():
+    nat, lib = _lib()
+    rc = lib.po_median7_fwd(None, 3, 10, 10, None, None, None)
+    assert rc == -1
+    assert "null pointer" in nat.last_error()
+    with pytest.raises(RuntimeError):
+        nat.call("po_median7_fwd", None, 3, 10, 10, None, None, None)
+
+
+def test_hip_ops_fail_loudly_without_gpu():
+    if torch.cuda.is_available():
+        pytest.skip("GPU present")
+    mp = pkg_mod("median_pool")
+    with pytest.raises(RuntimeError):
+        mp.MedianPool2d(7, same=True)(torch.rand(1, 3, 10, 10))
+
+
+def _layers(text):
+    out = []
+    for d in pkg_mod("cfg").parse_model_config_text(text):
+        t = d["type"]
+        if t == "net":
+            out.append((t, d["width"], d["height"], d["channels"]))
+        elif t == "convolutional":
+            out.append((t, int(d["filters"]), int(d["size"]), int(d["stride"]), int(d["batch_normalize"]),
+                        d["activation"]))
+        elif t == "route":
+            out.append((t, tuple(int(x) for x in d["layers"].split(","))))
+        elif t == "shortcut":
+            out.append((t, int(d["from"])))
+        elif t == "upsample":
+            out.append((t, int(d["stride"])))
+        elif t == "maxpool":
+            out.append((t, int(d["size"]), int(d["stride"])))
+        elif t == "yolo":
+            out.append((t, d["mask"].replace(" ", ""), int(d["classes"])))
+    return out
+
+
+@pytest.mark.skipif(not os.path.isdir(REF_CFG), reason="reference not mounted")
+def test_builtin_yolov3_dota_equals_reference_cfg():
+    G = pkg_mod("cfg_gen")
+    ref = _layers(open(os.path.join(REF_CFG, "yolov3-dota.cfg")).read())
+    assert _layers(G.yolov3(15, 608)) == ref
+
+
+@pytest.mark.skipif(not os.path.isdir(REF_CFG), reason="reference not mounted")
+def test_builtin_tiny_equals_reference_cfg_up_to_classes():
+    G = pkg_mod("cfg_gen")
+    ref = _layers(open(os.path.join(REF_CFG, "yolov3-tiny.cfg")).read())
+    mine = _layers(G.yolov3_tiny(80, 416))
+    assert mine == ref
+
+
+def test_conv_macs_match_survey():
+    import bench
+    dk = pkg_mod("darknet_v3")
+    assert bench.conv_macs(dk.Darknet("builtin:yolov3-dota")) == 69_841_000_000 or \
+        abs(bench.conv_macs(dk.Darknet("builtin:yolov3-dota")) / 69.841e9 - 1) < 1e-3
+    assert abs(bench.conv_macs(dk.Darknet("builtin:yolov3-tiny-dota")) / 2.732e9 - 1) < 2e-3
+
+
+def test_synthetic_weights_layout_and_parameter_count(tmp_path):
+    W, dk = pkg_mod("weights"), pkg_mod("darknet_v3")
+    stream = W.synthesize("builtin:yolov3-dota", seed=4)
+    assert stream.size == 61_651_732
+    path = str(tmp_path / "y.weights")
+    W.write_weights(path, stream)
+    assert os.path.getsize(path) == 20 + 4 * 61_651_732
+    net = dk.Darknet("builtin:yolov3-dota")
+    assert net.load_darknet_weights(path) == stream.size
+    nparam = sum(p.numel() for p in net.parameters())
+    assert nparam == 61_599_124
+    # save/load round trip through the reference layout
+    p2 = str(tmp_path / "y2.weights")
+    net.save_darknet_weights(p2)
+    assert open(p2, "rb").read()[20:] == open(path, "rb").read()[20:]
+
+
+def test_plan_structure_yolov3_on_cpu_buffers():
+    W, dk = pkg_mod("weights"), pkg_mod("darknet_v3")
+    net = dk.Darknet("builtin:mini3")
+    import tempfile
+    with tempfile.TemporaryDirectory() as td:
+        p = os.path.join(td, "m.weights")
+        W.write_weights(p, W.synthesize("builtin:mini3"))
+        net.load_darknet_weights(p)
+    plan = net.plan(2, 64, 64, torch.device("cpu"))
+    assert plan.heads == [17, 25, 33]
+    assert [plan.shp[h] for h in plan.heads] == [(4, 4, 60), (8, 8, 60), (16, 16, 60)]
+    assert plan.root[18] == 14 and plan.root[26] == 22           # single-layer routes alias
+    assert plan.fused == {4, 8, 12}                               # shortcuts fused into conv epilogues
+    names = [o[0] for o in plan.fwd_ops]
+    assert names.count("po_conv") + names.count("po_conv_first_fwd") == 22
+    # every leaky conv with a gradient gets exactly one masked (final) contribution
+    masked = {}
+    for name, args, desc in plan.bwd_ops:
+        if name == "po_conv" and args[7] is not None:
+            masked[args[4].value] = masked.get(args[4].value, 0) + 1
+    for i, d in enumerate(net.blocks):
+        if d["type"] == "convolutional" and plan._leaky(i) and plan.has_grad[i] and i > 0:
+            assert plan.ncons[i] >= 1

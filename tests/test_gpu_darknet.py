@@ -1,0 +1,109 @@
+"""GPU parity of the Darknet stack (implicit-GEMM fp32 MFMA conv forward and
+input-gradient, route/shortcut/upsample/maxpool) against the oracle's
+PyTorch-CPU fp32 forward and autograd backward on the same synthetic weights.
+
+Two fp32 implementations can take different LeakyReLU slopes (or maxpool
+arguments) where a pre-activation is within rounding of a tie; through a deep
+random network one such flip moves the input gradient by up to ~5e-2 relative
+(the fp32 oracle itself differs that much from a float64 run on yolov3-dota).
+So the backward is checked on aligned branches: the oracle is re-run with the
+branch decisions the HIP forward took, and separately every disagreeing
+branch is checked to be a rounding tie (|x| <= 1e-5 * max|x| of its layer).
+"""
+import pytest
+import torch
+
+import oracle
+from conftest import assert_branch_ties_only, pkg_mod, plan_branches
+
+pytestmark = pytest.mark.gpu
+
+DEV = torch.device("cuda", 0)
+
+
+def _net(cfg, tmp_path, seed=4):
+    dk, W, G = pkg_mod("darknet_v3"), pkg_mod("weights"), pkg_mod("cfg_gen")
+    path = str(tmp_path / "w.weights")
+    W.write_weights(path, W.synthesize(cfg, seed=seed))
+    net = dk.Darknet(cfg)
+    net.load_darknet_weights(path)
+    ref = oracle.OracleDarknet(G.cfg_text(cfg), path)
+    return net, ref
+
+
+def _rel(a, b):
+    return float((a - b).abs().max() / b.abs().max().clamp_min(1e-30))
+
+
+def _check(cfg, B, tmp_path, fwd_tol=5e-5, bwd_tol=1e-4):
+    net, ref = _net(cfg, tmp_path)
+    S = net.height
+    x = pkg_mod("synthetic").frames(B, S, seed=7)
+    xg = x.to(DEV).requires_grad_(True)
+    outs = net(xg)
+    plan = net.plan(B, S, S, DEV)
+    br = plan_branches(plan)
+    rec = {}
+    with torch.no_grad():
+        outs_nat = ref(x, record=rec)
+    for o, r in zip(outs, outs_nat):
+        assert o.shape == r.shape
+        assert _rel(o.detach().cpu(), r) < fwd_tol
+    assert_branch_ties_only(br, rec)
+    xr = x.clone().requires_grad_(True)
+    outs_ref = ref(xr, branch=br)
+    gen = torch.Generator().manual_seed(9)
+    grads = [torch.randn(o.shape, generator=gen) for o in outs_ref]
+    sum((o * g).sum() for o, g in zip(outs_ref, grads)).backward()
+    sum((o * g.to(DEV)).sum() for o, g in zip(outs, grads)).backward()
+    assert _rel(xg.grad.cpu(), xr.grad) < bwd_tol
+
+
+def test_mini3_fwd_bwd(tmp_path):
+    _check("builtin:mini3", 3, tmp_path)
+
+
+def test_mini3_96_batch5(tmp_path):
+    _check("builtin:mini3-96", 5, tmp_path)
+
+
+def test_tiny_dota_416(tmp_path):
+    # maxpool s2 and the ZeroPad2d + maxpool s1 block of yolov3-tiny
+    _check("builtin:yolov3-tiny-dota", 2, tmp_path)
+
+
+def test_yolov3_dota_608(tmp_path):
+    _check("builtin:yolov3-dota", 1, tmp_path)
+
+
+def test_conv_tile_variants(tmp_path):
+    """Chains that hit every po_conv tile shape (N=32/64/128+, large/small M,
+    stride-2 dgrad parity classes, odd spatial sizes, a non-fused shortcut)."""
+    G = pkg_mod("cfg_gen")
+    text = G._net(70) + G._conv(32, 3) + G._conv(64, 3, 2) + G._conv(48, 1) + G._conv(128, 3) + \
+        G._conv(256, 3, 2) + G._conv(96, 1) + G._conv(128, 3, 2) + G._conv(96, 1) + G._conv(128, 3) + \
+        G._shortcut(-3) + G._conv(60, 1, bn=False, act="linear") + G._yolo("0,1,2", G.DOTA_ANCHORS, 15, 9)
+    p = tmp_path / "chain.cfg"
+    p.write_text(text)
+    _check(str(p), 3, tmp_path)
+
+
+def test_large_m_tiles(tmp_path):
+    """Big-M layers (128x128 / 128x64 tiles, XCD remap over thousands of workgroups)."""
+    G = pkg_mod("cfg_gen")
+    text = G._net(256) + G._conv(32, 3) + G._conv(64, 3) + G._conv(128, 3, 2) + G._conv(256, 3) + \
+        G._conv(60, 1, bn=False, act="linear") + G._yolo("0,1,2", G.DOTA_ANCHORS, 15, 9)
+    p = tmp_path / "big.cfg"
+    p.write_text(text)
+    _check(str(p), 2, tmp_path)
+
+
+def test_heads_layout_matches_reference_view(tmp_path):
+    # channel = anchor*20 + field, as train_patch.py:459 views it
+    net, ref = _net("builtin:mini3", tmp_path)
+    x = pkg_mod("synthetic").frames(2, 64, seed=8)
+    heads_nhwc, plan = net.forward_nhwc(x.to(DEV))
+    outs = ref(x)
+    for h, r in zip(heads_nhwc, outs):
+        hc = h.detach().cpu()[..., :60].permute(0, 3, 1, 2)
+        assert _rel(hc, r) < 2e-5

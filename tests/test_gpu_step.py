@@ -1,0 +1,103 @@
+"""GPU parity of one full training iteration (train_patch.py:164-330) against
+the oracle: loss terms, bit-exact cell indices, objectness/class extraction,
+and the fp32 patch gradient within 1e-4 relative (north_star tolerance:
+max|g_hip - g_ref| / max|g_ref| <= 1e-4)."""
+import pytest
+import torch
+
+import oracle
+from conftest import pkg_mod, plan_branches
+
+pytestmark = pytest.mark.gpu
+DEV = torch.device("cuda", 0)
+
+
+def _trainer(cfg, tmp_path, objective="ce"):
+    tp, W, G = pkg_mod("train_patch"), pkg_mod("weights"), pkg_mod("cfg_gen")
+    path = str(tmp_path / "w.weights")
+    W.write_weights(path, W.synthesize(cfg, seed=4))
+    pc = pkg_mod("patch_config")
+    cfgobj = pc.patch_configs["paper_obj"]()
+
+    class _Cfg(type(cfgobj)):
+        def __init__(self):
+            super().__init__()
+            self.cfgfile = cfg
+            self.weightfile = path
+
+    pc.patch_configs["_test"] = _Cfg
+    tr = tp.PatchTrainer("_test", device=DEV, objective=objective, verbose=False)
+    ref_net = oracle.OracleDarknet(G.cfg_text(cfg), path)
+    return tr, ref_net
+
+
+def _run(cfg, B, P, tmp_path, objective="ce", seed=0):
+    sy, ld = pkg_mod("synthetic"), pkg_mod("load_data")
+    tr, ref_net = _trainer(cfg, tmp_path, objective)
+    S = ref_net.height
+    img, lab = sy.frames(B, S, seed=seed), sy.labels(B, seed=seed + 1)
+    patch, dr = sy.patch(P, seed=seed + 2), sy.draws(B, P, seed=seed + 3)
+    colors = ld.load_printability_colors("builtin:30values")
+    pg = patch.to(DEV).requires_grad_(True)
+    loss, terms = tr.losses(pg, img.to(DEV), lab.to(DEV), {k: v.to(DEV) for k, v in dr.items()})
+    # the oracle runs on the branch decisions (LeakyReLU slopes) the HIP forward took
+    br = plan_branches(tr.darknet_model.plan(B, S, S, DEV))
+    ref = oracle.train_step(patch, img, lab, dr, ref_net, colors, objective=objective, branch=br)
+    loss.backward()
+    return ref, terms, pg.grad.cpu()
+
+
+def _compare(ref, terms, grad, loss_tol=2e-5):
+    assert int(terms["flags"].item()) == 0
+    torch.testing.assert_close(terms["patch_center"].cpu(), ref["patch_center"], rtol=0, atol=0)
+    cells = terms["cells"].cpu().tolist()
+    assert cells == ref["cells"]                                   # bit-exact cell indices
+    torch.testing.assert_close(terms["obj"].cpu(), ref["obj"], rtol=0, atol=2e-5)
+    torch.testing.assert_close(terms["cls"].cpu(), ref["cls"], rtol=0, atol=2e-5)
+    for k in ("loss", "nps_loss", "tv_loss", "no_obj_loss", "no_cls_loss", "colorful_loss"):
+        a, b = float(terms[k]), float(ref[k])
+        assert abs(a - b) <= loss_tol * max(1.0, abs(b)), (k, a, b)
+    rel = float((grad - ref["grad"]).abs().max() / ref["grad"].abs().max())
+    assert rel < 1e-4, rel
+
+
+def test_step_mini3(tmp_path):
+    _compare(*_run("builtin:mini3", 6, 32, tmp_path))
+
+
+@pytest.mark.parametrize("objective", ["targeted", "untargeted"])
+def test_step_mini3_objectives(tmp_path, objective):
+    _compare(*_run("builtin:mini3", 4, 32, tmp_path, objective=objective))
+
+
+def test_step_yolov3_dota_608(tmp_path):
+    # config 1 shape (one 608x608 frame, 224x224 patch, yolov3-dota) plus a second frame
+    _compare(*_run("builtin:yolov3-dota", 2, 224, tmp_path, seed=40))
+
+
+def test_two_adam_steps_yolov3(tmp_path):
+    """BASELINE config 1: 1 frame, 2 Adam(amsgrad, lr 0.03) steps + clamp."""
+    sy, ld = pkg_mod("synthetic"), pkg_mod("load_data")
+    tr, ref_net = _trainer("builtin:yolov3-dota", tmp_path)
+    img, lab = sy.frames(1, 608, seed=50), sy.labels(1, seed=51)
+    patch, dr = sy.patch(224, seed=52), sy.draws(1, 224, seed=53)
+    colors = ld.load_printability_colors("builtin:30values")
+    pg = patch.to(DEV).requires_grad_(True)
+    opt = tr.make_optimizer(pg)
+    d = {k: v.to(DEV) for k, v in dr.items()}
+    brs = []
+    for _ in range(2):
+        loss, terms = tr.losses(pg, img.to(DEV), lab.to(DEV), d)
+        brs.append(plan_branches(tr.darknet_model.plan(1, 608, 608, DEV)))
+        loss.backward()
+        opt.step()
+        opt.zero_grad()
+        pg.data.clamp_(0, 1)
+    it = iter(brs)
+    ref = oracle.adam_amsgrad_steps(
+        patch, lambda p: oracle.train_step(p, img, lab, dr, ref_net, colors, branch=next(it))["grad"], 2)
+    # Adam's first steps move every element by ~lr whatever the gradient's size,
+    # so an element whose gradient is ~0 may move either way: require that
+    # >99% of the elements agree to 1e-4 after the two steps.
+    frac = float(((pg.detach().cpu() - ref).abs() > 1e-4).float().mean())
+    assert frac < 0.01, frac

@@ -1,0 +1,103 @@
+"""Known-answer tests pinning the oracle.  CPU only.
+
+The reference has no tests or golden vectors and may not be executed here
+(SURVEY.md §8c), so these analytic answers plus the committed fixtures
+(tests/golden/) are what pins the oracle."""
+import math
+
+import torch
+import torch.nn.functional as F
+
+import oracle
+from conftest import pkg_mod
+
+
+def test_kat1_identity_theta_reproduces_padded_patch():
+    # angle 0, scale 1, target (0.5, 0.5) -> theta = identity; grid_sample with
+    # it reproduces the padded patch (to sampling-coordinate rounding)
+    S, P = 96, 32
+    lab = torch.full((1, 4, 5), 1e-6)
+    # sel = (max-area row + min-area row)/2 with cols 2,3 giving target_size = P:
+    # sqrt((y*S/2)^2 + (w*S/2)^2) = P with y = w  ->  y = sqrt(2)*P/S
+    y = math.sqrt(2) * P / S
+    lab[0, 0] = torch.tensor([0.0, 0.5, 2 * y - 1e-6, 2 * y - 1e-6, 0.5])
+    dr = {"angle": torch.zeros(1), "ux": torch.tensor([0.5]), "uy": torch.tensor([0.5])}
+    theta, center, ts = oracle.patch_theta(lab, S, P, dr)
+    torch.testing.assert_close(theta[0], torch.tensor([[1., 0., 0.], [0., 1., 0.]]), rtol=0, atol=2e-6)
+    assert torch.equal(center, torch.tensor([[48.0, 48.0]]))
+    patch = torch.rand(1, 3, P, P, generator=torch.Generator().manual_seed(0))
+    padded = F.pad(patch, (32, 32, 32, 32))
+    grid = F.affine_grid(torch.eye(2, 3).unsqueeze(0), padded.shape, align_corners=False)
+    out = F.grid_sample(padded, grid, align_corners=False)
+    # the sampling coordinate is j +- rounding: not bit-exact, within ~1e-5
+    torch.testing.assert_close(out, padded, rtol=0, atol=1e-5)
+
+
+def test_kat2_tv_of_constant_patch():
+    P = 50
+    tv = oracle.total_variation(torch.full((3, P, P), 0.3))
+    assert abs(float(tv) - 2 * (P - 1) / P * 1e-6) < 1e-11
+
+
+def test_kat3_nps_of_printable_colour_patch():
+    colors = pkg_mod("load_data").load_printability_colors("builtin:30values")
+    k, P = 7, 40
+    patch = colors[k].view(3, 1, 1).expand(3, P, P).clone()
+    nps = oracle.nps_score(patch, colors)
+    assert abs(float(nps) - math.sqrt(1e-6 + 3e-12) / 3) < 1e-9
+    assert abs(float(nps) - 3.3333e-4) < 1e-7
+
+
+def test_kat4_colour_loss_of_grey_patch():
+    assert float(oracle.colorful_loss(torch.full((3, 16, 16), 0.5))) == 0.0
+
+
+def test_kat5_ce_of_equal_probabilities_is_ln15():
+    no_cls = torch.full((4, 9, 15), 0.5)
+    assert abs(float(oracle.noCLS_Loss_CE(no_cls, 14)) - math.log(15)) < 1e-6
+
+
+def test_kat6_obj_loss_of_half_objectness():
+    no_obj = torch.full((5, 9), 0.5)
+    loss = 4 * (1 - torch.mean(torch.max(no_obj, 1, keepdim=True)[0]))
+    assert float(loss) == 2.0
+
+
+def test_kat7_median_of_constant_and_gradient():
+    x = torch.full((1, 3, 12, 12), 0.25, requires_grad=True)
+    y = oracle.median_pool7(x)
+    assert torch.all(y == 0.25)
+    y.sum().backward()
+    assert abs(float(x.grad.sum()) - 3 * 144) < 1e-4
+
+
+def test_kat8_transposed_cell_index():
+    # centre (100, 300) at h=19, S=608: ix=3, iy=9, index = 3*19+9 = 66
+    assert oracle.cell_indices([19], 608, torch.tensor([[100.0, 300.0]])) == [[66]]
+
+
+def test_kat9_empty_label_frame_target_size():
+    lab = torch.full((1, 252, 5), 1e-6)
+    lab[0, 0] = 1.0
+    dr = {"angle": torch.zeros(1), "ux": torch.tensor([0.3]), "uy": torch.tensor([0.3])}
+    _, _, ts = oracle.patch_theta(lab, 608, 224, dr)
+    assert abs(float(ts) - 0.25 * 304 * math.sqrt(2)) < 1e-3
+    assert abs(float(ts) - 107.48) < 5e-3
+    assert abs(float(ts) / 224 - 0.4798) < 1e-4
+
+
+def test_position_clamps_q4():
+    lab = torch.full((2, 3, 5), 1e-6)
+    lab[:, 0] = torch.tensor([1.0, 0.5, 0.5, 0.1, 0.1])
+    dr = {"angle": torch.zeros(2), "ux": torch.tensor([0.05, 0.9]), "uy": torch.tensor([0.95, 0.1])}
+    _, center, _ = oracle.patch_theta(lab, 100, 20, dr)
+    torch.testing.assert_close(center, torch.tensor([[20.0, 80.0], [90.0, 10.0]]))
+
+
+def test_lab_transform_q2_q3():
+    # (max-area row + min-area row)/2; the padding row is the min-area row
+    lab = torch.full((1, 5, 5), 1e-6)
+    lab[0, 0] = torch.tensor([3.0, 0.2, 0.4, 0.1, 0.1])
+    lab[0, 1] = torch.tensor([5.0, 0.6, 0.8, 0.3, 0.2])
+    sel = oracle.lab_transform(lab)
+    torch.testing.assert_close(sel[0, 0], (lab[0, 1] + 1e-6) / 2)
