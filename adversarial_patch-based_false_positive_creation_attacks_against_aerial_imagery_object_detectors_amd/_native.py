@@ -19,7 +19,7 @@ class po_conv_desc(ctypes.Structure):
         "B", "Hin", "Win", "Cin_p", "Hout", "Wout", "Cout_p", "Hg", "Wg",
         "in_step", "out_step", "out_oy", "out_ox", "ntaps")] + [
         ("dh", c_int * 9), ("dw", c_int * 9),
-        ("N", c_int), ("act", c_int), ("accumulate", c_int)]
+        ("N", c_int), ("act", c_int), ("accumulate", c_int), ("tile", c_int)]
 
 
 _SIGS = {
@@ -28,7 +28,7 @@ _SIGS = {
     "po_median7_fwd": [c_void_p, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p],
     "po_median7_bwd": [c_void_p, c_void_p, c_int, c_int, c_int, c_void_p, c_void_p],
     "po_patch_params": [c_void_p, c_int, c_int, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int,
-                        c_void_p, c_void_p, c_void_p, c_void_p],
+                        c_void_p, c_void_p, c_void_p, c_void_p, c_void_p],
     "po_warp_fwd": [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int,
                     c_int, c_void_p, c_void_p],
     "po_warp_bwd": [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int,
@@ -40,11 +40,12 @@ _SIGS = {
     "po_cell_loss": [c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_int, c_int, c_void_p,
                      c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p],
     "po_conv": [ctypes.POINTER(po_conv_desc), c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
-                c_void_p, c_void_p, c_void_p],
+                c_void_p, c_void_p, c_void_p, c_void_p, c_void_p],
+    "po_conv_tile_info": [c_int, ctypes.POINTER(c_int), ctypes.POINTER(c_int), ctypes.POINTER(c_int)],
     "po_conv_first_fwd": [c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_int, c_int,
                           c_int, c_void_p, c_void_p],
     "po_conv_first_dgrad": [c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_int, c_int, c_void_p,
-                            c_void_p],
+                            c_void_p, c_void_p],
     "po_slice_accum": [c_void_p, c_int, c_int, c_void_p, c_int, c_int, c_int64, c_int, c_int,
                        c_void_p, c_int, c_void_p],
     "po_upsample2_fwd": [c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p, c_int, c_int, c_void_p],

@@ -1,0 +1,163 @@
+// First network layer on gfx950: 3 input channels (the NCHW image), 3x3,
+// as VALU direct convolution (K = 27 is too short for a matrix-core GEMM), and
+// its input gradient, restricted to the patch footprint on the training path.
+#include "common.h"
+
+namespace {
+// ------------------------------------------------------------------------
+// First layer: 3 input channels (NCHW image), 3x3, VALU direct convolution.
+// ------------------------------------------------------------------------
+template <int CO>
+__global__ __launch_bounds__(256) void first_fwd_k(const float* __restrict__ img, int B, int H, int W,
+                                                   int stride, int Ho, int Wo,
+                                                   const float* __restrict__ Wt,
+                                                   const float* __restrict__ bias, int Cout,
+                                                   int Cout_p, int act, float* __restrict__ y) {
+  __shared__ float ws[CO * 27];
+  __shared__ float bs[CO];
+  for (int t = threadIdx.x; t < CO * 27; t += 256) ws[t] = (t / 27) < Cout ? Wt[t] : 0.f;
+  for (int t = threadIdx.x; t < CO; t += 256) bs[t] = (t < Cout && bias) ? bias[t] : 0.f;
+  __syncthreads();
+  const int64_t p = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (p >= (int64_t)B * Ho * Wo) return;
+  const int b = (int)(p / ((int64_t)Ho * Wo));
+  const int rem = (int)(p - (int64_t)b * Ho * Wo);
+  const int i = rem / Wo, j = rem % Wo;
+  float x[27];
+#pragma unroll
+  for (int c = 0; c < 3; ++c)
+#pragma unroll
+    for (int kh = 0; kh < 3; ++kh)
+#pragma unroll
+      for (int kw = 0; kw < 3; ++kw) {
+        const int hi = i * stride - 1 + kh, wi = j * stride - 1 + kw;
+        x[c * 9 + kh * 3 + kw] = (hi >= 0 && hi < H && wi >= 0 && wi < W)
+                                     ? img[(((size_t)b * 3 + c) * H + hi) * W + wi] : 0.f;
+      }
+  float* yp = y + (size_t)p * Cout_p;
+#pragma unroll
+  for (int co4 = 0; co4 < CO; co4 += 4) {
+    float v[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      float s = 0.f;
+#pragma unroll
+      for (int k = 0; k < 27; ++k) s += ws[(co4 + u) * 27 + k] * x[k];
+      s += bs[co4 + u];
+      v[u] = act ? po::leaky(s) : s;
+    }
+    *reinterpret_cast<float4*>(yp + co4) = make_float4(v[0], v[1], v[2], v[3]);
+  }
+}
+
+template <int CO>
+__global__ __launch_bounds__(256) void first_dgrad_k(const float* __restrict__ D, int B, int H, int W,
+                                                     int stride, int Ho, int Wo,
+                                                     const float* __restrict__ Wt, int Cout,
+                                                     int Cout_p, const int32_t* __restrict__ roi,
+                                                     float* __restrict__ dimg) {
+  __shared__ float ws[CO * 27];
+  // roi mode: blockIdx.y = image, blockIdx.x tiles the image's box
+  const int b = roi ? (int)blockIdx.y : 0;
+  int x0 = 0, y0 = 0, x1 = W, y1 = H;
+  if (roi) {
+    x0 = roi[4 * b]; y0 = roi[4 * b + 1]; x1 = roi[4 * b + 2]; y1 = roi[4 * b + 3];
+    if ((int64_t)blockIdx.x * 256 >= (int64_t)(x1 - x0) * (y1 - y0)) return;   // whole block outside
+  }
+  for (int t = threadIdx.x; t < CO * 27; t += 256) ws[t] = (t / 27) < Cout ? Wt[t] : 0.f;
+  __syncthreads();
+  int h, w, bb;
+  if (roi) {
+    const int q = blockIdx.x * 256 + threadIdx.x;
+    const int bw = x1 - x0;
+    if (q >= bw * (y1 - y0)) return;
+    h = y0 + q / bw;
+    w = x0 + q % bw;
+    bb = b;
+  } else {
+    const int64_t p = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (p >= (int64_t)B * H * W) return;
+    bb = (int)(p / ((int64_t)H * W));
+    const int rem = (int)(p - (int64_t)bb * H * W);
+    h = rem / W;
+    w = rem % W;
+  }
+  const int b_ = bb;
+  float d0 = 0.f, d1 = 0.f, d2 = 0.f;
+#pragma unroll
+  for (int kh = 0; kh < 3; ++kh) {
+    const int th = h + 1 - kh;
+    if (th < 0 || th % stride) continue;
+    const int ho = th / stride;
+    if (ho >= Ho) continue;
+#pragma unroll
+    for (int kw = 0; kw < 3; ++kw) {
+      const int tw = w + 1 - kw;
+      if (tw < 0 || tw % stride) continue;
+      const int wo = tw / stride;
+      if (wo >= Wo) continue;
+      const float* dp = D + (((size_t)b_ * Ho + ho) * Wo + wo) * Cout_p;
+#pragma unroll
+      for (int co4 = 0; co4 < CO; co4 += 4) {
+        const float4 g = *reinterpret_cast<const float4*>(dp + co4);
+        const float gg[4] = {g.x, g.y, g.z, g.w};
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const float* wc = ws + (co4 + u) * 27 + kh * 3 + kw;
+          d0 += gg[u] * wc[0];
+          d1 += gg[u] * wc[9];
+          d2 += gg[u] * wc[18];
+        }
+      }
+    }
+  }
+  const size_t plane = (size_t)H * W;
+  float* o = dimg + (size_t)b_ * 3 * plane + (size_t)h * W + w;
+  o[0] = d0;
+  o[plane] = d1;
+  o[2 * plane] = d2;
+}
+}  // namespace
+
+extern "C" int po_conv_first_fwd(const float* img, int B, int H, int W, int stride, const float* Wt,
+                                 const float* bias, int Cout, int Cout_p, int act, float* y,
+                                 po_stream_t s) {
+  PO_REQUIRE(img && Wt && y, "po_conv_first_fwd: null pointer");
+  PO_REQUIRE(stride == 1 || stride == 2, "po_conv_first_fwd: stride %d", stride);
+  PO_REQUIRE(Cout > 0 && Cout <= 64 && Cout_p % 4 == 0 && Cout_p >= Cout, "po_conv_first_fwd: Cout=%d Cout_p=%d", Cout, Cout_p);
+  const int Ho = (H - 1) / stride + 1, Wo = (W - 1) / stride + 1;
+  const int64_t n = (int64_t)B * Ho * Wo;
+  dim3 grid(po::ceil_div(n, 256));
+  hipStream_t st = po::stream_of(s);
+  const int CO = Cout_p <= 16 ? 16 : (Cout_p <= 32 ? 32 : 64);
+  PO_REQUIRE(Cout_p == CO, "po_conv_first_fwd: Cout_p must be 16, 32 or 64 (got %d)", Cout_p);
+  if (CO == 16)
+    hipLaunchKernelGGL(first_fwd_k<16>, grid, dim3(256), 0, st, img, B, H, W, stride, Ho, Wo, Wt, bias, Cout, Cout_p, act, y);
+  else if (CO == 32)
+    hipLaunchKernelGGL(first_fwd_k<32>, grid, dim3(256), 0, st, img, B, H, W, stride, Ho, Wo, Wt, bias, Cout, Cout_p, act, y);
+  else
+    hipLaunchKernelGGL(first_fwd_k<64>, grid, dim3(256), 0, st, img, B, H, W, stride, Ho, Wo, Wt, bias, Cout, Cout_p, act, y);
+  return po::check_launch("po_conv_first_fwd");
+}
+
+extern "C" int po_conv_first_dgrad(const float* D, int B, int H, int W, int stride, const float* Wt,
+                                   int Cout, int Cout_p, const int32_t* roi, float* d_img,
+                                   po_stream_t s) {
+  PO_REQUIRE(D && Wt && d_img, "po_conv_first_dgrad: null pointer");
+  PO_REQUIRE(stride == 1 || stride == 2, "po_conv_first_dgrad: stride %d", stride);
+  const int CO = Cout_p <= 16 ? 16 : (Cout_p <= 32 ? 32 : 64);
+  PO_REQUIRE(Cout_p == CO && Cout <= Cout_p, "po_conv_first_dgrad: Cout_p must be 16, 32 or 64 (got %d)", Cout_p);
+  const int Ho = (H - 1) / stride + 1, Wo = (W - 1) / stride + 1;
+  // with a roi, blockIdx.y = image and blockIdx.x covers up to the whole image
+  // (blocks past the image's box exit at once)
+  const int64_t n = roi ? (int64_t)H * W : (int64_t)B * H * W;
+  dim3 grid(po::ceil_div(n, 256), roi ? B : 1);
+  hipStream_t st = po::stream_of(s);
+  if (CO == 16)
+    hipLaunchKernelGGL(first_dgrad_k<16>, grid, dim3(256), 0, st, D, B, H, W, stride, Ho, Wo, Wt, Cout, Cout_p, roi, d_img);
+  else if (CO == 32)
+    hipLaunchKernelGGL(first_dgrad_k<32>, grid, dim3(256), 0, st, D, B, H, W, stride, Ho, Wo, Wt, Cout, Cout_p, roi, d_img);
+  else
+    hipLaunchKernelGGL(first_dgrad_k<64>, grid, dim3(256), 0, st, D, B, H, W, stride, Ho, Wo, Wt, Cout, Cout_p, roi, d_img);
+  return po::check_launch("po_conv_first_dgrad");
+}

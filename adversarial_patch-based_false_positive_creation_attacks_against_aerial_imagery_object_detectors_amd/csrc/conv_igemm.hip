@@ -1,0 +1,305 @@
+// Convolutions of the Darknet stack on gfx950 fp32 matrix cores.
+//
+// po_conv: implicit GEMM  D[m][n] = sum_k A[m][k] * W[n][k]
+//   m = output pixel of the launch grid (b,i,j), n = output channel,
+//   k = (tap t, input channel c); A[m][(t,c)] = in[b, i*in_step+dh[t], j*in_step+dw[t], c]
+//   (zero outside the source).  The same kernel runs the forward conv
+//   (taps = the k x k window, BN folded into W/bias, leaky + shortcut in the
+//   epilogue) and the input-gradient (dgrad) convs (transposed weights, taps
+//   of one stride-parity class).
+//
+// Tiling: 256 threads = 4 waves, BM x BN block tile, BK input channels per
+// k-step, each wave owns (BM/WM) x (BN/WN) built from 32x32 tiles computed
+// with v_mfma_f32_32x32x2_f32 (exact fp32, 64 FLOP/clk/SIMD).  Operands go
+// global -> registers -> LDS (double buffered, one barrier per k-step).  LDS
+// rows are BK floats with their 16-byte chunks XOR-swizzled by row, which
+// makes both the ds_write_b128 staging and the ds_read_b128 fragment reads
+// bank-conflict free; each lane reads one 16-byte chunk per 4 MFMAs (the k
+// order inside a group of 8 is permuted identically for A and B).
+#include "common.h"
+#include <stdlib.h>
+#include <string.h>
+
+typedef float floatx16 __attribute__((ext_vector_type(16)));
+
+namespace {
+struct ConvArgs {
+  const float* in;
+  const float* W;
+  const float* bias;
+  float* y;
+  const float* res;
+  float* sum;
+  const float* mask;
+  float* y2;
+  const float* mask2;
+  int B, Hin, Win, Cin_p, Hout, Wout, Cout_p, Hg, Wg;
+  int in_step, out_step, out_oy, out_ox;
+  int ntaps, N, act, accumulate;
+  int M, ntiles_n;
+  int dh[9], dw[9];
+};
+
+template <int BM, int BN, int WM, int BK>
+__global__ __launch_bounds__(256) void conv_k(const ConvArgs a) {
+  constexpr int WN = 4 / WM;
+  constexpr int TM = BM / WM / 32;
+  constexpr int TN = BN / WN / 32;
+  static_assert(TM >= 1 && TN >= 1, "tile too small for 4 waves of 32x32");
+  constexpr int CPR = BK / 4;                  // 16-byte chunks per LDS row
+  constexpr int RPP = 256 / CPR;               // rows covered by one load pass of the workgroup
+  constexpr int AL = (BM + RPP - 1) / RPP;     // A float4 loads per thread per k-step
+  constexpr int BL = (BN + RPP - 1) / RPP;     // B float4 loads per thread per k-step
+  constexpr int SW = (BK == 16) ? 2 : 1;       // rows sharing a 256-byte bank line: 1 << SW
+  __shared__ __attribute__((aligned(16))) float smem[2 * (BM + BN) * BK];
+  float* As = smem;                            // [2][BM][BK]
+  float* Bs = smem + 2 * BM * BK;              // [2][BN][BK]
+
+  // XCD-aware bijective remap: consecutive logical tiles share an XCD's L2
+  const int nwg = gridDim.x, orig = blockIdx.x;
+  const int q = nwg / 8, r8 = nwg % 8, xcd = orig % 8;
+  const int wgid = (xcd < r8 ? xcd * (q + 1) : r8 * (q + 1) + (xcd - r8) * q) + orig / 8;
+  const int tn = wgid % a.ntiles_n, tm = wgid / a.ntiles_n;
+  const int m0 = tm * BM, n0 = tn * BN;
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave / WN, wn = wave % WN;
+  const int HgWg = a.Hg * a.Wg;
+  const int cth = tid % CPR, rth = tid / CPR;
+
+  // ---- A loader state (rows rth + RPP*r of the tile)
+  int a_hi[AL], a_wi[AL];
+  const float* a_img[AL];
+  bool a_ok[AL];
+#pragma unroll
+  for (int r = 0; r < AL; ++r) {
+    const int row = rth + RPP * r;
+    const int m = m0 + row;
+    a_ok[r] = (row < BM) && (m < a.M);
+    const int mm = a_ok[r] ? m : 0;
+    const int b = mm / HgWg, rem = mm - b * HgWg;
+    const int i = rem / a.Wg, j = rem - i * a.Wg;
+    a_img[r] = a.in + (size_t)b * a.Hin * a.Win * a.Cin_p + cth * 4;
+    a_hi[r] = i * a.in_step;
+    a_wi[r] = j * a.in_step;
+  }
+  // ---- B loader state
+  const size_t wrow = (size_t)a.ntaps * a.Cin_p;
+  bool b_ok[BL];
+  const float* b_ptr[BL];
+#pragma unroll
+  for (int r = 0; r < BL; ++r) {
+    const int row = rth + RPP * r;
+    b_ok[r] = (row < BN) && (n0 + row < a.N);
+    b_ptr[r] = a.W + (size_t)(b_ok[r] ? n0 + row : 0) * wrow + cth * 4;
+  }
+
+  float4 ra[AL], rb[BL];
+  auto gload = [&](int tap, int c0) {
+    const int dh = a.dh[tap], dw = a.dw[tap];
+#pragma unroll
+    for (int r = 0; r < AL; ++r) {
+      const int hi = a_hi[r] + dh, wi = a_wi[r] + dw;
+      if (a_ok[r] && hi >= 0 && hi < a.Hin && wi >= 0 && wi < a.Win)
+        ra[r] = *reinterpret_cast<const float4*>(a_img[r] + ((size_t)hi * a.Win + wi) * a.Cin_p + c0);
+      else
+        ra[r] = make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+#pragma unroll
+    for (int r = 0; r < BL; ++r)
+      rb[r] = b_ok[r] ? *reinterpret_cast<const float4*>(b_ptr[r] + (size_t)tap * a.Cin_p + c0)
+                      : make_float4(0.f, 0.f, 0.f, 0.f);
+  };
+  auto swz = [](int row, int chunk) { return (chunk ^ ((row >> SW) & (CPR - 1))) * 4; };
+  auto sstore = [&](int buf) {
+#pragma unroll
+    for (int r = 0; r < AL; ++r) {
+      const int row = rth + RPP * r;
+      if (row < BM)
+        *reinterpret_cast<float4*>(&As[(buf * BM + row) * BK + swz(row, cth)]) = ra[r];
+    }
+#pragma unroll
+    for (int r = 0; r < BL; ++r) {
+      const int row = rth + RPP * r;
+      if (row < BN)
+        *reinterpret_cast<float4*>(&Bs[(buf * BN + row) * BK + swz(row, cth)]) = rb[r];
+    }
+  };
+
+  floatx16 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.f;
+
+  const int kc = a.Cin_p / BK;
+  const int nks = a.ntaps * kc;
+  int tap = 0, c0 = 0;
+  gload(0, 0);
+  sstore(0);
+  __syncthreads();
+  const int arow = wm * TM * 32 + (lane & 31);
+  const int brow = wn * TN * 32 + (lane & 31);
+  const int h = lane >> 5;
+  for (int ks = 0; ks < nks; ++ks) {
+    const int buf = ks & 1;
+    const bool more = ks + 1 < nks;
+    if (more) {
+      c0 += BK;
+      if (c0 == a.Cin_p) { c0 = 0; ++tap; }
+      gload(tap, c0);
+    }
+    const float* Ab = As + buf * BM * BK;
+    const float* Bb = Bs + buf * BN * BK;
+#pragma unroll
+    for (int g = 0; g < BK / 8; ++g) {
+      float4 af[TM], bf[TN];
+#pragma unroll
+      for (int i = 0; i < TM; ++i) {
+        const int row = arow + i * 32;
+        af[i] = *reinterpret_cast<const float4*>(&Ab[row * BK + swz(row, 2 * g + h)]);
+      }
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        const int row = brow + j * 32;
+        bf[j] = *reinterpret_cast<const float4*>(&Bb[row * BK + swz(row, 2 * g + h)]);
+      }
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) {
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(af[i].x, bf[j].x, acc[i][j], 0, 0, 0);
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(af[i].y, bf[j].y, acc[i][j], 0, 0, 0);
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(af[i].z, bf[j].z, acc[i][j], 0, 0, 0);
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(af[i].w, bf[j].w, acc[i][j], 0, 0, 0);
+        }
+    }
+    if (more) sstore(buf ^ 1);
+    __syncthreads();
+  }
+
+  // ---- epilogue: destination pixel offsets of the BM tile rows via LDS
+  int* dst_pix = reinterpret_cast<int*>(smem);
+  if (tid < BM) {
+    const int m = m0 + tid;
+    int o = -1;
+    if (m < a.M) {
+      const int b = m / HgWg, rem = m - b * HgWg;
+      const int i = rem / a.Wg, j = rem - i * a.Wg;
+      o = (b * a.Hout + i * a.out_step + a.out_oy) * a.Wout + j * a.out_step + a.out_ox;
+    }
+    dst_pix[tid] = o;
+  }
+  __syncthreads();
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      const int n = n0 + wn * TN * 32 + j * 32 + (lane & 31);
+      if (n >= a.N) continue;
+      const float bv = a.bias ? a.bias[n] : 0.f;
+#pragma unroll
+      for (int e = 0; e < 16; ++e) {
+        const int row = wm * TM * 32 + i * 32 + (e & 3) + 8 * (e >> 2) + 4 * (lane >> 5);
+        const int pix = dst_pix[row];
+        if (pix < 0) continue;
+        const size_t o = (size_t)pix * a.Cout_p + n;
+        float v = acc[i][j][e] + bv;
+        if (a.act) v = po::leaky(v);
+        if (a.accumulate) v += a.y[o];
+        a.y[o] = a.mask ? v * po::leaky_grad(a.mask[o]) : v;
+        if (a.res) a.sum[o] = v + a.res[o];
+        if (a.y2) a.y2[o] = v * po::leaky_grad(a.mask2[o]);
+      }
+    }
+}
+
+template <int BM, int BN, int WM, int BK>
+int launch(const ConvArgs& a, hipStream_t st) {
+  ConvArgs b = a;
+  b.ntiles_n = po::ceil_div(a.N, BN);
+  const int ntiles = po::ceil_div(a.M, BM) * b.ntiles_n;
+  hipLaunchKernelGGL((conv_k<BM, BN, WM, BK>), dim3(ntiles), dim3(256), 0, st, b);
+  return po::check_launch("po_conv");
+}
+
+template <int BK>
+int dispatch(const ConvArgs& a, hipStream_t st, int bm, int bn) {
+  if (bm == 128 && bn == 128) return launch<128, 128, 2, BK>(a, st);
+  if (bm == 64 && bn == 128) return launch<64, 128, 1, BK>(a, st);
+  if (bm == 128 && bn == 64) return launch<128, 64, 4, BK>(a, st);
+  if (bm == 64 && bn == 64) return launch<64, 64, 2, BK>(a, st);
+  if (bm == 128 && bn == 32) return launch<128, 32, 4, BK>(a, st);
+  po::set_error("po_conv: no %dx%d tile", bm, bn);
+  return PO_EINVAL;
+}
+
+// ADVPATCH_CONV_TILE="BMxBNxBK" forces a tile (tuning experiments only).
+bool forced_tile(int& bm, int& bn, int& bk) {
+  const char* e = getenv("ADVPATCH_CONV_TILE");
+  return e && sscanf(e, "%dx%dx%d", &bm, &bn, &bk) == 3;
+}
+
+constexpr int kTiles[PO_CONV_NTILES][3] = {
+    {128, 128, 16}, {128, 128, 32}, {64, 128, 16}, {64, 128, 32}, {128, 64, 16},
+    {128, 64, 32},  {64, 64, 16},   {64, 64, 32},  {128, 32, 16}, {128, 32, 32}};
+}  // namespace
+
+extern "C" int po_conv_tile_info(int t, int* bm, int* bn, int* bk) {
+  PO_REQUIRE(t >= 1 && t <= PO_CONV_NTILES && bm && bn && bk, "po_conv_tile_info: bad tile %d", t);
+  *bm = kTiles[t - 1][0];
+  *bn = kTiles[t - 1][1];
+  *bk = kTiles[t - 1][2];
+  return PO_OK;
+}
+
+extern "C" int po_conv(const po_conv_desc* d, const float* in, const float* W, const float* bias,
+                       float* y_out, const float* res, float* sum_out, const float* mask_y,
+                       float* y2_out, const float* mask2, po_stream_t s) {
+  PO_REQUIRE(d && in && W && y_out, "po_conv: null pointer");
+  PO_REQUIRE((res == nullptr) == (sum_out == nullptr), "po_conv: res and sum_out must both be set or both NULL");
+  PO_REQUIRE((y2_out == nullptr) == (mask2 == nullptr), "po_conv: y2_out and mask2 must both be set or both NULL");
+  PO_REQUIRE(d->Cin_p % 16 == 0 && d->Cin_p > 0, "po_conv: Cin_p=%d must be a positive multiple of 16", d->Cin_p);
+  PO_REQUIRE(d->N > 0 && d->N % 16 == 0 && d->N <= d->Cout_p, "po_conv: N=%d must be a multiple of 16 <= Cout_p=%d", d->N, d->Cout_p);
+  PO_REQUIRE(d->ntaps >= 1 && d->ntaps <= 9, "po_conv: ntaps=%d", d->ntaps);
+  PO_REQUIRE(d->B > 0 && d->Hg > 0 && d->Wg > 0 && d->Hin > 0 && d->Win > 0, "po_conv: bad grid");
+  PO_REQUIRE((d->Hg - 1) * d->out_step + d->out_oy < d->Hout && (d->Wg - 1) * d->out_step + d->out_ox < d->Wout,
+             "po_conv: launch grid writes outside the destination");
+  PO_REQUIRE((int64_t)d->B * d->Hout * d->Wout < (1LL << 31), "po_conv: destination too large");
+  ConvArgs a;
+  a.in = in; a.W = W; a.bias = bias; a.y = y_out; a.res = res; a.sum = sum_out; a.mask = mask_y;
+  a.y2 = y2_out; a.mask2 = mask2;
+  a.B = d->B; a.Hin = d->Hin; a.Win = d->Win; a.Cin_p = d->Cin_p;
+  a.Hout = d->Hout; a.Wout = d->Wout; a.Cout_p = d->Cout_p; a.Hg = d->Hg; a.Wg = d->Wg;
+  a.in_step = d->in_step; a.out_step = d->out_step; a.out_oy = d->out_oy; a.out_ox = d->out_ox;
+  a.ntaps = d->ntaps; a.N = d->N; a.act = d->act; a.accumulate = d->accumulate;
+  a.M = d->B * d->Hg * d->Wg;
+  a.ntiles_n = 1;
+  for (int t = 0; t < 9; ++t) {
+    a.dh[t] = t < d->ntaps ? d->dh[t] : 0;
+    a.dw[t] = t < d->ntaps ? d->dw[t] : 0;
+  }
+  hipStream_t st = po::stream_of(s);
+  int bm, bn, bk;
+  PO_REQUIRE(d->tile >= 0 && d->tile <= PO_CONV_NTILES, "po_conv: tile %d out of range", d->tile);
+  if (d->tile > 0) {
+    bm = kTiles[d->tile - 1][0];
+    bn = kTiles[d->tile - 1][1];
+    bk = kTiles[d->tile - 1][2];
+  } else if (!forced_tile(bm, bn, bk)) {
+    // largest tile that still gives >= 2 workgroups per CU
+    const int64_t M = a.M;
+    const int N = a.N;
+    auto tiles = [&](int tbm, int tbn) { return (int64_t)po::ceil_div(M, tbm) * po::ceil_div(N, tbn); };
+    bk = (a.Cin_p % 32 == 0) ? 32 : 16;
+    if (N <= 32) { bm = 128; bn = 32; }
+    else if (N <= 64) { bn = 64; bm = tiles(128, 64) >= 512 ? 128 : 64; }
+    else if (tiles(128, 128) >= 512) { bm = 128; bn = 128; }
+    else if (tiles(64, 128) >= 512) { bm = 64; bn = 128; }
+    else { bm = 64; bn = 64; }
+  }
+  if (bk == 32 && a.Cin_p % 32 != 0) bk = 16;
+  return bk == 32 ? dispatch<32>(a, st, bm, bn) : dispatch<16>(a, st, bm, bn);
+}

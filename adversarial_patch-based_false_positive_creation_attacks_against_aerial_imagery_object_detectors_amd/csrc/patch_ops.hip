@@ -138,23 +138,31 @@ extern "C" int po_median7_bwd(const float* dy, const int32_t* argidx, int C, int
 // Placement parameters (load_data.py:453-509, 654-743)
 // ------------------------------------------------------------------------
 namespace {
-__global__ void patch_params_k(const float* __restrict__ lab, int B, int L,
-                               const float* __restrict__ angle, const float* __restrict__ ux,
-                               const float* __restrict__ uy, int do_rotate, int S, int P,
-                               float* __restrict__ theta, float* __restrict__ center,
-                               float* __restrict__ tsize) {
-  int b = blockIdx.x * blockDim.x + threadIdx.x;
-  if (b >= B) return;
+// one wave per image: the label scan is a wave reduction of (area, row) pairs
+__global__ __launch_bounds__(64) void patch_params_k(const float* __restrict__ lab, int B, int L,
+                                                     const float* __restrict__ angle, const float* __restrict__ ux,
+                                                     const float* __restrict__ uy, int do_rotate, int S, int P,
+                                                     float* __restrict__ theta, float* __restrict__ center,
+                                                     float* __restrict__ tsize, int32_t* __restrict__ roi) {
+  const int b = blockIdx.x;
+  const int lane = threadIdx.x;
   const float* lb = lab + (size_t)b * L * 5;
   // lab_transform: area = lab[:,:,3]*lab[:,:,4]; torch.max / torch.min over
   // rows, first index on ties (load_data.py:464-467)
-  float vmax = lb[3] * lb[4], vmin = vmax;
-  int imax = 0, imin = 0;
-  for (int l = 1; l < L; ++l) {
+  float vmax = -INFINITY, vmin = INFINITY;
+  int imax = 0x7fffffff, imin = 0x7fffffff;
+  for (int l = lane; l < L; l += 64) {
     float a = lb[l * 5 + 3] * lb[l * 5 + 4];
     if (a > vmax) { vmax = a; imax = l; }
     if (a < vmin) { vmin = a; imin = l; }
   }
+  for (int o = 32; o > 0; o >>= 1) {
+    const float ov = __shfl_xor(vmax, o), nv = __shfl_xor(vmin, o);
+    const int oi = __shfl_xor(imax, o), ni = __shfl_xor(imin, o);
+    if (ov > vmax || (ov == vmax && oi < imax)) { vmax = ov; imax = oi; }
+    if (nv < vmin || (nv == vmin && ni < imin)) { vmin = nv; imin = ni; }
+  }
+  if (lane != 0) return;
   float sel2, sel3;
   if (vmax > 0.99f) {                       // load_data.py:471-473
     sel2 = 0.25f; sel3 = 0.25f;
@@ -183,17 +191,42 @@ __global__ void patch_params_k(const float* __restrict__ lab, int B, int L,
   th[4] = cs / scale;
   th[5] = -tx * sn / scale + ty * cs / scale;
   if (tsize) tsize[b] = ts;
+  if (roi) {
+    // output pixels whose bilinear sample can touch the padded patch region:
+    // preimage of [pad-1, pad+P) x [pad-1, pad+P) under the pixel-space affine
+    const float half = 0.5f - 0.5f * fS;
+    const float A00 = th[0], A01 = th[1], A10 = th[3], A11 = th[4];
+    const float A02 = (th[0] + th[1]) * half + 0.5f * fS * th[2] + 0.5f * (fS - 1.f);
+    const float A12 = (th[3] + th[4]) * half + 0.5f * fS * th[5] + 0.5f * (fS - 1.f);
+    const float det = A00 * A11 - A01 * A10;
+    const int padL = (int)((S - P) / 2.0 + 0.5);
+    float jlo = 1e30f, jhi = -1e30f, ilo = 1e30f, ihi = -1e30f;
+    for (int k = 0; k < 4; ++k) {
+      const float X = (float)((k & 1) ? padL + P : padL - 1) - A02;
+      const float Y = (float)((k & 2) ? padL + P : padL - 1) - A12;
+      const float jj = (A11 * X - A01 * Y) / det, ii = (-A10 * X + A00 * Y) / det;
+      jlo = fminf(jlo, jj); jhi = fmaxf(jhi, jj);
+      ilo = fminf(ilo, ii); ihi = fmaxf(ihi, ii);
+    }
+    const float lo = -4.f, hi = fS + 4.f;      // clamp before the int conversion
+    jlo = fminf(fmaxf(jlo, lo), hi); jhi = fminf(fmaxf(jhi, lo), hi);
+    ilo = fminf(fmaxf(ilo, lo), hi); ihi = fminf(fmaxf(ihi, lo), hi);
+    roi[4 * b + 0] = max(0, (int)floorf(jlo) - 2);
+    roi[4 * b + 1] = max(0, (int)floorf(ilo) - 2);
+    roi[4 * b + 2] = min(S, (int)ceilf(jhi) + 3);
+    roi[4 * b + 3] = min(S, (int)ceilf(ihi) + 3);
+  }
 }
 }  // namespace
 
 extern "C" int po_patch_params(const float* lab, int B, int L, const float* angle, const float* ux,
                                const float* uy, int do_rotate, int S, int P, float* theta,
-                               float* center, float* target_size, po_stream_t s) {
+                               float* center, float* target_size, int32_t* roi, po_stream_t s) {
   PO_REQUIRE(lab && ux && uy && theta && center, "po_patch_params: null pointer");
   PO_REQUIRE(!do_rotate || angle, "po_patch_params: angle required when do_rotate");
   PO_REQUIRE(B > 0 && L > 0 && S > 0 && P > 0, "po_patch_params: bad shape");
-  hipLaunchKernelGGL(patch_params_k, dim3(po::ceil_div(B, 64)), dim3(64), 0, po::stream_of(s), lab,
-                     B, L, angle, ux, uy, do_rotate, S, P, theta, center, target_size);
+  hipLaunchKernelGGL(patch_params_k, dim3(B), dim3(64), 0, po::stream_of(s), lab, B, L, angle, ux, uy,
+                     do_rotate, S, P, theta, center, target_size, roi);
   return po::check_launch("po_patch_params");
 }
 

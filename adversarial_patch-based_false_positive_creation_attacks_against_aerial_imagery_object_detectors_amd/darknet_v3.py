@@ -20,6 +20,7 @@ is the same implicit GEMM with transposed/flipped weights (stride 2 split into
 its 4 parity classes), and the LeakyReLU derivative of the producing layer is
 applied in the epilogue of the last gradient contribution to it.
 """
+import os
 from itertools import chain
 
 import numpy as np
@@ -259,11 +260,37 @@ class NetPlan:
                     if s != INPUT:
                         ncons[s] += 1
         self.ncons, self.ext = ncons, ext
+        # Residual stages share one gradient buffer: for a shortcut s = y_b + x_f
+        # whose input f is consumed only by s and earlier blocks, dL/dx_f =
+        # dL/ds + (contributions processed after s), so G_f aliases G_s and the
+        # shortcut costs no pass; dL/dy_b = dL/ds * leaky'(y_b) is emitted as the
+        # second epilogue output of the dgrad that completes G_s.
+        consumers = [[] for _ in range(n)]
+        for j in range(n):
+            t = blocks[j]["type"]
+            if t == "yolo" or (t == "route" and len(self.srcs[j]) == 1) or root[j] != j or not has[j]:
+                continue
+            for s in self.srcs[j]:
+                if s != INPUT:
+                    consumers[s].append(j)
+        self.consumers = consumers
+        self.sc_alias = {}
+        for s in range(n):
+            d = blocks[s]
+            if d["type"] != "shortcut" or root[s] != s or not has[s]:
+                continue
+            b, f = self.srcs[s]
+            if f == b or ext[f] or not has[f] or root[f] != f:
+                continue
+            if all(j <= s for j in consumers[f]) and consumers[b] == [s] and self._leaky(b):
+                self.sc_alias[s] = (b, f)
         dev, B = self.device, self.B
         self.grad = [None] * n
-        for i in range(n):
-            if root[i] == i and has[i]:
+        for i in range(n - 1, -1, -1):
+            if root[i] == i and has[i] and self.grad[i] is None:
                 self.grad[i] = torch.zeros(B, self.shp[i][0], self.shp[i][1], self.cp[i], device=dev)
+            if i in self.sc_alias:
+                self.grad[self.sc_alias[i][1]] = self.grad[i]
 
     def _leaky(self, r):
         return (self.net.blocks[r]["type"] == "convolutional" and self.net._conv_meta[r]["act"] == "leaky")
@@ -313,7 +340,7 @@ class NetPlan:
                     f = f if f >= 0 else (i + 1) + f
                     res, sum_out = self.act[self.root[f]], self.act[i + 1]
                 args = (nat.ctypes.byref(desc), P(inp), P(wts["w"]), P(wts["bias"]), P(y_out), P(res),
-                        P(sum_out), None)
+                        P(sum_out), None, None, None)
                 fwd.append(("po_conv", args, desc))
             elif t == "shortcut":
                 if i in self.fused:
@@ -350,18 +377,37 @@ class NetPlan:
         # backward
         bwd = []
         done = [0] * self.n
-        pre = []
         root = self.root
         for r in range(self.n):
             if self.ext[r] and root[r] == r and self.has_grad[r]:
                 done[r] += 1        # the head gradient is copied in first (run_backward)
 
         def contrib(r):
+            """(accumulate?, leaky mask or None, completes G_r?) of the next
+            gradient contribution to block r."""
             acc = 1 if done[r] > 0 else 0
             final = (done[r] + 1 - (1 if self.ext[r] else 0)) == self.ncons[r]
             mask = self.act[r] if (final and self._leaky(r)) else None
             done[r] += 1
-            return acc, mask
+            return acc, mask, final
+
+        def dual_of(r, final):
+            """second output when this contribution completes an aliased shortcut's G."""
+            if final and r in self.sc_alias:
+                b, _ = self.sc_alias[r]
+                acc_b, mask_b, fin_b = contrib(b)
+                assert acc_b == 0 and fin_b and mask_b is not None
+                return self.grad[b], self.act[b]
+            return None, None
+
+        def fallback_dual(r, final):
+            # the completing contribution was not a conv dgrad: extract dL/dy_b with a masked copy
+            if final and r in self.sc_alias:
+                b, _ = self.sc_alias[r]
+                _, mask_b, _ = contrib(b)
+                M = self.B * self.shp[r][0] * self.shp[r][1]
+                bwd.append(("po_slice_accum", (P(self.grad[r]), self.cp[r], 0, P(self.grad[b]), self.cp[b], 0, M,
+                                               self.shp[r][2], 0, P(mask_b), self.cp[b]), None))
 
         for j in range(self.n - 1, -1, -1):
             d = blocks[j]
@@ -376,45 +422,59 @@ class NetPlan:
                 if src == INPUT:
                     if self.first_direct:
                         bwd.append(("po_conv_first_dgrad", (P(G), B, self.H, self.W, m["stride"], P(wts["w27"]),
-                                                            m["cout"], self.cp[j], "dimg"), None))
+                                                            m["cout"], self.cp[j], "roi", "dimg"), None))
                     else:
                         for desc, wd in self._dgrad_descs(j, INPUT, 0):
                             bwd.append(("po_conv", (nat.ctypes.byref(desc), P(G), P(wd), None, P(self.in_nhwc), None,
-                                                    None, None), desc))
+                                                    None, None, None, None), desc))
                         bwd.append(("po_nhwc_to_nchw", (P(self.in_nhwc), B, self.H, self.W, 3, 16, "dimg"), None))
                     continue
-                acc, mask = contrib(src)
+                acc, mask, final = contrib(src)
+                y2, m2 = dual_of(src, final)
                 for desc, wd in self._dgrad_descs(j, src, acc):
                     bwd.append(("po_conv", (nat.ctypes.byref(desc), P(G), P(wd), None, P(self.grad[src]), None, None,
-                                            P(mask)), desc))
+                                            P(mask), P(y2), P(m2)), desc))
             elif t == "shortcut":
+                if j in self.sc_alias:
+                    b, f = self.sc_alias[j]
+                    acc, mask, final = contrib(f)      # implicit: G_f aliases G_s
+                    assert acc == 0
+                    if mask is not None:               # f has no later contributor: apply its mask in place
+                        M = self.B * self.shp[f][0] * self.shp[f][1]
+                        bwd.append(("po_slice_accum", (P(G), self.cp[j], 0, P(self.grad[f]), self.cp[f], 0, M,
+                                                       self.shp[f][2], 0, P(mask), self.cp[f]), None))
+                    continue
                 M = self.B * self.shp[j][0] * self.shp[j][1]
                 C = self.shp[j][2]
-                for s in self.srcs[j]:
-                    acc, mask = contrib(s)
-                    bwd.append(("po_slice_accum", (P(G), self.cp[j], 0, P(self.grad[s]), self.cp[s], 0, M, C, acc,
-                                                   P(mask), self.cp[s]), None))
+                for s_ in self.srcs[j]:
+                    acc, mask, final = contrib(s_)
+                    bwd.append(("po_slice_accum", (P(G), self.cp[j], 0, P(self.grad[s_]), self.cp[s_], 0, M, C, acc,
+                                                   P(mask), self.cp[s_]), None))
+                    fallback_dual(s_, final)
             elif t == "route":
                 off = 0
                 M = self.B * self.shp[j][0] * self.shp[j][1]
-                for s in self.srcs[j]:
-                    C = self.shp[s][2]
-                    acc, mask = contrib(s)
-                    bwd.append(("po_slice_accum", (P(G), self.cp[j], off, P(self.grad[s]), self.cp[s], 0, M, C, acc,
-                                                   P(mask), self.cp[s]), None))
+                for s_ in self.srcs[j]:
+                    C = self.shp[s_][2]
+                    acc, mask, final = contrib(s_)
+                    bwd.append(("po_slice_accum", (P(G), self.cp[j], off, P(self.grad[s_]), self.cp[s_], 0, M, C, acc,
+                                                   P(mask), self.cp[s_]), None))
+                    fallback_dual(s_, final)
                     off += C
             elif t == "upsample":
-                s = self.srcs[j][0]
-                acc, mask = contrib(s)
-                hs, ws_, cs = self.shp[s]
-                bwd.append(("po_upsample2_bwd", (P(G), self.cp[j], 0, B, hs, ws_, cs, P(self.grad[s]), self.cp[s],
-                                                 acc, P(mask), self.cp[s]), None))
+                s_ = self.srcs[j][0]
+                acc, mask, final = contrib(s_)
+                hs, ws_, cs = self.shp[s_]
+                bwd.append(("po_upsample2_bwd", (P(G), self.cp[j], 0, B, hs, ws_, cs, P(self.grad[s_]), self.cp[s_],
+                                                 acc, P(mask), self.cp[s_]), None))
+                fallback_dual(s_, final)
             elif t == "maxpool":
-                s = self.srcs[j][0]
-                acc, mask = contrib(s)
-                hs, ws_, cs = self.shp[s]
-                bwd.append(("po_maxpool2_bwd", (P(G), P(self.argmax[j]), B, hs, ws_, cs, self.cp[s], int(d["stride"]),
-                                                P(self.grad[s]), acc, P(mask)), None))
+                s_ = self.srcs[j][0]
+                acc, mask, final = contrib(s_)
+                hs, ws_, cs = self.shp[s_]
+                bwd.append(("po_maxpool2_bwd", (P(G), P(self.argmax[j]), B, hs, ws_, cs, self.cp[s_], int(d["stride"]),
+                                                P(self.grad[s_]), acc, P(mask)), None))
+                fallback_dual(s_, final)
         self.bwd_ops = bwd
 
     def _dgrad_descs(self, j, src, acc):
@@ -448,6 +508,58 @@ class NetPlan:
                 out.append((desc, wd))
         return out
 
+    # ---------------- autotuning ----------------
+    def tune(self, cache, iters=4):
+        """Time every candidate tile of po_conv for each distinct launch shape of
+        this plan on the current GPU and keep the fastest (wave quantisation
+        over the 256 CUs and the k-step size decide it per shape).  ``cache``
+        maps a launch signature to its tile and is shared between plans."""
+        lib = self.lib
+        st = nat.stream()
+        bufs = {id(t): t for t in self.act + self.grad if t is not None}
+        if self.in_nhwc is not None:
+            bufs[id(self.in_nhwc)] = self.in_nhwc
+        with torch.no_grad():
+            for t in bufs.values():
+                t.uniform_(-1.0, 1.0)           # time on random data, not zeros (clock)
+        tiles = []
+        for t in range(1, 11):
+            bm, bn, bk = nat.c_int(), nat.c_int(), nat.c_int()
+            nat.call("po_conv_tile_info", t, nat.ctypes.byref(bm), nat.ctypes.byref(bn), nat.ctypes.byref(bk))
+            tiles.append((t, bm.value, bn.value, bk.value))
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        for name, args, desc in self.fwd_ops + self.bwd_ops:
+            if name != "po_conv":
+                continue
+            key = (desc.B, desc.Hin, desc.Win, desc.Cin_p, desc.Hg, desc.Wg, desc.in_step, desc.ntaps, desc.N,
+                   desc.accumulate, args[6] is not None, args[7] is not None, args[8] is not None)
+            if key in cache:
+                desc.tile = cache[key]
+                continue
+            best = None
+            for t, bm, bn, bk in tiles:
+                if bk == 32 and desc.Cin_p % 32:
+                    continue
+                if bn > max(32, desc.N):
+                    continue
+                desc.tile = t
+                for _ in range(2):
+                    lib.po_conv(*args, st)
+                e0.record()
+                for _ in range(iters):
+                    lib.po_conv(*args, st)
+                e1.record()
+                e1.synchronize()
+                ms = e0.elapsed_time(e1)
+                if best is None or ms < best[0]:
+                    best = (ms, t)
+            desc.tile = best[1]
+            cache[key] = best[1]
+        with torch.no_grad():
+            for t in bufs.values():
+                t.zero_()
+        torch.cuda.synchronize()
+
     # ---------------- execution ----------------
     def run_forward(self, x):
         """x: [B,3,H,W] contiguous CUDA float32 (NCHW).  Returns NHWC head buffers."""
@@ -465,9 +577,10 @@ class NetPlan:
                 raise RuntimeError("%s failed: %s" % (name, nat.last_error()))
         return [self.act[h] for h in self.heads]
 
-    def run_backward(self, d_heads, d_x):
+    def run_backward(self, d_heads, d_x, roi=None):
         """d_heads: NHWC gradient tensors of the head buffers (list, in head order);
-        d_x: [B,3,H,W] output buffer for the input gradient."""
+        d_x: [B,3,H,W] output buffer for the input gradient; roi: optional [B,4]
+        int32 boxes — d_x is then only computed inside them."""
         st = nat.stream()
         lib = self.lib
         for hi, h in enumerate(self.heads):
@@ -479,9 +592,13 @@ class NetPlan:
                      nat.c_void_p(self.grad[r].data_ptr()), self.cp[r], 0, M, self.cp[r], 0,
                      nat.c_void_p(mask.data_ptr()) if mask is not None else None, self.cp[r], st)
         dxp = nat.c_void_p(d_x.data_ptr())
+        roip = nat.c_void_p(roi.data_ptr()) if roi is not None else None
         for name, args, _ in self.bwd_ops:
             if args and args[-1] == "dimg":
-                args = args[:-1] + (dxp,)
+                if name == "po_conv_first_dgrad":
+                    args = args[:-2] + (roip, dxp)
+                else:
+                    args = args[:-1] + (dxp,)
             rc = getattr(lib, name)(*args, st)
             if rc:
                 raise RuntimeError("%s failed: %s" % (name, nat.last_error()))
@@ -490,9 +607,9 @@ class NetPlan:
 
 class _DarknetFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, plan, nchw):
+    def forward(ctx, x, plan, nchw, roi=None):
         heads = plan.run_forward(x.contiguous())
-        ctx.plan, ctx.gen, ctx.nchw = plan, plan.gen, nchw
+        ctx.plan, ctx.gen, ctx.nchw, ctx.roi = plan, plan.gen, nchw, roi
         if not nchw:
             return tuple(h.clone() if plan.net.clone_heads else h.detach() for h in heads)
         outs = []
@@ -522,8 +639,8 @@ class _DarknetFn(torch.autograd.Function):
                 g = gn
             d_heads.append(g.contiguous())
         d_x = torch.empty(plan.B, 3, plan.H, plan.W, device=plan.device)
-        plan.run_backward(d_heads, d_x)
-        return d_x, None, None
+        plan.run_backward(d_heads, d_x, ctx.roi)
+        return d_x, None, None, None
 
 
 class Darknet(nn.Module):
@@ -554,6 +671,7 @@ class Darknet(nn.Module):
         self._dev_device = None
         self._dgrad_cache = {}
         self._plans = {}
+        self._tile_cache = {}
 
     # ---------------- weights ----------------
     def load_darknet_weights(self, weights_path):
@@ -666,10 +784,16 @@ class Darknet(nn.Module):
         return self._dgrad_cache[key]
 
     def plan(self, B, H, W, device):
+        """The execution plan for a batch shape (built, and its conv tiles
+        autotuned on the device, on first use; ADVPATCH_TUNE=0 keeps the
+        built-in tile heuristic)."""
         self._prepare(device)
         key = (B, H, W, str(device))
         if key not in self._plans:
-            self._plans[key] = NetPlan(self, B, H, W, device)
+            p = NetPlan(self, B, H, W, device)
+            if torch.device(device).type == "cuda" and os.environ.get("ADVPATCH_TUNE", "1") != "0":
+                p.tune(self._tile_cache)
+            self._plans[key] = p
         return self._plans[key]
 
     # ---------------- forward ----------------
@@ -679,9 +803,11 @@ class Darknet(nn.Module):
         p = self.plan(x.size(0), x.size(2), x.size(3), x.device)
         return list(_DarknetFn.apply(x, p, True))
 
-    def forward_nhwc(self, x):
+    def forward_nhwc(self, x, input_roi=None):
         """Training-path forward: returns the NHWC head buffers [B, h, w, Cp]
-        (Cp = padded channel stride, channel = anchor*(5+C) + field)."""
+        (Cp = padded channel stride, channel = anchor*(5+C) + field).
+        ``input_roi`` [B,4] int32: the input gradient is only needed (and only
+        computed) inside these per-image boxes (the patch footprint)."""
         nat.ensure_device(x)
         p = self.plan(x.size(0), x.size(2), x.size(3), x.device)
-        return list(_DarknetFn.apply(x, p, False)), p
+        return list(_DarknetFn.apply(x, p, False, input_roi)), p

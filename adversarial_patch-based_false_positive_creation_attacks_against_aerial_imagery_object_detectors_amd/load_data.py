@@ -138,8 +138,8 @@ class HasSusRGB(nn.Module):
 # ---------------------------------------------------------------------------
 # Patch placement and warp
 # ---------------------------------------------------------------------------
-def patch_params(lab_batch, img_size, P, draws, do_rotate=True):
-    """(theta [B,6], patch_center [B,2], target_size [B]) on the device."""
+def patch_params(lab_batch, img_size, P, draws, do_rotate=True, with_roi=False):
+    """(theta [B,6], patch_center [B,2], target_size [B][, roi [B,4] int32]) on the device."""
     nat.ensure_device(lab_batch)
     lab = lab_batch.contiguous().float()
     B, L = lab.size(0), lab.size(1)
@@ -147,10 +147,13 @@ def patch_params(lab_batch, img_size, P, draws, do_rotate=True):
     theta = torch.empty(B, 6, device=dev)
     center = torch.empty(B, 2, device=dev)
     tsize = torch.empty(B, device=dev)
+    roi = torch.empty(B, 4, dtype=torch.int32, device=dev) if with_roi else None
     angle = draws["angle"].contiguous().float() if do_rotate else None
     nat.call("po_patch_params", nat.ptr(lab), B, L, nat.ptr(angle), nat.ptr(draws["ux"].contiguous().float()),
              nat.ptr(draws["uy"].contiguous().float()), int(bool(do_rotate)), int(img_size), int(P),
-             nat.ptr(theta), nat.ptr(center), nat.ptr(tsize), nat.stream())
+             nat.ptr(theta), nat.ptr(center), nat.ptr(tsize), nat.ptr(roi, torch.int32), nat.stream())
+    if with_roi:
+        return theta, center, tsize, roi
     return theta, center, tsize
 
 
@@ -200,6 +203,7 @@ class PatchTransformer(nn.Module):
         self.maxangle = 180 / 180 * math.pi
         self.medianpooler = MedianPool2d(7, same=True)
         self.generator = None
+        self.last_roi = None     # [B,4] int32 footprint boxes of the last placement
 
     def lab_transform(self, lab_batch_origin):
         """[B,L,5] -> [B,1,5] (load_data.py:453-478): (max-area row + min-area row)/2,
@@ -222,7 +226,8 @@ class PatchTransformer(nn.Module):
         B, P = lab_batch.size(0), mp.size(-1)
         if draws is None:
             draws = self.make_draws(B, P, adv_patch.device)
-        theta, center, _ = patch_params(lab_batch, img_size, P, draws, do_rotate)
+        theta, center, _, roi = patch_params(lab_batch, img_size, P, draws, do_rotate, with_roi=True)
+        self.last_roi = roi
         return mp, draws, theta, center
 
     def forward(self, adv_patch, lab_batch, img_size, do_rotate=True, rand_loc=False, draws=None):

@@ -174,9 +174,13 @@ class PatchTrainer(object):
         img_size = self.darknet_model.height
         p_img, center = self.patch_transformer.forward_composite(adv_patch, lab_batch, img_batch, img_size,
                                                                  do_rotate=True, draws=draws)
+        roi = self.patch_transformer.last_roi
         if p_img.size(-1) != self.darknet_model.width or p_img.size(-2) != self.darknet_model.height:
             p_img = F.interpolate(p_img, (self.darknet_model.height, self.darknet_model.width))
-        heads, plan = self.darknet_model.forward_nhwc(p_img)
+            roi = None
+        # the warp backward reads dL/dp_img only inside the patch footprint:
+        # the first conv's input gradient is computed there only
+        heads, plan = self.darknet_model.forward_nhwc(p_img, input_roi=roi)
         out2, obj, cls, cells, flags = cell_loss(heads, plan, img_size, center, TARGET_ID, objective)
         no_obj_loss, no_cls_loss = out2[0], out2[1]
         reg = regularisers(adv_patch, self.nps_calculator.colors)

