@@ -37,7 +37,9 @@ struct ConvArgs {
   int in_step, out_step, out_oy, out_ox;
   int ntaps, N, act, accumulate;
   int M, ntiles_n;
-  int dh[9], dw[9];
+  uint32_t in_bytes, w_bytes;   // buffer-resource extents (< 2^31)
+  // taps form a rectangular grid: tap t = th*tkw + tw -> (dh0 + th*sdh, dw0 + tw*sdw)
+  int tkw, dh0, dw0, sdh, sdw;
 };
 
 template <int BM, int BN, int WM, int BK>
@@ -62,53 +64,62 @@ __global__ __launch_bounds__(256) void conv_k(const ConvArgs a) {
   const int tn = wgid % a.ntiles_n, tm = wgid / a.ntiles_n;
   const int m0 = tm * BM, n0 = tn * BN;
 
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int tid = threadIdx.x & 255, lane = tid & 63, wave = tid >> 6;   // mask: lets the compiler bound rows
   const int wm = wave / WN, wn = wave % WN;
   const int HgWg = a.Hg * a.Wg;
   const int cth = tid % CPR, rth = tid / CPR;
 
-  // ---- A loader state (rows rth + RPP*r of the tile)
+  // ---- buffer resources over the input tensor and the weights: an offset at or
+  // beyond num_records reads zero in hardware, so out-of-image taps and ragged
+  // tile rows need neither branches nor clamped addresses
+  const uint32_t in_bytes = (uint32_t)__builtin_amdgcn_readfirstlane(a.in_bytes);
+  const uint32_t w_bytes = (uint32_t)__builtin_amdgcn_readfirstlane(a.w_bytes);
+  const __amdgpu_buffer_rsrc_t in_rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(a.in), 0, in_bytes, 0x00020000);
+  const __amdgpu_buffer_rsrc_t w_rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(a.W), 0, w_bytes, 0x00020000);
+  constexpr uint32_t kOOB = 0x80000000u;
+  const uint32_t pix_bytes = (uint32_t)a.Cin_p * 4u;
+
+  // ---- A loader state (rows rth + RPP*r of the tile): byte offset of the
+  // row's first channel chunk at tap (0,0); hi/wi for the bounds test
   int a_hi[AL], a_wi[AL];
-  const float* a_img[AL];
-  bool a_ok[AL];
+  uint32_t a_off[AL];
 #pragma unroll
   for (int r = 0; r < AL; ++r) {
     const int row = rth + RPP * r;
     const int m = m0 + row;
-    a_ok[r] = (row < BM) && (m < a.M);
-    const int mm = a_ok[r] ? m : 0;
+    const bool ok = (row < BM) && (m < a.M);
+    const int mm = ok ? m : 0;
     const int b = mm / HgWg, rem = mm - b * HgWg;
     const int i = rem / a.Wg, j = rem - i * a.Wg;
-    a_img[r] = a.in + (size_t)b * a.Hin * a.Win * a.Cin_p + cth * 4;
-    a_hi[r] = i * a.in_step;
+    a_off[r] = ((uint32_t)b * a.Hin * a.Win) * pix_bytes + cth * 16u;
+    // a row outside the GEMM gets a position no tap can bring into the image
+    a_hi[r] = ok ? i * a.in_step : -(1 << 20);
     a_wi[r] = j * a.in_step;
   }
   // ---- B loader state
-  const size_t wrow = (size_t)a.ntaps * a.Cin_p;
-  bool b_ok[BL];
-  const float* b_ptr[BL];
+  const uint32_t wrow_bytes = (uint32_t)a.ntaps * pix_bytes;
+  uint32_t b_off[BL];
 #pragma unroll
   for (int r = 0; r < BL; ++r) {
     const int row = rth + RPP * r;
-    b_ok[r] = (row < BN) && (n0 + row < a.N);
-    b_ptr[r] = a.W + (size_t)(b_ok[r] ? n0 + row : 0) * wrow + cth * 4;
+    const bool ok = (row < BN) && (n0 + row < a.N);
+    b_off[r] = ok ? (uint32_t)(n0 + row) * wrow_bytes + cth * 16u : kOOB;
   }
 
   float4 ra[AL], rb[BL];
-  auto gload = [&](int tap, int c0) {
-    const int dh = a.dh[tap], dw = a.dw[tap];
+  auto gload = [&](int tap, int dh, int dw, int c0) {
+    const uint32_t cb = (uint32_t)c0 * 4u;
 #pragma unroll
     for (int r = 0; r < AL; ++r) {
       const int hi = a_hi[r] + dh, wi = a_wi[r] + dw;
-      if (a_ok[r] && hi >= 0 && hi < a.Hin && wi >= 0 && wi < a.Win)
-        ra[r] = *reinterpret_cast<const float4*>(a_img[r] + ((size_t)hi * a.Win + wi) * a.Cin_p + c0);
-      else
-        ra[r] = make_float4(0.f, 0.f, 0.f, 0.f);
+      const bool ok = (unsigned)hi < (unsigned)a.Hin && (unsigned)wi < (unsigned)a.Win;
+      const uint32_t off = ok ? a_off[r] + ((uint32_t)hi * a.Win + wi) * pix_bytes + cb : kOOB;
+      ra[r] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(in_rs, off, 0, 0));
     }
+    const uint32_t tb = (uint32_t)tap * pix_bytes + cb;
 #pragma unroll
     for (int r = 0; r < BL; ++r)
-      rb[r] = b_ok[r] ? *reinterpret_cast<const float4*>(b_ptr[r] + (size_t)tap * a.Cin_p + c0)
-                      : make_float4(0.f, 0.f, 0.f, 0.f);
+      rb[r] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(w_rs, b_off[r] + tb, 0, 0));
   };
   auto swz = [](int row, int chunk) { return (chunk ^ ((row >> SW) & (CPR - 1))) * 4; };
   auto sstore = [&](int buf) {
@@ -136,8 +147,9 @@ __global__ __launch_bounds__(256) void conv_k(const ConvArgs a) {
 
   const int kc = a.Cin_p / BK;
   const int nks = a.ntaps * kc;
-  int tap = 0, c0 = 0;
-  gload(0, 0);
+  // k-step position: tap (th, tw) and channel offset c0, advanced incrementally
+  int tap = 0, th = 0, tw = 0, c0 = 0;
+  gload(0, a.dh0, a.dw0, 0);
   sstore(0);
   __syncthreads();
   const int arow = wm * TM * 32 + (lane & 31);
@@ -146,11 +158,6 @@ __global__ __launch_bounds__(256) void conv_k(const ConvArgs a) {
   for (int ks = 0; ks < nks; ++ks) {
     const int buf = ks & 1;
     const bool more = ks + 1 < nks;
-    if (more) {
-      c0 += BK;
-      if (c0 == a.Cin_p) { c0 = 0; ++tap; }
-      gload(tap, c0);
-    }
     const float* Ab = As + buf * BM * BK;
     const float* Bb = Bs + buf * BN * BK;
 #pragma unroll
@@ -165,6 +172,16 @@ __global__ __launch_bounds__(256) void conv_k(const ConvArgs a) {
       for (int j = 0; j < TN; ++j) {
         const int row = brow + j * 32;
         bf[j] = *reinterpret_cast<const float4*>(&Bb[row * BK + swz(row, 2 * g + h)]);
+      }
+      if (g == 0 && more) {
+        // issue the next k-step's staging loads behind this group's fragment reads
+        c0 += BK;
+        if (c0 == a.Cin_p) {
+          c0 = 0;
+          ++tap;
+          if (++tw == a.tkw) { tw = 0; ++th; }
+        }
+        gload(tap, a.dh0 + th * a.sdh, a.dw0 + tw * a.sdw, c0);
       }
 #pragma unroll
       for (int i = 0; i < TM; ++i)
@@ -277,10 +294,26 @@ extern "C" int po_conv(const po_conv_desc* d, const float* in, const float* W, c
   a.ntaps = d->ntaps; a.N = d->N; a.act = d->act; a.accumulate = d->accumulate;
   a.M = d->B * d->Hg * d->Wg;
   a.ntiles_n = 1;
-  for (int t = 0; t < 9; ++t) {
-    a.dh[t] = t < d->ntaps ? d->dh[t] : 0;
-    a.dw[t] = t < d->ntaps ? d->dw[t] : 0;
-  }
+  const int64_t in_bytes = (int64_t)d->B * d->Hin * d->Win * d->Cin_p * 4;
+  const int64_t w_bytes = (int64_t)d->N * d->ntaps * d->Cin_p * 4;
+  PO_REQUIRE(in_bytes < (1LL << 31) && w_bytes < (1LL << 31),
+             "po_conv: input (%lld B) and weights (%lld B) must each be < 2 GiB (32-bit buffer offsets)",
+             (long long)in_bytes, (long long)w_bytes);
+  a.in_bytes = (uint32_t)in_bytes;
+  a.w_bytes = (uint32_t)w_bytes;
+  // the tap list must be a rectangular grid, row-major, with constant steps
+  int tkw = 1;
+  while (tkw < d->ntaps && d->dh[tkw] == d->dh[0]) ++tkw;
+  PO_REQUIRE(d->ntaps % tkw == 0, "po_conv: taps are not a rectangular grid");
+  const int tkh = d->ntaps / tkw;
+  a.tkw = tkw;
+  a.dh0 = d->dh[0];
+  a.dw0 = d->dw[0];
+  a.sdh = tkh > 1 ? d->dh[tkw] - d->dh[0] : 0;
+  a.sdw = tkw > 1 ? d->dw[1] - d->dw[0] : 0;
+  for (int t = 0; t < d->ntaps; ++t)
+    PO_REQUIRE(d->dh[t] == a.dh0 + (t / tkw) * a.sdh && d->dw[t] == a.dw0 + (t % tkw) * a.sdw,
+               "po_conv: tap %d (%d,%d) breaks the rectangular tap grid", t, d->dh[t], d->dw[t]);
   hipStream_t st = po::stream_of(s);
   int bm, bn, bk;
   PO_REQUIRE(d->tile >= 0 && d->tile <= PO_CONV_NTILES, "po_conv: tile %d out of range", d->tile);

@@ -792,7 +792,20 @@ class Darknet(nn.Module):
         if key not in self._plans:
             p = NetPlan(self, B, H, W, device)
             if torch.device(device).type == "cuda" and os.environ.get("ADVPATCH_TUNE", "1") != "0":
+                path = os.environ.get("ADVPATCH_TUNE_CACHE")
+                if path and os.path.exists(path) and not self._tile_cache:
+                    import json
+                    with open(path) as f:
+                        self._tile_cache.update({tuple(json.loads(k)): v for k, v in json.load(f).items()})
+                n0 = len(self._tile_cache)
                 p.tune(self._tile_cache)
+                if path and len(self._tile_cache) != n0:
+                    import json
+                    os.makedirs(os.path.dirname(os.path.abspath(path)), exist_ok=True)
+                    tmp = "%s.%d.tmp" % (path, os.getpid())
+                    with open(tmp, "w") as f:
+                        json.dump({json.dumps(list(k)): v for k, v in self._tile_cache.items()}, f)
+                    os.replace(tmp, path)
             self._plans[key] = p
         return self._plans[key]
 

@@ -86,7 +86,7 @@ def cpu_baseline(cfg, S, P, seconds_budget=25.0):
     while True:
         oracle.train_step(patch, img, lab, dr, net, colors)
         n += 1
-        if time.time() - t0 > seconds_budget or n >= 8:
+        if time.time() - t0 > seconds_budget or n >= 40:
             break
     el = time.time() - t0
     cpu = platform.processor() or platform.machine()
@@ -111,17 +111,23 @@ def main():
     ap.add_argument("--batch", type=int, default=None, help="per-GPU batch")
     ap.add_argument("--config", default="yolov3", choices=sorted(CONFIGS))
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--dist-backend", default="nccl", help="nccl (= RCCL); gloo only to rehearse ranks on one GPU")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    ndev = torch.cuda.device_count()
     if world > 1:
-        torch.cuda.set_device(local)
-        torch.distributed.init_process_group("nccl", device_id=torch.device("cuda", local))
-    dev = torch.device("cuda", local)
+        torch.cuda.set_device(local % ndev)
+        if args.dist_backend == "nccl":
+            torch.distributed.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            torch.distributed.init_process_group(args.dist_backend)
+    dev = torch.device("cuda", local % ndev)
     cfg, S, P, Bdef = CONFIGS[args.config]
     B = args.batch or Bdef
+    os.environ.setdefault("ADVPATCH_TUNE_CACHE", os.path.join(ROOT, "weights", "conv_tiles_%s_b%d.json" % (args.config, B)))
 
     tp, pc, sy, W = ge._pkg("train_patch"), ge._pkg("patch_config"), ge._pkg("synthetic"), ge._pkg("weights")
     wpath = pc.synthetic_weights_path(cfg.split(":")[-1])
