@@ -19,7 +19,8 @@ class po_conv_desc(ctypes.Structure):
         "B", "Hin", "Win", "Cin_p", "Hout", "Wout", "Cout_p", "Hg", "Wg",
         "in_step", "out_step", "out_oy", "out_ox", "ntaps")] + [
         ("dh", c_int * 9), ("dw", c_int * 9),
-        ("N", c_int), ("act", c_int), ("accumulate", c_int), ("tile", c_int)]
+        ("N", c_int), ("act", c_int), ("accumulate", c_int), ("tile", c_int),
+        ("in_org", c_void_p), ("out_org", c_void_p)]
 
 
 _SIGS = {
@@ -37,8 +38,10 @@ _SIGS = {
     "po_apply_bwd": [c_void_p, c_void_p, c_int64, c_void_p, c_void_p, c_void_p],
     "po_regularisers": [c_void_p, c_int, c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_void_p,
                         c_void_p],
-    "po_cell_loss": [c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_int, c_int, c_void_p,
-                     c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p],
+    "po_cell_loss": [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_int,
+                     c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p],
+    "po_cell_windows": [c_void_p, c_int, c_int, c_int, c_void_p, c_int, c_void_p, c_int, c_void_p, c_void_p,
+                        c_void_p, c_void_p],
     "po_conv": [ctypes.POINTER(po_conv_desc), c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
                 c_void_p, c_void_p, c_void_p, c_void_p, c_void_p],
     "po_conv_tile_info": [c_int, ctypes.POINTER(c_int), ctypes.POINTER(c_int), ctypes.POINTER(c_int)],
@@ -48,6 +51,8 @@ _SIGS = {
                             c_void_p, c_void_p],
     "po_slice_accum": [c_void_p, c_int, c_int, c_void_p, c_int, c_int, c_int64, c_int, c_int,
                        c_void_p, c_int, c_void_p],
+    "po_view_move": [c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_int, c_int, c_int, c_int,
+                     c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_int, c_void_p],
     "po_upsample2_fwd": [c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p, c_int, c_int, c_void_p],
     "po_upsample2_bwd": [c_void_p, c_int, c_int, c_int, c_int, c_int, c_int, c_void_p, c_int, c_int,
                          c_void_p, c_int, c_void_p],

@@ -28,6 +28,34 @@ inline int ceil_div(int64_t a, int64_t b) { return (int)((a + b - 1) / b); }
 __device__ __forceinline__ float leaky_grad(float y) { return y > 0.f ? 1.f : 0.1f; }
 __device__ __forceinline__ float leaky(float v) { return v > 0.f ? v : v * 0.1f; }
 
+// torch.div(a, b, rounding_mode='floor') for float32 (ATen div_floor)
+__device__ __forceinline__ float div_floor(float a, float b) {
+  float mod = fmodf(a, b);
+  float div = (a - mod) / b;
+  if (mod != 0.f && ((b < 0.f) != (mod < 0.f))) div -= 1.f;
+  float fl;
+  if (div != 0.f) {
+    fl = floorf(div);
+    if (div - fl > 0.5f) fl += 1.f;
+  } else {
+    fl = copysignf(0.f, a / b);
+  }
+  return fl;
+}
+
+// Flat cell index of the patch centre (cx = column px, cy = row px) on a
+// hw x hw head (train_patch.py:446-467; SURVEY Q1: index = ix*hw + iy).
+// Sets *oob and clamps when the index leaves the map.
+__device__ __forceinline__ int head_cell(float cx, float cy, int S, int hw, bool* oob) {
+  const float stride = (float)((double)S / (double)hw);       // train_patch.py:446
+  const int ix = (int)div_floor(cx, stride);                   // 449-450, 463
+  const int iy = (int)div_floor(cy, stride);                   // 464
+  int index = ix * hw + iy;                                    // 467
+  *oob = index < 0 || index >= hw * hw;
+  if (*oob) index = index < 0 ? 0 : hw * hw - 1;
+  return index;
+}
+
 }  // namespace po
 
 #define PO_REQUIRE(cond, ...)          \

@@ -33,6 +33,8 @@ struct ConvArgs {
   const float* mask;
   float* y2;
   const float* mask2;
+  const int32_t* in_org;        // window origins [B,2] (NULL: full map)
+  const int32_t* out_org;
   int B, Hin, Win, Cin_p, Hout, Wout, Cout_p, Hg, Wg;
   int in_step, out_step, out_oy, out_ox;
   int ntaps, N, act, accumulate;
@@ -92,9 +94,13 @@ __global__ __launch_bounds__(256) void conv_k(const ConvArgs a) {
     const int b = mm / HgWg, rem = mm - b * HgWg;
     const int i = rem / a.Wg, j = rem - i * a.Wg;
     a_off[r] = ((uint32_t)b * a.Hin * a.Win) * pix_bytes + cth * 16u;
+    // window buffers: shift from output-buffer to input-buffer coordinates
+    int sy = 0, sx = 0;
+    if (a.out_org) { sy += a.out_org[2 * b]; sx += a.out_org[2 * b + 1]; }
+    if (a.in_org) { sy -= a.in_org[2 * b]; sx -= a.in_org[2 * b + 1]; }
     // a row outside the GEMM gets a position no tap can bring into the image
-    a_hi[r] = ok ? i * a.in_step : -(1 << 20);
-    a_wi[r] = j * a.in_step;
+    a_hi[r] = ok ? i * a.in_step + sy : -(1 << 20);
+    a_wi[r] = j * a.in_step + sx;
   }
   // ---- B loader state
   const uint32_t wrow_bytes = (uint32_t)a.ntaps * pix_bytes;
@@ -288,6 +294,10 @@ extern "C" int po_conv(const po_conv_desc* d, const float* in, const float* W, c
   ConvArgs a;
   a.in = in; a.W = W; a.bias = bias; a.y = y_out; a.res = res; a.sum = sum_out; a.mask = mask_y;
   a.y2 = y2_out; a.mask2 = mask2;
+  a.in_org = d->in_org; a.out_org = d->out_org;
+  if (d->in_org || d->out_org)
+    PO_REQUIRE(d->in_step == 1 && d->out_step == 1 && d->out_oy == 0 && d->out_ox == 0,
+               "po_conv: window buffers need in_step = out_step = 1 and no output offset");
   a.B = d->B; a.Hin = d->Hin; a.Win = d->Win; a.Cin_p = d->Cin_p;
   a.Hout = d->Hout; a.Wout = d->Wout; a.Cout_p = d->Cout_p; a.Hg = d->Hg; a.Wg = d->Wg;
   a.in_step = d->in_step; a.out_step = d->out_step; a.out_oy = d->out_oy; a.out_ox = d->out_ox;

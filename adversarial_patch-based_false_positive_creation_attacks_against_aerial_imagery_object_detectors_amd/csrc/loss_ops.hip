@@ -15,27 +15,13 @@ constexpr int MAXB = 4096;
 struct LossArgs {
   const float* heads[MAXH];
   float* dheads[MAXH];
-  int hw[MAXH];
+  const int32_t* org[MAXH];   // window origin [B,2] or NULL (full map)
+  int hw[MAXH], win[MAXH];    // map side, stored side
   int nheads, Cp, B, S, target, objective;
   const float* g2;
 };
 
 __device__ __forceinline__ float sigm(float x) { return 1.f / (1.f + expf(-x)); }
-
-// torch.div(a, b, rounding_mode='floor') for float32 (ATen div_floor)
-__device__ __forceinline__ float div_floor(float a, float b) {
-  float mod = fmodf(a, b);
-  float div = (a - mod) / b;
-  if (mod != 0.f && ((b < 0.f) != (mod < 0.f))) div -= 1.f;
-  float fl;
-  if (div != 0.f) {
-    fl = floorf(div);
-    if (div - fl > 0.5f) fl += 1.f;
-  } else {
-    fl = copysignf(0.f, a / b);
-  }
-  return fl;
-}
 
 __global__ __launch_bounds__(256) void cell_loss_k(LossArgs a, const float* __restrict__ center,
                                                    float* __restrict__ out2, float* __restrict__ obj_out,
@@ -51,23 +37,28 @@ __global__ __launch_bounds__(256) void cell_loss_k(LossArgs a, const float* __re
   const float g_obj = a.g2 ? a.g2[0] : 0.f, g_cls = a.g2 ? a.g2[1] : 0.f;
   for (int b = threadIdx.x; b < a.B; b += blockDim.x) {
     float obj[3 * MAXH];
-    int idx[MAXH];
     float best = 0.f;
     int kbest = -1;
     float cls_term = 0.f;
+    size_t off[MAXH];
     for (int h = 0; h < a.nheads; ++h) {
       const int hw = a.hw[h];
-      const float stride = (float)((double)a.S / (double)hw);       // train_patch.py:446
-      const int ix = (int)div_floor(center[2 * b + 0], stride);     // 449-450, 463
-      const int iy = (int)div_floor(center[2 * b + 1], stride);     // 464
-      int index = ix * hw + iy;                                      // 467
-      if (index < 0 || index >= hw * hw) {
-        atomicOr(&s_flag, 1);
-        index = index < 0 ? 0 : hw * hw - 1;
-      }
-      idx[h] = index;
+      bool oob;
+      const int index = po::head_cell(center[2 * b + 0], center[2 * b + 1], a.S, hw, &oob);
+      if (oob) atomicOr(&s_flag, 1);
       if (cells) cells[h * a.B + b] = index;
-      const float* cell = a.heads[h] + ((size_t)b * hw * hw + index) * a.Cp;
+      int r = index / hw, c = index - (index / hw) * hw;
+      if (a.org[h]) {
+        r -= a.org[h][2 * b];
+        c -= a.org[h][2 * b + 1];
+        if (r < 0 || r >= a.win[h] || c < 0 || c >= a.win[h]) {
+          atomicOr(&s_flag, 2);
+          r = min(max(r, 0), a.win[h] - 1);
+          c = min(max(c, 0), a.win[h] - 1);
+        }
+      }
+      off[h] = (((size_t)b * a.win[h] + r) * a.win[h] + c) * a.Cp;
+      const float* cell = a.heads[h] + off[h];
       for (int an = 0; an < 3; ++an) {
         const int k = h * 3 + an;
         const float* f = cell + an * NF;
@@ -83,7 +74,7 @@ __global__ __launch_bounds__(256) void cell_loss_k(LossArgs a, const float* __re
           if (cls_out) cls_out[((size_t)b * A + k) * NCLS + c] = p[c];
           if (p[c] > mx) { mx = p[c]; cmax = c; }
         }
-        float* dcell = a.dheads[h] ? a.dheads[h] + ((size_t)b * hw * hw + index) * a.Cp + an * NF : nullptr;
+        float* dcell = a.dheads[h] ? a.dheads[h] + off[h] + an * NF : nullptr;
         if (a.objective == 0) {
           // CrossEntropyLoss on probabilities (train_patch.py:534-546)
           float se = 0.f;
@@ -119,7 +110,7 @@ __global__ __launch_bounds__(256) void cell_loss_k(LossArgs a, const float* __re
     // objectness gradient: d/d obj[kbest] of 4*(1 - mean_b max_k obj) = -4/B
     const int h = kbest / 3, an = kbest % 3;
     if (a.dheads[h]) {
-      float* dcell = a.dheads[h] + ((size_t)b * a.hw[h] * a.hw[h] + idx[h]) * a.Cp + an * NF;
+      float* dcell = a.dheads[h] + off[h] + an * NF;
       const float o = obj[kbest];
       dcell[4] = (-4.f * invB * g_obj) * o * (1.f - o);
     }
@@ -138,7 +129,8 @@ __global__ __launch_bounds__(256) void cell_loss_k(LossArgs a, const float* __re
 }
 }  // namespace
 
-extern "C" int po_cell_loss(const float* const* heads, const int* hw, int nheads, int Cp, int B, int S,
+extern "C" int po_cell_loss(const float* const* heads, const int* hw, const int* win,
+                            const int32_t* const* org, int nheads, int Cp, int B, int S,
                             const float* center, int target, int objective, const float* g2,
                             float* const* d_heads, float* out2, float* obj_out, float* cls_out,
                             int32_t* cells, int32_t* flags, po_stream_t s) {
@@ -151,10 +143,17 @@ extern "C" int po_cell_loss(const float* const* heads, const int* hw, int nheads
   PO_REQUIRE(!d_heads || g2, "po_cell_loss: g2 required with d_heads");
   LossArgs a;
   for (int h = 0; h < MAXH; ++h) {
-    a.heads[h] = h < nheads ? heads[h] : nullptr;
-    a.dheads[h] = (d_heads && h < nheads) ? d_heads[h] : nullptr;
-    a.hw[h] = h < nheads ? hw[h] : 1;
-    if (h < nheads) PO_REQUIRE(heads[h] && hw[h] > 0, "po_cell_loss: bad head %d", h);
+    const bool on = h < nheads;
+    a.heads[h] = on ? heads[h] : nullptr;
+    a.dheads[h] = (d_heads && on) ? d_heads[h] : nullptr;
+    a.hw[h] = on ? hw[h] : 1;
+    a.org[h] = (org && on) ? org[h] : nullptr;
+    a.win[h] = a.org[h] ? (win ? win[h] : 0) : a.hw[h];
+    if (on) {
+      PO_REQUIRE(heads[h] && hw[h] > 0, "po_cell_loss: bad head %d", h);
+      PO_REQUIRE(a.win[h] > 0 && a.win[h] <= hw[h], "po_cell_loss: head %d window side %d (map %d)", h,
+                 a.win[h], hw[h]);
+    }
   }
   a.nheads = nheads;
   a.Cp = Cp;
@@ -166,4 +165,64 @@ extern "C" int po_cell_loss(const float* const* heads, const int* hw, int nheads
   hipLaunchKernelGGL(cell_loss_k, dim3(1), dim3(256), 0, po::stream_of(s), a, center, out2, obj_out,
                      cls_out, cells, flags);
   return po::check_launch("po_cell_loss");
+}
+
+// ---------------------------------------------------------------------------
+// Receptive-field windows: one thread per (window, image).
+namespace {
+struct WinArgs {
+  int hw[MAXH];
+  int nheads, nwin, maxhw, B, S;
+};
+
+__global__ __launch_bounds__(256) void cell_windows_k(WinArgs a, const float* __restrict__ center,
+                                                      const int32_t* __restrict__ lut,
+                                                      const int32_t* __restrict__ ext,
+                                                      int32_t* __restrict__ org, int32_t* __restrict__ flags) {
+  const int t = blockIdx.x * 256 + threadIdx.x;
+  if (t >= a.nwin * a.B) return;
+  const int w = t / a.B, b = t - w * a.B;
+  int lo_r = 1 << 30, hi_r = -(1 << 30), lo_c = 1 << 30, hi_c = -(1 << 30);
+  for (int h = 0; h < a.nheads; ++h) {
+    bool oob;
+    const int index = po::head_cell(center[2 * b + 0], center[2 * b + 1], a.S, a.hw[h], &oob);
+    const int r = index / a.hw[h], c = index - r * a.hw[h];
+    const int32_t* e = lut + ((size_t)(w * a.nheads + h) * a.maxhw) * 2;
+    if (e[2 * r] <= e[2 * r + 1]) {
+      lo_r = min(lo_r, e[2 * r]);
+      hi_r = max(hi_r, e[2 * r + 1]);
+    }
+    if (e[2 * c] <= e[2 * c + 1]) {
+      lo_c = min(lo_c, e[2 * c]);
+      hi_c = max(hi_c, e[2 * c + 1]);
+    }
+  }
+  const int side = ext[2 * w], map = ext[2 * w + 1];
+  if (lo_r > hi_r) { lo_r = 0; hi_r = 0; }
+  if (lo_c > hi_c) { lo_c = 0; hi_c = 0; }
+  if (flags && (hi_r - lo_r + 1 > side || hi_c - lo_c + 1 > side)) atomicOr(flags, 4);
+  org[2 * t] = min(max(lo_r, 0), map - side);
+  org[2 * t + 1] = min(max(lo_c, 0), map - side);
+}
+}  // namespace
+
+extern "C" int po_cell_windows(const float* center, int B, int S, int nheads, const int* hw, int nwin,
+                               const int32_t* lut, int maxhw, const int32_t* ext, int32_t* org,
+                               int32_t* flags, po_stream_t s) {
+  PO_REQUIRE(center && hw && lut && ext && org, "po_cell_windows: null pointer");
+  PO_REQUIRE(nheads >= 1 && nheads <= MAXH && nwin >= 1 && B >= 1, "po_cell_windows: bad sizes");
+  WinArgs a;
+  for (int h = 0; h < MAXH; ++h) {
+    a.hw[h] = h < nheads ? hw[h] : 1;
+    if (h < nheads) PO_REQUIRE(hw[h] >= 1 && hw[h] <= maxhw, "po_cell_windows: head %d side %d > maxhw %d", h,
+                               hw[h], maxhw);
+  }
+  a.nheads = nheads;
+  a.nwin = nwin;
+  a.maxhw = maxhw;
+  a.B = B;
+  a.S = S;
+  hipLaunchKernelGGL(cell_windows_k, dim3(po::ceil_div((int64_t)nwin * B, 256)), dim3(256), 0,
+                     po::stream_of(s), a, center, lut, ext, org, flags);
+  return po::check_launch("po_cell_windows");
 }

@@ -19,6 +19,37 @@ __global__ __launch_bounds__(256) void slice_accum_k(const float* __restrict__ s
   *d = v;
 }
 
+// window <-> full-map moves (po_view_move): one thread per dst element
+__global__ __launch_bounds__(256) void view_move_k(const float* __restrict__ src, int Hs, int Ws, int ss, int so,
+                                                   const int32_t* __restrict__ sorg, float* __restrict__ dst,
+                                                   int Hd, int Wd, int ds, int doff,
+                                                   const int32_t* __restrict__ dorg, int B, int C, int mode,
+                                                   int acc, const float* __restrict__ my, int ms) {
+  const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const int64_t tot = (int64_t)B * Hd * Wd * C;
+  if (t >= tot) return;
+  const int c = (int)(t % C);
+  const int64_t p = t / C;
+  const int x = (int)(p % Wd);
+  const int y = (int)((p / Wd) % Hd);
+  const int b = (int)(p / ((int64_t)Wd * Hd));
+  const int py = y + (dorg ? dorg[2 * b] : 0), px = x + (dorg ? dorg[2 * b + 1] : 0);   // map position
+  const int oy = sorg ? sorg[2 * b] : 0, ox = sorg ? sorg[2 * b + 1] : 0;
+  auto at = [&](int my_, int mx_) -> float {      // src at map position, 0 outside the buffer
+    const int ly = my_ - oy, lx = mx_ - ox;
+    if (ly < 0 || ly >= Hs || lx < 0 || lx >= Ws) return 0.f;
+    return src[(((int64_t)b * Hs + ly) * Ws + lx) * ss + so + c];
+  };
+  float v;
+  if (mode == 0) v = at(py, px);
+  else if (mode == 1) v = at(py >> 1, px >> 1);
+  else v = (at(2 * py, 2 * px) + at(2 * py, 2 * px + 1)) + (at(2 * py + 1, 2 * px) + at(2 * py + 1, 2 * px + 1));
+  float* d = dst + p * ds + doff + c;
+  if (acc) v += *d;
+  if (my) v *= po::leaky_grad(my[p * ms + c]);
+  *d = v;
+}
+
 __global__ __launch_bounds__(256) void up2_fwd_k(const float* __restrict__ src, int B, int H, int W,
                                                  int C, int ss, float* __restrict__ dst, int ds,
                                                  int doff) {
@@ -148,6 +179,22 @@ extern "C" int po_slice_accum(const float* src, int src_stride, int src_off, flo
   hipLaunchKernelGGL(slice_accum_k, dim3(po::ceil_div(M * C, 256)), dim3(256), 0, po::stream_of(s), src,
                      src_stride, src_off, dst, dst_stride, dst_off, M, C, accumulate, mask_y, mask_stride);
   return po::check_launch("po_slice_accum");
+}
+
+extern "C" int po_view_move(const float* src, int Hs, int Ws, int src_stride, int src_off,
+                            const int32_t* src_org, float* dst, int Hd, int Wd, int dst_stride, int dst_off,
+                            const int32_t* dst_org, int B, int C, int mode, int accumulate,
+                            const float* mask_y, int mask_stride, po_stream_t s) {
+  PO_REQUIRE(src && dst && B > 0 && C >= 0 && Hs > 0 && Ws > 0 && Hd > 0 && Wd > 0, "po_view_move: bad argument");
+  PO_REQUIRE(mode >= 0 && mode <= 2, "po_view_move: mode %d", mode);
+  PO_REQUIRE(src_off + C <= src_stride && dst_off + C <= dst_stride, "po_view_move: slice exceeds stride");
+  PO_REQUIRE(!mask_y || C <= mask_stride, "po_view_move: mask stride");
+  const int64_t tot = (int64_t)B * Hd * Wd * C;
+  if (!tot) return PO_OK;
+  hipLaunchKernelGGL(view_move_k, dim3(po::ceil_div(tot, 256)), dim3(256), 0, po::stream_of(s), src, Hs, Ws,
+                     src_stride, src_off, src_org, dst, Hd, Wd, dst_stride, dst_off, dst_org, B, C, mode,
+                     accumulate, mask_y, mask_stride);
+  return po::check_launch("po_view_move");
 }
 
 extern "C" int po_upsample2_fwd(const float* src, int B, int H, int W, int C, int src_stride, float* dst,

@@ -160,9 +160,10 @@ INPUT = -1
 class NetPlan:
     """All buffers and launch lists of one (B, H, W, device) configuration."""
 
-    def __init__(self, net, B, H, W, device):
+    def __init__(self, net, B, H, W, device, windowed=False):
         self.net, self.B, self.H, self.W, self.device = net, B, H, W, device
         self.gen = 0
+        self.conv_timer = None        # list: (start, end, MACs) HIP events of every po_conv launch
         blocks = net.blocks
         n = len(blocks)
         self.n = n
@@ -220,12 +221,21 @@ class NetPlan:
         self.shp, self.root, self.srcs, self.fused = shp, root, srcs, fused
         self.cp = [_cp(s[2]) for s in shp]
         dev = device
-        z = lambda i: torch.zeros(B, shp[i][0], shp[i][1], self.cp[i], device=dev)
+        self.win = [None] * n          # window side of a block's buffer (None: full map)
+        self.win_idx = {}              # block -> row of self.org
+        self.windowed = False
+        if windowed:
+            self._plan_windows()
+        self.dims = [(self.win[i], self.win[i]) if self.win[i] else shp[i][:2] for i in range(n)]
+        for i in range(n):
+            if root[i] != i:
+                self.dims[i] = self.dims[root[i]]
+        z = lambda i: torch.zeros(B, self.dims[i][0], self.dims[i][1], self.cp[i], device=dev)
         self.act = [z(i) if root[i] == i else None for i in range(n)]
         for i in range(n):
             if self.act[i] is None:
                 self.act[i] = self.act[root[i]]
-        self.argmax = {i: torch.zeros(B, shp[i][0], shp[i][1], self.cp[i], dtype=torch.int8, device=dev)
+        self.argmax = {i: torch.zeros(B, self.dims[i][0], self.dims[i][1], self.cp[i], dtype=torch.int8, device=dev)
                        for i, d in enumerate(blocks) if d["type"] == "maxpool"}
         first = blocks[0]
         self.first_direct = (first["type"] == "convolutional" and net._conv_meta[0]["k"] == 3
@@ -233,6 +243,148 @@ class NetPlan:
         self.in_nhwc = None if self.first_direct else torch.zeros(B, H, W, 16, device=dev)
         self._build_grad_plan()
         self._build_ops()
+
+    # ---------------- receptive-field windows ----------------
+    def _cone(self, seed):
+        """Map intervals (one axis) of every block needed for the loss to see
+        the head cells in ``seed`` {block: (lo, hi)}; propagated backwards
+        through the graph (conv: dilation by its window, upsample: /2,
+        route/shortcut: same box)."""
+        blocks, root, srcs, shp = self.net.blocks, self.root, self.srcs, self.shp
+        need = dict(seed)
+
+        def push(s, a, b):
+            if s == INPUT:
+                return
+            a, b = max(a, 0), min(b, shp[s][0] - 1)
+            if a > b:
+                return
+            need[s] = (min(need[s][0], a), max(need[s][1], b)) if s in need else (a, b)
+
+        for j in range(self.n - 1, -1, -1):
+            if root[j] != j or j not in need:
+                continue
+            lo, hi = need[j]
+            t = blocks[j]["type"]
+            if t == "convolutional":
+                m = self.net._conv_meta[j]
+                push(srcs[j][0], lo * m["stride"] - m["pad"], hi * m["stride"] - m["pad"] + m["k"] - 1)
+            elif t == "maxpool":
+                if int(blocks[j]["stride"]) == 2:
+                    push(srcs[j][0], 2 * lo, 2 * hi + 1)
+                else:
+                    push(srcs[j][0], lo, hi + 1)
+            elif t == "upsample":
+                push(srcs[j][0], lo // 2, hi // 2)
+            elif t in ("route", "shortcut"):
+                for s_ in srcs[j]:
+                    push(s_, lo, hi)
+        return need
+
+    def head_cells(self, v):
+        """Head cells (one axis) of a patch-centre coordinate v, as po_cell_loss
+        computes them (float32 floor division by S/hw, train_patch.py:446-450)."""
+        out = []
+        for h in self.heads:
+            hw = self.shp[self.root[h]][0]
+            stride = np.float32(self.H / hw)
+            out.append(int(min(max(np.floor(np.float32(v) / stride), 0), hw - 1)))
+        return out
+
+    def _plan_windows(self):
+        """Choose the blocks computed only on a box around the head cells.
+
+        The loss reads every head at one cell per image (train_patch.py:449-483),
+        so a block downstream of the last full-map dependency only matters on
+        the union of the head cells' receptive-field cones.  A block is
+        windowed when that box (its static side = the largest box over every
+        patch-centre position) is smaller than its map and nothing forces it
+        dense: shortcut blocks and their operands, maxpool, strided convs and
+        every source of a dense block keep full maps."""
+        blocks, root, srcs, shp, n = self.net.blocks, self.root, self.srcs, self.shp, self.n
+        if self.H != self.W or not self.heads:
+            return
+        hroots = [root[h] for h in self.heads]
+        hws = [shp[r][0] for r in hroots]
+        maxhw = max(hws)
+        nh = len(hroots)
+        BIG = 1 << 30
+        lo_t = np.full((n, nh, maxhw), BIG, dtype=np.int64)
+        hi_t = np.full((n, nh, maxhw), -BIG, dtype=np.int64)
+        for h, (r, hw) in enumerate(zip(hroots, hws)):
+            for c in range(hw):
+                for j, (lo, hi) in self._cone({r: (c, c)}).items():
+                    lo_t[j, h, c], hi_t[j, h, c] = lo, hi
+        # every combination of head cells a patch centre can produce
+        combos = sorted({tuple(self.head_cells(v)) for v in np.arange(0, self.H, 1.0 / 16)})
+        side = np.zeros(n, dtype=np.int64)
+        for cb in combos:
+            lo = np.min(np.stack([lo_t[:, h, c] for h, c in enumerate(cb)]), axis=0)
+            hi = np.max(np.stack([hi_t[:, h, c] for h, c in enumerate(cb)]), axis=0)
+            side = np.maximum(side, np.where(hi >= lo, hi - lo + 1, 0))
+        dense = [True] * n
+        for j in range(n):
+            if root[j] == j and 0 < side[j] < shp[j][0] and shp[j][0] == shp[j][1]:
+                dense[j] = False
+        for j in range(n):
+            t = blocks[j]["type"]
+            if t in ("shortcut", "maxpool") or (j + 1) in self.fused:
+                dense[j] = True
+                if t == "shortcut":
+                    for s_ in srcs[j]:
+                        if s_ != INPUT:
+                            dense[s_] = True
+            if t == "convolutional" and (self.net._conv_meta[j]["stride"] != 1 or j == 0):
+                dense[j] = True
+        for j in range(n - 1, -1, -1):         # a full-map block needs full-map sources
+            if root[j] == j and dense[j]:
+                for s_ in srcs[j]:
+                    if s_ != INPUT:
+                        dense[s_] = True
+        wins = [j for j in range(n) if root[j] == j and not dense[j]]
+        if not wins:
+            return
+        for w, j in enumerate(wins):
+            self.win[j] = int(side[j])
+            self.win_idx[j] = w
+        lut = np.zeros((len(wins), nh, maxhw, 2), dtype=np.int32)
+        ext = np.zeros((len(wins), 2), dtype=np.int32)
+        for w, j in enumerate(wins):
+            ok = hi_t[j] >= lo_t[j]
+            lut[w, :, :, 0] = np.where(ok, lo_t[j], 1)
+            lut[w, :, :, 1] = np.where(ok, hi_t[j], 0)
+            ext[w] = (self.win[j], shp[j][0])
+        dev = self.device
+        self.win_lut = torch.from_numpy(lut).to(dev)
+        self.win_ext = torch.from_numpy(ext).to(dev)
+        self.win_maxhw = maxhw
+        self.win_hw = hws
+        self.org = torch.zeros(len(wins), self.B, 2, dtype=torch.int32, device=dev)
+        self.win_flags = torch.zeros(1, dtype=torch.int32, device=dev)
+        self.windowed = True
+
+    def org_of(self, i):
+        """Device origin array [B,2] of block i's window (None: full map)."""
+        i = self.root[i] if i != INPUT else i
+        if i == INPUT or self.win[i] is None:
+            return None
+        return self.org[self.win_idx[i]]
+
+    def set_windows(self, center):
+        """Place every window around the head cells of ``center`` [B,2] (patch
+        centres, column/row px) for the next forward (po_cell_windows)."""
+        hw = (nat.c_int * len(self.win_hw))(*self.win_hw)
+        nat.call("po_cell_windows", nat.ptr(center.contiguous()), self.B, self.H, len(self.win_hw), hw,
+                 self.org.size(0), nat.ptr(self.win_lut, torch.int32), self.win_maxhw,
+                 nat.ptr(self.win_ext, torch.int32), nat.ptr(self.org, torch.int32),
+                 nat.ptr(self.win_flags, torch.int32), nat.stream())
+
+    def head_views(self):
+        """None (full-map heads) or (window sides, origin arrays) for po_cell_loss."""
+        if not self.windowed:
+            return None
+        win = [self.dims[self.root[h]][0] for h in self.heads]
+        return win, [self.org_of(h) for h in self.heads]
 
     # ---------------- gradient bookkeeping ----------------
     def _build_grad_plan(self):
@@ -288,7 +440,7 @@ class NetPlan:
         self.grad = [None] * n
         for i in range(n - 1, -1, -1):
             if root[i] == i and has[i] and self.grad[i] is None:
-                self.grad[i] = torch.zeros(B, self.shp[i][0], self.shp[i][1], self.cp[i], device=dev)
+                self.grad[i] = torch.zeros(B, self.dims[i][0], self.dims[i][1], self.cp[i], device=dev)
             if i in self.sc_alias:
                 self.grad[self.sc_alias[i][1]] = self.grad[i]
 
@@ -316,12 +468,13 @@ class NetPlan:
                     fwd.append(("po_conv_first_fwd", args, "img0"))
                     assert not fuse_next
                     continue
-                Hin, Win = (self.H, self.W) if src == INPUT else self.shp[src][:2]
+                Hin, Win = (self.H, self.W) if src == INPUT else self.dims[src]
                 cin_p = 16 if src == INPUT else self.cp[src]
                 desc = nat.po_conv_desc()
                 desc.B, desc.Hin, desc.Win, desc.Cin_p = B, Hin, Win, cin_p
-                desc.Hout, desc.Wout, desc.Cout_p = self.shp[i][0], self.shp[i][1], self.cp[i]
-                desc.Hg, desc.Wg = self.shp[i][0], self.shp[i][1]
+                desc.Hout, desc.Wout, desc.Cout_p = self.dims[i][0], self.dims[i][1], self.cp[i]
+                desc.Hg, desc.Wg = self.dims[i][0], self.dims[i][1]
+                desc.in_org, desc.out_org = self._orgp(src), self._orgp(i)
                 desc.in_step, desc.out_step, desc.out_oy, desc.out_ox = m["stride"], 1, 0, 0
                 k, pad = m["k"], m["pad"]
                 desc.ntaps = k * k
@@ -341,12 +494,13 @@ class NetPlan:
                     res, sum_out = self.act[self.root[f]], self.act[i + 1]
                 args = (nat.ctypes.byref(desc), P(inp), P(wts["w"]), P(wts["bias"]), P(y_out), P(res),
                         P(sum_out), None, None, None)
+                desc.macs = B * desc.Hg * desc.Wg * m["cout"] * m["cin"] * k * k      # logical channels
                 fwd.append(("po_conv", args, desc))
             elif t == "shortcut":
                 if i in self.fused:
                     continue
                 a, b = self.srcs[i]
-                M = B * self.shp[i][0] * self.shp[i][1]
+                M = B * self.dims[i][0] * self.dims[i][1]
                 C = self.shp[i][2]
                 fwd.append(("po_slice_accum", (P(self.act[a]), self.cp[a], 0, P(self.act[i]), self.cp[i], 0, M, C, 0,
                                                None, 0), None))
@@ -356,17 +510,25 @@ class NetPlan:
                 if len(self.srcs[i]) == 1:
                     continue
                 off = 0
-                M = B * self.shp[i][0] * self.shp[i][1]
+                M = B * self.dims[i][0] * self.dims[i][1]
                 for s in self.srcs[i]:
                     C = self.shp[s][2]
-                    fwd.append(("po_slice_accum", (P(self.act[s]), self.cp[s], 0, P(self.act[i]), self.cp[i], off, M, C,
-                                                   0, None, 0), None))
+                    if self._same_view(s, i):
+                        fwd.append(("po_slice_accum", (P(self.act[s]), self.cp[s], 0, P(self.act[i]), self.cp[i], off,
+                                                       M, C, 0, None, 0), None))
+                    else:
+                        fwd.append(("po_view_move", self._move(self.act[s], s, 0, self.act[i], i, off, C, 0, 0, None),
+                                    None))
                     off += C
             elif t == "upsample":
                 s = self.srcs[i][0]
                 hs, ws_, cs = self.shp[s]
-                fwd.append(("po_upsample2_fwd", (P(self.act[s]), B, hs, ws_, cs, self.cp[s], P(self.act[i]),
-                                                 self.cp[i], 0), None))
+                if self.win[i] is None and self.win[s] is None:
+                    fwd.append(("po_upsample2_fwd", (P(self.act[s]), B, hs, ws_, cs, self.cp[s], P(self.act[i]),
+                                                     self.cp[i], 0), None))
+                else:
+                    fwd.append(("po_view_move", self._move(self.act[s], s, 0, self.act[i], i, 0, cs, 1, 0, None),
+                                None))
             elif t == "maxpool":
                 s = self.srcs[i][0]
                 hs, ws_, cs = self.shp[s]
@@ -405,7 +567,7 @@ class NetPlan:
             if final and r in self.sc_alias:
                 b, _ = self.sc_alias[r]
                 _, mask_b, _ = contrib(b)
-                M = self.B * self.shp[r][0] * self.shp[r][1]
+                M = self.B * self.dims[r][0] * self.dims[r][1]
                 bwd.append(("po_slice_accum", (P(self.grad[r]), self.cp[r], 0, P(self.grad[b]), self.cp[b], 0, M,
                                                self.shp[r][2], 0, P(mask_b), self.cp[b]), None))
 
@@ -440,11 +602,11 @@ class NetPlan:
                     acc, mask, final = contrib(f)      # implicit: G_f aliases G_s
                     assert acc == 0
                     if mask is not None:               # f has no later contributor: apply its mask in place
-                        M = self.B * self.shp[f][0] * self.shp[f][1]
+                        M = self.B * self.dims[f][0] * self.dims[f][1]
                         bwd.append(("po_slice_accum", (P(G), self.cp[j], 0, P(self.grad[f]), self.cp[f], 0, M,
                                                        self.shp[f][2], 0, P(mask), self.cp[f]), None))
                     continue
-                M = self.B * self.shp[j][0] * self.shp[j][1]
+                M = self.B * self.dims[j][0] * self.dims[j][1]
                 C = self.shp[j][2]
                 for s_ in self.srcs[j]:
                     acc, mask, final = contrib(s_)
@@ -453,20 +615,27 @@ class NetPlan:
                     fallback_dual(s_, final)
             elif t == "route":
                 off = 0
-                M = self.B * self.shp[j][0] * self.shp[j][1]
+                M = self.B * self.dims[j][0] * self.dims[j][1]
                 for s_ in self.srcs[j]:
                     C = self.shp[s_][2]
                     acc, mask, final = contrib(s_)
-                    bwd.append(("po_slice_accum", (P(G), self.cp[j], off, P(self.grad[s_]), self.cp[s_], 0, M, C, acc,
-                                                   P(mask), self.cp[s_]), None))
+                    if self._same_view(s_, j):
+                        bwd.append(("po_slice_accum", (P(G), self.cp[j], off, P(self.grad[s_]), self.cp[s_], 0, M, C,
+                                                       acc, P(mask), self.cp[s_]), None))
+                    else:
+                        bwd.append(("po_view_move", self._move(G, j, off, self.grad[s_], s_, 0, C, 0, acc, mask),
+                                    None))
                     fallback_dual(s_, final)
                     off += C
             elif t == "upsample":
                 s_ = self.srcs[j][0]
                 acc, mask, final = contrib(s_)
                 hs, ws_, cs = self.shp[s_]
-                bwd.append(("po_upsample2_bwd", (P(G), self.cp[j], 0, B, hs, ws_, cs, P(self.grad[s_]), self.cp[s_],
-                                                 acc, P(mask), self.cp[s_]), None))
+                if self.win[j] is None and self.win[s_] is None:
+                    bwd.append(("po_upsample2_bwd", (P(G), self.cp[j], 0, B, hs, ws_, cs, P(self.grad[s_]),
+                                                     self.cp[s_], acc, P(mask), self.cp[s_]), None))
+                else:
+                    bwd.append(("po_view_move", self._move(G, j, 0, self.grad[s_], s_, 0, cs, 2, acc, mask), None))
                 fallback_dual(s_, final)
             elif t == "maxpool":
                 s_ = self.srcs[j][0]
@@ -477,11 +646,36 @@ class NetPlan:
                 fallback_dual(s_, final)
         self.bwd_ops = bwd
 
+    def _orgp(self, i):
+        o = self.org_of(i)
+        return o.data_ptr() if o is not None else None
+
+    def _same_view(self, a, b):
+        """Blocks a and b have buffers of the same spatial layout (both full
+        maps, or the same window)."""
+        ra, rb = self.root[a], self.root[b]
+        if self.win[ra] is None and self.win[rb] is None:
+            return True
+        return self.win[ra] is not None and self.win_idx.get(ra) == self.win_idx.get(rb)
+
+    def _move(self, src, si, soff, dst, di, doff, C, mode, acc, mask):
+        """po_view_move arguments: dst block di (=|+=) src block si (spatial views)."""
+        P = lambda t: nat.c_void_p(t.data_ptr()) if t is not None else None
+        Hs, Ws = self.dims[si]
+        Hd, Wd = self.dims[di]
+        o = lambda i: nat.c_void_p(self._orgp(i)) if self._orgp(i) is not None else None
+        return (P(src), Hs, Ws, self.cp[si], soff, o(si), P(dst), Hd, Wd, self.cp[di], doff, o(di), self.B, C,
+                mode, acc, P(mask), self.cp[di])
+
     def _dgrad_descs(self, j, src, acc):
         """po_conv launches computing d(input of conv j) (one per stride parity class)."""
         m = self.net._conv_meta[j]
         s, k, pad = m["stride"], m["k"], m["pad"]
-        Hin, Win = (self.H, self.W) if src == INPUT else self.shp[src][:2]
+        if self.win[j] is not None or (src != INPUT and self.win[src] is not None):
+            assert s == 1, "windowed dgrad needs a stride-1 conv"
+            Hin, Win = self.dims[src]
+        else:
+            Hin, Win = (self.H, self.W) if src == INPUT else self.shp[src][:2]
         cin_p = 16 if src == INPUT else self.cp[src]
         out = []
         for py in range(s):
@@ -494,8 +688,9 @@ class NetPlan:
                         if (py + pad - kh) % s == 0 and (px + pad - kw) % s == 0]
                 wd = self.net._dgrad_weight(j, taps, cin_p, self.device)
                 desc = nat.po_conv_desc()
-                desc.B, desc.Hin, desc.Win, desc.Cin_p = self.B, self.shp[j][0], self.shp[j][1], self.cp[j]
+                desc.B, desc.Hin, desc.Win, desc.Cin_p = self.B, self.dims[j][0], self.dims[j][1], self.cp[j]
                 desc.Hout, desc.Wout, desc.Cout_p = Hin, Win, cin_p
+                desc.in_org, desc.out_org = self._orgp(j), (self._orgp(src) if src != INPUT else None)
                 desc.Hg, desc.Wg = Hg, Wg
                 desc.in_step, desc.out_step, desc.out_oy, desc.out_ox = 1, s, py, px
                 desc.ntaps = len(taps)
@@ -505,8 +700,14 @@ class NetPlan:
                 desc.N = cin_p
                 desc.act = 0
                 desc.accumulate = acc
+                desc.macs = self.B * Hg * Wg * m["cin"] * len(taps) * m["cout"]
                 out.append((desc, wd))
         return out
+
+    def conv_macs(self):
+        """MACs (logical channels) of the po_conv launches of one forward +
+        backward of this plan — the work the MFMA kernel does per step."""
+        return sum(d.macs for name, _, d in self.fwd_ops + self.bwd_ops if name == "po_conv")
 
     # ---------------- autotuning ----------------
     def tune(self, cache, iters=4):
@@ -569,13 +770,24 @@ class NetPlan:
         xp = nat.c_void_p(x.data_ptr())
         if not self.first_direct:
             nat.call("po_nchw_to_nhwc", xp, self.B, self.H, self.W, 3, 16, nat.c_void_p(self.in_nhwc.data_ptr()), st)
-        for name, args, _ in self.fwd_ops:
+        for name, args, desc in self.fwd_ops:
             if name == "po_conv_first_fwd":
                 args = (xp,) + args[1:]
-            rc = getattr(lib, name)(*args, st)
-            if rc:
-                raise RuntimeError("%s failed: %s" % (name, nat.last_error()))
+            self._launch(lib, name, args, desc, st)
         return [self.act[h] for h in self.heads]
+
+    def _launch(self, lib, name, args, desc, st):
+        timer = self.conv_timer
+        if timer is not None and name == "po_conv":
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            rc = lib.po_conv(*args, st)
+            e1.record()
+            timer.append((e0, e1, desc.macs))
+        else:
+            rc = getattr(lib, name)(*args, st)
+        if rc:
+            raise RuntimeError("%s failed: %s" % (name, nat.last_error()))
 
     def run_backward(self, d_heads, d_x, roi=None):
         """d_heads: NHWC gradient tensors of the head buffers (list, in head order);
@@ -586,22 +798,20 @@ class NetPlan:
         for hi, h in enumerate(self.heads):
             r = self.root[h]
             g = d_heads[hi].contiguous()
-            M = self.B * self.shp[r][0] * self.shp[r][1]
+            M = self.B * self.dims[r][0] * self.dims[r][1]
             mask = self.act[r] if (self.ncons[r] == 0 and self._leaky(r)) else None
             nat.call("po_slice_accum", nat.c_void_p(g.data_ptr()), self.cp[r], 0,
                      nat.c_void_p(self.grad[r].data_ptr()), self.cp[r], 0, M, self.cp[r], 0,
                      nat.c_void_p(mask.data_ptr()) if mask is not None else None, self.cp[r], st)
         dxp = nat.c_void_p(d_x.data_ptr())
         roip = nat.c_void_p(roi.data_ptr()) if roi is not None else None
-        for name, args, _ in self.bwd_ops:
+        for name, args, desc in self.bwd_ops:
             if args and args[-1] == "dimg":
                 if name == "po_conv_first_dgrad":
                     args = args[:-2] + (roip, dxp)
                 else:
                     args = args[:-1] + (dxp,)
-            rc = getattr(lib, name)(*args, st)
-            if rc:
-                raise RuntimeError("%s failed: %s" % (name, nat.last_error()))
+            self._launch(lib, name, args, desc, st)
 
 
 
@@ -656,6 +866,8 @@ class Darknet(nn.Module):
         self.seen = 0
         self.header_info = np.array([0, 0, 0, self.seen, 0], dtype=np.int32)
         self.clone_heads = False
+        # receptive-field windows on the training path (ADVPATCH_WINDOWS=0: full maps)
+        self.window_heads = os.environ.get("ADVPATCH_WINDOWS", "1") != "0"
         self._conv_meta = {}
         cin = [int(self.hyperparams["channels"])]
         for i, (d, mod) in enumerate(zip(self.blocks, self.module_list)):
@@ -783,14 +995,16 @@ class Darknet(nn.Module):
             self._dgrad_cache[key] = Wd.float().contiguous().to(device)
         return self._dgrad_cache[key]
 
-    def plan(self, B, H, W, device):
+    def plan(self, B, H, W, device, windowed=False):
         """The execution plan for a batch shape (built, and its conv tiles
         autotuned on the device, on first use; ADVPATCH_TUNE=0 keeps the
-        built-in tile heuristic)."""
+        built-in tile heuristic).  ``windowed``: blocks past the last
+        full-map dependency run on receptive-field windows around the loss
+        cells (NetPlan._plan_windows); only the training path uses it."""
         self._prepare(device)
-        key = (B, H, W, str(device))
+        key = (B, H, W, str(device), bool(windowed))
         if key not in self._plans:
-            p = NetPlan(self, B, H, W, device)
+            p = NetPlan(self, B, H, W, device, windowed=windowed)
             if torch.device(device).type == "cuda" and os.environ.get("ADVPATCH_TUNE", "1") != "0":
                 path = os.environ.get("ADVPATCH_TUNE_CACHE")
                 if path and os.path.exists(path) and not self._tile_cache:
@@ -816,11 +1030,20 @@ class Darknet(nn.Module):
         p = self.plan(x.size(0), x.size(2), x.size(3), x.device)
         return list(_DarknetFn.apply(x, p, True))
 
-    def forward_nhwc(self, x, input_roi=None):
-        """Training-path forward: returns the NHWC head buffers [B, h, w, Cp]
-        (Cp = padded channel stride, channel = anchor*(5+C) + field).
+    def forward_nhwc(self, x, input_roi=None, center=None):
+        """Training-path forward: returns (head buffers, plan).  Head buffers
+        are NHWC [B, h, w, Cp] (Cp = padded channel stride, channel =
+        anchor*(5+C) + field).
         ``input_roi`` [B,4] int32: the input gradient is only needed (and only
-        computed) inside these per-image boxes (the patch footprint)."""
+        computed) inside these per-image boxes (the patch footprint).
+        ``center`` [B,2] (patch centres, px): the loss reads the heads only
+        at the cells of these centres (train_patch.py:449-483); the plan then
+        computes the blocks after the last full-map dependency on windows
+        around them, and the heads come back as windows
+        (``plan.head_views()``)."""
         nat.ensure_device(x)
-        p = self.plan(x.size(0), x.size(2), x.size(3), x.device)
+        windowed = center is not None and self.window_heads
+        p = self.plan(x.size(0), x.size(2), x.size(3), x.device, windowed=windowed)
+        if p.windowed:
+            p.set_windows(center)
         return list(_DarknetFn.apply(x, p, False, input_roi)), p

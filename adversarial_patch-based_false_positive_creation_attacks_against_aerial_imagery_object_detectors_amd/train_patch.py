@@ -54,11 +54,22 @@ TARGET_ID = 14       # train_patch.py:28 (helicopter)
 OBJECTIVES = {"ce": 0, "targeted": 1, "untargeted": 2}
 
 
+def _head_args(hw, views):
+    """ctypes arrays (hw, win, org) of po_cell_loss; views = None (full maps)
+    or (window sides, origin tensors [B,2] int32 or None per head)."""
+    n = len(hw)
+    hwa = (nat.c_int * n)(*hw)
+    if views is None:
+        return hwa, None, None
+    win, orgs = views
+    return hwa, (nat.c_int * n)(*win), nat.ptr_array(orgs)
+
+
 class _CellLoss(torch.autograd.Function):
     """(no_obj, no_cls) at the patch cells of the NHWC head buffers (po_cell_loss)."""
 
     @staticmethod
-    def forward(ctx, center, S, target, objective, hw, Cp, *heads):
+    def forward(ctx, center, S, target, objective, hw, Cp, views, *heads):
         B = center.size(0)
         dev = center.device
         A = 3 * len(heads)
@@ -67,35 +78,38 @@ class _CellLoss(torch.autograd.Function):
         cls = torch.empty(B, A, 15, device=dev)
         cells = torch.empty(len(heads), B, dtype=torch.int32, device=dev)
         flags = torch.zeros(1, dtype=torch.int32, device=dev)
-        hp = nat.ptr_array(heads)
-        hwa = (nat.c_int * len(hw))(*hw)
-        nat.call("po_cell_loss", hp, hwa, len(heads), Cp, B, S, nat.ptr(center.contiguous()), target, objective,
-                 None, None, nat.ptr(out2), nat.ptr(obj), nat.ptr(cls), nat.ptr(cells, torch.int32),
-                 nat.ptr(flags, torch.int32), nat.stream())
+        hwa, wina, orga = _head_args(hw, views)
+        nat.call("po_cell_loss", nat.ptr_array(heads), hwa, wina, orga, len(heads), Cp, B, S,
+                 nat.ptr(center.contiguous()), target, objective, None, None, nat.ptr(out2), nat.ptr(obj),
+                 nat.ptr(cls), nat.ptr(cells, torch.int32), nat.ptr(flags, torch.int32), nat.stream())
         ctx.save_for_backward(center, *heads)
-        ctx.meta = (S, target, objective, tuple(hw), Cp)
+        ctx.meta = (S, target, objective, tuple(hw), Cp, views)
         ctx.mark_non_differentiable(obj, cls, cells, flags)
         return out2, obj, cls, cells, flags
 
     @staticmethod
     def backward(ctx, g2, *unused):
         center, *heads = ctx.saved_tensors
-        S, target, objective, hw, Cp = ctx.meta
+        S, target, objective, hw, Cp, views = ctx.meta
         d_heads = [torch.zeros_like(h) for h in heads]
         out2 = torch.empty(2, device=center.device)
-        nat.call("po_cell_loss", nat.ptr_array(heads), (nat.c_int * len(hw))(*hw), len(heads), Cp, center.size(0),
-                 S, nat.ptr(center.contiguous()), target, objective, nat.ptr(g2.contiguous().float()),
+        hwa, wina, orga = _head_args(hw, views)
+        nat.call("po_cell_loss", nat.ptr_array(heads), hwa, wina, orga, len(heads), Cp, center.size(0), S,
+                 nat.ptr(center.contiguous()), target, objective, nat.ptr(g2.contiguous().float()),
                  nat.ptr_array(d_heads), nat.ptr(out2), None, None, None, None, nat.stream())
-        return (None, None, None, None, None, None) + tuple(d_heads)
+        return (None, None, None, None, None, None, None) + tuple(d_heads)
 
 
 def cell_loss(heads, plan, img_size, patch_center, target=TARGET_ID, objective="ce"):
-    """-> (out2 [2] = {no_obj_loss, no_cls_loss}, obj [B,9], cls [B,9,15], cells, flags)."""
+    """-> (out2 [2] = {no_obj_loss, no_cls_loss}, obj [B,9], cls [B,9,15], cells, flags).
+    ``heads`` are the plan's head buffers (full maps, or receptive-field
+    windows when the plan was run with the patch centres)."""
     hw = [plan.shp[h][0] for h in plan.heads]
     Cp = plan.cp[plan.heads[0]]
     for h in plan.heads:
         assert plan.cp[h] == Cp and plan.shp[h][0] == plan.shp[h][1]
-    return _CellLoss.apply(patch_center, int(img_size), int(target), OBJECTIVES[objective], hw, Cp, *heads)
+    return _CellLoss.apply(patch_center, int(img_size), int(target), OBJECTIVES[objective], hw, Cp,
+                           plan.head_views(), *heads)
 
 
 LOSS_KEYS = ("loss", "nps_loss", "tv_loss", "no_obj_loss", "no_cls_loss", "colorful_loss")
@@ -134,6 +148,7 @@ class PatchTrainer(object):
             print("training mode : ", mode)
         self.device = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
         self.objective = objective
+        self.last_plan = None      # NetPlan of the latest forward (tests, bench)
         self.darknet_model = Darknet(self.config.cfgfile)
         wf = self.config.weightfile
         if not os.path.exists(wf) and wf == patch_config.synthetic_weights_path("yolov3-dota"):
@@ -180,7 +195,8 @@ class PatchTrainer(object):
             roi = None
         # the warp backward reads dL/dp_img only inside the patch footprint:
         # the first conv's input gradient is computed there only
-        heads, plan = self.darknet_model.forward_nhwc(p_img, input_roi=roi)
+        heads, plan = self.darknet_model.forward_nhwc(p_img, input_roi=roi, center=center)
+        self.last_plan = plan
         out2, obj, cls, cells, flags = cell_loss(heads, plan, img_size, center, TARGET_ID, objective)
         no_obj_loss, no_cls_loss = out2[0], out2[1]
         reg = regularisers(adv_patch, self.nps_calculator.colors)

@@ -155,34 +155,18 @@ def main():
     tr.patch_transformer.generator = gen
 
     net = tr.darknet_model
-    flops_per_img = 4.0 * conv_macs(net)      # fwd + dgrad
-    plan = net.plan(B, S, S, dev)
-
-    # per-step HIP events around the Darknet forward and backward (the conv stack)
-    ev = []
-    orig_f, orig_b = plan.run_forward, plan.run_backward
-
-    def rf(x):
-        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        e0.record()
-        r = orig_f(x)
-        e1.record()
-        ev.append((e0, e1))
-        return r
-
-    def rb(*a):
-        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        e0.record()
-        orig_b(*a)
-        e1.record()
-        ev.append((e0, e1))
-
-    plan.run_forward, plan.run_backward = rf, rb
+    ref_flops_per_img = 4.0 * conv_macs(net)      # reference algorithm: dense fwd + dgrad
 
     for _ in range(args.warmup):
         tr.step(patch, opt, img, lab)
     torch.cuda.synchronize()
-    ev.clear()
+    # HIP events around every po_conv launch of the timed steps (the kernels
+    # run on torch's current stream, where the events are recorded)
+    if getattr(tr, "last_plan", None) is None:       # --warmup 0: build the plan outside the timed region
+        tr.losses(patch, img, lab)
+        torch.cuda.synchronize()
+    plan = tr.last_plan
+    plan.conv_timer = []
     if world > 1:
         torch.distributed.barrier()
     torch.cuda.synchronize()
@@ -197,10 +181,12 @@ def main():
         t = torch.tensor([elapsed], device=dev)
         torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
         elapsed = float(t)
-    net_ms = sum(a.elapsed_time(b) for a, b in ev) / args.steps
+    timer, plan.conv_timer = plan.conv_timer, None
+    conv_ms = sum(e0.elapsed_time(e1) for e0, e1, _ in timer) / args.steps
+    conv_flops = 2.0 * sum(m for _, _, m in timer) / args.steps
     ms_per_step = elapsed * 1000.0 / args.steps
     value = world * B * args.steps / elapsed
-    achieved = flops_per_img * B / (net_ms * 1e-3) / 1e12
+    achieved = conv_flops / (conv_ms * 1e-3) / 1e12
 
     if rank == 0:
         traffic = None
@@ -217,10 +203,14 @@ def main():
             "config": {"workload": "%s S=%d P=%d batch=%d per GPU, global %d" % (cfg, S, P, B, B * world),
                        "global_batch": B * world, "per_gpu_batch": B, "image_size": S, "patch_size": P,
                        "parallelism": "dp%d" % world},
-            "roofline": {"bound": "mfma", "kernel": "po_conv implicit-GEMM (Darknet fwd + dgrad, all launches of a step)",
+            "roofline": {"bound": "mfma", "kernel": "conv_k (po_conv implicit GEMM: every Darknet fwd + dgrad "
+                                                    "launch of a step)",
                          "achieved": achieved, "peak": PEAK_FP32_MFMA_TFLOPS, "unit": "TFLOP/s",
                          "frac": achieved / PEAK_FP32_MFMA_TFLOPS, "traffic": traffic,
-                         "algorithmic_flops_per_step": flops_per_img * B, "net_ms_per_step": net_ms},
+                         "flops_per_step": conv_flops, "conv_ms_per_step": conv_ms,
+                         "conv_launches_per_step": len(timer) // args.steps,
+                         "reference_dense_flops_per_step": ref_flops_per_img * B,
+                         "receptive_field_windows": bool(plan.windowed)},
             "loss": float(terms["loss"]),
         }
         if world == 1 and not args.no_cpu_baseline:

@@ -33,7 +33,7 @@ typedef void* po_stream_t;
 #define PO_EHIP -2     /* HIP runtime error */
 #define PO_EDEVICE -3  /* device is not gfx950 */
 
-#define PO_ABI_VERSION 3
+#define PO_ABI_VERSION 4
 
 int po_abi_version(void);
 const char* po_last_error(void);
@@ -99,7 +99,7 @@ int po_regularisers(const float* patch, int P, const float* colors, int ncol, co
                     float* workspace /* >= 16384 floats */, po_stream_t s);
 
 /* Loss head (train_patch.py:428-548 + 230-253):
- * for each head h (NHWC [B,hw_h,hw_h,Cp], Cp>=60, channel a*20+f), each image b:
+ * for each head h (map side hw_h, NHWC, Cp>=60, channel a*20+f), each image b:
  *   cell = floor(center/ (S/hw)) ; index = ix*hw + iy  (transposed)
  *   obj[b, h*3+a] = sigmoid(head[b, index, a*20+4]); cls[b,h*3+a,c] = sigmoid(.. a*20+5+c)
  * no_obj = 4*(1 - mean_b max_k obj)          (max: first index on ties)
@@ -107,22 +107,46 @@ int po_regularisers(const float* patch, int P, const float* colors, int ncol, co
  *          objective 1: sum_b mean_k (max_c cls - cls[target])  (noCLS_loss_targeted,
  *                       train_patch.py:550-577; max: first index on ties)
  *          objective 2: 0 (untargeted)
+ * Head buffers are either the full map [B,hw,hw,Cp] (org == NULL or org[h] ==
+ * NULL) or a window [B,win[h],win[h],Cp] whose per-image origin (row, col) in
+ * map coordinates is org[h][2b..2b+1] (po_cell_windows); win may be NULL when
+ * every head is a full map.
  * out2 [2] = {no_obj, no_cls}; obj_out [B,3*nheads], cls_out [B,3*nheads,15], cells [nheads,B]
- * (each may be NULL).  d_heads (may be NULL): gradient of g2[0]*no_obj + g2[1]*no_cls
- * (g2: DEVICE pointer, 2 floats)
+ * (each may be NULL).  d_heads (may be NULL, same layout as heads): gradient of
+ * g2[0]*no_obj + g2[1]*no_cls (g2: DEVICE pointer, 2 floats)
  * written at the selected cells only (other elements untouched — caller zeroes).
- * flags: bit0 set if any cell index was out of range (clamped). */
-int po_cell_loss(const float* const* heads, const int* hw, int nheads, int Cp, int B, int S,
-                 const float* center, int target, int objective, const float* g2,
-                 float* const* d_heads, float* out2, float* obj_out, float* cls_out,
+ * flags: bit0 set if any cell index was out of range (clamped), bit1 if a
+ * cell fell outside its head window (clamped; a planning error). */
+int po_cell_loss(const float* const* heads, const int* hw, const int* win, const int32_t* const* org,
+                 int nheads, int Cp, int B, int S, const float* center, int target, int objective,
+                 const float* g2, float* const* d_heads, float* out2, float* obj_out, float* cls_out,
                  int32_t* cells, int32_t* flags, po_stream_t s);
+
+/* Receptive-field windows of the loss (SURVEY Q1 cells): the loss reads each
+ * head at one cell per image, so every block downstream of the last
+ * full-map block is only needed on a small box around that cell.  For window
+ * w and image b:
+ *   cell_h = the head-h cell of po_cell_loss (row = index / hw, col = index % hw)
+ *   lo = min_h lut[w][h][cell_h][0], hi = max_h lut[w][h][cell_h][1]   (per axis)
+ *   org[w][b] = clamp(lo, 0, ext[w][1] - ext[w][0])  for rows and columns
+ * lut [nwin][nheads][maxhw][2] int32 (lo > hi: head h does not reach w),
+ * ext [nwin][2] = {window side, map side} (DEVICE), hw [nheads] (HOST).
+ * flags bit2 is set if a needed box did not fit its static window. */
+int po_cell_windows(const float* center, int B, int S, int nheads, const int* hw, int nwin,
+                    const int32_t* lut, int maxhw, const int32_t* ext, int32_t* org, int32_t* flags,
+                    po_stream_t s);
 
 /* ---------------- network ops (reference darknet_v3.py:37-100, 195-220) ---------------- */
 
 /* Tap list of an implicit-GEMM convolution launch.  For output pixel (b,i,j)
  * of the launch grid and tap t the source pixel is
  *   (b, i*in_step + dh[t], j*in_step + dw[t])  (zero outside [0,Hin)x[0,Win))
- * and the destination is (b, i*out_step + out_oy, j*out_step + out_ox). */
+ * and the destination is (b, i*out_step + out_oy, j*out_step + out_ox).
+ * Window buffers (in_org / out_org non-NULL, [B,2] int32 DEVICE, the
+ * per-image (row, col) map position of the buffer's pixel (0,0)): the source
+ * pixel becomes (i + out_org[b] + dh[t] - in_org[b]) in the source buffer's
+ * own coordinates (zero outside it); requires in_step = out_step = 1 and
+ * out_oy = out_ox = 0. */
 typedef struct po_conv_desc {
   int B;
   int Hin, Win, Cin_p;        /* source tensor (NHWC, channel stride Cin_p) */
@@ -136,6 +160,8 @@ typedef struct po_conv_desc {
   int accumulate;             /* 1: out = acc + out_prev (dst read) */
   int tile;                   /* 0: built-in heuristic; 1..PO_CONV_NTILES: fixed tile
                                  (po_conv_tile_info), chosen by the caller's autotuner */
+  const int32_t* in_org;      /* NULL: full-map source */
+  const int32_t* out_org;     /* NULL: full-map destination */
 } po_conv_desc;
 
 #define PO_CONV_NTILES 10
@@ -174,6 +200,17 @@ int po_conv_first_dgrad(const float* D, int B, int H, int W, int stride, const f
 int po_slice_accum(const float* src, int src_stride, int src_off, float* dst, int dst_stride,
                    int dst_off, int64_t M, int C, int accumulate, const float* mask_y,
                    int mask_stride, po_stream_t s);
+/* Spatially-aware copy between full-map and window buffers (NHWC).  Over
+ * every pixel (b,i,j) of dst [B,Hd,Wd] (map position p = (i,j) + dst_org[b]):
+ *   mode 0: v = src[p - src_org[b]]                  (route slice)
+ *   mode 1: v = src[p/2 - src_org[b]]                (nearest 2x upsample fwd)
+ *   mode 2: v = sum_{a,c in {0,1}} src[2p + (a,c) - src_org[b]]  (its backward)
+ * src pixels outside the src buffer read 0; channels src[off_s + c], dst[off_d + c];
+ * dst (=|+=) v, optionally * leaky'(mask_y) (mask in dst's pixel layout).
+ * NULL org = full map. */
+int po_view_move(const float* src, int Hs, int Ws, int src_stride, int src_off, const int32_t* src_org,
+                 float* dst, int Hd, int Wd, int dst_stride, int dst_off, const int32_t* dst_org, int B,
+                 int C, int mode, int accumulate, const float* mask_y, int mask_stride, po_stream_t s);
 /* nearest 2x upsample fwd (darknet_v3.py:103-113): dst[b,2h+y,2w+x, off+c] = src[b,h,w,c]. */
 int po_upsample2_fwd(const float* src, int B, int H, int W, int C, int src_stride, float* dst,
                      int dst_stride, int dst_off, po_stream_t s);

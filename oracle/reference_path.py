@@ -336,10 +336,15 @@ class OracleDarknet:
                     x = F.batch_norm(x, p["bn_rm"], p["bn_rv"], p["bn_w"], p["bn_b"],
                                      training=False, momentum=0.9, eps=1e-5)
                 if record is not None:
+                    if x.requires_grad:
+                        x.retain_grad()
                     record[i] = x
                 if p["act"] == "leaky":
                     if br is not None:
-                        x = x * torch.where(br[1], torch.ones((), dtype=x.dtype), torch.full((), 0.1, dtype=x.dtype))
+                        pos = br[1]
+                        if pos.dtype != torch.bool:        # tri-state: -1 = decide here
+                            pos = torch.where(pos < 0, x > 0, pos > 0)
+                        x = x * torch.where(pos, torch.ones((), dtype=x.dtype), torch.full((), 0.1, dtype=x.dtype))
                     else:
                         x = F.leaky_relu(x, 0.1)
                 elif p["act"] == "mish":
@@ -463,7 +468,7 @@ def noCLS_loss_targeted(no_cls, cls_ID):                           # train_patch
 # train_patch.py:157-330 one iteration of the batch loop
 # --------------------------------------------------------------------------
 def train_step(patch, img_batch, lab_batch, draws, net, colors, target_id=TARGET_ID,
-               objective="ce", weight_grad=False, branch=None):
+               objective="ce", weight_grad=False, branch=None, record=None):
     """One iteration of PatchTrainer.train's batch body (train_patch.py:164-327).
 
     ``patch`` is the [3,P,P] leaf.  Returns a dict of loss terms (float
@@ -471,14 +476,15 @@ def train_step(patch, img_batch, lab_batch, draws, net, colors, target_id=TARGET
     check (patch_center, cell indices, obj [B,9], cls [B,9,15]).
     ``objective``: "ce" (active, train_patch.py:253), "targeted"
     (noCLS_loss_targeted, train_patch.py:262) or "untargeted"
-    (train_patch.py:305-307).  ``branch``: see OracleDarknet.forward.
+    (train_patch.py:305-307).  ``branch``, ``record``: see OracleDarknet.forward
+    (recorded pre-activations keep their gradients).
     """
     leaf = patch.detach().clone().requires_grad_(True)
     img_size = net.height
     adv_batch_t, patch_center = patch_transformer(leaf, lab_batch, img_size, draws)  # 173-174
     p_img = patch_applier(img_batch, adv_batch_t)                                  # 183
     p_img = F.interpolate(p_img, (net.height, net.width))                         # 186-187
-    outputs = net(p_img, branch=branch)                                            # 197
+    outputs = net(p_img, branch=branch, record=record)                             # 197
     obj_l, cls_l = obj_cls_conf_find(outputs, img_size, patch_center)              # 207-208
     no_obj = no_obj_reshape(obj_l)                                                 # 213-214
     no_cls = no_cls_reshape(cls_l)                                                 # 216-217

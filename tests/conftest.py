@@ -3,6 +3,7 @@ import os
 import sys
 
 import pytest
+import torch
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 if ROOT not in sys.path:
@@ -46,13 +47,25 @@ def P():
 def plan_branches(plan):
     """Branch decisions the HIP forward took (LeakyReLU sign per leaky conv
     output, maxpool window argmax), NCHW on the CPU, for
-    OracleDarknet.forward(branch=...)."""
+    OracleDarknet.forward(branch=...).  Blocks the plan ran on a
+    receptive-field window give an int8 map: 1/0 inside the window, -1
+    (the oracle decides) outside it, where no value reaches the loss."""
     br = {}
     for i, d in enumerate(plan.net.blocks):
         C = plan.shp[i][2]
         if d["type"] == "convolutional" and plan._leaky(i):
-            br[i] = ("leaky", (plan.act[i][..., :C] > 0).permute(0, 3, 1, 2).cpu())
+            pos = (plan.act[i][..., :C] > 0).permute(0, 3, 1, 2).cpu()
+            if plan.win[i] is not None:
+                H, W = plan.shp[i][:2]
+                full = torch.full((plan.B, C, H, W), -1, dtype=torch.int8)
+                org = plan.org_of(i).cpu().tolist()
+                s = plan.win[i]
+                for b, (r0, c0) in enumerate(org):
+                    full[b, :, r0:r0 + s, c0:c0 + s] = pos[b].to(torch.int8)
+                pos = full
+            br[i] = ("leaky", pos)
         elif d["type"] == "maxpool":
+            assert plan.win[i] is None
             br[i] = ("maxpool", plan.argmax[i][..., :C].permute(0, 3, 1, 2).long().cpu())
     return br
 
@@ -64,7 +77,10 @@ def assert_branch_ties_only(br, record, tol=1e-5):
         if kind != "leaky" or i not in record:
             continue
         pre = record[i].detach()
-        mism = (pre > 0) != val
+        if val.dtype == torch.bool:
+            mism = (pre > 0) != val
+        else:
+            mism = ((pre > 0) != (val > 0)) & (val >= 0)
         if mism.any():
             worst = float(pre[mism].abs().max() / pre.abs().max())
             assert worst <= tol, "block %d: branch mismatch at |x|/max=%.3g (not a rounding tie)" % (i, worst)

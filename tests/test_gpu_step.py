@@ -41,7 +41,7 @@ def _run(cfg, B, P, tmp_path, objective="ce", seed=0):
     pg = patch.to(DEV).requires_grad_(True)
     loss, terms = tr.losses(pg, img.to(DEV), lab.to(DEV), {k: v.to(DEV) for k, v in dr.items()})
     # the oracle runs on the branch decisions (LeakyReLU slopes) the HIP forward took
-    br = plan_branches(tr.darknet_model.plan(B, S, S, DEV))
+    br = plan_branches(tr.last_plan)
     ref = oracle.train_step(patch, img, lab, dr, ref_net, colors, objective=objective, branch=br)
     loss.backward()
     return ref, terms, pg.grad.cpu()
@@ -85,7 +85,7 @@ def test_step_yolov3_dota_608(tmp_path):
     colors = ld.load_printability_colors("builtin:30values")
     pg = patch.to(DEV).requires_grad_(True)
     loss, terms = tr.losses(pg, img.to(DEV), lab.to(DEV), {k: v.to(DEV) for k, v in dr.items()})
-    br = plan_branches(tr.darknet_model.plan(B, S, S, DEV))
+    br = plan_branches(tr.last_plan)
     loss.backward()
     ref32 = oracle.train_step(patch, img, lab, dr, ref_net, colors, branch=br)
     ref64 = oracle.train_step_f64(patch, img, lab, dr, ref_net, colors, branch=br)
@@ -111,7 +111,7 @@ def test_two_adam_steps_yolov3(tmp_path):
     brs = []
     for _ in range(2):
         loss, terms = tr.losses(pg, img.to(DEV), lab.to(DEV), d)
-        brs.append(plan_branches(tr.darknet_model.plan(1, 608, 608, DEV)))
+        brs.append(plan_branches(tr.last_plan))
         loss.backward()
         opt.step()
         opt.zero_grad()
@@ -124,3 +124,33 @@ def test_two_adam_steps_yolov3(tmp_path):
     # >99% of the elements agree to 1e-4 after the two steps.
     frac = float(((pg.detach().cpu() - ref).abs() > 1e-4).float().mean())
     assert frac < 0.01, frac
+
+
+@pytest.mark.parametrize("cfg,B,P", [("builtin:mini3", 5, 32), ("builtin:yolov3-tiny-dota", 3, 96),
+                                     ("builtin:yolov3-dota", 3, 224)])
+def test_windowed_plan_matches_full_maps(tmp_path, cfg, B, P):
+    """Receptive-field windows (NetPlan._plan_windows) change which pixels are
+    computed, not how: the loss terms, cells and the patch gradient equal the
+    full-map plan's."""
+    sy = pkg_mod("synthetic")
+    tr, ref_net = _trainer(cfg, tmp_path)
+    S = ref_net.height
+    img, lab = sy.frames(B, S, seed=70).to(DEV), sy.labels(B, seed=71).to(DEV)
+    patch, dr = sy.patch(P, seed=72), {k: v.to(DEV) for k, v in sy.draws(B, P, seed=73).items()}
+    out = []
+    for windows in (False, True):
+        tr.darknet_model.window_heads = windows
+        pg = patch.to(DEV).requires_grad_(True)
+        loss, terms = tr.losses(pg, img, lab, dr)
+        loss.backward()
+        assert tr.last_plan.windowed == windows
+        if windows:
+            assert int(tr.last_plan.win_flags.item()) == 0
+        out.append((terms, pg.grad.detach().clone()))
+    (t0, g0), (t1, g1) = out
+    assert int(t1["flags"].item()) == 0
+    assert t0["cells"].tolist() == t1["cells"].tolist()
+    for k in ("loss", "no_obj_loss", "no_cls_loss"):
+        assert float(t0[k]) == float(t1[k]), (k, float(t0[k]), float(t1[k]))
+    torch.testing.assert_close(t1["obj"], t0["obj"], rtol=0, atol=0)
+    assert torch.equal(g0, g1), float((g0 - g1).abs().max())
