@@ -20,7 +20,7 @@ class po_conv_desc(ctypes.Structure):
         "in_step", "out_step", "out_oy", "out_ox", "ntaps")] + [
         ("dh", c_int * 9), ("dw", c_int * 9),
         ("N", c_int), ("act", c_int), ("accumulate", c_int), ("tile", c_int),
-        ("in_org", c_void_p), ("out_org", c_void_p)]
+        ("in_org", c_void_p), ("out_org", c_void_p), ("ksplit", c_int), ("workspace", c_void_p)]
 
 
 _SIGS = {

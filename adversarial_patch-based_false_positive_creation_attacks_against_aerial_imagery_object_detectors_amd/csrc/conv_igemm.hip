@@ -35,6 +35,8 @@ struct ConvArgs {
   const float* mask2;
   const int32_t* in_org;        // window origins [B,2] (NULL: full map)
   const int32_t* out_org;
+  float* ws;                    // split-K partials [ksplit][M][N] (ksplit > 1)
+  int ksplit;
   int B, Hin, Win, Cin_p, Hout, Wout, Cout_p, Hg, Wg;
   int in_step, out_step, out_oy, out_ox;
   int ntaps, N, act, accumulate;
@@ -152,10 +154,15 @@ __global__ __launch_bounds__(256) void conv_k(const ConvArgs a) {
       for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.f;
 
   const int kc = a.Cin_p / BK;
-  const int nks = a.ntaps * kc;
+  const int nks_all = a.ntaps * kc;
+  // split-K: this workgroup's contiguous range of k-steps
+  const int split = blockIdx.y;
+  const int ks0 = (int)((int64_t)split * nks_all / a.ksplit);
+  const int nks = (int)((int64_t)(split + 1) * nks_all / a.ksplit) - ks0;
   // k-step position: tap (th, tw) and channel offset c0, advanced incrementally
-  int tap = 0, th = 0, tw = 0, c0 = 0;
-  gload(0, a.dh0, a.dw0, 0);
+  int tap = ks0 / kc, c0 = (ks0 - tap * kc) * BK;
+  int th = tap / a.tkw, tw = tap - th * a.tkw;
+  gload(tap, a.dh0 + th * a.sdh, a.dw0 + tw * a.sdw, c0);
   sstore(0);
   __syncthreads();
   const int arow = wm * TM * 32 + (lane & 31);
@@ -203,8 +210,29 @@ __global__ __launch_bounds__(256) void conv_k(const ConvArgs a) {
     __syncthreads();
   }
 
-  // ---- epilogue: destination pixel offsets of the BM tile rows via LDS
-  int* dst_pix = reinterpret_cast<int*>(smem);
+  if (a.ksplit > 1) {
+    // raw partial sums; conv_reduce_k applies the epilogue in split order
+    float* ws = a.ws + (size_t)split * a.M * a.N;
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        const int n = n0 + wn * TN * 32 + j * 32 + (lane & 31);
+        if (n >= a.N) continue;
+#pragma unroll
+        for (int e = 0; e < 16; ++e) {
+          const int m = m0 + wm * TM * 32 + i * 32 + (e & 3) + 8 * (e >> 2) + 4 * (lane >> 5);
+          if (m < a.M) ws[(size_t)m * a.N + n] = acc[i][j][e];
+        }
+      }
+    return;
+  }
+
+  // ---- epilogue.  Each wave stages one 32x32 accumulator tile at a time
+  // through a private 4 KB LDS slot (the k-loop buffers are free now), then
+  // every lane handles 4 consecutive channels of a row: 16-byte loads of
+  // bias/mask/res and 16-byte stores of y/sum/y2, 128 contiguous bytes per row.
+  __shared__ int dst_pix[BM];
   if (tid < BM) {
     const int m = m0 + tid;
     int o = -1;
@@ -216,27 +244,83 @@ __global__ __launch_bounds__(256) void conv_k(const ConvArgs a) {
     dst_pix[tid] = o;
   }
   __syncthreads();
+  float* scr = smem + wave * 1024;
+  const int rr = lane >> 3, cc = (lane & 7) * 4;
 #pragma unroll
   for (int i = 0; i < TM; ++i)
 #pragma unroll
     for (int j = 0; j < TN; ++j) {
-      const int n = n0 + wn * TN * 32 + j * 32 + (lane & 31);
-      if (n >= a.N) continue;
-      const float bv = a.bias ? a.bias[n] : 0.f;
 #pragma unroll
-      for (int e = 0; e < 16; ++e) {
-        const int row = wm * TM * 32 + i * 32 + (e & 3) + 8 * (e >> 2) + 4 * (lane >> 5);
-        const int pix = dst_pix[row];
-        if (pix < 0) continue;
+      for (int e = 0; e < 16; ++e)
+        scr[((e & 3) + 8 * (e >> 2) + 4 * (lane >> 5)) * 32 + (lane & 31)] = acc[i][j][e];
+      __builtin_amdgcn_wave_barrier();
+      const int n = n0 + wn * TN * 32 + j * 32 + cc;
+      float4 bv = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (a.bias && n < a.N) bv = *reinterpret_cast<const float4*>(a.bias + n);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int row = rr + 8 * q;
+        const float4 v = *reinterpret_cast<const float4*>(scr + row * 32 + cc);
+        const int pix = dst_pix[wm * TM * 32 + i * 32 + row];
+        if (pix < 0 || n >= a.N) continue;
         const size_t o = (size_t)pix * a.Cout_p + n;
-        float v = acc[i][j][e] + bv;
-        if (a.act) v = po::leaky(v);
-        if (a.accumulate) v += a.y[o];
-        a.y[o] = a.mask ? v * po::leaky_grad(a.mask[o]) : v;
-        if (a.res) a.sum[o] = v + a.res[o];
-        if (a.y2) a.y2[o] = v * po::leaky_grad(a.mask2[o]);
+        float x[4] = {v.x + bv.x, v.y + bv.y, v.z + bv.z, v.w + bv.w};
+        if (a.act) {
+#pragma unroll
+          for (int c = 0; c < 4; ++c) x[c] = po::leaky(x[c]);
+        }
+        if (a.accumulate) {
+          const float4 p = *reinterpret_cast<const float4*>(a.y + o);
+          x[0] += p.x; x[1] += p.y; x[2] += p.z; x[3] += p.w;
+        }
+        float4 out = make_float4(x[0], x[1], x[2], x[3]);
+        if (a.mask) {
+          const float4 mk = *reinterpret_cast<const float4*>(a.mask + o);
+          out = make_float4(x[0] * po::leaky_grad(mk.x), x[1] * po::leaky_grad(mk.y),
+                            x[2] * po::leaky_grad(mk.z), x[3] * po::leaky_grad(mk.w));
+        }
+        *reinterpret_cast<float4*>(a.y + o) = out;
+        if (a.res) {
+          const float4 r = *reinterpret_cast<const float4*>(a.res + o);
+          *reinterpret_cast<float4*>(a.sum + o) = make_float4(x[0] + r.x, x[1] + r.y, x[2] + r.z, x[3] + r.w);
+        }
+        if (a.y2) {
+          const float4 mk = *reinterpret_cast<const float4*>(a.mask2 + o);
+          *reinterpret_cast<float4*>(a.y2 + o) =
+              make_float4(x[0] * po::leaky_grad(mk.x), x[1] * po::leaky_grad(mk.y), x[2] * po::leaky_grad(mk.z),
+                          x[3] * po::leaky_grad(mk.w));
+        }
       }
+      __builtin_amdgcn_wave_barrier();
     }
+}
+
+// Split-K reduction + epilogue: one thread per 4 output channels of a row.
+__global__ __launch_bounds__(256) void conv_reduce_k(const ConvArgs a) {
+  const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const int n4 = a.N / 4;
+  if (t >= (int64_t)a.M * n4) return;
+  const int m = (int)(t / n4), n = (int)(t - (int64_t)m * n4) * 4;
+  float4 v = *reinterpret_cast<const float4*>(a.ws + (size_t)m * a.N + n);
+  for (int s = 1; s < a.ksplit; ++s) {
+    const float4 p = *reinterpret_cast<const float4*>(a.ws + ((size_t)s * a.M + m) * a.N + n);
+    v.x += p.x; v.y += p.y; v.z += p.z; v.w += p.w;
+  }
+  const int HgWg = a.Hg * a.Wg;
+  const int b = m / HgWg, rem = m - b * HgWg;
+  const int i = rem / a.Wg, j = rem - i * a.Wg;
+  const size_t o = ((size_t)(b * a.Hout + i * a.out_step + a.out_oy) * a.Wout + j * a.out_step + a.out_ox) *
+                       a.Cout_p + n;
+  float r[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+  for (int c = 0; c < 4; ++c) {
+    float x = r[c] + (a.bias ? a.bias[n + c] : 0.f);
+    if (a.act) x = po::leaky(x);
+    if (a.accumulate) x += a.y[o + c];
+    a.y[o + c] = a.mask ? x * po::leaky_grad(a.mask[o + c]) : x;
+    if (a.res) a.sum[o + c] = x + a.res[o + c];
+    if (a.y2) a.y2[o + c] = x * po::leaky_grad(a.mask2[o + c]);
+  }
 }
 
 template <int BM, int BN, int WM, int BK>
@@ -244,7 +328,12 @@ int launch(const ConvArgs& a, hipStream_t st) {
   ConvArgs b = a;
   b.ntiles_n = po::ceil_div(a.N, BN);
   const int ntiles = po::ceil_div(a.M, BM) * b.ntiles_n;
-  hipLaunchKernelGGL((conv_k<BM, BN, WM, BK>), dim3(ntiles), dim3(256), 0, st, b);
+  hipLaunchKernelGGL((conv_k<BM, BN, WM, BK>), dim3(ntiles, a.ksplit), dim3(256), 0, st, b);
+  if (a.ksplit > 1) {
+    int rc = po::check_launch("po_conv");
+    if (rc) return rc;
+    hipLaunchKernelGGL(conv_reduce_k, dim3(po::ceil_div((int64_t)a.M * (a.N / 4), 256)), dim3(256), 0, st, b);
+  }
   return po::check_launch("po_conv");
 }
 
@@ -295,6 +384,10 @@ extern "C" int po_conv(const po_conv_desc* d, const float* in, const float* W, c
   a.in = in; a.W = W; a.bias = bias; a.y = y_out; a.res = res; a.sum = sum_out; a.mask = mask_y;
   a.y2 = y2_out; a.mask2 = mask2;
   a.in_org = d->in_org; a.out_org = d->out_org;
+  a.ksplit = d->ksplit > 1 ? d->ksplit : 1;
+  a.ws = d->workspace;
+  PO_REQUIRE(a.ksplit <= 64 && a.ksplit <= d->ntaps * (d->Cin_p / 16), "po_conv: ksplit %d out of range", a.ksplit);
+  PO_REQUIRE(a.ksplit == 1 || a.ws, "po_conv: ksplit > 1 needs a workspace");
   if (d->in_org || d->out_org)
     PO_REQUIRE(d->in_step == 1 && d->out_step == 1 && d->out_oy == 0 && d->out_ox == 0,
                "po_conv: window buffers need in_step = out_step = 1 and no output offset");

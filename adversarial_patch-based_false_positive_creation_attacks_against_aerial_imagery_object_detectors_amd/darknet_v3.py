@@ -164,6 +164,7 @@ class NetPlan:
         self.net, self.B, self.H, self.W, self.device = net, B, H, W, device
         self.gen = 0
         self.conv_timer = None        # list: (start, end, MACs) HIP events of every po_conv launch
+        self.ws = None                # split-K workspace (shared by every launch; stream-ordered)
         blocks = net.blocks
         n = len(blocks)
         self.n = n
@@ -495,6 +496,7 @@ class NetPlan:
                 args = (nat.ctypes.byref(desc), P(inp), P(wts["w"]), P(wts["bias"]), P(y_out), P(res),
                         P(sum_out), None, None, None)
                 desc.macs = B * desc.Hg * desc.Wg * m["cout"] * m["cin"] * k * k      # logical channels
+                desc.block, desc.kind = i, "fwd"
                 fwd.append(("po_conv", args, desc))
             elif t == "shortcut":
                 if i in self.fused:
@@ -701,6 +703,7 @@ class NetPlan:
                 desc.act = 0
                 desc.accumulate = acc
                 desc.macs = self.B * Hg * Wg * m["cin"] * len(taps) * m["cout"]
+                desc.block, desc.kind = j, "dgrad"
                 out.append((desc, wd))
         return out
 
@@ -710,11 +713,21 @@ class NetPlan:
         return sum(d.macs for name, _, d in self.fwd_ops + self.bwd_ops if name == "po_conv")
 
     # ---------------- autotuning ----------------
+    SPLITS = (2, 4, 8, 16, 32)
+    WS_FLOATS = 64 << 20          # split-K workspace cap (256 MB)
+
+    def _ensure_ws(self, floats):
+        if self.ws is None or self.ws.numel() < floats:
+            self.ws = torch.empty(floats, device=self.device)
+        return self.ws
+
     def tune(self, cache, iters=4):
-        """Time every candidate tile of po_conv for each distinct launch shape of
-        this plan on the current GPU and keep the fastest (wave quantisation
-        over the 256 CUs and the k-step size decide it per shape).  ``cache``
-        maps a launch signature to its tile and is shared between plans."""
+        """Time every candidate (tile, split-K) of po_conv for each distinct
+        launch shape of this plan on the current GPU and keep the fastest
+        (wave quantisation over the 256 CUs, the k-step size and, for launches
+        with few tiles — the receptive-field windows — splitting K over more
+        workgroups decide it per shape).  ``cache`` maps a launch signature
+        to (tile, ksplit) and is shared between plans."""
         lib = self.lib
         st = nat.stream()
         bufs = {id(t): t for t in self.act + self.grad if t is not None}
@@ -735,31 +748,50 @@ class NetPlan:
             key = (desc.B, desc.Hin, desc.Win, desc.Cin_p, desc.Hg, desc.Wg, desc.in_step, desc.ntaps, desc.N,
                    desc.accumulate, args[6] is not None, args[7] is not None, args[8] is not None)
             if key in cache:
-                desc.tile = cache[key]
+                self._set_tile(desc, cache[key])
                 continue
+            M = desc.B * desc.Hg * desc.Wg
             best = None
             for t, bm, bn, bk in tiles:
                 if bk == 32 and desc.Cin_p % 32:
                     continue
                 if bn > max(32, desc.N):
                     continue
-                desc.tile = t
-                for _ in range(2):
-                    lib.po_conv(*args, st)
-                e0.record()
-                for _ in range(iters):
-                    lib.po_conv(*args, st)
-                e1.record()
-                e1.synchronize()
-                ms = e0.elapsed_time(e1)
-                if best is None or ms < best[0]:
-                    best = (ms, t)
-            desc.tile = best[1]
-            cache[key] = best[1]
+                ntiles = -(-M // bm) * -(-desc.N // bn)
+                nks = desc.ntaps * desc.Cin_p // bk
+                cands = [1]
+                if ntiles < 256:
+                    cands += [k for k in self.SPLITS if k * ntiles <= 2048 and nks // k >= 4
+                              and k * M * desc.N <= self.WS_FLOATS]
+                for ks in cands:
+                    self._set_tile(desc, (t, ks))
+                    for _ in range(2):
+                        lib.po_conv(*args, st)
+                    e0.record()
+                    for _ in range(iters):
+                        lib.po_conv(*args, st)
+                    e1.record()
+                    e1.synchronize()
+                    ms = e0.elapsed_time(e1)
+                    if best is None or ms < best[0]:
+                        best = (ms, (t, ks))
+            self._set_tile(desc, best[1])
+            cache[key] = list(best[1])
+        for name, _, desc in self.fwd_ops + self.bwd_ops:     # the workspace may have grown
+            if name == "po_conv" and desc.ksplit > 1:
+                desc.workspace = self.ws.data_ptr()
         with torch.no_grad():
             for t in bufs.values():
                 t.zero_()
         torch.cuda.synchronize()
+
+    def _set_tile(self, desc, choice):
+        t, ks = (choice, 1) if isinstance(choice, int) else choice
+        desc.tile, desc.ksplit = t, ks
+        if ks > 1:
+            desc.workspace = self._ensure_ws(ks * desc.B * desc.Hg * desc.Wg * desc.N).data_ptr()
+        else:
+            desc.workspace = None
 
     # ---------------- execution ----------------
     def run_forward(self, x):

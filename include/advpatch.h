@@ -162,6 +162,11 @@ typedef struct po_conv_desc {
                                  (po_conv_tile_info), chosen by the caller's autotuner */
   const int32_t* in_org;      /* NULL: full-map source */
   const int32_t* out_org;     /* NULL: full-map destination */
+  int ksplit;                 /* <= 1: one pass over K; > 1: the k-steps are split over
+                                 ksplit workgroups per tile whose partial sums (workspace,
+                                 >= ksplit*M*N floats, M = B*Hg*Wg) are reduced in split
+                                 order by a second kernel that applies the epilogue */
+  float* workspace;
 } po_conv_desc;
 
 #define PO_CONV_NTILES 10

@@ -37,7 +37,7 @@ def test_library_exports_every_header_symbol():
 def test_conv_desc_struct_matches_header():
     text = open(HEADER).read()
     body = text[text.index("typedef struct po_conv_desc"):text.index("} po_conv_desc;")]
-    fields = re.findall(r"(?:int|int32_t\*)\s+([^;]+);", body)
+    fields = re.findall(r"(?:int|int32_t\*|float\*)\s+([^;]+);", body)
     names = []
     for f in fields:
         for part in f.split(","):

@@ -107,3 +107,37 @@ def test_heads_layout_matches_reference_view(tmp_path):
     for h, r in zip(heads_nhwc, outs):
         hc = h.detach().cpu()[..., :60].permute(0, 3, 1, 2)
         assert _rel(hc, r) < 2e-5
+
+
+@pytest.mark.parametrize("B,H,Cin,Cout,k", [(4, 5, 512, 1024, 3), (16, 1, 1024, 64, 1), (3, 7, 96, 128, 3)])
+def test_split_k_matches_single_pass(B, H, Cin, Cout, k):
+    """po_conv with the k-steps split over workgroups (partials reduced in
+    split order by the epilogue kernel) against one pass and torch conv2d."""
+    import ctypes
+    nat = pkg_mod("_native")
+    pad = (k - 1) // 2
+    gen = torch.Generator().manual_seed(11)
+    x = torch.randn(B, Cin, H, H, generator=gen)
+    w = torch.randn(Cout, Cin, k, k, generator=gen) * (2.0 / (Cin * k * k)) ** 0.5
+    bias = torch.randn(Cout, generator=gen) * 0.1
+    ref = torch.nn.functional.leaky_relu(torch.nn.functional.conv2d(x, w, bias, padding=pad), 0.1)
+    xd = x.permute(0, 2, 3, 1).contiguous().to(DEV)
+    wd = w.permute(0, 2, 3, 1).reshape(Cout, k * k, Cin).contiguous().to(DEV)
+    bd = bias.to(DEV)
+    outs = {}
+    for ks in (1, 2, 5, 8):
+        y = torch.full((B, H, H, Cout), float("nan"), device=DEV)
+        ws = torch.empty(ks * B * H * H * Cout, device=DEV)
+        d = nat.po_conv_desc()
+        d.B, d.Hin, d.Win, d.Cin_p, d.Hout, d.Wout, d.Cout_p, d.Hg, d.Wg = B, H, H, Cin, H, H, Cout, H, H
+        d.in_step, d.out_step, d.ntaps, d.N, d.act = 1, 1, k * k, Cout, 1
+        for kh in range(k):
+            for kw in range(k):
+                d.dh[kh * k + kw], d.dw[kh * k + kw] = kh - pad, kw - pad
+        d.ksplit, d.workspace = ks, ws.data_ptr()
+        nat.call("po_conv", ctypes.byref(d), nat.ptr(xd), nat.ptr(wd), nat.ptr(bd), nat.ptr(y), None, None, None,
+                 None, None, nat.stream())
+        outs[ks] = y.permute(0, 3, 1, 2).cpu()
+    for ks, y in outs.items():
+        assert _rel(y, ref) < 1e-5, (ks, _rel(y, ref))
+        assert _rel(y, outs[1]) < 1e-5, (ks, _rel(y, outs[1]))

@@ -150,7 +150,10 @@ def test_windowed_plan_matches_full_maps(tmp_path, cfg, B, P):
     (t0, g0), (t1, g1) = out
     assert int(t1["flags"].item()) == 0
     assert t0["cells"].tolist() == t1["cells"].tolist()
+    # the window launches may split K differently (autotuned), so the sums
+    # agree to fp32 reassociation, not bitwise
     for k in ("loss", "no_obj_loss", "no_cls_loss"):
-        assert float(t0[k]) == float(t1[k]), (k, float(t0[k]), float(t1[k]))
-    torch.testing.assert_close(t1["obj"], t0["obj"], rtol=0, atol=0)
-    assert torch.equal(g0, g1), float((g0 - g1).abs().max())
+        assert abs(float(t0[k]) - float(t1[k])) <= 1e-5 * max(1.0, abs(float(t0[k]))), (k, float(t0[k]), float(t1[k]))
+    torch.testing.assert_close(t1["obj"], t0["obj"], rtol=0, atol=1e-5)
+    rel = float((g0 - g1).abs().max() / g0.abs().max())
+    assert rel < 1e-4, rel

@@ -1,0 +1,66 @@
+"""Per-launch conv timing of the bench step (HIP events around every po_conv).
+
+    python tools/step_breakdown.py [--config yolov3] [--batch 16] [--steps 5] [--windows 1]
+"""
+import argparse
+import os
+import sys
+from collections import defaultdict
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+import torch  # noqa: E402
+
+import bench  # noqa: E402
+import __graft_entry__ as ge  # noqa: E402
+
+ap = argparse.ArgumentParser()
+ap.add_argument("--config", default="yolov3")
+ap.add_argument("--batch", type=int, default=None)
+ap.add_argument("--steps", type=int, default=5)
+ap.add_argument("--windows", type=int, default=1)
+args = ap.parse_args()
+cfg, S, P, Bdef = bench.CONFIGS[args.config]
+B = args.batch or Bdef
+os.environ.setdefault("ADVPATCH_TUNE_CACHE", os.path.join(ROOT, "weights", "conv_tiles_%s_b%d.json" % (args.config, B)))
+tp, pc, sy, W = ge._pkg("train_patch"), ge._pkg("patch_config"), ge._pkg("synthetic"), ge._pkg("weights")
+dev = torch.device("cuda", 0)
+wpath = pc.synthetic_weights_path(cfg.split(":")[-1])
+W.ensure_synthetic(cfg, wpath)
+
+
+class _Cfg(pc.ReproducePaperObj):
+    def __init__(self):
+        super().__init__()
+        self.cfgfile, self.weightfile, self.batch_size = cfg, wpath, B
+
+
+pc.patch_configs["_bd"] = _Cfg
+tr = tp.PatchTrainer("_bd", device=dev, verbose=False)
+tr.darknet_model.window_heads = bool(args.windows)
+img, lab = sy.frames(B, S, seed=1000).to(dev), sy.labels(B, seed=2000).to(dev)
+patch = sy.patch(P, seed=2).to(dev).requires_grad_(True)
+opt = tr.make_optimizer(patch)
+for _ in range(3):
+    tr.step(patch, opt, img, lab)
+torch.cuda.synchronize()
+plan = tr.last_plan
+plan.conv_timer = []
+for _ in range(args.steps):
+    tr.step(patch, opt, img, lab)
+torch.cuda.synchronize()
+timer = plan.conv_timer
+n = len(timer) // args.steps
+descs = [d for name, _, d in plan.fwd_ops + plan.bwd_ops if name == "po_conv"]
+assert len(descs) == n
+ms = defaultdict(float)
+for k, (e0, e1, _) in enumerate(timer):
+    ms[k % n] += e0.elapsed_time(e1) / args.steps
+tot = sum(ms.values())
+print("%-6s %-5s %5s %9s %5s %6s %4s %9s %7s %6s" % ("kind", "block", "B*Hg*Wg", "", "N", "K", "tile", "us", "TF", "%"))
+for k, d in enumerate(descs):
+    K = d.ntaps * d.Cin_p
+    M = d.B * d.Hg * d.Wg
+    print("%-6s %5d %9d %5d %6d %4d %9.1f %7.1f %6.2f" % (d.kind, d.block, M, d.N, K, d.tile, ms[k] * 1e3,
+                                                      2 * d.macs / (ms[k] * 1e-3) / 1e12, 100 * ms[k] / tot))
+print("total conv ms/step %.3f, launches %d, executed TFLOP/step %.3f" % (tot, n, 2 * sum(d.macs for d in descs) / 1e12))
