@@ -13,6 +13,8 @@ LIB_PATH = os.path.join(_HERE, "libadvpatch_hip.so")
 
 c_int, c_float, c_int64, c_void_p = ctypes.c_int, ctypes.c_float, ctypes.c_int64, ctypes.c_void_p
 
+PO_CONV_NTILES = 28   # include/advpatch.h
+
 
 class po_conv_desc(ctypes.Structure):
     _fields_ = [(n, c_int) for n in (

@@ -46,7 +46,12 @@ struct ConvArgs {
   int tkw, dh0, dw0, sdh, sdw;
 };
 
-template <int BM, int BN, int WM, int BK>
+// 16-byte LDS-DMA: lane l's 16 bytes from rsrc+voff land at lds + 16*l
+__device__ __forceinline__ void lds_dma16(__amdgpu_buffer_rsrc_t rs, float* lds, uint32_t voff) {
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (__attribute__((address_space(3))) void*)lds, 16, voff, 0, 0, 0);
+}
+
+template <int BM, int BN, int WM, int BK, bool GL>
 __global__ __launch_bounds__(256) void conv_k(const ConvArgs a) {
   constexpr int WN = 4 / WM;
   constexpr int TM = BM / WM / 32;
@@ -83,19 +88,29 @@ __global__ __launch_bounds__(256) void conv_k(const ConvArgs a) {
   constexpr uint32_t kOOB = 0x80000000u;
   const uint32_t pix_bytes = (uint32_t)a.Cin_p * 4u;
 
-  // ---- A loader state (rows rth + RPP*r of the tile): byte offset of the
-  // row's first channel chunk at tap (0,0); hi/wi for the bounds test
-  int a_hi[AL], a_wi[AL];
-  uint32_t a_off[AL];
+  // ---- A loader state.  Register staging (GL = false): thread (rth, cth)
+  // loads chunk cth of rows rth + RPP*r.  LDS-DMA staging (GL = true): the
+  // tile is cut into 1 KB pieces (RPI rows); lane L of the wave that owns
+  // piece p loads row p*RPI + L/CPR, and the chunk that lands in slot L%CPR
+  // of the XOR-swizzled row (the swizzle goes on the source address).
+  constexpr int RPI = 64 / CPR;                // rows per 1 KB piece
+  constexpr int NPA = BM / RPI, NPB = BN / RPI;
+  constexpr int PA = GL ? (NPA + 3) / 4 : AL;  // loader slots per thread / wave
+  constexpr int PB = GL ? (NPB + 3) / 4 : BL;
+  const int wave_u = __builtin_amdgcn_readfirstlane(wave);
+  auto a_row = [&](int r) { return GL ? (wave_u + 4 * r) * RPI + lane / CPR : rth + RPP * r; };
+  auto a_chunk = [&](int row) { return GL ? ((lane % CPR) ^ ((row >> SW) & (CPR - 1))) : cth; };
+  int a_hi[PA], a_wi[PA];
+  uint32_t a_off[PA];
 #pragma unroll
-  for (int r = 0; r < AL; ++r) {
-    const int row = rth + RPP * r;
+  for (int r = 0; r < PA; ++r) {
+    const int row = a_row(r);
     const int m = m0 + row;
     const bool ok = (row < BM) && (m < a.M);
     const int mm = ok ? m : 0;
     const int b = mm / HgWg, rem = mm - b * HgWg;
     const int i = rem / a.Wg, j = rem - i * a.Wg;
-    a_off[r] = ((uint32_t)b * a.Hin * a.Win) * pix_bytes + cth * 16u;
+    a_off[r] = ((uint32_t)b * a.Hin * a.Win) * pix_bytes + a_chunk(row) * 16u;
     // window buffers: shift from output-buffer to input-buffer coordinates
     int sy = 0, sx = 0;
     if (a.out_org) { sy += a.out_org[2 * b]; sx += a.out_org[2 * b + 1]; }
@@ -106,28 +121,45 @@ __global__ __launch_bounds__(256) void conv_k(const ConvArgs a) {
   }
   // ---- B loader state
   const uint32_t wrow_bytes = (uint32_t)a.ntaps * pix_bytes;
-  uint32_t b_off[BL];
+  uint32_t b_off[PB];
 #pragma unroll
-  for (int r = 0; r < BL; ++r) {
-    const int row = rth + RPP * r;
+  for (int r = 0; r < PB; ++r) {
+    const int row = a_row(r);
     const bool ok = (row < BN) && (n0 + row < a.N);
-    b_off[r] = ok ? (uint32_t)(n0 + row) * wrow_bytes + cth * 16u : kOOB;
+    b_off[r] = ok ? (uint32_t)(n0 + row) * wrow_bytes + a_chunk(row) * 16u : kOOB;
   }
 
-  float4 ra[AL], rb[BL];
+  float4 ra[GL ? 1 : AL], rb[GL ? 1 : BL];
+  auto a_offset = [&](int r, int dh, int dw, uint32_t cb) {
+    const int hi = a_hi[r] + dh, wi = a_wi[r] + dw;
+    const bool ok = (unsigned)hi < (unsigned)a.Hin && (unsigned)wi < (unsigned)a.Win;
+    return ok ? a_off[r] + ((uint32_t)hi * a.Win + wi) * pix_bytes + cb : kOOB;
+  };
   auto gload = [&](int tap, int dh, int dw, int c0) {
     const uint32_t cb = (uint32_t)c0 * 4u;
 #pragma unroll
-    for (int r = 0; r < AL; ++r) {
-      const int hi = a_hi[r] + dh, wi = a_wi[r] + dw;
-      const bool ok = (unsigned)hi < (unsigned)a.Hin && (unsigned)wi < (unsigned)a.Win;
-      const uint32_t off = ok ? a_off[r] + ((uint32_t)hi * a.Win + wi) * pix_bytes + cb : kOOB;
-      ra[r] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(in_rs, off, 0, 0));
-    }
+    for (int r = 0; r < AL; ++r)
+      ra[r] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(in_rs, a_offset(r, dh, dw, cb), 0, 0));
     const uint32_t tb = (uint32_t)tap * pix_bytes + cb;
 #pragma unroll
     for (int r = 0; r < BL; ++r)
       rb[r] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(w_rs, b_off[r] + tb, 0, 0));
+  };
+  auto gload_lds = [&](int buf, int tap, int dh, int dw, int c0) {
+    const uint32_t cb = (uint32_t)c0 * 4u;
+#pragma unroll
+    for (int r = 0; r < PA; ++r) {
+      const int p = wave_u + 4 * r;
+      if (p < NPA)
+        lds_dma16(in_rs, As + (buf * BM + p * RPI) * BK, a_offset(r, dh, dw, cb));
+    }
+    const uint32_t tb = (uint32_t)tap * pix_bytes + cb;
+#pragma unroll
+    for (int r = 0; r < PB; ++r) {
+      const int p = wave_u + 4 * r;
+      if (p < NPB)
+        lds_dma16(w_rs, Bs + (buf * BN + p * RPI) * BK, b_off[r] + tb);
+    }
   };
   auto swz = [](int row, int chunk) { return (chunk ^ ((row >> SW) & (CPR - 1))) * 4; };
   auto sstore = [&](int buf) {
@@ -162,8 +194,12 @@ __global__ __launch_bounds__(256) void conv_k(const ConvArgs a) {
   // k-step position: tap (th, tw) and channel offset c0, advanced incrementally
   int tap = ks0 / kc, c0 = (ks0 - tap * kc) * BK;
   int th = tap / a.tkw, tw = tap - th * a.tkw;
-  gload(tap, a.dh0 + th * a.sdh, a.dw0 + tw * a.sdw, c0);
-  sstore(0);
+  if constexpr (GL) {
+    gload_lds(0, tap, a.dh0 + th * a.sdh, a.dw0 + tw * a.sdw, c0);
+  } else {
+    gload(tap, a.dh0 + th * a.sdh, a.dw0 + tw * a.sdw, c0);
+    sstore(0);
+  }
   __syncthreads();
   const int arow = wm * TM * 32 + (lane & 31);
   const int brow = wn * TN * 32 + (lane & 31);
@@ -186,7 +222,11 @@ __global__ __launch_bounds__(256) void conv_k(const ConvArgs a) {
         const int row = brow + j * 32;
         bf[j] = *reinterpret_cast<const float4*>(&Bb[row * BK + swz(row, 2 * g + h)]);
       }
+#ifdef PO_ABLATE_NOLOAD
+      if (false) {      // ablation build (tools/): k-steps without staging loads
+#else
       if (g == 0 && more) {
+#endif
         // issue the next k-step's staging loads behind this group's fragment reads
         c0 += BK;
         if (c0 == a.Cin_p) {
@@ -194,7 +234,10 @@ __global__ __launch_bounds__(256) void conv_k(const ConvArgs a) {
           ++tap;
           if (++tw == a.tkw) { tw = 0; ++th; }
         }
-        gload(tap, a.dh0 + th * a.sdh, a.dw0 + tw * a.sdw, c0);
+        if constexpr (GL)
+          gload_lds(buf ^ 1, tap, a.dh0 + th * a.sdh, a.dw0 + tw * a.sdw, c0);
+        else
+          gload(tap, a.dh0 + th * a.sdh, a.dw0 + tw * a.sdw, c0);
       }
 #pragma unroll
       for (int i = 0; i < TM; ++i)
@@ -206,7 +249,11 @@ __global__ __launch_bounds__(256) void conv_k(const ConvArgs a) {
           acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(af[i].w, bf[j].w, acc[i][j], 0, 0, 0);
         }
     }
-    if (more) sstore(buf ^ 1);
+#ifndef PO_ABLATE_NOLOAD
+    if constexpr (!GL) {
+      if (more) sstore(buf ^ 1);
+    }
+#endif
     __syncthreads();
   }
 
@@ -323,12 +370,12 @@ __global__ __launch_bounds__(256) void conv_reduce_k(const ConvArgs a) {
   }
 }
 
-template <int BM, int BN, int WM, int BK>
+template <int BM, int BN, int WM, int BK, bool GL>
 int launch(const ConvArgs& a, hipStream_t st) {
   ConvArgs b = a;
   b.ntiles_n = po::ceil_div(a.N, BN);
   const int ntiles = po::ceil_div(a.M, BM) * b.ntiles_n;
-  hipLaunchKernelGGL((conv_k<BM, BN, WM, BK>), dim3(ntiles, a.ksplit), dim3(256), 0, st, b);
+  hipLaunchKernelGGL((conv_k<BM, BN, WM, BK, GL>), dim3(ntiles, a.ksplit), dim3(256), 0, st, b);
   if (a.ksplit > 1) {
     int rc = po::check_launch("po_conv");
     if (rc) return rc;
@@ -337,26 +384,39 @@ int launch(const ConvArgs& a, hipStream_t st) {
   return po::check_launch("po_conv");
 }
 
-template <int BK>
+template <int BK, bool GL>
 int dispatch(const ConvArgs& a, hipStream_t st, int bm, int bn) {
-  if (bm == 128 && bn == 128) return launch<128, 128, 2, BK>(a, st);
-  if (bm == 64 && bn == 128) return launch<64, 128, 1, BK>(a, st);
-  if (bm == 128 && bn == 64) return launch<128, 64, 4, BK>(a, st);
-  if (bm == 64 && bn == 64) return launch<64, 64, 2, BK>(a, st);
-  if (bm == 128 && bn == 32) return launch<128, 32, 4, BK>(a, st);
+  if (bm == 128 && bn == 128) return launch<128, 128, 2, BK, GL>(a, st);
+  if (bm == 64 && bn == 128) return launch<64, 128, 1, BK, GL>(a, st);
+  if (bm == 128 && bn == 64) return launch<128, 64, 4, BK, GL>(a, st);
+  if (bm == 64 && bn == 64) return launch<64, 64, 2, BK, GL>(a, st);
+  if (bm == 128 && bn == 32) return launch<128, 32, 4, BK, GL>(a, st);
+  if (bm == 256 && bn == 128) return launch<256, 128, 2, BK, GL>(a, st);
+  if (bm == 128 && bn == 256) return launch<128, 256, 2, BK, GL>(a, st);
   po::set_error("po_conv: no %dx%d tile", bm, bn);
   return PO_EINVAL;
 }
 
-// ADVPATCH_CONV_TILE="BMxBNxBK" forces a tile (tuning experiments only).
-bool forced_tile(int& bm, int& bn, int& bk) {
+// ADVPATCH_CONV_TILE="BMxBNxBK[g]" forces a tile (tuning experiments only;
+// a trailing 'g' selects LDS-DMA staging).
+bool forced_tile(int& bm, int& bn, int& bk, int& gl) {
   const char* e = getenv("ADVPATCH_CONV_TILE");
-  return e && sscanf(e, "%dx%dx%d", &bm, &bn, &bk) == 3;
+  char g = 0;
+  if (!e || sscanf(e, "%dx%dx%d%c", &bm, &bn, &bk, &g) < 3) return false;
+  gl = g == 'g';
+  return true;
 }
 
-constexpr int kTiles[PO_CONV_NTILES][3] = {
-    {128, 128, 16}, {128, 128, 32}, {64, 128, 16}, {64, 128, 32}, {128, 64, 16},
-    {128, 64, 32},  {64, 64, 16},   {64, 64, 32},  {128, 32, 16}, {128, 32, 32}};
+// tiles 1..10 stage through registers + ds_write; 11..20 are the same
+// shapes staged by LDS-DMA (buffer_load ... lds); 21..28 are the 8-accumulator
+// (64x128 / 128x64 per wave) shapes, register- then DMA-staged
+constexpr int kTiles[PO_CONV_NTILES][4] = {
+    {128, 128, 16, 0}, {128, 128, 32, 0}, {64, 128, 16, 0}, {64, 128, 32, 0}, {128, 64, 16, 0},
+    {128, 64, 32, 0},  {64, 64, 16, 0},   {64, 64, 32, 0},  {128, 32, 16, 0}, {128, 32, 32, 0},
+    {128, 128, 16, 1}, {128, 128, 32, 1}, {64, 128, 16, 1}, {64, 128, 32, 1}, {128, 64, 16, 1},
+    {128, 64, 32, 1},  {64, 64, 16, 1},   {64, 64, 32, 1},  {128, 32, 16, 1}, {128, 32, 32, 1},
+    {256, 128, 16, 0}, {256, 128, 32, 0}, {128, 256, 16, 0}, {128, 256, 32, 0},
+    {256, 128, 16, 1}, {256, 128, 32, 1}, {128, 256, 16, 1}, {128, 256, 32, 1}};
 }  // namespace
 
 extern "C" int po_conv_tile_info(int t, int* bm, int* bn, int* bk) {
@@ -418,13 +478,14 @@ extern "C" int po_conv(const po_conv_desc* d, const float* in, const float* W, c
     PO_REQUIRE(d->dh[t] == a.dh0 + (t / tkw) * a.sdh && d->dw[t] == a.dw0 + (t % tkw) * a.sdw,
                "po_conv: tap %d (%d,%d) breaks the rectangular tap grid", t, d->dh[t], d->dw[t]);
   hipStream_t st = po::stream_of(s);
-  int bm, bn, bk;
+  int bm, bn, bk, gl = 0;
   PO_REQUIRE(d->tile >= 0 && d->tile <= PO_CONV_NTILES, "po_conv: tile %d out of range", d->tile);
   if (d->tile > 0) {
     bm = kTiles[d->tile - 1][0];
     bn = kTiles[d->tile - 1][1];
     bk = kTiles[d->tile - 1][2];
-  } else if (!forced_tile(bm, bn, bk)) {
+    gl = kTiles[d->tile - 1][3];
+  } else if (!forced_tile(bm, bn, bk, gl)) {
     // largest tile that still gives >= 2 workgroups per CU
     const int64_t M = a.M;
     const int N = a.N;
@@ -437,5 +498,6 @@ extern "C" int po_conv(const po_conv_desc* d, const float* in, const float* W, c
     else { bm = 64; bn = 64; }
   }
   if (bk == 32 && a.Cin_p % 32 != 0) bk = 16;
-  return bk == 32 ? dispatch<32>(a, st, bm, bn) : dispatch<16>(a, st, bm, bn);
+  if (gl) return bk == 32 ? dispatch<32, true>(a, st, bm, bn) : dispatch<16, true>(a, st, bm, bn);
+  return bk == 32 ? dispatch<32, false>(a, st, bm, bn) : dispatch<16, false>(a, st, bm, bn);
 }

@@ -737,7 +737,7 @@ class NetPlan:
             for t in bufs.values():
                 t.uniform_(-1.0, 1.0)           # time on random data, not zeros (clock)
         tiles = []
-        for t in range(1, 11):
+        for t in range(1, nat.PO_CONV_NTILES + 1):
             bm, bn, bk = nat.c_int(), nat.c_int(), nat.c_int()
             nat.call("po_conv_tile_info", t, nat.ctypes.byref(bm), nat.ctypes.byref(bn), nat.ctypes.byref(bk))
             tiles.append((t, bm.value, bn.value, bk.value))

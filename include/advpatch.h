@@ -169,9 +169,12 @@ typedef struct po_conv_desc {
   float* workspace;
 } po_conv_desc;
 
-#define PO_CONV_NTILES 10
+#define PO_CONV_NTILES 28
 /* Tile `t` (1-based): block rows BM (output pixels), block columns BN (output
- * channels), k-step BK (input channels).  Returns PO_EINVAL for a bad index. */
+ * channels), k-step BK (input channels).  Tiles 1..10 stage operands through
+ * registers, 11..20 are the same shapes staged by LDS-DMA, 21..28 are
+ * 256x128 / 128x256 blocks (register, then LDS-DMA staging).  Returns
+ * PO_EINVAL for a bad index. */
 int po_conv_tile_info(int t, int* bm, int* bn, int* bk);
 
 /* v[m][n] = act(sum_k A[m][k] * W[n][k] + bias[n]) (+ y_out[m][n] if accumulate);

@@ -141,3 +141,30 @@ def test_split_k_matches_single_pass(B, H, Cin, Cout, k):
     for ks, y in outs.items():
         assert _rel(y, ref) < 1e-5, (ks, _rel(y, ref))
         assert _rel(y, outs[1]) < 1e-5, (ks, _rel(y, outs[1]))
+
+
+@pytest.mark.parametrize("tile", list(range(1, 29)))
+def test_every_conv_tile(tile):
+    """Every po_conv tile (register-staged 1..10, LDS-DMA-staged 11..20) on a
+    3x3 conv with zero padding, a ragged pixel count and a ragged channel
+    count, against torch conv2d."""
+    import ctypes
+    nat = pkg_mod("_native")
+    B, H, Cin, Cout, k = 3, 7, 96, 96, 3
+    gen = torch.Generator().manual_seed(tile)
+    x = torch.randn(B, Cin, H, H, generator=gen)
+    w = torch.randn(Cout, Cin, k, k, generator=gen) * (2.0 / (Cin * k * k)) ** 0.5
+    bias = torch.randn(Cout, generator=gen) * 0.1
+    ref = torch.nn.functional.conv2d(x, w, bias, padding=1)
+    y = torch.full((B, H, H, Cout), float("nan"), device=DEV)
+    d = nat.po_conv_desc()
+    d.B, d.Hin, d.Win, d.Cin_p, d.Hout, d.Wout, d.Cout_p, d.Hg, d.Wg = B, H, H, Cin, H, H, Cout, H, H
+    d.in_step, d.out_step, d.ntaps, d.N, d.act, d.tile = 1, 1, 9, Cout, 0, tile
+    for kh in range(3):
+        for kw in range(3):
+            d.dh[kh * 3 + kw], d.dw[kh * 3 + kw] = kh - 1, kw - 1
+    xd = x.permute(0, 2, 3, 1).contiguous().to(DEV)
+    wd = w.permute(0, 2, 3, 1).reshape(Cout, 9, Cin).contiguous().to(DEV)
+    nat.call("po_conv", ctypes.byref(d), nat.ptr(xd), nat.ptr(wd), nat.ptr(bias.to(DEV)), nat.ptr(y), None, None,
+             None, None, None, nat.stream())
+    assert _rel(y.permute(0, 3, 1, 2).cpu(), ref) < 1e-5

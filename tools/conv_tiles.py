@@ -9,7 +9,8 @@ SHAPES = [(16, 76, 128, 256, 3, 1), (16, 38, 256, 512, 3, 1), (16, 19, 512, 1024
           (16, 304, 32, 64, 3, 1), (16, 76, 256, 128, 1, 1), (16, 38, 512, 256, 1, 1), (16, 19, 1024, 512, 1, 1),
           (16, 304, 64, 32, 1, 1), (16, 152, 64, 128, 3, 2)]
 TILES = ["128x128x16", "128x128x32", "64x128x16", "64x128x32", "128x64x16", "128x64x32", "64x64x16", "64x64x32",
-         "128x32x16", "128x32x32", "default"]
+         "128x128x16g", "128x128x32g", "64x128x16g", "64x128x32g", "64x64x16g", "64x64x32g",
+         "128x32x16", "128x32x32", "256x128x16", "256x128x16g", "128x256x16", "128x256x16g", "default"]
 st = nat.stream()
 for (B, H, Cin, Cout, k, s) in SHAPES:
     pad = (k - 1) // 2

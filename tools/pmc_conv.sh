@@ -1,17 +1,18 @@
 #!/bin/bash
 # PMC passes over the conv microbenchmark (one counter group per pass).
+# usage: tools/pmc_conv.sh OUTDIR "B H Cin Cout k s iters" [TILE]
 set -e
 cd /tmp && export TMPDIR=/tmp
 cd "$GRAFT_REPO_ROOT"
-OUT=gpurun_out/pmc_conv
+OUT=${1:-gpurun_out/pmc_conv}
+SHAPE=${2:-"16 76 128 256 3 1 30"}
+export ADVPATCH_CONV_TILE=${3:-128x128x16}
 mkdir -p $OUT
-SHAPE="16 76 128 256 3 1 30"
 timeout -k 10 120 python tools/conv_micro.py $SHAPE > $OUT/plain.txt 2>&1
-rocprofv3 -L > $OUT/counters.txt 2>&1 || true
 i=0
 for grp in "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_MFMA SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_INSTS_SALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES" \
            "SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_MFMA SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_VMEM GRBM_GUI_ACTIVE" \
            "SQ_VALU_MFMA_BUSY_CYCLES SQ_LDS_BANK_CONFLICT SQ_WAIT_INST_LDS SQ_INST_CYCLES_VMEM_RD GRBM_COUNT"; do
   i=$((i+1))
-  timeout -k 10 180 rocprofv3 --pmc $grp --kernel-include-regex conv_k -d $OUT/p$i -o p$i --output-format csv -- python tools/conv_micro.py $SHAPE > $OUT/p$i.log 2>&1 || echo "pass $i failed"
+  timeout -k 10 180 rocprofv3 --pmc $grp --kernel-include-regex conv_k --output-format csv -d $OUT/p$i -o p$i -- python tools/conv_micro.py $SHAPE > $OUT/p$i.log 2>&1 || { echo "pass $i failed"; exit 1; }
 done
