@@ -13,7 +13,8 @@ LIB_PATH = os.path.join(_HERE, "libadvpatch_hip.so")
 
 c_int, c_float, c_int64, c_void_p = ctypes.c_int, ctypes.c_float, ctypes.c_int64, ctypes.c_void_p
 
-PO_CONV_NTILES = 28   # include/advpatch.h
+PO_CONV_NTILES = 45   # include/advpatch.h
+PO_AMAX_SUB = 64      # sub-slots per max|x| slot
 
 
 class po_conv_desc(ctypes.Structure):
@@ -22,7 +23,9 @@ class po_conv_desc(ctypes.Structure):
         "in_step", "out_step", "out_oy", "out_ox", "ntaps")] + [
         ("dh", c_int * 9), ("dw", c_int * 9),
         ("N", c_int), ("act", c_int), ("accumulate", c_int), ("tile", c_int),
-        ("in_org", c_void_p), ("out_org", c_void_p), ("ksplit", c_int), ("workspace", c_void_p)]
+        ("in_org", c_void_p), ("out_org", c_void_p), ("ksplit", c_int), ("workspace", c_void_p),
+        ("prec", c_int), ("w_shift", c_int), ("in_amax", c_void_p), ("y_amax", c_void_p),
+        ("sum_amax", c_void_p), ("y2_amax", c_void_p)]
 
 
 _SIGS = {
@@ -46,22 +49,24 @@ _SIGS = {
                         c_void_p, c_void_p],
     "po_conv": [ctypes.POINTER(po_conv_desc), c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
                 c_void_p, c_void_p, c_void_p, c_void_p, c_void_p],
-    "po_conv_tile_info": [c_int, ctypes.POINTER(c_int), ctypes.POINTER(c_int), ctypes.POINTER(c_int)],
+    "po_conv_tile_info": [c_int, ctypes.POINTER(c_int), ctypes.POINTER(c_int), ctypes.POINTER(c_int),
+                          ctypes.POINTER(c_int)],
     "po_conv_first_fwd": [c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_int, c_int,
-                          c_int, c_void_p, c_void_p],
+                          c_int, c_void_p, c_void_p, c_void_p],
     "po_conv_first_dgrad": [c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_int, c_int, c_void_p,
                             c_void_p, c_void_p],
     "po_slice_accum": [c_void_p, c_int, c_int, c_void_p, c_int, c_int, c_int64, c_int, c_int,
-                       c_void_p, c_int, c_void_p],
+                       c_void_p, c_int, c_void_p, c_void_p],
     "po_view_move": [c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_int, c_int, c_int, c_int,
-                     c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_int, c_void_p],
-    "po_upsample2_fwd": [c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p, c_int, c_int, c_void_p],
+                     c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_int, c_void_p, c_void_p],
+    "po_upsample2_fwd": [c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p, c_int, c_int, c_void_p,
+                         c_void_p],
     "po_upsample2_bwd": [c_void_p, c_int, c_int, c_int, c_int, c_int, c_int, c_void_p, c_int, c_int,
-                         c_void_p, c_int, c_void_p],
+                         c_void_p, c_int, c_void_p, c_void_p],
     "po_maxpool2_fwd": [c_void_p, c_int, c_int, c_int, c_int, c_int, c_int, c_void_p, c_void_p,
-                        c_void_p],
-    "po_maxpool2_bwd": [c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_int, c_void_p, c_int,
                         c_void_p, c_void_p],
+    "po_maxpool2_bwd": [c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_int, c_void_p, c_int,
+                        c_void_p, c_void_p, c_void_p],
     "po_nhwc_to_nchw": [c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p, c_void_p],
     "po_nchw_to_nhwc": [c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p, c_void_p],
 }

@@ -56,6 +56,34 @@ __device__ __forceinline__ int head_cell(float cx, float cy, int S, int hw, bool
   return index;
 }
 
+// Per-tensor max|x| slots of the split-precision (fp16x3) convolutions.  A
+// slot is PO_AMAX_SUB uint32 sub-slots holding float bits (non-negative floats
+// order like their bit patterns, so atomicMax on the bits is a float max); the
+// bound of the tensor is the max over the sub-slots.  Writers spread over the
+// sub-slots by workgroup and skip the atomic when the sub-slot already holds a
+// larger value (a stale read only costs an extra atomic), so thousands of
+// workgroups do not serialise on one address.  Every lane of the wave must
+// call amax_commit (v >= 0).
+__device__ __forceinline__ uint32_t wave_max_u32(uint32_t u) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) u = max(u, (uint32_t)__shfl_xor((int)u, o));
+  return u;
+}
+
+__device__ __forceinline__ void amax_commit(uint32_t* slot, float v) {
+  const uint32_t u = wave_max_u32(__float_as_uint(v));
+  if ((threadIdx.x & 63) == 0 && u) {
+    uint32_t* s = slot + ((blockIdx.x + blockIdx.y * 7 + (threadIdx.x >> 6) * 13) & (PO_AMAX_SUB - 1));
+    if (u > __atomic_load_n(s, __ATOMIC_RELAXED)) atomicMax(s, u);
+  }
+}
+
+// max over the sub-slots (one load per lane), uniform across the wave
+__device__ __forceinline__ uint32_t amax_read(const uint32_t* slot) {
+  const uint32_t u = wave_max_u32(slot[threadIdx.x & (PO_AMAX_SUB - 1)]);
+  return (uint32_t)__builtin_amdgcn_readfirstlane(u);
+}
+
 }  // namespace po
 
 #define PO_REQUIRE(cond, ...)          \

@@ -1,0 +1,166 @@
+// Pieces shared by the two implicit-GEMM convolution kernels of po_conv:
+//   conv_k    (conv_igemm.hip) exact fp32 operands on v_mfma_f32_32x32x2_f32;
+//   conv_h3_k (conv_h3.hip)    fp32 operands split into two fp16 pieces under a
+//                              per-tensor power-of-two scale, three
+//                              v_mfma_f32_32x32x16_f16 products, fp32 accumulate.
+// Both accumulate 32x32 tiles with the same C/D register layout
+// (row = (e&3) + 8*(e>>2) + 4*(lane>>5), col = lane&31), so the epilogue, the
+// split-K partial store and the split-K reduction are common.
+#pragma once
+#include "common.h"
+
+typedef float floatx16 __attribute__((ext_vector_type(16)));
+
+namespace po {
+
+struct ConvArgs {
+  const float* in;
+  const void* W;                // fp32 [N][ntaps][Cin_p]  or  fp16 [2][N][ntaps][Cin_p] (prec 1)
+  const float* bias;
+  float* y;
+  const float* res;
+  float* sum;
+  const float* mask;
+  float* y2;
+  const float* mask2;
+  const int32_t* in_org;        // window origins [B,2] (NULL: full map)
+  const int32_t* out_org;
+  float* ws;                    // split-K partials [ksplit][M][N] (ksplit > 1)
+  const uint32_t* in_amax;      // prec 1: max|in| slot (float bits)
+  uint32_t* y_amax;             // optional max|output| slots
+  uint32_t* sum_amax;
+  uint32_t* y2_amax;
+  int prec, w_shift;            // prec 1: weights pre-scaled by 2^w_shift
+  int ksplit;
+  int B, Hin, Win, Cin_p, Hout, Wout, Cout_p, Hg, Wg;
+  int in_step, out_step, out_oy, out_ox;
+  int ntaps, N, act, accumulate;
+  int M, ntiles_n;
+  uint32_t in_bytes, w_bytes;   // buffer-resource extents (< 2^31)
+  // taps form a rectangular grid: tap t = th*tkw + tw -> (dh0 + th*sdh, dw0 + tw*sdw)
+  int tkw, dh0, dw0, sdh, sdw;
+};
+
+// Input scale exponent of a prec-1 launch: the input is multiplied by 2^e
+// (exact) so that its largest magnitude lies in [2^13, 2^14) — inside fp16's
+// range with 2 binades of headroom, while the low piece of every element that
+// matters stays far above fp16's subnormal floor.
+__device__ __forceinline__ int input_shift(const ConvArgs& a) {
+  if (a.prec != 1) return 0;
+  const uint32_t bits = amax_read(a.in_amax);
+  const int e = (int)((bits >> 23) & 0xff) - 127;      // amax in [2^e, 2^(e+1)) (normal)
+  return min(max(13 - e, -120), 120);
+}
+
+// XCD-aware bijective remap: consecutive logical tiles share an XCD's L2
+__device__ __forceinline__ int xcd_remap() {
+  const int nwg = gridDim.x, orig = blockIdx.x;
+  const int q = nwg / 8, r8 = nwg % 8, xcd = orig % 8;
+  return (xcd < r8 ? xcd * (q + 1) : r8 * (q + 1) + (xcd - r8) * q) + orig / 8;
+}
+
+// Raw partial sums of one split-K slice (the reduction applies the epilogue)
+template <int TM, int TN>
+__device__ __forceinline__ void store_partials(const ConvArgs& a, const floatx16 (&acc)[TM][TN], int m0, int n0,
+                                               int wm, int wn, int lane) {
+  float* ws = a.ws + (size_t)blockIdx.y * a.M * a.N;
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      const int n = n0 + wn * TN * 32 + j * 32 + (lane & 31);
+      if (n >= a.N) continue;
+#pragma unroll
+      for (int e = 0; e < 16; ++e) {
+        const int m = m0 + wm * TM * 32 + i * 32 + (e & 3) + 8 * (e >> 2) + 4 * (lane >> 5);
+        if (m < a.M) ws[(size_t)m * a.N + n] = acc[i][j][e];
+      }
+    }
+}
+
+// Epilogue.  Each wave stages one 32x32 accumulator tile at a time through a
+// private 4 KB slot of `smem` (the k-loop buffers are free by now), then every
+// lane handles 4 consecutive channels of a row: 16-byte loads of
+// bias/mask/res and 16-byte stores of y/sum/y2, 128 contiguous bytes per row.
+// v = acc * 2^-sh + bias (sh = 0 for fp32 operands; ldexp is exact).
+template <int BM, int TM, int TN>
+__device__ __forceinline__ void conv_epilogue(const ConvArgs& a, const floatx16 (&acc)[TM][TN], float* smem,
+                                              int* dst_pix, int m0, int n0, int wm, int wn, int sh) {
+  const int tid = threadIdx.x & 255, lane = tid & 63, wave = tid >> 6;
+  const int HgWg = a.Hg * a.Wg;
+  if (tid < BM) {
+    const int m = m0 + tid;
+    int o = -1;
+    if (m < a.M) {
+      const int b = m / HgWg, rem = m - b * HgWg;
+      const int i = rem / a.Wg, j = rem - i * a.Wg;
+      o = (b * a.Hout + i * a.out_step + a.out_oy) * a.Wout + j * a.out_step + a.out_ox;
+    }
+    dst_pix[tid] = o;
+  }
+  __syncthreads();
+  float* scr = smem + wave * 1024;
+  const int rr = lane >> 3, cc = (lane & 7) * 4;
+  float my = 0.f, ms = 0.f, my2 = 0.f;
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+#pragma unroll
+      for (int e = 0; e < 16; ++e)
+        scr[((e & 3) + 8 * (e >> 2) + 4 * (lane >> 5)) * 32 + (lane & 31)] = acc[i][j][e];
+      __builtin_amdgcn_wave_barrier();
+      const int n = n0 + wn * TN * 32 + j * 32 + cc;
+      float4 bv = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (a.bias && n < a.N) bv = *reinterpret_cast<const float4*>(a.bias + n);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int row = rr + 8 * q;
+        const float4 v = *reinterpret_cast<const float4*>(scr + row * 32 + cc);
+        const int pix = dst_pix[wm * TM * 32 + i * 32 + row];
+        if (pix < 0 || n >= a.N) continue;
+        const size_t o = (size_t)pix * a.Cout_p + n;
+        float x[4] = {__builtin_ldexpf(v.x, -sh) + bv.x, __builtin_ldexpf(v.y, -sh) + bv.y,
+                      __builtin_ldexpf(v.z, -sh) + bv.z, __builtin_ldexpf(v.w, -sh) + bv.w};
+        if (a.act) {
+#pragma unroll
+          for (int c = 0; c < 4; ++c) x[c] = leaky(x[c]);
+        }
+        if (a.accumulate) {
+          const float4 p = *reinterpret_cast<const float4*>(a.y + o);
+          x[0] += p.x; x[1] += p.y; x[2] += p.z; x[3] += p.w;
+        }
+        float4 out = make_float4(x[0], x[1], x[2], x[3]);
+        if (a.mask) {
+          const float4 mk = *reinterpret_cast<const float4*>(a.mask + o);
+          out = make_float4(x[0] * leaky_grad(mk.x), x[1] * leaky_grad(mk.y), x[2] * leaky_grad(mk.z),
+                            x[3] * leaky_grad(mk.w));
+        }
+        *reinterpret_cast<float4*>(a.y + o) = out;
+        my = fmaxf(my, fmaxf(fmaxf(fabsf(out.x), fabsf(out.y)), fmaxf(fabsf(out.z), fabsf(out.w))));
+        if (a.res) {
+          const float4 r = *reinterpret_cast<const float4*>(a.res + o);
+          const float4 sm = make_float4(x[0] + r.x, x[1] + r.y, x[2] + r.z, x[3] + r.w);
+          *reinterpret_cast<float4*>(a.sum + o) = sm;
+          ms = fmaxf(ms, fmaxf(fmaxf(fabsf(sm.x), fabsf(sm.y)), fmaxf(fabsf(sm.z), fabsf(sm.w))));
+        }
+        if (a.y2) {
+          const float4 mk = *reinterpret_cast<const float4*>(a.mask2 + o);
+          const float4 o2 = make_float4(x[0] * leaky_grad(mk.x), x[1] * leaky_grad(mk.y),
+                                        x[2] * leaky_grad(mk.z), x[3] * leaky_grad(mk.w));
+          *reinterpret_cast<float4*>(a.y2 + o) = o2;
+          my2 = fmaxf(my2, fmaxf(fmaxf(fabsf(o2.x), fabsf(o2.y)), fmaxf(fabsf(o2.z), fabsf(o2.w))));
+        }
+      }
+      __builtin_amdgcn_wave_barrier();
+    }
+  if (a.y_amax) amax_commit(a.y_amax, my);
+  if (a.sum_amax) amax_commit(a.sum_amax, ms);
+  if (a.y2_amax) amax_commit(a.y2_amax, my2);
+}
+
+// conv_h3.hip: launch of the split-precision kernel for tile (bm, bn, bk)
+// (the split-K reduction, when a.ksplit > 1, is launched by the caller)
+int launch_h3(const ConvArgs& a, hipStream_t st, int bm, int bn, int bk);
+
+}  // namespace po

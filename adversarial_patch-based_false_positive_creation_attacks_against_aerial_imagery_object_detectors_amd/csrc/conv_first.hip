@@ -12,14 +12,16 @@ __global__ __launch_bounds__(256) void first_fwd_k(const float* __restrict__ img
                                                    int stride, int Ho, int Wo,
                                                    const float* __restrict__ Wt,
                                                    const float* __restrict__ bias, int Cout,
-                                                   int Cout_p, int act, float* __restrict__ y) {
+                                                   int Cout_p, int act, float* __restrict__ y,
+                                                   uint32_t* __restrict__ amax) {
   __shared__ float ws[CO * 27];
   __shared__ float bs[CO];
   for (int t = threadIdx.x; t < CO * 27; t += 256) ws[t] = (t / 27) < Cout ? Wt[t] : 0.f;
   for (int t = threadIdx.x; t < CO; t += 256) bs[t] = (t < Cout && bias) ? bias[t] : 0.f;
   __syncthreads();
-  const int64_t p = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  if (p >= (int64_t)B * Ho * Wo) return;
+  const int64_t p0 = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const bool live = p0 < (int64_t)B * Ho * Wo;
+  const int64_t p = live ? p0 : 0;
   const int b = (int)(p / ((int64_t)Ho * Wo));
   const int rem = (int)(p - (int64_t)b * Ho * Wo);
   const int i = rem / Wo, j = rem % Wo;
@@ -35,6 +37,7 @@ __global__ __launch_bounds__(256) void first_fwd_k(const float* __restrict__ img
                                      ? img[(((size_t)b * 3 + c) * H + hi) * W + wi] : 0.f;
       }
   float* yp = y + (size_t)p * Cout_p;
+  float vmax = 0.f;
 #pragma unroll
   for (int co4 = 0; co4 < CO; co4 += 4) {
     float v[4];
@@ -45,9 +48,11 @@ __global__ __launch_bounds__(256) void first_fwd_k(const float* __restrict__ img
       for (int k = 0; k < 27; ++k) s += ws[(co4 + u) * 27 + k] * x[k];
       s += bs[co4 + u];
       v[u] = act ? po::leaky(s) : s;
+      vmax = fmaxf(vmax, fabsf(v[u]));
     }
-    *reinterpret_cast<float4*>(yp + co4) = make_float4(v[0], v[1], v[2], v[3]);
+    if (live) *reinterpret_cast<float4*>(yp + co4) = make_float4(v[0], v[1], v[2], v[3]);
   }
+  if (amax) po::amax_commit(amax, live ? vmax : 0.f);
 }
 
 template <int CO>
@@ -121,7 +126,7 @@ __global__ __launch_bounds__(256) void first_dgrad_k(const float* __restrict__ D
 
 extern "C" int po_conv_first_fwd(const float* img, int B, int H, int W, int stride, const float* Wt,
                                  const float* bias, int Cout, int Cout_p, int act, float* y,
-                                 po_stream_t s) {
+                                 uint32_t* amax, po_stream_t s) {
   PO_REQUIRE(img && Wt && y, "po_conv_first_fwd: null pointer");
   PO_REQUIRE(stride == 1 || stride == 2, "po_conv_first_fwd: stride %d", stride);
   PO_REQUIRE(Cout > 0 && Cout <= 64 && Cout_p % 4 == 0 && Cout_p >= Cout, "po_conv_first_fwd: Cout=%d Cout_p=%d", Cout, Cout_p);
@@ -132,11 +137,11 @@ extern "C" int po_conv_first_fwd(const float* img, int B, int H, int W, int stri
   const int CO = Cout_p <= 16 ? 16 : (Cout_p <= 32 ? 32 : 64);
   PO_REQUIRE(Cout_p == CO, "po_conv_first_fwd: Cout_p must be 16, 32 or 64 (got %d)", Cout_p);
   if (CO == 16)
-    hipLaunchKernelGGL(first_fwd_k<16>, grid, dim3(256), 0, st, img, B, H, W, stride, Ho, Wo, Wt, bias, Cout, Cout_p, act, y);
+    hipLaunchKernelGGL(first_fwd_k<16>, grid, dim3(256), 0, st, img, B, H, W, stride, Ho, Wo, Wt, bias, Cout, Cout_p, act, y, amax);
   else if (CO == 32)
-    hipLaunchKernelGGL(first_fwd_k<32>, grid, dim3(256), 0, st, img, B, H, W, stride, Ho, Wo, Wt, bias, Cout, Cout_p, act, y);
+    hipLaunchKernelGGL(first_fwd_k<32>, grid, dim3(256), 0, st, img, B, H, W, stride, Ho, Wo, Wt, bias, Cout, Cout_p, act, y, amax);
   else
-    hipLaunchKernelGGL(first_fwd_k<64>, grid, dim3(256), 0, st, img, B, H, W, stride, Ho, Wo, Wt, bias, Cout, Cout_p, act, y);
+    hipLaunchKernelGGL(first_fwd_k<64>, grid, dim3(256), 0, st, img, B, H, W, stride, Ho, Wo, Wt, bias, Cout, Cout_p, act, y, amax);
   return po::check_launch("po_conv_first_fwd");
 }
 

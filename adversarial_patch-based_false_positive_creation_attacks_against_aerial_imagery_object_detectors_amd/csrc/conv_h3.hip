@@ -1,0 +1,268 @@
+// Split-precision ("fp16x3") implicit-GEMM convolution on gfx950 fp16 matrix cores.
+//
+// Same GEMM as conv_k (conv_igemm.hip): D[m][n] = sum_k A[m][k] * W[n][k] with
+// m = output pixel, n = output channel, k = (tap, input channel).  Each fp32
+// operand x is represented, after an exact power-of-two scale s that puts the
+// tensor's max|x| in [2^13, 2^14), as x*s = hi + lo with
+//   hi = fp16_rne(x*s),  lo = fp16_rne(x*s - hi)        (x*s - hi is exact in fp32)
+// so x*s is kept to ~22 significant bits (|x*s - hi - lo| <= 2^-22 |x*s|), and
+//   A.W ~ Ahi.Whi + Ahi.Wlo + Alo.Whi                   (the dropped Alo.Wlo ~ 2^-22)
+// on v_mfma_f32_32x32x16_f16 (fp16 products are exact in fp32; fp32 accumulate).
+// Three 32x32x16 MFMAs (3 x 32 cycles) replace eight exact-fp32 32x32x2 MFMAs
+// (8 x 64 cycles) per 32x32x16 block: 5.3x the fp32 matrix rate.  The result
+// is scaled back by 2^-(shift_in + shift_w) (ldexp, exact) in the epilogue.
+//
+// Operands: the activations/gradients stay fp32 in HBM; each k-step's A tile
+// is loaded through registers, scaled and split into two fp16 LDS images (hi,
+// lo).  The weights are split once on the host into fp16 hi/lo planes
+// ([2][N][ntaps][Cin_p], pre-scaled by 2^w_shift) and staged as they are.
+// The input scale comes from the max|in| slot that the kernels producing the
+// input atomicMax'd (po_conv_desc.in_amax).
+//
+// LDS rows are BK halfs (BK/8 16-byte chunks) with chunks XOR-swizzled by
+// (row / rows-per-256B-line), which makes the ds_write_b128 staging and the
+// ds_read_b128 fragment reads (lane l: row l&31, chunk 2g + (l>>5)) conflict-free.
+#include "conv_common.h"
+
+namespace {
+using po::ConvArgs;
+typedef _Float16 half8 __attribute__((ext_vector_type(8)));
+typedef _Float16 half2_t __attribute__((ext_vector_type(2)));
+
+__device__ __forceinline__ uint32_t pk_f16(float a, float b) {
+  half2_t h;
+  h[0] = (_Float16)a;
+  h[1] = (_Float16)b;
+  return __builtin_bit_cast(uint32_t, h);
+}
+
+// 8 fp32 values (scaled by 2^sh) -> hi and lo fp16 chunks
+__device__ __forceinline__ void split8(const float4 u, const float4 v, int sh, uint4& hi, uint4& lo) {
+  float x[8] = {u.x, u.y, u.z, u.w, v.x, v.y, v.z, v.w};
+#pragma unroll
+  for (int i = 0; i < 8; ++i) x[i] = __builtin_ldexpf(x[i], sh);
+  uint32_t h[4], l[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    h[i] = pk_f16(x[2 * i], x[2 * i + 1]);
+    const half2_t hh = __builtin_bit_cast(half2_t, h[i]);
+    l[i] = pk_f16(x[2 * i] - (float)hh[0], x[2 * i + 1] - (float)hh[1]);
+  }
+  hi = make_uint4(h[0], h[1], h[2], h[3]);
+  lo = make_uint4(l[0], l[1], l[2], l[3]);
+}
+
+template <int BM, int BN, int WM, int BK>
+__global__ __launch_bounds__(256) void conv_h3_k(const ConvArgs a) {
+  constexpr int WN = 4 / WM;
+  constexpr int TM = BM / WM / 32;
+  constexpr int TN = BN / WN / 32;
+  static_assert(TM >= 1 && TN >= 1, "tile too small for 4 waves of 32x32");
+  static_assert(BK == 16 || BK == 32 || BK == 64, "BK");
+  constexpr int CPR = BK / 8;                  // 16-byte chunks (8 halfs) per LDS row
+  constexpr int RPP = 256 / CPR;               // rows per staging pass of the workgroup
+  constexpr int AL = (BM + RPP - 1) / RPP;     // A passes per k-step
+  constexpr int BL = (BN + RPP - 1) / RPP;
+  constexpr int SW = (BK == 16) ? 3 : (BK == 32 ? 2 : 1);   // log2(rows per 256-byte bank line)
+  // LDS: [2 buffers][hi, lo][BM rows][BK halfs] for A, then the same for B
+  constexpr int A_HALFS = BM * BK, B_HALFS = BN * BK;
+  __shared__ __attribute__((aligned(16))) _Float16 smem_h[2 * 2 * (A_HALFS + B_HALFS)];
+  static_assert(sizeof(smem_h) >= 4 * 4096, "the epilogue needs 16 KB of LDS");
+  _Float16* As = smem_h;                       // [2][2][BM][BK]
+  _Float16* Bs = smem_h + 4 * A_HALFS;         // [2][2][BN][BK]
+
+  const int wgid = po::xcd_remap();
+  const int tn = wgid % a.ntiles_n, tm = wgid / a.ntiles_n;
+  const int m0 = tm * BM, n0 = tn * BN;
+  const int tid = threadIdx.x & 255, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave / WN, wn = wave % WN;
+  const int HgWg = a.Hg * a.Wg;
+  const int cth = tid % CPR, rth = tid / CPR;
+  const int sh_in = po::input_shift(a);
+
+  const uint32_t in_bytes = (uint32_t)__builtin_amdgcn_readfirstlane(a.in_bytes);
+  const uint32_t w_bytes = (uint32_t)__builtin_amdgcn_readfirstlane(a.w_bytes);
+  const __amdgpu_buffer_rsrc_t in_rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(a.in), 0, in_bytes, 0x00020000);
+  const __amdgpu_buffer_rsrc_t w_rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(a.W), 0, 2 * w_bytes, 0x00020000);
+  constexpr uint32_t kOOB = 0x80000000u;
+  const uint32_t pix_bytes = (uint32_t)a.Cin_p * 4u;     // fp32 input pixel
+  const uint32_t wpix_bytes = (uint32_t)a.Cin_p * 2u;    // fp16 weight row per tap
+
+  // ---- A loader: thread (rth, cth) loads channels [8 cth, 8 cth + 8) of rows rth + RPP*r
+  int a_hi[AL], a_wi[AL];
+  uint32_t a_off[AL];
+#pragma unroll
+  for (int r = 0; r < AL; ++r) {
+    const int row = rth + RPP * r;
+    const int m = m0 + row;
+    const bool ok = (row < BM) && (m < a.M);
+    const int mm = ok ? m : 0;
+    const int b = mm / HgWg, rem = mm - b * HgWg;
+    const int i = rem / a.Wg, j = rem - i * a.Wg;
+    a_off[r] = ((uint32_t)b * a.Hin * a.Win) * pix_bytes + cth * 32u;
+    int sy = 0, sx = 0;
+    if (a.out_org) { sy += a.out_org[2 * b]; sx += a.out_org[2 * b + 1]; }
+    if (a.in_org) { sy -= a.in_org[2 * b]; sx -= a.in_org[2 * b + 1]; }
+    a_hi[r] = ok ? i * a.in_step + sy : -(1 << 20);
+    a_wi[r] = j * a.in_step + sx;
+  }
+  // ---- B loader: same thread grid over weight rows; hi plane, lo plane at +w_bytes
+  const uint32_t wrow_bytes = (uint32_t)a.ntaps * wpix_bytes;
+  uint32_t b_off[BL];
+#pragma unroll
+  for (int r = 0; r < BL; ++r) {
+    const int row = rth + RPP * r;
+    const bool ok = (row < BN) && (n0 + row < a.N);
+    b_off[r] = ok ? (uint32_t)(n0 + row) * wrow_bytes + cth * 16u : kOOB;
+  }
+
+  float4 ra[AL][2];
+  uint4 rbh[BL], rbl[BL];
+  auto gload = [&](int tap, int dh, int dw, int c0) {
+#pragma unroll
+    for (int r = 0; r < AL; ++r) {
+      const int hi = a_hi[r] + dh, wi = a_wi[r] + dw;
+      const bool ok = (unsigned)hi < (unsigned)a.Hin && (unsigned)wi < (unsigned)a.Win;
+      const uint32_t o = ok ? a_off[r] + ((uint32_t)hi * a.Win + wi) * pix_bytes + (uint32_t)c0 * 4u : kOOB;
+      ra[r][0] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(in_rs, o, 0, 0));
+      ra[r][1] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(in_rs, o + 16u, 0, 0));
+    }
+    const uint32_t tb = (uint32_t)tap * wpix_bytes + (uint32_t)c0 * 2u;
+#pragma unroll
+    for (int r = 0; r < BL; ++r) {
+      rbh[r] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(w_rs, b_off[r] + tb, 0, 0));
+      rbl[r] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(w_rs, b_off[r] + tb + w_bytes, 0, 0));
+    }
+  };
+  auto swz = [](int row, int chunk) { return (chunk ^ ((row >> SW) & (CPR - 1))) * 8; };
+  auto sstore = [&](int buf) {
+#pragma unroll
+    for (int r = 0; r < AL; ++r) {
+      const int row = rth + RPP * r;
+      if (row < BM) {
+        uint4 h, l;
+        split8(ra[r][0], ra[r][1], sh_in, h, l);
+        _Float16* base = As + (buf * 2) * A_HALFS + row * BK + swz(row, cth);
+        *reinterpret_cast<uint4*>(base) = h;
+        *reinterpret_cast<uint4*>(base + A_HALFS) = l;
+      }
+    }
+#pragma unroll
+    for (int r = 0; r < BL; ++r) {
+      const int row = rth + RPP * r;
+      if (row < BN) {
+        _Float16* base = Bs + (buf * 2) * B_HALFS + row * BK + swz(row, cth);
+        *reinterpret_cast<uint4*>(base) = rbh[r];
+        *reinterpret_cast<uint4*>(base + B_HALFS) = rbl[r];
+      }
+    }
+  };
+
+  floatx16 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.f;
+
+  const int kc = a.Cin_p / BK;
+  const int nks_all = a.ntaps * kc;
+  const int split = blockIdx.y;
+  const int ks0 = (int)((int64_t)split * nks_all / a.ksplit);
+  const int nks = (int)((int64_t)(split + 1) * nks_all / a.ksplit) - ks0;
+  int tap = ks0 / kc, c0 = (ks0 - tap * kc) * BK;
+  int th = tap / a.tkw, tw = tap - th * a.tkw;
+  gload(tap, a.dh0 + th * a.sdh, a.dw0 + tw * a.sdw, c0);
+  sstore(0);
+  __syncthreads();
+  const int arow = wm * TM * 32 + (lane & 31);
+  const int brow = wn * TN * 32 + (lane & 31);
+  const int h = lane >> 5;
+  for (int ks = 0; ks < nks; ++ks) {
+    const int buf = ks & 1;
+    const bool more = ks + 1 < nks;
+    const _Float16* Ab = As + buf * 2 * A_HALFS;
+    const _Float16* Bb = Bs + buf * 2 * B_HALFS;
+#pragma unroll
+    for (int g = 0; g < BK / 16; ++g) {
+      half8 ah[TM], al[TM], bh[TN], bl[TN];
+#pragma unroll
+      for (int i = 0; i < TM; ++i) {
+        const int row = arow + i * 32;
+        const int o = row * BK + swz(row, 2 * g + h);
+        ah[i] = *reinterpret_cast<const half8*>(Ab + o);
+        al[i] = *reinterpret_cast<const half8*>(Ab + A_HALFS + o);
+      }
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        const int row = brow + j * 32;
+        const int o = row * BK + swz(row, 2 * g + h);
+        bh[j] = *reinterpret_cast<const half8*>(Bb + o);
+        bl[j] = *reinterpret_cast<const half8*>(Bb + B_HALFS + o);
+      }
+      if (g == 0 && more) {
+        c0 += BK;
+        if (c0 == a.Cin_p) {
+          c0 = 0;
+          ++tap;
+          if (++tw == a.tkw) { tw = 0; ++th; }
+        }
+        gload(tap, a.dh0 + th * a.sdh, a.dw0 + tw * a.sdw, c0);
+      }
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) {
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(al[i], bh[j], acc[i][j], 0, 0, 0);
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[i], bl[j], acc[i][j], 0, 0, 0);
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[i], bh[j], acc[i][j], 0, 0, 0);
+        }
+    }
+    if (more) sstore(buf ^ 1);
+    __syncthreads();
+  }
+
+  if (a.ksplit > 1) {
+    po::store_partials<TM, TN>(a, acc, m0, n0, wm, wn, lane);
+    return;
+  }
+  __shared__ int dst_pix[BM];
+  po::conv_epilogue<BM, TM, TN>(a, acc, reinterpret_cast<float*>(smem_h), dst_pix, m0, n0, wm, wn,
+                                sh_in + a.w_shift);
+}
+
+template <int BM, int BN, int WM, int BK>
+int launch(const ConvArgs& a, hipStream_t st) {
+  ConvArgs b = a;
+  b.ntiles_n = po::ceil_div(a.N, BN);
+  const int ntiles = po::ceil_div(a.M, BM) * b.ntiles_n;
+  hipLaunchKernelGGL((conv_h3_k<BM, BN, WM, BK>), dim3(ntiles, a.ksplit), dim3(256), 0, st, b);
+  return po::check_launch("po_conv (fp16x3)");
+}
+
+template <int BK>
+int dispatch(const ConvArgs& a, hipStream_t st, int bm, int bn) {
+  if (bm == 128 && bn == 128) return launch<128, 128, 2, BK>(a, st);
+  if (bm == 64 && bn == 128) return launch<64, 128, 1, BK>(a, st);
+  if (bm == 128 && bn == 64) return launch<128, 64, 4, BK>(a, st);
+  if (bm == 64 && bn == 64) return launch<64, 64, 2, BK>(a, st);
+  if (bm == 128 && bn == 32) return launch<128, 32, 4, BK>(a, st);
+  if constexpr (BK <= 32) {
+    if (bm == 256 && bn == 128) return launch<256, 128, 2, BK>(a, st);
+    if (bm == 128 && bn == 256) return launch<128, 256, 2, BK>(a, st);
+  }
+  po::set_error("po_conv (fp16x3): no %dx%dx%d tile", bm, bn, BK);
+  return PO_EINVAL;
+}
+}  // namespace
+
+namespace po {
+int launch_h3(const ConvArgs& a, hipStream_t st, int bm, int bn, int bk) {
+  if (bk == 16) return dispatch<16>(a, st, bm, bn);
+  if (bk == 32) return dispatch<32>(a, st, bm, bn);
+  if (bk == 64) return dispatch<64>(a, st, bm, bn);
+  set_error("po_conv (fp16x3): no k-step %d", bk);
+  return PO_EINVAL;
+}
+}  // namespace po

@@ -16,35 +16,12 @@
 // makes both the ds_write_b128 staging and the ds_read_b128 fragment reads
 // bank-conflict free; each lane reads one 16-byte chunk per 4 MFMAs (the k
 // order inside a group of 8 is permuted identically for A and B).
-#include "common.h"
+#include "conv_common.h"
 #include <stdlib.h>
 #include <string.h>
 
-typedef float floatx16 __attribute__((ext_vector_type(16)));
-
 namespace {
-struct ConvArgs {
-  const float* in;
-  const float* W;
-  const float* bias;
-  float* y;
-  const float* res;
-  float* sum;
-  const float* mask;
-  float* y2;
-  const float* mask2;
-  const int32_t* in_org;        // window origins [B,2] (NULL: full map)
-  const int32_t* out_org;
-  float* ws;                    // split-K partials [ksplit][M][N] (ksplit > 1)
-  int ksplit;
-  int B, Hin, Win, Cin_p, Hout, Wout, Cout_p, Hg, Wg;
-  int in_step, out_step, out_oy, out_ox;
-  int ntaps, N, act, accumulate;
-  int M, ntiles_n;
-  uint32_t in_bytes, w_bytes;   // buffer-resource extents (< 2^31)
-  // taps form a rectangular grid: tap t = th*tkw + tw -> (dh0 + th*sdh, dw0 + tw*sdw)
-  int tkw, dh0, dw0, sdh, sdw;
-};
+using po::ConvArgs;
 
 // 16-byte LDS-DMA: lane l's 16 bytes from rsrc+voff land at lds + 16*l
 __device__ __forceinline__ void lds_dma16(__amdgpu_buffer_rsrc_t rs, float* lds, uint32_t voff) {
@@ -66,10 +43,7 @@ __global__ __launch_bounds__(256) void conv_k(const ConvArgs a) {
   float* As = smem;                            // [2][BM][BK]
   float* Bs = smem + 2 * BM * BK;              // [2][BN][BK]
 
-  // XCD-aware bijective remap: consecutive logical tiles share an XCD's L2
-  const int nwg = gridDim.x, orig = blockIdx.x;
-  const int q = nwg / 8, r8 = nwg % 8, xcd = orig % 8;
-  const int wgid = (xcd < r8 ? xcd * (q + 1) : r8 * (q + 1) + (xcd - r8) * q) + orig / 8;
+  const int wgid = po::xcd_remap();
   const int tn = wgid % a.ntiles_n, tm = wgid / a.ntiles_n;
   const int m0 = tm * BM, n0 = tn * BN;
 
@@ -84,7 +58,7 @@ __global__ __launch_bounds__(256) void conv_k(const ConvArgs a) {
   const uint32_t in_bytes = (uint32_t)__builtin_amdgcn_readfirstlane(a.in_bytes);
   const uint32_t w_bytes = (uint32_t)__builtin_amdgcn_readfirstlane(a.w_bytes);
   const __amdgpu_buffer_rsrc_t in_rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(a.in), 0, in_bytes, 0x00020000);
-  const __amdgpu_buffer_rsrc_t w_rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(a.W), 0, w_bytes, 0x00020000);
+  const __amdgpu_buffer_rsrc_t w_rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(a.W), 0, w_bytes, 0x00020000);
   constexpr uint32_t kOOB = 0x80000000u;
   const uint32_t pix_bytes = (uint32_t)a.Cin_p * 4u;
 
@@ -258,116 +232,57 @@ __global__ __launch_bounds__(256) void conv_k(const ConvArgs a) {
   }
 
   if (a.ksplit > 1) {
-    // raw partial sums; conv_reduce_k applies the epilogue in split order
-    float* ws = a.ws + (size_t)split * a.M * a.N;
-#pragma unroll
-    for (int i = 0; i < TM; ++i)
-#pragma unroll
-      for (int j = 0; j < TN; ++j) {
-        const int n = n0 + wn * TN * 32 + j * 32 + (lane & 31);
-        if (n >= a.N) continue;
-#pragma unroll
-        for (int e = 0; e < 16; ++e) {
-          const int m = m0 + wm * TM * 32 + i * 32 + (e & 3) + 8 * (e >> 2) + 4 * (lane >> 5);
-          if (m < a.M) ws[(size_t)m * a.N + n] = acc[i][j][e];
-        }
-      }
+    po::store_partials<TM, TN>(a, acc, m0, n0, wm, wn, lane);
     return;
   }
-
-  // ---- epilogue.  Each wave stages one 32x32 accumulator tile at a time
-  // through a private 4 KB LDS slot (the k-loop buffers are free now), then
-  // every lane handles 4 consecutive channels of a row: 16-byte loads of
-  // bias/mask/res and 16-byte stores of y/sum/y2, 128 contiguous bytes per row.
   __shared__ int dst_pix[BM];
-  if (tid < BM) {
-    const int m = m0 + tid;
-    int o = -1;
-    if (m < a.M) {
-      const int b = m / HgWg, rem = m - b * HgWg;
-      const int i = rem / a.Wg, j = rem - i * a.Wg;
-      o = (b * a.Hout + i * a.out_step + a.out_oy) * a.Wout + j * a.out_step + a.out_ox;
-    }
-    dst_pix[tid] = o;
-  }
-  __syncthreads();
-  float* scr = smem + wave * 1024;
-  const int rr = lane >> 3, cc = (lane & 7) * 4;
-#pragma unroll
-  for (int i = 0; i < TM; ++i)
-#pragma unroll
-    for (int j = 0; j < TN; ++j) {
-#pragma unroll
-      for (int e = 0; e < 16; ++e)
-        scr[((e & 3) + 8 * (e >> 2) + 4 * (lane >> 5)) * 32 + (lane & 31)] = acc[i][j][e];
-      __builtin_amdgcn_wave_barrier();
-      const int n = n0 + wn * TN * 32 + j * 32 + cc;
-      float4 bv = make_float4(0.f, 0.f, 0.f, 0.f);
-      if (a.bias && n < a.N) bv = *reinterpret_cast<const float4*>(a.bias + n);
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const int row = rr + 8 * q;
-        const float4 v = *reinterpret_cast<const float4*>(scr + row * 32 + cc);
-        const int pix = dst_pix[wm * TM * 32 + i * 32 + row];
-        if (pix < 0 || n >= a.N) continue;
-        const size_t o = (size_t)pix * a.Cout_p + n;
-        float x[4] = {v.x + bv.x, v.y + bv.y, v.z + bv.z, v.w + bv.w};
-        if (a.act) {
-#pragma unroll
-          for (int c = 0; c < 4; ++c) x[c] = po::leaky(x[c]);
-        }
-        if (a.accumulate) {
-          const float4 p = *reinterpret_cast<const float4*>(a.y + o);
-          x[0] += p.x; x[1] += p.y; x[2] += p.z; x[3] += p.w;
-        }
-        float4 out = make_float4(x[0], x[1], x[2], x[3]);
-        if (a.mask) {
-          const float4 mk = *reinterpret_cast<const float4*>(a.mask + o);
-          out = make_float4(x[0] * po::leaky_grad(mk.x), x[1] * po::leaky_grad(mk.y),
-                            x[2] * po::leaky_grad(mk.z), x[3] * po::leaky_grad(mk.w));
-        }
-        *reinterpret_cast<float4*>(a.y + o) = out;
-        if (a.res) {
-          const float4 r = *reinterpret_cast<const float4*>(a.res + o);
-          *reinterpret_cast<float4*>(a.sum + o) = make_float4(x[0] + r.x, x[1] + r.y, x[2] + r.z, x[3] + r.w);
-        }
-        if (a.y2) {
-          const float4 mk = *reinterpret_cast<const float4*>(a.mask2 + o);
-          *reinterpret_cast<float4*>(a.y2 + o) =
-              make_float4(x[0] * po::leaky_grad(mk.x), x[1] * po::leaky_grad(mk.y), x[2] * po::leaky_grad(mk.z),
-                          x[3] * po::leaky_grad(mk.w));
-        }
-      }
-      __builtin_amdgcn_wave_barrier();
-    }
+  po::conv_epilogue<BM, TM, TN>(a, acc, smem, dst_pix, m0, n0, wm, wn, 0);
 }
 
 // Split-K reduction + epilogue: one thread per 4 output channels of a row.
 __global__ __launch_bounds__(256) void conv_reduce_k(const ConvArgs a) {
-  const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const int64_t t0 = (int64_t)blockIdx.x * 256 + threadIdx.x;
   const int n4 = a.N / 4;
-  if (t >= (int64_t)a.M * n4) return;
+  const bool live = t0 < (int64_t)a.M * n4;
+  const int64_t t = live ? t0 : 0;
+  const int sh = po::input_shift(a) + (a.prec == 1 ? a.w_shift : 0);
   const int m = (int)(t / n4), n = (int)(t - (int64_t)m * n4) * 4;
-  float4 v = *reinterpret_cast<const float4*>(a.ws + (size_t)m * a.N + n);
-  for (int s = 1; s < a.ksplit; ++s) {
-    const float4 p = *reinterpret_cast<const float4*>(a.ws + ((size_t)s * a.M + m) * a.N + n);
-    v.x += p.x; v.y += p.y; v.z += p.z; v.w += p.w;
-  }
-  const int HgWg = a.Hg * a.Wg;
-  const int b = m / HgWg, rem = m - b * HgWg;
-  const int i = rem / a.Wg, j = rem - i * a.Wg;
-  const size_t o = ((size_t)(b * a.Hout + i * a.out_step + a.out_oy) * a.Wout + j * a.out_step + a.out_ox) *
-                       a.Cout_p + n;
-  float r[4] = {v.x, v.y, v.z, v.w};
+  float my = 0.f, ms = 0.f, my2 = 0.f;
+  if (live) {
+    float4 v = *reinterpret_cast<const float4*>(a.ws + (size_t)m * a.N + n);
+    for (int s = 1; s < a.ksplit; ++s) {
+      const float4 p = *reinterpret_cast<const float4*>(a.ws + ((size_t)s * a.M + m) * a.N + n);
+      v.x += p.x; v.y += p.y; v.z += p.z; v.w += p.w;
+    }
+    const int HgWg = a.Hg * a.Wg;
+    const int b = m / HgWg, rem = m - b * HgWg;
+    const int i = rem / a.Wg, j = rem - i * a.Wg;
+    const size_t o = ((size_t)(b * a.Hout + i * a.out_step + a.out_oy) * a.Wout + j * a.out_step + a.out_ox) *
+                         a.Cout_p + n;
+    float r[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
-  for (int c = 0; c < 4; ++c) {
-    float x = r[c] + (a.bias ? a.bias[n + c] : 0.f);
-    if (a.act) x = po::leaky(x);
-    if (a.accumulate) x += a.y[o + c];
-    a.y[o + c] = a.mask ? x * po::leaky_grad(a.mask[o + c]) : x;
-    if (a.res) a.sum[o + c] = x + a.res[o + c];
-    if (a.y2) a.y2[o + c] = x * po::leaky_grad(a.mask2[o + c]);
+    for (int c = 0; c < 4; ++c) {
+      float x = __builtin_ldexpf(r[c], -sh) + (a.bias ? a.bias[n + c] : 0.f);
+      if (a.act) x = po::leaky(x);
+      if (a.accumulate) x += a.y[o + c];
+      const float yv = a.mask ? x * po::leaky_grad(a.mask[o + c]) : x;
+      a.y[o + c] = yv;
+      my = fmaxf(my, fabsf(yv));
+      if (a.res) {
+        const float sv = x + a.res[o + c];
+        a.sum[o + c] = sv;
+        ms = fmaxf(ms, fabsf(sv));
+      }
+      if (a.y2) {
+        const float v2 = x * po::leaky_grad(a.mask2[o + c]);
+        a.y2[o + c] = v2;
+        my2 = fmaxf(my2, fabsf(v2));
+      }
+    }
   }
+  if (a.y_amax) po::amax_commit(a.y_amax, my);
+  if (a.sum_amax) po::amax_commit(a.sum_amax, ms);
+  if (a.y2_amax) po::amax_commit(a.y2_amax, my2);
 }
 
 template <int BM, int BN, int WM, int BK, bool GL>
@@ -407,23 +322,30 @@ bool forced_tile(int& bm, int& bn, int& bk, int& gl) {
   return true;
 }
 
-// tiles 1..10 stage through registers + ds_write; 11..20 are the same
-// shapes staged by LDS-DMA (buffer_load ... lds); 21..28 are the 8-accumulator
-// (64x128 / 128x64 per wave) shapes, register- then DMA-staged
-constexpr int kTiles[PO_CONV_NTILES][4] = {
-    {128, 128, 16, 0}, {128, 128, 32, 0}, {64, 128, 16, 0}, {64, 128, 32, 0}, {128, 64, 16, 0},
-    {128, 64, 32, 0},  {64, 64, 16, 0},   {64, 64, 32, 0},  {128, 32, 16, 0}, {128, 32, 32, 0},
-    {128, 128, 16, 1}, {128, 128, 32, 1}, {64, 128, 16, 1}, {64, 128, 32, 1}, {128, 64, 16, 1},
-    {128, 64, 32, 1},  {64, 64, 16, 1},   {64, 64, 32, 1},  {128, 32, 16, 1}, {128, 32, 32, 1},
-    {256, 128, 16, 0}, {256, 128, 32, 0}, {128, 256, 16, 0}, {128, 256, 32, 0},
-    {256, 128, 16, 1}, {256, 128, 32, 1}, {128, 256, 16, 1}, {128, 256, 32, 1}};
+// {BM, BN, BK, LDS-DMA staging, precision}.  prec 0 (exact fp32): tiles
+// 1..10 stage through registers + ds_write; 11..20 are the same shapes staged
+// by LDS-DMA (buffer_load ... lds); 21..28 are the 8-accumulator (64x128 /
+// 128x64 per wave) shapes, register- then DMA-staged.  prec 1 (fp16x3,
+// conv_h3.hip): 29..45, register staging (the A tile is split on its way to LDS).
+constexpr int kTiles[PO_CONV_NTILES][5] = {
+    {128, 128, 16, 0, 0}, {128, 128, 32, 0, 0}, {64, 128, 16, 0, 0}, {64, 128, 32, 0, 0}, {128, 64, 16, 0, 0},
+    {128, 64, 32, 0, 0},  {64, 64, 16, 0, 0},   {64, 64, 32, 0, 0},  {128, 32, 16, 0, 0}, {128, 32, 32, 0, 0},
+    {128, 128, 16, 1, 0}, {128, 128, 32, 1, 0}, {64, 128, 16, 1, 0}, {64, 128, 32, 1, 0}, {128, 64, 16, 1, 0},
+    {128, 64, 32, 1, 0},  {64, 64, 16, 1, 0},   {64, 64, 32, 1, 0},  {128, 32, 16, 1, 0}, {128, 32, 32, 1, 0},
+    {256, 128, 16, 0, 0}, {256, 128, 32, 0, 0}, {128, 256, 16, 0, 0}, {128, 256, 32, 0, 0},
+    {256, 128, 16, 1, 0}, {256, 128, 32, 1, 0}, {128, 256, 16, 1, 0}, {128, 256, 32, 1, 0},
+    {128, 128, 16, 0, 1}, {64, 128, 16, 0, 1},  {128, 64, 16, 0, 1},  {64, 64, 16, 0, 1},  {128, 32, 16, 0, 1},
+    {128, 128, 32, 0, 1}, {64, 128, 32, 0, 1},  {128, 64, 32, 0, 1},  {64, 64, 32, 0, 1},  {128, 32, 32, 0, 1},
+    {256, 128, 32, 0, 1}, {128, 256, 32, 0, 1},
+    {128, 128, 64, 0, 1}, {64, 128, 64, 0, 1},  {128, 64, 64, 0, 1},  {64, 64, 64, 0, 1},  {128, 32, 64, 0, 1}};
 }  // namespace
 
-extern "C" int po_conv_tile_info(int t, int* bm, int* bn, int* bk) {
+extern "C" int po_conv_tile_info(int t, int* bm, int* bn, int* bk, int* prec) {
   PO_REQUIRE(t >= 1 && t <= PO_CONV_NTILES && bm && bn && bk, "po_conv_tile_info: bad tile %d", t);
   *bm = kTiles[t - 1][0];
   *bn = kTiles[t - 1][1];
   *bk = kTiles[t - 1][2];
+  if (prec) *prec = kTiles[t - 1][4];
   return PO_OK;
 }
 
@@ -444,6 +366,15 @@ extern "C" int po_conv(const po_conv_desc* d, const float* in, const float* W, c
   a.in = in; a.W = W; a.bias = bias; a.y = y_out; a.res = res; a.sum = sum_out; a.mask = mask_y;
   a.y2 = y2_out; a.mask2 = mask2;
   a.in_org = d->in_org; a.out_org = d->out_org;
+  a.prec = d->prec;
+  a.w_shift = d->w_shift;
+  a.in_amax = d->in_amax;
+  a.y_amax = d->y_amax;
+  a.sum_amax = d->sum_amax;
+  a.y2_amax = d->y2_amax;
+  PO_REQUIRE(a.prec == 0 || a.prec == 1, "po_conv: prec %d", a.prec);
+  PO_REQUIRE(a.prec == 0 || a.in_amax, "po_conv: prec 1 needs the input's max|x| slot (in_amax)");
+  PO_REQUIRE(!sum_out || !a.sum_amax || a.sum_amax != a.y_amax, "po_conv: y and sum share an amax slot");
   a.ksplit = d->ksplit > 1 ? d->ksplit : 1;
   a.ws = d->workspace;
   PO_REQUIRE(a.ksplit <= 64 && a.ksplit <= d->ntaps * (d->Cin_p / 16), "po_conv: ksplit %d out of range", a.ksplit);
@@ -458,9 +389,10 @@ extern "C" int po_conv(const po_conv_desc* d, const float* in, const float* W, c
   a.M = d->B * d->Hg * d->Wg;
   a.ntiles_n = 1;
   const int64_t in_bytes = (int64_t)d->B * d->Hin * d->Win * d->Cin_p * 4;
-  const int64_t w_bytes = (int64_t)d->N * d->ntaps * d->Cin_p * 4;
-  PO_REQUIRE(in_bytes < (1LL << 31) && w_bytes < (1LL << 31),
-             "po_conv: input (%lld B) and weights (%lld B) must each be < 2 GiB (32-bit buffer offsets)",
+  // prec 1: w_bytes is one fp16 plane (the lo plane follows it)
+  const int64_t w_bytes = (int64_t)d->N * d->ntaps * d->Cin_p * (a.prec == 1 ? 2 : 4);
+  PO_REQUIRE(in_bytes < (1LL << 31) && w_bytes < (1LL << 30),
+             "po_conv: input (%lld B) must be < 2 GiB and weights (%lld B) < 1 GiB (32-bit buffer offsets)",
              (long long)in_bytes, (long long)w_bytes);
   a.in_bytes = (uint32_t)in_bytes;
   a.w_bytes = (uint32_t)w_bytes;
@@ -485,6 +417,8 @@ extern "C" int po_conv(const po_conv_desc* d, const float* in, const float* W, c
     bn = kTiles[d->tile - 1][1];
     bk = kTiles[d->tile - 1][2];
     gl = kTiles[d->tile - 1][3];
+    PO_REQUIRE(kTiles[d->tile - 1][4] == a.prec, "po_conv: tile %d is not a prec-%d tile", d->tile, a.prec);
+    PO_REQUIRE(a.Cin_p % bk == 0, "po_conv: tile %d needs Cin_p %% %d == 0 (Cin_p=%d)", d->tile, bk, a.Cin_p);
   } else if (!forced_tile(bm, bn, bk, gl)) {
     // largest tile that still gives >= 2 workgroups per CU
     const int64_t M = a.M;
@@ -497,7 +431,19 @@ extern "C" int po_conv(const po_conv_desc* d, const float* in, const float* W, c
     else if (tiles(64, 128) >= 512) { bm = 64; bn = 128; }
     else { bm = 64; bn = 64; }
   }
-  if (bk == 32 && a.Cin_p % 32 != 0) bk = 16;
+  while (bk > 16 && a.Cin_p % bk != 0) bk /= 2;
+  int rc;
+  if (a.prec == 1) {
+    ConvArgs b = a;
+    b.ntiles_n = po::ceil_div(a.N, bn);
+    rc = po::launch_h3(b, st, bm, bn, bk);
+    if (rc == PO_OK && a.ksplit > 1) {
+      hipLaunchKernelGGL(conv_reduce_k, dim3(po::ceil_div((int64_t)a.M * (a.N / 4), 256)), dim3(256), 0, st, b);
+      rc = po::check_launch("po_conv (split-K reduce)");
+    }
+    return rc;
+  }
+  if (bk > 32) bk = 32;
   if (gl) return bk == 32 ? dispatch<32, true>(a, st, bm, bn) : dispatch<16, true>(a, st, bm, bn);
   return bk == 32 ? dispatch<32, false>(a, st, bm, bn) : dispatch<16, false>(a, st, bm, bn);
 }

@@ -7,16 +7,20 @@ namespace {
 __global__ __launch_bounds__(256) void slice_accum_k(const float* __restrict__ src, int ss, int so,
                                                      float* __restrict__ dst, int ds, int doff,
                                                      int64_t M, int C, int acc,
-                                                     const float* __restrict__ my, int ms) {
+                                                     const float* __restrict__ my, int ms,
+                                                     uint32_t* __restrict__ amax) {
   const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  if (t >= M * C) return;
-  const int64_t m = t / C;
-  const int c = (int)(t - m * C);
-  float v = src[m * ss + so + c];
-  float* d = dst + m * ds + doff + c;
-  if (acc) v += *d;
-  if (my) v *= po::leaky_grad(my[m * ms + c]);
-  *d = v;
+  float v = 0.f;
+  if (t < M * C) {
+    const int64_t m = t / C;
+    const int c = (int)(t - m * C);
+    v = src[m * ss + so + c];
+    float* d = dst + m * ds + doff + c;
+    if (acc) v += *d;
+    if (my) v *= po::leaky_grad(my[m * ms + c]);
+    *d = v;
+  }
+  if (amax) po::amax_commit(amax, fabsf(v));
 }
 
 // window <-> full-map moves (po_view_move): one thread per dst element
@@ -24,10 +28,12 @@ __global__ __launch_bounds__(256) void view_move_k(const float* __restrict__ src
                                                    const int32_t* __restrict__ sorg, float* __restrict__ dst,
                                                    int Hd, int Wd, int ds, int doff,
                                                    const int32_t* __restrict__ dorg, int B, int C, int mode,
-                                                   int acc, const float* __restrict__ my, int ms) {
-  const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
+                                                   int acc, const float* __restrict__ my, int ms,
+                                                   uint32_t* __restrict__ amax) {
+  const int64_t t0 = (int64_t)blockIdx.x * 256 + threadIdx.x;
   const int64_t tot = (int64_t)B * Hd * Wd * C;
-  if (t >= tot) return;
+  const bool live = t0 < tot;
+  const int64_t t = live ? t0 : 0;
   const int c = (int)(t % C);
   const int64_t p = t / C;
   const int x = (int)(p % Wd);
@@ -40,38 +46,48 @@ __global__ __launch_bounds__(256) void view_move_k(const float* __restrict__ src
     if (ly < 0 || ly >= Hs || lx < 0 || lx >= Ws) return 0.f;
     return src[(((int64_t)b * Hs + ly) * Ws + lx) * ss + so + c];
   };
-  float v;
-  if (mode == 0) v = at(py, px);
-  else if (mode == 1) v = at(py >> 1, px >> 1);
-  else v = (at(2 * py, 2 * px) + at(2 * py, 2 * px + 1)) + (at(2 * py + 1, 2 * px) + at(2 * py + 1, 2 * px + 1));
-  float* d = dst + p * ds + doff + c;
-  if (acc) v += *d;
-  if (my) v *= po::leaky_grad(my[p * ms + c]);
-  *d = v;
+  float v = 0.f;
+  if (live) {
+    if (mode == 0) v = at(py, px);
+    else if (mode == 1) v = at(py >> 1, px >> 1);
+    else v = (at(2 * py, 2 * px) + at(2 * py, 2 * px + 1)) + (at(2 * py + 1, 2 * px) + at(2 * py + 1, 2 * px + 1));
+    float* d = dst + p * ds + doff + c;
+    if (acc) v += *d;
+    if (my) v *= po::leaky_grad(my[p * ms + c]);
+    *d = v;
+  }
+  if (amax) po::amax_commit(amax, fabsf(v));
 }
 
 __global__ __launch_bounds__(256) void up2_fwd_k(const float* __restrict__ src, int B, int H, int W,
                                                  int C, int ss, float* __restrict__ dst, int ds,
-                                                 int doff) {
-  const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
+                                                 int doff, uint32_t* __restrict__ amax) {
+  const int64_t t0 = (int64_t)blockIdx.x * 256 + threadIdx.x;
   const int64_t tot = (int64_t)B * 2 * H * 2 * W * C;
-  if (t >= tot) return;
+  const bool live = t0 < tot;
+  const int64_t t = live ? t0 : 0;
   const int c = (int)(t % C);
   int64_t p = t / C;                       // output pixel (b, y, x) at 2H x 2W
   const int x = (int)(p % (2 * W));
   p /= 2 * W;
   const int y = (int)(p % (2 * H));
   const int b = (int)(p / (2 * H));
-  const float v = src[(((int64_t)b * H + y / 2) * W + x / 2) * ss + c];   // nearest: floor(dst/2)
-  dst[(((int64_t)b * 2 * H + y) * 2 * W + x) * ds + doff + c] = v;
+  float v = 0.f;
+  if (live) {
+    v = src[(((int64_t)b * H + y / 2) * W + x / 2) * ss + c];   // nearest: floor(dst/2)
+    dst[(((int64_t)b * 2 * H + y) * 2 * W + x) * ds + doff + c] = v;
+  }
+  if (amax) po::amax_commit(amax, fabsf(v));
 }
 
 __global__ __launch_bounds__(256) void up2_bwd_k(const float* __restrict__ src, int ss, int so, int B,
                                                  int H, int W, int C, float* __restrict__ dst, int ds,
-                                                 int acc, const float* __restrict__ my, int ms) {
-  const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
+                                                 int acc, const float* __restrict__ my, int ms,
+                                                 uint32_t* __restrict__ amax) {
+  const int64_t t0 = (int64_t)blockIdx.x * 256 + threadIdx.x;
   const int64_t tot = (int64_t)B * H * W * C;
-  if (t >= tot) return;
+  const bool live = t0 < tot;
+  const int64_t t = live ? t0 : 0;
   const int c = (int)(t % C);
   const int64_t p = t / C;
   const int x = (int)(p % W);
@@ -79,37 +95,46 @@ __global__ __launch_bounds__(256) void up2_bwd_k(const float* __restrict__ src, 
   const int b = (int)(p / ((int64_t)W * H));
   const float* s0 = src + (((int64_t)b * 2 * H + 2 * y) * 2 * W + 2 * x) * ss + so + c;
   const int64_t rs = (int64_t)2 * W * ss;
-  float v = (s0[0] + s0[ss]) + (s0[rs] + s0[rs + ss]);
-  float* d = dst + p * ds + c;
-  if (acc) v += *d;
-  if (my) v *= po::leaky_grad(my[p * ms + c]);
-  *d = v;
+  float v = 0.f;
+  if (live) {
+    v = (s0[0] + s0[ss]) + (s0[rs] + s0[rs + ss]);
+    float* d = dst + p * ds + c;
+    if (acc) v += *d;
+    if (my) v *= po::leaky_grad(my[p * ms + c]);
+    *d = v;
+  }
+  if (amax) po::amax_commit(amax, fabsf(v));
 }
 
 // k=2 max pool; stride 2 (no padding) or stride 1 over ZeroPad2d((0,1,0,1))
 __global__ __launch_bounds__(256) void maxpool2_fwd_k(const float* __restrict__ src, int B, int H, int W,
                                                       int C, int Cp, int stride, int Ho, int Wo,
-                                                      float* __restrict__ dst, int8_t* __restrict__ am) {
+                                                      float* __restrict__ dst, int8_t* __restrict__ am,
+                                                      uint32_t* __restrict__ amax) {
   const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
   const int64_t tot = (int64_t)B * Ho * Wo * Cp;
-  if (t >= tot) return;
-  const int c = (int)(t % Cp);
-  const int64_t p = t / Cp;
-  const int x = (int)(p % Wo);
-  const int y = (int)((p / Wo) % Ho);
-  const int b = (int)(p / ((int64_t)Wo * Ho));
-  if (c >= C) { dst[t] = 0.f; am[t] = 0; return; }
   float best = 0.f;
-  int arg = -1;
+  if (t < tot) {
+    const int c = (int)(t % Cp);
+    const int64_t p = t / Cp;
+    const int x = (int)(p % Wo);
+    const int y = (int)((p / Wo) % Ho);
+    const int b = (int)(p / ((int64_t)Wo * Ho));
+    int arg = 0;
+    if (c < C) {
+      arg = -1;
 #pragma unroll
-  for (int k = 0; k < 4; ++k) {
-    const int yy = y * stride + (k >> 1), xx = x * stride + (k & 1);
-    // outside the source = the zero padding of ZeroPad2d (stride-1 case)
-    const float v = (yy < H && xx < W) ? src[(((int64_t)b * H + yy) * W + xx) * Cp + c] : 0.f;
-    if (arg < 0 || v > best || isnan(v)) { best = v; arg = k; }
+      for (int k = 0; k < 4; ++k) {
+        const int yy = y * stride + (k >> 1), xx = x * stride + (k & 1);
+        // outside the source = the zero padding of ZeroPad2d (stride-1 case)
+        const float v = (yy < H && xx < W) ? src[(((int64_t)b * H + yy) * W + xx) * Cp + c] : 0.f;
+        if (arg < 0 || v > best || isnan(v)) { best = v; arg = k; }
+      }
+    }
+    dst[t] = best;
+    am[t] = (int8_t)arg;
   }
-  dst[t] = best;
-  am[t] = (int8_t)arg;
+  if (amax) po::amax_commit(amax, fabsf(best));
 }
 
 // gather form: each source pixel sums the outputs whose argmax selected it
@@ -117,17 +142,19 @@ __global__ __launch_bounds__(256) void maxpool2_bwd_k(const float* __restrict__ 
                                                       const int8_t* __restrict__ am, int B, int H, int W,
                                                       int C, int Cp, int stride, int Ho, int Wo,
                                                       float* __restrict__ ds, int acc,
-                                                      const float* __restrict__ my) {
-  const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
+                                                      const float* __restrict__ my,
+                                                      uint32_t* __restrict__ amax) {
+  const int64_t t0 = (int64_t)blockIdx.x * 256 + threadIdx.x;
   const int64_t tot = (int64_t)B * H * W * Cp;
-  if (t >= tot) return;
+  const bool live = t0 < tot;
+  const int64_t t = live ? t0 : 0;
   const int c = (int)(t % Cp);
   const int64_t p = t / Cp;
   const int x = (int)(p % W);
   const int y = (int)((p / W) % H);
   const int b = (int)(p / ((int64_t)W * H));
   float v = 0.f;
-  if (c < C) {
+  if (live && c < C) {
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
       const int dy = k >> 1, dx = k & 1;
@@ -139,9 +166,12 @@ __global__ __launch_bounds__(256) void maxpool2_bwd_k(const float* __restrict__ 
       if (am[o] == k) v += dd[o];
     }
   }
-  if (acc) v += ds[t];
-  if (my) v *= po::leaky_grad(my[t]);
-  ds[t] = v;
+  if (live) {
+    if (acc) v += ds[t];
+    if (my) v *= po::leaky_grad(my[t]);
+    ds[t] = v;
+  }
+  if (amax) po::amax_commit(amax, fabsf(v));
 }
 
 __global__ __launch_bounds__(256) void nhwc2nchw_k(const float* __restrict__ s, int B, int H, int W, int C,
@@ -172,19 +202,19 @@ __global__ __launch_bounds__(256) void nchw2nhwc_k(const float* __restrict__ s, 
 
 extern "C" int po_slice_accum(const float* src, int src_stride, int src_off, float* dst, int dst_stride,
                               int dst_off, int64_t M, int C, int accumulate, const float* mask_y,
-                              int mask_stride, po_stream_t s) {
+                              int mask_stride, uint32_t* amax, po_stream_t s) {
   PO_REQUIRE(src && dst && M >= 0 && C >= 0, "po_slice_accum: bad argument");
   PO_REQUIRE(src_off + C <= src_stride && dst_off + C <= dst_stride, "po_slice_accum: slice exceeds stride");
   if (M * C == 0) return PO_OK;
   hipLaunchKernelGGL(slice_accum_k, dim3(po::ceil_div(M * C, 256)), dim3(256), 0, po::stream_of(s), src,
-                     src_stride, src_off, dst, dst_stride, dst_off, M, C, accumulate, mask_y, mask_stride);
+                     src_stride, src_off, dst, dst_stride, dst_off, M, C, accumulate, mask_y, mask_stride, amax);
   return po::check_launch("po_slice_accum");
 }
 
 extern "C" int po_view_move(const float* src, int Hs, int Ws, int src_stride, int src_off,
                             const int32_t* src_org, float* dst, int Hd, int Wd, int dst_stride, int dst_off,
                             const int32_t* dst_org, int B, int C, int mode, int accumulate,
-                            const float* mask_y, int mask_stride, po_stream_t s) {
+                            const float* mask_y, int mask_stride, uint32_t* amax, po_stream_t s) {
   PO_REQUIRE(src && dst && B > 0 && C >= 0 && Hs > 0 && Ws > 0 && Hd > 0 && Wd > 0, "po_view_move: bad argument");
   PO_REQUIRE(mode >= 0 && mode <= 2, "po_view_move: mode %d", mode);
   PO_REQUIRE(src_off + C <= src_stride && dst_off + C <= dst_stride, "po_view_move: slice exceeds stride");
@@ -193,26 +223,26 @@ extern "C" int po_view_move(const float* src, int Hs, int Ws, int src_stride, in
   if (!tot) return PO_OK;
   hipLaunchKernelGGL(view_move_k, dim3(po::ceil_div(tot, 256)), dim3(256), 0, po::stream_of(s), src, Hs, Ws,
                      src_stride, src_off, src_org, dst, Hd, Wd, dst_stride, dst_off, dst_org, B, C, mode,
-                     accumulate, mask_y, mask_stride);
+                     accumulate, mask_y, mask_stride, amax);
   return po::check_launch("po_view_move");
 }
 
 extern "C" int po_upsample2_fwd(const float* src, int B, int H, int W, int C, int src_stride, float* dst,
-                                int dst_stride, int dst_off, po_stream_t s) {
+                                int dst_stride, int dst_off, uint32_t* amax, po_stream_t s) {
   PO_REQUIRE(src && dst && C <= src_stride && dst_off + C <= dst_stride, "po_upsample2_fwd: bad argument");
   const int64_t tot = (int64_t)B * 4 * H * W * C;
   hipLaunchKernelGGL(up2_fwd_k, dim3(po::ceil_div(tot, 256)), dim3(256), 0, po::stream_of(s), src, B, H, W,
-                     C, src_stride, dst, dst_stride, dst_off);
+                     C, src_stride, dst, dst_stride, dst_off, amax);
   return po::check_launch("po_upsample2_fwd");
 }
 
 extern "C" int po_upsample2_bwd(const float* src, int src_stride, int src_off, int B, int H, int W, int C,
                                 float* dst, int dst_stride, int accumulate, const float* mask_y,
-                                int mask_stride, po_stream_t s) {
+                                int mask_stride, uint32_t* amax, po_stream_t s) {
   PO_REQUIRE(src && dst && src_off + C <= src_stride && C <= dst_stride, "po_upsample2_bwd: bad argument");
   const int64_t tot = (int64_t)B * H * W * C;
   hipLaunchKernelGGL(up2_bwd_k, dim3(po::ceil_div(tot, 256)), dim3(256), 0, po::stream_of(s), src,
-                     src_stride, src_off, B, H, W, C, dst, dst_stride, accumulate, mask_y, mask_stride);
+                     src_stride, src_off, B, H, W, C, dst, dst_stride, accumulate, mask_y, mask_stride, amax);
   return po::check_launch("po_upsample2_bwd");
 }
 
@@ -222,25 +252,25 @@ static inline void pool_out(int H, int W, int stride, int& Ho, int& Wo) {
 }
 
 extern "C" int po_maxpool2_fwd(const float* src, int B, int H, int W, int C, int Cp, int stride, float* dst,
-                               int8_t* argmax, po_stream_t s) {
+                               int8_t* argmax, uint32_t* amax, po_stream_t s) {
   PO_REQUIRE(src && dst && argmax && (stride == 1 || stride == 2) && C <= Cp, "po_maxpool2_fwd: bad argument");
   int Ho, Wo;
   pool_out(H, W, stride, Ho, Wo);
   const int64_t tot = (int64_t)B * Ho * Wo * Cp;
   hipLaunchKernelGGL(maxpool2_fwd_k, dim3(po::ceil_div(tot, 256)), dim3(256), 0, po::stream_of(s), src, B, H,
-                     W, C, Cp, stride, Ho, Wo, dst, argmax);
+                     W, C, Cp, stride, Ho, Wo, dst, argmax, amax);
   return po::check_launch("po_maxpool2_fwd");
 }
 
 extern "C" int po_maxpool2_bwd(const float* d_dst, const int8_t* argmax, int B, int H, int W, int C, int Cp,
                                int stride, float* d_src, int accumulate, const float* mask_y,
-                               po_stream_t s) {
+                               uint32_t* amax, po_stream_t s) {
   PO_REQUIRE(d_dst && argmax && d_src && (stride == 1 || stride == 2), "po_maxpool2_bwd: bad argument");
   int Ho, Wo;
   pool_out(H, W, stride, Ho, Wo);
   const int64_t tot = (int64_t)B * H * W * Cp;
   hipLaunchKernelGGL(maxpool2_bwd_k, dim3(po::ceil_div(tot, 256)), dim3(256), 0, po::stream_of(s), d_dst,
-                     argmax, B, H, W, C, Cp, stride, Ho, Wo, d_src, accumulate, mask_y);
+                     argmax, B, H, W, C, Cp, stride, Ho, Wo, d_src, accumulate, mask_y, amax);
   return po::check_launch("po_maxpool2_bwd");
 }
 

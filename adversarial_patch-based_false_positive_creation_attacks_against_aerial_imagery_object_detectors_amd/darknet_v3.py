@@ -20,6 +20,7 @@ is the same implicit GEMM with transposed/flipped weights (stride 2 split into
 its 4 parity classes), and the LeakyReLU derivative of the producing layer is
 applied in the epilogue of the last gradient contribution to it.
 """
+import math
 import os
 from itertools import chain
 
@@ -243,6 +244,8 @@ class NetPlan:
                              and net._conv_meta[0]["cin"] == 3 and net._conv_meta[0]["cout"] <= 64)
         self.in_nhwc = None if self.first_direct else torch.zeros(B, H, W, 16, device=dev)
         self._build_grad_plan()
+        self.prec = 1 if net.conv_prec == "fp16x3" else 0
+        self._build_slots()
         self._build_ops()
 
     # ---------------- receptive-field windows ----------------
@@ -448,6 +451,41 @@ class NetPlan:
     def _leaky(self, r):
         return (self.net.blocks[r]["type"] == "convolutional" and self.net._conv_meta[r]["act"] == "leaky")
 
+    # ---------------- max|x| slots (fp16x3 operand scales) ----------------
+    def _build_slots(self):
+        """One uint32 slot per activation/gradient tensor: every kernel writing
+        the tensor atomicMax's max|value| into it, and a fp16x3 po_conv reading
+        it as its A operand takes its power-of-two scale from it (zeroed at the
+        start of every forward)."""
+        idx = {}
+        for t in self.act + self.grad + [self.in_nhwc]:
+            if t is not None and t.data_ptr() not in idx:
+                idx[t.data_ptr()] = len(idx)
+        self._slot_idx = idx
+        self.amax = torch.zeros(len(idx), nat.PO_AMAX_SUB, dtype=torch.int32, device=self.device)
+
+    def slot(self, t):
+        """Device address of tensor t's max|x| slot (None for None)."""
+        if t is None:
+            return None
+        return nat.c_void_p(self.amax.data_ptr() + 4 * nat.PO_AMAX_SUB * self._slot_idx[t.data_ptr()])
+
+    def _conv_prec(self, desc, src, wts_or_j, taps=None, cin_p=None):
+        """Precision of one po_conv launch and its weight pointer: fp16x3 for
+        every conv whose input is a network tensor (the NHWC copy of the image
+        has no max|x| slot and keeps exact fp32)."""
+        if self.prec == 1 and src != INPUT:
+            if taps is None:
+                w16, shift = self.net._dev16(wts_or_j)
+            else:
+                w16, shift = self.net._dgrad_weight16(wts_or_j, taps, cin_p, self.device)
+            desc.prec, desc.w_shift = 1, shift
+            return w16
+        desc.prec, desc.w_shift = 0, 0
+        if taps is None:
+            return self.net._dev[wts_or_j]["w"]
+        return self.net._dgrad_weight(wts_or_j, taps, cin_p, self.device)
+
     # ---------------- launch lists ----------------
     def _build_ops(self):
         net, blocks, B = self.net, self.net.blocks, self.B
@@ -465,7 +503,7 @@ class NetPlan:
                 y_out = self.act[i]
                 if i == 0 and self.first_direct:
                     args = (None, B, self.H, self.W, m["stride"], P(wts["w27"]), P(wts["bias"]), m["cout"],
-                            self.cp[i], 1 if m["act"] == "leaky" else 0, P(y_out))
+                            self.cp[i], 1 if m["act"] == "leaky" else 0, P(y_out), self.slot(y_out))
                     fwd.append(("po_conv_first_fwd", args, "img0"))
                     assert not fuse_next
                     continue
@@ -493,7 +531,11 @@ class NetPlan:
                     f = int(sc["from"])
                     f = f if f >= 0 else (i + 1) + f
                     res, sum_out = self.act[self.root[f]], self.act[i + 1]
-                args = (nat.ctypes.byref(desc), P(inp), P(wts["w"]), P(wts["bias"]), P(y_out), P(res),
+                wptr = self._conv_prec(desc, src, i)
+                desc.in_amax = self.slot(inp).value if src != INPUT else None
+                desc.y_amax = self.slot(y_out).value
+                desc.sum_amax = self.slot(sum_out).value if sum_out is not None else None
+                args = (nat.ctypes.byref(desc), P(inp), P(wptr), P(wts["bias"]), P(y_out), P(res),
                         P(sum_out), None, None, None)
                 desc.macs = B * desc.Hg * desc.Wg * m["cout"] * m["cin"] * k * k      # logical channels
                 desc.block, desc.kind = i, "fwd"
@@ -505,9 +547,9 @@ class NetPlan:
                 M = B * self.dims[i][0] * self.dims[i][1]
                 C = self.shp[i][2]
                 fwd.append(("po_slice_accum", (P(self.act[a]), self.cp[a], 0, P(self.act[i]), self.cp[i], 0, M, C, 0,
-                                               None, 0), None))
+                                               None, 0, self.slot(self.act[i])), None))
                 fwd.append(("po_slice_accum", (P(self.act[b]), self.cp[b], 0, P(self.act[i]), self.cp[i], 0, M, C, 1,
-                                               None, 0), None))
+                                               None, 0, self.slot(self.act[i])), None))
             elif t == "route":
                 if len(self.srcs[i]) == 1:
                     continue
@@ -517,7 +559,7 @@ class NetPlan:
                     C = self.shp[s][2]
                     if self._same_view(s, i):
                         fwd.append(("po_slice_accum", (P(self.act[s]), self.cp[s], 0, P(self.act[i]), self.cp[i], off,
-                                                       M, C, 0, None, 0), None))
+                                                       M, C, 0, None, 0, self.slot(self.act[i])), None))
                     else:
                         fwd.append(("po_view_move", self._move(self.act[s], s, 0, self.act[i], i, off, C, 0, 0, None),
                                     None))
@@ -527,7 +569,7 @@ class NetPlan:
                 hs, ws_, cs = self.shp[s]
                 if self.win[i] is None and self.win[s] is None:
                     fwd.append(("po_upsample2_fwd", (P(self.act[s]), B, hs, ws_, cs, self.cp[s], P(self.act[i]),
-                                                     self.cp[i], 0), None))
+                                                     self.cp[i], 0, self.slot(self.act[i])), None))
                 else:
                     fwd.append(("po_view_move", self._move(self.act[s], s, 0, self.act[i], i, 0, cs, 1, 0, None),
                                 None))
@@ -535,7 +577,7 @@ class NetPlan:
                 s = self.srcs[i][0]
                 hs, ws_, cs = self.shp[s]
                 fwd.append(("po_maxpool2_fwd", (P(self.act[s]), B, hs, ws_, cs, self.cp[s], int(d["stride"]),
-                                                P(self.act[i]), P(self.argmax[i])), None))
+                                                P(self.act[i]), P(self.argmax[i]), self.slot(self.act[i])), None))
         self.fwd_ops = fwd
 
         # backward
@@ -571,7 +613,8 @@ class NetPlan:
                 _, mask_b, _ = contrib(b)
                 M = self.B * self.dims[r][0] * self.dims[r][1]
                 bwd.append(("po_slice_accum", (P(self.grad[r]), self.cp[r], 0, P(self.grad[b]), self.cp[b], 0, M,
-                                               self.shp[r][2], 0, P(mask_b), self.cp[b]), None))
+                                               self.shp[r][2], 0, P(mask_b), self.cp[b], self.slot(self.grad[b])),
+                            None))
 
         for j in range(self.n - 1, -1, -1):
             d = blocks[j]
@@ -588,14 +631,14 @@ class NetPlan:
                         bwd.append(("po_conv_first_dgrad", (P(G), B, self.H, self.W, m["stride"], P(wts["w27"]),
                                                             m["cout"], self.cp[j], "roi", "dimg"), None))
                     else:
-                        for desc, wd in self._dgrad_descs(j, INPUT, 0):
+                        for desc, wd in self._dgrad_descs(j, INPUT, 0, G, self.in_nhwc):
                             bwd.append(("po_conv", (nat.ctypes.byref(desc), P(G), P(wd), None, P(self.in_nhwc), None,
                                                     None, None, None, None), desc))
                         bwd.append(("po_nhwc_to_nchw", (P(self.in_nhwc), B, self.H, self.W, 3, 16, "dimg"), None))
                     continue
                 acc, mask, final = contrib(src)
                 y2, m2 = dual_of(src, final)
-                for desc, wd in self._dgrad_descs(j, src, acc):
+                for desc, wd in self._dgrad_descs(j, src, acc, G, self.grad[src], y2):
                     bwd.append(("po_conv", (nat.ctypes.byref(desc), P(G), P(wd), None, P(self.grad[src]), None, None,
                                             P(mask), P(y2), P(m2)), desc))
             elif t == "shortcut":
@@ -606,14 +649,15 @@ class NetPlan:
                     if mask is not None:               # f has no later contributor: apply its mask in place
                         M = self.B * self.dims[f][0] * self.dims[f][1]
                         bwd.append(("po_slice_accum", (P(G), self.cp[j], 0, P(self.grad[f]), self.cp[f], 0, M,
-                                                       self.shp[f][2], 0, P(mask), self.cp[f]), None))
+                                                       self.shp[f][2], 0, P(mask), self.cp[f], self.slot(self.grad[f])),
+                                    None))
                     continue
                 M = self.B * self.dims[j][0] * self.dims[j][1]
                 C = self.shp[j][2]
                 for s_ in self.srcs[j]:
                     acc, mask, final = contrib(s_)
                     bwd.append(("po_slice_accum", (P(G), self.cp[j], 0, P(self.grad[s_]), self.cp[s_], 0, M, C, acc,
-                                                   P(mask), self.cp[s_]), None))
+                                                   P(mask), self.cp[s_], self.slot(self.grad[s_])), None))
                     fallback_dual(s_, final)
             elif t == "route":
                 off = 0
@@ -623,7 +667,7 @@ class NetPlan:
                     acc, mask, final = contrib(s_)
                     if self._same_view(s_, j):
                         bwd.append(("po_slice_accum", (P(G), self.cp[j], off, P(self.grad[s_]), self.cp[s_], 0, M, C,
-                                                       acc, P(mask), self.cp[s_]), None))
+                                                       acc, P(mask), self.cp[s_], self.slot(self.grad[s_])), None))
                     else:
                         bwd.append(("po_view_move", self._move(G, j, off, self.grad[s_], s_, 0, C, 0, acc, mask),
                                     None))
@@ -635,7 +679,8 @@ class NetPlan:
                 hs, ws_, cs = self.shp[s_]
                 if self.win[j] is None and self.win[s_] is None:
                     bwd.append(("po_upsample2_bwd", (P(G), self.cp[j], 0, B, hs, ws_, cs, P(self.grad[s_]),
-                                                     self.cp[s_], acc, P(mask), self.cp[s_]), None))
+                                                     self.cp[s_], acc, P(mask), self.cp[s_], self.slot(self.grad[s_])),
+                                None))
                 else:
                     bwd.append(("po_view_move", self._move(G, j, 0, self.grad[s_], s_, 0, cs, 2, acc, mask), None))
                 fallback_dual(s_, final)
@@ -644,7 +689,7 @@ class NetPlan:
                 acc, mask, final = contrib(s_)
                 hs, ws_, cs = self.shp[s_]
                 bwd.append(("po_maxpool2_bwd", (P(G), P(self.argmax[j]), B, hs, ws_, cs, self.cp[s_], int(d["stride"]),
-                                                P(self.grad[s_]), acc, P(mask)), None))
+                                                P(self.grad[s_]), acc, P(mask), self.slot(self.grad[s_])), None))
                 fallback_dual(s_, final)
         self.bwd_ops = bwd
 
@@ -667,10 +712,12 @@ class NetPlan:
         Hd, Wd = self.dims[di]
         o = lambda i: nat.c_void_p(self._orgp(i)) if self._orgp(i) is not None else None
         return (P(src), Hs, Ws, self.cp[si], soff, o(si), P(dst), Hd, Wd, self.cp[di], doff, o(di), self.B, C,
-                mode, acc, P(mask), self.cp[di])
+                mode, acc, P(mask), self.cp[di], self.slot(dst))
 
-    def _dgrad_descs(self, j, src, acc):
-        """po_conv launches computing d(input of conv j) (one per stride parity class)."""
+    def _dgrad_descs(self, j, src, acc, G, dst, dst2=None):
+        """po_conv launches computing d(input of conv j) (one per stride parity
+        class): G = dL/d(output of j), dst (and dst2, the dual output) receive
+        the input gradient."""
         m = self.net._conv_meta[j]
         s, k, pad = m["stride"], m["k"], m["pad"]
         if self.win[j] is not None or (src != INPUT and self.win[src] is not None):
@@ -688,8 +735,11 @@ class NetPlan:
                     continue
                 taps = [(kh, kw) for kh in range(k) for kw in range(k)
                         if (py + pad - kh) % s == 0 and (px + pad - kw) % s == 0]
-                wd = self.net._dgrad_weight(j, taps, cin_p, self.device)
                 desc = nat.po_conv_desc()
+                wd = self._conv_prec(desc, src, j, taps, cin_p)
+                desc.in_amax = self.slot(G).value
+                desc.y_amax = self.slot(dst).value
+                desc.y2_amax = self.slot(dst2).value if dst2 is not None else None
                 desc.B, desc.Hin, desc.Win, desc.Cin_p = self.B, self.dims[j][0], self.dims[j][1], self.cp[j]
                 desc.Hout, desc.Wout, desc.Cout_p = Hin, Win, cin_p
                 desc.in_org, desc.out_org = self._orgp(j), (self._orgp(src) if src != INPUT else None)
@@ -736,24 +786,26 @@ class NetPlan:
         with torch.no_grad():
             for t in bufs.values():
                 t.uniform_(-1.0, 1.0)           # time on random data, not zeros (clock)
+        self.amax.fill_(0x3F800000)             # max|x| = 1.0 for the U(-1,1) buffers
         tiles = []
         for t in range(1, nat.PO_CONV_NTILES + 1):
-            bm, bn, bk = nat.c_int(), nat.c_int(), nat.c_int()
-            nat.call("po_conv_tile_info", t, nat.ctypes.byref(bm), nat.ctypes.byref(bn), nat.ctypes.byref(bk))
-            tiles.append((t, bm.value, bn.value, bk.value))
+            bm, bn, bk, pr = nat.c_int(), nat.c_int(), nat.c_int(), nat.c_int()
+            nat.call("po_conv_tile_info", t, nat.ctypes.byref(bm), nat.ctypes.byref(bn), nat.ctypes.byref(bk),
+                     nat.ctypes.byref(pr))
+            tiles.append((t, bm.value, bn.value, bk.value, pr.value))
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         for name, args, desc in self.fwd_ops + self.bwd_ops:
             if name != "po_conv":
                 continue
             key = (desc.B, desc.Hin, desc.Win, desc.Cin_p, desc.Hg, desc.Wg, desc.in_step, desc.ntaps, desc.N,
-                   desc.accumulate, args[6] is not None, args[7] is not None, args[8] is not None)
+                   desc.accumulate, args[6] is not None, args[7] is not None, args[8] is not None, desc.prec)
             if key in cache:
                 self._set_tile(desc, cache[key])
                 continue
             M = desc.B * desc.Hg * desc.Wg
             best = None
-            for t, bm, bn, bk in tiles:
-                if bk == 32 and desc.Cin_p % 32:
+            for t, bm, bn, bk, pr in tiles:
+                if pr != desc.prec or desc.Cin_p % bk:
                     continue
                 if bn > max(32, desc.N):
                     continue
@@ -783,6 +835,7 @@ class NetPlan:
         with torch.no_grad():
             for t in bufs.values():
                 t.zero_()
+        self.amax.zero_()
         torch.cuda.synchronize()
 
     def _set_tile(self, desc, choice):
@@ -799,6 +852,7 @@ class NetPlan:
         self.gen += 1
         st = nat.stream()
         lib = self.lib
+        self.amax.zero_()
         xp = nat.c_void_p(x.data_ptr())
         if not self.first_direct:
             nat.call("po_nchw_to_nhwc", xp, self.B, self.H, self.W, 3, 16, nat.c_void_p(self.in_nhwc.data_ptr()), st)
@@ -834,7 +888,8 @@ class NetPlan:
             mask = self.act[r] if (self.ncons[r] == 0 and self._leaky(r)) else None
             nat.call("po_slice_accum", nat.c_void_p(g.data_ptr()), self.cp[r], 0,
                      nat.c_void_p(self.grad[r].data_ptr()), self.cp[r], 0, M, self.cp[r], 0,
-                     nat.c_void_p(mask.data_ptr()) if mask is not None else None, self.cp[r], st)
+                     nat.c_void_p(mask.data_ptr()) if mask is not None else None, self.cp[r],
+                     self.slot(self.grad[r]), st)
         dxp = nat.c_void_p(d_x.data_ptr())
         roip = nat.c_void_p(roi.data_ptr()) if roi is not None else None
         for name, args, desc in self.bwd_ops:
@@ -900,6 +955,11 @@ class Darknet(nn.Module):
         self.clone_heads = False
         # receptive-field windows on the training path (ADVPATCH_WINDOWS=0: full maps)
         self.window_heads = os.environ.get("ADVPATCH_WINDOWS", "1") != "0"
+        # conv operand precision: "fp16x3" (split fp16 MFMA, fp32-accurate; default)
+        # or "fp32" (exact fp32 MFMA)
+        self.conv_prec = os.environ.get("ADVPATCH_CONV_PREC", "fp16x3")
+        if self.conv_prec not in ("fp16x3", "fp32"):
+            raise ValueError("ADVPATCH_CONV_PREC must be fp16x3 or fp32, got %r" % self.conv_prec)
         self._conv_meta = {}
         cin = [int(self.hyperparams["channels"])]
         for i, (d, mod) in enumerate(zip(self.blocks, self.module_list)):
@@ -1014,6 +1074,30 @@ class Darknet(nn.Module):
             self._dev[i] = ent
         self._dev_device = device
 
+    @staticmethod
+    def _split16(w):
+        """fp32 weights -> (fp16 [2, *w.shape] = hi, lo pieces of w * 2^shift,
+        shift), with max|w * 2^shift| in [2^13, 2^14) (po_conv prec 1)."""
+        m = float(w.abs().max())
+        shift = 14 - math.frexp(m)[1] if m > 0 else 0
+        ws = w * (2.0 ** shift)                       # exact: power of two, no overflow
+        hi = ws.half()
+        lo = (ws - hi.float()).half()
+        return torch.stack([hi, lo]).contiguous(), shift
+
+    def _dev16(self, i):
+        """Split-fp16 forward weights of conv i (built on first use)."""
+        ent = self._dev[i]
+        if "w16" not in ent:
+            ent["w16"], ent["w16_shift"] = self._split16(ent["w"])
+        return ent["w16"], ent["w16_shift"]
+
+    def _dgrad_weight16(self, j, taps, cin_p, device):
+        key = (j, tuple(taps), cin_p, "f16")
+        if key not in self._dgrad_cache:
+            self._dgrad_cache[key] = self._split16(self._dgrad_weight(j, taps, cin_p, device))
+        return self._dgrad_cache[key]
+
     def _dgrad_weight(self, j, taps, cin_p, device):
         """[Cin_p][len(taps)][Cout_p] weights of one dgrad launch of conv j."""
         key = (j, tuple(taps), cin_p)
@@ -1034,7 +1118,7 @@ class Darknet(nn.Module):
         full-map dependency run on receptive-field windows around the loss
         cells (NetPlan._plan_windows); only the training path uses it."""
         self._prepare(device)
-        key = (B, H, W, str(device), bool(windowed))
+        key = (B, H, W, str(device), bool(windowed), self.conv_prec)
         if key not in self._plans:
             p = NetPlan(self, B, H, W, device, windowed=windowed)
             if torch.device(device).type == "cuda" and os.environ.get("ADVPATCH_TUNE", "1") != "0":

@@ -33,7 +33,8 @@ typedef void* po_stream_t;
 #define PO_EHIP -2     /* HIP runtime error */
 #define PO_EDEVICE -3  /* device is not gfx950 */
 
-#define PO_ABI_VERSION 4
+#define PO_ABI_VERSION 5
+#define PO_AMAX_SUB 64  /* sub-slots per max|x| slot (see po_conv_desc) */
 
 int po_abi_version(void);
 const char* po_last_error(void);
@@ -167,15 +168,36 @@ typedef struct po_conv_desc {
                                  >= ksplit*M*N floats, M = B*Hg*Wg) are reduced in split
                                  order by a second kernel that applies the epilogue */
   float* workspace;
+  /* Operand precision.  0: exact fp32 MFMA (v_mfma_f32_32x32x2_f32); W is fp32
+   * [N][ntaps][Cin_p].  1: split fp16 ("fp16x3"): every operand x is scaled by
+   * a power of two s and written as x*s = hi + lo with hi = fp16(x*s),
+   * lo = fp16(x*s - hi); the product uses hi*hi' + hi*lo' + lo*hi' on
+   * v_mfma_f32_32x32x16_f16 with fp32 accumulation and is scaled back
+   * exactly (relative error per product <= ~3*2^-22).
+   * W is then fp16 [2][N][ntaps][Cin_p] (hi plane, lo plane) of the fp32
+   * weights times 2^w_shift, and in_amax must point at the max|in| slot. */
+  int prec;
+  int w_shift;
+  /* Per-tensor max|x| slots (DEVICE): a slot is PO_AMAX_SUB uint32 holding float
+   * bits, atomicMax'd by writers spread over the sub-slots; the tensor's bound
+   * is the max over them.  The caller zeroes a slot before its tensor is
+   * first written.  in_amax:
+   * an upper bound of max|in| (required for prec 1, written by the kernels that
+   * produced `in`); y_amax / sum_amax / y2_amax (each may be NULL): receive
+   * max|y_out| / max|sum_out| / max|y2_out| of the values this launch writes. */
+  const uint32_t* in_amax;
+  uint32_t* y_amax;
+  uint32_t* sum_amax;
+  uint32_t* y2_amax;
 } po_conv_desc;
 
-#define PO_CONV_NTILES 28
+#define PO_CONV_NTILES 45
 /* Tile `t` (1-based): block rows BM (output pixels), block columns BN (output
  * channels), k-step BK (input channels).  Tiles 1..10 stage operands through
  * registers, 11..20 are the same shapes staged by LDS-DMA, 21..28 are
  * 256x128 / 128x256 blocks (register, then LDS-DMA staging).  Returns
  * PO_EINVAL for a bad index. */
-int po_conv_tile_info(int t, int* bm, int* bn, int* bk);
+int po_conv_tile_info(int t, int* bm, int* bn, int* bk, int* prec);
 
 /* v[m][n] = act(sum_k A[m][k] * W[n][k] + bias[n]) (+ y_out[m][n] if accumulate);
  * W [N][ntaps][Cin_p] (BN folded on the host).
@@ -194,7 +216,8 @@ int po_conv(const po_conv_desc* d, const float* in, const float* W, const float*
 /* First layer, 3 input channels NCHW image -> NHWC Cout_p (VALU direct conv):
  * y = leaky(conv3x3(img, W[Cout][27]) + bias). */
 int po_conv_first_fwd(const float* img, int B, int H, int W, int stride, const float* Wt,
-                      const float* bias, int Cout, int Cout_p, int act, float* y, po_stream_t s);
+                      const float* bias, int Cout, int Cout_p, int act, float* y, uint32_t* amax,
+                      po_stream_t s);
 /* Its input gradient: d_img[b,c,h,w] (NCHW) from D [B,Ho,Wo,Cout_p] (already
  * multiplied by leaky'), W [Cout][27].  roi (may be NULL) [B,4] int32
  * {x0,y0,x1,y1}: only pixels x0<=w<x1, y0<=h<y1 of image b are computed (the
@@ -207,7 +230,7 @@ int po_conv_first_dgrad(const float* D, int B, int H, int W, int stride, const f
  * strides are channel strides; M pixels. */
 int po_slice_accum(const float* src, int src_stride, int src_off, float* dst, int dst_stride,
                    int dst_off, int64_t M, int C, int accumulate, const float* mask_y,
-                   int mask_stride, po_stream_t s);
+                   int mask_stride, uint32_t* amax, po_stream_t s);
 /* Spatially-aware copy between full-map and window buffers (NHWC).  Over
  * every pixel (b,i,j) of dst [B,Hd,Wd] (map position p = (i,j) + dst_org[b]):
  *   mode 0: v = src[p - src_org[b]]                  (route slice)
@@ -215,25 +238,28 @@ int po_slice_accum(const float* src, int src_stride, int src_off, float* dst, in
  *   mode 2: v = sum_{a,c in {0,1}} src[2p + (a,c) - src_org[b]]  (its backward)
  * src pixels outside the src buffer read 0; channels src[off_s + c], dst[off_d + c];
  * dst (=|+=) v, optionally * leaky'(mask_y) (mask in dst's pixel layout).
- * NULL org = full map. */
+ * NULL org = full map.
+ * The data-movement entries below and po_conv_first_fwd take an optional
+ * `amax` slot (see po_conv_desc): max|value written| is atomicMax'd into it. */
 int po_view_move(const float* src, int Hs, int Ws, int src_stride, int src_off, const int32_t* src_org,
                  float* dst, int Hd, int Wd, int dst_stride, int dst_off, const int32_t* dst_org, int B,
-                 int C, int mode, int accumulate, const float* mask_y, int mask_stride, po_stream_t s);
+                 int C, int mode, int accumulate, const float* mask_y, int mask_stride, uint32_t* amax,
+                 po_stream_t s);
 /* nearest 2x upsample fwd (darknet_v3.py:103-113): dst[b,2h+y,2w+x, off+c] = src[b,h,w,c]. */
 int po_upsample2_fwd(const float* src, int B, int H, int W, int C, int src_stride, float* dst,
-                     int dst_stride, int dst_off, po_stream_t s);
+                     int dst_stride, int dst_off, uint32_t* amax, po_stream_t s);
 /* its backward: dst[b,h,w,c] (=|+=) sum of the 4 src pixels (src at 2H x 2W,
  * channel offset src_off), optionally * leaky'(mask_y). */
 int po_upsample2_bwd(const float* src, int src_stride, int src_off, int B, int H, int W, int C,
                      float* dst, int dst_stride, int accumulate, const float* mask_y,
-                     int mask_stride, po_stream_t s);
+                     int mask_stride, uint32_t* amax, po_stream_t s);
 /* max pool k=2 (stride 2, or stride 1 after ZeroPad2d((0,1,0,1)), darknet_v3.py:61-69);
  * argmax [B,Ho,Wo,C] int8 window position. */
 int po_maxpool2_fwd(const float* src, int B, int H, int W, int C, int Cp, int stride, float* dst,
-                    int8_t* argmax, po_stream_t s);
+                    int8_t* argmax, uint32_t* amax, po_stream_t s);
 int po_maxpool2_bwd(const float* d_dst, const int8_t* argmax, int B, int H, int W, int C, int Cp,
                     int stride, float* d_src, int accumulate, const float* mask_y,
-                    po_stream_t s);
+                    uint32_t* amax, po_stream_t s);
 
 /* NCHW [B,C,H,W] <-> NHWC [B,H,W,Cp] layout conversion (heads in and out of
  * the drop-in Darknet.forward API). */

@@ -21,11 +21,12 @@ pytestmark = pytest.mark.gpu
 DEV = torch.device("cuda", 0)
 
 
-def _net(cfg, tmp_path, seed=4):
+def _net(cfg, tmp_path, seed=4, prec="fp16x3"):
     dk, W, G = pkg_mod("darknet_v3"), pkg_mod("weights"), pkg_mod("cfg_gen")
     path = str(tmp_path / "w.weights")
     W.write_weights(path, W.synthesize(cfg, seed=seed))
     net = dk.Darknet(cfg)
+    net.conv_prec = prec
     net.load_darknet_weights(path)
     ref = oracle.OracleDarknet(G.cfg_text(cfg), path)
     return net, ref
@@ -35,8 +36,8 @@ def _rel(a, b):
     return float((a - b).abs().max() / b.abs().max().clamp_min(1e-30))
 
 
-def _check(cfg, B, tmp_path, fwd_tol=5e-5, bwd_tol=1e-4):
-    net, ref = _net(cfg, tmp_path)
+def _check(cfg, B, tmp_path, fwd_tol=5e-5, bwd_tol=1e-4, prec="fp16x3"):
+    net, ref = _net(cfg, tmp_path, prec=prec)
     S = net.height
     x = pkg_mod("synthetic").frames(B, S, seed=7)
     xg = x.to(DEV).requires_grad_(True)
@@ -57,23 +58,34 @@ def _check(cfg, B, tmp_path, fwd_tol=5e-5, bwd_tol=1e-4):
     sum((o * g).sum() for o, g in zip(outs_ref, grads)).backward()
     sum((o * g.to(DEV)).sum() for o, g in zip(outs, grads)).backward()
     assert _rel(xg.grad.cpu(), xr.grad) < bwd_tol
+    # every max|x| slot bounds its tensor (the fp16x3 operand scales rely on it)
+    for t in plan.act + plan.grad:
+        if t is not None:
+            bound = float(plan.amax[plan._slot_idx[t.data_ptr()]].view(torch.float32).max())
+            assert float(t.abs().max()) <= bound
 
 
-def test_mini3_fwd_bwd(tmp_path):
-    _check("builtin:mini3", 3, tmp_path)
+PRECS = ["fp16x3", "fp32"]
+
+
+@pytest.mark.parametrize("prec", PRECS)
+def test_mini3_fwd_bwd(tmp_path, prec):
+    _check("builtin:mini3", 3, tmp_path, prec=prec)
 
 
 def test_mini3_96_batch5(tmp_path):
     _check("builtin:mini3-96", 5, tmp_path)
 
 
-def test_tiny_dota_416(tmp_path):
+@pytest.mark.parametrize("prec", PRECS)
+def test_tiny_dota_416(tmp_path, prec):
     # maxpool s2 and the ZeroPad2d + maxpool s1 block of yolov3-tiny
-    _check("builtin:yolov3-tiny-dota", 2, tmp_path)
+    _check("builtin:yolov3-tiny-dota", 2, tmp_path, prec=prec)
 
 
-def test_yolov3_dota_608(tmp_path):
-    _check("builtin:yolov3-dota", 1, tmp_path)
+@pytest.mark.parametrize("prec", PRECS)
+def test_yolov3_dota_608(tmp_path, prec):
+    _check("builtin:yolov3-dota", 1, tmp_path, prec=prec)
 
 
 def test_conv_tile_variants(tmp_path):
@@ -109,10 +121,24 @@ def test_heads_layout_matches_reference_view(tmp_path):
         assert _rel(hc, r) < 2e-5
 
 
+def _conv_operands(nat, wd, x, prec):
+    """(weight tensor, shift, amax slot) of a direct po_conv call: fp32 weights
+    for prec 0, the split fp16 planes and max|x| slot for prec 1 (fp16x3)."""
+    if prec == 0:
+        return wd, 0, None
+    w16, shift = pkg_mod("darknet_v3").Darknet._split16(wd)
+    slot = torch.zeros(64, dtype=torch.int32)
+    slot[5] = torch.tensor([float(x.abs().max())], dtype=torch.float32).view(torch.int32)   # any sub-slot
+    slot = slot.to(DEV)
+    return w16, shift, slot
+
+
+@pytest.mark.parametrize("prec", [0, 1])
 @pytest.mark.parametrize("B,H,Cin,Cout,k", [(4, 5, 512, 1024, 3), (16, 1, 1024, 64, 1), (3, 7, 96, 128, 3)])
-def test_split_k_matches_single_pass(B, H, Cin, Cout, k):
+def test_split_k_matches_single_pass(B, H, Cin, Cout, k, prec):
     """po_conv with the k-steps split over workgroups (partials reduced in
-    split order by the epilogue kernel) against one pass and torch conv2d."""
+    split order by the epilogue kernel) against one pass and torch conv2d,
+    for both operand precisions."""
     import ctypes
     nat = pkg_mod("_native")
     pad = (k - 1) // 2
@@ -120,14 +146,17 @@ def test_split_k_matches_single_pass(B, H, Cin, Cout, k):
     x = torch.randn(B, Cin, H, H, generator=gen)
     w = torch.randn(Cout, Cin, k, k, generator=gen) * (2.0 / (Cin * k * k)) ** 0.5
     bias = torch.randn(Cout, generator=gen) * 0.1
-    ref = torch.nn.functional.leaky_relu(torch.nn.functional.conv2d(x, w, bias, padding=pad), 0.1)
+    ref = torch.nn.functional.leaky_relu(torch.nn.functional.conv2d(x.double(), w.double(), bias.double(),
+                                                                    padding=pad), 0.1)
     xd = x.permute(0, 2, 3, 1).contiguous().to(DEV)
     wd = w.permute(0, 2, 3, 1).reshape(Cout, k * k, Cin).contiguous().to(DEV)
+    wt, shift, slot = _conv_operands(nat, wd, x, prec)
     bd = bias.to(DEV)
     outs = {}
     for ks in (1, 2, 5, 8):
         y = torch.full((B, H, H, Cout), float("nan"), device=DEV)
         ws = torch.empty(ks * B * H * H * Cout, device=DEV)
+        yslot = torch.zeros(64, dtype=torch.int32, device=DEV)
         d = nat.po_conv_desc()
         d.B, d.Hin, d.Win, d.Cin_p, d.Hout, d.Wout, d.Cout_p, d.Hg, d.Wg = B, H, H, Cin, H, H, Cout, H, H
         d.in_step, d.out_step, d.ntaps, d.N, d.act = 1, 1, k * k, Cout, 1
@@ -135,27 +164,34 @@ def test_split_k_matches_single_pass(B, H, Cin, Cout, k):
             for kw in range(k):
                 d.dh[kh * k + kw], d.dw[kh * k + kw] = kh - pad, kw - pad
         d.ksplit, d.workspace = ks, ws.data_ptr()
-        nat.call("po_conv", ctypes.byref(d), nat.ptr(xd), nat.ptr(wd), nat.ptr(bd), nat.ptr(y), None, None, None,
-                 None, None, nat.stream())
+        d.prec, d.w_shift = prec, shift
+        d.in_amax = slot.data_ptr() if slot is not None else None
+        d.y_amax = yslot.data_ptr()
+        nat.call("po_conv", ctypes.byref(d), nat.ptr(xd), nat.ptr(wt, wt.dtype), nat.ptr(bd), nat.ptr(y), None,
+                 None, None, None, None, nat.stream())
         outs[ks] = y.permute(0, 3, 1, 2).cpu()
+        assert float(yslot.cpu().view(torch.float32).max()) == float(y.abs().max())      # max|y| slot
     for ks, y in outs.items():
-        assert _rel(y, ref) < 1e-5, (ks, _rel(y, ref))
+        assert _rel(y.double(), ref) < 1e-5, (ks, _rel(y.double(), ref))
         assert _rel(y, outs[1]) < 1e-5, (ks, _rel(y, outs[1]))
 
 
-@pytest.mark.parametrize("tile", list(range(1, 29)))
+@pytest.mark.parametrize("tile", list(range(1, 46)))
 def test_every_conv_tile(tile):
-    """Every po_conv tile (register-staged 1..10, LDS-DMA-staged 11..20) on a
-    3x3 conv with zero padding, a ragged pixel count and a ragged channel
-    count, against torch conv2d."""
+    """Every po_conv tile (exact fp32: register-staged 1..10 and 21..24,
+    LDS-DMA-staged 11..20 and 25..28; fp16x3: 29..45) on a 3x3 conv with zero
+    padding, a ragged pixel count and a ragged channel count, against a
+    float64 torch conv2d."""
     import ctypes
     nat = pkg_mod("_native")
-    B, H, Cin, Cout, k = 3, 7, 96, 96, 3
+    bm, bn, bk, pr = (ctypes.c_int() for _ in range(4))
+    nat.call("po_conv_tile_info", tile, ctypes.byref(bm), ctypes.byref(bn), ctypes.byref(bk), ctypes.byref(pr))
+    B, H, Cin, Cout, k = 3, 7, 128 if bk.value == 64 else 96, 96, 3
     gen = torch.Generator().manual_seed(tile)
     x = torch.randn(B, Cin, H, H, generator=gen)
     w = torch.randn(Cout, Cin, k, k, generator=gen) * (2.0 / (Cin * k * k)) ** 0.5
     bias = torch.randn(Cout, generator=gen) * 0.1
-    ref = torch.nn.functional.conv2d(x, w, bias, padding=1)
+    ref = torch.nn.functional.conv2d(x.double(), w.double(), bias.double(), padding=1)
     y = torch.full((B, H, H, Cout), float("nan"), device=DEV)
     d = nat.po_conv_desc()
     d.B, d.Hin, d.Win, d.Cin_p, d.Hout, d.Wout, d.Cout_p, d.Hg, d.Wg = B, H, H, Cin, H, H, Cout, H, H
@@ -165,6 +201,9 @@ def test_every_conv_tile(tile):
             d.dh[kh * 3 + kw], d.dw[kh * 3 + kw] = kh - 1, kw - 1
     xd = x.permute(0, 2, 3, 1).contiguous().to(DEV)
     wd = w.permute(0, 2, 3, 1).reshape(Cout, 9, Cin).contiguous().to(DEV)
-    nat.call("po_conv", ctypes.byref(d), nat.ptr(xd), nat.ptr(wd), nat.ptr(bias.to(DEV)), nat.ptr(y), None, None,
-             None, None, None, nat.stream())
-    assert _rel(y.permute(0, 3, 1, 2).cpu(), ref) < 1e-5
+    wt, shift, slot = _conv_operands(nat, wd, x, pr.value)
+    d.prec, d.w_shift = pr.value, shift
+    d.in_amax = slot.data_ptr() if slot is not None else None
+    nat.call("po_conv", ctypes.byref(d), nat.ptr(xd), nat.ptr(wt, wt.dtype), nat.ptr(bias.to(DEV)), nat.ptr(y),
+             None, None, None, None, None, nat.stream())
+    assert _rel(y.permute(0, 3, 1, 2).cpu().double(), ref) < 3e-6     # fp32-class error either way

@@ -12,7 +12,7 @@ pytestmark = pytest.mark.gpu
 DEV = torch.device("cuda", 0)
 
 
-def _trainer(cfg, tmp_path, objective="ce"):
+def _trainer(cfg, tmp_path, objective="ce", prec="fp16x3"):
     tp, W, G = pkg_mod("train_patch"), pkg_mod("weights"), pkg_mod("cfg_gen")
     path = str(tmp_path / "w.weights")
     W.write_weights(path, W.synthesize(cfg, seed=4))
@@ -27,6 +27,7 @@ def _trainer(cfg, tmp_path, objective="ce"):
 
     pc.patch_configs["_test"] = _Cfg
     tr = tp.PatchTrainer("_test", device=DEV, objective=objective, verbose=False)
+    tr.darknet_model.conv_prec = prec
     ref_net = oracle.OracleDarknet(G.cfg_text(cfg), path)
     return tr, ref_net
 
@@ -71,14 +72,15 @@ def test_step_mini3_objectives(tmp_path, objective):
     _compare(*_run("builtin:mini3", 4, 32, tmp_path, objective=objective))
 
 
-def test_step_yolov3_dota_608(tmp_path):
+@pytest.mark.parametrize("prec", ["fp16x3", "fp32"])
+def test_step_yolov3_dota_608(tmp_path, prec):
     """yolov3-dota, two 608x608 frames, 224x224 patch.  Through 75 layers two
     fp32 implementations differ by more than 1e-4 even on aligned branches
     (different summation orders), so both are measured against a float64
     evaluation of the same ops: the HIP gradient must be within 1e-4 of it,
     or no further from it than 2x the fp32 oracle is."""
     sy, ld = pkg_mod("synthetic"), pkg_mod("load_data")
-    tr, ref_net = _trainer("builtin:yolov3-dota", tmp_path)
+    tr, ref_net = _trainer("builtin:yolov3-dota", tmp_path, prec=prec)
     B, P, S = 2, 224, 608
     img, lab = sy.frames(B, S, seed=40), sy.labels(B, seed=41)
     patch, dr = sy.patch(P, seed=42), sy.draws(B, P, seed=43)
@@ -94,7 +96,7 @@ def test_step_yolov3_dota_608(tmp_path):
     scale = g64.abs().max()
     err_hip = float((pg.grad.cpu().double() - g64).abs().max() / scale)
     err_32 = float((ref32["grad"].double() - g64).abs().max() / scale)
-    print("yolov3 patch grad vs float64: hip %.3g, fp32 oracle %.3g" % (err_hip, err_32))
+    print("yolov3 (%s) patch grad vs float64: hip %.3g, fp32 oracle %.3g" % (prec, err_hip, err_32))
     assert err_hip <= max(1e-4, 2.0 * err_32), (err_hip, err_32)
 
 

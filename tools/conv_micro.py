@@ -24,7 +24,13 @@ for kh in range(k):
         d.dh[kh * k + kw] = kh - pad
         d.dw[kh * k + kw] = kw - pad
 d.N, d.act, d.accumulate = Cout, 1, 0
-args = (ctypes.byref(d), nat.ptr(x), nat.ptr(w), nat.ptr(b), nat.ptr(y), None, None, None, None, None)
+if os.environ.get("MICRO_PREC", "0") == "1":          # fp16x3 operands
+    slot = torch.zeros(64, dtype=torch.int32, device=dev)
+    slot[0] = torch.tensor([float(x.abs().max())]).view(torch.int32)[0]
+    w, d.w_shift = ge._pkg("darknet_v3").Darknet._split16(w)
+    d.prec, d.in_amax = 1, slot.data_ptr()
+d.tile = int(os.environ.get("MICRO_TILE", "0"))
+args = (ctypes.byref(d), nat.ptr(x), nat.ptr(w, w.dtype), nat.ptr(b), nat.ptr(y), None, None, None, None, None)
 st = nat.stream()
 for _ in range(3):
     nat.call("po_conv", *args, st)

@@ -1,12 +1,14 @@
 #!/bin/bash
 # PMC passes over the conv microbenchmark (one counter group per pass).
-# usage: tools/pmc_conv.sh OUTDIR "B H Cin Cout k s iters" [TILE]
+# usage: [MICRO_PREC=1] tools/pmc_conv.sh OUTDIR "B H Cin Cout k s iters" [TILE]
+#   TILE: a po_conv tile index (1..45) or "BMxBNxBK[g]"
 set -e
 cd /tmp && export TMPDIR=/tmp
 cd "$GRAFT_REPO_ROOT"
 OUT=${1:-gpurun_out/pmc_conv}
 SHAPE=${2:-"16 76 128 256 3 1 30"}
-export ADVPATCH_CONV_TILE=${3:-128x128x16}
+TILE=${3:-128x128x16}
+if [[ "$TILE" =~ ^[0-9]+$ ]]; then export MICRO_TILE=$TILE; else export ADVPATCH_CONV_TILE=$TILE; fi
 mkdir -p $OUT
 timeout -k 10 120 python tools/conv_micro.py $SHAPE > $OUT/plain.txt 2>&1
 i=0
@@ -14,5 +16,5 @@ for grp in "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_MFMA SQ_INSTS_LDS SQ_INSTS_VMEM_RD S
            "SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_MFMA SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_VMEM GRBM_GUI_ACTIVE" \
            "SQ_VALU_MFMA_BUSY_CYCLES SQ_LDS_BANK_CONFLICT SQ_WAIT_INST_LDS SQ_INST_CYCLES_VMEM_RD GRBM_COUNT"; do
   i=$((i+1))
-  timeout -k 10 180 rocprofv3 --pmc $grp --kernel-include-regex conv_k --output-format csv -d $OUT/p$i -o p$i -- python tools/conv_micro.py $SHAPE > $OUT/p$i.log 2>&1 || { echo "pass $i failed"; exit 1; }
+  timeout -k 10 180 rocprofv3 --pmc $grp --kernel-include-regex 'conv_k|conv_h3_k' --output-format csv -d $OUT/p$i -o p$i -- python tools/conv_micro.py $SHAPE > $OUT/p$i.log 2>&1 || { echo "pass $i failed"; exit 1; }
 done

@@ -57,10 +57,10 @@ ms = defaultdict(float)
 for k, (e0, e1, _) in enumerate(timer):
     ms[k % n] += e0.elapsed_time(e1) / args.steps
 tot = sum(ms.values())
-print("%-6s %-5s %5s %9s %5s %6s %4s %9s %7s %6s" % ("kind", "block", "B*Hg*Wg", "", "N", "K", "tile", "us", "TF", "%"))
+print("%-6s %5s %9s %5s %6s %4s %3s %9s %7s %6s" % ("kind", "block", "B*Hg*Wg", "N", "K", "tile", "ks", "us", "TF", "%"))
 for k, d in enumerate(descs):
     K = d.ntaps * d.Cin_p
     M = d.B * d.Hg * d.Wg
-    print("%-6s %5d %9d %5d %6d %4d %9.1f %7.1f %6.2f" % (d.kind, d.block, M, d.N, K, d.tile, ms[k] * 1e3,
+    print("%-6s %5d %9d %5d %6d %4d %3d %9.1f %7.1f %6.2f" % (d.kind, d.block, M, d.N, K, d.tile, d.ksplit, ms[k] * 1e3,
                                                       2 * d.macs / (ms[k] * 1e-3) / 1e12, 100 * ms[k] / tot))
 print("total conv ms/step %.3f, launches %d, executed TFLOP/step %.3f" % (tot, n, 2 * sum(d.macs for d in descs) / 1e12))
