@@ -13,7 +13,7 @@ LIB_PATH = os.path.join(_HERE, "libadvpatch_hip.so")
 
 c_int, c_float, c_int64, c_void_p = ctypes.c_int, ctypes.c_float, ctypes.c_int64, ctypes.c_void_p
 
-PO_CONV_NTILES = 45   # include/advpatch.h
+PO_CONV_NTILES = 52   # include/advpatch.h
 PO_AMAX_SUB = 64      # sub-slots per max|x| slot
 
 
@@ -25,7 +25,8 @@ class po_conv_desc(ctypes.Structure):
         ("N", c_int), ("act", c_int), ("accumulate", c_int), ("tile", c_int),
         ("in_org", c_void_p), ("out_org", c_void_p), ("ksplit", c_int), ("workspace", c_void_p),
         ("prec", c_int), ("w_shift", c_int), ("in_amax", c_void_p), ("y_amax", c_void_p),
-        ("sum_amax", c_void_p), ("y2_amax", c_void_p)]
+        ("sum_amax", c_void_p), ("y2_amax", c_void_p), ("ybits", c_void_p), ("mbits", c_void_p),
+        ("m2bits", c_void_p)]
 
 
 _SIGS = {

@@ -30,6 +30,9 @@ struct ConvArgs {
   uint32_t* y_amax;             // optional max|output| slots
   uint32_t* sum_amax;
   uint32_t* y2_amax;
+  uint32_t* ybits;              // optional: sign bits (y > 0) of y_out, [pixel][Cout_p/32] words
+  const uint32_t* mbits;        // optional: leaky mask as sign bits (replaces mask)
+  const uint32_t* m2bits;       //                                   (replaces mask2)
   int prec, w_shift;            // prec 1: weights pre-scaled by 2^w_shift
   int ksplit;
   int B, Hin, Win, Cin_p, Hout, Wout, Cout_p, Hg, Wg;
@@ -78,15 +81,24 @@ __device__ __forceinline__ void store_partials(const ConvArgs& a, const floatx16
     }
 }
 
+// leaky'(.) factors of 4 consecutive channels n..n+3 from a sign-bit word
+__device__ __forceinline__ float4 leaky_grad_bits(uint32_t w, int n) {
+  const uint32_t b = w >> (n & 31);
+  return make_float4((b & 1) ? 1.f : 0.1f, (b & 2) ? 1.f : 0.1f, (b & 4) ? 1.f : 0.1f, (b & 8) ? 1.f : 0.1f);
+}
+
 // Epilogue.  Each wave stages one 32x32 accumulator tile at a time through a
 // private 4 KB slot of `smem` (the k-loop buffers are free by now), then every
 // lane handles 4 consecutive channels of a row: 16-byte loads of
 // bias/mask/res and 16-byte stores of y/sum/y2, 128 contiguous bytes per row.
 // v = acc * 2^-sh + bias (sh = 0 for fp32 operands; ldexp is exact).
+// Waves 0..3 hold the accumulators; in a warp-specialized launch the other
+// waves (active = false) only take part in the barrier and the slot commits.
 template <int BM, int TM, int TN>
 __device__ __forceinline__ void conv_epilogue(const ConvArgs& a, const floatx16 (&acc)[TM][TN], float* smem,
-                                              int* dst_pix, int m0, int n0, int wm, int wn, int sh) {
-  const int tid = threadIdx.x & 255, lane = tid & 63, wave = tid >> 6;
+                                              int* dst_pix, int m0, int n0, int wm, int wn, int sh,
+                                              bool active = true) {
+  const int tid = threadIdx.x, lane = tid & 63, wave = (tid >> 6) & 3;
   const int HgWg = a.Hg * a.Wg;
   if (tid < BM) {
     const int m = m0 + tid;
@@ -106,6 +118,7 @@ __device__ __forceinline__ void conv_epilogue(const ConvArgs& a, const floatx16 
   for (int i = 0; i < TM; ++i)
 #pragma unroll
     for (int j = 0; j < TN; ++j) {
+      if (!active) break;
 #pragma unroll
       for (int e = 0; e < 16; ++e)
         scr[((e & 3) + 8 * (e >> 2) + 4 * (lane >> 5)) * 32 + (lane & 31)] = acc[i][j][e];
@@ -113,43 +126,65 @@ __device__ __forceinline__ void conv_epilogue(const ConvArgs& a, const floatx16 
       const int n = n0 + wn * TN * 32 + j * 32 + cc;
       float4 bv = make_float4(0.f, 0.f, 0.f, 0.f);
       if (a.bias && n < a.N) bv = *reinterpret_cast<const float4*>(a.bias + n);
+      const int wpp = a.Cout_p >> 5;            // sign-bit words per pixel (bits need Cout_p % 32 == 0)
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
         const int row = rr + 8 * q;
         const float4 v = *reinterpret_cast<const float4*>(scr + row * 32 + cc);
         const int pix = dst_pix[wm * TM * 32 + i * 32 + row];
-        if (pix < 0 || n >= a.N) continue;
-        const size_t o = (size_t)pix * a.Cout_p + n;
-        float x[4] = {__builtin_ldexpf(v.x, -sh) + bv.x, __builtin_ldexpf(v.y, -sh) + bv.y,
-                      __builtin_ldexpf(v.z, -sh) + bv.z, __builtin_ldexpf(v.w, -sh) + bv.w};
-        if (a.act) {
+        const bool live = pix >= 0 && n < a.N;
+        uint32_t nib = 0;
+        if (live) {
+          const size_t o = (size_t)pix * a.Cout_p + n;
+          const size_t wo = (size_t)pix * wpp + (n >> 5);
+          float x[4] = {__builtin_ldexpf(v.x, -sh) + bv.x, __builtin_ldexpf(v.y, -sh) + bv.y,
+                        __builtin_ldexpf(v.z, -sh) + bv.z, __builtin_ldexpf(v.w, -sh) + bv.w};
+          if (a.act) {
 #pragma unroll
-          for (int c = 0; c < 4; ++c) x[c] = leaky(x[c]);
+            for (int c = 0; c < 4; ++c) x[c] = leaky(x[c]);
+          }
+          if (a.accumulate) {
+            const float4 p = *reinterpret_cast<const float4*>(a.y + o);
+            x[0] += p.x; x[1] += p.y; x[2] += p.z; x[3] += p.w;
+          }
+          float4 out = make_float4(x[0], x[1], x[2], x[3]);
+          if (a.mbits) {
+            const float4 g = leaky_grad_bits(a.mbits[wo], n);
+            out = make_float4(x[0] * g.x, x[1] * g.y, x[2] * g.z, x[3] * g.w);
+          } else if (a.mask) {
+            const float4 mk = *reinterpret_cast<const float4*>(a.mask + o);
+            out = make_float4(x[0] * leaky_grad(mk.x), x[1] * leaky_grad(mk.y), x[2] * leaky_grad(mk.z),
+                              x[3] * leaky_grad(mk.w));
+          }
+          *reinterpret_cast<float4*>(a.y + o) = out;
+          nib = (out.x > 0.f ? 1u : 0u) | (out.y > 0.f ? 2u : 0u) | (out.z > 0.f ? 4u : 0u) | (out.w > 0.f ? 8u : 0u);
+          my = fmaxf(my, fmaxf(fmaxf(fabsf(out.x), fabsf(out.y)), fmaxf(fabsf(out.z), fabsf(out.w))));
+          if (a.res) {
+            const float4 r = *reinterpret_cast<const float4*>(a.res + o);
+            const float4 sm = make_float4(x[0] + r.x, x[1] + r.y, x[2] + r.z, x[3] + r.w);
+            *reinterpret_cast<float4*>(a.sum + o) = sm;
+            ms = fmaxf(ms, fmaxf(fmaxf(fabsf(sm.x), fabsf(sm.y)), fmaxf(fabsf(sm.z), fabsf(sm.w))));
+          }
+          if (a.y2) {
+            float4 g;
+            if (a.m2bits) {
+              g = leaky_grad_bits(a.m2bits[wo], n);
+            } else {
+              const float4 mk = *reinterpret_cast<const float4*>(a.mask2 + o);
+              g = make_float4(leaky_grad(mk.x), leaky_grad(mk.y), leaky_grad(mk.z), leaky_grad(mk.w));
+            }
+            const float4 o2 = make_float4(x[0] * g.x, x[1] * g.y, x[2] * g.z, x[3] * g.w);
+            *reinterpret_cast<float4*>(a.y2 + o) = o2;
+            my2 = fmaxf(my2, fmaxf(fmaxf(fabsf(o2.x), fabsf(o2.y)), fmaxf(fabsf(o2.z), fabsf(o2.w))));
+          }
         }
-        if (a.accumulate) {
-          const float4 p = *reinterpret_cast<const float4*>(a.y + o);
-          x[0] += p.x; x[1] += p.y; x[2] += p.z; x[3] += p.w;
-        }
-        float4 out = make_float4(x[0], x[1], x[2], x[3]);
-        if (a.mask) {
-          const float4 mk = *reinterpret_cast<const float4*>(a.mask + o);
-          out = make_float4(x[0] * leaky_grad(mk.x), x[1] * leaky_grad(mk.y), x[2] * leaky_grad(mk.z),
-                            x[3] * leaky_grad(mk.w));
-        }
-        *reinterpret_cast<float4*>(a.y + o) = out;
-        my = fmaxf(my, fmaxf(fmaxf(fabsf(out.x), fabsf(out.y)), fmaxf(fabsf(out.z), fabsf(out.w))));
-        if (a.res) {
-          const float4 r = *reinterpret_cast<const float4*>(a.res + o);
-          const float4 sm = make_float4(x[0] + r.x, x[1] + r.y, x[2] + r.z, x[3] + r.w);
-          *reinterpret_cast<float4*>(a.sum + o) = sm;
-          ms = fmaxf(ms, fmaxf(fmaxf(fabsf(sm.x), fabsf(sm.y)), fmaxf(fabsf(sm.z), fabsf(sm.w))));
-        }
-        if (a.y2) {
-          const float4 mk = *reinterpret_cast<const float4*>(a.mask2 + o);
-          const float4 o2 = make_float4(x[0] * leaky_grad(mk.x), x[1] * leaky_grad(mk.y),
-                                        x[2] * leaky_grad(mk.z), x[3] * leaky_grad(mk.w));
-          *reinterpret_cast<float4*>(a.y2 + o) = o2;
-          my2 = fmaxf(my2, fmaxf(fmaxf(fabsf(o2.x), fabsf(o2.y)), fmaxf(fabsf(o2.z), fabsf(o2.w))));
+        if (a.ybits) {
+          // the 8 lanes of a row hold channels n0' .. n0' + 31 of one word: OR their nibbles
+          uint32_t w = nib << (4 * (lane & 7));
+          w |= (uint32_t)__shfl_xor((int)w, 1);
+          w |= (uint32_t)__shfl_xor((int)w, 2);
+          w |= (uint32_t)__shfl_xor((int)w, 4);
+          if (live && (lane & 7) == 0) a.ybits[(size_t)pix * wpp + (n >> 5)] = w;
         }
       }
       __builtin_amdgcn_wave_barrier();
@@ -161,6 +196,7 @@ __device__ __forceinline__ void conv_epilogue(const ConvArgs& a, const floatx16 
 
 // conv_h3.hip: launch of the split-precision kernel for tile (bm, bn, bk)
 // (the split-K reduction, when a.ksplit > 1, is launched by the caller)
-int launch_h3(const ConvArgs& a, hipStream_t st, int bm, int bn, int bk);
+// (dma = 1: the LDS-DMA multi-stage kernel)
+int launch_h3(const ConvArgs& a, hipStream_t st, int bm, int bn, int bk, int dma);
 
 }  // namespace po

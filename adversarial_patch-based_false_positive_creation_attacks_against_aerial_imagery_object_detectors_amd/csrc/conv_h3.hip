@@ -28,6 +28,31 @@ namespace {
 using po::ConvArgs;
 typedef _Float16 half8 __attribute__((ext_vector_type(8)));
 typedef _Float16 half2_t __attribute__((ext_vector_type(2)));
+typedef int i32x4 __attribute__((ext_vector_type(4)));
+
+// Buffer resource (raw, stride 0) over [base, base + bytes): offsets at or past
+// `bytes` read zero.
+__device__ __forceinline__ i32x4 make_rsrc(const void* base, uint32_t bytes) {
+  const uint64_t p = (uint64_t)base;
+  i32x4 r;
+  r[0] = __builtin_amdgcn_readfirstlane((int)(uint32_t)p);
+  r[1] = __builtin_amdgcn_readfirstlane((int)(uint32_t)(p >> 32));
+  r[2] = __builtin_amdgcn_readfirstlane((int)bytes);
+  r[3] = 0x00020000;
+  return r;
+}
+
+// 16-byte LDS-DMA (buffer_load_dwordx4 ... lds): lane l's 16 bytes from
+// rsrc + voff land at lds + 16 l.  Issued as inline asm so that hipcc's
+// wait-count pass, which cannot tell which LDS bytes a DMA writes, does not
+// drain every DMA in flight before each ds_read; the kernel orders the DMAs
+// itself (counted vmcnt + s_barrier).
+__device__ __forceinline__ void lds_dma16(i32x4 rsrc, const void* lds, uint32_t voff) {
+  const uint32_t m0 = __builtin_amdgcn_readfirstlane(
+      (uint32_t)(uintptr_t)((__attribute__((address_space(3))) const char*)lds));
+  asm volatile("s_mov_b32 m0, %0\n\tbuffer_load_dwordx4 %1, %2, 0 offen lds" ::"s"(m0), "v"(voff), "s"(rsrc)
+               : "memory", "m0");
+}
 
 __device__ __forceinline__ uint32_t pk_f16(float a, float b) {
   half2_t h;
@@ -36,15 +61,18 @@ __device__ __forceinline__ uint32_t pk_f16(float a, float b) {
   return __builtin_bit_cast(uint32_t, h);
 }
 
-// 8 fp32 values (scaled by 2^sh) -> hi and lo fp16 chunks
-__device__ __forceinline__ void split8(const float4 u, const float4 v, int sh, uint4& hi, uint4& lo) {
+// 8 fp32 values times sc (a power of two) -> hi and lo fp16 chunks.  The
+// empty asm keeps the compiler from re-deriving fp32(hi) with a second
+// conversion of x: it is read back from the packed halves.
+__device__ __forceinline__ void split8(const float4 u, const float4 v, float sc, uint4& hi, uint4& lo) {
   float x[8] = {u.x, u.y, u.z, u.w, v.x, v.y, v.z, v.w};
 #pragma unroll
-  for (int i = 0; i < 8; ++i) x[i] = __builtin_ldexpf(x[i], sh);
+  for (int i = 0; i < 8; ++i) x[i] *= sc;
   uint32_t h[4], l[4];
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
     h[i] = pk_f16(x[2 * i], x[2 * i + 1]);
+    asm volatile("" : "+v"(h[i]));
     const half2_t hh = __builtin_bit_cast(half2_t, h[i]);
     l[i] = pk_f16(x[2 * i] - (float)hh[0], x[2 * i + 1] - (float)hh[1]);
   }
@@ -79,6 +107,7 @@ __global__ __launch_bounds__(256) void conv_h3_k(const ConvArgs a) {
   const int HgWg = a.Hg * a.Wg;
   const int cth = tid % CPR, rth = tid / CPR;
   const int sh_in = po::input_shift(a);
+  const float sc_in = __builtin_ldexpf(1.f, sh_in);
 
   const uint32_t in_bytes = (uint32_t)__builtin_amdgcn_readfirstlane(a.in_bytes);
   const uint32_t w_bytes = (uint32_t)__builtin_amdgcn_readfirstlane(a.w_bytes);
@@ -141,7 +170,7 @@ __global__ __launch_bounds__(256) void conv_h3_k(const ConvArgs a) {
       const int row = rth + RPP * r;
       if (row < BM) {
         uint4 h, l;
-        split8(ra[r][0], ra[r][1], sh_in, h, l);
+        split8(ra[r][0], ra[r][1], sc_in, h, l);
         _Float16* base = As + (buf * 2) * A_HALFS + row * BK + swz(row, cth);
         *reinterpret_cast<uint4*>(base) = h;
         *reinterpret_cast<uint4*>(base + A_HALFS) = l;
@@ -171,7 +200,9 @@ __global__ __launch_bounds__(256) void conv_h3_k(const ConvArgs a) {
   const int split = blockIdx.y;
   const int ks0 = (int)((int64_t)split * nks_all / a.ksplit);
   const int nks = (int)((int64_t)(split + 1) * nks_all / a.ksplit) - ks0;
-  int tap = ks0 / kc, c0 = (ks0 - tap * kc) * BK;
+  // k-steps run channel-chunk major, tap minor: the taps of one channel
+  // chunk re-read the same (shifted) pixels while they are still in L1/L2
+  int tap = ks0 % a.ntaps, c0 = (ks0 / a.ntaps) * BK;
   int th = tap / a.tkw, tw = tap - th * a.tkw;
   gload(tap, a.dh0 + th * a.sdh, a.dw0 + tw * a.sdw, c0);
   sstore(0);
@@ -201,12 +232,17 @@ __global__ __launch_bounds__(256) void conv_h3_k(const ConvArgs a) {
         bh[j] = *reinterpret_cast<const half8*>(Bb + o);
         bl[j] = *reinterpret_cast<const half8*>(Bb + B_HALFS + o);
       }
+#if defined(PO_ABLATE_NOLOAD) || defined(PO_ABLATE_NOSTORE)
+      if (false) {      // ablation builds (tools/): k-steps without staging loads
+#else
       if (g == 0 && more) {
-        c0 += BK;
-        if (c0 == a.Cin_p) {
-          c0 = 0;
-          ++tap;
-          if (++tw == a.tkw) { tw = 0; ++th; }
+#endif
+        if (++tap == a.ntaps) {
+          tap = th = tw = 0;
+          c0 += BK;
+        } else if (++tw == a.tkw) {
+          tw = 0;
+          ++th;
         }
         gload(tap, a.dh0 + th * a.sdh, a.dw0 + tw * a.sdw, c0);
       }
@@ -219,7 +255,9 @@ __global__ __launch_bounds__(256) void conv_h3_k(const ConvArgs a) {
           acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[i], bh[j], acc[i][j], 0, 0, 0);
         }
     }
+#ifndef PO_ABLATE_NOSTORE
     if (more) sstore(buf ^ 1);
+#endif
     __syncthreads();
   }
 
@@ -230,6 +268,221 @@ __global__ __launch_bounds__(256) void conv_h3_k(const ConvArgs a) {
   __shared__ int dst_pix[BM];
   po::conv_epilogue<BM, TM, TN>(a, acc, reinterpret_cast<float*>(smem_h), dst_pix, m0, n0, wm, wn,
                                 sh_in + a.w_shift);
+}
+
+// LDS-DMA variant: no staging registers.  Each k-step's A tile (fp32) and
+// the weights' hi/lo fp16 tiles are copied global -> LDS by buffer_load ... lds
+// (16 bytes per lane, 1 KB per wave-instruction, XOR swizzle applied on the
+// source address) into an NS-stage ring, NS - 1 k-steps ahead of the MFMAs;
+// the A fragments are split into hi/lo as they are read from LDS.  Every wave
+// issues the same number D of DMAs per stage (dummy out-of-range copies past
+// the last k-step), so "stage ks has landed" is s_waitcnt vmcnt(D * (NS - 2))
+// followed by a raw s_barrier (a __syncthreads would drain every stage).
+template <int BM, int BN, int WM, int BK, int NS>
+__global__ __launch_bounds__(256) void conv_h3d_k(const ConvArgs a) {
+  constexpr int WN = 4 / WM;
+  constexpr int TM = BM / WM / 32;
+  constexpr int TN = BN / WN / 32;
+  static_assert(TM >= 1 && TN >= 1, "tile too small for 4 waves of 32x32");
+  constexpr int RA = BK * 4, RB = BK * 2;          // LDS row bytes: A fp32, B fp16
+  constexpr int CPA = RA / 16, CPB = RB / 16;      // 16-byte chunks per row
+  constexpr int SWA = RA == 64 ? 2 : (RA == 128 ? 1 : 0);   // log2(rows per 256-byte bank line)
+  constexpr int SWB = RB == 32 ? 3 : (RB == 64 ? 2 : 1);
+  constexpr int RPA = 1024 / RA, RPB = 1024 / RB;  // rows per 1 KB DMA piece
+  constexpr int NPA = BM / RPA, NPB = BN / RPB;    // pieces per tile (per B plane)
+  static_assert(NPA % 4 == 0 && NPB % 4 == 0, "every wave must issue the same DMA count");
+  constexpr int PA = NPA / 4, PB = NPB / 4;        // pieces per wave
+  constexpr int D = PA + 2 * PB;                   // DMAs per wave per stage
+  static_assert(D * (NS - 2) <= 63, "vmcnt range");
+  constexpr int A_BYTES = BM * RA, B_BYTES = BN * RB;
+  constexpr int SB = A_BYTES + 2 * B_BYTES;        // bytes per stage
+  static_assert(NS * SB >= 16384, "the epilogue needs 16 KB of LDS");
+  // ONE __shared__ array (a second LDS object makes hipcc drain the DMAs
+  // before every ds_read): NS stages, then the epilogue's pixel table
+  __shared__ __attribute__((aligned(16))) char smem[NS * SB + BM * 4];
+
+  const int wgid = po::xcd_remap();
+  const int tn = wgid % a.ntiles_n, tm = wgid / a.ntiles_n;
+  const int m0 = tm * BM, n0 = tn * BN;
+  const int tid = threadIdx.x & 255, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave / WN, wn = wave % WN;
+  const int HgWg = a.Hg * a.Wg;
+  const int sh_in = po::input_shift(a);
+  const float sc_in = __builtin_ldexpf(1.f, sh_in);
+
+  const uint32_t in_bytes = (uint32_t)__builtin_amdgcn_readfirstlane(a.in_bytes);
+  const uint32_t w_bytes = (uint32_t)__builtin_amdgcn_readfirstlane(a.w_bytes);
+  const i32x4 in_rs = make_rsrc(a.in, in_bytes);
+  const i32x4 w_rs = make_rsrc(a.W, 2 * w_bytes);
+  constexpr uint32_t kOOB = 0x80000000u;
+  const uint32_t pix_bytes = (uint32_t)a.Cin_p * 4u;
+  const uint32_t wpix_bytes = (uint32_t)a.Cin_p * 2u;
+
+  // A pieces of this wave: p = wave + 4r, lane -> row p*RPA + lane/CPA and the
+  // source chunk that belongs in LDS slot lane%CPA of the swizzled row
+  int a_hi[PA], a_wi[PA];
+  uint32_t a_off[PA];
+#pragma unroll
+  for (int r = 0; r < PA; ++r) {
+    const int row = (wave + 4 * r) * RPA + lane / CPA;
+    const int m = m0 + row;
+    const bool ok = m < a.M;
+    const int mm = ok ? m : 0;
+    const int b = mm / HgWg, rem = mm - b * HgWg;
+    const int i = rem / a.Wg, j = rem - i * a.Wg;
+    const int chunk = (lane % CPA) ^ ((row >> SWA) & (CPA - 1));
+    a_off[r] = ((uint32_t)b * a.Hin * a.Win) * pix_bytes + chunk * 16u;
+    int sy = 0, sx = 0;
+    if (a.out_org) { sy += a.out_org[2 * b]; sx += a.out_org[2 * b + 1]; }
+    if (a.in_org) { sy -= a.in_org[2 * b]; sx -= a.in_org[2 * b + 1]; }
+    a_hi[r] = ok ? i * a.in_step + sy : -(1 << 20);
+    a_wi[r] = j * a.in_step + sx;
+  }
+  const uint32_t wrow_bytes = (uint32_t)a.ntaps * wpix_bytes;
+  uint32_t b_off[PB];
+#pragma unroll
+  for (int r = 0; r < PB; ++r) {
+    const int row = (wave + 4 * r) * RPB + lane / CPB;
+    const int chunk = (lane % CPB) ^ ((row >> SWB) & (CPB - 1));
+    b_off[r] = (n0 + row < a.N) ? (uint32_t)(n0 + row) * wrow_bytes + chunk * 16u : kOOB;
+  }
+  auto dma = [&](char* lds, i32x4 rs, uint32_t voff) { lds_dma16(rs, lds, voff); };
+
+  const int kc = a.Cin_p / BK;
+  const int nks_all = a.ntaps * kc;
+  const int split = blockIdx.y;
+  const int ks0 = (int)((int64_t)split * nks_all / a.ksplit);
+  const int nks = (int)((int64_t)(split + 1) * nks_all / a.ksplit) - ks0;
+  // k-steps run channel-chunk major, tap minor: the taps of one channel
+  // chunk re-read the same (shifted) pixels while they are still in L1/L2
+  int tap = ks0 % a.ntaps, c0 = (ks0 / a.ntaps) * BK;
+  int th = tap / a.tkw, tw = tap - th * a.tkw;
+  int issued = 0;                               // k-steps issued so far (relative to ks0)
+  // issue the DMAs of the next k-step into stage slot issued % NS (out-of-range
+  // zero copies once the k-steps are exhausted, to keep the per-wave count)
+  auto issue = [&]() {
+    const bool live = issued < nks;
+    char* st = smem + (issued % NS) * SB;
+    const int dh = a.dh0 + th * a.sdh, dw = a.dw0 + tw * a.sdw;
+#pragma unroll
+    for (int r = 0; r < PA; ++r) {
+      const int hi = a_hi[r] + dh, wi = a_wi[r] + dw;
+      const bool ok = live && (unsigned)hi < (unsigned)a.Hin && (unsigned)wi < (unsigned)a.Win;
+      dma(st + (wave + 4 * r) * 1024, in_rs,
+          ok ? a_off[r] + ((uint32_t)hi * a.Win + wi) * pix_bytes + (uint32_t)c0 * 4u : kOOB);
+    }
+    const uint32_t tb = (uint32_t)tap * wpix_bytes + (uint32_t)c0 * 2u;
+#pragma unroll
+    for (int r = 0; r < PB; ++r) {
+      const uint32_t o = live ? b_off[r] + tb : kOOB;
+      dma(st + A_BYTES + (wave + 4 * r) * 1024, w_rs, o);
+      dma(st + A_BYTES + B_BYTES + (wave + 4 * r) * 1024, w_rs, o + w_bytes);
+    }
+    ++issued;
+    if (++tap == a.ntaps) {
+      tap = th = tw = 0;
+      c0 += BK;
+    } else if (++tw == a.tkw) {
+      tw = 0;
+      ++th;
+    }
+  };
+
+  floatx16 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.f;
+
+#pragma unroll
+  for (int s = 0; s < NS - 1; ++s) issue();
+  const int arow = wm * TM * 32 + (lane & 31);
+  const int brow = wn * TN * 32 + (lane & 31);
+  const int h = lane >> 5;
+  for (int ks = 0; ks < nks; ++ks) {
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(D * (NS - 2)) : "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    issue();                                    // into the slot read during step ks - 1
+    const char* st = smem + (ks % NS) * SB;
+    const float* Ab = reinterpret_cast<const float*>(st);
+    const _Float16* Bh = reinterpret_cast<const _Float16*>(st + A_BYTES);
+    const _Float16* Bl = reinterpret_cast<const _Float16*>(st + A_BYTES + B_BYTES);
+#pragma unroll
+    for (int g = 0; g < BK / 16; ++g) {
+      half8 ah[TM], al[TM], bh[TN], bl[TN];
+#pragma unroll
+      for (int i = 0; i < TM; ++i) {
+        const int row = arow + i * 32;
+        const float* rp = Ab + row * BK;
+        const int f = (row >> SWA) & (CPA - 1);
+        const float4 u = *reinterpret_cast<const float4*>(rp + ((4 * g + 2 * h) ^ f) * 4);
+        const float4 v = *reinterpret_cast<const float4*>(rp + ((4 * g + 2 * h + 1) ^ f) * 4);
+#ifdef PO_ABLATE_NOSPLIT
+        ah[i] = __builtin_bit_cast(half8, u);          // ablation: the LDS bytes as they are
+        al[i] = __builtin_bit_cast(half8, v);
+#else
+        uint4 hi, lo;
+        split8(u, v, sc_in, hi, lo);
+        ah[i] = __builtin_bit_cast(half8, hi);
+        al[i] = __builtin_bit_cast(half8, lo);
+#endif
+      }
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        const int row = brow + j * 32;
+        const int o = row * BK + (((2 * g + h) ^ ((row >> SWB) & (CPB - 1))) * 8);
+        bh[j] = *reinterpret_cast<const half8*>(Bh + o);
+        bl[j] = *reinterpret_cast<const half8*>(Bl + o);
+      }
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) {
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(al[i], bh[j], acc[i][j], 0, 0, 0);
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[i], bl[j], acc[i][j], 0, 0, 0);
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[i], bh[j], acc[i][j], 0, 0, 0);
+        }
+    }
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");     // the trailing (dummy) DMAs write LDS
+  __syncthreads();
+
+  if (a.ksplit > 1) {
+    po::store_partials<TM, TN>(a, acc, m0, n0, wm, wn, lane);
+    return;
+  }
+  po::conv_epilogue<BM, TM, TN>(a, acc, reinterpret_cast<float*>(smem), reinterpret_cast<int*>(smem + NS * SB),
+                                m0, n0, wm, wn, sh_in + a.w_shift);
+}
+
+template <int BM, int BN, int WM, int BK, int NS>
+int launch_dma(const ConvArgs& a, hipStream_t st) {
+  ConvArgs b = a;
+  b.ntiles_n = po::ceil_div(a.N, BN);
+  const int ntiles = po::ceil_div(a.M, BM) * b.ntiles_n;
+  hipLaunchKernelGGL((conv_h3d_k<BM, BN, WM, BK, NS>), dim3(ntiles, a.ksplit), dim3(256), 0, st, b);
+  return po::check_launch("po_conv (fp16x3, LDS-DMA)");
+}
+
+// LDS-DMA tiles: {BM, BN, BK} -> stage count and wave layout
+int dispatch_dma(const ConvArgs& a, hipStream_t st, int bm, int bn, int bk) {
+  if (bk == 32) {
+    if (bm == 128 && bn == 128) return launch_dma<128, 128, 4, 32, 3>(a, st);
+    if (bm == 128 && bn == 64) return launch_dma<128, 64, 4, 32, 4>(a, st);
+    if (bm == 64 && bn == 128) return launch_dma<64, 128, 2, 32, 4>(a, st);
+    if (bm == 64 && bn == 64) return launch_dma<64, 64, 2, 32, 4>(a, st);
+    if (bm == 256 && bn == 128) return launch_dma<256, 128, 4, 32, 3>(a, st);
+  }
+  if (bk == 16) {
+    if (bm == 128 && bn == 128) return launch_dma<128, 128, 4, 16, 4>(a, st);
+    if (bm == 256 && bn == 128) return launch_dma<256, 128, 4, 16, 4>(a, st);
+  }
+  po::set_error("po_conv (fp16x3 LDS-DMA): no %dx%dx%d tile", bm, bn, bk);
+  return PO_EINVAL;
 }
 
 template <int BM, int BN, int WM, int BK>
@@ -258,7 +511,8 @@ int dispatch(const ConvArgs& a, hipStream_t st, int bm, int bn) {
 }  // namespace
 
 namespace po {
-int launch_h3(const ConvArgs& a, hipStream_t st, int bm, int bn, int bk) {
+int launch_h3(const ConvArgs& a, hipStream_t st, int bm, int bn, int bk, int dma) {
+  if (dma) return dispatch_dma(a, st, bm, bn, bk);
   if (bk == 16) return dispatch<16>(a, st, bm, bn);
   if (bk == 32) return dispatch<32>(a, st, bm, bn);
   if (bk == 64) return dispatch<64>(a, st, bm, bn);

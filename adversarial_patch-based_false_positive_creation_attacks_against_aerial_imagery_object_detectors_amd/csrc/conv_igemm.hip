@@ -166,7 +166,9 @@ __global__ __launch_bounds__(256) void conv_k(const ConvArgs a) {
   const int ks0 = (int)((int64_t)split * nks_all / a.ksplit);
   const int nks = (int)((int64_t)(split + 1) * nks_all / a.ksplit) - ks0;
   // k-step position: tap (th, tw) and channel offset c0, advanced incrementally
-  int tap = ks0 / kc, c0 = (ks0 - tap * kc) * BK;
+  // k-steps run channel-chunk major, tap minor: the taps of one channel
+  // chunk re-read the same (shifted) pixels while they are still in L1/L2
+  int tap = ks0 % a.ntaps, c0 = (ks0 / a.ntaps) * BK;
   int th = tap / a.tkw, tw = tap - th * a.tkw;
   if constexpr (GL) {
     gload_lds(0, tap, a.dh0 + th * a.sdh, a.dw0 + tw * a.sdw, c0);
@@ -202,11 +204,12 @@ __global__ __launch_bounds__(256) void conv_k(const ConvArgs a) {
       if (g == 0 && more) {
 #endif
         // issue the next k-step's staging loads behind this group's fragment reads
-        c0 += BK;
-        if (c0 == a.Cin_p) {
-          c0 = 0;
-          ++tap;
-          if (++tw == a.tkw) { tw = 0; ++th; }
+        if (++tap == a.ntaps) {
+          tap = th = tw = 0;
+          c0 += BK;
+        } else if (++tw == a.tkw) {
+          tw = 0;
+          ++th;
         }
         if constexpr (GL)
           gload_lds(buf ^ 1, tap, a.dh0 + th * a.sdh, a.dw0 + tw * a.sdw, c0);
@@ -248,6 +251,7 @@ __global__ __launch_bounds__(256) void conv_reduce_k(const ConvArgs a) {
   const int sh = po::input_shift(a) + (a.prec == 1 ? a.w_shift : 0);
   const int m = (int)(t / n4), n = (int)(t - (int64_t)m * n4) * 4;
   float my = 0.f, ms = 0.f, my2 = 0.f;
+  uint32_t nib = 0;
   if (live) {
     float4 v = *reinterpret_cast<const float4*>(a.ws + (size_t)m * a.N + n);
     for (int s = 1; s < a.ksplit; ++s) {
@@ -260,13 +264,18 @@ __global__ __launch_bounds__(256) void conv_reduce_k(const ConvArgs a) {
     const size_t o = ((size_t)(b * a.Hout + i * a.out_step + a.out_oy) * a.Wout + j * a.out_step + a.out_ox) *
                          a.Cout_p + n;
     float r[4] = {v.x, v.y, v.z, v.w};
+    const size_t wo = (o / a.Cout_p) * (size_t)(a.Cout_p >> 5) + (n >> 5);
+    const float4 g1 = a.mbits ? po::leaky_grad_bits(a.mbits[wo], n) : make_float4(0.f, 0.f, 0.f, 0.f);
+    const float4 g2 = a.m2bits ? po::leaky_grad_bits(a.m2bits[wo], n) : make_float4(0.f, 0.f, 0.f, 0.f);
+    const float g1v[4] = {g1.x, g1.y, g1.z, g1.w}, g2v[4] = {g2.x, g2.y, g2.z, g2.w};
 #pragma unroll
     for (int c = 0; c < 4; ++c) {
       float x = __builtin_ldexpf(r[c], -sh) + (a.bias ? a.bias[n + c] : 0.f);
       if (a.act) x = po::leaky(x);
       if (a.accumulate) x += a.y[o + c];
-      const float yv = a.mask ? x * po::leaky_grad(a.mask[o + c]) : x;
+      const float yv = a.mbits ? x * g1v[c] : (a.mask ? x * po::leaky_grad(a.mask[o + c]) : x);
       a.y[o + c] = yv;
+      nib |= (yv > 0.f ? 1u : 0u) << c;
       my = fmaxf(my, fabsf(yv));
       if (a.res) {
         const float sv = x + a.res[o + c];
@@ -274,10 +283,24 @@ __global__ __launch_bounds__(256) void conv_reduce_k(const ConvArgs a) {
         ms = fmaxf(ms, fabsf(sv));
       }
       if (a.y2) {
-        const float v2 = x * po::leaky_grad(a.mask2[o + c]);
+        const float v2 = x * (a.m2bits ? g2v[c] : po::leaky_grad(a.mask2[o + c]));
         a.y2[o + c] = v2;
         my2 = fmaxf(my2, fabsf(v2));
       }
+    }
+  }
+  if (a.ybits) {
+    // threads 8k .. 8k+7 hold the 32 channels of one sign-bit word (N % 32 == 0)
+    uint32_t w = nib << (4 * (threadIdx.x & 7));
+    w |= (uint32_t)__shfl_xor((int)w, 1);
+    w |= (uint32_t)__shfl_xor((int)w, 2);
+    w |= (uint32_t)__shfl_xor((int)w, 4);
+    if (live && (threadIdx.x & 7) == 0) {
+      const int HgWg = a.Hg * a.Wg;
+      const int b = m / HgWg, rem = m - b * HgWg;
+      const int i = rem / a.Wg, j = rem - i * a.Wg;
+      const size_t pix = (size_t)(b * a.Hout + i * a.out_step + a.out_oy) * a.Wout + j * a.out_step + a.out_ox;
+      a.ybits[pix * (a.Cout_p >> 5) + (n >> 5)] = w;
     }
   }
   if (a.y_amax) po::amax_commit(a.y_amax, my);
@@ -326,7 +349,9 @@ bool forced_tile(int& bm, int& bn, int& bk, int& gl) {
 // 1..10 stage through registers + ds_write; 11..20 are the same shapes staged
 // by LDS-DMA (buffer_load ... lds); 21..28 are the 8-accumulator (64x128 /
 // 128x64 per wave) shapes, register- then DMA-staged.  prec 1 (fp16x3,
-// conv_h3.hip): 29..45, register staging (the A tile is split on its way to LDS).
+// conv_h3.hip): 29..45 four-wave kernels with register staging (the A tile is
+// split on its way to LDS), 46..52 the LDS-DMA multi-stage kernel (the
+// "staging" column = 1; A is split as it is read from LDS).
 constexpr int kTiles[PO_CONV_NTILES][5] = {
     {128, 128, 16, 0, 0}, {128, 128, 32, 0, 0}, {64, 128, 16, 0, 0}, {64, 128, 32, 0, 0}, {128, 64, 16, 0, 0},
     {128, 64, 32, 0, 0},  {64, 64, 16, 0, 0},   {64, 64, 32, 0, 0},  {128, 32, 16, 0, 0}, {128, 32, 32, 0, 0},
@@ -337,7 +362,9 @@ constexpr int kTiles[PO_CONV_NTILES][5] = {
     {128, 128, 16, 0, 1}, {64, 128, 16, 0, 1},  {128, 64, 16, 0, 1},  {64, 64, 16, 0, 1},  {128, 32, 16, 0, 1},
     {128, 128, 32, 0, 1}, {64, 128, 32, 0, 1},  {128, 64, 32, 0, 1},  {64, 64, 32, 0, 1},  {128, 32, 32, 0, 1},
     {256, 128, 32, 0, 1}, {128, 256, 32, 0, 1},
-    {128, 128, 64, 0, 1}, {64, 128, 64, 0, 1},  {128, 64, 64, 0, 1},  {64, 64, 64, 0, 1},  {128, 32, 64, 0, 1}};
+    {128, 128, 64, 0, 1}, {64, 128, 64, 0, 1},  {128, 64, 64, 0, 1},  {64, 64, 64, 0, 1},  {128, 32, 64, 0, 1},
+    {128, 128, 32, 1, 1}, {128, 64, 32, 1, 1},  {64, 128, 32, 1, 1},  {64, 64, 32, 1, 1},  {256, 128, 32, 1, 1},
+    {128, 128, 16, 1, 1}, {256, 128, 16, 1, 1}};
 }  // namespace
 
 extern "C" int po_conv_tile_info(int t, int* bm, int* bn, int* bk, int* prec) {
@@ -354,7 +381,11 @@ extern "C" int po_conv(const po_conv_desc* d, const float* in, const float* W, c
                        float* y2_out, const float* mask2, po_stream_t s) {
   PO_REQUIRE(d && in && W && y_out, "po_conv: null pointer");
   PO_REQUIRE((res == nullptr) == (sum_out == nullptr), "po_conv: res and sum_out must both be set or both NULL");
-  PO_REQUIRE((y2_out == nullptr) == (mask2 == nullptr), "po_conv: y2_out and mask2 must both be set or both NULL");
+  PO_REQUIRE((y2_out == nullptr) == (mask2 == nullptr && d->m2bits == nullptr),
+             "po_conv: y2_out needs mask2 or m2bits (and neither without y2_out)");
+  PO_REQUIRE(!(mask_y && d->mbits) && !(mask2 && d->m2bits), "po_conv: give a mask as floats or as bits, not both");
+  PO_REQUIRE(!(d->ybits || d->mbits || d->m2bits) || (d->N % 32 == 0 && d->Cout_p % 32 == 0),
+             "po_conv: sign-bit masks need N and Cout_p multiples of 32 (N=%d Cout_p=%d)", d->N, d->Cout_p);
   PO_REQUIRE(d->Cin_p % 16 == 0 && d->Cin_p > 0, "po_conv: Cin_p=%d must be a positive multiple of 16", d->Cin_p);
   PO_REQUIRE(d->N > 0 && d->N % 16 == 0 && d->N <= d->Cout_p, "po_conv: N=%d must be a multiple of 16 <= Cout_p=%d", d->N, d->Cout_p);
   PO_REQUIRE(d->ntaps >= 1 && d->ntaps <= 9, "po_conv: ntaps=%d", d->ntaps);
@@ -372,6 +403,9 @@ extern "C" int po_conv(const po_conv_desc* d, const float* in, const float* W, c
   a.y_amax = d->y_amax;
   a.sum_amax = d->sum_amax;
   a.y2_amax = d->y2_amax;
+  a.ybits = d->ybits;
+  a.mbits = d->mbits;
+  a.m2bits = d->m2bits;
   PO_REQUIRE(a.prec == 0 || a.prec == 1, "po_conv: prec %d", a.prec);
   PO_REQUIRE(a.prec == 0 || a.in_amax, "po_conv: prec 1 needs the input's max|x| slot (in_amax)");
   PO_REQUIRE(!sum_out || !a.sum_amax || a.sum_amax != a.y_amax, "po_conv: y and sum share an amax slot");
@@ -436,7 +470,7 @@ extern "C" int po_conv(const po_conv_desc* d, const float* in, const float* W, c
   if (a.prec == 1) {
     ConvArgs b = a;
     b.ntiles_n = po::ceil_div(a.N, bn);
-    rc = po::launch_h3(b, st, bm, bn, bk);
+    rc = po::launch_h3(b, st, bm, bn, bk, gl);
     if (rc == PO_OK && a.ksplit > 1) {
       hipLaunchKernelGGL(conv_reduce_k, dim3(po::ceil_div((int64_t)a.M * (a.N / 4), 256)), dim3(256), 0, st, b);
       rc = po::check_launch("po_conv (split-K reduce)");

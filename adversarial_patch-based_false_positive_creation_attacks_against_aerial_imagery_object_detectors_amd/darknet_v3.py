@@ -246,6 +246,7 @@ class NetPlan:
         self._build_grad_plan()
         self.prec = 1 if net.conv_prec == "fp16x3" else 0
         self._build_slots()
+        self._build_bits()
         self._build_ops()
 
     # ---------------- receptive-field windows ----------------
@@ -464,6 +465,37 @@ class NetPlan:
         self._slot_idx = idx
         self.amax = torch.zeros(len(idx), nat.PO_AMAX_SUB, dtype=torch.int32, device=self.device)
 
+    def _build_bits(self):
+        """Sign bits of the leaky conv outputs that the backward uses as
+        LeakyReLU masks: written by the forward conv epilogue, read by the
+        dgrad epilogues instead of the fp32 activation (1/32 of the bytes).
+        Only po_conv outputs with a channel stride that is a multiple of 32."""
+        self.bits = {}
+        if os.environ.get("ADVPATCH_MASK_BITS", "1") == "0":
+            return
+        for i, d in enumerate(self.net.blocks):
+            if (d["type"] == "convolutional" and self.root[i] == i and self._leaky(i) and self.has_grad[i]
+                    and self.cp[i] % 32 == 0 and not (i == 0 and self.first_direct)):
+                self.bits[self.act[i].data_ptr()] = torch.zeros(self.B, self.dims[i][0], self.dims[i][1],
+                                                                self.cp[i] // 32, dtype=torch.int32,
+                                                                device=self.device)
+
+    def _img_ptr(self, t, b0):
+        """Pointer to image b0 of a [B, ...] tensor (or to a bits tensor given by
+        its address: the bits of the activation it belongs to)."""
+        if t is None:
+            return None
+        if isinstance(t, int):
+            bt = next(b for b in self.bits.values() if b.data_ptr() == t)
+            return nat.c_void_p(t + b0 * bt[0].numel() * bt.element_size())
+        return nat.c_void_p(t.data_ptr() + b0 * t[0].numel() * t.element_size())
+
+    def bits_of(self, t):
+        """Device address of the sign-bit copy of activation t (None if it has none)."""
+        if t is None or t.data_ptr() not in self.bits:
+            return None
+        return self.bits[t.data_ptr()].data_ptr()
+
     def slot(self, t):
         """Device address of tensor t's max|x| slot (None for None)."""
         if t is None:
@@ -535,6 +567,7 @@ class NetPlan:
                 desc.in_amax = self.slot(inp).value if src != INPUT else None
                 desc.y_amax = self.slot(y_out).value
                 desc.sum_amax = self.slot(sum_out).value if sum_out is not None else None
+                desc.ybits = self.bits_of(y_out)
                 args = (nat.ctypes.byref(desc), P(inp), P(wptr), P(wts["bias"]), P(y_out), P(res),
                         P(sum_out), None, None, None)
                 desc.macs = B * desc.Hg * desc.Wg * m["cout"] * m["cin"] * k * k      # logical channels
@@ -631,16 +664,22 @@ class NetPlan:
                         bwd.append(("po_conv_first_dgrad", (P(G), B, self.H, self.W, m["stride"], P(wts["w27"]),
                                                             m["cout"], self.cp[j], "roi", "dimg"), None))
                     else:
-                        for desc, wd in self._dgrad_descs(j, INPUT, 0, G, self.in_nhwc):
-                            bwd.append(("po_conv", (nat.ctypes.byref(desc), P(G), P(wd), None, P(self.in_nhwc), None,
+                        for desc, wd, b0 in self._dgrad_descs(j, INPUT, 0, G, self.in_nhwc):
+                            bwd.append(("po_conv", (nat.ctypes.byref(desc), self._img_ptr(G, b0), P(wd), None,
+                                                    self._img_ptr(self.in_nhwc, b0), None,
                                                     None, None, None, None), desc))
                         bwd.append(("po_nhwc_to_nchw", (P(self.in_nhwc), B, self.H, self.W, 3, 16, "dimg"), None))
                     continue
                 acc, mask, final = contrib(src)
                 y2, m2 = dual_of(src, final)
-                for desc, wd in self._dgrad_descs(j, src, acc, G, self.grad[src], y2):
-                    bwd.append(("po_conv", (nat.ctypes.byref(desc), P(G), P(wd), None, P(self.grad[src]), None, None,
-                                            P(mask), P(y2), P(m2)), desc))
+                for desc, wd, b0 in self._dgrad_descs(j, src, acc, G, self.grad[src], y2):
+                    Pb = lambda t: self._img_ptr(t, b0)
+                    mb, m2b = self._img_ptr(self.bits_of(mask), b0), self._img_ptr(self.bits_of(m2), b0)
+                    desc.mbits = mb.value if mb is not None else None
+                    desc.m2bits = m2b.value if m2b is not None else None
+                    bwd.append(("po_conv", (nat.ctypes.byref(desc), Pb(G), P(wd), None, Pb(self.grad[src]), None, None,
+                                            None if desc.mbits else Pb(mask), Pb(y2),
+                                            None if desc.m2bits else Pb(m2)), desc))
             elif t == "shortcut":
                 if j in self.sc_alias:
                     b, f = self.sc_alias[j]
@@ -727,34 +766,36 @@ class NetPlan:
             Hin, Win = (self.H, self.W) if src == INPUT else self.shp[src][:2]
         cin_p = 16 if src == INPUT else self.cp[src]
         out = []
-        for py in range(s):
-            for px in range(s):
-                Hg = (Hin - py + s - 1) // s
-                Wg = (Win - px + s - 1) // s
-                if Hg <= 0 or Wg <= 0:
-                    continue
-                taps = [(kh, kw) for kh in range(k) for kw in range(k)
-                        if (py + pad - kh) % s == 0 and (px + pad - kw) % s == 0]
-                desc = nat.po_conv_desc()
-                wd = self._conv_prec(desc, src, j, taps, cin_p)
-                desc.in_amax = self.slot(G).value
-                desc.y_amax = self.slot(dst).value
-                desc.y2_amax = self.slot(dst2).value if dst2 is not None else None
-                desc.B, desc.Hin, desc.Win, desc.Cin_p = self.B, self.dims[j][0], self.dims[j][1], self.cp[j]
-                desc.Hout, desc.Wout, desc.Cout_p = Hin, Win, cin_p
-                desc.in_org, desc.out_org = self._orgp(j), (self._orgp(src) if src != INPUT else None)
-                desc.Hg, desc.Wg = Hg, Wg
-                desc.in_step, desc.out_step, desc.out_oy, desc.out_ox = 1, s, py, px
-                desc.ntaps = len(taps)
-                for ti, (kh, kw) in enumerate(taps):
-                    desc.dh[ti] = (py + pad - kh) // s
-                    desc.dw[ti] = (px + pad - kw) // s
-                desc.N = cin_p
-                desc.act = 0
-                desc.accumulate = acc
-                desc.macs = self.B * Hg * Wg * m["cin"] * len(taps) * m["cout"]
-                desc.block, desc.kind = j, "dgrad"
-                out.append((desc, wd))
+        # one launch per parity class over the whole batch (image-range groups,
+        # ``groups``, measured no faster: the G re-reads hit the Infinity Cache)
+        groups = [(0, self.B)]
+        for (b0, nb), py, px in [(g, py, px) for g in groups for py in range(s) for px in range(s)]:
+            Hg = (Hin - py + s - 1) // s
+            Wg = (Win - px + s - 1) // s
+            if Hg <= 0 or Wg <= 0:
+                continue
+            taps = [(kh, kw) for kh in range(k) for kw in range(k)
+                    if (py + pad - kh) % s == 0 and (px + pad - kw) % s == 0]
+            desc = nat.po_conv_desc()
+            wd = self._conv_prec(desc, src, j, taps, cin_p)
+            desc.in_amax = self.slot(G).value
+            desc.y_amax = self.slot(dst).value
+            desc.y2_amax = self.slot(dst2).value if dst2 is not None else None
+            desc.B, desc.Hin, desc.Win, desc.Cin_p = nb, self.dims[j][0], self.dims[j][1], self.cp[j]
+            desc.Hout, desc.Wout, desc.Cout_p = Hin, Win, cin_p
+            desc.in_org, desc.out_org = self._orgp(j), (self._orgp(src) if src != INPUT else None)
+            desc.Hg, desc.Wg = Hg, Wg
+            desc.in_step, desc.out_step, desc.out_oy, desc.out_ox = 1, s, py, px
+            desc.ntaps = len(taps)
+            for ti, (kh, kw) in enumerate(taps):
+                desc.dh[ti] = (py + pad - kh) // s
+                desc.dw[ti] = (px + pad - kw) // s
+            desc.N = cin_p
+            desc.act = 0
+            desc.accumulate = acc
+            desc.macs = nb * Hg * Wg * m["cin"] * len(taps) * m["cout"]
+            desc.block, desc.kind = j, "dgrad"
+            out.append((desc, wd, b0))
         return out
 
     def conv_macs(self):
@@ -798,7 +839,8 @@ class NetPlan:
             if name != "po_conv":
                 continue
             key = (desc.B, desc.Hin, desc.Win, desc.Cin_p, desc.Hg, desc.Wg, desc.in_step, desc.ntaps, desc.N,
-                   desc.accumulate, args[6] is not None, args[7] is not None, args[8] is not None, desc.prec)
+                   desc.accumulate, args[6] is not None, args[7] is not None or bool(desc.mbits),
+                   args[8] is not None, desc.prec, bool(desc.ybits))
             if key in cache:
                 self._set_tile(desc, cache[key])
                 continue

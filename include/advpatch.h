@@ -189,9 +189,17 @@ typedef struct po_conv_desc {
   uint32_t* y_amax;
   uint32_t* sum_amax;
   uint32_t* y2_amax;
+  /* Leaky masks as sign bits ([pixel][Cout_p/32] uint32 words, bit c%32 of word
+   * c/32 = (value of channel c > 0); need N % 32 == 0 and Cout_p % 32 == 0).
+   * ybits: written with the signs of y_out (each launch writes whole words of
+   * the pixels/channels it computes).  mbits / m2bits (each may be NULL):
+   * replace mask_y / mask2 (leaky'(v) = bit ? 1 : 0.1), 1/32 of their bytes. */
+  uint32_t* ybits;
+  const uint32_t* mbits;
+  const uint32_t* m2bits;
 } po_conv_desc;
 
-#define PO_CONV_NTILES 45
+#define PO_CONV_NTILES 52
 /* Tile `t` (1-based): block rows BM (output pixels), block columns BN (output
  * channels), k-step BK (input channels).  Tiles 1..10 stage operands through
  * registers, 11..20 are the same shapes staged by LDS-DMA, 21..28 are

@@ -144,7 +144,7 @@ def test_plan_structure_yolov3_on_cpu_buffers():
     # every leaky conv with a gradient gets exactly one masked (final) contribution
     masked = {}
     for name, args, desc in plan.bwd_ops:
-        if name == "po_conv" and args[7] is not None:
+        if name == "po_conv" and (args[7] is not None or desc.mbits):
             masked[args[4].value] = masked.get(args[4].value, 0) + 1
     for i, d in enumerate(net.blocks):
         if d["type"] == "convolutional" and plan._leaky(i) and plan.has_grad[i] and i > 0:

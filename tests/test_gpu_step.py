@@ -159,3 +159,24 @@ def test_windowed_plan_matches_full_maps(tmp_path, cfg, B, P):
     torch.testing.assert_close(t1["obj"], t0["obj"], rtol=0, atol=1e-5)
     rel = float((g0 - g1).abs().max() / g0.abs().max())
     assert rel < 1e-4, rel
+
+
+@pytest.mark.parametrize("cfg,B,P", [("builtin:mini3", 4, 32), ("builtin:yolov3-dota", 2, 224)])
+def test_sign_bit_masks_match_fp32_masks(tmp_path, cfg, B, P, monkeypatch):
+    """The dgrad epilogues' LeakyReLU masks read as sign bits (NetPlan._build_bits)
+    select the same slopes as the fp32 activations: identical gradients."""
+    sy = pkg_mod("synthetic")
+    out = []
+    monkeypatch.setenv("ADVPATCH_TUNE", "0")          # same tiles (summation order) in both runs
+    for bits in ("1", "0"):
+        monkeypatch.setenv("ADVPATCH_MASK_BITS", bits)
+        tr, _ = _trainer(cfg, tmp_path)
+        S = tr.darknet_model.height
+        img, lab = sy.frames(B, S, seed=80).to(DEV), sy.labels(B, seed=81).to(DEV)
+        dr = {k: v.to(DEV) for k, v in sy.draws(B, P, seed=83).items()}
+        pg = sy.patch(P, seed=82).to(DEV).requires_grad_(True)
+        loss, terms = tr.losses(pg, img, lab, dr)
+        loss.backward()
+        assert bool(tr.last_plan.bits) == (bits == "1")
+        out.append(pg.grad.detach().clone())
+    assert torch.equal(out[0], out[1])

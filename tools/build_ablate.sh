@@ -1,0 +1,17 @@
+#!/bin/bash
+# Ablation builds of libadvpatch_hip.so into tools/bin/ (git-ignored):
+#   tools/build_ablate.sh TAG -DMACRO [...]  ->  tools/bin/libadvpatch_TAG.so
+set -e
+TAG=$1; shift
+ROOT=$(cd "$(dirname "$0")/.." && pwd)
+SRC=$ROOT/adversarial_patch-based_false_positive_creation_attacks_against_aerial_imagery_object_detectors_amd/csrc
+OUT=$ROOT/tools/bin
+TMP=$(mktemp -d)
+mkdir -p "$OUT"
+for f in patch_ops loss_ops conv_first conv_igemm conv_h3 net_ops; do
+  /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -fPIC -std=c++17 -munsafe-fp-atomics -Wno-inline-asm "$@" -c "$SRC/$f.hip" -o "$TMP/$f.o" &
+done
+wait
+/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o "$OUT/libadvpatch_$TAG.so" "$TMP"/*.o
+rm -rf "$TMP"
+echo "$OUT/libadvpatch_$TAG.so"

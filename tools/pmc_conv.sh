@@ -12,9 +12,9 @@ if [[ "$TILE" =~ ^[0-9]+$ ]]; then export MICRO_TILE=$TILE; else export ADVPATCH
 mkdir -p $OUT
 timeout -k 10 120 python tools/conv_micro.py $SHAPE > $OUT/plain.txt 2>&1
 i=0
-for grp in "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_MFMA SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_INSTS_SALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES" \
-           "SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_MFMA SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_VMEM GRBM_GUI_ACTIVE" \
-           "SQ_VALU_MFMA_BUSY_CYCLES SQ_LDS_BANK_CONFLICT SQ_WAIT_INST_LDS SQ_INST_CYCLES_VMEM_RD GRBM_COUNT"; do
+for grp in "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_MFMA SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_INSTS_SALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE" \
+           "SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_VMEM SQ_ACTIVE_INST_SCA SQ_WAIT_INST_LDS GRBM_COUNT" \
+           "SQ_VALU_MFMA_BUSY_CYCLES SQ_VALU_MFMA_COEXEC_CYCLES SQ_LDS_IDX_ACTIVE SQ_LDS_BANK_CONFLICT SQ_LDS_CMD_FIFO_FULL SQ_LDS_DATA_FIFO_FULL SQ_INST_LEVEL_VMEM SQ_THREAD_CYCLES_VALU TA_BUSY TA_ADDR_STALLED_BY_TC_CYCLES"; do
   i=$((i+1))
-  timeout -k 10 180 rocprofv3 --pmc $grp --kernel-include-regex 'conv_k|conv_h3_k' --output-format csv -d $OUT/p$i -o p$i -- python tools/conv_micro.py $SHAPE > $OUT/p$i.log 2>&1 || { echo "pass $i failed"; exit 1; }
+  timeout -k 10 180 rocprofv3 --pmc $grp --kernel-include-regex 'conv_' --output-format csv -d $OUT/p$i -o p$i -- python tools/conv_micro.py $SHAPE > $OUT/p$i.log 2>&1 || { echo "pass $i failed"; exit 1; }
 done

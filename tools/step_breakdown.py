@@ -64,3 +64,10 @@ for k, d in enumerate(descs):
     print("%-6s %5d %9d %5d %6d %4d %3d %9.1f %7.1f %6.2f" % (d.kind, d.block, M, d.N, K, d.tile, d.ksplit, ms[k] * 1e3,
                                                       2 * d.macs / (ms[k] * 1e-3) / 1e12, 100 * ms[k] / tot))
 print("total conv ms/step %.3f, launches %d, executed TFLOP/step %.3f" % (tot, n, 2 * sum(d.macs for d in descs) / 1e12))
+if os.environ.get("BREAKDOWN_JSON"):
+    import json
+    with open(os.environ["BREAKDOWN_JSON"], "w") as f:
+        json.dump({"steps": args.steps, "launches": [
+            {"kind": d.kind, "block": d.block, "M": d.B * d.Hg * d.Wg, "N": d.N, "K": d.ntaps * d.Cin_p,
+             "tile": d.tile, "ksplit": d.ksplit, "macs": d.macs, "us_events": ms[k] * 1e3}
+            for k, d in enumerate(descs)]}, f)
