@@ -821,6 +821,14 @@ class NetPlan:
         to (tile, ksplit) and is shared between plans."""
         lib = self.lib
         st = nat.stream()
+        convs = [(args, desc) for name, args, desc in self.fwd_ops + self.bwd_ops if name == "po_conv"]
+        if all(self._tune_key(args, desc) in cache for args, desc in convs):
+            for args, desc in convs:                 # every shape already tuned: no launches
+                self._set_tile(desc, cache[self._tune_key(args, desc)])
+            for args, desc in convs:
+                if desc.ksplit > 1:
+                    desc.workspace = self.ws.data_ptr()
+            return
         bufs = {id(t): t for t in self.act + self.grad if t is not None}
         if self.in_nhwc is not None:
             bufs[id(self.in_nhwc)] = self.in_nhwc
@@ -838,9 +846,7 @@ class NetPlan:
         for name, args, desc in self.fwd_ops + self.bwd_ops:
             if name != "po_conv":
                 continue
-            key = (desc.B, desc.Hin, desc.Win, desc.Cin_p, desc.Hg, desc.Wg, desc.in_step, desc.ntaps, desc.N,
-                   desc.accumulate, args[6] is not None, args[7] is not None or bool(desc.mbits),
-                   args[8] is not None, desc.prec, bool(desc.ybits))
+            key = self._tune_key(args, desc)
             if key in cache:
                 self._set_tile(desc, cache[key])
                 continue
@@ -879,6 +885,12 @@ class NetPlan:
                 t.zero_()
         self.amax.zero_()
         torch.cuda.synchronize()
+
+    @staticmethod
+    def _tune_key(args, desc):
+        return (desc.B, desc.Hin, desc.Win, desc.Cin_p, desc.Hg, desc.Wg, desc.in_step, desc.ntaps, desc.N,
+                desc.accumulate, args[6] is not None, args[7] is not None or bool(desc.mbits),
+                args[8] is not None, desc.prec, bool(desc.ybits))
 
     def _set_tile(self, desc, choice):
         t, ks = (choice, 1) if isinstance(choice, int) else choice

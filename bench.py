@@ -25,7 +25,11 @@ sys.path.insert(0, ROOT)
 import __graft_entry__ as ge  # noqa: E402
 
 PEAK_FP32_MFMA_TFLOPS = 157.3   # MI355X dense fp32 matrix peak (MI355X_MICROARCH.md)
+PEAK_FP16_MFMA_TFLOPS = 2500.0  # MI355X dense fp16/bf16 matrix peak (no sparsity)
 PEAK_HBM_GBS = 8000.0
+# fp32-equivalent peak of each conv operand precision: exact fp32 MFMA, or
+# fp16x3 (three fp16 MFMA products per fp32 product)
+PEAK_CONV = {"fp32": PEAK_FP32_MFMA_TFLOPS, "fp16x3": PEAK_FP16_MFMA_TFLOPS / 3.0}
 
 CONFIGS = {
     # name: (cfg, S, P, default per-GPU batch)
@@ -190,23 +194,29 @@ def main():
 
     if rank == 0:
         traffic = None
-        tfile = os.path.join(ROOT, "profiles", "traffic_%s_b%d.json" % (args.config, B))
+        prec = net.conv_prec
+        tfile = os.path.join(ROOT, "profiles", "traffic_%s_b%d_%s.json" % (args.config, B, prec))
         if os.path.exists(tfile):
             with open(tfile) as f:
-                traffic = json.load(f).get("hbm_bytes_per_step")
+                traffic = json.load(f).get("conv_hbm_bytes_per_step")
+        peak = PEAK_CONV[prec]
         line = {
             "metric": "patch-opt images/sec (608x608, YOLOv3-DOTA) at 1/2/4/8 MI355X" if args.config == "yolov3"
             else "patch-opt images/sec (416x416, YOLOv3-tiny-15)",
             "value": value, "unit": "images/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
             "ms_per_step": ms_per_step, "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
-            "dtype": "fp32", "data": "synthetic (seeded DOTA-shaped frames/labels, synthetic calibrated weights)",
+            "dtype": "fp32" if prec == "fp32" else "fp32 (fp16x3 split MFMA, fp32 accumulate)", "data": "synthetic (seeded DOTA-shaped frames/labels, synthetic calibrated weights)",
             "config": {"workload": "%s S=%d P=%d batch=%d per GPU, global %d" % (cfg, S, P, B, B * world),
                        "global_batch": B * world, "per_gpu_batch": B, "image_size": S, "patch_size": P,
                        "parallelism": "dp%d" % world},
-            "roofline": {"bound": "mfma", "kernel": "conv_k (po_conv implicit GEMM: every Darknet fwd + dgrad "
-                                                    "launch of a step)",
-                         "achieved": achieved, "peak": PEAK_FP32_MFMA_TFLOPS, "unit": "TFLOP/s",
-                         "frac": achieved / PEAK_FP32_MFMA_TFLOPS, "traffic": traffic,
+            "roofline": {"bound": "mfma", "kernel": "po_conv implicit GEMM (%s): every Darknet fwd + dgrad launch "
+                                                    "of a step" % ("conv_h3_k/conv_h3d_k, fp16x3" if prec == "fp16x3"
+                                                                   else "conv_k, fp32"),
+                         "achieved": achieved, "peak": peak, "unit": "TFLOP/s",
+                         "frac": achieved / peak, "traffic": traffic,
+                         "peak_note": "fp32-equivalent: fp16 dense 2500 / 3 products" if prec == "fp16x3"
+                                      else "fp32 dense MFMA",
+                         "frac_of_fp32_mfma_peak": achieved / PEAK_FP32_MFMA_TFLOPS,
                          "flops_per_step": conv_flops, "conv_ms_per_step": conv_ms,
                          "conv_launches_per_step": len(timer) // args.steps,
                          "reference_dense_flops_per_step": ref_flops_per_img * B,

@@ -11,7 +11,7 @@ KiB; on gfx950 FETCH_SIZE reports half the bytes of wide (16 B/lane)
 coalesced reads, which is what every hot kernel here issues, so
     hbm_bytes = (2 * FETCH_SIZE + WRITE_SIZE) * 1024.
 
-usage: python tools/pmc_summary.py OUTDIR ROUND CONFIG BATCH NSTEPS
+usage: python tools/pmc_summary.py OUTDIR ROUND CONFIG BATCH NSTEPS [PREC]
 """
 import csv
 import glob
@@ -41,6 +41,7 @@ def rows(pattern, d):
 
 def main():
     outdir, rnd, cfg, batch, nsteps = sys.argv[1], sys.argv[2], sys.argv[3], int(sys.argv[4]), int(sys.argv[5])
+    prec = sys.argv[6] if len(sys.argv) > 6 else "fp16x3"
     trace = rows("*kernel_trace.csv", os.path.join(outdir, "trace"))
     if not trace:
         raise SystemExit("no kernel trace under %s" % outdir)
@@ -93,12 +94,14 @@ def main():
                 lines += ["", "%s:" % f, "```", txt[-1], "```"]
     with open(os.path.join(pdir, "summary_%s.md" % tag), "w") as fh:
         fh.write("\n".join(lines) + "\n")
-    conv = table.get("conv_k", {})
-    with open(os.path.join(ROOT, "profiles", "traffic_%s.json" % tag), "w") as fh:
-        json.dump({"round": rnd, "kernel": "conv_k (all po_conv launches of one step)",
-                   "hbm_bytes_per_step": conv.get("hbm_bytes_per_step"),
-                   "conv_ms_per_step": conv.get("ms_per_step"),
-                   "conv_calls_per_step": conv.get("calls_per_step"),
+    conv = [table[k] for k in table if k in ("conv_k", "conv_h3_k", "conv_h3d_k", "conv_reduce_k")]
+    hb = [t["hbm_bytes_per_step"] for t in conv]
+    with open(os.path.join(ROOT, "profiles", "traffic_%s_%s.json" % (tag, prec)), "w") as fh:
+        json.dump({"round": rnd, "prec": prec,
+                   "kernel": "po_conv launches of one step (conv_k / conv_h3_k / conv_h3d_k + split-K reduce)",
+                   "conv_hbm_bytes_per_step": None if None in hb else sum(hb),
+                   "conv_ms_per_step": sum(t["ms_per_step"] for t in conv),
+                   "conv_calls_per_step": sum(t["calls_per_step"] for t in conv),
                    "families": table}, fh, indent=1)
     print("\n".join(lines))
 
