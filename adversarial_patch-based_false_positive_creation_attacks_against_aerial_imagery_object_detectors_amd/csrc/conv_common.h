@@ -196,7 +196,8 @@ __device__ __forceinline__ void conv_epilogue(const ConvArgs& a, const floatx16 
 
 // conv_h3.hip: launch of the split-precision kernel for tile (bm, bn, bk)
 // (the split-K reduction, when a.ksplit > 1, is launched by the caller)
-// (dma = 1: the LDS-DMA multi-stage kernel)
-int launch_h3(const ConvArgs& a, hipStream_t st, int bm, int bn, int bk, int dma);
+// (staging 1: the LDS-DMA multi-stage kernel; 2: the halo kernel for
+// stride-1 3x3 convs on full maps)
+int launch_h3(const ConvArgs& a, hipStream_t st, int bm, int bn, int bk, int staging);
 
 }  // namespace po

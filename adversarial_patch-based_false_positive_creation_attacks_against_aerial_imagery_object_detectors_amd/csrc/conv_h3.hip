@@ -485,6 +485,250 @@ int dispatch_dma(const ConvArgs& a, hipStream_t st, int bm, int bn, int bk) {
   return PO_EINVAL;
 }
 
+// Halo variant for stride-1 3x3 convolutions on full maps (the forward convs
+// and the stride-1 input-gradient convs of the big Darknet stages).  The A
+// rows of the nine taps of one channel chunk are the same input pixels
+// shifted by dh*W + dw (flat NHWC pixel index), so the chunk's input rows
+// [m0 - (W+1), m0 + BM + W + 1) are loaded and split ONCE into an LDS halo
+// image, and each tap reads its A fragments from it at a shifted row; a tap
+// that leaves the image reads a zero row.  Only the weights are staged per
+// k-step (register path, double buffered); the next chunk's halo rows are
+// loaded into registers while the current chunk's nine taps run.
+template <int BM, int BN, int WM, int WMAX>
+__global__ __launch_bounds__(256) void conv_h3h_k(const ConvArgs a) {
+  constexpr int BK = 16;
+  constexpr int WN = 4 / WM;
+  constexpr int TM = BM / WM / 32;
+  constexpr int TN = BN / WN / 32;
+  static_assert(TM >= 1 && TN >= 1, "tile too small for 4 waves of 32x32");
+  constexpr int CPR = BK / 8;                  // 16-byte chunks per LDS row
+  constexpr int SW = 3;                        // log2(rows per 256-byte bank line) for 32-byte rows
+  constexpr int HR = BM + 2 * (WMAX + 1);      // halo rows (largest W)
+  constexpr int HZ = HR;                       // the zero row
+  constexpr int H_HALFS = (HR + 1) * BK;       // one halo plane
+  constexpr int B_HALFS = BN * BK;
+  constexpr int HL = (HR * CPR + 255) / 256;   // halo chunk loads per thread
+  constexpr int BL = (BN * CPR + 255) / 256;   // weight chunk loads per thread (per plane)
+  constexpr int PF = 3;                        // weight k-steps in flight (register ring)
+  static_assert(9 % PF == 0, "ring slot of k-step 9c + t must not depend on c");
+  __shared__ __attribute__((aligned(16))) _Float16 smem_h[2 * H_HALFS + 4 * B_HALFS];
+  static_assert(sizeof(smem_h) >= 4 * 4096, "the epilogue needs 16 KB of LDS");
+  _Float16* Hs = smem_h;                       // [hi, lo][HR + 1][BK]
+  _Float16* Bs = smem_h + 2 * H_HALFS;         // [2 buffers][hi, lo][BN][BK]
+
+  const int wgid = po::xcd_remap();
+  const int tn = wgid % a.ntiles_n, tm = wgid / a.ntiles_n;
+  const int m0 = tm * BM, n0 = tn * BN;
+  const int tid = threadIdx.x & 255, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave / WN, wn = wave % WN;
+  const int W = a.Win, H = a.Hin;
+  const int sh_in = po::input_shift(a);
+  const float sc_in = __builtin_ldexpf(1.f, sh_in);
+  const uint32_t in_bytes = (uint32_t)__builtin_amdgcn_readfirstlane(a.in_bytes);
+  const uint32_t w_bytes = (uint32_t)__builtin_amdgcn_readfirstlane(a.w_bytes);
+  const __amdgpu_buffer_rsrc_t in_rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(a.in), 0, in_bytes, 0x00020000);
+  const __amdgpu_buffer_rsrc_t w_rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(a.W), 0, 2 * w_bytes, 0x00020000);
+  constexpr uint32_t kOOB = 0x80000000u;
+  const uint32_t pix_bytes = (uint32_t)a.Cin_p * 4u;
+  const uint32_t wpix_bytes = (uint32_t)a.Cin_p * 2u;
+  const int hrows = BM + 2 * (W + 1);          // halo rows of this launch
+  const int p_lo = m0 - (W + 1);               // flat input pixel of halo row 0
+
+  // halo loader: chunk load q = tid + 256 r -> halo row q / CPR, channel chunk q % CPR
+  uint32_t h_off[HL];
+#pragma unroll
+  for (int r = 0; r < HL; ++r) {
+    const int q = tid + 256 * r;
+    const int row = q / CPR, p = p_lo + row;
+    h_off[r] = (row < hrows && p >= 0 && p < a.M) ? (uint32_t)p * pix_bytes + (q % CPR) * 32u : kOOB;
+  }
+  const uint32_t wrow_bytes = (uint32_t)a.ntaps * wpix_bytes;
+  uint32_t b_off[BL];
+#pragma unroll
+  for (int r = 0; r < BL; ++r) {
+    const int q = tid + 256 * r;
+    const int row = q / CPR;
+    b_off[r] = (row < BN && n0 + row < a.N) ? (uint32_t)(n0 + row) * wrow_bytes + (q % CPR) * 16u : kOOB;
+  }
+  float4 rh[HL][2];
+  uint4 rbh[PF][BL], rbl[PF][BL];
+  auto load_halo = [&](int c0) {
+#pragma unroll
+    for (int r = 0; r < HL; ++r) {
+      const uint32_t o = h_off[r] + (h_off[r] == kOOB ? 0u : (uint32_t)c0 * 4u);
+      rh[r][0] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(in_rs, o, 0, 0));
+      rh[r][1] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(in_rs, o + 16u, 0, 0));
+    }
+  };
+  // weights of k-step (tap, c0) into ring slot `set` (past the end: out of range = zeros, never stored)
+  auto load_w = [&](int set, int tap, int c0, bool live) {
+    const uint32_t tb = (uint32_t)tap * wpix_bytes + (uint32_t)c0 * 2u;
+#pragma unroll
+    for (int r = 0; r < BL; ++r) {
+      const uint32_t o = live ? b_off[r] + tb : kOOB;
+      rbh[set][r] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(w_rs, o, 0, 0));
+      rbl[set][r] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(w_rs, o + w_bytes, 0, 0));
+    }
+  };
+  auto swz = [](int row, int chunk) { return (chunk ^ ((row >> SW) & (CPR - 1))) * 8; };
+  auto store_halo = [&]() {
+#pragma unroll
+    for (int r = 0; r < HL; ++r) {
+      const int q = tid + 256 * r;
+      const int row = q / CPR;
+      if (row < HR) {
+        uint4 hh, ll;
+        split8(rh[r][0], rh[r][1], sc_in, hh, ll);
+        _Float16* base = Hs + row * BK + swz(row, q % CPR);
+        *reinterpret_cast<uint4*>(base) = hh;
+        *reinterpret_cast<uint4*>(base + H_HALFS) = ll;
+      }
+    }
+  };
+  auto store_w = [&](int set, int buf) {
+#pragma unroll
+    for (int r = 0; r < BL; ++r) {
+      const int q = tid + 256 * r;
+      const int row = q / CPR;
+      if (row < BN) {
+        _Float16* base = Bs + (buf * 2) * B_HALFS + row * BK + swz(row, q % CPR);
+        *reinterpret_cast<uint4*>(base) = rbh[set][r];
+        *reinterpret_cast<uint4*>(base + B_HALFS) = rbl[set][r];
+      }
+    }
+  };
+
+  // per lane, fragment row i and tap t: the swizzled LDS offset of its halo
+  // row (the zero row when the tap leaves the image) — no address math in
+  // the k-loop
+  const int HW = H * W;
+  int aoff[TM][9];
+  const int h = lane >> 5;
+#pragma unroll
+  for (int i = 0; i < TM; ++i) {
+    const int r = wm * TM * 32 + i * 32 + (lane & 31);
+    const int m = m0 + r;
+    const int rem = m % HW;
+    const int y = m < a.M ? rem / W : -(1 << 20), x = rem % W;
+#pragma unroll
+    for (int t = 0; t < 9; ++t) {
+      const int dh = a.dh0 + (t / 3) * a.sdh, dw = a.dw0 + (t % 3) * a.sdw;
+      const bool ok = (unsigned)(y + dh) < (unsigned)H && (unsigned)(x + dw) < (unsigned)W;
+      const int row = ok ? r + W + 1 + dh * W + dw : HZ;
+      aoff[i][t] = row * BK + swz(row, h);
+    }
+  }
+  const int brow = wn * TN * 32 + (lane & 31);
+  int boff[TN];
+#pragma unroll
+  for (int j = 0; j < TN; ++j) boff[j] = (brow + j * 32) * BK + swz(brow + j * 32, h);
+
+  floatx16 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.f;
+
+  // k-steps: channel chunk c (16 channels) outside, tap 0..8 inside; this
+  // workgroup's split-K range is whole chunks [cb, ce)
+  const int nch = a.Cin_p / BK;
+  const int cb = (int)((int64_t)blockIdx.y * nch / a.ksplit);
+  const int ce = (int)((int64_t)(blockIdx.y + 1) * nch / a.ksplit);
+  if (tid < 2 * CPR) *reinterpret_cast<uint4*>(Hs + (tid / CPR) * H_HALFS + HZ * BK + (tid % CPR) * 8) = make_uint4(0, 0, 0, 0);
+  load_halo(cb * BK);
+#pragma unroll
+  for (int s = 0; s < PF; ++s) load_w(s, s, cb * BK, true);         // taps 0..PF-1 of the first chunk
+  store_halo();
+  store_w(0, 0);
+  __syncthreads();
+  for (int c = cb; c < ce; ++c) {
+    const int c0 = c * BK;
+    const bool next_chunk = c + 1 < ce;
+    if (next_chunk) load_halo(c0 + BK);
+#pragma unroll
+    for (int t = 0; t < 9; ++t) {
+      // global k-step g = 9c + t; B of step g is in ring slot g % PF (= t % PF: 9 % PF == 0),
+      // LDS buffer g & 1
+      const int buf = t & 1 ? (c & 1) ^ 1 : c & 1;      // (9c + t) & 1
+      const _Float16* Bb = Bs + buf * 2 * B_HALFS;
+      half8 ah[TM], al[TM], bh[TN], bl[TN];
+#pragma unroll
+      for (int i = 0; i < TM; ++i) {
+        ah[i] = *reinterpret_cast<const half8*>(Hs + aoff[i][t]);
+        al[i] = *reinterpret_cast<const half8*>(Hs + H_HALFS + aoff[i][t]);
+      }
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        bh[j] = *reinterpret_cast<const half8*>(Bb + boff[j]);
+        bl[j] = *reinterpret_cast<const half8*>(Bb + B_HALFS + boff[j]);
+      }
+      // refill the slot of step g with step g + PF
+      const int tp = t + PF;
+      const bool more_w = tp < 9 || next_chunk;
+      load_w(t % PF, tp < 9 ? tp : tp - 9, tp < 9 ? c0 : c0 + BK, more_w);     // (9c + t) % 3 = t % 3
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) {
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(al[i], bh[j], acc[i][j], 0, 0, 0);
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[i], bl[j], acc[i][j], 0, 0, 0);
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[i], bh[j], acc[i][j], 0, 0, 0);
+        }
+      const bool more = t < 8 || next_chunk;
+      if (more) {
+        store_w((t + 1) % PF, buf ^ 1);              // step g + 1, loaded PF - 1 steps ago
+        if (t == 8) {
+          __syncthreads();                         // every wave is done with this chunk's halo
+          store_halo();
+        }
+      }
+      __syncthreads();
+    }
+  }
+
+  if (a.ksplit > 1) {
+    po::store_partials<TM, TN>(a, acc, m0, n0, wm, wn, lane);
+    return;
+  }
+  __shared__ int dst_pix[BM];
+  po::conv_epilogue<BM, TM, TN>(a, acc, reinterpret_cast<float*>(smem_h), dst_pix, m0, n0, wm, wn,
+                                sh_in + a.w_shift);
+}
+
+template <int BM, int BN, int WM, int WMAX>
+int launch_halo(const ConvArgs& a, hipStream_t st) {
+  ConvArgs b = a;
+  b.ntiles_n = po::ceil_div(a.N, BN);
+  const int ntiles = po::ceil_div(a.M, BM) * b.ntiles_n;
+  hipLaunchKernelGGL((conv_h3h_k<BM, BN, WM, WMAX>), dim3(ntiles, a.ksplit), dim3(256), 0, st, b);
+  return po::check_launch("po_conv (fp16x3 halo)");
+}
+
+int dispatch_halo(const ConvArgs& a, hipStream_t st, int bm, int bn) {
+  // eligibility: stride-1 3x3 tap grid on a full map of equal input/output size
+  const bool grid3 = a.ntaps == 9 && a.tkw == 3 && (a.sdh == 1 || a.sdh == -1) && (a.sdw == 1 || a.sdw == -1) &&
+                     a.dh0 == -a.sdh && a.dw0 == -a.sdw;
+  if (!(grid3 && a.in_step == 1 && a.out_step == 1 && a.out_oy == 0 && a.out_ox == 0 && !a.in_org && !a.out_org &&
+        a.Hin == a.Hout && a.Win == a.Wout && a.Hg == a.Hin && a.Wg == a.Win && a.Cin_p % 16 == 0)) {
+    po::set_error("po_conv (fp16x3 halo): needs a stride-1 3x3 conv on a full map");
+    return PO_EINVAL;
+  }
+  if (a.Win <= 40) {
+    if (bm == 128 && bn == 128) return launch_halo<128, 128, 2, 40>(a, st);
+    if (bm == 128 && bn == 64) return launch_halo<128, 64, 4, 40>(a, st);
+  } else if (a.Win <= 160) {
+    if (bm == 128 && bn == 128) return launch_halo<128, 128, 2, 160>(a, st);
+    if (bm == 128 && bn == 64) return launch_halo<128, 64, 4, 160>(a, st);
+  } else {
+    po::set_error("po_conv (fp16x3 halo): map width %d > 160", a.Win);
+    return PO_EINVAL;
+  }
+  po::set_error("po_conv (fp16x3 halo): no %dx%d tile", bm, bn);
+  return PO_EINVAL;
+}
+
 template <int BM, int BN, int WM, int BK>
 int launch(const ConvArgs& a, hipStream_t st) {
   ConvArgs b = a;
@@ -511,8 +755,9 @@ int dispatch(const ConvArgs& a, hipStream_t st, int bm, int bn) {
 }  // namespace
 
 namespace po {
-int launch_h3(const ConvArgs& a, hipStream_t st, int bm, int bn, int bk, int dma) {
-  if (dma) return dispatch_dma(a, st, bm, bn, bk);
+int launch_h3(const ConvArgs& a, hipStream_t st, int bm, int bn, int bk, int staging) {
+  if (staging == 2) return dispatch_halo(a, st, bm, bn);
+  if (staging == 1) return dispatch_dma(a, st, bm, bn, bk);
   if (bk == 16) return dispatch<16>(a, st, bm, bn);
   if (bk == 32) return dispatch<32>(a, st, bm, bn);
   if (bk == 64) return dispatch<64>(a, st, bm, bn);

@@ -351,7 +351,8 @@ bool forced_tile(int& bm, int& bn, int& bk, int& gl) {
 // 128x64 per wave) shapes, register- then DMA-staged.  prec 1 (fp16x3,
 // conv_h3.hip): 29..45 four-wave kernels with register staging (the A tile is
 // split on its way to LDS), 46..52 the LDS-DMA multi-stage kernel (the
-// "staging" column = 1; A is split as it is read from LDS).
+// "staging" column = 1; A is split as it is read from LDS), 53..54 the halo
+// kernel (staging 2: stride-1 3x3 convs on full maps only).
 constexpr int kTiles[PO_CONV_NTILES][5] = {
     {128, 128, 16, 0, 0}, {128, 128, 32, 0, 0}, {64, 128, 16, 0, 0}, {64, 128, 32, 0, 0}, {128, 64, 16, 0, 0},
     {128, 64, 32, 0, 0},  {64, 64, 16, 0, 0},   {64, 64, 32, 0, 0},  {128, 32, 16, 0, 0}, {128, 32, 32, 0, 0},
@@ -364,7 +365,7 @@ constexpr int kTiles[PO_CONV_NTILES][5] = {
     {256, 128, 32, 0, 1}, {128, 256, 32, 0, 1},
     {128, 128, 64, 0, 1}, {64, 128, 64, 0, 1},  {128, 64, 64, 0, 1},  {64, 64, 64, 0, 1},  {128, 32, 64, 0, 1},
     {128, 128, 32, 1, 1}, {128, 64, 32, 1, 1},  {64, 128, 32, 1, 1},  {64, 64, 32, 1, 1},  {256, 128, 32, 1, 1},
-    {128, 128, 16, 1, 1}, {256, 128, 16, 1, 1}};
+    {128, 128, 16, 1, 1}, {256, 128, 16, 1, 1}, {128, 128, 16, 2, 1}, {128, 64, 16, 2, 1}};
 }  // namespace
 
 extern "C" int po_conv_tile_info(int t, int* bm, int* bn, int* bk, int* prec) {

@@ -865,7 +865,9 @@ class NetPlan:
                               and k * M * desc.N <= self.WS_FLOATS]
                 for ks in cands:
                     self._set_tile(desc, (t, ks))
-                    for _ in range(2):
+                    if lib.po_conv(*args, st) != 0:      # tile not applicable to this launch
+                        continue
+                    for _ in range(1):
                         lib.po_conv(*args, st)
                     e0.record()
                     for _ in range(iters):

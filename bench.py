@@ -221,7 +221,7 @@ def main():
                          "conv_launches_per_step": len(timer) // args.steps,
                          "reference_dense_flops_per_step": ref_flops_per_img * B,
                          "receptive_field_windows": bool(plan.windowed)},
-            "loss": float(terms["loss"]),
+            "loss": float(terms["loss"].detach()),
         }
         if world == 1 and not args.no_cpu_baseline:
             line["cpu_baseline"] = cpu_baseline(cfg, S, P)

@@ -176,10 +176,10 @@ def test_split_k_matches_single_pass(B, H, Cin, Cout, k, prec):
         assert _rel(y, outs[1]) < 1e-5, (ks, _rel(y, outs[1]))
 
 
-@pytest.mark.parametrize("tile", list(range(1, 53)))
+@pytest.mark.parametrize("tile", list(range(1, 55)))
 def test_every_conv_tile(tile):
     """Every po_conv tile (exact fp32: register-staged 1..10 and 21..24,
-    LDS-DMA-staged 11..20 and 25..28; fp16x3: 29..45, LDS-DMA 46..52) on a 3x3 conv with zero
+    LDS-DMA-staged 11..20 and 25..28; fp16x3: 29..45, LDS-DMA 46..52, halo 53..54) on a 3x3 conv with zero
     padding, a ragged pixel count and a ragged channel count, against a
     float64 torch conv2d."""
     import ctypes
