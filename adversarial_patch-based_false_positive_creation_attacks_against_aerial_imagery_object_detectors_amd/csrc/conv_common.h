@@ -156,7 +156,7 @@ __device__ __forceinline__ void conv_epilogue(const ConvArgs& a, const floatx16 
             out = make_float4(x[0] * leaky_grad(mk.x), x[1] * leaky_grad(mk.y), x[2] * leaky_grad(mk.z),
                               x[3] * leaky_grad(mk.w));
           }
-          *reinterpret_cast<float4*>(a.y + o) = out;
+          if (a.y) *reinterpret_cast<float4*>(a.y + o) = out;     // NULL: only signs/sum wanted
           nib = (out.x > 0.f ? 1u : 0u) | (out.y > 0.f ? 2u : 0u) | (out.z > 0.f ? 4u : 0u) | (out.w > 0.f ? 8u : 0u);
           my = fmaxf(my, fmaxf(fmaxf(fabsf(out.x), fabsf(out.y)), fmaxf(fabsf(out.z), fabsf(out.w))));
           if (a.res) {

@@ -649,9 +649,10 @@ __global__ __launch_bounds__(256) void conv_h3h_k(const ConvArgs a) {
     if (next_chunk) load_halo(c0 + BK);
 #pragma unroll
     for (int t = 0; t < 9; ++t) {
-      // global k-step g = 9c + t; B of step g is in ring slot g % PF (= t % PF: 9 % PF == 0),
-      // LDS buffer g & 1
-      const int buf = t & 1 ? (c & 1) ^ 1 : c & 1;      // (9c + t) & 1
+      // k-step g = 9(c - cb) + t of this split's range; B of step g is in ring
+      // slot g % PF (= t % PF: 9 % PF == 0), LDS buffer g & 1
+      const int cr = (c - cb) & 1;
+      const int buf = t & 1 ? cr ^ 1 : cr;               // (9(c - cb) + t) & 1
       const _Float16* Bb = Bs + buf * 2 * B_HALFS;
       half8 ah[TM], al[TM], bh[TN], bl[TN];
 #pragma unroll

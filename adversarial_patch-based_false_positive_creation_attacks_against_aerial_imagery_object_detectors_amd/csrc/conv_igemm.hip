@@ -274,7 +274,7 @@ __global__ __launch_bounds__(256) void conv_reduce_k(const ConvArgs a) {
       if (a.act) x = po::leaky(x);
       if (a.accumulate) x += a.y[o + c];
       const float yv = a.mbits ? x * g1v[c] : (a.mask ? x * po::leaky_grad(a.mask[o + c]) : x);
-      a.y[o + c] = yv;
+      if (a.y) a.y[o + c] = yv;
       nib |= (yv > 0.f ? 1u : 0u) << c;
       my = fmaxf(my, fabsf(yv));
       if (a.res) {
@@ -380,7 +380,11 @@ extern "C" int po_conv_tile_info(int t, int* bm, int* bn, int* bk, int* prec) {
 extern "C" int po_conv(const po_conv_desc* d, const float* in, const float* W, const float* bias,
                        float* y_out, const float* res, float* sum_out, const float* mask_y,
                        float* y2_out, const float* mask2, po_stream_t s) {
-  PO_REQUIRE(d && in && W && y_out, "po_conv: null pointer");
+  PO_REQUIRE(d && in && W, "po_conv: null pointer");
+  // y_out may be NULL only when the launch still writes something: the shortcut
+  // sum or the sign bits (a forward activation used only as a LeakyReLU mask)
+  PO_REQUIRE(y_out || ((sum_out || d->ybits) && !d->accumulate && !mask_y && !d->mbits && !y2_out),
+             "po_conv: y_out may be NULL only for a plain forward conv that writes sum_out or ybits");
   PO_REQUIRE((res == nullptr) == (sum_out == nullptr), "po_conv: res and sum_out must both be set or both NULL");
   PO_REQUIRE((y2_out == nullptr) == (mask2 == nullptr && d->m2bits == nullptr),
              "po_conv: y2_out needs mask2 or m2bits (and neither without y2_out)");

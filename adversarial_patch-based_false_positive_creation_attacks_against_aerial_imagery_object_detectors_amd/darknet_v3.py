@@ -248,6 +248,7 @@ class NetPlan:
         self._build_slots()
         self._build_bits()
         self._build_ops()
+        self._drop_mask_only_outputs()
 
     # ---------------- receptive-field windows ----------------
     def _cone(self, seed):
@@ -489,6 +490,40 @@ class NetPlan:
             bt = next(b for b in self.bits.values() if b.data_ptr() == t)
             return nat.c_void_p(t + b0 * bt[0].numel() * bt.element_size())
         return nat.c_void_p(t.data_ptr() + b0 * t[0].numel() * t.element_size())
+
+    def _drop_mask_only_outputs(self):
+        """A conv output whose fp32 values no launch reads — the activation
+        before a fused shortcut, which the backward uses only as a LeakyReLU
+        mask and takes from its sign bits — is not stored: the forward
+        epilogue writes only its signs and the shortcut sum
+        (ADVPATCH_DROP_MASK_ONLY=0 keeps every output)."""
+        self.y_dropped = set()
+        if os.environ.get("ADVPATCH_DROP_MASK_ONLY", "1") == "0":
+            return
+        used = {self.act[h].data_ptr() for h in self.heads}
+        for name, args, desc in self.fwd_ops + self.bwd_ops:
+            for pos, v in enumerate(args):
+                if name == "po_conv" and pos == 4 and desc.kind == "fwd":
+                    continue                          # a forward conv's own output
+                if isinstance(v, nat.c_void_p) and v.value:
+                    used.add(v.value)
+        for k, (name, args, desc) in enumerate(self.fwd_ops):
+            if name != "po_conv" or args[6] is None or not desc.ybits or args[4].value in used:
+                continue
+            self.fwd_ops[k] = (name, args[:4] + (None,) + args[5:], desc)
+            desc.y_amax = None
+            self.y_dropped.add(desc.block)
+
+    def leaky_signs(self, i):
+        """bool [B, h, w, C]: output of leaky conv i > 0 — from the fp32
+        activation, or from its sign bits when it is not stored."""
+        C = self.shp[i][2]
+        if i in self.y_dropped:
+            bits = self.bits[self.act[i].data_ptr()]
+            sh = torch.arange(32, device=bits.device, dtype=torch.int32)
+            b = (bits.unsqueeze(-1) >> sh) & 1
+            return b.reshape(*bits.shape[:3], -1)[..., :C].bool()
+        return self.act[i][..., :C] > 0
 
     def bits_of(self, t):
         """Device address of the sign-bit copy of activation t (None if it has none)."""

@@ -216,7 +216,10 @@ int po_conv_tile_info(int t, int* bm, int* bn, int* bk, int* prec);
  *                                      conv feeding a shortcut, taken from the
  *                                      completed shortcut gradient; y2_out and
  *                                      mask2 both NULL or both set)
- * All outputs share the destination layout (pixel-major, stride Cout_p). */
+ * All outputs share the destination layout (pixel-major, stride Cout_p).
+ * y_out may be NULL for a forward launch (no accumulate, mask_y, mbits or
+ * y2_out) that writes sum_out or ybits: an activation read only as a LeakyReLU
+ * mask need not be stored. */
 int po_conv(const po_conv_desc* d, const float* in, const float* W, const float* bias,
             float* y_out, const float* res, float* sum_out, const float* mask_y,
             float* y2_out, const float* mask2, po_stream_t s);

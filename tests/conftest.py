@@ -54,7 +54,7 @@ def plan_branches(plan):
     for i, d in enumerate(plan.net.blocks):
         C = plan.shp[i][2]
         if d["type"] == "convolutional" and plan._leaky(i):
-            pos = (plan.act[i][..., :C] > 0).permute(0, 3, 1, 2).cpu()
+            pos = plan.leaky_signs(i).permute(0, 3, 1, 2).cpu()
             if plan.win[i] is not None:
                 H, W = plan.shp[i][:2]
                 full = torch.full((plan.B, C, H, W), -1, dtype=torch.int8)

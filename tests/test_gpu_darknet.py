@@ -133,13 +133,16 @@ def _conv_operands(nat, wd, x, prec):
     return w16, shift, slot
 
 
-@pytest.mark.parametrize("prec", [0, 1])
+@pytest.mark.parametrize("prec,tile", [(0, 0), (1, 0), (1, 53), (1, 54)])
 @pytest.mark.parametrize("B,H,Cin,Cout,k", [(4, 5, 512, 1024, 3), (16, 1, 1024, 64, 1), (3, 7, 96, 128, 3)])
-def test_split_k_matches_single_pass(B, H, Cin, Cout, k, prec):
+def test_split_k_matches_single_pass(B, H, Cin, Cout, k, prec, tile):
     """po_conv with the k-steps split over workgroups (partials reduced in
     split order by the epilogue kernel) against one pass and torch conv2d,
-    for both operand precisions."""
+    for both operand precisions, with the default tile and with the halo
+    kernel's tiles (whose split ranges start on odd channel chunks)."""
     import ctypes
+    if tile and k != 3:
+        pytest.skip("the halo kernel takes 3x3 convs only")
     nat = pkg_mod("_native")
     pad = (k - 1) // 2
     gen = torch.Generator().manual_seed(11)
@@ -159,7 +162,7 @@ def test_split_k_matches_single_pass(B, H, Cin, Cout, k, prec):
         yslot = torch.zeros(64, dtype=torch.int32, device=DEV)
         d = nat.po_conv_desc()
         d.B, d.Hin, d.Win, d.Cin_p, d.Hout, d.Wout, d.Cout_p, d.Hg, d.Wg = B, H, H, Cin, H, H, Cout, H, H
-        d.in_step, d.out_step, d.ntaps, d.N, d.act = 1, 1, k * k, Cout, 1
+        d.in_step, d.out_step, d.ntaps, d.N, d.act, d.tile = 1, 1, k * k, Cout, 1, tile
         for kh in range(k):
             for kw in range(k):
                 d.dh[kh * k + kw], d.dw[kh * k + kw] = kh - pad, kw - pad

@@ -164,12 +164,15 @@ def test_windowed_plan_matches_full_maps(tmp_path, cfg, B, P):
 @pytest.mark.parametrize("cfg,B,P", [("builtin:mini3", 4, 32), ("builtin:yolov3-dota", 2, 224)])
 def test_sign_bit_masks_match_fp32_masks(tmp_path, cfg, B, P, monkeypatch):
     """The dgrad epilogues' LeakyReLU masks read as sign bits (NetPlan._build_bits)
-    select the same slopes as the fp32 activations: identical gradients."""
+    select the same slopes as the fp32 activations, and dropping the fp32 copy
+    of mask-only activations (NetPlan._drop_mask_only_outputs) changes
+    nothing: identical gradients."""
     sy = pkg_mod("synthetic")
     out = []
     monkeypatch.setenv("ADVPATCH_TUNE", "0")          # same tiles (summation order) in both runs
-    for bits in ("1", "0"):
+    for bits, drop in (("1", "1"), ("1", "0"), ("0", "1")):
         monkeypatch.setenv("ADVPATCH_MASK_BITS", bits)
+        monkeypatch.setenv("ADVPATCH_DROP_MASK_ONLY", drop)
         tr, _ = _trainer(cfg, tmp_path)
         S = tr.darknet_model.height
         img, lab = sy.frames(B, S, seed=80).to(DEV), sy.labels(B, seed=81).to(DEV)
@@ -177,6 +180,11 @@ def test_sign_bit_masks_match_fp32_masks(tmp_path, cfg, B, P, monkeypatch):
         pg = sy.patch(P, seed=82).to(DEV).requires_grad_(True)
         loss, terms = tr.losses(pg, img, lab, dr)
         loss.backward()
-        assert bool(tr.last_plan.bits) == (bits == "1")
+        plan = tr.last_plan
+        assert bool(plan.bits) == (bits == "1")
+        # activations before a fused shortcut are stored only as sign bits
+        assert bool(plan.y_dropped) == (bits == "1" and drop == "1" and bool(plan.fused))
+        for i in plan.y_dropped:
+            assert plan.leaky_signs(i).shape == (B,) + plan.dims[i] + (plan.shp[i][2],)
         out.append(pg.grad.detach().clone())
-    assert torch.equal(out[0], out[1])
+    assert torch.equal(out[0], out[1]) and torch.equal(out[0], out[2])
