@@ -26,7 +26,7 @@ class po_conv_desc(ctypes.Structure):
         ("in_org", c_void_p), ("out_org", c_void_p), ("ksplit", c_int), ("workspace", c_void_p),
         ("prec", c_int), ("w_shift", c_int), ("in_amax", c_void_p), ("y_amax", c_void_p),
         ("sum_amax", c_void_p), ("y2_amax", c_void_p), ("ybits", c_void_p), ("mbits", c_void_p),
-        ("m2bits", c_void_p)]
+        ("m2bits", c_void_p), ("gbox", c_void_p)]
 
 
 _SIGS = {
@@ -48,6 +48,7 @@ _SIGS = {
                      c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p],
     "po_cell_windows": [c_void_p, c_int, c_int, c_int, c_void_p, c_int, c_void_p, c_int, c_void_p, c_void_p,
                         c_void_p, c_void_p],
+    "po_grad_boxes": [c_void_p, c_int, c_int, c_void_p, c_int, c_int, c_void_p, c_void_p],
     "po_conv": [ctypes.POINTER(po_conv_desc), c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
                 c_void_p, c_void_p, c_void_p, c_void_p, c_void_p],
     "po_conv_tile_info": [c_int, ctypes.POINTER(c_int), ctypes.POINTER(c_int), ctypes.POINTER(c_int),

@@ -25,6 +25,8 @@ struct ConvArgs {
   const float* mask2;
   const int32_t* in_org;        // window origins [B,2] (NULL: full map)
   const int32_t* out_org;
+  const int32_t* gbox;          // optional per-image boxes [B][4] (r0, c0, r1, c1) of the destination:
+                                // only grid points whose output pixel lies in the box are computed
   float* ws;                    // split-K partials [ksplit][M][N] (ksplit > 1)
   const uint32_t* in_amax;      // prec 1: max|in| slot (float bits)
   uint32_t* y_amax;             // optional max|output| slots
@@ -53,6 +55,65 @@ __device__ __forceinline__ int input_shift(const ConvArgs& a) {
   const uint32_t bits = amax_read(a.in_amax);
   const int e = (int)((bits >> 23) & 0xff) - 127;      // amax in [2^e, 2^(e+1)) (normal)
   return min(max(13 - e, -120), 120);
+}
+
+// ---- launch-grid enumeration.  GEMM row m is image b = m / (Hg*Wg) and, in
+// that image, grid point l = m % (Hg*Wg): row-major over the whole Hg x Wg
+// grid, or (a.gbox set) row-major over the image's box only, the rows past the
+// box's area computing nothing.  Grid point (i, j) writes destination pixel
+// (i*out_step + out_oy, j*out_step + out_ox).
+struct GridBox {
+  int i0, j0, h, w;
+};
+// first i with i*step + off >= lo;  one past the last i < n with i*step + off < hi
+__device__ __forceinline__ int grid_lo(int lo, int off, int step) {
+  const int d = lo - off;
+  return d <= 0 ? 0 : (d + step - 1) / step;
+}
+__device__ __forceinline__ int grid_hi(int hi, int off, int step, int n) {
+  const int d = hi - 1 - off;
+  return d < 0 ? 0 : min(n, d / step + 1);
+}
+__device__ __forceinline__ GridBox grid_box(const ConvArgs& a, int b) {
+  const int4 bx = reinterpret_cast<const int4*>(a.gbox)[b];
+  const int i0 = grid_lo(bx.x, a.out_oy, a.out_step), i1 = grid_hi(bx.z, a.out_oy, a.out_step, a.Hg);
+  const int j0 = grid_lo(bx.y, a.out_ox, a.out_step), j1 = grid_hi(bx.w, a.out_ox, a.out_step, a.Wg);
+  return {i0, j0, max(i1 - i0, 0), max(j1 - j0, 0)};
+}
+// GEMM row m -> image b and grid point (i, j); false: the row computes nothing
+__device__ __forceinline__ bool grid_point(const ConvArgs& a, int m, int& b, int& i, int& j) {
+  const int HgWg = a.Hg * a.Wg;
+  if (m >= a.M) {
+    b = i = j = 0;
+    return false;
+  }
+  b = m / HgWg;
+  const int l = m - b * HgWg;
+  if (!a.gbox) {
+    i = l / a.Wg;
+    j = l - i * a.Wg;
+    return true;
+  }
+  const GridBox g = grid_box(a, b);
+  if (l >= g.h * g.w) {
+    i = j = 0;
+    return false;
+  }
+  const int q = l / g.w;
+  i = g.i0 + q;
+  j = g.j0 + (l - q * g.w);
+  return true;
+}
+// does the tile of GEMM rows [m0, m0 + rows) hold a row that computes something?
+__device__ __forceinline__ bool tile_live(const ConvArgs& a, int m0, int rows) {
+  if (!a.gbox) return true;
+  const int HgWg = a.Hg * a.Wg;
+  const int m1 = min(m0 + rows, a.M);
+  for (int b = m0 / HgWg; b * HgWg < m1; ++b) {
+    const GridBox g = grid_box(a, b);
+    if (max(m0 - b * HgWg, 0) < g.h * g.w) return true;
+  }
+  return false;
 }
 
 // XCD-aware bijective remap: consecutive logical tiles share an XCD's L2
@@ -99,16 +160,11 @@ __device__ __forceinline__ void conv_epilogue(const ConvArgs& a, const floatx16 
                                               int* dst_pix, int m0, int n0, int wm, int wn, int sh,
                                               bool active = true) {
   const int tid = threadIdx.x, lane = tid & 63, wave = (tid >> 6) & 3;
-  const int HgWg = a.Hg * a.Wg;
   if (tid < BM) {
-    const int m = m0 + tid;
-    int o = -1;
-    if (m < a.M) {
-      const int b = m / HgWg, rem = m - b * HgWg;
-      const int i = rem / a.Wg, j = rem - i * a.Wg;
-      o = (b * a.Hout + i * a.out_step + a.out_oy) * a.Wout + j * a.out_step + a.out_ox;
-    }
-    dst_pix[tid] = o;
+    int b, i, j;
+    dst_pix[tid] = grid_point(a, m0 + tid, b, i, j)
+                       ? (b * a.Hout + i * a.out_step + a.out_oy) * a.Wout + j * a.out_step + a.out_ox
+                       : -1;
   }
   __syncthreads();
   float* scr = smem + wave * 1024;

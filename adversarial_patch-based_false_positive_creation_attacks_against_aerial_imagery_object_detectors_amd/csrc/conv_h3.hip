@@ -102,9 +102,9 @@ __global__ __launch_bounds__(256) void conv_h3_k(const ConvArgs a) {
   const int wgid = po::xcd_remap();
   const int tn = wgid % a.ntiles_n, tm = wgid / a.ntiles_n;
   const int m0 = tm * BM, n0 = tn * BN;
+  if (!po::tile_live(a, m0, BM)) return;      // every row of the tile is outside its image's box
   const int tid = threadIdx.x & 255, lane = tid & 63, wave = tid >> 6;
   const int wm = wave / WN, wn = wave % WN;
-  const int HgWg = a.Hg * a.Wg;
   const int cth = tid % CPR, rth = tid / CPR;
   const int sh_in = po::input_shift(a);
   const float sc_in = __builtin_ldexpf(1.f, sh_in);
@@ -124,10 +124,9 @@ __global__ __launch_bounds__(256) void conv_h3_k(const ConvArgs a) {
   for (int r = 0; r < AL; ++r) {
     const int row = rth + RPP * r;
     const int m = m0 + row;
-    const bool ok = (row < BM) && (m < a.M);
-    const int mm = ok ? m : 0;
-    const int b = mm / HgWg, rem = mm - b * HgWg;
-    const int i = rem / a.Wg, j = rem - i * a.Wg;
+    int b = 0, i = 0, j = 0;
+    const bool ok = (row < BM) && po::grid_point(a, m, b, i, j);
+    if (!ok) b = 0;
     a_off[r] = ((uint32_t)b * a.Hin * a.Win) * pix_bytes + cth * 32u;
     int sy = 0, sx = 0;
     if (a.out_org) { sy += a.out_org[2 * b]; sx += a.out_org[2 * b + 1]; }
@@ -304,10 +303,10 @@ __global__ __launch_bounds__(256) void conv_h3d_k(const ConvArgs a) {
   const int wgid = po::xcd_remap();
   const int tn = wgid % a.ntiles_n, tm = wgid / a.ntiles_n;
   const int m0 = tm * BM, n0 = tn * BN;
+  if (!po::tile_live(a, m0, BM)) return;      // every row of the tile is outside its image's box
   const int tid = threadIdx.x & 255, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = wave / WN, wn = wave % WN;
-  const int HgWg = a.Hg * a.Wg;
   const int sh_in = po::input_shift(a);
   const float sc_in = __builtin_ldexpf(1.f, sh_in);
 
@@ -327,10 +326,9 @@ __global__ __launch_bounds__(256) void conv_h3d_k(const ConvArgs a) {
   for (int r = 0; r < PA; ++r) {
     const int row = (wave + 4 * r) * RPA + lane / CPA;
     const int m = m0 + row;
-    const bool ok = m < a.M;
-    const int mm = ok ? m : 0;
-    const int b = mm / HgWg, rem = mm - b * HgWg;
-    const int i = rem / a.Wg, j = rem - i * a.Wg;
+    int b = 0, i = 0, j = 0;
+    const bool ok = po::grid_point(a, m, b, i, j);
+    if (!ok) b = 0;
     const int chunk = (lane % CPA) ^ ((row >> SWA) & (CPA - 1));
     a_off[r] = ((uint32_t)b * a.Hin * a.Win) * pix_bytes + chunk * 16u;
     int sy = 0, sx = 0;
@@ -712,8 +710,9 @@ int dispatch_halo(const ConvArgs& a, hipStream_t st, int bm, int bn) {
   const bool grid3 = a.ntaps == 9 && a.tkw == 3 && (a.sdh == 1 || a.sdh == -1) && (a.sdw == 1 || a.sdw == -1) &&
                      a.dh0 == -a.sdh && a.dw0 == -a.sdw;
   if (!(grid3 && a.in_step == 1 && a.out_step == 1 && a.out_oy == 0 && a.out_ox == 0 && !a.in_org && !a.out_org &&
+        !a.gbox &&
         a.Hin == a.Hout && a.Win == a.Wout && a.Hg == a.Hin && a.Wg == a.Win && a.Cin_p % 16 == 0)) {
-    po::set_error("po_conv (fp16x3 halo): needs a stride-1 3x3 conv on a full map");
+    po::set_error("po_conv (fp16x3 halo): needs a stride-1 3x3 conv on a full map (no gbox)");
     return PO_EINVAL;
   }
   if (a.Win <= 40) {

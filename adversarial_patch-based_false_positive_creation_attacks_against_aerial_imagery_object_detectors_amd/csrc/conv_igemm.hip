@@ -46,10 +46,10 @@ __global__ __launch_bounds__(256) void conv_k(const ConvArgs a) {
   const int wgid = po::xcd_remap();
   const int tn = wgid % a.ntiles_n, tm = wgid / a.ntiles_n;
   const int m0 = tm * BM, n0 = tn * BN;
+  if (!po::tile_live(a, m0, BM)) return;      // every row of the tile is outside its image's box
 
   const int tid = threadIdx.x & 255, lane = tid & 63, wave = tid >> 6;   // mask: lets the compiler bound rows
   const int wm = wave / WN, wn = wave % WN;
-  const int HgWg = a.Hg * a.Wg;
   const int cth = tid % CPR, rth = tid / CPR;
 
   // ---- buffer resources over the input tensor and the weights: an offset at or
@@ -80,10 +80,9 @@ __global__ __launch_bounds__(256) void conv_k(const ConvArgs a) {
   for (int r = 0; r < PA; ++r) {
     const int row = a_row(r);
     const int m = m0 + row;
-    const bool ok = (row < BM) && (m < a.M);
-    const int mm = ok ? m : 0;
-    const int b = mm / HgWg, rem = mm - b * HgWg;
-    const int i = rem / a.Wg, j = rem - i * a.Wg;
+    int b = 0, i = 0, j = 0;
+    const bool ok = (row < BM) && po::grid_point(a, m, b, i, j);
+    if (!ok) b = 0;
     a_off[r] = ((uint32_t)b * a.Hin * a.Win) * pix_bytes + a_chunk(row) * 16u;
     // window buffers: shift from output-buffer to input-buffer coordinates
     int sy = 0, sx = 0;
@@ -246,10 +245,12 @@ __global__ __launch_bounds__(256) void conv_k(const ConvArgs a) {
 __global__ __launch_bounds__(256) void conv_reduce_k(const ConvArgs a) {
   const int64_t t0 = (int64_t)blockIdx.x * 256 + threadIdx.x;
   const int n4 = a.N / 4;
-  const bool live = t0 < (int64_t)a.M * n4;
-  const int64_t t = live ? t0 : 0;
+  const int64_t t = t0 < (int64_t)a.M * n4 ? t0 : 0;
   const int sh = po::input_shift(a) + (a.prec == 1 ? a.w_shift : 0);
   const int m = (int)(t / n4), n = (int)(t - (int64_t)m * n4) * 4;
+  int b, i, j;
+  const bool live = t0 < (int64_t)a.M * n4 && po::grid_point(a, m, b, i, j);
+  const size_t pix = live ? (size_t)(b * a.Hout + i * a.out_step + a.out_oy) * a.Wout + j * a.out_step + a.out_ox : 0;
   float my = 0.f, ms = 0.f, my2 = 0.f;
   uint32_t nib = 0;
   if (live) {
@@ -258,13 +259,9 @@ __global__ __launch_bounds__(256) void conv_reduce_k(const ConvArgs a) {
       const float4 p = *reinterpret_cast<const float4*>(a.ws + ((size_t)s * a.M + m) * a.N + n);
       v.x += p.x; v.y += p.y; v.z += p.z; v.w += p.w;
     }
-    const int HgWg = a.Hg * a.Wg;
-    const int b = m / HgWg, rem = m - b * HgWg;
-    const int i = rem / a.Wg, j = rem - i * a.Wg;
-    const size_t o = ((size_t)(b * a.Hout + i * a.out_step + a.out_oy) * a.Wout + j * a.out_step + a.out_ox) *
-                         a.Cout_p + n;
+    const size_t o = pix * a.Cout_p + n;
     float r[4] = {v.x, v.y, v.z, v.w};
-    const size_t wo = (o / a.Cout_p) * (size_t)(a.Cout_p >> 5) + (n >> 5);
+    const size_t wo = pix * (size_t)(a.Cout_p >> 5) + (n >> 5);
     const float4 g1 = a.mbits ? po::leaky_grad_bits(a.mbits[wo], n) : make_float4(0.f, 0.f, 0.f, 0.f);
     const float4 g2 = a.m2bits ? po::leaky_grad_bits(a.m2bits[wo], n) : make_float4(0.f, 0.f, 0.f, 0.f);
     const float g1v[4] = {g1.x, g1.y, g1.z, g1.w}, g2v[4] = {g2.x, g2.y, g2.z, g2.w};
@@ -295,13 +292,7 @@ __global__ __launch_bounds__(256) void conv_reduce_k(const ConvArgs a) {
     w |= (uint32_t)__shfl_xor((int)w, 1);
     w |= (uint32_t)__shfl_xor((int)w, 2);
     w |= (uint32_t)__shfl_xor((int)w, 4);
-    if (live && (threadIdx.x & 7) == 0) {
-      const int HgWg = a.Hg * a.Wg;
-      const int b = m / HgWg, rem = m - b * HgWg;
-      const int i = rem / a.Wg, j = rem - i * a.Wg;
-      const size_t pix = (size_t)(b * a.Hout + i * a.out_step + a.out_oy) * a.Wout + j * a.out_step + a.out_ox;
-      a.ybits[pix * (a.Cout_p >> 5) + (n >> 5)] = w;
-    }
+    if (live && (threadIdx.x & 7) == 0) a.ybits[pix * (a.Cout_p >> 5) + (n >> 5)] = w;
   }
   if (a.y_amax) po::amax_commit(a.y_amax, my);
   if (a.sum_amax) po::amax_commit(a.sum_amax, ms);
@@ -401,7 +392,8 @@ extern "C" int po_conv(const po_conv_desc* d, const float* in, const float* W, c
   ConvArgs a;
   a.in = in; a.W = W; a.bias = bias; a.y = y_out; a.res = res; a.sum = sum_out; a.mask = mask_y;
   a.y2 = y2_out; a.mask2 = mask2;
-  a.in_org = d->in_org; a.out_org = d->out_org;
+  a.in_org = d->in_org; a.out_org = d->out_org; a.gbox = d->gbox;
+  PO_REQUIRE(!d->gbox || !d->out_org, "po_conv: gbox needs a full-map destination (out_org NULL)");
   a.prec = d->prec;
   a.w_shift = d->w_shift;
   a.in_amax = d->in_amax;

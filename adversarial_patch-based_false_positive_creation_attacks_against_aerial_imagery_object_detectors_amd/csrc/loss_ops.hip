@@ -226,3 +226,65 @@ extern "C" int po_cell_windows(const float* center, int B, int S, int nheads, co
                      po::stream_of(s), a, center, lut, ext, org, flags);
   return po::check_launch("po_cell_windows");
 }
+
+// ---------------------------------------------------------------------------
+// Gradient cones: one thread per image walks the block program in order.
+namespace {
+__device__ __forceinline__ int fdiv(int a, int b) { return a >= 0 ? a / b : -((-a + b - 1) / b); }
+__device__ __forceinline__ int cdiv(int a, int b) { return -fdiv(-a, b); }
+
+// inclusive source interval [a, b] -> inclusive interval of the destination
+// pixels that read a source pixel in it
+__device__ __forceinline__ void cone_map(int kind, int k, int s, int pad, int a, int b, int& lo, int& hi) {
+  switch (kind) {
+    case 0: lo = cdiv(a + pad - k + 1, s); hi = fdiv(b + pad, s); break;   // out o reads [o*s - pad, o*s - pad + k)
+    case 2: lo = fdiv(a, 2); hi = fdiv(b, 2); break;
+    case 3: lo = a - 1; hi = b; break;
+    case 4: lo = 2 * a; hi = 2 * b + 1; break;
+    default: lo = a; hi = b; break;
+  }
+}
+
+__global__ __launch_bounds__(64) void grad_boxes_k(const int32_t* __restrict__ roi, int B, int S,
+                                                   const int32_t* __restrict__ prog, int nprog,
+                                                   int32_t* __restrict__ boxes) {
+  const int b = blockIdx.x * 64 + threadIdx.x;
+  if (b >= B) return;
+  for (int r = 0; r < nprog; ++r) {
+    int4* d = reinterpret_cast<int4*>(boxes) + (size_t)prog[8 * r] * B + b;
+    *d = make_int4(0, 0, 0, 0);
+  }
+  for (int r = 0; r < nprog; ++r) {
+    const int32_t* p = prog + 8 * r;
+    int sr0, sc0, sr1, sc1;                    // source box, half-open
+    if (p[1] < 0) {
+      if (roi) { sc0 = roi[4 * b]; sr0 = roi[4 * b + 1]; sc1 = roi[4 * b + 2]; sr1 = roi[4 * b + 3]; }
+      else { sr0 = sc0 = 0; sr1 = sc1 = S; }
+    } else {
+      const int4 v = reinterpret_cast<const int4*>(boxes)[(size_t)p[1] * B + b];
+      sr0 = v.x; sc0 = v.y; sr1 = v.z; sc1 = v.w;
+    }
+    if (sr0 >= sr1 || sc0 >= sc1) continue;
+    int r0, r1, c0, c1;
+    cone_map(p[2], p[3], p[4], p[5], sr0, sr1 - 1, r0, r1);
+    cone_map(p[2], p[3], p[4], p[5], sc0, sc1 - 1, c0, c1);
+    r0 = max(r0, 0); c0 = max(c0, 0);
+    r1 = min(r1, p[6] - 1); c1 = min(c1, p[7] - 1);
+    if (r0 > r1 || c0 > c1) continue;
+    int4* d = reinterpret_cast<int4*>(boxes) + (size_t)p[0] * B + b;
+    int4 o = *d;
+    if (o.x >= o.z || o.y >= o.w) o = make_int4(r0, c0, r1 + 1, c1 + 1);
+    else o = make_int4(min(o.x, r0), min(o.y, c0), max(o.z, r1 + 1), max(o.w, c1 + 1));
+    *d = o;
+  }
+}
+}  // namespace
+
+extern "C" int po_grad_boxes(const int32_t* roi, int B, int S, const int32_t* prog, int nprog, int nbox,
+                             int32_t* boxes, po_stream_t s) {
+  PO_REQUIRE(prog && boxes, "po_grad_boxes: null pointer");
+  PO_REQUIRE(B >= 1 && S >= 1 && nprog >= 1 && nbox >= 1, "po_grad_boxes: bad sizes");
+  hipLaunchKernelGGL(grad_boxes_k, dim3(po::ceil_div(B, 64)), dim3(64), 0, po::stream_of(s), roi, B, S, prog, nprog,
+                     boxes);
+  return po::check_launch("po_grad_boxes");
+}

@@ -247,6 +247,7 @@ class NetPlan:
         self.prec = 1 if net.conv_prec == "fp16x3" else 0
         self._build_slots()
         self._build_bits()
+        self._build_cones()
         self._build_ops()
         self._drop_mask_only_outputs()
 
@@ -391,6 +392,113 @@ class NetPlan:
             return None
         win = [self.dims[self.root[h]][0] for h in self.heads]
         return win, [self.org_of(h) for h in self.heads]
+
+    # ---------------- gradient cones ----------------
+    CONE_MAX_FRAC = 0.6           # a block's gradient is boxed when its typical cone is smaller
+
+    def _cone_prog(self):
+        """Rows {dst, src, kind, k, stride, pad, Hdst, Wdst} of po_grad_boxes:
+        the forward influence of the input through every block, in order."""
+        rows = []
+        for j, d in enumerate(self.net.blocks):
+            if self.root[j] != j:
+                continue
+            t = d["type"]
+            H, W = self.shp[j][:2]
+            for s in self.srcs[j]:
+                src = -1 if s == INPUT else s
+                if t == "convolutional":
+                    m = self.net._conv_meta[j]
+                    rows.append((j, src, 0, m["k"], m["stride"], m["pad"], H, W))
+                elif t == "maxpool":
+                    rows.append((j, src, 2 if int(d["stride"]) == 2 else 3, 2, 0, 0, H, W))
+                elif t == "upsample":
+                    rows.append((j, src, 4, 0, 0, 0, H, W))
+                else:
+                    rows.append((j, src, 1, 0, 0, 0, H, W))
+        return rows
+
+    @staticmethod
+    def cone_boxes_host(prog, nbox, roi):
+        """Host restatement of po_grad_boxes for one image: roi (x0, y0, x1, y1)
+        -> {block: (r0, c0, r1, c1)} half-open (tests, planning)."""
+        def fdiv(a, b):
+            return a // b
+
+        def cmap(kind, k, s, pad, a, b):
+            if kind == 0:
+                return -fdiv(-(a + pad - k + 1), s), fdiv(b + pad, s)
+            if kind == 2:
+                return fdiv(a, 2), fdiv(b, 2)
+            if kind == 3:
+                return a - 1, b
+            if kind == 4:
+                return 2 * a, 2 * b + 1
+            return a, b
+
+        box = {}
+        for dst, src, kind, k, s, pad, H, W in prog:
+            box.setdefault(dst, (0, 0, 0, 0))
+        for dst, src, kind, k, s, pad, H, W in prog:
+            if src < 0:
+                r0, c0, r1, c1 = roi[1], roi[0], roi[3], roi[2]
+            else:
+                r0, c0, r1, c1 = box[src]
+            if r0 >= r1 or c0 >= c1:
+                continue
+            a0, a1 = cmap(kind, k, s, pad, r0, r1 - 1)
+            b0, b1 = cmap(kind, k, s, pad, c0, c1 - 1)
+            a0, b0, a1, b1 = max(a0, 0), max(b0, 0), min(a1, H - 1), min(b1, W - 1)
+            if a0 > a1 or b0 > b1:
+                continue
+            o = box[dst]
+            if o[0] >= o[2] or o[1] >= o[3]:
+                box[dst] = (a0, b0, a1 + 1, b1 + 1)
+            else:
+                box[dst] = (min(o[0], a0), min(o[1], b0), max(o[2], a1 + 1), max(o[3], b1 + 1))
+        return box
+
+    def _build_cones(self):
+        """Blocks whose input gradient is computed on the gradient cone only.
+
+        The patch gradient needs dL/d(image) only on the patch footprint (the
+        po_patch_params roi), so block j's gradient is only needed on the
+        pixels the footprint influences (po_grad_boxes).  A dgrad writing the
+        gradient of such a block gets the block's per-image box (po_conv
+        gbox).  Chosen when the cone of a centred S/3 footprint covers less
+        than CONE_MAX_FRAC of the map: the early high-resolution stages
+        (ADVPATCH_GRAD_CONES=0 disables)."""
+        self.cone_blocks = set()
+        self.cone_boxes = None
+        if os.environ.get("ADVPATCH_GRAD_CONES", "1") == "0" or self.H != self.W:
+            return
+        prog = self._cone_prog()
+        S = self.H
+        a = S // 3
+        est = self.cone_boxes_host(prog, self.n, (a, a, S - a, S - a))
+        for j, (r0, c0, r1, c1) in est.items():
+            H, W = self.shp[j][:2]
+            if (self.has_grad[j] and self.win[j] is None and self.grad[j] is not None
+                    and (r1 - r0) * (c1 - c0) < self.CONE_MAX_FRAC * H * W):
+                self.cone_blocks.add(j)
+        if not self.cone_blocks:
+            return
+        self.cone_prog = torch.tensor(prog, dtype=torch.int32, device=self.device).contiguous()
+        self.cone_boxes = torch.zeros(self.n, self.B, 4, dtype=torch.int32, device=self.device)
+
+    def set_cones(self, roi):
+        """Evaluate the gradient cones of roi [B,4] (None: the whole image)."""
+        if self.cone_boxes is None:
+            return
+        nat.call("po_grad_boxes", nat.c_void_p(roi.data_ptr()) if roi is not None else None, self.B, self.H,
+                 nat.c_void_p(self.cone_prog.data_ptr()), self.cone_prog.size(0), self.n,
+                 nat.c_void_p(self.cone_boxes.data_ptr()), nat.stream())
+
+    def _cone_ptr(self, s, b0):
+        """po_conv gbox of a dgrad writing block s's gradient (images from b0)."""
+        if s == INPUT or s not in self.cone_blocks:
+            return None
+        return self.cone_boxes[s, b0].data_ptr()
 
     # ---------------- gradient bookkeeping ----------------
     def _build_grad_plan(self):
@@ -709,6 +817,7 @@ class NetPlan:
                 y2, m2 = dual_of(src, final)
                 for desc, wd, b0 in self._dgrad_descs(j, src, acc, G, self.grad[src], y2):
                     Pb = lambda t: self._img_ptr(t, b0)
+                    desc.gbox = self._cone_ptr(src, b0)
                     mb, m2b = self._img_ptr(self.bits_of(mask), b0), self._img_ptr(self.bits_of(m2), b0)
                     desc.mbits = mb.value if mb is not None else None
                     desc.m2bits = m2b.value if m2b is not None else None
@@ -871,6 +980,10 @@ class NetPlan:
             for t in bufs.values():
                 t.uniform_(-1.0, 1.0)           # time on random data, not zeros (clock)
         self.amax.fill_(0x3F800000)             # max|x| = 1.0 for the U(-1,1) buffers
+        if self.cone_boxes is not None:         # boxed dgrads: time them on a centred S/3 footprint
+            a = self.H // 3
+            roi = torch.tensor([[a, a, self.H - a, self.H - a]] * self.B, dtype=torch.int32, device=self.device)
+            self.set_cones(roi)
         tiles = []
         for t in range(1, nat.PO_CONV_NTILES + 1):
             bm, bn, bk, pr = nat.c_int(), nat.c_int(), nat.c_int(), nat.c_int()
@@ -912,6 +1025,8 @@ class NetPlan:
                     ms = e0.elapsed_time(e1)
                     if best is None or ms < best[0]:
                         best = (ms, (t, ks))
+            if best is None:
+                raise RuntimeError("po_conv: no tile applies to launch %s (%s)" % (key, nat.last_error()))
             self._set_tile(desc, best[1])
             cache[key] = list(best[1])
         for name, _, desc in self.fwd_ops + self.bwd_ops:     # the workspace may have grown
@@ -927,7 +1042,7 @@ class NetPlan:
     def _tune_key(args, desc):
         return (desc.B, desc.Hin, desc.Win, desc.Cin_p, desc.Hg, desc.Wg, desc.in_step, desc.ntaps, desc.N,
                 desc.accumulate, args[6] is not None, args[7] is not None or bool(desc.mbits),
-                args[8] is not None, desc.prec, bool(desc.ybits))
+                args[8] is not None, desc.prec, bool(desc.ybits), bool(desc.gbox))
 
     def _set_tile(self, desc, choice):
         t, ks = (choice, 1) if isinstance(choice, int) else choice
@@ -983,6 +1098,7 @@ class NetPlan:
                      self.slot(self.grad[r]), st)
         dxp = nat.c_void_p(d_x.data_ptr())
         roip = nat.c_void_p(roi.data_ptr()) if roi is not None else None
+        self.set_cones(roi)
         for name, args, desc in self.bwd_ops:
             if args and args[-1] == "dimg":
                 if name == "po_conv_first_dgrad":

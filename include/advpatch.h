@@ -33,7 +33,7 @@ typedef void* po_stream_t;
 #define PO_EHIP -2     /* HIP runtime error */
 #define PO_EDEVICE -3  /* device is not gfx950 */
 
-#define PO_ABI_VERSION 5
+#define PO_ABI_VERSION 6
 #define PO_AMAX_SUB 64  /* sub-slots per max|x| slot (see po_conv_desc) */
 
 int po_abi_version(void);
@@ -137,6 +137,22 @@ int po_cell_windows(const float* center, int B, int S, int nheads, const int* hw
                     const int32_t* lut, int maxhw, const int32_t* ext, int32_t* org, int32_t* flags,
                     po_stream_t s);
 
+/* Gradient cones of the input-gradient path.  The patch gradient needs
+ * dL/d(image) only inside the patch footprint roi (po_patch_params), so the
+ * gradient of block j is only needed on the forward influence cone of roi at
+ * j: the pixels of j that depend on an roi pixel.  This evaluates that cone
+ * (a box per image and block) by interval arithmetic over `prog`, nprog rows
+ * of 8 int32 (DEVICE) {dst, src, kind, k, stride, pad, Hdst, Wdst}, in order
+ * (every dst index < nbox, a src's rows before any row reading it):
+ *   src -1 = roi; kind 0 conv (k, stride, pad), 1 identity (route/shortcut/
+ *   yolo), 2 maxpool size 2 stride 2, 3 maxpool size 2 stride 1 (window
+ *   [o, o+1]), 4 nearest 2x upsample.  Rows with the same dst are unioned.
+ * roi [B,4] {x0, y0, x1, y1} (NULL: the whole S x S image); boxes [nbox][B][4]
+ * int32 {r0, c0, r1, c1} half-open, clipped to [0,Hdst) x [0,Wdst); an empty
+ * cone is {0,0,0,0}.  Boxes of blocks no row writes are left untouched. */
+int po_grad_boxes(const int32_t* roi, int B, int S, const int32_t* prog, int nprog, int nbox, int32_t* boxes,
+                  po_stream_t s);
+
 /* ---------------- network ops (reference darknet_v3.py:37-100, 195-220) ---------------- */
 
 /* Tap list of an implicit-GEMM convolution launch.  For output pixel (b,i,j)
@@ -197,6 +213,12 @@ typedef struct po_conv_desc {
   uint32_t* ybits;
   const uint32_t* mbits;
   const uint32_t* m2bits;
+  /* Gradient cones (optional, DEVICE [B][4] int32 = {r0, c0, r1, c1} per image,
+   * half-open, destination-map coordinates; po_grad_boxes): only the grid
+   * points whose destination pixel lies in the image's box are computed, the
+   * rest of the destination is left untouched.  Needs a full-map destination
+   * (out_org = NULL). */
+  const int32_t* gbox;
 } po_conv_desc;
 
 #define PO_CONV_NTILES 54

@@ -1,0 +1,142 @@
+"""Gradient cones (po_grad_boxes + po_conv gbox): the patch gradient only needs
+dL/d(image) on the patch footprint, so the input-gradient convs of the early
+stages compute their output only on the footprint's forward influence cone.
+
+Checked here: the device cone evaluation against its host restatement
+(NetPlan.cone_boxes_host), a boxed po_conv against the unboxed launch (inside
+the box: identical values; outside: untouched), and a training step with
+cones against one without (the same forward; the patch gradient agrees to
+fp32 reassociation, the tiles being tuned per plan and launch kind)."""
+import ctypes
+
+import pytest
+import torch
+
+from conftest import pkg_mod
+
+pytestmark = pytest.mark.gpu
+DEV = torch.device("cuda", 0)
+
+
+def _conv(nat, x, wt, shift, slot, bias, dst, box, prec, tile, ks, geo):
+    """One po_conv launch; geo = (Hin, Hout, Hg, out_step, out_oy, out_ox)."""
+    B, Hin, _, Cin = x.shape
+    Cout = dst.shape[-1]
+    _, Hout, Hg, step, oy, ox = geo
+    d = nat.po_conv_desc()
+    d.B, d.Hin, d.Win, d.Cin_p, d.Hout, d.Wout, d.Cout_p, d.Hg, d.Wg = B, Hin, Hin, Cin, Hout, Hout, Cout, Hg, Hg
+    d.in_step, d.out_step, d.out_oy, d.out_ox, d.ntaps, d.N, d.act, d.tile = 1, step, oy, ox, 9, Cout, 1, tile
+    for kh in range(3):
+        for kw in range(3):
+            d.dh[kh * 3 + kw], d.dw[kh * 3 + kw] = kh - 1, kw - 1
+    ws = torch.empty(max(ks, 1) * B * Hg * Hg * Cout, device=DEV)
+    d.ksplit, d.workspace = ks, ws.data_ptr()
+    d.prec, d.w_shift = prec, shift
+    d.in_amax = slot.data_ptr() if slot is not None else None
+    d.gbox = box.data_ptr() if box is not None else None
+    nat.call("po_conv", ctypes.byref(d), nat.ptr(x), nat.ptr(wt, wt.dtype), nat.ptr(bias), nat.ptr(dst), None,
+             None, None, None, None, nat.stream())
+    torch.cuda.synchronize()
+
+
+@pytest.mark.parametrize("prec,tile", [(0, 1), (0, 11), (1, 34), (1, 46), (1, 29)])
+@pytest.mark.parametrize("ks", [1, 3])
+@pytest.mark.parametrize("geo", [(21, 21, 21, 1, 0, 0), (11, 22, 11, 2, 1, 0)])
+def test_boxed_conv_matches_full_launch(prec, tile, ks, geo):
+    from test_gpu_darknet import _conv_operands
+    nat = pkg_mod("_native")
+    B, Cin, Cout = 4, 64, 64
+    Hin, Hout = geo[0], geo[1]
+    gen = torch.Generator().manual_seed(5)
+    x = torch.randn(B, Hin, Hin, Cin, generator=gen)
+    w = torch.randn(Cout, 9, Cin, generator=gen) * (2.0 / (9 * Cin)) ** 0.5
+    bias = (torch.randn(Cout, generator=gen) * 0.1).to(DEV)
+    wt, shift, slot = _conv_operands(nat, w.to(DEV), x.permute(0, 3, 1, 2), prec)
+    xd = x.to(DEV)
+    # image 0: an inner box, 1: the whole map, 2: empty, 3: a box touching the corner
+    boxes = torch.tensor([[3, 5, 12, 17], [0, 0, Hout, Hout], [7, 7, 7, 9], [Hout - 4, 0, Hout, 6]],
+                         dtype=torch.int32)
+    full = torch.full((B, Hout, Hout, Cout), float("nan"), device=DEV)
+    boxed = torch.full_like(full, float("nan"))
+    _conv(nat, xd, wt, shift, slot, bias, full, None, prec, tile, ks, geo)
+    _conv(nat, xd, wt, shift, slot, bias, boxed, boxes.to(DEV), prec, tile, ks, geo)
+    full, boxed = full.cpu(), boxed.cpu()
+    inside = torch.zeros(B, Hout, Hout, dtype=torch.bool)
+    for b, (r0, c0, r1, c1) in enumerate(boxes.tolist()):
+        inside[b, r0:r1, c0:c1] = True
+    written = ~torch.isnan(full[..., 0])                 # the grid's destination pixels
+    assert torch.equal(boxed[inside & written], full[inside & written])
+    assert torch.isnan(boxed[~(inside & written)]).all()
+
+
+def test_grad_boxes_match_host_restatement(tmp_path):
+    from test_gpu_darknet import _net
+    net, _ = _net("builtin:yolov3-dota", tmp_path)
+    B, S = 5, 608
+    plan = net.plan(B, S, S, DEV)
+    assert plan.cone_blocks, "the 304/152/76 stages should be boxed"
+    gen = torch.Generator().manual_seed(3)
+    roi = []
+    for b in range(B):
+        x0, y0 = int(torch.randint(0, S - 8, (1,), generator=gen)), int(torch.randint(0, S - 8, (1,), generator=gen))
+        x1, y1 = x0 + int(torch.randint(1, S - x0 + 1, (1,), generator=gen)), \
+            y0 + int(torch.randint(1, S - y0 + 1, (1,), generator=gen))
+        roi.append([x0, y0, x1, y1])
+    roi[0] = [0, 0, S, S]
+    roi[1] = [300, 300, 301, 301]
+    plan.set_cones(torch.tensor(roi, dtype=torch.int32, device=DEV))
+    got = plan.cone_boxes.cpu()
+    prog = plan._cone_prog()
+    for b in range(B):
+        want = plan.cone_boxes_host(prog, plan.n, roi[b])
+        for j, box in want.items():
+            assert tuple(got[j, b].tolist()) == box, (b, j)
+    # the whole image as footprint: every cone is its full map
+    plan.set_cones(None)
+    for j in plan.cone_blocks:
+        H, W = plan.shp[j][:2]
+        assert plan.cone_boxes[j].cpu().tolist() == [[0, 0, H, W]] * B
+
+
+@pytest.mark.parametrize("prec", ["fp32", "fp16x3"])
+def test_cones_leave_the_patch_gradient_unchanged(tmp_path, monkeypatch, prec):
+    """With the built-in tile choice (no autotuning) the boxed dgrads run the
+    same tiles as the full ones: exact fp32 operands give the identical patch
+    gradient; fp16x3 differs only through the max|x| operand scales (a boxed
+    launch bounds the values it writes, a full one the whole map)."""
+    from test_gpu_step import _trainer
+    sy = pkg_mod("synthetic")
+    B, P = 3, 224
+    monkeypatch.setenv("ADVPATCH_TUNE", "0")
+    out = []
+    for cones in ("1", "0"):
+        monkeypatch.setenv("ADVPATCH_GRAD_CONES", cones)
+        tr, _ = _trainer("builtin:yolov3-dota", tmp_path, prec=prec)
+        img, lab = sy.frames(B, 608, seed=90).to(DEV), sy.labels(B, seed=91).to(DEV)
+        dr = {k: v.to(DEV) for k, v in sy.draws(B, P, seed=93).items()}
+        pg = sy.patch(P, seed=92).to(DEV).requires_grad_(True)
+        loss, terms = tr.losses(pg, img, lab, dr)
+        loss.backward()
+        assert bool(tr.last_plan.cone_blocks) == (cones == "1")
+        out.append((float(loss.detach()), terms["cells"].tolist(), pg.grad.detach().clone()))
+    (l1, c1, g1), (l0, c0, g0) = out
+    assert c1 == c0 and l1 == l0                  # the same forward
+    if prec == "fp32":
+        assert torch.equal(g1, g0)
+    else:
+        rel = float((g1 - g0).abs().max() / g0.abs().max())
+        assert rel < 1e-5, rel
+
+
+def test_halo_tiles_refuse_boxes():
+    """The halo kernel maps tile rows to contiguous pixels: a boxed launch
+    must be refused (the autotuner then skips it), not computed wrongly."""
+    from test_gpu_darknet import _conv_operands
+    nat = pkg_mod("_native")
+    x = torch.randn(2, 9, 9, 32, device=DEV)
+    w = torch.randn(32, 9, 32, device=DEV)
+    wt, shift, slot = _conv_operands(nat, w, x.permute(0, 3, 1, 2).cpu(), 1)
+    box = torch.tensor([[0, 0, 4, 4]] * 2, dtype=torch.int32, device=DEV)
+    y = torch.zeros(2, 9, 9, 32, device=DEV)
+    with pytest.raises(RuntimeError, match="halo"):
+        _conv(nat, x, wt, shift, slot, torch.zeros(32, device=DEV), y, box, 1, 53, 1, (9, 9, 9, 1, 0, 0))
