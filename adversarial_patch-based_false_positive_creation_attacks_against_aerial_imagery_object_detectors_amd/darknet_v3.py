@@ -164,7 +164,8 @@ class NetPlan:
     def __init__(self, net, B, H, W, device, windowed=False):
         self.net, self.B, self.H, self.W, self.device = net, B, H, W, device
         self.gen = 0
-        self.conv_timer = None        # list: (start, end, MACs) HIP events of every po_conv launch
+        self.conv_timer = None        # list: (start, end, desc, cones) of every po_conv launch (launch_macs)
+        self._cone_snap = None
         self.ws = None                # split-K workspace (shared by every launch; stream-ordered)
         blocks = net.blocks
         n = len(blocks)
@@ -394,7 +395,7 @@ class NetPlan:
         return win, [self.org_of(h) for h in self.heads]
 
     # ---------------- gradient cones ----------------
-    CONE_MAX_FRAC = 0.6           # a block's gradient is boxed when its typical cone is smaller
+    CONE_MAX_FRAC = 0.85          # a block's gradient is boxed when its typical cone is smaller
 
     def _cone_prog(self):
         """Rows {dst, src, kind, k, stride, pad, Hdst, Wdst} of po_grad_boxes:
@@ -476,10 +477,11 @@ class NetPlan:
         S = self.H
         a = S // 3
         est = self.cone_boxes_host(prog, self.n, (a, a, S - a, S - a))
+        frac = float(os.environ.get("ADVPATCH_CONE_MAX_FRAC", self.CONE_MAX_FRAC))
         for j, (r0, c0, r1, c1) in est.items():
             H, W = self.shp[j][:2]
             if (self.has_grad[j] and self.win[j] is None and self.grad[j] is not None
-                    and (r1 - r0) * (c1 - c0) < self.CONE_MAX_FRAC * H * W):
+                    and (r1 - r0) * (c1 - c0) < frac * H * W):
                 self.cone_blocks.add(j)
         if not self.cone_blocks:
             return
@@ -493,6 +495,24 @@ class NetPlan:
         nat.call("po_grad_boxes", nat.c_void_p(roi.data_ptr()) if roi is not None else None, self.B, self.H,
                  nat.c_void_p(self.cone_prog.data_ptr()), self.cone_prog.size(0), self.n,
                  nat.c_void_p(self.cone_boxes.data_ptr()), nat.stream())
+
+    @staticmethod
+    def launch_macs(desc, cones=None):
+        """MACs one po_conv launch computes: desc.macs for a full grid; for a
+        boxed launch (cones = the step's po_grad_boxes output) only its
+        per-image boxes' grid points, counted as the kernels enumerate them."""
+        if cones is None or not desc.gbox:
+            return desc.macs
+
+        def span(lo, hi, off, step, n):
+            a = 0 if lo - off <= 0 else -(-(lo - off) // step)
+            b = 0 if hi - 1 - off < 0 else min(n, (hi - 1 - off) // step + 1)
+            return max(b - a, 0)
+
+        bx = cones[desc.cone_block, desc.cone_b0:desc.cone_b0 + desc.B].cpu().tolist()
+        pts = sum(span(r0, r1, desc.out_oy, desc.out_step, desc.Hg) * span(c0, c1, desc.out_ox, desc.out_step, desc.Wg)
+                  for r0, c0, r1, c1 in bx)
+        return desc.macs * pts / (desc.B * desc.Hg * desc.Wg)
 
     def _cone_ptr(self, s, b0):
         """po_conv gbox of a dgrad writing block s's gradient (images from b0)."""
@@ -818,6 +838,7 @@ class NetPlan:
                 for desc, wd, b0 in self._dgrad_descs(j, src, acc, G, self.grad[src], y2):
                     Pb = lambda t: self._img_ptr(t, b0)
                     desc.gbox = self._cone_ptr(src, b0)
+                    desc.cone_block, desc.cone_b0 = src, b0
                     mb, m2b = self._img_ptr(self.bits_of(mask), b0), self._img_ptr(self.bits_of(m2), b0)
                     desc.mbits = mb.value if mb is not None else None
                     desc.m2bits = m2b.value if m2b is not None else None
@@ -1075,7 +1096,7 @@ class NetPlan:
             e0.record()
             rc = lib.po_conv(*args, st)
             e1.record()
-            timer.append((e0, e1, desc.macs))
+            timer.append((e0, e1, desc, self._cone_snap if desc.gbox else None))
         else:
             rc = getattr(lib, name)(*args, st)
         if rc:
@@ -1099,6 +1120,8 @@ class NetPlan:
         dxp = nat.c_void_p(d_x.data_ptr())
         roip = nat.c_void_p(roi.data_ptr()) if roi is not None else None
         self.set_cones(roi)
+        if self.conv_timer is not None and self.cone_boxes is not None:
+            self._cone_snap = self.cone_boxes.clone()        # this step's cones, for launch_macs
         for name, args, desc in self.bwd_ops:
             if args and args[-1] == "dimg":
                 if name == "po_conv_first_dgrad":

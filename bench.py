@@ -186,8 +186,9 @@ def main():
         torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
         elapsed = float(t)
     timer, plan.conv_timer = plan.conv_timer, None
-    conv_ms = sum(e0.elapsed_time(e1) for e0, e1, _ in timer) / args.steps
-    conv_flops = 2.0 * sum(m for _, _, m in timer) / args.steps
+    conv_ms = sum(e0.elapsed_time(e1) for e0, e1, _, _ in timer) / args.steps
+    # MACs actually computed: a boxed dgrad (gradient cones) counts its boxes only
+    conv_flops = 2.0 * sum(plan.launch_macs(d, c) for _, _, d, c in timer) / args.steps
     ms_per_step = elapsed * 1000.0 / args.steps
     value = world * B * args.steps / elapsed
     achieved = conv_flops / (conv_ms * 1e-3) / 1e12

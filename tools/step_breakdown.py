@@ -54,20 +54,23 @@ n = len(timer) // args.steps
 descs = [d for name, _, d in plan.fwd_ops + plan.bwd_ops if name == "po_conv"]
 assert len(descs) == n
 ms = defaultdict(float)
-for k, (e0, e1, _) in enumerate(timer):
+macs = defaultdict(float)
+for k, (e0, e1, d, c) in enumerate(timer):
     ms[k % n] += e0.elapsed_time(e1) / args.steps
+    macs[k % n] += plan.launch_macs(d, c) / args.steps
 tot = sum(ms.values())
 print("%-6s %5s %9s %5s %6s %4s %3s %9s %7s %6s" % ("kind", "block", "B*Hg*Wg", "N", "K", "tile", "ks", "us", "TF", "%"))
 for k, d in enumerate(descs):
     K = d.ntaps * d.Cin_p
     M = d.B * d.Hg * d.Wg
     print("%-6s %5d %9d %5d %6d %4d %3d %9.1f %7.1f %6.2f" % (d.kind, d.block, M, d.N, K, d.tile, d.ksplit, ms[k] * 1e3,
-                                                      2 * d.macs / (ms[k] * 1e-3) / 1e12, 100 * ms[k] / tot))
-print("total conv ms/step %.3f, launches %d, executed TFLOP/step %.3f" % (tot, n, 2 * sum(d.macs for d in descs) / 1e12))
+                                                      2 * macs[k] / (ms[k] * 1e-3) / 1e12, 100 * ms[k] / tot))
+print("total conv ms/step %.3f, launches %d, executed TFLOP/step %.3f" % (tot, n, 2 * sum(macs.values()) / 1e12))
 if os.environ.get("BREAKDOWN_JSON"):
     import json
     with open(os.environ["BREAKDOWN_JSON"], "w") as f:
         json.dump({"steps": args.steps, "launches": [
             {"kind": d.kind, "block": d.block, "M": d.B * d.Hg * d.Wg, "N": d.N, "K": d.ntaps * d.Cin_p,
-             "tile": d.tile, "ksplit": d.ksplit, "macs": d.macs, "us_events": ms[k] * 1e3}
+             "tile": d.tile, "ksplit": d.ksplit, "macs": macs[k], "boxed": bool(d.gbox),
+             "us_events": ms[k] * 1e3}
             for k, d in enumerate(descs)]}, f)
