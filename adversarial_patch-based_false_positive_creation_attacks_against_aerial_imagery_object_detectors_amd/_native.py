@@ -49,6 +49,10 @@ _SIGS = {
     "po_cell_windows": [c_void_p, c_int, c_int, c_int, c_void_p, c_int, c_void_p, c_int, c_void_p, c_void_p,
                         c_void_p, c_void_p],
     "po_grad_boxes": [c_void_p, c_int, c_int, c_void_p, c_int, c_int, c_void_p, c_void_p],
+    "po_max_prob": [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p, c_void_p,
+                    c_void_p],
+    "po_max_prob_bwd": [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p,
+                        c_void_p, c_void_p, c_void_p],
     "po_conv": [ctypes.POINTER(po_conv_desc), c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
                 c_void_p, c_void_p, c_void_p, c_void_p, c_void_p],
     "po_conv_tile_info": [c_int, ctypes.POINTER(c_int), ctypes.POINTER(c_int), ctypes.POINTER(c_int),

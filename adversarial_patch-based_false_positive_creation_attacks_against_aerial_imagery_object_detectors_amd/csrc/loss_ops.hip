@@ -228,6 +228,147 @@ extern "C" int po_cell_windows(const float* center, int B, int S, int nheads, co
 }
 
 // ---------------------------------------------------------------------------
+// MaxProbExtractor (load_data.py:125-311): per image, the max over every head,
+// anchor and cell of the objectness (field 4) and of the class-cls_id
+// confidence (field 5+cls_id), raw or after sigmoid.  bbox_decode
+// (load_data.py:63-122) rewrites only fields 0..3, so the maxima read the head
+// logits directly.  Flat index of the reference's output_cat [B,5+C,sum 3hw]:
+// head offset + a*h*w + (row*w + col) (load_data.py:188-198).
+// Grid (B, 2): blockIdx.y = 0 objectness, 1 class.  Each lane scans indices in
+// increasing order (strict > keeps the first), then wave shuffles and one LDS
+// pass merge (value, index) pairs with torch.max's rules: NaN wins, ties go to
+// the smaller index.
+namespace {
+struct MaxProbArgs {
+  const float* heads[MAXH];
+  float* dheads[MAXH];       // backward only
+  int64_t sb[MAXH];         // element strides: image, channel, pixel
+  int64_t sc[MAXH];
+  int64_t sp[MAXH];
+  int hw[MAXH];              // pixels per map (h*w)
+  int base[MAXH];            // flat index offset of the head
+  int nheads, nf, field_obj, field_cls, sigmoid_mode;
+};
+
+__device__ __forceinline__ bool mp_better(float v, int i, float bv, int bi) {
+  const bool vn = v != v, bn = bv != bv;
+  if (vn || bn) return vn && (!bn || i < bi);
+  return v > bv || (v == bv && i < bi);
+}
+
+__global__ __launch_bounds__(256) void max_prob_k(MaxProbArgs a, float* __restrict__ out, int32_t* __restrict__ idx,
+                                                  int B) {
+  const int b = blockIdx.x, q = blockIdx.y;
+  const int field = q == 0 ? a.field_obj : a.field_cls;
+  float best = -INFINITY;
+  int bi = 0x7fffffff;
+  for (int h = 0; h < a.nheads; ++h) {
+    const float* base = a.heads[h] + (int64_t)b * a.sb[h];
+    const int hw = a.hw[h];
+    for (int an = 0; an < 3; ++an) {
+      const float* ch = base + (int64_t)(an * a.nf + field) * a.sc[h];
+      for (int p = threadIdx.x; p < hw; p += 256) {
+        float v = ch[(int64_t)p * a.sp[h]];
+        if (a.sigmoid_mode) v = sigm(v);
+        const int i = a.base[h] + an * hw + p;
+        if (mp_better(v, i, best, bi)) { best = v; bi = i; }
+      }
+    }
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const float ov = __shfl_xor(best, o);
+    const int oi = __shfl_xor(bi, o);
+    if (mp_better(ov, oi, best, bi)) { best = ov; bi = oi; }
+  }
+  __shared__ float s_v[4];
+  __shared__ int s_i[4];
+  if ((threadIdx.x & 63) == 0) { s_v[threadIdx.x >> 6] = best; s_i[threadIdx.x >> 6] = bi; }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    for (int w = 1; w < 4; ++w)
+      if (mp_better(s_v[w], s_i[w], best, bi)) { best = s_v[w]; bi = s_i[w]; }
+    out[q * B + b] = best;
+    idx[q * B + b] = bi;
+  }
+}
+
+// backward: one thread per (image, quantity) adds g * d(value)/d(logit) at the
+// selected element (objectness and class fields never coincide)
+__global__ __launch_bounds__(64) void max_prob_bwd_k(MaxProbArgs a, const int32_t* __restrict__ idx,
+                                                     const float* __restrict__ g, int B) {
+  const int t = blockIdx.x * 64 + threadIdx.x;
+  if (t >= 2 * B) return;
+  const int q = t / B, b = t - q * B;
+  const int i = idx[t];
+  int h = 0;
+  while (h + 1 < a.nheads && i >= a.base[h + 1]) ++h;
+  const int loc = i - a.base[h], an = loc / a.hw[h], p = loc - an * a.hw[h];
+  const int64_t off = (int64_t)b * a.sb[h] + (int64_t)(an * a.nf + (q == 0 ? a.field_obj : a.field_cls)) * a.sc[h] +
+                      (int64_t)p * a.sp[h];
+  float d = g[t];
+  if (a.sigmoid_mode) {
+    const float s = sigm(a.heads[h][off]);
+    d *= s * (1.f - s);
+  }
+  a.dheads[h][off] += d;
+}
+
+int max_prob_args(MaxProbArgs& a, const float* const* heads, const int* h, const int* w, const int64_t* strides,
+                  int nheads, int num_cls, int cls_id, int sigmoid_mode) {
+  PO_REQUIRE(heads && h && w && strides, "po_max_prob: null pointer");
+  PO_REQUIRE(nheads >= 1 && nheads <= MAXH, "po_max_prob: 1..%d heads supported, got %d", MAXH, nheads);
+  PO_REQUIRE(num_cls >= 1 && cls_id >= 0 && cls_id < num_cls, "po_max_prob: cls_id %d of %d classes", cls_id,
+             num_cls);
+  int64_t base = 0;
+  for (int k = 0; k < MAXH; ++k) {
+    const bool on = k < nheads;
+    a.heads[k] = on ? heads[k] : nullptr;
+    a.dheads[k] = nullptr;
+    a.sb[k] = on ? strides[3 * k] : 0;
+    a.sc[k] = on ? strides[3 * k + 1] : 0;
+    a.sp[k] = on ? strides[3 * k + 2] : 0;
+    a.hw[k] = on ? h[k] * w[k] : 1;
+    a.base[k] = (int)base;
+    if (on) {
+      PO_REQUIRE(heads[k] && h[k] > 0 && w[k] > 0, "po_max_prob: bad head %d", k);
+      base += 3LL * h[k] * w[k];
+    }
+  }
+  PO_REQUIRE(base < (1LL << 31), "po_max_prob: %lld anchors overflow the int32 index", (long long)base);
+  a.nheads = nheads;
+  a.nf = 5 + num_cls;
+  a.field_obj = 4;
+  a.field_cls = 5 + cls_id;
+  a.sigmoid_mode = sigmoid_mode ? 1 : 0;
+  return PO_OK;
+}
+}  // namespace
+
+extern "C" int po_max_prob(const float* const* heads, const int* h, const int* w, const int64_t* strides, int nheads,
+                           int B, int num_cls, int cls_id, int sigmoid_mode, float* out, int32_t* idx, po_stream_t s) {
+  MaxProbArgs a;
+  if (int rc = max_prob_args(a, heads, h, w, strides, nheads, num_cls, cls_id, sigmoid_mode)) return rc;
+  PO_REQUIRE(out && idx && B >= 1 && B <= 65535, "po_max_prob: bad output or batch %d", B);
+  hipLaunchKernelGGL(max_prob_k, dim3(B, 2), dim3(256), 0, po::stream_of(s), a, out, idx, B);
+  return po::check_launch("po_max_prob");
+}
+
+extern "C" int po_max_prob_bwd(const float* const* heads, const int* h, const int* w, const int64_t* strides,
+                               int nheads, int B, int num_cls, int cls_id, int sigmoid_mode, const int32_t* idx,
+                               const float* g, float* const* d_heads, po_stream_t s) {
+  MaxProbArgs a;
+  if (int rc = max_prob_args(a, heads, h, w, strides, nheads, num_cls, cls_id, sigmoid_mode)) return rc;
+  PO_REQUIRE(idx && g && d_heads && B >= 1, "po_max_prob_bwd: null pointer");
+  for (int k = 0; k < nheads; ++k) {
+    PO_REQUIRE(d_heads[k], "po_max_prob_bwd: null gradient of head %d", k);
+    a.dheads[k] = d_heads[k];          // the pointer table travels by value in the kernel arguments
+  }
+  hipLaunchKernelGGL(max_prob_bwd_k, dim3(po::ceil_div(2 * B, 64)), dim3(64), 0, po::stream_of(s), a, idx, g, B);
+  return po::check_launch("po_max_prob_bwd");
+}
+
+// ---------------------------------------------------------------------------
 // Gradient cones: one thread per image walks the block program in order.
 namespace {
 __device__ __forceinline__ int fdiv(int a, int b) { return a >= 0 ? a / b : -((-a + b - 1) / b); }

@@ -28,6 +28,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from . import _native as nat
+from .max_prob import MaxProbExtractor  # noqa: F401  (load_data.py:125-311)
 from .median_pool import MedianPool2d
 from .printability import PRINTABLE_RGB_30
 from . import synthetic

@@ -123,6 +123,25 @@ int po_cell_loss(const float* const* heads, const int* hw, const int* win, const
                  const float* g2, float* const* d_heads, float* out2, float* obj_out, float* cls_out,
                  int32_t* cells, int32_t* flags, po_stream_t s);
 
+/* MaxProbExtractor.forward (load_data.py:125-311; bbox_decode 63-122 rewrites
+ * only the box fields, so it is not run): per image b, the max over every head
+ * h, anchor a (3 per head) and cell p of
+ *   q = 0: objectness logit (field 4),  q = 1: class cls_id logit (field 5+cls_id)
+ * (sigmoid of the logit when sigmoid_mode), field f of anchor a at channel
+ * a*(5+num_cls)+f.  Head h is h[h] x w[h] pixels at element strides
+ * strides[3h..3h+2] = {image, channel, pixel} (NCHW: {C*hw, hw, 1}; an NHWC
+ * buffer: {hw*Cp, 1, Cp}).  out [2][B] = maxima; idx [2][B] = flat index of
+ * the reference's output_cat [B,5+C,sum 3hw]: sum_{h'<h} 3hw' + a*hw + p.
+ * Ties: the first index (torch.max); NaN wins.  heads/h/w/strides are HOST arrays
+ * of nheads (<= 4) entries. */
+int po_max_prob(const float* const* heads, const int* h, const int* w, const int64_t* strides, int nheads, int B,
+                int num_cls, int cls_id, int sigmoid_mode, float* out, int32_t* idx, po_stream_t s);
+/* Its backward: d_heads[h] (same strides, caller-zeroed) += g[q][b] *
+ * d(value)/d(logit) at the element idx[q][b] selected (g: DEVICE [2][B]). */
+int po_max_prob_bwd(const float* const* heads, const int* h, const int* w, const int64_t* strides, int nheads,
+                    int B, int num_cls, int cls_id, int sigmoid_mode, const int32_t* idx, const float* g,
+                    float* const* d_heads, po_stream_t s);
+
 /* Receptive-field windows of the loss (SURVEY Q1 cells): the loss reads each
  * head at one cell per image, so every block downstream of the last
  * full-map block is only needed on a small box around that cell.  For window

@@ -26,7 +26,7 @@ __all__ = [
     "colorful_loss", "OracleDarknet", "read_darknet_weights", "obj_cls_conf_find",
     "no_obj_reshape", "no_cls_reshape", "noCLS_Loss_CE", "noCLS_loss_targeted",
     "train_step", "train_step_f64", "adam_amsgrad_steps", "patch_theta", "cell_indices", "TV_FACTOR", "NPS_FACTOR",
-    "TARGET_ID",
+    "TARGET_ID", "bbox_decode", "max_prob_extractor",
 ]
 
 # train_patch.py:25-28
@@ -462,6 +462,65 @@ def noCLS_loss_targeted(no_cls, cls_ID):                           # train_patch
         mx, _ = torch.max(no_cls[i, :, :], dim=1)
         batch_loss[i] = torch.mean(mx - t)
     return torch.sum(batch_loss)
+
+
+# --------------------------------------------------------------------------
+# load_data.py:63-122 bbox_decode, 125-311 MaxProbExtractor (constructed at
+# train_patch.py:74-75; its call at 255 is commented out in the reference)
+# --------------------------------------------------------------------------
+def bbox_decode(output, num_classes, anchors, num_anchors, img_size=(608, 608)):
+    """load_data.py:63-122 (CPU: the reference's .cuda() calls dropped)."""
+    batch, h, w = output.size(0), output.size(2), output.size(3)
+    stride_h = img_size[1] / h
+    stride_w = img_size[0] / w
+    scaled = [(aw / stride_w, ah / stride_h) for aw, ah in anchors]
+    output = output.view(batch * num_anchors, 5 + num_classes, h * w)
+    output = output.transpose(0, 1).contiguous()
+    output = output.view(5 + num_classes, batch * num_anchors * h * w)
+    grid_x = torch.linspace(0, w - 1, w).repeat(h, 1).repeat(batch * num_anchors, 1, 1).view(
+        batch * num_anchors * h * w)
+    grid_y = torch.linspace(0, h - 1, h).repeat(w, 1).t().repeat(batch * num_anchors, 1, 1).view(
+        batch * num_anchors * h * w)
+    xs = torch.sigmoid(output[0]) + grid_x
+    ys = torch.sigmoid(output[1]) + grid_y
+    anchor_w = torch.Tensor(scaled).index_select(1, torch.LongTensor([0]))
+    anchor_h = torch.Tensor(scaled).index_select(1, torch.LongTensor([1]))
+    anchor_w = anchor_w.repeat(batch, 1).repeat(1, 1, h * w).view(batch * num_anchors * h * w)
+    anchor_h = anchor_h.repeat(batch, 1).repeat(1, 1, h * w).view(batch * num_anchors * h * w)
+    ws = torch.exp(output[2]) * anchor_w
+    hs = torch.exp(output[3]) * anchor_h
+    output = output.clone()          # the reference writes rows 0..3 in place of a fresh copy
+    output[0] = xs / w
+    output[1] = ys / h
+    output[2] = ws / w
+    output[3] = hs / h
+    output = output.view(5 + num_classes, batch * num_anchors, h * w)
+    output = output.transpose(0, 1).contiguous()
+    return output.view(batch, num_anchors * (5 + num_classes), h, w)
+
+
+def max_prob_extractor(outputs, cls_id, num_cls, anchors_per_head, sigmoid_mode=False):
+    """MaxProbExtractor.forward (load_data.py:160-228, 311): decode every head,
+    concatenate to [B, 5+C, sum 3*h*w] (index = head offset + a*h*w + cell) and
+    take the per-image max of the objectness row and of row 5+cls_id, raw or
+    after sigmoid.  Returns (max_obj [B], max_cls [B], obj_idx [B], cls_idx [B])."""
+    singles = []
+    for i, output in enumerate(outputs):
+        batch, h, w = output.size(0), output.size(2), output.size(3)
+        output = bbox_decode(output, num_cls, anchors_per_head[i], 3)
+        output = output.view(batch, 3, 5 + num_cls, h * w)
+        output = output.transpose(1, 2).contiguous()
+        singles.append(output.view(batch, 5 + num_cls, 3 * h * w))
+    cat = torch.cat(singles, 2)
+    if sigmoid_mode:
+        obj = torch.sigmoid(cat[:, 4, :])
+        cls = torch.sigmoid(cat[:, 5:5 + num_cls, :])[:, cls_id, :]
+    else:
+        obj = cat[:, 4, :]
+        cls = cat[:, 5:5 + num_cls, :][:, cls_id, :]
+    max_cls, ci = torch.max(cls, dim=1)
+    max_obj, oi = torch.max(obj, dim=1)
+    return max_obj, max_cls, oi, ci
 
 
 # --------------------------------------------------------------------------

@@ -101,3 +101,20 @@ def test_lab_transform_q2_q3():
     lab[0, 1] = torch.tensor([5.0, 0.6, 0.8, 0.3, 0.2])
     sel = oracle.lab_transform(lab)
     torch.testing.assert_close(sel[0, 0], (lab[0, 1] + 1e-6) / 2)
+
+
+def test_max_prob_extractor_reads_the_logit_fields():
+    """MaxProbExtractor (load_data.py:125-311): bbox_decode rewrites fields 0..3
+    only, so the per-image maxima are the maxima of the raw field-4 and
+    field-(5+cls) logits over head-major, anchor-major, cell-minor indices."""
+    gen = torch.Generator().manual_seed(0)
+    heads = [torch.randn(2, 60, s, s, generator=gen) for s in (4, 8)]
+    anchors = [[(10, 13), (16, 30), (33, 23)], [(30, 61), (62, 45), (59, 119)]]
+    mo, mc, oi, ci = oracle.max_prob_extractor(heads, 7, 15, anchors)
+    flat_o = torch.cat([h.view(2, 3, 20, -1)[:, :, 4].reshape(2, -1) for h in heads], 1)
+    flat_c = torch.cat([h.view(2, 3, 20, -1)[:, :, 5 + 7].reshape(2, -1) for h in heads], 1)
+    assert torch.equal(mo, flat_o.max(1).values) and torch.equal(oi, flat_o.max(1).indices)
+    assert torch.equal(mc, flat_c.max(1).values) and torch.equal(ci, flat_c.max(1).indices)
+    so, sc, _, _ = oracle.max_prob_extractor(heads, 7, 15, anchors, sigmoid_mode=True)
+    torch.testing.assert_close(so, torch.sigmoid(mo), rtol=0, atol=0)
+    torch.testing.assert_close(sc, torch.sigmoid(mc), rtol=0, atol=0)
