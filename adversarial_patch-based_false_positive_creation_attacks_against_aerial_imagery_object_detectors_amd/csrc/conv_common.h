@@ -16,6 +16,7 @@ namespace po {
 struct ConvArgs {
   const float* in;
   const void* W;                // fp32 [N][ntaps][Cin_p]  or  fp16 [2][N][ntaps][Cin_p] (prec 1)
+  const void* Wf;               // optional (prec 1): the same fp16 weights in MFMA fragment order
   const float* bias;
   float* y;
   const float* res;
@@ -158,9 +159,9 @@ __device__ __forceinline__ float4 leaky_grad_bits(uint32_t w, int n) {
 template <int BM, int TM, int TN>
 __device__ __forceinline__ void conv_epilogue(const ConvArgs& a, const floatx16 (&acc)[TM][TN], float* smem,
                                               int* dst_pix, int m0, int n0, int wm, int wn, int sh,
-                                              bool active = true) {
+                                              bool active = true, bool fill_dst = true) {
   const int tid = threadIdx.x, lane = tid & 63, wave = (tid >> 6) & 3;
-  if (tid < BM) {
+  if (fill_dst && tid < BM) {     // else the caller has written dst_pix (2-D tiles)
     int b, i, j;
     dst_pix[tid] = grid_point(a, m0 + tid, b, i, j)
                        ? (b * a.Hout + i * a.out_step + a.out_oy) * a.Wout + j * a.out_step + a.out_ox
@@ -253,7 +254,9 @@ __device__ __forceinline__ void conv_epilogue(const ConvArgs& a, const floatx16 
 // conv_h3.hip: launch of the split-precision kernel for tile (bm, bn, bk)
 // (the split-K reduction, when a.ksplit > 1, is launched by the caller)
 // (staging 1: the LDS-DMA multi-stage kernel; 2: the halo kernel for
-// stride-1 3x3 convs on full maps)
+// stride-1 3x3 convs on full maps; 3: the 2-D tile halo kernel for stride-1/2
+// 3x3 convs on full maps; 4: the same with fragment-ordered weights read from
+// global memory)
 int launch_h3(const ConvArgs& a, hipStream_t st, int bm, int bn, int bk, int staging);
 
 }  // namespace po

@@ -7,6 +7,11 @@ namespace {
 // ------------------------------------------------------------------------
 // First layer: 3 input channels (NCHW image), 3x3, VALU direct convolution.
 // ------------------------------------------------------------------------
+// One thread per output pixel.  The weights are read with wave-uniform
+// indices straight from global memory, so they arrive through the scalar cache
+// as SGPR operands of the FMAs (no LDS broadcast reads); each thread's CO
+// outputs go to LDS and the workgroup then writes its 256 pixels x Cout_p
+// floats as one contiguous, fully coalesced 16-byte-per-lane stream.
 template <int CO>
 __global__ __launch_bounds__(256) void first_fwd_k(const float* __restrict__ img, int B, int H, int W,
                                                    int stride, int Ho, int Wo,
@@ -14,13 +19,12 @@ __global__ __launch_bounds__(256) void first_fwd_k(const float* __restrict__ img
                                                    const float* __restrict__ bias, int Cout,
                                                    int Cout_p, int act, float* __restrict__ y,
                                                    uint32_t* __restrict__ amax) {
-  __shared__ float ws[CO * 27];
-  __shared__ float bs[CO];
-  for (int t = threadIdx.x; t < CO * 27; t += 256) ws[t] = (t / 27) < Cout ? Wt[t] : 0.f;
-  for (int t = threadIdx.x; t < CO; t += 256) bs[t] = (t < Cout && bias) ? bias[t] : 0.f;
-  __syncthreads();
-  const int64_t p0 = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  const bool live = p0 < (int64_t)B * Ho * Wo;
+  constexpr int LS = CO + 1;                         // LDS row stride (bank-conflict-free column writes)
+  __shared__ float ys[256 * LS];
+  const int64_t npix = (int64_t)B * Ho * Wo;
+  const int64_t pbase = (int64_t)blockIdx.x * 256;
+  const int64_t p0 = pbase + threadIdx.x;
+  const bool live = p0 < npix;
   const int64_t p = live ? p0 : 0;
   const int b = (int)(p / ((int64_t)Ho * Wo));
   const int rem = (int)(p - (int64_t)b * Ho * Wo);
@@ -36,23 +40,29 @@ __global__ __launch_bounds__(256) void first_fwd_k(const float* __restrict__ img
         x[c * 9 + kh * 3 + kw] = (hi >= 0 && hi < H && wi >= 0 && wi < W)
                                      ? img[(((size_t)b * 3 + c) * H + hi) * W + wi] : 0.f;
       }
-  float* yp = y + (size_t)p * Cout_p;
   float vmax = 0.f;
 #pragma unroll
-  for (int co4 = 0; co4 < CO; co4 += 4) {
-    float v[4];
-#pragma unroll
-    for (int u = 0; u < 4; ++u) {
+  for (int co = 0; co < CO; ++co) {
+    float v = 0.f;
+    if (co < Cout) {                                 // wave-uniform
       float s = 0.f;
 #pragma unroll
-      for (int k = 0; k < 27; ++k) s += ws[(co4 + u) * 27 + k] * x[k];
-      s += bs[co4 + u];
-      v[u] = act ? po::leaky(s) : s;
-      vmax = fmaxf(vmax, fabsf(v[u]));
+      for (int k = 0; k < 27; ++k) s += Wt[co * 27 + k] * x[k];
+      s += bias ? bias[co] : 0.f;
+      v = act ? po::leaky(s) : s;
     }
-    if (live) *reinterpret_cast<float4*>(yp + co4) = make_float4(v[0], v[1], v[2], v[3]);
+    vmax = fmaxf(vmax, fabsf(v));
+    ys[threadIdx.x * LS + co] = v;
   }
   if (amax) po::amax_commit(amax, live ? vmax : 0.f);
+  __syncthreads();
+  const int64_t nlive = min((int64_t)256, npix - pbase);
+  float* yb = y + pbase * CO;
+  for (int f = threadIdx.x; f < nlive * (CO / 4); f += 256) {
+    const int px = f / (CO / 4), ch = (f % (CO / 4)) * 4;
+    const float* r = ys + px * LS + ch;
+    *reinterpret_cast<float4*>(yb + (int64_t)f * 4) = make_float4(r[0], r[1], r[2], r[3]);
+  }
 }
 
 template <int CO>

@@ -729,6 +729,463 @@ int dispatch_halo(const ConvArgs& a, hipStream_t st, int bm, int bn) {
   return PO_EINVAL;
 }
 
+// 2-D tile halo variant for 3x3 convs of input step S (1 or 2) on full maps:
+// a tile is TH x TW output pixels of one image (BM = TH*TW), so the input halo
+// of one channel chunk is (S(TH-1)+3) x (S(TW-1)+3) pixels — 1.41x the tile's
+// pixels at S = 1 with 8 x 16 tiles, where the row-contiguous halo of
+// conv_h3h_k loads 1 + 2(W+1)/BM rows per tile row (3.4x at W = 152, 5.8x at
+// 304) — and strided convs load each input pixel of the tile's footprint once
+// instead of once per tap.  The halo is loaded (hardware zero fill outside
+// the image) and split into fp16 hi/lo once per chunk, every tap reads its A
+// fragments at a precomputed shifted LDS row, the weights run through the
+// 3-deep register ring of conv_h3h_k, and the next chunk's halo is fetched
+// during the current chunk's nine taps.  No split-K: its partial rows are
+// GEMM rows, which 2-D tiles do not enumerate.
+template <int BM, int BN, int WM, int TW, int S>
+__global__ __launch_bounds__(256) void conv_h3q_k(const ConvArgs a) {
+  constexpr int BK = 16;
+  constexpr int TH = BM / TW;
+  constexpr int WN = 4 / WM;
+  constexpr int TM = BM / WM / 32;
+  constexpr int TN = BN / WN / 32;
+  static_assert(TM >= 1 && TN >= 1 && TH * TW == BM, "tile");
+  constexpr int CPR = BK / 8;                  // 16-byte chunks per LDS row
+  constexpr int SW = 3;                        // log2(rows per 256-byte bank line) for 32-byte rows
+  constexpr int HWD = S * (TW - 1) + 3;        // halo width, height, pixels
+  constexpr int HHT = S * (TH - 1) + 3;
+  constexpr int HP = HWD * HHT;
+  constexpr int H_HALFS = HP * BK;             // one halo plane
+  constexpr int B_HALFS = BN * BK;
+  constexpr int HL = (HP * CPR + 255) / 256;   // halo chunk loads per thread
+  constexpr int BL = (BN * CPR + 255) / 256;   // weight chunk loads per thread (per plane)
+  constexpr int PF = 3;                        // weight k-steps in flight (register ring)
+  static_assert(9 % PF == 0, "ring slot of k-step 9c + t must not depend on c");
+  __shared__ __attribute__((aligned(16))) _Float16 smem_h[2 * H_HALFS + 4 * B_HALFS];
+  static_assert(sizeof(smem_h) >= 4 * 4096, "the epilogue needs 16 KB of LDS");
+  _Float16* Hs = smem_h;                       // [hi, lo][HP][BK]
+  _Float16* Bs = smem_h + 2 * H_HALFS;         // [2 buffers][hi, lo][BN][BK]
+
+  const int wgid = po::xcd_remap();
+  const int tn = wgid % a.ntiles_n, tm = wgid / a.ntiles_n;
+  const int n0 = tn * BN;
+  const int tilesx = (a.Wout + TW - 1) / TW, tpi = tilesx * ((a.Hout + TH - 1) / TH);
+  const int b = tm / tpi, tr = tm - b * tpi;
+  const int oy0 = (tr / tilesx) * TH, ox0 = (tr - (tr / tilesx) * tilesx) * TW;
+  const int iy0 = S * oy0 - 1, ix0 = S * ox0 - 1;     // input pixel of halo (0, 0)
+  const int tid = threadIdx.x & 255, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave / WN, wn = wave % WN;
+  const int sh_in = po::input_shift(a);
+  const float sc_in = __builtin_ldexpf(1.f, sh_in);
+  const uint32_t in_bytes = (uint32_t)__builtin_amdgcn_readfirstlane(a.in_bytes);
+  const uint32_t w_bytes = (uint32_t)__builtin_amdgcn_readfirstlane(a.w_bytes);
+  const __amdgpu_buffer_rsrc_t in_rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(a.in), 0, in_bytes, 0x00020000);
+  const __amdgpu_buffer_rsrc_t w_rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(a.W), 0, 2 * w_bytes, 0x00020000);
+  constexpr uint32_t kOOB = 0x80000000u;
+  const uint32_t pix_bytes = (uint32_t)a.Cin_p * 4u;
+  const uint32_t wpix_bytes = (uint32_t)a.Cin_p * 2u;
+
+  // halo loader: chunk load q = tid + 256 r -> halo pixel q / CPR, channel chunk q % CPR
+  uint32_t h_off[HL];
+#pragma unroll
+  for (int r = 0; r < HL; ++r) {
+    const int q = tid + 256 * r;
+    const int row = q / CPR;
+    const int hy = row / HWD, hx = row - (row / HWD) * HWD;
+    const int iy = iy0 + hy, ix = ix0 + hx;
+    const bool ok = row < HP && (unsigned)iy < (unsigned)a.Hin && (unsigned)ix < (unsigned)a.Win;
+    h_off[r] = ok ? ((uint32_t)(b * a.Hin + iy) * a.Win + ix) * pix_bytes + (q % CPR) * 32u : kOOB;
+  }
+  const uint32_t wrow_bytes = (uint32_t)a.ntaps * wpix_bytes;
+  uint32_t b_off[BL];
+#pragma unroll
+  for (int r = 0; r < BL; ++r) {
+    const int q = tid + 256 * r;
+    const int row = q / CPR;
+    b_off[r] = (row < BN && n0 + row < a.N) ? (uint32_t)(n0 + row) * wrow_bytes + (q % CPR) * 16u : kOOB;
+  }
+  float4 rh[HL][2];
+  uint4 rbh[PF][BL], rbl[PF][BL];
+  auto load_halo = [&](int c0) {
+#pragma unroll
+    for (int r = 0; r < HL; ++r) {
+      const uint32_t o = h_off[r] + (h_off[r] == kOOB ? 0u : (uint32_t)c0 * 4u);
+      rh[r][0] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(in_rs, o, 0, 0));
+      rh[r][1] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(in_rs, o + 16u, 0, 0));
+    }
+  };
+  auto load_w = [&](int set, int tap, int c0, bool live) {
+    const uint32_t tb = (uint32_t)tap * wpix_bytes + (uint32_t)c0 * 2u;
+#pragma unroll
+    for (int r = 0; r < BL; ++r) {
+      const uint32_t o = live ? b_off[r] + tb : kOOB;
+      rbh[set][r] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(w_rs, o, 0, 0));
+      rbl[set][r] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(w_rs, o + w_bytes, 0, 0));
+    }
+  };
+  auto swz = [](int row, int chunk) { return (chunk ^ ((row >> SW) & (CPR - 1))) * 8; };
+  auto store_halo = [&]() {
+#pragma unroll
+    for (int r = 0; r < HL; ++r) {
+      const int q = tid + 256 * r;
+      const int row = q / CPR;
+      if (row < HP) {
+        uint4 hh, ll;
+        split8(rh[r][0], rh[r][1], sc_in, hh, ll);
+        _Float16* base = Hs + row * BK + swz(row, q % CPR);
+        *reinterpret_cast<uint4*>(base) = hh;
+        *reinterpret_cast<uint4*>(base + H_HALFS) = ll;
+      }
+    }
+  };
+  auto store_w = [&](int set, int buf) {
+#pragma unroll
+    for (int r = 0; r < BL; ++r) {
+      const int q = tid + 256 * r;
+      const int row = q / CPR;
+      if (row < BN) {
+        _Float16* base = Bs + (buf * 2) * B_HALFS + row * BK + swz(row, q % CPR);
+        *reinterpret_cast<uint4*>(base) = rbh[set][r];
+        *reinterpret_cast<uint4*>(base + B_HALFS) = rbl[set][r];
+      }
+    }
+  };
+
+  // per lane, fragment row i (tile pixel (ly, lx)) and tap t: the swizzled
+  // LDS offset of its halo pixel (S ly + 1 + dh, S lx + 1 + dw)
+  int aoff[TM][9];
+  const int h = lane >> 5;
+#pragma unroll
+  for (int i = 0; i < TM; ++i) {
+    const int r = wm * TM * 32 + i * 32 + (lane & 31);
+    const int ly = r / TW, lx = r - (r / TW) * TW;
+#pragma unroll
+    for (int t = 0; t < 9; ++t) {
+      const int dh = a.dh0 + (t / 3) * a.sdh, dw = a.dw0 + (t % 3) * a.sdw;
+      const int row = (S * ly + 1 + dh) * HWD + S * lx + 1 + dw;
+      aoff[i][t] = row * BK + swz(row, h);
+    }
+  }
+  const int brow = wn * TN * 32 + (lane & 31);
+  int boff[TN];
+#pragma unroll
+  for (int j = 0; j < TN; ++j) boff[j] = (brow + j * 32) * BK + swz(brow + j * 32, h);
+
+  floatx16 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.f;
+
+  const int nch = a.Cin_p / BK;
+  load_halo(0);
+#pragma unroll
+  for (int s = 0; s < PF; ++s) load_w(s, s, 0, true);                // taps 0..PF-1 of the first chunk
+  store_halo();
+  store_w(0, 0);
+  __syncthreads();
+  for (int c = 0; c < nch; ++c) {
+    const int c0 = c * BK;
+    const bool next_chunk = c + 1 < nch;
+    if (next_chunk) load_halo(c0 + BK);
+#pragma unroll
+    for (int t = 0; t < 9; ++t) {
+      const int cr = c & 1;
+      const int buf = t & 1 ? cr ^ 1 : cr;               // (9c + t) & 1
+      const _Float16* Bb = Bs + buf * 2 * B_HALFS;
+      half8 ah[TM], al[TM], bh[TN], bl[TN];
+#pragma unroll
+      for (int i = 0; i < TM; ++i) {
+        ah[i] = *reinterpret_cast<const half8*>(Hs + aoff[i][t]);
+        al[i] = *reinterpret_cast<const half8*>(Hs + H_HALFS + aoff[i][t]);
+      }
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        bh[j] = *reinterpret_cast<const half8*>(Bb + boff[j]);
+        bl[j] = *reinterpret_cast<const half8*>(Bb + B_HALFS + boff[j]);
+      }
+      const int tp = t + PF;
+      const bool more_w = tp < 9 || next_chunk;
+      load_w(t % PF, tp < 9 ? tp : tp - 9, tp < 9 ? c0 : c0 + BK, more_w);
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) {
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(al[i], bh[j], acc[i][j], 0, 0, 0);
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[i], bl[j], acc[i][j], 0, 0, 0);
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[i], bh[j], acc[i][j], 0, 0, 0);
+        }
+      const bool more = t < 8 || next_chunk;
+      if (more) {
+        store_w((t + 1) % PF, buf ^ 1);
+        if (t == 8) {
+          __syncthreads();                         // every wave is done with this chunk's halo
+          store_halo();
+        }
+      }
+      __syncthreads();
+    }
+  }
+
+  __shared__ int dst_pix[BM];
+  if (tid < BM) {
+    const int oy = oy0 + tid / TW, ox = ox0 + tid % TW;
+    dst_pix[tid] = (oy < a.Hout && ox < a.Wout) ? (b * a.Hout + oy) * a.Wout + ox : -1;
+  }
+  po::conv_epilogue<BM, TM, TN>(a, acc, reinterpret_cast<float*>(smem_h), dst_pix, 0, n0, wm, wn,
+                                sh_in + a.w_shift, true, false);
+}
+
+template <int BM, int BN, int WM, int TW, int S>
+int launch_quad(const ConvArgs& a, hipStream_t st) {
+  ConvArgs b = a;
+  b.ntiles_n = po::ceil_div(a.N, BN);
+  constexpr int TH = BM / TW;
+  const int64_t ntiles = (int64_t)a.B * po::ceil_div(a.Hout, TH) * po::ceil_div(a.Wout, TW) * b.ntiles_n;
+  if (ntiles >= (1LL << 31)) {
+    po::set_error("po_conv (fp16x3 2-D halo): too many tiles");
+    return PO_EINVAL;
+  }
+  hipLaunchKernelGGL((conv_h3q_k<BM, BN, WM, TW, S>), dim3((unsigned)ntiles, 1), dim3(256), 0, st, b);
+  return po::check_launch("po_conv (fp16x3 2-D halo)");
+}
+
+int dispatch_quad(const ConvArgs& a, hipStream_t st, int bm, int bn) {
+  // eligibility: a 3x3 tap grid (either orientation) of input step 1 or 2 on
+  // full maps, output grid = the whole destination, no split-K, no boxes
+  const bool grid3 = a.ntaps == 9 && a.tkw == 3 && (a.sdh == 1 || a.sdh == -1) && (a.sdw == 1 || a.sdw == -1) &&
+                     a.dh0 == -a.sdh && a.dw0 == -a.sdw;
+  if (!(grid3 && (a.in_step == 1 || a.in_step == 2) && a.out_step == 1 && a.out_oy == 0 && a.out_ox == 0 &&
+        !a.in_org && !a.out_org && !a.gbox && a.ksplit == 1 && a.Hg == a.Hout && a.Wg == a.Wout &&
+        a.Cin_p % 16 == 0)) {
+    po::set_error("po_conv (fp16x3 2-D halo): needs a 3x3 conv of input step 1 or 2 on full maps "
+                  "(no gbox, no split-K)");
+    return PO_EINVAL;
+  }
+  if (a.in_step == 1) {
+    if (bm == 128 && bn == 128) return launch_quad<128, 128, 2, 16, 1>(a, st);
+    if (bm == 128 && bn == 64) return launch_quad<128, 64, 4, 16, 1>(a, st);
+  } else {
+    if (bm == 128 && bn == 128) return launch_quad<128, 128, 2, 16, 2>(a, st);
+    if (bm == 128 && bn == 64) return launch_quad<128, 64, 4, 16, 2>(a, st);
+  }
+  po::set_error("po_conv (fp16x3 2-D halo): no %dx%d tile", bm, bn);
+  return PO_EINVAL;
+}
+
+// 2-D tile halo kernel with chunk-staged, fragment-ordered weights (staging
+// 4).  The host lays the split weights out in MFMA B-fragment order,
+// Wf[plane][N/32][tap][Cin_p/16][64 lanes][8 halves] (lane l: output channel
+// 32 nb + (l & 31), input channels 16 c + 8 (l >> 5) .. + 8).  Per channel
+// chunk the workgroup loads, at the start of the previous chunk, BOTH the
+// chunk's input halo and all nine taps of its weight fragments into
+// registers, and writes them to LDS at the chunk boundary (two barriers per
+// chunk).  Inside a chunk the nine taps then run from LDS only: no global
+// load is waited on and no barrier is crossed between MFMAs, so the loads of
+// the next chunk have a whole chunk of MFMA work to land.  B fragment reads
+// are one contiguous 1 KB per wave-instruction (conflict-free).
+template <int BM, int BN, int WM, int TW, int S>
+__global__ __launch_bounds__(256) void conv_h3g_k(const ConvArgs a) {
+  constexpr int BK = 16;
+  constexpr int TH = BM / TW;
+  constexpr int WN = 4 / WM;
+  constexpr int TM = BM / WM / 32;
+  constexpr int TN = BN / WN / 32;
+  static_assert(TM >= 1 && TN >= 1 && TH * TW == BM, "tile");
+  constexpr int CPR = BK / 8;
+  constexpr int SW = 3;
+  constexpr int HWD = S * (TW - 1) + 3;
+  constexpr int HHT = S * (TH - 1) + 3;
+  constexpr int HP = HWD * HHT;
+  constexpr int H_HALFS = HP * BK;             // one halo plane
+  constexpr int NB = BN / 32;                  // 32-column fragment blocks of the tile
+  constexpr int F_HALFS = NB * 9 * 512;        // one weight plane of a chunk (9 taps)
+  constexpr int HL = (HP * CPR + 255) / 256;   // halo 16-byte pieces per thread
+  constexpr int BQ = (2 * F_HALFS / 8 + 255) / 256;   // weight 16-byte pieces per thread
+  static_assert((2 * F_HALFS / 8) % 256 == 0, "weight pieces divide over the workgroup");
+  constexpr int SMEM_HALFS = 2 * H_HALFS + 2 * F_HALFS > 8192 ? 2 * H_HALFS + 2 * F_HALFS : 8192;
+  __shared__ __attribute__((aligned(16))) _Float16 smem_h[SMEM_HALFS];
+  _Float16* Hs = smem_h;                       // [hi, lo][HP][BK]
+  _Float16* Fs = smem_h + 2 * H_HALFS;         // [hi, lo][NB][9][64][8]
+
+  const int wgid = po::xcd_remap();
+  const int tn = wgid % a.ntiles_n, tm = wgid / a.ntiles_n;
+  const int n0 = tn * BN;
+  const int tilesx = (a.Wout + TW - 1) / TW, tpi = tilesx * ((a.Hout + TH - 1) / TH);
+  const int b = tm / tpi, tr = tm - b * tpi;
+  const int oy0 = (tr / tilesx) * TH, ox0 = (tr - (tr / tilesx) * tilesx) * TW;
+  const int iy0 = S * oy0 - 1, ix0 = S * ox0 - 1;
+  const int tid = threadIdx.x & 255, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave / WN, wn = wave % WN;
+  const int sh_in = po::input_shift(a);
+  const float sc_in = __builtin_ldexpf(1.f, sh_in);
+  const uint32_t in_bytes = (uint32_t)__builtin_amdgcn_readfirstlane(a.in_bytes);
+  const uint32_t w_bytes = (uint32_t)__builtin_amdgcn_readfirstlane(a.w_bytes);
+  const __amdgpu_buffer_rsrc_t in_rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(a.in), 0, in_bytes, 0x00020000);
+  const __amdgpu_buffer_rsrc_t wf_rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(a.Wf), 0, 2 * w_bytes, 0x00020000);
+  constexpr uint32_t kOOB = 0x80000000u;
+  const uint32_t pix_bytes = (uint32_t)a.Cin_p * 4u;
+  const int nch = a.Cin_p / BK;
+
+  uint32_t h_off[HL];
+#pragma unroll
+  for (int r = 0; r < HL; ++r) {
+    const int q = tid + 256 * r;
+    const int row = q / CPR;
+    const int hy = row / HWD, hx = row - (row / HWD) * HWD;
+    const int iy = iy0 + hy, ix = ix0 + hx;
+    const bool ok = row < HP && (unsigned)iy < (unsigned)a.Hin && (unsigned)ix < (unsigned)a.Win;
+    h_off[r] = ok ? ((uint32_t)(b * a.Hin + iy) * a.Win + ix) * pix_bytes + (q % CPR) * 32u : kOOB;
+  }
+  // weight piece q = tid + 256 r: plane, block jb, tap t, lane-piece lp (16 bytes)
+  uint32_t f_off[BQ];
+#pragma unroll
+  for (int r = 0; r < BQ; ++r) {
+    const int q = tid + 256 * r;
+    const int plane = q / (F_HALFS / 8), rem = q - plane * (F_HALFS / 8);
+    const int jb = rem / (9 * 64), t = (rem / 64) % 9, lp = rem % 64;
+    const int nb = (n0 >> 5) + jb;
+    f_off[r] = nb * 32 < a.N ? (uint32_t)plane * w_bytes + (uint32_t)((nb * a.ntaps + t) * nch) * 1024u + lp * 16u
+                             : kOOB;
+  }
+  float4 rh[HL][2];
+  uint4 rf[BQ];
+  auto load_chunk = [&](int c) {
+#pragma unroll
+    for (int r = 0; r < BQ; ++r) {
+      const uint32_t o = f_off[r] == kOOB ? kOOB : f_off[r] + (uint32_t)c * 1024u;
+      rf[r] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(wf_rs, o, 0, 0));
+    }
+#pragma unroll
+    for (int r = 0; r < HL; ++r) {
+      const uint32_t o = h_off[r] + (h_off[r] == kOOB ? 0u : (uint32_t)c * BK * 4u);
+      rh[r][0] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(in_rs, o, 0, 0));
+      rh[r][1] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(in_rs, o + 16u, 0, 0));
+    }
+  };
+  auto swz = [](int row, int chunk) { return (chunk ^ ((row >> SW) & (CPR - 1))) * 8; };
+  auto store_chunk = [&]() {
+#pragma unroll
+    for (int r = 0; r < BQ; ++r) *reinterpret_cast<uint4*>(Fs + (tid + 256 * r) * 8) = rf[r];
+#pragma unroll
+    for (int r = 0; r < HL; ++r) {
+      const int q = tid + 256 * r;
+      const int row = q / CPR;
+      if (row < HP) {
+        uint4 hh, ll;
+        split8(rh[r][0], rh[r][1], sc_in, hh, ll);
+        _Float16* base = Hs + row * BK + swz(row, q % CPR);
+        *reinterpret_cast<uint4*>(base) = hh;
+        *reinterpret_cast<uint4*>(base + H_HALFS) = ll;
+      }
+    }
+  };
+
+  int aoff[TM][9];
+  const int h = lane >> 5;
+#pragma unroll
+  for (int i = 0; i < TM; ++i) {
+    const int r = wm * TM * 32 + i * 32 + (lane & 31);
+    const int ly = r / TW, lx = r - (r / TW) * TW;
+#pragma unroll
+    for (int t = 0; t < 9; ++t) {
+      const int dh = a.dh0 + (t / 3) * a.sdh, dw = a.dw0 + (t % 3) * a.sdw;
+      const int row = (S * ly + 1 + dh) * HWD + S * lx + 1 + dw;
+      aoff[i][t] = row * BK + swz(row, h);
+    }
+  }
+  const _Float16* fb = Fs + (wn * TN * 9 * 64 + lane) * 8;    // this lane's fragment of block wn*TN, tap 0
+
+  floatx16 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.f;
+
+  load_chunk(0);
+  store_chunk();
+  __syncthreads();
+  for (int c = 0; c < nch; ++c) {
+    const bool next_chunk = c + 1 < nch;
+    if (next_chunk) load_chunk(c + 1);          // lands during this chunk's 9 taps
+#pragma unroll
+    for (int t = 0; t < 9; ++t) {
+      half8 ah[TM], al[TM], bh[TN], bl[TN];
+#pragma unroll
+      for (int i = 0; i < TM; ++i) {
+        ah[i] = *reinterpret_cast<const half8*>(Hs + aoff[i][t]);
+        al[i] = *reinterpret_cast<const half8*>(Hs + H_HALFS + aoff[i][t]);
+      }
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        bh[j] = *reinterpret_cast<const half8*>(fb + (j * 9 + t) * 512);
+        bl[j] = *reinterpret_cast<const half8*>(fb + F_HALFS + (j * 9 + t) * 512);
+      }
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) {
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(al[i], bh[j], acc[i][j], 0, 0, 0);
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[i], bl[j], acc[i][j], 0, 0, 0);
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[i], bh[j], acc[i][j], 0, 0, 0);
+        }
+    }
+    __syncthreads();                               // every wave is done with this chunk's LDS
+    if (next_chunk) {
+      store_chunk();
+      __syncthreads();
+    }
+  }
+
+  __shared__ int dst_pix[BM];
+  if (tid < BM) {
+    const int oy = oy0 + tid / TW, ox = ox0 + tid % TW;
+    dst_pix[tid] = (oy < a.Hout && ox < a.Wout) ? (b * a.Hout + oy) * a.Wout + ox : -1;
+  }
+  po::conv_epilogue<BM, TM, TN>(a, acc, reinterpret_cast<float*>(smem_h), dst_pix, 0, n0, wm, wn,
+                                sh_in + a.w_shift, true, false);
+}
+
+template <int BM, int BN, int WM, int TW, int S>
+int launch_gfrag(const ConvArgs& a, hipStream_t st) {
+  ConvArgs b = a;
+  b.ntiles_n = po::ceil_div(a.N, BN);
+  constexpr int TH = BM / TW;
+  const int64_t ntiles = (int64_t)a.B * po::ceil_div(a.Hout, TH) * po::ceil_div(a.Wout, TW) * b.ntiles_n;
+  if (ntiles >= (1LL << 31)) {
+    po::set_error("po_conv (fp16x3 fragment-weight halo): too many tiles");
+    return PO_EINVAL;
+  }
+  hipLaunchKernelGGL((conv_h3g_k<BM, BN, WM, TW, S>), dim3((unsigned)ntiles, 1), dim3(256), 0, st, b);
+  return po::check_launch("po_conv (fp16x3 fragment-weight halo)");
+}
+
+int dispatch_gfrag(const ConvArgs& a, hipStream_t st, int bm, int bn) {
+  const bool grid3 = a.ntaps == 9 && a.tkw == 3 && (a.sdh == 1 || a.sdh == -1) && (a.sdw == 1 || a.sdw == -1) &&
+                     a.dh0 == -a.sdh && a.dw0 == -a.sdw;
+  if (!(a.Wf && a.N % 32 == 0 && grid3 && (a.in_step == 1 || a.in_step == 2) && a.out_step == 1 &&
+        a.out_oy == 0 && a.out_ox == 0 && !a.in_org && !a.out_org && !a.gbox && a.ksplit == 1 &&
+        a.Hg == a.Hout && a.Wg == a.Wout && a.Cin_p % 16 == 0)) {
+    po::set_error("po_conv (fp16x3 fragment-weight halo): needs fragment-ordered weights (Wfrag), N %% 32 == 0 "
+                  "and a 3x3 conv of input step 1 or 2 on full maps (no gbox, no split-K)");
+    return PO_EINVAL;
+  }
+  if (a.in_step == 1) {
+    if (bm == 128 && bn == 128) return launch_gfrag<128, 128, 2, 16, 1>(a, st);
+    if (bm == 128 && bn == 64) return launch_gfrag<128, 64, 4, 16, 1>(a, st);
+    if (bm == 256 && bn == 128) return launch_gfrag<256, 128, 2, 16, 1>(a, st);
+    if (bm == 256 && bn == 64) return launch_gfrag<256, 64, 4, 16, 1>(a, st);
+  } else {
+    if (bm == 128 && bn == 128) return launch_gfrag<128, 128, 2, 16, 2>(a, st);
+    if (bm == 128 && bn == 64) return launch_gfrag<128, 64, 4, 16, 2>(a, st);
+  }
+  po::set_error("po_conv (fp16x3 fragment-weight halo): no %dx%d tile for input step %d", bm, bn, a.in_step);
+  return PO_EINVAL;
+}
+
 template <int BM, int BN, int WM, int BK>
 int launch(const ConvArgs& a, hipStream_t st) {
   ConvArgs b = a;
@@ -756,6 +1213,8 @@ int dispatch(const ConvArgs& a, hipStream_t st, int bm, int bn) {
 
 namespace po {
 int launch_h3(const ConvArgs& a, hipStream_t st, int bm, int bn, int bk, int staging) {
+  if (staging == 4) return dispatch_gfrag(a, st, bm, bn);
+  if (staging == 3) return dispatch_quad(a, st, bm, bn);
   if (staging == 2) return dispatch_halo(a, st, bm, bn);
   if (staging == 1) return dispatch_dma(a, st, bm, bn, bk);
   if (bk == 16) return dispatch<16>(a, st, bm, bn);

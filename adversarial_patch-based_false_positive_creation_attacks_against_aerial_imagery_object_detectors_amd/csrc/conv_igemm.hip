@@ -343,7 +343,9 @@ bool forced_tile(int& bm, int& bn, int& bk, int& gl) {
 // conv_h3.hip): 29..45 four-wave kernels with register staging (the A tile is
 // split on its way to LDS), 46..52 the LDS-DMA multi-stage kernel (the
 // "staging" column = 1; A is split as it is read from LDS), 53..54 the halo
-// kernel (staging 2: stride-1 3x3 convs on full maps only).
+// kernel (staging 2: stride-1 3x3 convs on full maps only), 55..56 the 2-D
+// tile halo kernel (staging 3: 3x3 convs of input step 1 or 2 on full maps),
+// 57..60 the same with fragment-ordered weights from global (staging 4).
 constexpr int kTiles[PO_CONV_NTILES][5] = {
     {128, 128, 16, 0, 0}, {128, 128, 32, 0, 0}, {64, 128, 16, 0, 0}, {64, 128, 32, 0, 0}, {128, 64, 16, 0, 0},
     {128, 64, 32, 0, 0},  {64, 64, 16, 0, 0},   {64, 64, 32, 0, 0},  {128, 32, 16, 0, 0}, {128, 32, 32, 0, 0},
@@ -356,7 +358,9 @@ constexpr int kTiles[PO_CONV_NTILES][5] = {
     {256, 128, 32, 0, 1}, {128, 256, 32, 0, 1},
     {128, 128, 64, 0, 1}, {64, 128, 64, 0, 1},  {128, 64, 64, 0, 1},  {64, 64, 64, 0, 1},  {128, 32, 64, 0, 1},
     {128, 128, 32, 1, 1}, {128, 64, 32, 1, 1},  {64, 128, 32, 1, 1},  {64, 64, 32, 1, 1},  {256, 128, 32, 1, 1},
-    {128, 128, 16, 1, 1}, {256, 128, 16, 1, 1}, {128, 128, 16, 2, 1}, {128, 64, 16, 2, 1}};
+    {128, 128, 16, 1, 1}, {256, 128, 16, 1, 1}, {128, 128, 16, 2, 1}, {128, 64, 16, 2, 1},
+    {128, 128, 16, 3, 1}, {128, 64, 16, 3, 1},
+    {128, 128, 16, 4, 1}, {128, 64, 16, 4, 1}, {256, 128, 16, 4, 1}, {256, 64, 16, 4, 1}};
 }  // namespace
 
 extern "C" int po_conv_tile_info(int t, int* bm, int* bn, int* bk, int* prec) {
@@ -390,7 +394,7 @@ extern "C" int po_conv(const po_conv_desc* d, const float* in, const float* W, c
              "po_conv: launch grid writes outside the destination");
   PO_REQUIRE((int64_t)d->B * d->Hout * d->Wout < (1LL << 31), "po_conv: destination too large");
   ConvArgs a;
-  a.in = in; a.W = W; a.bias = bias; a.y = y_out; a.res = res; a.sum = sum_out; a.mask = mask_y;
+  a.in = in; a.W = W; a.Wf = d->Wfrag; a.bias = bias; a.y = y_out; a.res = res; a.sum = sum_out; a.mask = mask_y;
   a.y2 = y2_out; a.mask2 = mask2;
   a.in_org = d->in_org; a.out_org = d->out_org; a.gbox = d->gbox;
   PO_REQUIRE(!d->gbox || !d->out_org, "po_conv: gbox needs a full-map destination (out_org NULL)");

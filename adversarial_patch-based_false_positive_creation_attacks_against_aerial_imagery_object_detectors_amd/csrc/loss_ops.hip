@@ -386,38 +386,46 @@ __device__ __forceinline__ void cone_map(int kind, int k, int s, int pad, int a,
   }
 }
 
+// One workgroup per image: the program and the image's boxes are staged in
+// LDS, lane 0 walks the (dependent) rows there, and the workgroup writes the
+// boxes back; global-memory latency is paid once per box, not once per row.
 __global__ __launch_bounds__(64) void grad_boxes_k(const int32_t* __restrict__ roi, int B, int S,
-                                                   const int32_t* __restrict__ prog, int nprog,
+                                                   const int32_t* __restrict__ prog, int nprog, int nbox,
                                                    int32_t* __restrict__ boxes) {
-  const int b = blockIdx.x * 64 + threadIdx.x;
-  if (b >= B) return;
-  for (int r = 0; r < nprog; ++r) {
-    int4* d = reinterpret_cast<int4*>(boxes) + (size_t)prog[8 * r] * B + b;
-    *d = make_int4(0, 0, 0, 0);
-  }
-  for (int r = 0; r < nprog; ++r) {
-    const int32_t* p = prog + 8 * r;
-    int sr0, sc0, sr1, sc1;                    // source box, half-open
-    if (p[1] < 0) {
-      if (roi) { sc0 = roi[4 * b]; sr0 = roi[4 * b + 1]; sc1 = roi[4 * b + 2]; sr1 = roi[4 * b + 3]; }
-      else { sr0 = sc0 = 0; sr1 = sc1 = S; }
-    } else {
-      const int4 v = reinterpret_cast<const int4*>(boxes)[(size_t)p[1] * B + b];
-      sr0 = v.x; sc0 = v.y; sr1 = v.z; sc1 = v.w;
+  extern __shared__ int4 sm[];
+  int4* sbox = sm;                                    // [nbox]
+  int32_t* sprog = reinterpret_cast<int32_t*>(sm + nbox);   // [nprog][8]
+  const int b = blockIdx.x;
+  for (int k = threadIdx.x; k < nbox; k += 64) sbox[k] = reinterpret_cast<const int4*>(boxes)[(size_t)k * B + b];
+  for (int k = threadIdx.x; k < 8 * nprog; k += 64) sprog[k] = prog[k];
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    for (int r = 0; r < nprog; ++r) sbox[sprog[8 * r]] = make_int4(0, 0, 0, 0);
+    for (int r = 0; r < nprog; ++r) {
+      const int32_t* p = sprog + 8 * r;
+      int sr0, sc0, sr1, sc1;                  // source box, half-open
+      if (p[1] < 0) {
+        if (roi) { sc0 = roi[4 * b]; sr0 = roi[4 * b + 1]; sc1 = roi[4 * b + 2]; sr1 = roi[4 * b + 3]; }
+        else { sr0 = sc0 = 0; sr1 = sc1 = S; }
+      } else {
+        const int4 v = sbox[p[1]];
+        sr0 = v.x; sc0 = v.y; sr1 = v.z; sc1 = v.w;
+      }
+      if (sr0 >= sr1 || sc0 >= sc1) continue;
+      int r0, r1, c0, c1;
+      cone_map(p[2], p[3], p[4], p[5], sr0, sr1 - 1, r0, r1);
+      cone_map(p[2], p[3], p[4], p[5], sc0, sc1 - 1, c0, c1);
+      r0 = max(r0, 0); c0 = max(c0, 0);
+      r1 = min(r1, p[6] - 1); c1 = min(c1, p[7] - 1);
+      if (r0 > r1 || c0 > c1) continue;
+      int4 o = sbox[p[0]];
+      if (o.x >= o.z || o.y >= o.w) o = make_int4(r0, c0, r1 + 1, c1 + 1);
+      else o = make_int4(min(o.x, r0), min(o.y, c0), max(o.z, r1 + 1), max(o.w, c1 + 1));
+      sbox[p[0]] = o;
     }
-    if (sr0 >= sr1 || sc0 >= sc1) continue;
-    int r0, r1, c0, c1;
-    cone_map(p[2], p[3], p[4], p[5], sr0, sr1 - 1, r0, r1);
-    cone_map(p[2], p[3], p[4], p[5], sc0, sc1 - 1, c0, c1);
-    r0 = max(r0, 0); c0 = max(c0, 0);
-    r1 = min(r1, p[6] - 1); c1 = min(c1, p[7] - 1);
-    if (r0 > r1 || c0 > c1) continue;
-    int4* d = reinterpret_cast<int4*>(boxes) + (size_t)p[0] * B + b;
-    int4 o = *d;
-    if (o.x >= o.z || o.y >= o.w) o = make_int4(r0, c0, r1 + 1, c1 + 1);
-    else o = make_int4(min(o.x, r0), min(o.y, c0), max(o.z, r1 + 1), max(o.w, c1 + 1));
-    *d = o;
   }
+  __syncthreads();
+  for (int k = threadIdx.x; k < nbox; k += 64) reinterpret_cast<int4*>(boxes)[(size_t)k * B + b] = sbox[k];
 }
 }  // namespace
 
@@ -425,7 +433,8 @@ extern "C" int po_grad_boxes(const int32_t* roi, int B, int S, const int32_t* pr
                              int32_t* boxes, po_stream_t s) {
   PO_REQUIRE(prog && boxes, "po_grad_boxes: null pointer");
   PO_REQUIRE(B >= 1 && S >= 1 && nprog >= 1 && nbox >= 1, "po_grad_boxes: bad sizes");
-  hipLaunchKernelGGL(grad_boxes_k, dim3(po::ceil_div(B, 64)), dim3(64), 0, po::stream_of(s), roi, B, S, prog, nprog,
-                     boxes);
+  const size_t lds = (size_t)nbox * 16 + (size_t)nprog * 32;
+  PO_REQUIRE(lds <= 65536, "po_grad_boxes: %d boxes and %d rows exceed the 64 KB staging limit", nbox, nprog);
+  hipLaunchKernelGGL(grad_boxes_k, dim3(B), dim3(64), lds, po::stream_of(s), roi, B, S, prog, nprog, nbox, boxes);
   return po::check_launch("po_grad_boxes");
 }

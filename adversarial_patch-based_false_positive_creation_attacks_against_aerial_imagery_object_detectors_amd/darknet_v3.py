@@ -675,6 +675,7 @@ class NetPlan:
             else:
                 w16, shift = self.net._dgrad_weight16(wts_or_j, taps, cin_p, self.device)
             desc.prec, desc.w_shift = 1, shift
+            desc.Wfrag = self.net._frag16(w16)
             return w16
         desc.prec, desc.w_shift = 0, 0
         if taps is None:
@@ -1204,6 +1205,7 @@ class Darknet(nn.Module):
         self._dev = None
         self._dev_device = None
         self._dgrad_cache = {}
+        self._frag = {}
         self._plans = {}
         self._tile_cache = {}
 
@@ -1265,6 +1267,7 @@ class Darknet(nn.Module):
         """Drop device-side folded weights and plans (after a weight change)."""
         self._dev = None
         self._dgrad_cache = {}
+        self._frag = {}
         self._plans = {}
 
     def _folded(self, i):
@@ -1288,6 +1291,7 @@ class Darknet(nn.Module):
             if "unsupported" in m:
                 raise NotImplementedError("activation %r (block %d) is not on the HIP path" % (m["unsupported"], i))
         self._dev, self._dgrad_cache, self._plans = {}, {}, {}
+        self._frag = {}
         self._folded_cache = {}
         for i, m in self._conv_meta.items():
             W, bias = self._folded(i)
@@ -1314,6 +1318,21 @@ class Darknet(nn.Module):
         hi = ws.half()
         lo = (ws - hi.float()).half()
         return torch.stack([hi, lo]).contiguous(), shift
+
+    def _frag16(self, w16):
+        """Device address of w16 ([2][N][taps][Cin_p] fp16) in MFMA B-fragment
+        order [2][N/32][taps][Cin_p/16][64][8] (po_conv_desc.Wfrag), built once
+        per weight tensor; None when N is not a multiple of 32."""
+        if w16.dim() != 4:
+            return None
+        two, N, T, C = w16.shape
+        if N % 32 or C % 16:
+            return None
+        key = w16.data_ptr()
+        if key not in self._frag:
+            f = w16.view(2, N // 32, 32, T, C // 16, 2, 8).permute(0, 1, 3, 4, 5, 2, 6).contiguous()
+            self._frag[key] = (w16, f)          # keep w16 alive with its key
+        return nat.c_void_p(self._frag[key][1].data_ptr())
 
     def _dev16(self, i):
         """Split-fp16 forward weights of conv i (built on first use)."""

@@ -33,7 +33,7 @@ typedef void* po_stream_t;
 #define PO_EHIP -2     /* HIP runtime error */
 #define PO_EDEVICE -3  /* device is not gfx950 */
 
-#define PO_ABI_VERSION 6
+#define PO_ABI_VERSION 7
 #define PO_AMAX_SUB 64  /* sub-slots per max|x| slot (see po_conv_desc) */
 
 int po_abi_version(void);
@@ -238,14 +238,25 @@ typedef struct po_conv_desc {
    * rest of the destination is left untouched.  Needs a full-map destination
    * (out_org = NULL). */
   const int32_t* gbox;
+  /* Optional (prec 1, tiles 57..60): the split fp16 weights W in MFMA fragment
+   * order, [2][N/32][ntaps][Cin_p/16][64][8] halves: element (lane l, e) of
+   * block (nb, tap, c) is W[32 nb + (l & 31)][tap][16 c + 8 (l >> 5) + e].
+   * Needs N % 32 == 0; NULL: those tiles do not apply. */
+  const void* Wfrag;
 } po_conv_desc;
 
-#define PO_CONV_NTILES 54
+#define PO_CONV_NTILES 60
 /* Tile `t` (1-based): block rows BM (output pixels), block columns BN (output
  * channels), k-step BK (input channels).  Tiles 1..10 stage operands through
  * registers, 11..20 are the same shapes staged by LDS-DMA, 21..28 are
- * 256x128 / 128x256 blocks (register, then LDS-DMA staging).  Returns
- * PO_EINVAL for a bad index. */
+ * 256x128 / 128x256 blocks (register, then LDS-DMA staging); these are the
+ * exact-fp32 (prec 0) tiles.  29..54 are fp16x3 (prec 1) tiles: register
+ * staging, LDS-DMA multi-stage (46..52) and the row halo kernel for stride-1
+ * 3x3 convs (53..54); 55..56 are the 2-D tile halo kernel (8 x 16 output
+ * pixels per tile) for 3x3 convs of input step 1 or 2 on full maps without
+ * split-K or boxes; 57..60 the same 2-D tiles (and 16 x 16-pixel ones at input
+ * step 1) reading the weights as MFMA fragments from Wfrag.  A tile that does not apply to a launch makes po_conv
+ * return PO_EINVAL.  Returns PO_EINVAL for a bad index. */
 int po_conv_tile_info(int t, int* bm, int* bn, int* bk, int* prec);
 
 /* v[m][n] = act(sum_k A[m][k] * W[n][k] + bias[n]) (+ y_out[m][n] if accumulate);

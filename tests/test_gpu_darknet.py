@@ -179,10 +179,11 @@ def test_split_k_matches_single_pass(B, H, Cin, Cout, k, prec, tile):
         assert _rel(y, outs[1]) < 1e-5, (ks, _rel(y, outs[1]))
 
 
-@pytest.mark.parametrize("tile", list(range(1, 55)))
+@pytest.mark.parametrize("tile", list(range(1, 61)))
 def test_every_conv_tile(tile):
     """Every po_conv tile (exact fp32: register-staged 1..10 and 21..24,
-    LDS-DMA-staged 11..20 and 25..28; fp16x3: 29..45, LDS-DMA 46..52, halo 53..54) on a 3x3 conv with zero
+    LDS-DMA-staged 11..20 and 25..28; fp16x3: 29..45, LDS-DMA 46..52, halo 53..54,
+    2-D halo 55..56, fragment-weight 2-D halo 57..60) on a 3x3 conv with zero
     padding, a ragged pixel count and a ragged channel count, against a
     float64 torch conv2d."""
     import ctypes
@@ -207,6 +208,66 @@ def test_every_conv_tile(tile):
     wt, shift, slot = _conv_operands(nat, wd, x, pr.value)
     d.prec, d.w_shift = pr.value, shift
     d.in_amax = slot.data_ptr() if slot is not None else None
+    wf = _frag(wt) if pr.value == 1 else None
+    d.Wfrag = wf.data_ptr() if wf is not None else None
     nat.call("po_conv", ctypes.byref(d), nat.ptr(xd), nat.ptr(wt, wt.dtype), nat.ptr(bias.to(DEV)), nat.ptr(y),
              None, None, None, None, None, nat.stream())
     assert _rel(y.permute(0, 3, 1, 2).cpu().double(), ref) < 3e-6     # fp32-class error either way
+
+
+def _frag(w16):
+    """po_conv_desc.Wfrag layout of split weights [2][N][taps][Cin_p]."""
+    two, N, T, C = w16.shape
+    return w16.view(2, N // 32, 32, T, C // 16, 2, 8).permute(0, 1, 3, 4, 5, 2, 6).contiguous()
+
+
+@pytest.mark.parametrize("quad,row", [(55, 29), (56, 31), (57, 29), (58, 31), (59, None), (60, None)])
+@pytest.mark.parametrize("step,H,flip", [(1, 37, False), (1, 40, True), (2, 61, False), (2, 64, False)])
+def test_quad_halo_tiles_match_row_tiles(quad, row, step, H, flip):
+    """The 2-D tile halo kernel (tiles 55/56: 8 x 16 output pixels per tile,
+    input step 1 or 2, either tap orientation) runs the same k-steps and MFMA
+    sequence as the register-staged tile of the same BM x BN x BK: identical
+    outputs (ragged edges at H = 37 / 61), and both within fp32 class of a
+    float64 conv2d.  A boxed launch is refused."""
+    import ctypes
+    nat = pkg_mod("_native")
+    B, Cin, Cout = 2, 48, 96
+    Ho = (H - 1) // step + 1
+    gen = torch.Generator().manual_seed(H + step)
+    x = torch.randn(B, Cin, H, H, generator=gen)
+    w = torch.randn(Cout, Cin, 3, 3, generator=gen) * (2.0 / (Cin * 9)) ** 0.5
+    bias = torch.randn(Cout, generator=gen) * 0.1
+    wk = w.flip(2, 3) if flip else w            # flipped tap order: dh0 = +1, sdh = -1 (dgrad orientation)
+    ref = torch.nn.functional.conv2d(x.double(), w.double(), bias.double(), padding=1, stride=step)
+    xd = x.permute(0, 2, 3, 1).contiguous().to(DEV)
+    wd = wk.permute(0, 2, 3, 1).reshape(Cout, 9, Cin).contiguous().to(DEV)
+    wt, shift, slot = _conv_operands(nat, wd, x, 1)
+    wf = _frag(wt)
+    if quad in (59, 60) and step == 2:
+        pytest.skip("16 x 16 tiles take input step 1 only")
+
+    def run(tile, box=None):
+        y = torch.full((B, Ho, Ho, Cout), float("nan"), device=DEV)
+        d = nat.po_conv_desc()
+        d.B, d.Hin, d.Win, d.Cin_p, d.Hout, d.Wout, d.Cout_p, d.Hg, d.Wg = B, H, H, Cin, Ho, Ho, Cout, Ho, Ho
+        d.in_step, d.out_step, d.ntaps, d.N, d.act, d.tile = step, 1, 9, Cout, 1, tile
+        for kh in range(3):
+            for kw in range(3):
+                s_ = -1 if flip else 1
+                d.dh[kh * 3 + kw], d.dw[kh * 3 + kw] = s_ * (kh - 1), s_ * (kw - 1)
+        d.prec, d.w_shift, d.in_amax = 1, shift, slot.data_ptr()
+        d.gbox = box.data_ptr() if box is not None else None
+        d.Wfrag = wf.data_ptr()
+        nat.call("po_conv", ctypes.byref(d), nat.ptr(xd), nat.ptr(wt, wt.dtype), nat.ptr(bias.to(DEV)), nat.ptr(y),
+                 None, None, None, None, None, nat.stream())
+        torch.cuda.synchronize()
+        return y.permute(0, 3, 1, 2).cpu()
+
+    yq = run(quad)
+    assert not torch.isnan(yq).any()
+    if row is not None:
+        assert torch.equal(yq, run(row))
+    assert _rel(yq.double(), torch.nn.functional.leaky_relu(ref, 0.1)) < 3e-6
+    box = torch.tensor([[0, 0, 4, 4]] * B, dtype=torch.int32, device=DEV)
+    with pytest.raises(RuntimeError, match="halo"):
+        run(quad, box)
