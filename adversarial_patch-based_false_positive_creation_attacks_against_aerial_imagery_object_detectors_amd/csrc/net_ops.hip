@@ -106,72 +106,91 @@ __global__ __launch_bounds__(256) void up2_bwd_k(const float* __restrict__ src, 
   if (amax) po::amax_commit(amax, fabsf(v));
 }
 
-// k=2 max pool; stride 2 (no padding) or stride 1 over ZeroPad2d((0,1,0,1))
+// k=2 max pool; stride 2 (no padding) or stride 1 over ZeroPad2d((0,1,0,1)).
+// Grid: x = one output row (b, y), y = 256-thread slices of that row's
+// (pixel, 4-channel group) pairs: each thread moves 16 bytes per pixel and
+// needs one 32-bit division for its indices.
 __global__ __launch_bounds__(256) void maxpool2_fwd_k(const float* __restrict__ src, int B, int H, int W,
                                                       int C, int Cp, int stride, int Ho, int Wo,
                                                       float* __restrict__ dst, int8_t* __restrict__ am,
                                                       uint32_t* __restrict__ amax) {
-  const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  const int64_t tot = (int64_t)B * Ho * Wo * Cp;
-  float best = 0.f;
-  if (t < tot) {
-    const int c = (int)(t % Cp);
-    const int64_t p = t / Cp;
-    const int x = (int)(p % Wo);
-    const int y = (int)((p / Wo) % Ho);
-    const int b = (int)(p / ((int64_t)Wo * Ho));
-    int arg = 0;
-    if (c < C) {
-      arg = -1;
+  const int row = blockIdx.x, b = row / Ho, y = row - b * Ho;
+  const int c4n = Cp >> 2;
+  const int q = blockIdx.y * 256 + threadIdx.x;
+  float vmax = 0.f;
+  if (q < Wo * c4n) {
+    const int x = q / c4n, c = (q - x * c4n) * 4;
+    float bv[4] = {0.f, 0.f, 0.f, 0.f};
+    int arg[4] = {0, 0, 0, 0};
 #pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        const int yy = y * stride + (k >> 1), xx = x * stride + (k & 1);
-        // outside the source = the zero padding of ZeroPad2d (stride-1 case)
-        const float v = (yy < H && xx < W) ? src[(((int64_t)b * H + yy) * W + xx) * Cp + c] : 0.f;
-        if (arg < 0 || v > best || isnan(v)) { best = v; arg = k; }
-      }
+    for (int k = 0; k < 4; ++k) {
+      const int yy = y * stride + (k >> 1), xx = x * stride + (k & 1);
+      // outside the source = the zero padding of ZeroPad2d (stride-1 case)
+      const float4 v4 = (yy < H && xx < W)
+                            ? *reinterpret_cast<const float4*>(src + (((int64_t)b * H + yy) * W + xx) * Cp + c)
+                            : make_float4(0.f, 0.f, 0.f, 0.f);
+      const float v[4] = {v4.x, v4.y, v4.z, v4.w};
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+        if (k == 0 || v[u] > bv[u] || isnan(v[u])) { bv[u] = v[u]; arg[u] = k; }
     }
-    dst[t] = best;
-    am[t] = (int8_t)arg;
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+      if (c + u >= C) { bv[u] = 0.f; arg[u] = 0; }
+    const int64_t o = ((int64_t)row * Wo + x) * Cp + c;
+    *reinterpret_cast<float4*>(dst + o) = make_float4(bv[0], bv[1], bv[2], bv[3]);
+    *reinterpret_cast<char4*>(am + o) = make_char4((char)arg[0], (char)arg[1], (char)arg[2], (char)arg[3]);
+    vmax = fmaxf(fmaxf(fabsf(bv[0]), fabsf(bv[1])), fmaxf(fabsf(bv[2]), fabsf(bv[3])));
   }
-  if (amax) po::amax_commit(amax, fabsf(best));
+  if (amax) po::amax_commit(amax, vmax);
 }
 
-// gather form: each source pixel sums the outputs whose argmax selected it
+// gather form: each source pixel sums, in window-position order, the outputs
+// whose argmax selected it
 __global__ __launch_bounds__(256) void maxpool2_bwd_k(const float* __restrict__ dd,
                                                       const int8_t* __restrict__ am, int B, int H, int W,
                                                       int C, int Cp, int stride, int Ho, int Wo,
                                                       float* __restrict__ ds, int acc,
                                                       const float* __restrict__ my,
                                                       uint32_t* __restrict__ amax) {
-  const int64_t t0 = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  const int64_t tot = (int64_t)B * H * W * Cp;
-  const bool live = t0 < tot;
-  const int64_t t = live ? t0 : 0;
-  const int c = (int)(t % Cp);
-  const int64_t p = t / Cp;
-  const int x = (int)(p % W);
-  const int y = (int)((p / W) % H);
-  const int b = (int)(p / ((int64_t)W * H));
-  float v = 0.f;
-  if (live && c < C) {
+  const int row = blockIdx.x, b = row / H, y = row - b * H;
+  const int c4n = Cp >> 2;
+  const int q = blockIdx.y * 256 + threadIdx.x;
+  float vmax = 0.f;
+  if (q < W * c4n) {
+    const int x = q / c4n, c = (q - x * c4n) * 4;
+    float v[4] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
-      const int dy = k >> 1, dx = k & 1;
-      const int ty = y - dy, tx = x - dx;
+      const int ty = y - (k >> 1), tx = x - (k & 1);
       if (ty < 0 || tx < 0 || ty % stride || tx % stride) continue;
       const int oy = ty / stride, ox = tx / stride;
       if (oy >= Ho || ox >= Wo) continue;
       const int64_t o = (((int64_t)b * Ho + oy) * Wo + ox) * Cp + c;
-      if (am[o] == k) v += dd[o];
+      const char4 a = *reinterpret_cast<const char4*>(am + o);
+      const float4 g = *reinterpret_cast<const float4*>(dd + o);
+      if (a.x == k) v[0] += g.x;
+      if (a.y == k) v[1] += g.y;
+      if (a.z == k) v[2] += g.z;
+      if (a.w == k) v[3] += g.w;
     }
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+      if (c + u >= C) v[u] = 0.f;
+    const int64_t t = ((int64_t)row * W + x) * Cp + c;
+    if (acc) {
+      const float4 p = *reinterpret_cast<const float4*>(ds + t);
+      v[0] += p.x; v[1] += p.y; v[2] += p.z; v[3] += p.w;
+    }
+    if (my) {
+      const float4 m = *reinterpret_cast<const float4*>(my + t);
+      v[0] *= po::leaky_grad(m.x); v[1] *= po::leaky_grad(m.y);
+      v[2] *= po::leaky_grad(m.z); v[3] *= po::leaky_grad(m.w);
+    }
+    *reinterpret_cast<float4*>(ds + t) = make_float4(v[0], v[1], v[2], v[3]);
+    vmax = fmaxf(fmaxf(fabsf(v[0]), fabsf(v[1])), fmaxf(fabsf(v[2]), fabsf(v[3])));
   }
-  if (live) {
-    if (acc) v += ds[t];
-    if (my) v *= po::leaky_grad(my[t]);
-    ds[t] = v;
-  }
-  if (amax) po::amax_commit(amax, fabsf(v));
+  if (amax) po::amax_commit(amax, vmax);
 }
 
 __global__ __launch_bounds__(256) void nhwc2nchw_k(const float* __restrict__ s, int B, int H, int W, int C,
@@ -256,9 +275,11 @@ extern "C" int po_maxpool2_fwd(const float* src, int B, int H, int W, int C, int
   PO_REQUIRE(src && dst && argmax && (stride == 1 || stride == 2) && C <= Cp, "po_maxpool2_fwd: bad argument");
   int Ho, Wo;
   pool_out(H, W, stride, Ho, Wo);
-  const int64_t tot = (int64_t)B * Ho * Wo * Cp;
-  hipLaunchKernelGGL(maxpool2_fwd_k, dim3(po::ceil_div(tot, 256)), dim3(256), 0, po::stream_of(s), src, B, H,
-                     W, C, Cp, stride, Ho, Wo, dst, argmax, amax);
+  PO_REQUIRE(Cp % 4 == 0 && (int64_t)B * Ho < (1LL << 31) && (int64_t)Wo * Cp < (1LL << 30),
+             "po_maxpool2_fwd: Cp %d must be a multiple of 4 (sizes within 32-bit grids)", Cp);
+  if ((int64_t)B * Ho * Wo == 0) return PO_OK;
+  hipLaunchKernelGGL(maxpool2_fwd_k, dim3(B * Ho, po::ceil_div((int64_t)Wo * (Cp / 4), 256)), dim3(256), 0,
+                     po::stream_of(s), src, B, H, W, C, Cp, stride, Ho, Wo, dst, argmax, amax);
   return po::check_launch("po_maxpool2_fwd");
 }
 
@@ -268,9 +289,12 @@ extern "C" int po_maxpool2_bwd(const float* d_dst, const int8_t* argmax, int B, 
   PO_REQUIRE(d_dst && argmax && d_src && (stride == 1 || stride == 2), "po_maxpool2_bwd: bad argument");
   int Ho, Wo;
   pool_out(H, W, stride, Ho, Wo);
-  const int64_t tot = (int64_t)B * H * W * Cp;
-  hipLaunchKernelGGL(maxpool2_bwd_k, dim3(po::ceil_div(tot, 256)), dim3(256), 0, po::stream_of(s), d_dst,
-                     argmax, B, H, W, C, Cp, stride, Ho, Wo, d_src, accumulate, mask_y, amax);
+  PO_REQUIRE(Cp % 4 == 0 && (int64_t)B * H < (1LL << 31) && (int64_t)W * Cp < (1LL << 30),
+             "po_maxpool2_bwd: Cp %d must be a multiple of 4 (sizes within 32-bit grids)", Cp);
+  if ((int64_t)B * H * W == 0) return PO_OK;
+  hipLaunchKernelGGL(maxpool2_bwd_k, dim3(B * H, po::ceil_div((int64_t)W * (Cp / 4), 256)), dim3(256), 0,
+                     po::stream_of(s), d_dst, argmax, B, H, W, C, Cp, stride, Ho, Wo, d_src, accumulate, mask_y,
+                     amax);
   return po::check_launch("po_maxpool2_bwd");
 }
 

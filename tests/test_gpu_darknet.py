@@ -271,3 +271,40 @@ def test_quad_halo_tiles_match_row_tiles(quad, row, step, H, flip):
     box = torch.tensor([[0, 0, 4, 4]] * B, dtype=torch.int32, device=DEV)
     with pytest.raises(RuntimeError, match="halo"):
         run(quad, box)
+
+
+@pytest.mark.parametrize("stride,H,W,C,Cp", [(2, 13, 10, 12, 16), (1, 9, 7, 16, 16), (2, 416 // 8, 52, 30, 32)])
+def test_maxpool_ops_match_torch(stride, H, W, C, Cp):
+    """po_maxpool2_fwd/bwd (darknet_v3.py:61-69: MaxPool2d(2,2), or
+    ZeroPad2d((0,1,0,1)) + MaxPool2d(2,1)) against torch on NHWC buffers with
+    padded channels; backward with accumulate and a LeakyReLU mask."""
+    import torch.nn.functional as F
+    nat = pkg_mod("_native")
+    B = 3
+    gen = torch.Generator().manual_seed(H * W + C)
+    x = torch.randn(B, C, H, W, generator=gen)
+    xr = x.clone().requires_grad_(True)
+    xp = F.pad(xr, (0, 1, 0, 1)) if stride == 1 else xr
+    ref = F.max_pool2d(xp, 2, stride)
+    Ho, Wo = ref.shape[2:]
+    g = torch.randn(ref.shape, generator=gen)
+    ref.backward(g)
+    src = torch.zeros(B, H, W, Cp)
+    src[..., :C] = x.permute(0, 2, 3, 1)
+    src = src.to(DEV)
+    dst = torch.full((B, Ho, Wo, Cp), float("nan"), device=DEV)
+    am = torch.zeros(B, Ho, Wo, Cp, dtype=torch.int8, device=DEV)
+    nat.call("po_maxpool2_fwd", nat.ptr(src), B, H, W, C, Cp, stride, nat.ptr(dst), nat.ptr(am, torch.int8), None,
+             nat.stream())
+    assert torch.equal(dst[..., :C].permute(0, 3, 1, 2).cpu(), ref.detach())
+    assert (dst[..., C:] == 0).all()
+    gd = torch.zeros(B, Ho, Wo, Cp)
+    gd[..., :C] = g.permute(0, 2, 3, 1)
+    prev = torch.randn(B, H, W, Cp, generator=gen)
+    mask = torch.randn(B, H, W, Cp, generator=gen)
+    ds = prev.clone().to(DEV)
+    gdd, maskd = gd.to(DEV), mask.to(DEV)        # keep the device copies alive across the launch
+    nat.call("po_maxpool2_bwd", nat.ptr(gdd), nat.ptr(am, torch.int8), B, H, W, C, Cp, stride, nat.ptr(ds), 1,
+             nat.ptr(maskd), None, nat.stream())
+    want = (xr.grad.permute(0, 2, 3, 1) + prev[..., :C]) * torch.where(mask[..., :C] > 0, 1.0, 0.1)
+    torch.testing.assert_close(ds[..., :C].cpu(), want, rtol=1e-6, atol=1e-6)

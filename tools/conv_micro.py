@@ -29,6 +29,9 @@ if os.environ.get("MICRO_PREC", "0") == "1":          # fp16x3 operands
     slot[0] = torch.tensor([float(x.abs().max())]).view(torch.int32)[0]
     w, d.w_shift = ge._pkg("darknet_v3").Darknet._split16(w)
     d.prec, d.in_amax = 1, slot.data_ptr()
+    wf = ge._pkg("darknet_v3").Darknet.__new__(ge._pkg("darknet_v3").Darknet)
+    wf._frag = {}
+    d.Wfrag = wf._frag16(w)                             # fragment-ordered copy (tiles 57..60)
 d.tile = int(os.environ.get("MICRO_TILE", "0"))
 args = (ctypes.byref(d), nat.ptr(x), nat.ptr(w, w.dtype), nat.ptr(b), nat.ptr(y), None, None, None, None, None)
 st = nat.stream()
