@@ -94,11 +94,11 @@ def main():
                 lines += ["", "%s:" % f, "```", txt[-1], "```"]
     with open(os.path.join(pdir, "summary_%s.md" % tag), "w") as fh:
         fh.write("\n".join(lines) + "\n")
-    conv = [table[k] for k in table if k in ("conv_k", "conv_h3_k", "conv_h3d_k", "conv_h3h_k", "conv_reduce_k")]
+    conv = [table[k] for k in table if k.startswith("conv_") and k.endswith("_k")]
     hb = [t["hbm_bytes_per_step"] for t in conv]
     with open(os.path.join(ROOT, "profiles", "traffic_%s_%s.json" % (tag, prec)), "w") as fh:
         json.dump({"round": rnd, "prec": prec,
-                   "kernel": "po_conv launches of one step (conv_k / conv_h3_k / conv_h3d_k / conv_h3h_k + split-K reduce)",
+                   "kernel": "po_conv launches of one step (conv_k / conv_h3*_k tile families + split-K reduce)",
                    "conv_hbm_bytes_per_step": None if None in hb else sum(hb),
                    "conv_ms_per_step": sum(t["ms_per_step"] for t in conv),
                    "conv_calls_per_step": sum(t["calls_per_step"] for t in conv),
