@@ -65,6 +65,92 @@ __global__ __launch_bounds__(256) void first_fwd_k(const float* __restrict__ img
   }
 }
 
+// Two pixels per thread (p and p + 256 of a 512-pixel block) as the two
+// lanes of packed fp32 FMAs (v_pk_fma_f32, the scalar-cache weight broadcast
+// to both halves): half the FMA issue slots and half the weight loads per
+// pixel of first_fwd_k, same per-pixel summation order (bit-identical).  The
+// taps are read through a buffer resource: out-of-image taps read zero from
+// the hardware range check instead of branching.  The two 256-pixel halves
+// are staged through LDS and stored as two contiguous 16-byte-per-lane streams.
+typedef float f2_t __attribute__((ext_vector_type(2)));
+template <int CO>
+__global__ __launch_bounds__(256) void first_fwd2_k(const float* __restrict__ img, int B, int H, int W,
+                                                    int stride, int Ho, int Wo,
+                                                    const float* __restrict__ Wt,
+                                                    const float* __restrict__ bias, int Cout,
+                                                    int act, float* __restrict__ y,
+                                                    uint32_t* __restrict__ amax) {
+  constexpr int LS = CO + 1;
+  __shared__ float ys[256 * LS];
+  const int64_t npix = (int64_t)B * Ho * Wo;
+  const int64_t pbase = (int64_t)blockIdx.x * 512;
+  const int tid = threadIdx.x;
+  const uint32_t img_bytes = (uint32_t)((int64_t)B * 3 * H * W * 4);
+  const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(img), 0, img_bytes, 0x00020000);
+  constexpr uint32_t kOOB = 0x80000000u;
+  const uint32_t plane = (uint32_t)H * W * 4u;
+  f2_t x[27];
+#pragma unroll
+  for (int q = 0; q < 2; ++q) {
+    const int p0 = (int)pbase + q * 256 + tid;      // npix < 2^31 (host check): 32-bit divisions
+    const bool live = p0 < (int)npix;
+    const int p = live ? p0 : 0;
+    const int b = p / (Ho * Wo);
+    const int rem = p - b * Ho * Wo;
+    const int i = rem / Wo, j = rem - i * Wo;
+    const uint32_t ib = (uint32_t)b * 3u * plane;
+#pragma unroll
+    for (int kh = 0; kh < 3; ++kh)
+#pragma unroll
+      for (int kw = 0; kw < 3; ++kw) {
+        const int hi = i * stride - 1 + kh, wi = j * stride - 1 + kw;
+        const bool ok = live && (unsigned)hi < (unsigned)H && (unsigned)wi < (unsigned)W;
+        const uint32_t o = ok ? ib + ((uint32_t)hi * W + wi) * 4u : kOOB;
+#pragma unroll
+        for (int c = 0; c < 3; ++c)
+          x[c * 9 + kh * 3 + kw][q] = __builtin_bit_cast(
+              float, __builtin_amdgcn_raw_buffer_load_b32(rs, ok ? o + c * plane : kOOB, 0, 0));
+      }
+  }
+  f2_t out[CO];
+  f2_t vmax = {0.f, 0.f};
+#pragma unroll
+  for (int co = 0; co < CO; ++co) {
+    f2_t v = {0.f, 0.f};
+    if (co < Cout) {                                 // wave-uniform
+      f2_t s = {0.f, 0.f};
+#pragma unroll
+      for (int k = 0; k < 27; ++k) s = __builtin_elementwise_fma((f2_t)(Wt[co * 27 + k]), x[k], s);
+      s += (f2_t)(bias ? bias[co] : 0.f);
+      v = s;
+      if (act) {
+        v[0] = po::leaky(s[0]);
+        v[1] = po::leaky(s[1]);
+      }
+    }
+    vmax[0] = fmaxf(vmax[0], fabsf(v[0]));
+    vmax[1] = fmaxf(vmax[1], fabsf(v[1]));
+    out[co] = v;
+  }
+  const bool live1 = pbase + 256 + tid < npix;
+  if (amax) po::amax_commit(amax, fmaxf(pbase + tid < npix ? vmax[0] : 0.f, live1 ? vmax[1] : 0.f));
+#pragma unroll
+  for (int q = 0; q < 2; ++q) {
+    if (q) __syncthreads();
+#pragma unroll
+    for (int co = 0; co < CO; ++co) ys[tid * LS + co] = out[co][q];
+    __syncthreads();
+    const int64_t hb = pbase + q * 256;
+    const int64_t nlive = min((int64_t)256, npix - hb);
+    float* yb = y + hb * CO;
+    for (int f = tid; f < nlive * (CO / 4); f += 256) {
+      const int px = f / (CO / 4), ch = (f % (CO / 4)) * 4;
+      const float* r = ys + px * LS + ch;
+      *reinterpret_cast<float4*>(yb + (int64_t)f * 4) = make_float4(r[0], r[1], r[2], r[3]);
+    }
+  }
+}
+
 template <int CO>
 __global__ __launch_bounds__(256) void first_dgrad_k(const float* __restrict__ D, int B, int H, int W,
                                                      int stride, int Ho, int Wo,
@@ -146,7 +232,14 @@ extern "C" int po_conv_first_fwd(const float* img, int B, int H, int W, int stri
   hipStream_t st = po::stream_of(s);
   const int CO = Cout_p <= 16 ? 16 : (Cout_p <= 32 ? 32 : 64);
   PO_REQUIRE(Cout_p == CO, "po_conv_first_fwd: Cout_p must be 16, 32 or 64 (got %d)", Cout_p);
-  if (CO == 16)
+  PO_REQUIRE((int64_t)B * 3 * H * W * 4 < (1LL << 31) && n + 512 < (1LL << 31),
+             "po_conv_first_fwd: image batch must be < 2 GiB");
+  dim3 grid2(po::ceil_div(n, 512));
+  if (CO == 16 && !getenv("PO_FIRST_V1"))
+    hipLaunchKernelGGL(first_fwd2_k<16>, grid2, dim3(256), 0, st, img, B, H, W, stride, Ho, Wo, Wt, bias, Cout, act, y, amax);
+  else if (CO == 32 && !getenv("PO_FIRST_V1"))
+    hipLaunchKernelGGL(first_fwd2_k<32>, grid2, dim3(256), 0, st, img, B, H, W, stride, Ho, Wo, Wt, bias, Cout, act, y, amax);
+  else if (CO == 16)
     hipLaunchKernelGGL(first_fwd_k<16>, grid, dim3(256), 0, st, img, B, H, W, stride, Ho, Wo, Wt, bias, Cout, Cout_p, act, y, amax);
   else if (CO == 32)
     hipLaunchKernelGGL(first_fwd_k<32>, grid, dim3(256), 0, st, img, B, H, W, stride, Ho, Wo, Wt, bias, Cout, Cout_p, act, y, amax);

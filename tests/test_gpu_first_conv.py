@@ -1,0 +1,58 @@
+"""po_conv_first_fwd (the 3-channel first Darknet conv, darknet_v3.py:9-100
+conv + BN-folded bias + LeakyReLU 0.1, cfg.py:37-56) on the GPU: the packed
+two-pixel kernel (first_fwd2_k) is bit-identical to the one-pixel kernel
+(first_fwd_k, PO_FIRST_V1=1) and matches a PyTorch fp32 conv within fp32
+rounding; ragged pixel counts (not a multiple of the 512-pixel block) and
+image borders (zero padding) are covered."""
+import ctypes
+import os
+
+import pytest
+import torch
+
+from conftest import pkg_mod
+
+pytestmark = pytest.mark.gpu
+
+
+def _run(img, w, b, stride, cout_p, act, v1=False):
+    nat = pkg_mod("_native")
+    B, _, H, W = img.shape
+    Ho, Wo = (H - 1) // stride + 1, (W - 1) // stride + 1
+    y = torch.full((B, Ho, Wo, cout_p), float("nan"), device=img.device)
+    amax = torch.zeros(nat.PO_AMAX_SUB, dtype=torch.int32, device=img.device)
+    old = os.environ.pop("PO_FIRST_V1", None)
+    try:
+        if v1:
+            os.environ["PO_FIRST_V1"] = "1"
+        nat.call("po_conv_first_fwd", nat.ptr(img), B, H, W, stride, nat.ptr(w), nat.ptr(b), w.size(0), cout_p,
+                 act, nat.ptr(y), nat.ptr(amax, torch.int32), nat.stream())
+        torch.cuda.synchronize()
+    finally:
+        os.environ.pop("PO_FIRST_V1", None)
+        if old is not None:
+            os.environ["PO_FIRST_V1"] = old
+    amax_f = amax.view(torch.float32).max().item()
+    return y, amax_f
+
+
+@pytest.mark.parametrize("B,H,W,stride,cout", [(2, 37, 53, 1, 32), (3, 29, 31, 2, 32), (1, 64, 64, 1, 16),
+                                              (1, 41, 23, 2, 16)])
+def test_first_fwd_packed_matches_v1_and_torch(B, H, W, stride, cout):
+    dev = torch.device("cuda", 0)
+    g = torch.Generator().manual_seed(B * 1000 + H)
+    img = torch.rand(B, 3, H, W, generator=g).to(dev)
+    w = (torch.randn(cout, 3, 3, 3, generator=g) * 0.3).to(dev)
+    b = (torch.randn(cout, generator=g) * 0.1).to(dev)
+    w27 = w.reshape(cout, 27).contiguous()
+    for act in (0, 1):
+        y2, m2 = _run(img, w27, b, stride, cout, act)
+        y1, m1 = _run(img, w27, b, stride, cout, act, v1=True)
+        assert torch.equal(y2, y1), "packed kernel differs from the one-pixel kernel"
+        assert m2 == m1
+        ref = torch.nn.functional.conv2d(img.cpu().double(), w.cpu().double(), b.cpu().double(), stride, 1)
+        if act:
+            ref = torch.nn.functional.leaky_relu(ref, 0.1)
+        ref = ref.permute(0, 2, 3, 1).float()
+        torch.testing.assert_close(y2.cpu(), ref, rtol=1e-5, atol=1e-5)
+        assert abs(m2 - ref.abs().max().item()) <= 1e-5 * max(1.0, m2)
