@@ -242,49 +242,73 @@ __global__ __launch_bounds__(256) void conv_k(const ConvArgs a) {
 }
 
 // Split-K reduction + epilogue: one thread per 4 output channels of a row.
+// The slices are summed in split order (deterministic); their loads are
+// issued four at a time so that a thread has four 16-byte reads in flight
+// instead of one dependent read per slice.  Every epilogue operand is moved
+// as one 16-byte vector (o is a multiple of 4 floats).  32-bit indices: the
+// host checks M * N < 2^31.
+__device__ __forceinline__ float4 ld4(const float* p) { return *reinterpret_cast<const float4*>(p); }
+__device__ __forceinline__ void st4(float* p, float x, float y, float z, float w) {
+  *reinterpret_cast<float4*>(p) = make_float4(x, y, z, w);
+}
+__device__ __forceinline__ void add4(float4& v, const float4 p) { v.x += p.x; v.y += p.y; v.z += p.z; v.w += p.w; }
+
 __global__ __launch_bounds__(256) void conv_reduce_k(const ConvArgs a) {
-  const int64_t t0 = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  const int n4 = a.N / 4;
-  const int64_t t = t0 < (int64_t)a.M * n4 ? t0 : 0;
+  const int t0 = (int)blockIdx.x * 256 + (int)threadIdx.x;
+  const int n4 = a.N >> 2;
+  const int tot = a.M * n4;
+  const int t = t0 < tot ? t0 : 0;
   const int sh = po::input_shift(a) + (a.prec == 1 ? a.w_shift : 0);
-  const int m = (int)(t / n4), n = (int)(t - (int64_t)m * n4) * 4;
+  const int m = t / n4, n = (t - m * n4) * 4;
   int b, i, j;
-  const bool live = t0 < (int64_t)a.M * n4 && po::grid_point(a, m, b, i, j);
+  const bool live = t0 < tot && po::grid_point(a, m, b, i, j);
   const size_t pix = live ? (size_t)(b * a.Hout + i * a.out_step + a.out_oy) * a.Wout + j * a.out_step + a.out_ox : 0;
   float my = 0.f, ms = 0.f, my2 = 0.f;
   uint32_t nib = 0;
   if (live) {
-    float4 v = *reinterpret_cast<const float4*>(a.ws + (size_t)m * a.N + n);
-    for (int s = 1; s < a.ksplit; ++s) {
-      const float4 p = *reinterpret_cast<const float4*>(a.ws + ((size_t)s * a.M + m) * a.N + n);
-      v.x += p.x; v.y += p.y; v.z += p.z; v.w += p.w;
+    const size_t slice = (size_t)a.M * a.N;
+    const float* wp = a.ws + (size_t)m * a.N + n;
+    float4 v = ld4(wp);
+    int s = 1;
+    for (; s + 3 < a.ksplit; s += 4) {
+      const float4 p0 = ld4(wp + s * slice), p1 = ld4(wp + (s + 1) * slice);
+      const float4 p2 = ld4(wp + (s + 2) * slice), p3 = ld4(wp + (s + 3) * slice);
+      add4(v, p0); add4(v, p1); add4(v, p2); add4(v, p3);
     }
+    for (; s < a.ksplit; ++s) add4(v, ld4(wp + s * slice));
     const size_t o = pix * a.Cout_p + n;
     float r[4] = {v.x, v.y, v.z, v.w};
     const size_t wo = pix * (size_t)(a.Cout_p >> 5) + (n >> 5);
     const float4 g1 = a.mbits ? po::leaky_grad_bits(a.mbits[wo], n) : make_float4(0.f, 0.f, 0.f, 0.f);
     const float4 g2 = a.m2bits ? po::leaky_grad_bits(a.m2bits[wo], n) : make_float4(0.f, 0.f, 0.f, 0.f);
+    const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
+    const float4 yin = a.accumulate ? ld4(a.y + o) : z4;
+    const float4 mk = (!a.mbits && a.mask) ? ld4(a.mask + o) : z4;
+    const float4 rs = a.res ? ld4(a.res + o) : z4;
+    const float4 mk2 = (a.y2 && !a.m2bits) ? ld4(a.mask2 + o) : z4;
+    const float4 bs = a.bias ? ld4(a.bias + n) : z4;
     const float g1v[4] = {g1.x, g1.y, g1.z, g1.w}, g2v[4] = {g2.x, g2.y, g2.z, g2.w};
+    const float yiv[4] = {yin.x, yin.y, yin.z, yin.w}, mkv[4] = {mk.x, mk.y, mk.z, mk.w};
+    const float rsv[4] = {rs.x, rs.y, rs.z, rs.w}, mk2v[4] = {mk2.x, mk2.y, mk2.z, mk2.w};
+    const float bsv[4] = {bs.x, bs.y, bs.z, bs.w};
+    float yo[4], so[4], y2o[4];
 #pragma unroll
     for (int c = 0; c < 4; ++c) {
-      float x = __builtin_ldexpf(r[c], -sh) + (a.bias ? a.bias[n + c] : 0.f);
+      float x = __builtin_ldexpf(r[c], -sh) + bsv[c];
       if (a.act) x = po::leaky(x);
-      if (a.accumulate) x += a.y[o + c];
-      const float yv = a.mbits ? x * g1v[c] : (a.mask ? x * po::leaky_grad(a.mask[o + c]) : x);
-      if (a.y) a.y[o + c] = yv;
+      if (a.accumulate) x += yiv[c];
+      const float yv = a.mbits ? x * g1v[c] : (a.mask ? x * po::leaky_grad(mkv[c]) : x);
+      yo[c] = yv;
       nib |= (yv > 0.f ? 1u : 0u) << c;
       my = fmaxf(my, fabsf(yv));
-      if (a.res) {
-        const float sv = x + a.res[o + c];
-        a.sum[o + c] = sv;
-        ms = fmaxf(ms, fabsf(sv));
-      }
-      if (a.y2) {
-        const float v2 = x * (a.m2bits ? g2v[c] : po::leaky_grad(a.mask2[o + c]));
-        a.y2[o + c] = v2;
-        my2 = fmaxf(my2, fabsf(v2));
-      }
+      so[c] = x + rsv[c];
+      if (a.res) ms = fmaxf(ms, fabsf(so[c]));
+      y2o[c] = x * (a.m2bits ? g2v[c] : po::leaky_grad(mk2v[c]));
+      if (a.y2) my2 = fmaxf(my2, fabsf(y2o[c]));
     }
+    if (a.y) st4(a.y + o, yo[0], yo[1], yo[2], yo[3]);
+    if (a.res) st4(a.sum + o, so[0], so[1], so[2], so[3]);
+    if (a.y2) st4(a.y2 + o, y2o[0], y2o[1], y2o[2], y2o[3]);
   }
   if (a.ybits) {
     // threads 8k .. 8k+7 hold the 32 channels of one sign-bit word (N % 32 == 0)
@@ -306,6 +330,7 @@ int launch(const ConvArgs& a, hipStream_t st) {
   const int ntiles = po::ceil_div(a.M, BM) * b.ntiles_n;
   hipLaunchKernelGGL((conv_k<BM, BN, WM, BK, GL>), dim3(ntiles, a.ksplit), dim3(256), 0, st, b);
   if (a.ksplit > 1) {
+    PO_REQUIRE((int64_t)a.M * a.N < (1LL << 31), "po_conv: split-K output too large");
     int rc = po::check_launch("po_conv");
     if (rc) return rc;
     hipLaunchKernelGGL(conv_reduce_k, dim3(po::ceil_div((int64_t)a.M * (a.N / 4), 256)), dim3(256), 0, st, b);
@@ -471,6 +496,7 @@ extern "C" int po_conv(const po_conv_desc* d, const float* in, const float* W, c
   if (a.prec == 1) {
     ConvArgs b = a;
     b.ntiles_n = po::ceil_div(a.N, bn);
+    PO_REQUIRE(a.ksplit == 1 || (int64_t)a.M * a.N < (1LL << 31), "po_conv: split-K output too large");
     rc = po::launch_h3(b, st, bm, bn, bk, gl);
     if (rc == PO_OK && a.ksplit > 1) {
       hipLaunchKernelGGL(conv_reduce_k, dim3(po::ceil_div((int64_t)a.M * (a.N / 4), 256)), dim3(256), 0, st, b);

@@ -205,6 +205,61 @@ __global__ __launch_bounds__(256) void nhwc2nchw_k(const float* __restrict__ s, 
   d[t] = s[(((int64_t)b * H + y) * W + x) * Cp + c];
 }
 
+// po_view_move with every channel offset and stride a multiple of 4: one
+// thread per 4 channels (16-byte loads/stores), 32-bit index math (host check)
+__device__ __forceinline__ float4 vm_at4(const float* __restrict__ src, int b, int Hs, int Ws, int ss, int so, int c,
+                                         int ly, int lx) {
+  if (ly < 0 || ly >= Hs || lx < 0 || lx >= Ws) return make_float4(0.f, 0.f, 0.f, 0.f);
+  return *reinterpret_cast<const float4*>(src + ((size_t)(b * Hs + ly) * Ws + lx) * ss + so + c);
+}
+
+__global__ __launch_bounds__(256) void view_move4_k(const float* __restrict__ src, int Hs, int Ws, int ss, int so,
+                                                    const int32_t* __restrict__ sorg, float* __restrict__ dst,
+                                                    int Hd, int Wd, int ds, int doff,
+                                                    const int32_t* __restrict__ dorg, int B, int C4, int mode,
+                                                    int acc, const float* __restrict__ my, int ms,
+                                                    uint32_t* __restrict__ amax) {
+  const int t0 = (int)blockIdx.x * 256 + (int)threadIdx.x;
+  const int tot = B * Hd * Wd * C4;
+  const bool live = t0 < tot;
+  const int t = live ? t0 : 0;
+  const int p = t / C4;
+  const int c = (t - p * C4) * 4;
+  const int b = p / (Hd * Wd);
+  const int r = p - b * Hd * Wd;
+  const int y = r / Wd, x = r - y * Wd;
+  const int py = y + (dorg ? dorg[2 * b] : 0), px = x + (dorg ? dorg[2 * b + 1] : 0);
+  const int oy = sorg ? sorg[2 * b] : 0, ox = sorg ? sorg[2 * b + 1] : 0;
+  float vm = 0.f;
+  if (live) {
+    float4 v;
+    if (mode == 0) {
+      v = vm_at4(src, b, Hs, Ws, ss, so, c, py - oy, px - ox);
+    } else if (mode == 1) {
+      v = vm_at4(src, b, Hs, Ws, ss, so, c, (py >> 1) - oy, (px >> 1) - ox);
+    } else {
+      const float4 a0 = vm_at4(src, b, Hs, Ws, ss, so, c, 2 * py - oy, 2 * px - ox);
+      const float4 a1 = vm_at4(src, b, Hs, Ws, ss, so, c, 2 * py - oy, 2 * px + 1 - ox);
+      const float4 a2 = vm_at4(src, b, Hs, Ws, ss, so, c, 2 * py + 1 - oy, 2 * px - ox);
+      const float4 a3 = vm_at4(src, b, Hs, Ws, ss, so, c, 2 * py + 1 - oy, 2 * px + 1 - ox);
+      v = make_float4((a0.x + a1.x) + (a2.x + a3.x), (a0.y + a1.y) + (a2.y + a3.y),
+                      (a0.z + a1.z) + (a2.z + a3.z), (a0.w + a1.w) + (a2.w + a3.w));
+    }
+    float4* d = reinterpret_cast<float4*>(dst + (size_t)p * ds + doff + c);
+    if (acc) {
+      const float4 o = *d;
+      v.x += o.x; v.y += o.y; v.z += o.z; v.w += o.w;
+    }
+    if (my) {
+      const float4 m = *reinterpret_cast<const float4*>(my + (size_t)p * ms + c);
+      v.x *= po::leaky_grad(m.x); v.y *= po::leaky_grad(m.y); v.z *= po::leaky_grad(m.z); v.w *= po::leaky_grad(m.w);
+    }
+    *d = v;
+    vm = fmaxf(fmaxf(fabsf(v.x), fabsf(v.y)), fmaxf(fabsf(v.z), fabsf(v.w)));
+  }
+  if (amax) po::amax_commit(amax, vm);
+}
+
 __global__ __launch_bounds__(256) void nchw2nhwc_k(const float* __restrict__ s, int B, int H, int W, int C,
                                                    int Cp, float* __restrict__ d) {
   const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
@@ -240,6 +295,16 @@ extern "C" int po_view_move(const float* src, int Hs, int Ws, int src_stride, in
   PO_REQUIRE(!mask_y || C <= mask_stride, "po_view_move: mask stride");
   const int64_t tot = (int64_t)B * Hd * Wd * C;
   if (!tot) return PO_OK;
+  const bool v4 = C % 4 == 0 && src_stride % 4 == 0 && src_off % 4 == 0 && dst_stride % 4 == 0 && dst_off % 4 == 0 &&
+                  (!mask_y || mask_stride % 4 == 0) && ((uintptr_t)src | (uintptr_t)dst | (uintptr_t)mask_y) % 16 == 0 &&
+                  tot + 1024 < (1LL << 31) && (int64_t)B * Hs * Ws * src_stride < (1LL << 31) &&
+                  !getenv("PO_VIEW_MOVE_V1");
+  if (v4) {
+    hipLaunchKernelGGL(view_move4_k, dim3(po::ceil_div(tot / 4, 256)), dim3(256), 0, po::stream_of(s), src, Hs, Ws,
+                       src_stride, src_off, src_org, dst, Hd, Wd, dst_stride, dst_off, dst_org, B, C / 4, mode,
+                       accumulate, mask_y, mask_stride, amax);
+    return po::check_launch("po_view_move");
+  }
   hipLaunchKernelGGL(view_move_k, dim3(po::ceil_div(tot, 256)), dim3(256), 0, po::stream_of(s), src, Hs, Ws,
                      src_stride, src_off, src_org, dst, Hd, Wd, dst_stride, dst_off, dst_org, B, C, mode,
                      accumulate, mask_y, mask_stride, amax);
