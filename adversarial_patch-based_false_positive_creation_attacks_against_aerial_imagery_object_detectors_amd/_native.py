@@ -73,6 +73,8 @@ _SIGS = {
                         c_void_p, c_void_p],
     "po_maxpool2_bwd": [c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_int, c_void_p, c_int,
                         c_void_p, c_void_p, c_void_p],
+    "po_maxpool2_bwd_box": [c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_int, c_void_p, c_int,
+                            c_void_p, c_void_p, c_void_p, c_void_p],
     "po_nhwc_to_nchw": [c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p, c_void_p],
     "po_nchw_to_nhwc": [c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p, c_void_p],
 }

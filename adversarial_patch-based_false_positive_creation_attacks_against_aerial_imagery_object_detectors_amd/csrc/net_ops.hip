@@ -147,6 +147,43 @@ __global__ __launch_bounds__(256) void maxpool2_fwd_k(const float* __restrict__ 
 
 // gather form: each source pixel sums, in window-position order, the outputs
 // whose argmax selected it
+// One (pixel, 4 channels) of the max-pool input gradient: the window
+// positions k of the (up to 4) outputs whose window holds the pixel.
+__device__ __forceinline__ float mp_bwd_px(const float* __restrict__ dd, const int8_t* __restrict__ am, int b, int y,
+                                           int x, int c, int H, int W, int C, int Cp, int stride, int Ho, int Wo,
+                                           float* __restrict__ ds, int acc, const float* __restrict__ my) {
+  float v[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const int ty = y - (k >> 1), tx = x - (k & 1);
+    if (ty < 0 || tx < 0 || ty % stride || tx % stride) continue;
+    const int oy = ty / stride, ox = tx / stride;
+    if (oy >= Ho || ox >= Wo) continue;
+    const int64_t o = (((int64_t)b * Ho + oy) * Wo + ox) * Cp + c;
+    const char4 a = *reinterpret_cast<const char4*>(am + o);
+    const float4 g = *reinterpret_cast<const float4*>(dd + o);
+    if (a.x == k) v[0] += g.x;
+    if (a.y == k) v[1] += g.y;
+    if (a.z == k) v[2] += g.z;
+    if (a.w == k) v[3] += g.w;
+  }
+#pragma unroll
+  for (int u = 0; u < 4; ++u)
+    if (c + u >= C) v[u] = 0.f;
+  const int64_t t = (((int64_t)b * H + y) * W + x) * Cp + c;
+  if (acc) {
+    const float4 p = *reinterpret_cast<const float4*>(ds + t);
+    v[0] += p.x; v[1] += p.y; v[2] += p.z; v[3] += p.w;
+  }
+  if (my) {
+    const float4 m = *reinterpret_cast<const float4*>(my + t);
+    v[0] *= po::leaky_grad(m.x); v[1] *= po::leaky_grad(m.y);
+    v[2] *= po::leaky_grad(m.z); v[3] *= po::leaky_grad(m.w);
+  }
+  *reinterpret_cast<float4*>(ds + t) = make_float4(v[0], v[1], v[2], v[3]);
+  return fmaxf(fmaxf(fabsf(v[0]), fabsf(v[1])), fmaxf(fabsf(v[2]), fabsf(v[3])));
+}
+
 __global__ __launch_bounds__(256) void maxpool2_bwd_k(const float* __restrict__ dd,
                                                       const int8_t* __restrict__ am, int B, int H, int W,
                                                       int C, int Cp, int stride, int Ho, int Wo,
@@ -159,36 +196,36 @@ __global__ __launch_bounds__(256) void maxpool2_bwd_k(const float* __restrict__ 
   float vmax = 0.f;
   if (q < W * c4n) {
     const int x = q / c4n, c = (q - x * c4n) * 4;
-    float v[4] = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      const int ty = y - (k >> 1), tx = x - (k & 1);
-      if (ty < 0 || tx < 0 || ty % stride || tx % stride) continue;
-      const int oy = ty / stride, ox = tx / stride;
-      if (oy >= Ho || ox >= Wo) continue;
-      const int64_t o = (((int64_t)b * Ho + oy) * Wo + ox) * Cp + c;
-      const char4 a = *reinterpret_cast<const char4*>(am + o);
-      const float4 g = *reinterpret_cast<const float4*>(dd + o);
-      if (a.x == k) v[0] += g.x;
-      if (a.y == k) v[1] += g.y;
-      if (a.z == k) v[2] += g.z;
-      if (a.w == k) v[3] += g.w;
-    }
-#pragma unroll
-    for (int u = 0; u < 4; ++u)
-      if (c + u >= C) v[u] = 0.f;
-    const int64_t t = ((int64_t)row * W + x) * Cp + c;
-    if (acc) {
-      const float4 p = *reinterpret_cast<const float4*>(ds + t);
-      v[0] += p.x; v[1] += p.y; v[2] += p.z; v[3] += p.w;
-    }
-    if (my) {
-      const float4 m = *reinterpret_cast<const float4*>(my + t);
-      v[0] *= po::leaky_grad(m.x); v[1] *= po::leaky_grad(m.y);
-      v[2] *= po::leaky_grad(m.z); v[3] *= po::leaky_grad(m.w);
-    }
-    *reinterpret_cast<float4*>(ds + t) = make_float4(v[0], v[1], v[2], v[3]);
-    vmax = fmaxf(fmaxf(fabsf(v[0]), fabsf(v[1])), fmaxf(fabsf(v[2]), fabsf(v[3])));
+    vmax = mp_bwd_px(dd, am, b, y, x, c, H, W, C, Cp, stride, Ho, Wo, ds, acc, my);
+  }
+  if (amax) po::amax_commit(amax, vmax);
+}
+
+// Gradient-cone form: only the pixels of each image's box (boxes[4 b ..] =
+// r0, c0, r1, c1, half-open, from po_grad_boxes) are written; the rest of
+// d_src is left as it is (nothing downstream of the cone reads it).  Grid
+// (B, rows): workgroup (b, r) walks rows r0 + r, r0 + r + gridDim.y, ... of the
+// box, its threads the box's columns x channel quads.
+__global__ __launch_bounds__(256) void maxpool2_bwd_box_k(const float* __restrict__ dd,
+                                                          const int8_t* __restrict__ am, int B, int H, int W,
+                                                          int C, int Cp, int stride, int Ho, int Wo,
+                                                          float* __restrict__ ds, int acc,
+                                                          const float* __restrict__ my,
+                                                          const int32_t* __restrict__ boxes,
+                                                          uint32_t* __restrict__ amax) {
+  const int b = blockIdx.x;
+  const int4 bx = reinterpret_cast<const int4*>(boxes)[b];
+  const int r0 = max(bx.x, 0), c0 = max(bx.y, 0), r1 = min(bx.z, H), c1 = min(bx.w, W);
+  const int c4n = Cp >> 2;
+  const int nq = (c1 - c0) * c4n;
+  float vmax = 0.f;
+  if (c1 > c0) {
+    for (int y = r0 + (int)blockIdx.y; y < r1; y += (int)gridDim.y)
+      for (int q = threadIdx.x; q < nq; q += 256) {
+        const int xr = q / c4n;
+        vmax = fmaxf(vmax, mp_bwd_px(dd, am, b, y, c0 + xr, (q - xr * c4n) * 4, H, W, C, Cp, stride, Ho, Wo, ds,
+                                     acc, my));
+      }
   }
   if (amax) po::amax_commit(amax, vmax);
 }
@@ -361,6 +398,23 @@ extern "C" int po_maxpool2_bwd(const float* d_dst, const int8_t* argmax, int B, 
                      po::stream_of(s), d_dst, argmax, B, H, W, C, Cp, stride, Ho, Wo, d_src, accumulate, mask_y,
                      amax);
   return po::check_launch("po_maxpool2_bwd");
+}
+
+extern "C" int po_maxpool2_bwd_box(const float* d_dst, const int8_t* argmax, int B, int H, int W, int C, int Cp,
+                                   int stride, float* d_src, int accumulate, const float* mask_y,
+                                   const int32_t* boxes, uint32_t* amax, po_stream_t s) {
+  if (!boxes)
+    return po_maxpool2_bwd(d_dst, argmax, B, H, W, C, Cp, stride, d_src, accumulate, mask_y, amax, s);
+  PO_REQUIRE(d_dst && argmax && d_src && (stride == 1 || stride == 2), "po_maxpool2_bwd_box: bad argument");
+  int Ho, Wo;
+  pool_out(H, W, stride, Ho, Wo);
+  PO_REQUIRE(Cp % 4 == 0 && B < 65536 && (int64_t)W * Cp < (1LL << 30),
+             "po_maxpool2_bwd_box: Cp %d must be a multiple of 4 (sizes within 32-bit grids)", Cp);
+  if ((int64_t)B * H * W == 0) return PO_OK;
+  const int rows = H < 32 ? H : 32;
+  hipLaunchKernelGGL(maxpool2_bwd_box_k, dim3(B, rows), dim3(256), 0, po::stream_of(s), d_dst, argmax, B, H, W, C,
+                     Cp, stride, Ho, Wo, d_src, accumulate, mask_y, boxes, amax);
+  return po::check_launch("po_maxpool2_bwd_box");
 }
 
 extern "C" int po_nhwc_to_nchw(const float* src, int B, int H, int W, int C, int Cp, float* dst,

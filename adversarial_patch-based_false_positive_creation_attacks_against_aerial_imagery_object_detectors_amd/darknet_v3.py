@@ -893,8 +893,12 @@ class NetPlan:
                 s_ = self.srcs[j][0]
                 acc, mask, final = contrib(s_)
                 hs, ws_, cs = self.shp[s_]
-                bwd.append(("po_maxpool2_bwd", (P(G), P(self.argmax[j]), B, hs, ws_, cs, self.cp[s_], int(d["stride"]),
-                                                P(self.grad[s_]), acc, P(mask), self.slot(self.grad[s_])), None))
+                # on a gradient-cone source only its per-image boxes are written
+                cone = self._cone_ptr(s_, 0)
+                bwd.append(("po_maxpool2_bwd_box", (P(G), P(self.argmax[j]), B, hs, ws_, cs, self.cp[s_],
+                                                    int(d["stride"]), P(self.grad[s_]), acc, P(mask),
+                                                    nat.c_void_p(cone) if cone else None,
+                                                    self.slot(self.grad[s_])), None))
                 fallback_dual(s_, final)
         self.bwd_ops = bwd
 

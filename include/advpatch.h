@@ -33,7 +33,7 @@ typedef void* po_stream_t;
 #define PO_EHIP -2     /* HIP runtime error */
 #define PO_EDEVICE -3  /* device is not gfx950 */
 
-#define PO_ABI_VERSION 7
+#define PO_ABI_VERSION 8
 #define PO_AMAX_SUB 64  /* sub-slots per max|x| slot (see po_conv_desc) */
 
 int po_abi_version(void);
@@ -323,6 +323,12 @@ int po_maxpool2_fwd(const float* src, int B, int H, int W, int C, int Cp, int st
 int po_maxpool2_bwd(const float* d_dst, const int8_t* argmax, int B, int H, int W, int C, int Cp,
                     int stride, float* d_src, int accumulate, const float* mask_y,
                     uint32_t* amax, po_stream_t s);
+/* po_maxpool2_bwd restricted to each image's gradient-cone box (boxes[4 b ..]
+ * = r0, c0, r1, c1 half-open in the d_src map, from po_grad_boxes); pixels
+ * outside the box are not written.  boxes == NULL: the full map. */
+int po_maxpool2_bwd_box(const float* d_dst, const int8_t* argmax, int B, int H, int W, int C, int Cp,
+                        int stride, float* d_src, int accumulate, const float* mask_y,
+                        const int32_t* boxes, uint32_t* amax, po_stream_t s);
 
 /* NCHW [B,C,H,W] <-> NHWC [B,H,W,Cp] layout conversion (heads in and out of
  * the drop-in Darknet.forward API). */

@@ -98,8 +98,10 @@ def test_grad_boxes_match_host_restatement(tmp_path):
         assert plan.cone_boxes[j].cpu().tolist() == [[0, 0, H, W]] * B
 
 
-@pytest.mark.parametrize("prec", ["fp32", "fp16x3"])
-def test_cones_leave_the_patch_gradient_unchanged(tmp_path, monkeypatch, prec):
+@pytest.mark.parametrize("cfg,S,prec", [("builtin:yolov3-dota", 608, "fp32"), ("builtin:yolov3-dota", 608, "fp16x3"),
+                                        ("builtin:yolov3-tiny-dota", 416, "fp32"),
+                                        ("builtin:yolov3-tiny-dota", 416, "fp16x3")])
+def test_cones_leave_the_patch_gradient_unchanged(tmp_path, monkeypatch, cfg, S, prec):
     """With the built-in tile choice (no autotuning) the boxed dgrads run the
     same tiles as the full ones: exact fp32 operands give the identical patch
     gradient; fp16x3 differs only through the max|x| operand scales (a boxed
@@ -111,8 +113,8 @@ def test_cones_leave_the_patch_gradient_unchanged(tmp_path, monkeypatch, prec):
     out = []
     for cones in ("1", "0"):
         monkeypatch.setenv("ADVPATCH_GRAD_CONES", cones)
-        tr, _ = _trainer("builtin:yolov3-dota", tmp_path, prec=prec)
-        img, lab = sy.frames(B, 608, seed=90).to(DEV), sy.labels(B, seed=91).to(DEV)
+        tr, _ = _trainer(cfg, tmp_path, prec=prec)
+        img, lab = sy.frames(B, S, seed=90).to(DEV), sy.labels(B, seed=91).to(DEV)
         dr = {k: v.to(DEV) for k, v in sy.draws(B, P, seed=93).items()}
         pg = sy.patch(P, seed=92).to(DEV).requires_grad_(True)
         loss, terms = tr.losses(pg, img, lab, dr)
@@ -126,6 +128,42 @@ def test_cones_leave_the_patch_gradient_unchanged(tmp_path, monkeypatch, prec):
     else:
         rel = float((g1 - g0).abs().max() / g0.abs().max())
         assert rel < 1e-5, rel
+
+
+@pytest.mark.parametrize("stride,H,W", [(2, 22, 18), (1, 13, 13)])
+def test_boxed_maxpool_bwd_matches_full(stride, H, W):
+    """po_maxpool2_bwd_box: inside each image's box the values of the full
+    po_maxpool2_bwd (accumulate + leaky mask), outside it d_src untouched;
+    an empty box writes nothing, boxes == NULL is the full kernel."""
+    nat = pkg_mod("_native")
+    B, C, Cp = 4, 20, 32
+    Ho, Wo = (H // 2, W // 2) if stride == 2 else (H, W)
+    gen = torch.Generator().manual_seed(11)
+    src = torch.randn(B, H, W, Cp, generator=gen).to(DEV)
+    dst = torch.empty(B, Ho, Wo, Cp, device=DEV)
+    am = torch.zeros(B, Ho, Wo, Cp, dtype=torch.int8, device=DEV)
+    nat.call("po_maxpool2_fwd", nat.ptr(src), B, H, W, C, Cp, stride, nat.ptr(dst), nat.ptr(am, torch.int8), None,
+             nat.stream())
+    g = torch.randn(B, Ho, Wo, Cp, generator=gen).to(DEV)
+    prev = torch.randn(B, H, W, Cp, generator=gen).to(DEV)
+    mask = torch.randn(B, H, W, Cp, generator=gen).to(DEV)
+    boxes = torch.tensor([[2, 3, 9, 11], [0, 0, H, W], [5, 5, 5, 8], [H - 3, W - 4, H + 2, W + 5]],
+                         dtype=torch.int32, device=DEV)
+    full, boxed, nobox = prev.clone(), prev.clone(), prev.clone()
+    nat.call("po_maxpool2_bwd", nat.ptr(g), nat.ptr(am, torch.int8), B, H, W, C, Cp, stride, nat.ptr(full), 1,
+             nat.ptr(mask), None, nat.stream())
+    nat.call("po_maxpool2_bwd_box", nat.ptr(g), nat.ptr(am, torch.int8), B, H, W, C, Cp, stride, nat.ptr(boxed), 1,
+             nat.ptr(mask), nat.ptr(boxes, torch.int32), None, nat.stream())
+    nat.call("po_maxpool2_bwd_box", nat.ptr(g), nat.ptr(am, torch.int8), B, H, W, C, Cp, stride, nat.ptr(nobox), 1,
+             nat.ptr(mask), None, None, nat.stream())
+    torch.cuda.synchronize()
+    assert torch.equal(nobox, full)
+    inside = torch.zeros(B, H, W, dtype=torch.bool)
+    for b, (r0, c0, r1, c1) in enumerate(boxes.cpu().tolist()):
+        inside[b, max(r0, 0):min(r1, H), max(c0, 0):min(c1, W)] = True
+    inside = inside.to(DEV)
+    assert torch.equal(boxed[inside], full[inside])
+    assert torch.equal(boxed[~inside], prev[~inside])
 
 
 def test_halo_tiles_refuse_boxes():

@@ -4,7 +4,7 @@
 #   2. rocprofv3 --kernel-trace --stats of the same bench command
 #   3. two PMC passes (FETCH_SIZE, WRITE_SIZE: they do not fit one TCC pass)
 #   then, back in the build container after gpurun merged gpurun_out/:
-#   python tools/pmc_summary.py gpurun_out/prof_<round>_<cfg> <round> <cfg> <B> 12
+#   python tools/pmc_summary.py gpurun_out/prof_<round>_<cfg> <round> <cfg> <B> 22
 #   -> profiles/<round>/ + profiles/traffic_<cfg>_b<B>.json
 # Usage: tools/profile_round.sh ROUND [CONFIG] [BATCH]
 set -e
@@ -27,5 +27,5 @@ timeout -k 10 400 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/pmc_fe
 timeout -k 10 400 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/pmc_write" -o run -- python $BENCH \
     > "$OUT/bench_write.json" 2> "$OUT/pmc_write.err"
 tools/conv_traffic.sh "$OUT/conv_traffic" "$CFG" > "$OUT/conv_traffic.log" 2>&1
-python tools/pmc_summary.py "$OUT" "$ROUND" "$CFG" "$BATCH" $((STEPS + WARM)) > "$OUT/summary.txt"
+python tools/pmc_summary.py "$OUT" "$ROUND" "$CFG" "$BATCH" $((2 * STEPS + WARM)) > "$OUT/summary.txt"
 python tools/conv_traffic.py "$OUT/conv_traffic" --top 60 > "$OUT/conv_traffic.txt"
