@@ -360,6 +360,11 @@ __global__ __launch_bounds__(256) void warp_bwd_a_k(const float* __restrict__ d_
 
 // Backward phase B: per patch element (pr, pc), gather over images and over the
 // output pixels whose bilinear footprint covers padded-input pixel (pr+padT, pc+padL).
+// A workgroup holds WB_EL patch elements x WB_G image groups: group q sums the
+// images q, q + WB_G, ... in increasing order, then the WB_G partials are added
+// in group order through LDS (deterministic, no atomics, no workspace); the
+// batch is spread over WB_G x more workgroups than one thread per element.
+constexpr int WB_EL = 32, WB_G = 8;
 __global__ __launch_bounds__(256) void warp_bwd_b_k(const float* __restrict__ gfac,
                                                     const float* __restrict__ mp,
                                                     const float* __restrict__ noise,
@@ -367,14 +372,17 @@ __global__ __launch_bounds__(256) void warp_bwd_b_k(const float* __restrict__ gf
                                                     const float* __restrict__ bright,
                                                     const float* __restrict__ theta, WarpGeom g,
                                                     int B, float* __restrict__ d_mp) {
-  const int e = blockIdx.x * 256 + threadIdx.x;
-  if (e >= g.P * g.P) return;
+  __shared__ float part[3][WB_G][WB_EL];
+  const int el = threadIdx.x % WB_EL, q = threadIdx.x / WB_EL;
+  const int e0 = blockIdx.x * WB_EL + el;
+  const bool live = e0 < g.P * g.P;
+  const int e = live ? e0 : 0;
   const int pr = e / g.P, pc = e % g.P;
   const int r = pr + g.padT, c = pc + g.padL;
   const size_t plane = (size_t)g.S * g.S;
   const float fS = (float)g.S, half = 0.5f - 0.5f * fS;
   float d0 = 0.f, d1 = 0.f, d2 = 0.f;
-  for (int b = 0; b < B; ++b) {
+  for (int b = q; b < (live ? B : 0); b += WB_G) {
     const float* th = theta + 6 * b;
     // pixel-space affine: ix = A00 j + A01 i + A02, iy = A10 j + A11 i + A12
     const float A00 = th[0], A01 = th[1], A10 = th[3], A11 = th[4];
@@ -426,10 +434,16 @@ __global__ __launch_bounds__(256) void warp_bwd_b_k(const float* __restrict__ gf
     }
     d0 += dd[0]; d1 += dd[1]; d2 += dd[2];
   }
-  const size_t pp = (size_t)g.P * g.P;
-  d_mp[e] = d0;
-  d_mp[e + pp] = d1;
-  d_mp[e + 2 * pp] = d2;
+  part[0][q][el] = d0;
+  part[1][q][el] = d1;
+  part[2][q][el] = d2;
+  __syncthreads();
+  if (q < 3 && live) {
+    float t = part[q][0][el];
+#pragma unroll
+    for (int k = 1; k < WB_G; ++k) t += part[q][k][el];
+    d_mp[e + (size_t)q * g.P * g.P] = t;
+  }
 }
 
 WarpGeom make_geom(int S, int P) {
@@ -468,7 +482,7 @@ extern "C" int po_warp_bwd(const float* d_out, const float* patch_mp, const floa
                      contrast, bright, theta, g, mode, work);
   int rc = po::check_launch("po_warp_bwd(a)");
   if (rc) return rc;
-  hipLaunchKernelGGL(warp_bwd_b_k, dim3(po::ceil_div(P * P, 256)), dim3(256), 0, po::stream_of(s),
+  hipLaunchKernelGGL(warp_bwd_b_k, dim3(po::ceil_div(P * P, WB_EL)), dim3(256), 0, po::stream_of(s),
                      work, patch_mp, noise, contrast, bright, theta, g, B, d_patch_mp);
   return po::check_launch("po_warp_bwd(b)");
 }
