@@ -1,7 +1,8 @@
 // Loss head: per-anchor objectness/class extraction at the patch cell and the
 // creation-attack losses (reference train_patch.py:428-548, 230-253), forward
 // and the sparse gradient into the head tensors.  One workgroup; one thread per
-// image; the batch means are summed by thread 0 in image order (deterministic).
+// (image, anchor), per-image reductions in anchor order, and the batch means
+// summed by thread 0 in image order (deterministic).
 #pragma clang fp contract(off)
 #include "common.h"
 #include <math.h>
@@ -23,30 +24,36 @@ struct LossArgs {
 
 __device__ __forceinline__ float sigm(float x) { return 1.f / (1.f + expf(-x)); }
 
+// One thread per (image, anchor) of a chunk of CL_IMG images (the anchors'
+// sigmoid / class / CE work runs in parallel); then one thread per image of
+// the chunk takes the first-index max objectness and sums the class terms in
+// anchor order, as the one-thread-per-image form did (same values, same order).
+constexpr int CL_IMG = 16;
 __global__ __launch_bounds__(256) void cell_loss_k(LossArgs a, const float* __restrict__ center,
                                                    float* __restrict__ out2, float* __restrict__ obj_out,
                                                    float* __restrict__ cls_out, int32_t* __restrict__ cells,
                                                    int32_t* __restrict__ flags) {
   __shared__ float s_max[MAXB];
   __shared__ float s_cls[MAXB];
+  __shared__ float c_obj[CL_IMG][3 * MAXH];
+  __shared__ float c_cls[CL_IMG][3 * MAXH];
+  __shared__ int c_off[CL_IMG][MAXH];
   __shared__ int s_flag;
   if (threadIdx.x == 0) s_flag = 0;
   __syncthreads();
   const int A = 3 * a.nheads;
   const float invB = 1.f / (float)a.B;
   const float g_obj = a.g2 ? a.g2[0] : 0.f, g_cls = a.g2 ? a.g2[1] : 0.f;
-  for (int b = threadIdx.x; b < a.B; b += blockDim.x) {
-    float obj[3 * MAXH];
-    float best = 0.f;
-    int kbest = -1;
-    float cls_term = 0.f;
-    size_t off[MAXH];
-    for (int h = 0; h < a.nheads; ++h) {
+  for (int b0 = 0; b0 < a.B; b0 += CL_IMG) {
+    const int lb = threadIdx.x / A, k = threadIdx.x - lb * A;
+    const int b = b0 + lb;
+    if (lb < CL_IMG && b < a.B) {
+      const int h = k / 3, an = k - h * 3;
       const int hw = a.hw[h];
       bool oob;
       const int index = po::head_cell(center[2 * b + 0], center[2 * b + 1], a.S, hw, &oob);
       if (oob) atomicOr(&s_flag, 1);
-      if (cells) cells[h * a.B + b] = index;
+      if (cells && an == 0) cells[h * a.B + b] = index;
       int r = index / hw, c = index - (index / hw) * hw;
       if (a.org[h]) {
         r -= a.org[h][2 * b];
@@ -57,65 +64,74 @@ __global__ __launch_bounds__(256) void cell_loss_k(LossArgs a, const float* __re
           c = min(max(c, 0), a.win[h] - 1);
         }
       }
-      off[h] = (((size_t)b * a.win[h] + r) * a.win[h] + c) * a.Cp;
-      const float* cell = a.heads[h] + off[h];
-      for (int an = 0; an < 3; ++an) {
-        const int k = h * 3 + an;
-        const float* f = cell + an * NF;
-        const float o = sigm(f[4]);                                  // 470-476
-        obj[k] = o;
-        if (obj_out) obj_out[(size_t)b * A + k] = o;
-        if (kbest < 0 || o > best) { best = o; kbest = k; }          // torch.max: first index
-        float p[NCLS];
-        float mx = -INFINITY;
-        int cmax = 0;
-        for (int c = 0; c < NCLS; ++c) {
-          p[c] = sigm(f[5 + c]);                                     // 481
-          if (cls_out) cls_out[((size_t)b * A + k) * NCLS + c] = p[c];
-          if (p[c] > mx) { mx = p[c]; cmax = c; }
-        }
-        float* dcell = a.dheads[h] ? a.dheads[h] + off[h] + an * NF : nullptr;
-        if (a.objective == 0) {
-          // CrossEntropyLoss on probabilities (train_patch.py:534-546)
-          float se = 0.f;
-          for (int c = 0; c < NCLS; ++c) se += expf(p[c] - mx);
-          const float lse = mx + logf(se);
-          cls_term += lse - p[a.target];
-          if (dcell) {
-            const float g = g_cls * invB / (float)A;
-            for (int c = 0; c < NCLS; ++c) {
-              float sm = expf(p[c] - mx) / se;
-              float dp = g * (sm - (c == a.target ? 1.f : 0.f));
-              dcell[5 + c] = dp * p[c] * (1.f - p[c]);
-            }
+      const size_t off = (((size_t)b * a.win[h] + r) * a.win[h] + c) * a.Cp;
+      if (an == 0) c_off[lb][h] = (int)(off / a.Cp);
+      const float* f = a.heads[h] + off + an * NF;
+      const float o = sigm(f[4]);                                    // 470-476
+      c_obj[lb][k] = o;
+      if (obj_out) obj_out[(size_t)b * A + k] = o;
+      float p[NCLS];
+      float mx = -INFINITY;
+      int cmax = 0;
+      for (int cc = 0; cc < NCLS; ++cc) {
+        p[cc] = sigm(f[5 + cc]);                                     // 481
+        if (cls_out) cls_out[((size_t)b * A + k) * NCLS + cc] = p[cc];
+        if (p[cc] > mx) { mx = p[cc]; cmax = cc; }
+      }
+      float* dcell = a.dheads[h] ? a.dheads[h] + off + an * NF : nullptr;
+      float cls_term = 0.f;
+      if (a.objective == 0) {
+        // CrossEntropyLoss on probabilities (train_patch.py:534-546)
+        float se = 0.f;
+        for (int cc = 0; cc < NCLS; ++cc) se += expf(p[cc] - mx);
+        const float lse = mx + logf(se);
+        cls_term = lse - p[a.target];
+        if (dcell) {
+          const float g = g_cls * invB / (float)A;
+          for (int cc = 0; cc < NCLS; ++cc) {
+            float sm = expf(p[cc] - mx) / se;
+            float dp = g * (sm - (cc == a.target ? 1.f : 0.f));
+            dcell[5 + cc] = dp * p[cc] * (1.f - p[cc]);
           }
-        } else if (a.objective == 1) {
-          // noCLS_loss_targeted (train_patch.py:565-575): sum_b mean_k (max - target)
-          cls_term += mx - p[a.target];
-          if (dcell) {
-            const float g = g_cls / (float)A;
-            for (int c = 0; c < NCLS; ++c) {
-              float dp = (c == cmax ? g : 0.f) - (c == a.target ? g : 0.f);
-              dcell[5 + c] = dp * p[c] * (1.f - p[c]);
-            }
-          }
-        } else if (dcell) {
-          for (int c = 0; c < NCLS; ++c) dcell[5 + c] = 0.f;
         }
-        if (dcell) dcell[4] = 0.f;
+      } else if (a.objective == 1) {
+        // noCLS_loss_targeted (train_patch.py:565-575): sum_b mean_k (max - target)
+        cls_term = mx - p[a.target];
+        if (dcell) {
+          const float g = g_cls / (float)A;
+          for (int cc = 0; cc < NCLS; ++cc) {
+            float dp = (cc == cmax ? g : 0.f) - (cc == a.target ? g : 0.f);
+            dcell[5 + cc] = dp * p[cc] * (1.f - p[cc]);
+          }
+        }
+      } else if (dcell) {
+        for (int cc = 0; cc < NCLS; ++cc) dcell[5 + cc] = 0.f;
+      }
+      if (dcell) dcell[4] = 0.f;
+      c_cls[lb][k] = cls_term;
+    }
+    __syncthreads();
+    const int fb = b0 + (int)threadIdx.x;
+    if ((int)threadIdx.x < CL_IMG && fb < a.B) {
+      const int lb2 = threadIdx.x;
+      float best = 0.f, cls_term = 0.f;
+      int kbest = -1;
+      for (int kk = 0; kk < A; ++kk) {
+        const float o = c_obj[lb2][kk];
+        if (kbest < 0 || o > best) { best = o; kbest = kk; }          // torch.max: first index
+        cls_term += c_cls[lb2][kk];
+      }
+      s_max[fb] = best;
+      s_cls[fb] = cls_term / (a.objective == 0 ? (float)A : (a.objective == 1 ? (float)A : 1.f));
+      // objectness gradient: d/d obj[kbest] of 4*(1 - mean_b max_k obj) = -4/B
+      const int h = kbest / 3, an = kbest % 3;
+      if (a.dheads[h]) {
+        float* dcell = a.dheads[h] + (size_t)c_off[lb2][h] * a.Cp + an * NF;
+        dcell[4] = (-4.f * invB * g_obj) * best * (1.f - best);
       }
     }
-    s_max[b] = best;
-    s_cls[b] = cls_term / (a.objective == 0 ? (float)A : (a.objective == 1 ? (float)A : 1.f));
-    // objectness gradient: d/d obj[kbest] of 4*(1 - mean_b max_k obj) = -4/B
-    const int h = kbest / 3, an = kbest % 3;
-    if (a.dheads[h]) {
-      float* dcell = a.dheads[h] + off[h] + an * NF;
-      const float o = obj[kbest];
-      dcell[4] = (-4.f * invB * g_obj) * o * (1.f - o);
-    }
+    __syncthreads();
   }
-  __syncthreads();
   if (threadIdx.x == 0) {
     float sm = 0.f, sc = 0.f;
     for (int b = 0; b < a.B; ++b) {
@@ -371,7 +387,12 @@ extern "C" int po_max_prob_bwd(const float* const* heads, const int* h, const in
 // ---------------------------------------------------------------------------
 // Gradient cones: one thread per image walks the block program in order.
 namespace {
-__device__ __forceinline__ int fdiv(int a, int b) { return a >= 0 ? a / b : -((-a + b - 1) / b); }
+// floor division; the strides on the cone program are 1 or 2 (shift paths)
+__device__ __forceinline__ int fdiv(int a, int b) {
+  if (b == 1) return a;
+  if (b == 2) return a >> 1;                      // arithmetic shift = floor(a / 2)
+  return a >= 0 ? a / b : -((-a + b - 1) / b);
+}
 __device__ __forceinline__ int cdiv(int a, int b) { return -fdiv(-a, b); }
 
 // inclusive source interval [a, b] -> inclusive interval of the destination

@@ -1026,6 +1026,7 @@ class NetPlan:
                 continue
             M = desc.B * desc.Hg * desc.Wg
             best = None
+            timed = []
             for t, bm, bn, bk, pr in tiles:
                 if pr != desc.prec or desc.Cin_p % bk:
                     continue
@@ -1049,10 +1050,28 @@ class NetPlan:
                     e1.record()
                     e1.synchronize()
                     ms = e0.elapsed_time(e1)
+                    timed.append((ms, (t, ks)))
                     if best is None or ms < best[0]:
                         best = (ms, (t, ks))
             if best is None:
                 raise RuntimeError("po_conv: no tile applies to launch %s (%s)" % (key, nat.last_error()))
+            # refinement: the three fastest candidates again, in interleaved
+            # rounds of longer runs, keeping each one's best round (a single
+            # short timing per candidate picks noisily between close tiles)
+            finalists = [c for _, c in sorted(timed)[:3]]
+            if len(finalists) > 1:
+                score = {c: float("inf") for c in finalists}
+                for _ in range(3):
+                    for c in finalists:
+                        self._set_tile(desc, c)
+                        lib.po_conv(*args, st)
+                        e0.record()
+                        for _ in range(2 * iters):
+                            lib.po_conv(*args, st)
+                        e1.record()
+                        e1.synchronize()
+                        score[c] = min(score[c], e0.elapsed_time(e1))
+                best = min((v, c) for c, v in score.items())
             self._set_tile(desc, best[1])
             cache[key] = list(best[1])
         for name, _, desc in self.fwd_ops + self.bwd_ops:     # the workspace may have grown

@@ -229,7 +229,11 @@ class PatchTrainer(object):
         return terms
 
     def make_optimizer(self, adv_patch):
-        return optim.Adam([adv_patch], lr=self.config.start_learning_rate, amsgrad=True)
+        """Adam(amsgrad) as the reference (train_patch.py:131-136); on the GPU
+        PyTorch's fused single-kernel implementation (same update rule) instead
+        of the multi-launch foreach one."""
+        return optim.Adam([adv_patch], lr=self.config.start_learning_rate, amsgrad=True,
+                          fused=bool(adv_patch.is_cuda) or None)
 
     # ------------------------------------------------------------------
     def train(self, max_n_epochs=401, save_dir="training_patches_saves/trained_patches", num_workers=10,
