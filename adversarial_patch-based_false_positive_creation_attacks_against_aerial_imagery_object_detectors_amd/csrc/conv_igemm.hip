@@ -241,10 +241,10 @@ __global__ __launch_bounds__(256) void conv_k(const ConvArgs a) {
   po::conv_epilogue<BM, TM, TN>(a, acc, smem, dst_pix, m0, n0, wm, wn, 0);
 }
 
-// Split-K reduction + epilogue: one thread per 4 output channels of a row.
-// The slices are summed in split order (deterministic); their loads are
-// issued four at a time so that a thread has four 16-byte reads in flight
-// instead of one dependent read per slice.  Every epilogue operand is moved
+// Split-K reduction + epilogue: one thread per 8 output channels of a row.
+// The slices are summed in split order (deterministic); a thread's loads
+// are issued two slices (four 16-byte reads) at a time instead of one
+// dependent read per slice.  Every epilogue operand is moved
 // as one 16-byte vector (o is a multiple of 4 floats).  32-bit indices: the
 // host checks M * N < 2^31.
 __device__ __forceinline__ float4 ld4(const float* p) { return *reinterpret_cast<const float4*>(p); }
@@ -253,13 +253,15 @@ __device__ __forceinline__ void st4(float* p, float x, float y, float z, float w
 }
 __device__ __forceinline__ void add4(float4& v, const float4 p) { v.x += p.x; v.y += p.y; v.z += p.z; v.w += p.w; }
 
+// RQ channel quads (8 channels) per thread: twice the slice loads in flight.
+constexpr int RQ = 2;
 __global__ __launch_bounds__(256) void conv_reduce_k(const ConvArgs a) {
   const int t0 = (int)blockIdx.x * 256 + (int)threadIdx.x;
-  const int n4 = a.N >> 2;
-  const int tot = a.M * n4;
+  const int n8 = a.N / (4 * RQ);                   // N % 16 == 0 (host check)
+  const int tot = a.M * n8;
   const int t = t0 < tot ? t0 : 0;
   const int sh = po::input_shift(a) + (a.prec == 1 ? a.w_shift : 0);
-  const int m = t / n4, n = (t - m * n4) * 4;
+  const int m = t / n8, n0 = (t - m * n8) * 4 * RQ;
   int b, i, j;
   const bool live = t0 < tot && po::grid_point(a, m, b, i, j);
   const size_t pix = live ? (size_t)(b * a.Hout + i * a.out_step + a.out_oy) * a.Wout + j * a.out_step + a.out_ox : 0;
@@ -267,56 +269,69 @@ __global__ __launch_bounds__(256) void conv_reduce_k(const ConvArgs a) {
   uint32_t nib = 0;
   if (live) {
     const size_t slice = (size_t)a.M * a.N;
-    const float* wp = a.ws + (size_t)m * a.N + n;
-    float4 v = ld4(wp);
-    int s = 1;
-    for (; s + 3 < a.ksplit; s += 4) {
-      const float4 p0 = ld4(wp + s * slice), p1 = ld4(wp + (s + 1) * slice);
-      const float4 p2 = ld4(wp + (s + 2) * slice), p3 = ld4(wp + (s + 3) * slice);
-      add4(v, p0); add4(v, p1); add4(v, p2); add4(v, p3);
-    }
-    for (; s < a.ksplit; ++s) add4(v, ld4(wp + s * slice));
-    const size_t o = pix * a.Cout_p + n;
-    float r[4] = {v.x, v.y, v.z, v.w};
-    const size_t wo = pix * (size_t)(a.Cout_p >> 5) + (n >> 5);
-    const float4 g1 = a.mbits ? po::leaky_grad_bits(a.mbits[wo], n) : make_float4(0.f, 0.f, 0.f, 0.f);
-    const float4 g2 = a.m2bits ? po::leaky_grad_bits(a.m2bits[wo], n) : make_float4(0.f, 0.f, 0.f, 0.f);
-    const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
-    const float4 yin = a.accumulate ? ld4(a.y + o) : z4;
-    const float4 mk = (!a.mbits && a.mask) ? ld4(a.mask + o) : z4;
-    const float4 rs = a.res ? ld4(a.res + o) : z4;
-    const float4 mk2 = (a.y2 && !a.m2bits) ? ld4(a.mask2 + o) : z4;
-    const float4 bs = a.bias ? ld4(a.bias + n) : z4;
-    const float g1v[4] = {g1.x, g1.y, g1.z, g1.w}, g2v[4] = {g2.x, g2.y, g2.z, g2.w};
-    const float yiv[4] = {yin.x, yin.y, yin.z, yin.w}, mkv[4] = {mk.x, mk.y, mk.z, mk.w};
-    const float rsv[4] = {rs.x, rs.y, rs.z, rs.w}, mk2v[4] = {mk2.x, mk2.y, mk2.z, mk2.w};
-    const float bsv[4] = {bs.x, bs.y, bs.z, bs.w};
-    float yo[4], so[4], y2o[4];
+    const float* wp = a.ws + (size_t)m * a.N + n0;
+    float4 v[RQ];
 #pragma unroll
-    for (int c = 0; c < 4; ++c) {
-      float x = __builtin_ldexpf(r[c], -sh) + bsv[c];
-      if (a.act) x = po::leaky(x);
-      if (a.accumulate) x += yiv[c];
-      const float yv = a.mbits ? x * g1v[c] : (a.mask ? x * po::leaky_grad(mkv[c]) : x);
-      yo[c] = yv;
-      nib |= (yv > 0.f ? 1u : 0u) << c;
-      my = fmaxf(my, fabsf(yv));
-      so[c] = x + rsv[c];
-      if (a.res) ms = fmaxf(ms, fabsf(so[c]));
-      y2o[c] = x * (a.m2bits ? g2v[c] : po::leaky_grad(mk2v[c]));
-      if (a.y2) my2 = fmaxf(my2, fabsf(y2o[c]));
+    for (int q = 0; q < RQ; ++q) v[q] = ld4(wp + 4 * q);
+    int s = 1;
+    for (; s + 1 < a.ksplit; s += 2) {
+      float4 p0[RQ], p1[RQ];
+#pragma unroll
+      for (int q = 0; q < RQ; ++q) {
+        p0[q] = ld4(wp + s * slice + 4 * q);
+        p1[q] = ld4(wp + (s + 1) * slice + 4 * q);
+      }
+#pragma unroll
+      for (int q = 0; q < RQ; ++q) { add4(v[q], p0[q]); add4(v[q], p1[q]); }
     }
-    if (a.y) st4(a.y + o, yo[0], yo[1], yo[2], yo[3]);
-    if (a.res) st4(a.sum + o, so[0], so[1], so[2], so[3]);
-    if (a.y2) st4(a.y2 + o, y2o[0], y2o[1], y2o[2], y2o[3]);
+    for (; s < a.ksplit; ++s)
+#pragma unroll
+      for (int q = 0; q < RQ; ++q) add4(v[q], ld4(wp + s * slice + 4 * q));
+    const size_t wo = pix * (size_t)(a.Cout_p >> 5) + (n0 >> 5);
+    const uint32_t w1 = a.mbits ? a.mbits[wo] : 0u, w2 = a.m2bits ? a.m2bits[wo] : 0u;
+#pragma unroll
+    for (int q = 0; q < RQ; ++q) {
+      const int n = n0 + 4 * q;
+      const size_t o = pix * a.Cout_p + n;
+      const float r[4] = {v[q].x, v[q].y, v[q].z, v[q].w};
+      const float4 g1 = po::leaky_grad_bits(w1, n);
+      const float4 g2 = po::leaky_grad_bits(w2, n);
+      const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
+      const float4 yin = a.accumulate ? ld4(a.y + o) : z4;
+      const float4 mk = (!a.mbits && a.mask) ? ld4(a.mask + o) : z4;
+      const float4 rs = a.res ? ld4(a.res + o) : z4;
+      const float4 mk2 = (a.y2 && !a.m2bits) ? ld4(a.mask2 + o) : z4;
+      const float4 bs = a.bias ? ld4(a.bias + n) : z4;
+      const float g1v[4] = {g1.x, g1.y, g1.z, g1.w}, g2v[4] = {g2.x, g2.y, g2.z, g2.w};
+      const float yiv[4] = {yin.x, yin.y, yin.z, yin.w}, mkv[4] = {mk.x, mk.y, mk.z, mk.w};
+      const float rsv[4] = {rs.x, rs.y, rs.z, rs.w}, mk2v[4] = {mk2.x, mk2.y, mk2.z, mk2.w};
+      const float bsv[4] = {bs.x, bs.y, bs.z, bs.w};
+      float yo[4], so[4], y2o[4];
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        float x = __builtin_ldexpf(r[c], -sh) + bsv[c];
+        if (a.act) x = po::leaky(x);
+        if (a.accumulate) x += yiv[c];
+        const float yv = a.mbits ? x * g1v[c] : (a.mask ? x * po::leaky_grad(mkv[c]) : x);
+        yo[c] = yv;
+        nib |= (yv > 0.f ? 1u : 0u) << (4 * q + c);
+        my = fmaxf(my, fabsf(yv));
+        so[c] = x + rsv[c];
+        if (a.res) ms = fmaxf(ms, fabsf(so[c]));
+        y2o[c] = x * (a.m2bits ? g2v[c] : po::leaky_grad(mk2v[c]));
+        if (a.y2) my2 = fmaxf(my2, fabsf(y2o[c]));
+      }
+      if (a.y) st4(a.y + o, yo[0], yo[1], yo[2], yo[3]);
+      if (a.res) st4(a.sum + o, so[0], so[1], so[2], so[3]);
+      if (a.y2) st4(a.y2 + o, y2o[0], y2o[1], y2o[2], y2o[3]);
+    }
   }
   if (a.ybits) {
-    // threads 8k .. 8k+7 hold the 32 channels of one sign-bit word (N % 32 == 0)
-    uint32_t w = nib << (4 * (threadIdx.x & 7));
+    // threads 4k .. 4k+3 hold the 32 channels of one sign-bit word (N % 32 == 0)
+    uint32_t w = nib << (4 * RQ * (threadIdx.x & 3));
     w |= (uint32_t)__shfl_xor((int)w, 1);
     w |= (uint32_t)__shfl_xor((int)w, 2);
-    w |= (uint32_t)__shfl_xor((int)w, 4);
-    if (live && (threadIdx.x & 7) == 0) a.ybits[pix * (a.Cout_p >> 5) + (n >> 5)] = w;
+    if (live && (threadIdx.x & 3) == 0) a.ybits[pix * (a.Cout_p >> 5) + (n0 >> 5)] = w;
   }
   if (a.y_amax) po::amax_commit(a.y_amax, my);
   if (a.sum_amax) po::amax_commit(a.sum_amax, ms);
@@ -333,7 +348,7 @@ int launch(const ConvArgs& a, hipStream_t st) {
     PO_REQUIRE((int64_t)a.M * a.N < (1LL << 31), "po_conv: split-K output too large");
     int rc = po::check_launch("po_conv");
     if (rc) return rc;
-    hipLaunchKernelGGL(conv_reduce_k, dim3(po::ceil_div((int64_t)a.M * (a.N / 4), 256)), dim3(256), 0, st, b);
+    hipLaunchKernelGGL(conv_reduce_k, dim3(po::ceil_div((int64_t)a.M * (a.N / (4 * RQ)), 256)), dim3(256), 0, st, b);
   }
   return po::check_launch("po_conv");
 }
@@ -499,7 +514,7 @@ extern "C" int po_conv(const po_conv_desc* d, const float* in, const float* W, c
     PO_REQUIRE(a.ksplit == 1 || (int64_t)a.M * a.N < (1LL << 31), "po_conv: split-K output too large");
     rc = po::launch_h3(b, st, bm, bn, bk, gl);
     if (rc == PO_OK && a.ksplit > 1) {
-      hipLaunchKernelGGL(conv_reduce_k, dim3(po::ceil_div((int64_t)a.M * (a.N / 4), 256)), dim3(256), 0, st, b);
+      hipLaunchKernelGGL(conv_reduce_k, dim3(po::ceil_div((int64_t)a.M * (a.N / (4 * RQ)), 256)), dim3(256), 0, st, b);
       rc = po::check_launch("po_conv (split-K reduce)");
     }
     return rc;
