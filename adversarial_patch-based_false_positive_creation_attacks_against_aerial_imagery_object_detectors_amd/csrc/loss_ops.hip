@@ -408,8 +408,9 @@ __device__ __forceinline__ void cone_map(int kind, int k, int s, int pad, int a,
 }
 
 // One workgroup per image: the program and the image's boxes are staged in
-// LDS, lane 0 walks the (dependent) rows there, and the workgroup writes the
-// boxes back; global-memory latency is paid once per box, not once per row.
+// LDS, lanes 0 and 1 walk the (dependent) rows there, one axis each, and the
+// workgroup writes the boxes back; global-memory latency is paid once per
+// box, not once per row.
 __global__ __launch_bounds__(64) void grad_boxes_k(const int32_t* __restrict__ roi, int B, int S,
                                                    const int32_t* __restrict__ prog, int nprog, int nbox,
                                                    int32_t* __restrict__ boxes) {
@@ -420,29 +421,43 @@ __global__ __launch_bounds__(64) void grad_boxes_k(const int32_t* __restrict__ r
   for (int k = threadIdx.x; k < nbox; k += 64) sbox[k] = reinterpret_cast<const int4*>(boxes)[(size_t)k * B + b];
   for (int k = threadIdx.x; k < 8 * nprog; k += 64) sprog[k] = prog[k];
   __syncthreads();
-  if (threadIdx.x == 0) {
-    for (int r = 0; r < nprog; ++r) sbox[sprog[8 * r]] = make_int4(0, 0, 0, 0);
+  if (threadIdx.x < 2) {
+    // lane 0 walks the row intervals, lane 1 the column intervals (a box's
+    // two axes are set together; "skip this row" is agreed by a lane swap)
+    const int d = threadIdx.x;
+    int* sb = reinterpret_cast<int*>(sbox);            // box k: [r0, c0, r1, c1] at 4 k
+    for (int r = 0; r < nprog; ++r) {
+      sb[4 * sprog[8 * r] + d] = 0;
+      sb[4 * sprog[8 * r] + d + 2] = 0;
+    }
     for (int r = 0; r < nprog; ++r) {
       const int32_t* p = sprog + 8 * r;
-      int sr0, sc0, sr1, sc1;                  // source box, half-open
+      int s0, s1;                                      // source interval, half-open
       if (p[1] < 0) {
-        if (roi) { sc0 = roi[4 * b]; sr0 = roi[4 * b + 1]; sc1 = roi[4 * b + 2]; sr1 = roi[4 * b + 3]; }
-        else { sr0 = sc0 = 0; sr1 = sc1 = S; }
+        if (roi) { s0 = roi[4 * b + 1 - d]; s1 = roi[4 * b + 3 - d]; }   // roi = x0, y0, x1, y1
+        else { s0 = 0; s1 = S; }
       } else {
-        const int4 v = sbox[p[1]];
-        sr0 = v.x; sc0 = v.y; sr1 = v.z; sc1 = v.w;
+        s0 = sb[4 * p[1] + d];
+        s1 = sb[4 * p[1] + d + 2];
       }
-      if (sr0 >= sr1 || sc0 >= sc1) continue;
-      int r0, r1, c0, c1;
-      cone_map(p[2], p[3], p[4], p[5], sr0, sr1 - 1, r0, r1);
-      cone_map(p[2], p[3], p[4], p[5], sc0, sc1 - 1, c0, c1);
-      r0 = max(r0, 0); c0 = max(c0, 0);
-      r1 = min(r1, p[6] - 1); c1 = min(c1, p[7] - 1);
-      if (r0 > r1 || c0 > c1) continue;
-      int4 o = sbox[p[0]];
-      if (o.x >= o.z || o.y >= o.w) o = make_int4(r0, c0, r1 + 1, c1 + 1);
-      else o = make_int4(min(o.x, r0), min(o.y, c0), max(o.z, r1 + 1), max(o.w, c1 + 1));
-      sbox[p[0]] = o;
+      int bad = s0 >= s1;
+      bad |= __shfl_xor(bad, 1);
+      if (bad) continue;
+      int lo, hi;
+      cone_map(p[2], p[3], p[4], p[5], s0, s1 - 1, lo, hi);
+      lo = max(lo, 0);
+      hi = min(hi, p[6 + d] - 1);
+      bad = lo > hi;
+      bad |= __shfl_xor(bad, 1);
+      if (bad) continue;
+      int* o = sb + 4 * p[0];
+      if (o[d] >= o[d + 2]) {
+        o[d] = lo;
+        o[d + 2] = hi + 1;
+      } else {
+        o[d] = min(o[d], lo);
+        o[d + 2] = max(o[d + 2], hi + 1);
+      }
     }
   }
   __syncthreads();
