@@ -328,6 +328,47 @@ __global__ __launch_bounds__(256) void warp_fwd_k(const float* __restrict__ img,
   }
 }
 
+// Four consecutive pixels of a row per thread (S % 4 == 0): the same
+// per-pixel arithmetic as warp_fwd_k, with 16-byte image reads and output
+// writes, threads laid over the image's (row, pixel quad) grid.
+__global__ __launch_bounds__(256) void warp_fwd4_k(const float* __restrict__ img,
+                                                   const float* __restrict__ mp,
+                                                   const float* __restrict__ noise,
+                                                   const float* __restrict__ contrast,
+                                                   const float* __restrict__ bright,
+                                                   const float* __restrict__ theta, WarpGeom g, int mode,
+                                                   float* __restrict__ out) {
+  const int b = blockIdx.y;
+  const int sq = g.S >> 2;
+  const int q = blockIdx.x * 256 + threadIdx.x;
+  if (q >= g.S * sq) return;
+  const int i = q / sq, j0 = (q - i * sq) * 4;
+  const size_t plane = (size_t)g.S * g.S;
+  const size_t o = (size_t)b * 3 * plane + (size_t)i * g.S + j0;
+  const float* th = theta + 6 * b;
+  const float* nz = noise + (size_t)b * 3 * g.P * g.P;
+  const float cb = contrast[b], bb = bright[b];
+  float v[3][4];
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {
+    float adv[3], msk;
+    bool rng[3];
+    const bool hit = warp_pixel(th, g, mp, nz, cb, bb, i, j0 + u, adv, msk, rng);
+#pragma unroll
+    for (int ch = 0; ch < 3; ++ch) v[ch][u] = hit ? adv[ch] * msk : 0.f;   // load_data.py:791-792
+  }
+#pragma unroll
+  for (int ch = 0; ch < 3; ++ch) {
+    if (mode == 1) {                                                       // load_data.py:820
+      const float4 m = *reinterpret_cast<const float4*>(img + o + ch * plane);
+      const float mv[4] = {m.x, m.y, m.z, m.w};
+#pragma unroll
+      for (int u = 0; u < 4; ++u) v[ch][u] = (v[ch][u] == 0.f) ? mv[u] : v[ch][u];
+    }
+    *reinterpret_cast<float4*>(out + o + ch * plane) = make_float4(v[ch][0], v[ch][1], v[ch][2], v[ch][3]);
+  }
+}
+
 // Backward phase A: per output pixel of the footprint,
 // gfac = d_out * [out != 0 (mode 1)] * msk_t * [0 <= adv_t <= 1]
 __global__ __launch_bounds__(256) void warp_bwd_a_k(const float* __restrict__ d_out,
@@ -463,6 +504,11 @@ extern "C" int po_warp_fwd(const float* img, const float* patch_mp, const float*
   PO_REQUIRE(patch_mp && noise && contrast && bright && theta && out, "po_warp_fwd: null pointer");
   PO_REQUIRE(mode == 0 || (mode == 1 && img), "po_warp_fwd: mode must be 0 or 1 (1 needs img)");
   PO_REQUIRE(B > 0 && S > 1 && P > 0 && P <= S, "po_warp_fwd: bad shape B=%d S=%d P=%d", B, S, P);
+  if (S % 4 == 0 && ((uintptr_t)img | (uintptr_t)out) % 16 == 0 && !getenv("PO_WARP_V1")) {
+    hipLaunchKernelGGL(warp_fwd4_k, dim3(po::ceil_div(S * (S / 4), 256), B), dim3(256), 0, po::stream_of(s), img,
+                       patch_mp, noise, contrast, bright, theta, make_geom(S, P), mode, out);
+    return po::check_launch("po_warp_fwd");
+  }
   dim3 grid(po::ceil_div(S, 256), S, B);
   hipLaunchKernelGGL(warp_fwd_k, grid, dim3(256), 0, po::stream_of(s), img, patch_mp, noise, contrast,
                      bright, theta, make_geom(S, P), mode, out);

@@ -1,4 +1,6 @@
-"""po_conv_first_fwd (the 3-channel first Darknet conv, darknet_v3.py:9-100
+"""HBM-bound producer kernels vs their one-element-per-thread forms.
+
+po_conv_first_fwd (the 3-channel first Darknet conv, darknet_v3.py:9-100
 conv + BN-folded bias + LeakyReLU 0.1, cfg.py:37-56) on the GPU: the packed
 two-pixel kernel (first_fwd2_k) is bit-identical to the one-pixel kernel
 (first_fwd_k, PO_FIRST_V1=1) and matches a PyTorch fp32 conv within fp32
@@ -56,3 +58,41 @@ def test_first_fwd_packed_matches_v1_and_torch(B, H, W, stride, cout):
         ref = ref.permute(0, 2, 3, 1).float()
         torch.testing.assert_close(y2.cpu(), ref, rtol=1e-5, atol=1e-5)
         assert abs(m2 - ref.abs().max().item()) <= 1e-5 * max(1.0, m2)
+
+
+@pytest.mark.parametrize("mode", [0, 1])
+def test_warp_fwd_quad_kernel_bit_identical(mode):
+    """po_warp_fwd (PatchTransformer affine warp + composite, load_data.py:
+    726-792, 820): the four-pixels-per-thread kernel writes the same bits as
+    the one-pixel kernel (PO_WARP_V1=1), patch inside, partly outside and
+    fully outside the frame."""
+    nat = pkg_mod("_native")
+    dev = torch.device("cuda", 0)
+    g = torch.Generator().manual_seed(7 + mode)
+    B, S, P = 3, 64, 24
+    img = torch.rand(B, 3, S, S, generator=g).to(dev)
+    mp = torch.rand(3, P, P, generator=g).to(dev)
+    noise = (torch.rand(B, 3, P, P, generator=g) * 2 - 1).to(dev)
+    contrast = (torch.rand(B, generator=g) * 0.4 + 0.8).to(dev)
+    bright = (torch.rand(B, generator=g) * 0.2 - 0.1).to(dev)
+    theta = torch.tensor([[1.6, 0.4, 0.1, -0.4, 1.6, -0.2],      # scaled, rotated, inside
+                          [0.9, -1.1, 0.9, 1.1, 0.9, -0.8],      # large, partly outside
+                          [2.0, 0.0, 3.5, 0.0, 2.0, 3.5]],       # off the frame
+                         dtype=torch.float32, device=dev)
+    outs = []
+    for v1 in (False, True):
+        out = torch.full((B, 3, S, S), float("nan"), device=dev)
+        old = os.environ.pop("PO_WARP_V1", None)
+        try:
+            if v1:
+                os.environ["PO_WARP_V1"] = "1"
+            nat.call("po_warp_fwd", nat.ptr(img) if mode == 1 else None, nat.ptr(mp), nat.ptr(noise),
+                     nat.ptr(contrast), nat.ptr(bright), nat.ptr(theta), B, S, P, mode, nat.ptr(out), nat.stream())
+            torch.cuda.synchronize()
+        finally:
+            os.environ.pop("PO_WARP_V1", None)
+            if old is not None:
+                os.environ["PO_WARP_V1"] = old
+        outs.append(out)
+    assert torch.equal(outs[0], outs[1])
+    assert (outs[0] != (img if mode == 1 else 0)).any()      # the patch landed somewhere
