@@ -13,7 +13,8 @@ LIB_PATH = os.path.join(_HERE, "libadvpatch_hip.so")
 
 c_int, c_float, c_int64, c_void_p = ctypes.c_int, ctypes.c_float, ctypes.c_int64, ctypes.c_void_p
 
-PO_CONV_NTILES = 60   # include/advpatch.h
+PO_ABI_VERSION = 9    # include/advpatch.h
+PO_CONV_NTILES = 61   # include/advpatch.h
 PO_AMAX_SUB = 64      # sub-slots per max|x| slot
 
 
@@ -26,7 +27,7 @@ class po_conv_desc(ctypes.Structure):
         ("in_org", c_void_p), ("out_org", c_void_p), ("ksplit", c_int), ("workspace", c_void_p),
         ("prec", c_int), ("w_shift", c_int), ("in_amax", c_void_p), ("y_amax", c_void_p),
         ("sum_amax", c_void_p), ("y2_amax", c_void_p), ("ybits", c_void_p), ("mbits", c_void_p),
-        ("m2bits", c_void_p), ("gbox", c_void_p), ("Wfrag", c_void_p)]
+        ("m2bits", c_void_p), ("gbox", c_void_p), ("Wfrag", c_void_p), ("Wwino", c_void_p)]
 
 
 _SIGS = {
@@ -35,7 +36,10 @@ _SIGS = {
     "po_median7_fwd": [c_void_p, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p],
     "po_median7_bwd": [c_void_p, c_void_p, c_int, c_int, c_int, c_void_p, c_void_p],
     "po_patch_params": [c_void_p, c_int, c_int, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int,
-                        c_void_p, c_void_p, c_void_p, c_void_p, c_void_p],
+                        c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p],
+    "po_draws": [ctypes.c_uint64, ctypes.c_uint64, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p,
+                 c_void_p, c_void_p, c_void_p],
+    "po_check_finite": [c_void_p, c_int64, c_int, c_void_p, c_void_p],
     "po_warp_fwd": [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int,
                     c_int, c_void_p, c_void_p],
     "po_warp_bwd": [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int,
@@ -92,6 +96,12 @@ def load():
         raise ImportError("libadvpatch_hip.so is not built (%s); run `python -c 'import "
                           "__graft_entry__ as g; g.build()'` or `make -C csrc`" % LIB_PATH)
     lib = ctypes.CDLL(LIB_PATH)
+    lib.po_abi_version.argtypes = []
+    lib.po_abi_version.restype = c_int
+    got = lib.po_abi_version()
+    if got != PO_ABI_VERSION:
+        raise ImportError("libadvpatch_hip.so has ABI %d, this package needs %d: rebuild it "
+                          "(make -C csrc, or __graft_entry__.build())" % (got, PO_ABI_VERSION))
     for name, argtypes in _SIGS.items():
         fn = getattr(lib, name)
         fn.argtypes = argtypes

@@ -1,0 +1,303 @@
+// Winograd F(2x2, 3x3) convolution on the fp32 matrix cores (po_conv prec 0,
+// tile staging 5).
+//
+// For a stride-1 3x3 correlation (the Darknet forward convs and the input
+// gradients of stride-1 3x3 convs, darknet_v3.py:37-59 and their autograd
+// backward) every 2x2 output block ("tile") is
+//     Y = A^T [ sum_c (G g_c G^T) .* (B^T d_c B) ] A
+// with d_c the 4x4 input patch of channel c.  Per tile that is 16 products
+// per channel instead of 36: the contraction becomes 16 independent GEMMs
+//     M_xi[tile][n] = sum_c V_xi[tile][c] * U_xi[c][n]
+// (xi = 0..15 transform components), 4/9 of the direct conv's MFMA work.
+// Every operand stays fp32 (v_mfma_f32_32x32x2_f32, fp32 accumulate); the
+// weight transform G g G^T is done once on the host in float64.  Measured
+// rounding error ~1.5-2x that of the direct fp32 conv (tools/ notes in
+// DESIGN.md §3.5); the parity tests bound the end-to-end gradient.
+//
+// Workgroup: 256 threads = 4 waves; 64 tiles (two 32-row MFMA blocks) x 32
+// output channels; wave w owns components 4w..4w+3.  k-step = 16 input
+// channels:
+//   * each thread loads the 4x4 input patch of one tile for 4 channels
+//     (16 x 16-byte buffer loads; out-of-image pixels read 0 through the
+//     buffer resource's range check), transforms it in registers (B^T d B on
+//     float4 lanes) and writes the 16 components to LDS V[buf][xi][tile][k]
+//     (16-byte chunks XOR-swizzled by tile: conflict-free writes and reads);
+//   * the B operand (U, pre-arranged on the host in MFMA fragment order) is
+//     read straight from global memory/L2 into registers, one k-step ahead;
+//   * V is double-buffered (2 x 64 KB): the transform of step k+1 is issued
+//     between the MFMAs of step k, one barrier per step.
+// Epilogue: the 16 component accumulators go through LDS (128 KB, the V
+// buffers), every thread inverse-transforms (A^T M A) 8 (tile, channel)
+// pairs and applies po_conv's epilogue (bias, LeakyReLU, accumulate, masks
+// as floats or sign bits, fused shortcut, dual output, sign bits, max|x|).
+#pragma clang fp contract(off)
+#include "conv_common.h"
+
+namespace {
+using po::ConvArgs;
+
+constexpr int WT = 64;   // tiles (GEMM rows) per workgroup
+constexpr int WN = 32;   // output channels per workgroup
+constexpr int WK = 16;   // input channels per k-step
+constexpr uint32_t kOOB = 0x80000000u;
+
+// tile-grid enumeration: GEMM row m -> image b, tile (ti, tj); with a.gbox
+// only the tiles of the image's box (destination pixels [r0,r1) x [c0,c1))
+__device__ __forceinline__ bool tile_point(const ConvArgs& a, int Ht, int Wt, int m, int& b, int& ti, int& tj) {
+  const int per = Ht * Wt;
+  b = ti = tj = 0;
+  if (m >= a.B * per) return false;
+  b = m / per;
+  const int l = m - b * per;
+  if (!a.gbox) {
+    ti = l / Wt;
+    tj = l - ti * Wt;
+    return true;
+  }
+  const int4 bx = reinterpret_cast<const int4*>(a.gbox)[b];
+  const int t0 = bx.x >> 1, t1 = (bx.z + 1) >> 1, u0 = bx.y >> 1, u1 = (bx.w + 1) >> 1;
+  const int h = max(t1 - t0, 0), w = max(u1 - u0, 0);
+  if (l >= h * w) return false;
+  const int q = l / w;
+  ti = t0 + q;
+  tj = u0 + (l - q * w);
+  return true;
+}
+
+__device__ __forceinline__ float4 f4add(float4 x, float4 y) { return make_float4(x.x + y.x, x.y + y.y, x.z + y.z, x.w + y.w); }
+__device__ __forceinline__ float4 f4sub(float4 x, float4 y) { return make_float4(x.x - y.x, x.y - y.y, x.z - y.z, x.w - y.w); }
+
+// LDS V/M element (component xi, tile t, 16-byte chunk ch) — chunk swizzled by tile
+__device__ __forceinline__ int vidx(int xi, int t, int ch) { return ((xi * WT + t) * WK) + ((ch ^ ((t >> 2) & 3)) << 2); }
+
+// scalar po_conv epilogue of one destination element (conv_common.h conv_epilogue)
+struct EpiMax {
+  float y = 0.f, s = 0.f, y2 = 0.f;
+};
+__device__ __forceinline__ float epi_store(const ConvArgs& a, size_t pix, int n, float v, EpiMax& mx) {
+  const size_t o = pix * (size_t)a.Cout_p + n;
+  const size_t wo = pix * (size_t)(a.Cout_p >> 5) + (n >> 5);
+  float x = v + (a.bias ? a.bias[n] : 0.f);
+  if (a.act) x = po::leaky(x);
+  if (a.accumulate) x += a.y[o];
+  float out = x;
+  if (a.mbits) out = x * (((a.mbits[wo] >> (n & 31)) & 1u) ? 1.f : 0.1f);
+  else if (a.mask) out = x * po::leaky_grad(a.mask[o]);
+  if (a.y) a.y[o] = out;
+  mx.y = fmaxf(mx.y, fabsf(out));
+  if (a.res) {
+    const float sm = x + a.res[o];
+    a.sum[o] = sm;
+    mx.s = fmaxf(mx.s, fabsf(sm));
+  }
+  if (a.y2) {
+    const float g = a.m2bits ? (((a.m2bits[wo] >> (n & 31)) & 1u) ? 1.f : 0.1f) : po::leaky_grad(a.mask2[o]);
+    const float o2 = x * g;
+    a.y2[o] = o2;
+    mx.y2 = fmaxf(mx.y2, fabsf(o2));
+  }
+  return out;
+}
+
+__global__ __launch_bounds__(256) void conv_wino_k(const ConvArgs a, const float* __restrict__ U, int Ht, int Wt) {
+  __shared__ __attribute__((aligned(16))) float smem[2 * 16 * WT * WK];     // 128 KB
+  __shared__ int s_live;
+  const int wgid = po::xcd_remap();
+  const int tn = wgid % a.ntiles_n, tm = wgid / a.ntiles_n;
+  const int m0 = tm * WT, n0 = tn * WN;
+  const int tid = threadIdx.x & 255, lane = tid & 63, wave = tid >> 6;
+
+  // ---- loader: thread = (tile r, channel chunk q)
+  const int r = tid & 63, q = tid >> 6;
+  int b, ti, tj;
+  const bool live = tile_point(a, Ht, Wt, m0 + r, b, ti, tj);
+  if (tid == 0) s_live = 0;
+  __syncthreads();
+  if (live) s_live = 1;
+  __syncthreads();
+  if (!s_live) return;                      // every tile of the block is outside its image's box
+
+  const uint32_t in_bytes = (uint32_t)__builtin_amdgcn_readfirstlane(a.in_bytes);
+  const __amdgpu_buffer_rsrc_t in_rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(a.in), 0, in_bytes, 0x00020000);
+  const uint32_t pix_bytes = (uint32_t)a.Cin_p * 4u;
+  uint32_t poff[16];
+#pragma unroll
+  for (int u = 0; u < 4; ++u)
+#pragma unroll
+    for (int v = 0; v < 4; ++v) {
+      const int y = 2 * ti - 1 + u, x = 2 * tj - 1 + v;
+      const bool ok = live && (unsigned)y < (unsigned)a.Hin && (unsigned)x < (unsigned)a.Win;
+      poff[u * 4 + v] = ok ? (((uint32_t)b * a.Hin + y) * a.Win + x) * pix_bytes + 16u * q : kOOB;
+    }
+  float4 ra[16];
+  auto gload = [&](int ks) {
+    const uint32_t cb = (uint32_t)ks * (WK * 4u);
+#pragma unroll
+    for (int p = 0; p < 16; ++p) {
+      const uint32_t off = poff[p] == kOOB ? kOOB : poff[p] + cb;
+      ra[p] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(in_rs, off, 0, 0));
+    }
+  };
+  // B^T d B of 4 channels at once, written as 16 components of chunk q of tile r
+  auto transform = [&](float* Vb) {
+    float4 t[4][4];
+#pragma unroll
+    for (int v = 0; v < 4; ++v) {          // columns: B^T applied over rows u
+      const float4 d0 = ra[0 * 4 + v], d1 = ra[1 * 4 + v], d2 = ra[2 * 4 + v], d3 = ra[3 * 4 + v];
+      t[0][v] = f4sub(d0, d2);
+      t[1][v] = f4add(d1, d2);
+      t[2][v] = f4sub(d2, d1);
+      t[3][v] = f4sub(d1, d3);
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {          // rows: B applied over columns v
+      const float4 e[4] = {f4sub(t[u][0], t[u][2]), f4add(t[u][1], t[u][2]), f4sub(t[u][2], t[u][1]),
+                           f4sub(t[u][1], t[u][3])};
+#pragma unroll
+      for (int v = 0; v < 4; ++v) *reinterpret_cast<float4*>(Vb + vidx(u * 4 + v, r, q)) = e[v];
+    }
+  };
+
+  // ---- B operand: U in fragment order [nb][kc][xi][lane][8]
+  const int kc_n = a.Cin_p / WK;
+  const float* Ub = U + ((size_t)tn * kc_n * 16) * 512 + (size_t)lane * 8;
+  float4 bc[4][2], bn[4][2];
+  auto bload = [&](float4 (&dst)[4][2], int ks) {
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      const float* p = Ub + ((size_t)ks * 16 + wave * 4 + c) * 512;
+      dst[c][0] = *reinterpret_cast<const float4*>(p);
+      dst[c][1] = *reinterpret_cast<const float4*>(p + 4);
+    }
+  };
+
+  floatx16 acc[4][2];
+#pragma unroll
+  for (int c = 0; c < 4; ++c)
+#pragma unroll
+    for (int mb = 0; mb < 2; ++mb)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) acc[c][mb][e] = 0.f;
+
+  const int h = lane >> 5;
+  gload(0);
+  transform(smem);
+  if (kc_n > 1) gload(1);
+  bload(bc, 0);
+  __syncthreads();
+  for (int ks = 0; ks < kc_n; ++ks) {
+    const float* Vb = smem + (ks & 1) * (16 * WT * WK);
+    if (ks + 1 < kc_n) bload(bn, ks + 1);
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      const int xi = wave * 4 + c;
+      float4 a0[2][2];
+#pragma unroll
+      for (int mb = 0; mb < 2; ++mb) {
+        const int t = mb * 32 + (lane & 31);
+        a0[mb][0] = *reinterpret_cast<const float4*>(Vb + vidx(xi, t, 2 * h));
+        a0[mb][1] = *reinterpret_cast<const float4*>(Vb + vidx(xi, t, 2 * h + 1));
+      }
+      const float bv[8] = {bc[c][0].x, bc[c][0].y, bc[c][0].z, bc[c][0].w,
+                           bc[c][1].x, bc[c][1].y, bc[c][1].z, bc[c][1].w};
+#pragma unroll
+      for (int mb = 0; mb < 2; ++mb) {
+        const float av[8] = {a0[mb][0].x, a0[mb][0].y, a0[mb][0].z, a0[mb][0].w,
+                             a0[mb][1].x, a0[mb][1].y, a0[mb][1].z, a0[mb][1].w};
+#pragma unroll
+        for (int s = 0; s < 8; ++s)             // MFMA step s, half h <-> channel 8h + s
+          acc[c][mb] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[s], bv[s], acc[c][mb], 0, 0, 0);
+      }
+    }
+    if (ks + 1 < kc_n) transform(smem + ((ks + 1) & 1) * (16 * WT * WK));
+    if (ks + 2 < kc_n) gload(ks + 2);
+    __syncthreads();
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      bc[c][0] = bn[c][0];
+      bc[c][1] = bn[c][1];
+    }
+  }
+
+  // ---- epilogue: components -> LDS M[xi][tile][32 ch] (C layout: row = tile, col = channel)
+  float* M = smem;
+#pragma unroll
+  for (int c = 0; c < 4; ++c)
+#pragma unroll
+    for (int mb = 0; mb < 2; ++mb)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) {
+        const int t = mb * 32 + (e & 3) + 8 * (e >> 2) + 4 * h;
+        M[((wave * 4 + c) * WT + t) * WN + (lane & 31)] = acc[c][mb][e];
+      }
+  __syncthreads();
+  EpiMax mx;
+  const int n = n0 + (lane & 31);
+  const int wpp = a.Cout_p >> 5;
+#pragma unroll 1
+  for (int it = 0; it < WT / 8; ++it) {
+    const int t = (tid >> 5) + 8 * it;               // 8 tiles per pass, 32 channels each
+    int bb, tti, ttj;
+    const bool tl = tile_point(a, Ht, Wt, m0 + t, bb, tti, ttj);
+    float m[16];
+#pragma unroll
+    for (int xi = 0; xi < 16; ++xi) m[xi] = M[(xi * WT + t) * WN + (lane & 31)];
+    // A^T m A, A^T = [[1,1,1,0],[0,1,-1,-1]]
+    float s0[4], s1[4];
+#pragma unroll
+    for (int v = 0; v < 4; ++v) {
+      s0[v] = m[0 * 4 + v] + m[1 * 4 + v] + m[2 * 4 + v];
+      s1[v] = m[1 * 4 + v] - m[2 * 4 + v] - m[3 * 4 + v];
+    }
+    const float yv[2][2] = {{s0[0] + s0[1] + s0[2], s0[1] - s0[2] - s0[3]},
+                            {s1[0] + s1[1] + s1[2], s1[1] - s1[2] - s1[3]}};
+    int4 bx = make_int4(0, 0, 1 << 30, 1 << 30);
+    if (a.gbox && tl) bx = reinterpret_cast<const int4*>(a.gbox)[bb];
+#pragma unroll
+    for (int di = 0; di < 2; ++di)
+#pragma unroll
+      for (int dj = 0; dj < 2; ++dj) {
+        const int i = 2 * tti + di, j = 2 * ttj + dj;
+        const bool ok = tl && n < a.N && i < a.Hout && j < a.Wout && i >= bx.x && i < bx.z && j >= bx.y && j < bx.w;
+        const size_t pix = ((size_t)bb * a.Hout + i) * a.Wout + j;
+        float out = 0.f;
+        if (ok) out = epi_store(a, pix, n, yv[di][dj], mx);
+        if (a.ybits) {
+          // 32 lanes = 32 channels of one pixel: one sign-bit word
+          const uint64_t bits = __ballot(ok && out > 0.f);
+          const uint32_t w = (uint32_t)(bits >> (lane & 32));
+          if (ok && (lane & 31) == 0) a.ybits[pix * wpp + (n0 >> 5)] = w;
+        }
+      }
+  }
+  if (a.y_amax) po::amax_commit(a.y_amax, mx.y);
+  if (a.sum_amax) po::amax_commit(a.sum_amax, mx.s);
+  if (a.y2_amax) po::amax_commit(a.y2_amax, mx.y2);
+}
+}  // namespace
+
+namespace po {
+// po_conv tile staging 5: Winograd F(2x2,3x3).  Applies to a stride-1 3x3
+// correlation over the full 3x3 neighbourhood on full maps (no windows, no
+// split-K, destination = source grid) with N % 32 == 0, Cin_p % 16 == 0 and
+// the transformed weights (po_conv_desc.Wwino).
+int launch_wino(const ConvArgs& a, const float* U, hipStream_t st) {
+  PO_REQUIRE(U, "po_conv: Winograd tile needs the transformed weights (Wwino)");
+  PO_REQUIRE(a.prec == 0 && a.ntaps == 9 && a.tkw == 3 && (a.sdh == 1 || a.sdh == -1) && (a.sdw == 1 || a.sdw == -1) &&
+                 a.dh0 == -a.sdh && a.dw0 == -a.sdw,
+             "po_conv: Winograd tile needs a full 3x3 neighbourhood of taps");
+  PO_REQUIRE(a.in_step == 1 && a.out_step == 1 && a.out_oy == 0 && a.out_ox == 0 && !a.in_org && !a.out_org,
+             "po_conv: Winograd tile needs stride 1 on full maps");
+  PO_REQUIRE(a.ksplit == 1, "po_conv: Winograd tile has no split-K");
+  PO_REQUIRE(a.Hg == a.Hout && a.Wg == a.Wout && a.Hin == a.Hout && a.Win == a.Wout,
+             "po_conv: Winograd tile needs source, grid and destination of one size");
+  PO_REQUIRE(a.N % WN == 0 && a.Cin_p % WK == 0, "po_conv: Winograd tile needs N %% 32 == 0 and Cin_p %% 16 == 0");
+  const int Ht = (a.Hout + 1) / 2, Wt = (a.Wout + 1) / 2;
+  PO_REQUIRE((int64_t)a.B * Ht * Wt < (1LL << 31), "po_conv: too many tiles");
+  ConvArgs b = a;
+  b.ntiles_n = a.N / WN;
+  const int ntm = ceil_div((int64_t)a.B * Ht * Wt, WT);
+  hipLaunchKernelGGL(conv_wino_k, dim3(ntm * b.ntiles_n), dim3(256), 0, st, b, U, Ht, Wt);
+  return check_launch("po_conv (winograd)");
+}
+}  // namespace po

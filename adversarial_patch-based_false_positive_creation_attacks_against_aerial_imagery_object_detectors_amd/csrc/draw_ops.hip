@@ -1,0 +1,106 @@
+// Per-step random draws of the patch transformer and the patch-gradient
+// finiteness guard.
+//
+// po_draws replaces the reference's draws (load_data.py:548-574 contrast /
+// brightness / noise from the CUDA RNG, 607-614 angle, 693-707 target_x/y from
+// the CPU RNG) with a counter-based generator: every variate is a pure
+// function of (seed, step counter, GLOBAL image index, element), so a rank
+// that processes images [b0, b0+B) of a global batch draws exactly the rows
+// a single process would draw for them — the data-parallel result does not
+// depend on the number of ranks and a step needs no host RNG.
+//
+// Generator: Philox4x32-10 (Salmon et al., SC'11), key = seed, counter =
+// {element group, global image, step lo, step hi}; one call gives 4 uniform
+// u = (x >> 8) * 2^-24 in [0,1).  Noise element e of image b is lane e%4 of
+// group e/4; the per-image scalars are groups 0xFFFFFFFF {contrast, bright,
+// angle, ux} and 0xFFFFFFFE {uy}.  oracle/draws_ref.py restates it in numpy.
+#pragma clang fp contract(off)
+#include "common.h"
+
+namespace {
+
+struct u4 {
+  uint32_t x, y, z, w;
+};
+
+__device__ __forceinline__ u4 philox4x32_10(u4 c, uint32_t k0, uint32_t k1) {
+  constexpr uint32_t M0 = 0xD2511F53u, M1 = 0xCD9E8D57u, W0 = 0x9E3779B9u, W1 = 0xBB67AE85u;
+#pragma unroll
+  for (int r = 0; r < 10; ++r) {
+    const uint32_t lo0 = M0 * c.x, hi0 = __umulhi(M0, c.x);
+    const uint32_t lo1 = M1 * c.z, hi1 = __umulhi(M1, c.z);
+    c = u4{hi1 ^ c.y ^ k0, lo1, hi0 ^ c.w ^ k1, lo0};
+    k0 += W0;
+    k1 += W1;
+  }
+  return c;
+}
+
+__device__ __forceinline__ float unif(uint32_t x) { return (float)(x >> 8) * 0x1p-24f; }
+// from + u * span, rounded as two separate fp32 operations (no fma)
+__device__ __forceinline__ float affine(float u, float span, float from) { return __fadd_rn(__fmul_rn(u, span), from); }
+
+constexpr float kPi = 3.14159265358979323846f;
+
+__global__ __launch_bounds__(256) void draws_k(uint32_t k0, uint32_t k1, uint32_t c_lo, uint32_t c_hi, int b0,
+                                               int n, float* __restrict__ contrast, float* __restrict__ bright,
+                                               float* __restrict__ noise, float* __restrict__ angle,
+                                               float* __restrict__ ux, float* __restrict__ uy) {
+  const int b = blockIdx.y;
+  const uint32_t gb = (uint32_t)(b0 + b);
+  const int g = blockIdx.x * 256 + threadIdx.x;        // element group of 4 noise values
+  const int ngroups = (n + 3) / 4;
+  if (g < ngroups && noise) {
+    const u4 r = philox4x32_10(u4{(uint32_t)g, gb, c_lo, c_hi}, k0, k1);
+    float* o = noise + (size_t)b * n;
+    const float v[4] = {affine(unif(r.x), 2.0f, -1.0f), affine(unif(r.y), 2.0f, -1.0f),
+                        affine(unif(r.z), 2.0f, -1.0f), affine(unif(r.w), 2.0f, -1.0f)};
+    const int e0 = 4 * g;
+    if (e0 + 4 <= n && (n & 3) == 0) {
+      *reinterpret_cast<float4*>(o + e0) = make_float4(v[0], v[1], v[2], v[3]);
+    } else {
+      for (int q = 0; q < 4 && e0 + q < n; ++q) o[e0 + q] = v[q];
+    }
+  }
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    const u4 s = philox4x32_10(u4{0xFFFFFFFFu, gb, c_lo, c_hi}, k0, k1);
+    const u4 t = philox4x32_10(u4{0xFFFFFFFEu, gb, c_lo, c_hi}, k0, k1);
+    if (contrast) contrast[b] = affine(unif(s.x), 0.4f, 0.8f);      // U(0.8, 1.2)   load_data.py:548-553
+    if (bright) bright[b] = affine(unif(s.y), 0.2f, -0.1f);         // U(-0.1, 0.1)  556-561
+    if (angle) angle[b] = affine(unif(s.z), 2.0f * kPi, -kPi);      // U(-pi, pi)    607-614
+    if (ux) ux[b] = unif(s.w);                                       // U(0,1)        693-707
+    if (uy) uy[b] = unif(t.x);
+  }
+}
+
+// flags[0] |= bit if any of x[0..n) is NaN or +-Inf
+__global__ __launch_bounds__(256) void check_finite_k(const float* __restrict__ x, int64_t n, int32_t bit,
+                                                      int32_t* __restrict__ flags) {
+  bool bad = false;
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256)
+    bad |= !isfinite(x[i]);
+  if (__any(bad) && (threadIdx.x & 63) == 0) atomicOr(flags, bit);
+}
+
+}  // namespace
+
+extern "C" int po_draws(uint64_t seed, uint64_t counter, int b0, int B, int P, float* contrast, float* bright,
+                        float* noise, float* angle, float* ux, float* uy, po_stream_t s) {
+  PO_REQUIRE(B >= 1 && B <= 65535 && b0 >= 0 && P >= 1, "po_draws: bad sizes (b0=%d B=%d P=%d)", b0, B, P);
+  const int64_t n = 3LL * P * P;
+  PO_REQUIRE(n < (1LL << 31), "po_draws: patch too large");
+  const int ngroups = (int)((n + 3) / 4);
+  dim3 grid(noise ? po::ceil_div(ngroups, 256) : 1, B);
+  hipLaunchKernelGGL(draws_k, grid, dim3(256), 0, po::stream_of(s), (uint32_t)seed, (uint32_t)(seed >> 32),
+                     (uint32_t)counter, (uint32_t)(counter >> 32), b0, (int)n, contrast, bright, noise, angle, ux,
+                     uy);
+  return po::check_launch("po_draws");
+}
+
+extern "C" int po_check_finite(const float* x, int64_t n, int32_t bit, int32_t* flags, po_stream_t s) {
+  PO_REQUIRE(x && flags && n >= 0, "po_check_finite: null pointer");
+  if (n == 0) return PO_OK;
+  const int grid = (int)std::min<int64_t>(po::ceil_div(n, 256), 1024);
+  hipLaunchKernelGGL(check_finite_k, dim3(grid), dim3(256), 0, po::stream_of(s), x, n, bit, flags);
+  return po::check_launch("po_check_finite");
+}

@@ -140,7 +140,7 @@ __global__ __launch_bounds__(256) void cell_loss_k(LossArgs a, const float* __re
     }
     out2[0] = 4.f * (1.f - sm / (float)a.B);                       // train_patch.py:236-239
     out2[1] = a.objective == 0 ? sc / (float)a.B : (a.objective == 1 ? sc : 0.f);
-    if (flags) flags[0] = s_flag;
+    if (flags && s_flag) atomicOr(flags, s_flag);       // accumulates over calls
   }
 }
 }  // namespace

@@ -143,7 +143,8 @@ __global__ __launch_bounds__(64) void patch_params_k(const float* __restrict__ l
                                                      const float* __restrict__ angle, const float* __restrict__ ux,
                                                      const float* __restrict__ uy, int do_rotate, int S, int P,
                                                      float* __restrict__ theta, float* __restrict__ center,
-                                                     float* __restrict__ tsize, int32_t* __restrict__ roi) {
+                                                     float* __restrict__ tsize, int32_t* __restrict__ roi,
+                                                     double* __restrict__ affine) {
   const int b = blockIdx.x;
   const int lane = threadIdx.x;
   const float* lb = lab + (size_t)b * L * 5;
@@ -163,70 +164,83 @@ __global__ __launch_bounds__(64) void patch_params_k(const float* __restrict__ l
     if (nv < vmin || (nv == vmin && ni < imin)) { vmin = nv; imin = ni; }
   }
   if (lane != 0) return;
-  float sel2, sel3;
-  if (vmax > 0.99f) {                       // load_data.py:471-473
-    sel2 = 0.25f; sel3 = 0.25f;
-  } else {                                  // load_data.py:474-477
-    sel2 = (lb[imax * 5 + 2] + lb[imin * 5 + 2]) / 2.f;
-    sel3 = (lb[imax * 5 + 3] + lb[imin * 5 + 3]) / 2.f;
-  }
+  // patch centre in fp32 exactly as the reference (load_data.py:703-715): the
+  // loss cell index is derived from it and must be bit-exact
   const float fS = (float)S;
-  float l2 = sel2 * fS, l3 = sel3 * fS;      // load_data.py:651-655
-  float h2 = l2 * 0.5f, h3 = l3 * 0.5f;      // .mul(1/pre_scale), SCALE_FACTOR=2
-  float ts = sqrtf(h2 * h2 + h3 * h3);       // load_data.py:662-663
-  float tx_ = fmaxf(ux[b], 0.2f);            // load_data.py:703
-  float ty_ = fminf(uy[b], 0.8f);            // load_data.py:706
-  center[2 * b + 0] = tx_ * fS;              // load_data.py:712-715
-  center[2 * b + 1] = ty_ * fS;
-  float scale = ts / (float)P;               // load_data.py:717
-  float tx = (-tx_ + 0.5f) * 2.f;            // load_data.py:726
-  float ty = (-ty_ + 0.5f) * 2.f;            // load_data.py:727
-  float a = do_rotate ? angle[b] : 0.f;
-  float sn = sinf(a), cs = cosf(a);
-  float* th = theta + 6 * b;                 // load_data.py:738-743
-  th[0] = cs / scale;
-  th[1] = sn / scale;
-  th[2] = tx * cs / scale + ty * sn / scale;
-  th[3] = -sn / scale;
-  th[4] = cs / scale;
-  th[5] = -tx * sn / scale + ty * cs / scale;
-  if (tsize) tsize[b] = ts;
+  const float tx_f = fmaxf(ux[b], 0.2f);     // load_data.py:703
+  const float ty_f = fminf(uy[b], 0.8f);     // load_data.py:706
+  center[2 * b + 0] = tx_f * fS;             // load_data.py:712-715
+  center[2 * b + 1] = ty_f * fS;
+  // Placement geometry in float64 (from the same fp32 labels and draws).  The
+  // translation terms of theta reach |tx cos / scale| ~ 10-20 and cancel in the
+  // affine grid down to the patch's ~0.4; in fp32 that cancellation leaves
+  // ~1e-4 px of error in the sampling coordinates, i.e. ~1e-4 relative in the
+  // bilinear weights and the patch gradient.  In double the HIP warp samples
+  // where the exact (float64) evaluation of the reference formulas samples.
+  double sel2, sel3;
+  if (vmax > 0.99f) {                        // load_data.py:471-473
+    sel2 = 0.25; sel3 = 0.25;
+  } else {                                   // load_data.py:474-477
+    sel2 = ((double)lb[imax * 5 + 2] + (double)lb[imin * 5 + 2]) / 2.0;
+    sel3 = ((double)lb[imax * 5 + 3] + (double)lb[imin * 5 + 3]) / 2.0;
+  }
+  const double dS = (double)S;
+  const double h2 = sel2 * dS * 0.5, h3 = sel3 * dS * 0.5;   // load_data.py:651-655, 1/SCALE_FACTOR
+  const double ts = sqrt(h2 * h2 + h3 * h3);                 // load_data.py:662-663
+  const double txd = fmax((double)ux[b], 0.2), tyd = fmin((double)uy[b], 0.8);
+  const double scale = ts / (double)P;                       // load_data.py:717
+  const double tx = (-txd + 0.5) * 2.0;                      // load_data.py:726
+  const double ty = (-tyd + 0.5) * 2.0;                      // load_data.py:727
+  const double a = do_rotate ? (double)angle[b] : 0.0;
+  const double sn = sin(a), cs = cos(a);
+  const double th[6] = {cs / scale, sn / scale, tx * cs / scale + ty * sn / scale,      // load_data.py:738-743
+                        -sn / scale, cs / scale, -tx * sn / scale + ty * cs / scale};
+  float* tho = theta + 6 * b;
+  for (int k = 0; k < 6; ++k) tho[k] = (float)th[k];
+  if (tsize) tsize[b] = (float)ts;
+  // pixel-space affine of affine_grid + grid_sample (align_corners=False):
+  // ix = A00 j + A01 i + A02, iy = A10 j + A11 i + A12 for output pixel (i, j)
+  const double half = 0.5 - 0.5 * dS;
+  const double A00 = th[0], A01 = th[1], A10 = th[3], A11 = th[4];
+  const double A02 = (th[0] + th[1]) * half + 0.5 * dS * th[2] + 0.5 * (dS - 1.0);
+  const double A12 = (th[3] + th[4]) * half + 0.5 * dS * th[5] + 0.5 * (dS - 1.0);
+  if (affine) {
+    double* af = affine + 6 * b;
+    af[0] = A00; af[1] = A01; af[2] = A02; af[3] = A10; af[4] = A11; af[5] = A12;
+  }
   if (roi) {
     // output pixels whose bilinear sample can touch the padded patch region:
     // preimage of [pad-1, pad+P) x [pad-1, pad+P) under the pixel-space affine
-    const float half = 0.5f - 0.5f * fS;
-    const float A00 = th[0], A01 = th[1], A10 = th[3], A11 = th[4];
-    const float A02 = (th[0] + th[1]) * half + 0.5f * fS * th[2] + 0.5f * (fS - 1.f);
-    const float A12 = (th[3] + th[4]) * half + 0.5f * fS * th[5] + 0.5f * (fS - 1.f);
-    const float det = A00 * A11 - A01 * A10;
+    const double det = A00 * A11 - A01 * A10;
     const int padL = (int)((S - P) / 2.0 + 0.5);
-    float jlo = 1e30f, jhi = -1e30f, ilo = 1e30f, ihi = -1e30f;
+    double jlo = 1e30, jhi = -1e30, ilo = 1e30, ihi = -1e30;
     for (int k = 0; k < 4; ++k) {
-      const float X = (float)((k & 1) ? padL + P : padL - 1) - A02;
-      const float Y = (float)((k & 2) ? padL + P : padL - 1) - A12;
-      const float jj = (A11 * X - A01 * Y) / det, ii = (-A10 * X + A00 * Y) / det;
-      jlo = fminf(jlo, jj); jhi = fmaxf(jhi, jj);
-      ilo = fminf(ilo, ii); ihi = fmaxf(ihi, ii);
+      const double X = (double)((k & 1) ? padL + P : padL - 1) - A02;
+      const double Y = (double)((k & 2) ? padL + P : padL - 1) - A12;
+      const double jj = (A11 * X - A01 * Y) / det, ii = (-A10 * X + A00 * Y) / det;
+      jlo = fmin(jlo, jj); jhi = fmax(jhi, jj);
+      ilo = fmin(ilo, ii); ihi = fmax(ihi, ii);
     }
-    const float lo = -4.f, hi = fS + 4.f;      // clamp before the int conversion
-    jlo = fminf(fmaxf(jlo, lo), hi); jhi = fminf(fmaxf(jhi, lo), hi);
-    ilo = fminf(fmaxf(ilo, lo), hi); ihi = fminf(fmaxf(ihi, lo), hi);
-    roi[4 * b + 0] = max(0, (int)floorf(jlo) - 2);
-    roi[4 * b + 1] = max(0, (int)floorf(ilo) - 2);
-    roi[4 * b + 2] = min(S, (int)ceilf(jhi) + 3);
-    roi[4 * b + 3] = min(S, (int)ceilf(ihi) + 3);
+    const double lo = -4.0, hi = dS + 4.0;      // clamp before the int conversion
+    jlo = fmin(fmax(jlo, lo), hi); jhi = fmin(fmax(jhi, lo), hi);
+    ilo = fmin(fmax(ilo, lo), hi); ihi = fmin(fmax(ihi, lo), hi);
+    roi[4 * b + 0] = max(0, (int)floor(jlo) - 2);
+    roi[4 * b + 1] = max(0, (int)floor(ilo) - 2);
+    roi[4 * b + 2] = min(S, (int)ceil(jhi) + 3);
+    roi[4 * b + 3] = min(S, (int)ceil(ihi) + 3);
   }
 }
 }  // namespace
 
 extern "C" int po_patch_params(const float* lab, int B, int L, const float* angle, const float* ux,
                                const float* uy, int do_rotate, int S, int P, float* theta,
-                               float* center, float* target_size, int32_t* roi, po_stream_t s) {
+                               float* center, float* target_size, int32_t* roi, double* affine,
+                               po_stream_t s) {
   PO_REQUIRE(lab && ux && uy && theta && center, "po_patch_params: null pointer");
   PO_REQUIRE(!do_rotate || angle, "po_patch_params: angle required when do_rotate");
   PO_REQUIRE(B > 0 && L > 0 && S > 0 && P > 0, "po_patch_params: bad shape");
   hipLaunchKernelGGL(patch_params_k, dim3(B), dim3(64), 0, po::stream_of(s), lab, B, L, angle, ux, uy,
-                     do_rotate, S, P, theta, center, target_size, roi);
+                     do_rotate, S, P, theta, center, target_size, roi, affine);
   return po::check_launch("po_patch_params");
 }
 
@@ -238,22 +252,25 @@ struct WarpGeom {
   int S, P, padL, padT;
 };
 
-// torch.linspace(-1,1,S) (scalar / CUDA formula) * (S-1) / S  (affine_grid base, align_corners=False)
-__device__ __forceinline__ float grid_base(int j, int S) {
-  const float step = 2.0f / (float)(S - 1);
-  float v = (j < S / 2) ? (-1.0f + step * (float)j) : (1.0f - step * (float)(S - 1 - j));
-  v = v * (float)(S - 1);
-  return v / (float)S;
+// Source coordinate (ix: column, iy: row) in the padded patch of output pixel
+// (i, j): affine_grid (align_corners=False) + grid_sampler_unnormalize folded
+// into the pixel-space affine af (po_patch_params), evaluated in float64.
+__device__ __forceinline__ void sample_coord(const double* af, int i, int j, double& ix, double& iy) {
+  ix = fma(af[0], (double)j, fma(af[1], (double)i, af[2]));
+  iy = fma(af[3], (double)j, fma(af[4], (double)i, af[5]));
 }
 
-// source coordinate (ix: column, iy: row) for output pixel (i, j)
-__device__ __forceinline__ void sample_coord(const float* th, int i, int j, int S, float& ix, float& iy) {
-  const float x = grid_base(j, S), y = grid_base(i, S);
-  const float gx = th[0] * x + th[1] * y + th[2];
-  const float gy = th[3] * x + th[4] * y + th[5];
-  const float fS = (float)S;
-  ix = ((gx + 1.f) * fS - 1.f) / 2.f;   // grid_sampler_unnormalize, align_corners=False
-  iy = ((gy + 1.f) * fS - 1.f) / 2.f;
+// Bilinear corner (x0, y0) and weights {nw, ne, sw, se} of a sample point
+// (weights from the float64 coordinate, rounded once to fp32)
+__device__ __forceinline__ void bilinear(double ix, double iy, int& x0, int& y0, float w[4]) {
+  const double fx = floor(ix), fy = floor(iy);
+  x0 = (int)fx;
+  y0 = (int)fy;
+  const double ex = ix - fx, ey = iy - fy;              // in [0, 1)
+  w[0] = (float)((1.0 - ex) * (1.0 - ey));
+  w[1] = (float)(ex * (1.0 - ey));
+  w[2] = (float)((1.0 - ex) * ey);
+  w[3] = (float)(ex * ey);
 }
 
 __device__ __forceinline__ float aug_value(const float* __restrict__ mp, const float* __restrict__ nz,
@@ -265,24 +282,20 @@ __device__ __forceinline__ float aug_value(const float* __restrict__ mp, const f
 
 // Forward of one output pixel: adv_t[3] (clamped) and msk_t.  Returns false
 // if no neighbour lies inside the padded patch region (output exactly 0).
-__device__ __forceinline__ bool warp_pixel(const float* th, const WarpGeom& g, const float* mp,
+__device__ __forceinline__ bool warp_pixel(const double* af, const WarpGeom& g, const float* mp,
                                            const float* nz, float contrast, float bright, int i, int j,
                                            float adv[3], float& msk, bool raw_in_range[3]) {
-  float ix, iy;
-  sample_coord(th, i, j, g.S, ix, iy);
-  const float fx = floorf(ix), fy = floorf(iy);
-  if (!(fx >= (float)(g.padL - 1) && fx <= (float)(g.padL + g.P - 1) &&
-        fy >= (float)(g.padT - 1) && fy <= (float)(g.padT + g.P - 1)))
+  double ix, iy;
+  sample_coord(af, i, j, ix, iy);
+  // no corner inside the padded patch region [pad, pad+P): output exactly 0
+  if (!(ix >= (double)(g.padL - 1) && ix < (double)(g.padL + g.P) && iy >= (double)(g.padT - 1) &&
+        iy < (double)(g.padT + g.P)))
     return false;
-  const int x0 = (int)fx, y0 = (int)fy;
-  const float xs = (float)(x0 + 1), ys = (float)(y0 + 1);
-  const float w_nw = (xs - ix) * (ys - iy);
-  const float w_ne = (ix - (float)x0) * (ys - iy);
-  const float w_sw = (xs - ix) * (iy - (float)y0);
-  const float w_se = (ix - (float)x0) * (iy - (float)y0);
+  int x0, y0;
+  float w[4];
+  bilinear(ix, iy, x0, y0, w);
   const int cx[4] = {x0, x0 + 1, x0, x0 + 1};
   const int cy[4] = {y0, y0, y0 + 1, y0 + 1};
-  const float w[4] = {w_nw, w_ne, w_sw, w_se};
   float a0 = 0.f, a1 = 0.f, a2 = 0.f, m = 0.f;
 #pragma unroll
   for (int k = 0; k < 4; ++k) {
@@ -309,7 +322,7 @@ __global__ __launch_bounds__(256) void warp_fwd_k(const float* __restrict__ img,
                                                   const float* __restrict__ noise,
                                                   const float* __restrict__ contrast,
                                                   const float* __restrict__ bright,
-                                                  const float* __restrict__ theta, WarpGeom g, int mode,
+                                                  const double* __restrict__ affine, WarpGeom g, int mode,
                                                   float* __restrict__ out) {
   const int b = blockIdx.z;
   const int i = blockIdx.y, j = blockIdx.x * 256 + threadIdx.x;
@@ -318,7 +331,7 @@ __global__ __launch_bounds__(256) void warp_fwd_k(const float* __restrict__ img,
   const size_t o = (size_t)b * 3 * plane + (size_t)i * g.S + j;
   float adv[3], msk;
   bool rng[3];
-  const bool hit = warp_pixel(theta + 6 * b, g, mp, noise + (size_t)b * 3 * g.P * g.P, contrast[b],
+  const bool hit = warp_pixel(affine + 6 * b, g, mp, noise + (size_t)b * 3 * g.P * g.P, contrast[b],
                               bright[b], i, j, adv, msk, rng);
 #pragma unroll
   for (int ch = 0; ch < 3; ++ch) {
@@ -336,7 +349,7 @@ __global__ __launch_bounds__(256) void warp_fwd4_k(const float* __restrict__ img
                                                    const float* __restrict__ noise,
                                                    const float* __restrict__ contrast,
                                                    const float* __restrict__ bright,
-                                                   const float* __restrict__ theta, WarpGeom g, int mode,
+                                                   const double* __restrict__ affine, WarpGeom g, int mode,
                                                    float* __restrict__ out) {
   const int b = blockIdx.y;
   const int sq = g.S >> 2;
@@ -345,7 +358,7 @@ __global__ __launch_bounds__(256) void warp_fwd4_k(const float* __restrict__ img
   const int i = q / sq, j0 = (q - i * sq) * 4;
   const size_t plane = (size_t)g.S * g.S;
   const size_t o = (size_t)b * 3 * plane + (size_t)i * g.S + j0;
-  const float* th = theta + 6 * b;
+  const double* th = affine + 6 * b;
   const float* nz = noise + (size_t)b * 3 * g.P * g.P;
   const float cb = contrast[b], bb = bright[b];
   float v[3][4];
@@ -376,7 +389,7 @@ __global__ __launch_bounds__(256) void warp_bwd_a_k(const float* __restrict__ d_
                                                     const float* __restrict__ noise,
                                                     const float* __restrict__ contrast,
                                                     const float* __restrict__ bright,
-                                                    const float* __restrict__ theta, WarpGeom g,
+                                                    const double* __restrict__ affine, WarpGeom g,
                                                     int mode, float* __restrict__ gfac) {
   const int b = blockIdx.z;
   const int i = blockIdx.y, j = blockIdx.x * 256 + threadIdx.x;
@@ -385,7 +398,7 @@ __global__ __launch_bounds__(256) void warp_bwd_a_k(const float* __restrict__ d_
   const size_t o = (size_t)b * 3 * plane + (size_t)i * g.S + j;
   float adv[3], msk;
   bool rng[3];
-  if (!warp_pixel(theta + 6 * b, g, mp, noise + (size_t)b * 3 * g.P * g.P, contrast[b], bright[b],
+  if (!warp_pixel(affine + 6 * b, g, mp, noise + (size_t)b * 3 * g.P * g.P, contrast[b], bright[b],
                   i, j, adv, msk, rng))
     return;   // never read by phase B
 #pragma unroll
@@ -411,7 +424,7 @@ __global__ __launch_bounds__(256) void warp_bwd_b_k(const float* __restrict__ gf
                                                     const float* __restrict__ noise,
                                                     const float* __restrict__ contrast,
                                                     const float* __restrict__ bright,
-                                                    const float* __restrict__ theta, WarpGeom g,
+                                                    const double* __restrict__ affine, WarpGeom g,
                                                     int B, float* __restrict__ d_mp) {
   __shared__ float part[3][WB_G][WB_EL];
   const int el = threadIdx.x % WB_EL, q = threadIdx.x / WB_EL;
@@ -421,42 +434,38 @@ __global__ __launch_bounds__(256) void warp_bwd_b_k(const float* __restrict__ gf
   const int pr = e / g.P, pc = e % g.P;
   const int r = pr + g.padT, c = pc + g.padL;
   const size_t plane = (size_t)g.S * g.S;
-  const float fS = (float)g.S, half = 0.5f - 0.5f * fS;
   float d0 = 0.f, d1 = 0.f, d2 = 0.f;
   for (int b = q; b < (live ? B : 0); b += WB_G) {
-    const float* th = theta + 6 * b;
-    // pixel-space affine: ix = A00 j + A01 i + A02, iy = A10 j + A11 i + A12
-    const float A00 = th[0], A01 = th[1], A10 = th[3], A11 = th[4];
-    const float A02 = (th[0] + th[1]) * half + 0.5f * fS * th[2] + 0.5f * (fS - 1.f);
-    const float A12 = (th[3] + th[4]) * half + 0.5f * fS * th[5] + 0.5f * (fS - 1.f);
-    const float det = A00 * A11 - A01 * A10;
-    float jlo = 1e30f, jhi = -1e30f, ilo = 1e30f, ihi = -1e30f;
+    const double* af = affine + 6 * b;
+    // output pixels whose sample point can have (r, c) as a bilinear corner:
+    // the preimage of (c-1, c+1) x (r-1, r+1) under the pixel-space affine
+    const double A00 = af[0], A01 = af[1], A02 = af[2], A10 = af[3], A11 = af[4], A12 = af[5];
+    const double det = A00 * A11 - A01 * A10;
+    double jlo = 1e30, jhi = -1e30, ilo = 1e30, ihi = -1e30;
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
-      const float X = (float)c + ((k & 1) ? 1.f : -1.f) - A02;
-      const float Y = (float)r + ((k & 2) ? 1.f : -1.f) - A12;
-      const float jj = (A11 * X - A01 * Y) / det;
-      const float ii = (-A10 * X + A00 * Y) / det;
-      jlo = fminf(jlo, jj); jhi = fmaxf(jhi, jj);
-      ilo = fminf(ilo, ii); ihi = fmaxf(ihi, ii);
+      const double X = (double)c + ((k & 1) ? 1.0 : -1.0) - A02;
+      const double Y = (double)r + ((k & 2) ? 1.0 : -1.0) - A12;
+      const double jj = (A11 * X - A01 * Y) / det;
+      const double ii = (-A10 * X + A00 * Y) / det;
+      jlo = fmin(jlo, jj); jhi = fmax(jhi, jj);
+      ilo = fmin(ilo, ii); ihi = fmax(ihi, ii);
     }
-    if (!(jhi >= -1.f && jlo <= fS && ihi >= -1.f && ilo <= fS)) continue;
-    const int j0 = max(0, (int)floorf(jlo) - 1), j1 = min(g.S - 1, (int)ceilf(jhi) + 1);
-    const int i0 = max(0, (int)floorf(ilo) - 1), i1 = min(g.S - 1, (int)ceilf(ihi) + 1);
+    if (!(jhi >= -1.0 && jlo <= (double)g.S && ihi >= -1.0 && ilo <= (double)g.S)) continue;
+    const int j0 = max(0, (int)floor(jlo) - 1), j1 = min(g.S - 1, (int)ceil(jhi) + 1);
+    const int i0 = max(0, (int)floor(ilo) - 1), i1 = min(g.S - 1, (int)ceil(ihi) + 1);
     float a0 = 0.f, a1 = 0.f, a2 = 0.f;
     const float* gb = gfac + (size_t)b * 3 * plane;
     for (int i = i0; i <= i1; ++i)
       for (int j = j0; j <= j1; ++j) {
-        float ix, iy;
-        sample_coord(th, i, j, g.S, ix, iy);
-        const float fx = floorf(ix), fy = floorf(iy);
-        const int x0 = (int)fx, y0 = (int)fy;
+        double ix, iy;
+        sample_coord(af, i, j, ix, iy);
+        int x0, y0;
+        float wb[4];
+        bilinear(ix, iy, x0, y0, wb);
         const int dx = c - x0, dy = r - y0;
         if (dx < 0 || dx > 1 || dy < 0 || dy > 1) continue;
-        const float xs = (float)(x0 + 1), ys = (float)(y0 + 1);
-        const float wx = dx ? (ix - (float)x0) : (xs - ix);
-        const float wy = dy ? (iy - (float)y0) : (ys - iy);
-        const float w = wx * wy;
+        const float w = wb[2 * dy + dx];
         const size_t o = (size_t)i * g.S + j;
         a0 += w * gb[o];
         a1 += w * gb[o + plane];
@@ -499,37 +508,37 @@ WarpGeom make_geom(int S, int P) {
 }  // namespace
 
 extern "C" int po_warp_fwd(const float* img, const float* patch_mp, const float* noise,
-                           const float* contrast, const float* bright, const float* theta, int B,
+                           const float* contrast, const float* bright, const double* affine, int B,
                            int S, int P, int mode, float* out, po_stream_t s) {
-  PO_REQUIRE(patch_mp && noise && contrast && bright && theta && out, "po_warp_fwd: null pointer");
+  PO_REQUIRE(patch_mp && noise && contrast && bright && affine && out, "po_warp_fwd: null pointer");
   PO_REQUIRE(mode == 0 || (mode == 1 && img), "po_warp_fwd: mode must be 0 or 1 (1 needs img)");
   PO_REQUIRE(B > 0 && S > 1 && P > 0 && P <= S, "po_warp_fwd: bad shape B=%d S=%d P=%d", B, S, P);
   if (S % 4 == 0 && ((uintptr_t)img | (uintptr_t)out) % 16 == 0 && !getenv("PO_WARP_V1")) {
     hipLaunchKernelGGL(warp_fwd4_k, dim3(po::ceil_div(S * (S / 4), 256), B), dim3(256), 0, po::stream_of(s), img,
-                       patch_mp, noise, contrast, bright, theta, make_geom(S, P), mode, out);
+                       patch_mp, noise, contrast, bright, affine, make_geom(S, P), mode, out);
     return po::check_launch("po_warp_fwd");
   }
   dim3 grid(po::ceil_div(S, 256), S, B);
   hipLaunchKernelGGL(warp_fwd_k, grid, dim3(256), 0, po::stream_of(s), img, patch_mp, noise, contrast,
-                     bright, theta, make_geom(S, P), mode, out);
+                     bright, affine, make_geom(S, P), mode, out);
   return po::check_launch("po_warp_fwd");
 }
 
 extern "C" int po_warp_bwd(const float* d_out, const float* patch_mp, const float* noise,
-                           const float* contrast, const float* bright, const float* theta, int B,
+                           const float* contrast, const float* bright, const double* affine, int B,
                            int S, int P, int mode, float* work, float* d_patch_mp, po_stream_t s) {
-  PO_REQUIRE(d_out && patch_mp && noise && contrast && bright && theta && work && d_patch_mp,
+  PO_REQUIRE(d_out && patch_mp && noise && contrast && bright && affine && work && d_patch_mp,
              "po_warp_bwd: null pointer");
   PO_REQUIRE(mode == 0 || mode == 1, "po_warp_bwd: mode must be 0 or 1");
   PO_REQUIRE(B > 0 && S > 1 && P > 0 && P <= S, "po_warp_bwd: bad shape");
   WarpGeom g = make_geom(S, P);
   dim3 grid(po::ceil_div(S, 256), S, B);
   hipLaunchKernelGGL(warp_bwd_a_k, grid, dim3(256), 0, po::stream_of(s), d_out, patch_mp, noise,
-                     contrast, bright, theta, g, mode, work);
+                     contrast, bright, affine, g, mode, work);
   int rc = po::check_launch("po_warp_bwd(a)");
   if (rc) return rc;
   hipLaunchKernelGGL(warp_bwd_b_k, dim3(po::ceil_div(P * P, WB_EL)), dim3(256), 0, po::stream_of(s),
-                     work, patch_mp, noise, contrast, bright, theta, g, B, d_patch_mp);
+                     work, patch_mp, noise, contrast, bright, affine, g, B, d_patch_mp);
   return po::check_launch("po_warp_bwd(b)");
 }
 

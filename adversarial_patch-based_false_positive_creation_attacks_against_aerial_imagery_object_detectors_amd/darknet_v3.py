@@ -682,6 +682,19 @@ class NetPlan:
             return self.net._dev[wts_or_j]["w"]
         return self.net._dgrad_weight(wts_or_j, taps, cin_p, self.device)
 
+    def _attach_wino(self, desc, w):
+        """Winograd F(2x2,3x3) weights (po_conv tile 61) of an exact-fp32
+        launch that is a stride-1 3x3 correlation on full maps."""
+        desc.Wwino = None
+        if (desc.prec != 0 or desc.ntaps != 9 or desc.in_step != 1 or desc.out_step != 1 or desc.in_org
+                or desc.out_org or w.dim() != 3 or w.size(0) % 32 or w.size(2) % 16
+                or os.environ.get("ADVPATCH_WINOGRAD", "1") == "0"):
+            return
+        offs = [(desc.dh[t], desc.dw[t]) for t in range(9)]
+        if sorted(offs) != [(a, b) for a in (-1, 0, 1) for b in (-1, 0, 1)]:
+            return
+        desc.Wwino = self.net._wino(w, offs)
+
     # ---------------- launch lists ----------------
     def _build_ops(self):
         net, blocks, B = self.net, self.net.blocks, self.B
@@ -728,6 +741,7 @@ class NetPlan:
                     f = f if f >= 0 else (i + 1) + f
                     res, sum_out = self.act[self.root[f]], self.act[i + 1]
                 wptr = self._conv_prec(desc, src, i)
+                self._attach_wino(desc, wptr)
                 desc.in_amax = self.slot(inp).value if src != INPUT else None
                 desc.y_amax = self.slot(y_out).value
                 desc.sum_amax = self.slot(sum_out).value if sum_out is not None else None
@@ -961,6 +975,7 @@ class NetPlan:
                 desc.dh[ti] = (py + pad - kh) // s
                 desc.dw[ti] = (px + pad - kw) // s
             desc.N = cin_p
+            self._attach_wino(desc, wd)
             desc.act = 0
             desc.accumulate = acc
             desc.macs = nb * Hg * Wg * m["cin"] * len(taps) * m["cout"]
@@ -1156,6 +1171,26 @@ class NetPlan:
 
 
 
+# Winograd F(2x2,3x3): U = G g G^T with G = [[1,0,0],[.5,.5,.5],[.5,-.5,.5],[0,0,1]]
+_WINO_G = ((1.0, 0.0, 0.0), (0.5, 0.5, 0.5), (0.5, -0.5, 0.5), (0.0, 0.0, 1.0))
+
+
+def wino_transform(w, offs):
+    """po_conv_desc.Wwino of launch weights w [N][9][Cin_p] (fp32) whose tap t
+    reads source offset offs[t] = (dh, dw) in {-1,0,1}^2: U = G g G^T in
+    float64, rounded once to fp32, in MFMA fragment order
+    [N/32][Cin_p/16][16][64 lanes][8], element (lane l, s) of block (nb, kc, xi)
+    = U[xi][16 kc + 8 (l >> 5) + s][32 nb + (l & 31)]."""
+    N, T, C = w.shape
+    assert T == 9 and N % 32 == 0 and C % 16 == 0
+    g = torch.zeros(N, C, 3, 3, dtype=torch.float64, device=w.device)
+    for t, (dh, dw) in enumerate(offs):
+        g[:, :, dh + 1, dw + 1] = w[:, t, :].double()
+    G = torch.tensor(_WINO_G, dtype=torch.float64, device=w.device)
+    U = torch.einsum("xa,ncab,yb->xycn", G, g, G).reshape(16, C, N).float()        # [xi][c][n]
+    return U.view(16, C // 16, 2, 8, N // 32, 32).permute(4, 1, 0, 2, 5, 3).contiguous()
+
+
 class _DarknetFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, plan, nchw, roi=None):
@@ -1209,9 +1244,10 @@ class Darknet(nn.Module):
         self.clone_heads = False
         # receptive-field windows on the training path (ADVPATCH_WINDOWS=0: full maps)
         self.window_heads = os.environ.get("ADVPATCH_WINDOWS", "1") != "0"
-        # conv operand precision: "fp16x3" (split fp16 MFMA, fp32-accurate; default)
-        # or "fp32" (exact fp32 MFMA)
-        self.conv_prec = os.environ.get("ADVPATCH_CONV_PREC", "fp16x3")
+        # conv operand precision: "fp32" (exact fp32 MFMA, the reference's
+        # arithmetic; default) or "fp16x3" (operands split into two fp16
+        # pieces, ~22 significant bits, three fp16 MFMA products; opt-in)
+        self.conv_prec = os.environ.get("ADVPATCH_CONV_PREC", "fp32")
         if self.conv_prec not in ("fp16x3", "fp32"):
             raise ValueError("ADVPATCH_CONV_PREC must be fp16x3 or fp32, got %r" % self.conv_prec)
         self._conv_meta = {}
@@ -1355,6 +1391,14 @@ class Darknet(nn.Module):
         if key not in self._frag:
             f = w16.view(2, N // 32, 32, T, C // 16, 2, 8).permute(0, 1, 3, 4, 5, 2, 6).contiguous()
             self._frag[key] = (w16, f)          # keep w16 alive with its key
+        return nat.c_void_p(self._frag[key][1].data_ptr())
+
+    def _wino(self, w, offs):
+        """Device address of the Winograd weights of launch weights w with tap
+        offsets offs (wino_transform), built once per (weights, tap order)."""
+        key = (w.data_ptr(), tuple(offs))
+        if key not in self._frag:
+            self._frag[key] = (w, wino_transform(w, offs))      # keep w alive with its key
         return nat.c_void_p(self._frag[key][1].data_ptr())
 
     def _dev16(self, i):

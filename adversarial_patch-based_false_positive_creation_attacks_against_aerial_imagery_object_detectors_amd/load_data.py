@@ -15,8 +15,10 @@ DotaDataset            load_data.py:859-978 (host data loader)     (PIL / numpy,
 
 Randomness: the reference draws contrast/brightness/noise/angle from the CUDA
 RNG and target_x/target_y from the CPU RNG (load_data.py:548-707).  Here all
-draws are made on the device (``synthetic.draws_torch``) unless passed in
-explicitly with ``draws=`` (parity tests), so a step has no host<->device sync.
+draws are made on the device by the counter-based ``po_draws`` (keyed by seed,
+step counter and GLOBAL image index, so a data-parallel rank draws exactly the
+rows of its shard) unless passed in explicitly with ``draws=`` (parity tests);
+a step has no host<->device sync.
 """
 import fnmatch
 import math
@@ -140,7 +142,9 @@ class HasSusRGB(nn.Module):
 # Patch placement and warp
 # ---------------------------------------------------------------------------
 def patch_params(lab_batch, img_size, P, draws, do_rotate=True, with_roi=False):
-    """(theta [B,6], patch_center [B,2], target_size [B][, roi [B,4] int32]) on the device."""
+    """(theta [B,6], patch_center [B,2], target_size [B][, roi [B,4] int32,
+    affine [B,6] float64]) on the device.  ``affine`` is the pixel-space
+    sampling map the warp kernels use (po_patch_params)."""
     nat.ensure_device(lab_batch)
     lab = lab_batch.contiguous().float()
     B, L = lab.size(0), lab.size(1)
@@ -149,12 +153,14 @@ def patch_params(lab_batch, img_size, P, draws, do_rotate=True, with_roi=False):
     center = torch.empty(B, 2, device=dev)
     tsize = torch.empty(B, device=dev)
     roi = torch.empty(B, 4, dtype=torch.int32, device=dev) if with_roi else None
+    affine = torch.empty(B, 6, dtype=torch.float64, device=dev) if with_roi else None
     angle = draws["angle"].contiguous().float() if do_rotate else None
     nat.call("po_patch_params", nat.ptr(lab), B, L, nat.ptr(angle), nat.ptr(draws["ux"].contiguous().float()),
              nat.ptr(draws["uy"].contiguous().float()), int(bool(do_rotate)), int(img_size), int(P),
-             nat.ptr(theta), nat.ptr(center), nat.ptr(tsize), nat.ptr(roi, torch.int32), nat.stream())
+             nat.ptr(theta), nat.ptr(center), nat.ptr(tsize), nat.ptr(roi, torch.int32),
+             nat.ptr(affine, torch.float64), nat.stream())
     if with_roi:
-        return theta, center, tsize, roi
+        return theta, center, tsize, roi, affine
     return theta, center, tsize
 
 
@@ -162,26 +168,26 @@ class _Warp(torch.autograd.Function):
     """Augment + warp + clamp*mask (mode 0) or + composite onto img (mode 1)."""
 
     @staticmethod
-    def forward(ctx, mp, noise, contrast, bright, theta, img, S, mode):
+    def forward(ctx, mp, noise, contrast, bright, affine, img, S, mode):
         mp = mp.contiguous()
-        B = theta.size(0)
+        B = affine.size(0)
         P = mp.size(-1)
         out = torch.empty(B, 3, S, S, device=mp.device)
         nat.call("po_warp_fwd", nat.ptr(img.contiguous() if img is not None else None), nat.ptr(mp),
-                 nat.ptr(noise), nat.ptr(contrast), nat.ptr(bright), nat.ptr(theta), B, S, P, mode,
+                 nat.ptr(noise), nat.ptr(contrast), nat.ptr(bright), nat.ptr(affine, torch.float64), B, S, P, mode,
                  nat.ptr(out), nat.stream())
-        ctx.save_for_backward(mp, noise, contrast, bright, theta)
+        ctx.save_for_backward(mp, noise, contrast, bright, affine)
         ctx.S, ctx.mode = S, mode
         return out
 
     @staticmethod
     def backward(ctx, d_out):
-        mp, noise, contrast, bright, theta = ctx.saved_tensors
+        mp, noise, contrast, bright, affine = ctx.saved_tensors
         d_out = d_out.contiguous()
         work = torch.empty_like(d_out)
         d_mp = torch.empty_like(mp)
         nat.call("po_warp_bwd", nat.ptr(d_out), nat.ptr(mp), nat.ptr(noise), nat.ptr(contrast),
-                 nat.ptr(bright), nat.ptr(theta), theta.size(0), ctx.S, mp.size(-1), ctx.mode,
+                 nat.ptr(bright), nat.ptr(affine, torch.float64), affine.size(0), ctx.S, mp.size(-1), ctx.mode,
                  nat.ptr(work), nat.ptr(d_mp), nat.stream())
         return d_mp, None, None, None, None, None, None, None
 
@@ -203,7 +209,11 @@ class PatchTransformer(nn.Module):
         self.minangle = -180 / 180 * math.pi
         self.maxangle = 180 / 180 * math.pi
         self.medianpooler = MedianPool2d(7, same=True)
-        self.generator = None
+        # on-device counter-based draws (po_draws): key, step counter, and the
+        # global index of this process's first image (data-parallel shards)
+        self.draw_seed = 3
+        self.draw_step = 0
+        self.draw_b0 = 0
         self.last_roi = None     # [B,4] int32 footprint boxes of the last placement
 
     def lab_transform(self, lab_batch_origin):
@@ -219,7 +229,11 @@ class PatchTransformer(nn.Module):
         return sel.unsqueeze(1)
 
     def make_draws(self, B, P, device):
-        return synthetic.draws_torch(B, P, device, self.generator)
+        """This step's draws for images draw_b0 .. draw_b0+B-1 of the global
+        batch; advances the step counter."""
+        d = synthetic.draws_device(self.draw_seed, self.draw_step, self.draw_b0, B, P, device)
+        self.draw_step += 1
+        return d
 
     def _prep(self, adv_patch, lab_batch, img_size, do_rotate, draws):
         nat.ensure_device(adv_patch)
@@ -227,24 +241,24 @@ class PatchTransformer(nn.Module):
         B, P = lab_batch.size(0), mp.size(-1)
         if draws is None:
             draws = self.make_draws(B, P, adv_patch.device)
-        theta, center, _, roi = patch_params(lab_batch, img_size, P, draws, do_rotate, with_roi=True)
+        theta, center, _, roi, affine = patch_params(lab_batch, img_size, P, draws, do_rotate, with_roi=True)
         self.last_roi = roi
-        return mp, draws, theta, center
+        return mp, draws, affine, center
 
     def forward(self, adv_patch, lab_batch, img_size, do_rotate=True, rand_loc=False, draws=None):
         """-> (adv_batch_t [B,1,3,S,S], patch_center [B,2] = (x*S, y*S))."""
-        mp, d, theta, center = self._prep(adv_patch, lab_batch, img_size, do_rotate, draws)
+        mp, d, affine, center = self._prep(adv_patch, lab_batch, img_size, do_rotate, draws)
         out = _Warp.apply(mp, d["noise"].contiguous(), d["contrast"].contiguous(),
-                          d["bright"].contiguous(), theta, None, int(img_size), 0)
+                          d["bright"].contiguous(), affine, None, int(img_size), 0)
         return out.unsqueeze(1), center
 
     def forward_composite(self, adv_patch, lab_batch, img_batch, img_size, do_rotate=True, draws=None):
         """Fused PatchTransformer + PatchApplier (the training step's path):
         -> (p_img_batch [B,3,S,S], patch_center [B,2]) without materialising
         adv_batch_t."""
-        mp, d, theta, center = self._prep(adv_patch, lab_batch, img_size, do_rotate, draws)
+        mp, d, affine, center = self._prep(adv_patch, lab_batch, img_size, do_rotate, draws)
         out = _Warp.apply(mp, d["noise"].contiguous(), d["contrast"].contiguous(),
-                          d["bright"].contiguous(), theta, img_batch.contiguous(), int(img_size), 1)
+                          d["bright"].contiguous(), affine, img_batch.contiguous(), int(img_size), 1)
         return out, center
 
 

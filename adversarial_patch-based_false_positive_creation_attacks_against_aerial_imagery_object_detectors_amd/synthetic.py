@@ -11,8 +11,8 @@ benches and parity tests run on synthetic data of the DOTA loader's shapes:
 * draws   the PatchTransformer random draws (load_data.py:548-707)      seed 3
 
 All generators use numpy's PCG64 so the oracle and the HIP path see the
-same bytes.  ``draws_torch`` is the on-device generator the training loop
-uses (torch's Philox, seeded per step).
+same bytes.  ``draws_device`` is the on-device generator the training loop
+uses (po_draws: counter-based Philox keyed by the global image index).
 """
 import math
 
@@ -65,17 +65,46 @@ def draws(B, P, seed=3):
     }
 
 
-def draws_torch(B, P, device, generator=None):
-    """On-device draws with the reference's distributions (load_data.py:548-707)."""
-    kw = {"device": device, "generator": generator, "dtype": torch.float32}
-    return {
-        "contrast": torch.empty(B, device=device).uniform_(0.8, 1.2, generator=generator),
-        "bright": torch.empty(B, device=device).uniform_(-0.1, 0.1, generator=generator),
-        "noise": torch.empty(B, 3, P, P, device=device).uniform_(-1.0, 1.0, generator=generator),
-        "angle": torch.empty(B, device=device).uniform_(-math.pi, math.pi, generator=generator),
-        "ux": torch.rand(B, **kw),
-        "uy": torch.rand(B, **kw),
-    }
+def draws_device(seed, counter, b0, B, P, device):
+    """On-device counter-based draws (po_draws, csrc/draw_ops.hip) for images
+    b0 .. b0+B-1 of a global batch at step ``counter``: the rows do not depend
+    on how the global batch is split over ranks."""
+    from . import _native as nat
+    dev = torch.device(device)
+    f = lambda *shape: torch.empty(*shape, device=dev)
+    d = {"contrast": f(B), "bright": f(B), "noise": f(B, 3, P, P), "angle": f(B), "ux": f(B), "uy": f(B)}
+    nat.call("po_draws", int(seed) & 0xFFFFFFFFFFFFFFFF, int(counter) & 0xFFFFFFFFFFFFFFFF, int(b0), int(B), int(P),
+             *(nat.ptr(d[k]) for k in ("contrast", "bright", "noise", "angle", "ux", "uy")), nat.stream())
+    return d
+
+
+def frames_slice(b0, B, S, seed=0):
+    """Images b0 .. b0+B-1 of a seeded global batch of frames, one PCG64
+    stream per image (a rank generates only its shard)."""
+    out = np.empty((B, 3, S, S), dtype=np.float32)
+    for i in range(B):
+        g = np.random.Generator(np.random.PCG64([seed, b0 + i]))
+        out[i] = g.integers(0, 256, size=(3, S, S), dtype=np.uint8).astype(np.float32) / np.float32(255.0)
+    return torch.from_numpy(out)
+
+
+def labels_slice(b0, B, L=MAX_LAB, seed=1, n_classes=15):
+    """Label rows of images b0 .. b0+B-1 of a seeded global batch (one stream
+    per image; the empty-label rule keys on the global index)."""
+    out = np.full((B, L, 5), 1e-6, dtype=np.float32)
+    for i in range(B):
+        gi = b0 + i
+        if gi % 8 == 7:
+            out[i, 0, :] = 1.0
+            continue
+        g = np.random.Generator(np.random.PCG64([seed, gi]))
+        n = int(min(max(g.poisson(9.0), 1), 50))
+        out[i, :n, 0] = g.integers(0, n_classes, size=n)
+        out[i, :n, 1] = g.uniform(0.05, 0.95, size=n)
+        out[i, :n, 2] = g.uniform(0.05, 0.95, size=n)
+        out[i, :n, 3] = g.uniform(0.01, 0.20, size=n)
+        out[i, :n, 4] = g.uniform(0.01, 0.20, size=n)
+    return torch.from_numpy(out)
 
 
 def shard(t, rank, world):

@@ -16,11 +16,15 @@ with every op of one iteration on the MI355X HIP path:
     -> Adam(amsgrad) + clamp_(0,1) in PyTorch-ROCm.
 
 No host synchronisation happens inside a step (the reference does 2*3*B
-``int()`` syncs in ``obj_cls_conf_find`` plus 5 ``.cpu()`` per iteration).
-Multi-GPU: one process per GPU (torchrun); each rank runs its shard of the
-global batch and the patch gradient (with the loss scalars) is averaged with a
-single all-reduce — replacing the reference's ``nn.DataParallel``
-(train_patch.py:63-71).
+``int()`` syncs in ``obj_cls_conf_find`` plus 5 ``.cpu()`` per iteration);
+error flags (cell out of range, window misplaced, non-finite gradient) are
+OR-ed into a device word and checked once per epoch (``check_flags``).
+Multi-GPU: one process per GPU (torchrun); each rank runs a contiguous shard
+of every global batch (``GlobalBatchSampler``; draws keyed by the global image
+index), weights its loss terms by its share (``shard_weights``) and ONE
+all-reduce(SUM) of [patch grad | loss scalars] yields exactly the global-batch
+gradient, whatever the number of ranks — replacing the reference's
+``nn.DataParallel`` (train_patch.py:63-71), which scatters one global batch.
 """
 import fnmatch
 import os
@@ -69,7 +73,7 @@ class _CellLoss(torch.autograd.Function):
     """(no_obj, no_cls) at the patch cells of the NHWC head buffers (po_cell_loss)."""
 
     @staticmethod
-    def forward(ctx, center, S, target, objective, hw, Cp, views, *heads):
+    def forward(ctx, center, S, target, objective, hw, Cp, views, flags, *heads):
         B = center.size(0)
         dev = center.device
         A = 3 * len(heads)
@@ -77,7 +81,8 @@ class _CellLoss(torch.autograd.Function):
         obj = torch.empty(B, A, device=dev)
         cls = torch.empty(B, A, 15, device=dev)
         cells = torch.empty(len(heads), B, dtype=torch.int32, device=dev)
-        flags = torch.zeros(1, dtype=torch.int32, device=dev)
+        if flags is None:
+            flags = torch.zeros(1, dtype=torch.int32, device=dev)
         hwa, wina, orga = _head_args(hw, views)
         nat.call("po_cell_loss", nat.ptr_array(heads), hwa, wina, orga, len(heads), Cp, B, S,
                  nat.ptr(center.contiguous()), target, objective, None, None, nat.ptr(out2), nat.ptr(obj),
@@ -97,45 +102,130 @@ class _CellLoss(torch.autograd.Function):
         nat.call("po_cell_loss", nat.ptr_array(heads), hwa, wina, orga, len(heads), Cp, center.size(0), S,
                  nat.ptr(center.contiguous()), target, objective, nat.ptr(g2.contiguous().float()),
                  nat.ptr_array(d_heads), nat.ptr(out2), None, None, None, None, nat.stream())
-        return (None, None, None, None, None, None, None) + tuple(d_heads)
+        return (None, None, None, None, None, None, None, None) + tuple(d_heads)
 
 
-def cell_loss(heads, plan, img_size, patch_center, target=TARGET_ID, objective="ce"):
+def cell_loss(heads, plan, img_size, patch_center, target=TARGET_ID, objective="ce", flags=None):
     """-> (out2 [2] = {no_obj_loss, no_cls_loss}, obj [B,9], cls [B,9,15], cells, flags).
     ``heads`` are the plan's head buffers (full maps, or receptive-field
-    windows when the plan was run with the patch centres)."""
+    windows when the plan was run with the patch centres); ``flags``: an
+    int32 [1] device accumulator the kernel ORs its error bits into (a fresh
+    zero word when None)."""
     hw = [plan.shp[h][0] for h in plan.heads]
     Cp = plan.cp[plan.heads[0]]
     for h in plan.heads:
         assert plan.cp[h] == Cp and plan.shp[h][0] == plan.shp[h][1]
     return _CellLoss.apply(patch_center, int(img_size), int(target), OBJECTIVES[objective], hw, Cp,
-                           plan.head_views(), *heads)
+                           plan.head_views(), flags, *heads)
 
 
 LOSS_KEYS = ("loss", "nps_loss", "tv_loss", "no_obj_loss", "no_cls_loss", "colorful_loss")
 
+# error bits of the trainer's device flag word (check_flags)
+FLAG_BITS = {1: "patch-centre cell outside its head map (clamped)",
+             2: "loss cell outside its receptive-field window (planning error)",
+             4: "receptive-field window too small for the needed box (planning error)",
+             8: "non-finite patch gradient (NaN/Inf; the reference ran under detect_anomaly)"}
+FLAG_NONFINITE = 8
+
+
+def shard_weights(n_local, n_global, world, objective="ce"):
+    """(w_img, w_cls, w_patch): multipliers that make the per-rank losses add
+    up to the global-batch loss under an all-reduce SUM.
+
+    * image terms that are batch MEANS (objectness, CE) count with this
+      rank's share of the global batch, n_local / n_global;
+    * the targeted class term is a batch SUM (noCLS_loss_targeted,
+      train_patch.py:575) and counts with weight 1;
+    * the patch terms (NPS, TV, colour) are identical on every rank and
+      count 1/world each.
+    Unequal (ragged last) shards come out right too."""
+    w_img = float(n_local) / float(n_global)
+    w_cls = 1.0 if objective == "targeted" else w_img
+    return w_img, w_cls, 1.0 / float(world)
+
+
+def combine_terms(no_obj_loss, no_cls_loss, nps, tv, colorful, objective="ce", weights=None, tv_floor=None):
+    """The reference's loss (train_patch.py:230-314):
+
+        loss = 0.01*NPS + max(2.5*TV, 0.1) + 4*(1 - mean max obj) + COLOUR [+ CLS]
+
+    ``weights`` = shard_weights(...) for a data-parallel rank (None: one
+    process, no scaling).  Returns (loss, terms dict) with every term already
+    weighted, so the SUM over ranks of each is its global value."""
+    nps_loss = nps * NPS_FACTOR
+    tv_loss = tv * TV_FACTOR
+    if tv_floor is None:
+        tv_floor = torch.tensor(0.1, device=tv.device, dtype=tv.dtype)
+    tv_term = torch.max(tv_loss, tv_floor)
+    if weights is not None:
+        w_img, w_cls, w_patch = weights
+        no_obj_loss, no_cls_loss = no_obj_loss * w_img, no_cls_loss * w_cls
+        nps_loss, tv_loss, tv_term, colorful = nps_loss * w_patch, tv_loss * w_patch, tv_term * w_patch, colorful * w_patch
+    loss = nps_loss + tv_term + no_obj_loss + colorful
+    if objective != "untargeted":
+        loss = loss + no_cls_loss
+    return loss, {"loss": loss, "nps_loss": nps_loss, "tv_loss": tv_loss, "no_obj_loss": no_obj_loss,
+                  "no_cls_loss": no_cls_loss, "colorful_loss": colorful}
+
 
 def allreduce_patch_grad(grad, terms, group=None):
     """Data-parallel reduction of one step: every rank holds
-    the gradient of its local-mean loss; ONE all-reduce of the fused buffer
-    [patch grad | 6 loss scalars] averages them, which equals the
-    global-batch gradient for equal shards (the NPS/TV/colour terms are
-    identical on every rank).  RCCL (backend "nccl") reduces with AVG; gloo
-    with SUM then a division.  ``grad`` is updated in place, ``terms``' loss
-    scalars are replaced by their averages."""
+    the gradient of its WEIGHTED loss (combine_terms with shard_weights), so
+    ONE all-reduce(SUM) of the fused buffer [patch grad | 6 loss scalars]
+    gives the global-batch gradient and loss terms on every rank (RCCL over
+    xGMI with backend "nccl"; gloo on CPU).  ``grad`` is updated in place,
+    ``terms``' loss scalars are replaced by their global values."""
     import torch.distributed as dist
-    world = dist.get_world_size(group)
     flat = torch.cat([grad.reshape(-1)] + [terms[k].detach().reshape(1).to(grad.dtype) for k in LOSS_KEYS])
-    if dist.get_backend(group) == "nccl":
-        dist.all_reduce(flat, op=dist.ReduceOp.AVG, group=group)
-    else:
-        dist.all_reduce(flat, op=dist.ReduceOp.SUM, group=group)
-        flat.div_(world)
+    dist.all_reduce(flat, op=dist.ReduceOp.SUM, group=group)
     n = grad.numel()
     grad.copy_(flat[:n].view_as(grad))
     for i, k in enumerate(LOSS_KEYS):
         terms[k] = flat[n + i]
     return grad
+
+
+class GlobalBatchSampler(torch.utils.data.Sampler):
+    """Distributed batch sampler with the reference's DataParallel semantics
+    (train_patch.py:63-71, 123-127: ONE shuffled loader of ``global_batch``
+    images per step, scattered over the GPUs).
+
+    Every rank draws the same permutation (seed + epoch, ``set_epoch``) and
+    yields its CONTIGUOUS slice [lo, hi) of each global batch, so the images of
+    global step k are the same for any number of ranks and so are their
+    transformer draws (keyed by the global index lo + i).  A ragged last batch
+    is split as evenly as possible (the loss weights account for it); a
+    final batch with fewer images than ranks is dropped when world > 1."""
+
+    def __init__(self, n_items, global_batch, rank=0, world=1, shuffle=True, seed=0):
+        self.n, self.G, self.rank, self.world = int(n_items), int(global_batch), int(rank), int(world)
+        self.shuffle, self.seed, self.epoch = shuffle, int(seed), 0
+
+    def set_epoch(self, epoch):
+        self.epoch = int(epoch)
+
+    def __len__(self):
+        nb = -(-self.n // self.G)
+        if self.world > 1 and nb and self.n - (nb - 1) * self.G < self.world:
+            nb -= 1
+        return nb
+
+    def shard_of(self, k):
+        """(lo, hi, n_global) of this rank's slice of global batch k."""
+        ng = min(self.G, self.n - k * self.G)
+        return self.rank * ng // self.world, (self.rank + 1) * ng // self.world, ng
+
+    def __iter__(self):
+        if self.shuffle:
+            g = torch.Generator()
+            g.manual_seed(self.seed + self.epoch)
+            perm = torch.randperm(self.n, generator=g).tolist()
+        else:
+            perm = list(range(self.n))
+        for k in range(len(self)):
+            lo, hi, _ = self.shard_of(k)
+            yield perm[k * self.G + lo:k * self.G + hi]
 
 
 class PatchTrainer(object):
@@ -163,7 +253,13 @@ class PatchTrainer(object):
         self.colorful_loss = HasSusRGB().to(self.device)
         self.dist = distributed if distributed is not None else (
             torch.distributed.is_available() and torch.distributed.is_initialized())
+        self.rank = torch.distributed.get_rank() if self.dist else 0
+        self.world = torch.distributed.get_world_size() if self.dist else 1
         self._tv_floor = None
+        # device word of error bits (FLAG_BITS), OR-ed by the kernels, read by check_flags()
+        self.flags = torch.zeros(1, dtype=torch.int32, device=self.device)
+        # NaN/Inf guard on the patch gradient (replaces detect_anomaly, train_patch.py:158)
+        self.check_finite = os.environ.get("ADVPATCH_CHECK_FINITE", "1") != "0"
 
     # ------------------------------------------------------------------
     def generate_patch(self, type):
@@ -182,9 +278,11 @@ class PatchTrainer(object):
         return torch.from_numpy(np.asarray(img, dtype=np.uint8).copy()).permute(2, 0, 1).float().div_(255.0)
 
     # ------------------------------------------------------------------
-    def losses(self, adv_patch, img_batch, lab_batch, draws=None, objective=None):
+    def losses(self, adv_patch, img_batch, lab_batch, draws=None, objective=None, weights=None):
         """Forward of one iteration (train_patch.py:164-314) on the HIP path.
-        Returns (loss, terms dict); ``loss.backward()`` yields adv_patch.grad."""
+        ``weights``: shard_weights(...) of a data-parallel rank (None: the
+        whole batch is here).  Returns (loss, terms dict); ``loss.backward()``
+        yields adv_patch.grad."""
         objective = objective or self.objective
         img_size = self.darknet_model.height
         p_img, center = self.patch_transformer.forward_composite(adv_patch, lab_batch, img_batch, img_size,
@@ -197,36 +295,44 @@ class PatchTrainer(object):
         # the first conv's input gradient is computed there only
         heads, plan = self.darknet_model.forward_nhwc(p_img, input_roi=roi, center=center)
         self.last_plan = plan
-        out2, obj, cls, cells, flags = cell_loss(heads, plan, img_size, center, TARGET_ID, objective)
-        no_obj_loss, no_cls_loss = out2[0], out2[1]
+        out2, obj, cls, cells, flags = cell_loss(heads, plan, img_size, center, TARGET_ID, objective,
+                                                 flags=self.flags)
         reg = regularisers(adv_patch, self.nps_calculator.colors)
-        nps_loss = reg[0] * NPS_FACTOR
-        tv_loss = reg[1] * TV_FACTOR
-        colorful = reg[2]
         if self._tv_floor is None or self._tv_floor.device != adv_patch.device:
             self._tv_floor = torch.tensor(0.1, device=adv_patch.device)
-        loss = nps_loss + torch.max(tv_loss, self._tv_floor) + no_obj_loss + colorful
-        if objective != "untargeted":
-            loss = loss + no_cls_loss
-        terms = {"loss": loss, "nps_loss": nps_loss, "tv_loss": tv_loss, "no_obj_loss": no_obj_loss,
-                 "no_cls_loss": no_cls_loss, "colorful_loss": colorful, "patch_center": center,
-                 "obj": obj, "cls": cls, "cells": cells, "flags": flags}
+        loss, terms = combine_terms(out2[0], out2[1], reg[0], reg[1], reg[2], objective, weights, self._tv_floor)
+        terms.update({"patch_center": center, "obj": obj, "cls": cls, "cells": cells, "flags": flags})
         return loss, terms
 
     def allreduce_grad(self, adv_patch, terms):
-        """One all-reduce(avg) of [patch grad | loss scalars] over all ranks."""
+        """One all-reduce(SUM) of [patch grad | weighted loss scalars] over all ranks."""
         if self.dist:
             allreduce_patch_grad(adv_patch.grad, terms)
 
-    def step(self, adv_patch, optimizer, img_batch, lab_batch, draws=None):
+    def step(self, adv_patch, optimizer, img_batch, lab_batch, draws=None, weights=None):
         """One full iteration: forward, backward, [all-reduce], Adam, clamp (train_patch.py:164-330)."""
-        loss, terms = self.losses(adv_patch, img_batch, lab_batch, draws)
+        loss, terms = self.losses(adv_patch, img_batch, lab_batch, draws, weights=weights)
         loss.backward()
         self.allreduce_grad(adv_patch, terms)
+        if self.check_finite:
+            g = adv_patch.grad
+            nat.call("po_check_finite", nat.ptr(g), g.numel(), FLAG_NONFINITE, nat.ptr(self.flags, torch.int32),
+                     nat.stream())
         optimizer.step()
         optimizer.zero_grad()
         adv_patch.data.clamp_(0, 1)
         return terms
+
+    def check_flags(self):
+        """Raise if any kernel raised an error bit since the trainer was built
+        (one device->host read; call it per epoch, not per step)."""
+        f = int(self.flags.item())
+        plan = self.last_plan
+        if plan is not None and getattr(plan, "windowed", False):
+            f |= int(plan.win_flags.item())
+        if f:
+            raise RuntimeError("advpatch step error flags 0x%x: %s" % (
+                f, "; ".join(v for k, v in FLAG_BITS.items() if f & k)))
 
     def make_optimizer(self, adv_patch):
         """Adam(amsgrad) as the reference (train_patch.py:131-136); on the GPU
@@ -237,42 +343,69 @@ class PatchTrainer(object):
 
     # ------------------------------------------------------------------
     def train(self, max_n_epochs=401, save_dir="training_patches_saves/trained_patches", num_workers=10,
-              data=None):
+              data=None, seed=0):
         """Optimise a patch on the configured dataset (train_patch.py:85-389).
-        ``data``: optional iterable of (img_batch, lab_batch) replacing the DataLoader."""
+        ``config.batch_size`` is the GLOBAL batch, as in the reference; under
+        torchrun every rank loads its contiguous shard of each global batch
+        (GlobalBatchSampler).  ``data``: optional iterable of (img_batch,
+        lab_batch) replacing the DataLoader (under torchrun: this rank's
+        equal shards)."""
         img_size = self.darknet_model.height
         batch_size = self.config.batch_size
         max_lab = 252
+        rank0 = self.rank == 0
+        torch.manual_seed(seed)
         adv_patch = self.generate_patch("random").to(self.device).requires_grad_(True)
+        sampler = None
         if data is None:
             n_images = len(fnmatch.filter(os.listdir(self.config.img_dir), "*.png")) + \
                 len(fnmatch.filter(os.listdir(self.config.img_dir), "*.jpg"))
-            if self.verbose:
+            if self.verbose and rank0:
                 print("Total images in TrainSet : ", n_images)
-            loader = torch.utils.data.DataLoader(
-                DotaDataset(self.config.img_dir, self.config.lab_dir, max_lab, img_size, shuffle=True),
-                batch_size=batch_size, shuffle=True, num_workers=num_workers, pin_memory=True)
+            ds = DotaDataset(self.config.img_dir, self.config.lab_dir, max_lab, img_size, shuffle=True)
+            sampler = GlobalBatchSampler(len(ds), batch_size, self.rank, self.world, shuffle=True, seed=seed)
+            loader = torch.utils.data.DataLoader(ds, batch_sampler=sampler, num_workers=num_workers,
+                                                 pin_memory=True, persistent_workers=num_workers > 0)
         else:
             loader = data
         optimizer = self.make_optimizer(adv_patch)
         scheduler = self.config.scheduler_factory(optimizer)
         ep_loss_list = []
-        keys = ("loss", "nps_loss", "tv_loss", "no_obj_loss", "no_cls_loss", "colorful_loss")
+        keys = LOSS_KEYS
+        step = 0
+        self.patch_transformer.draw_seed = seed + 3
         for epoch in range(max_n_epochs):
+            if sampler is not None:
+                sampler.set_epoch(epoch)
             sums = {k: torch.zeros((), device=self.device) for k in keys}
             nb = 0
             et0 = time.time()
-            for img_batch, lab_batch in loader:
+            for k, (img_batch, lab_batch) in enumerate(loader):
                 img_batch = img_batch.to(self.device, non_blocking=True)
                 lab_batch = lab_batch.to(self.device, non_blocking=True)
-                terms = self.step(adv_patch, optimizer, img_batch, lab_batch)
-                for k in keys:
-                    sums[k] += terms[k].detach()
+                weights = None
+                if sampler is not None:
+                    lo, hi, ng = sampler.shard_of(k)
+                    b0 = lo
+                    if self.dist:
+                        weights = shard_weights(hi - lo, ng, self.world, self.objective)
+                else:
+                    n = img_batch.size(0)
+                    b0 = self.rank * n
+                    if self.dist:
+                        weights = shard_weights(n, n * self.world, self.world, self.objective)
+                # draws of global step `step`, rows of this rank's images
+                self.patch_transformer.draw_step, self.patch_transformer.draw_b0 = step, b0
+                terms = self.step(adv_patch, optimizer, img_batch, lab_batch, weights=weights)
+                for key in keys:
+                    sums[key] += terms[key].detach()
                 nb += 1
-            ep = {k: (v / max(nb, 1)).item() for k, v in sums.items()}
-            scheduler.step(ep["loss"] * max(nb, 1))
+                step += 1
+            self.check_flags()
+            ep = {key: (v / max(nb, 1)).item() for key, v in sums.items()}
+            scheduler.step(ep["loss"] * max(nb, 1))        # the reference steps on the epoch SUM (332)
             ep_loss_list.append(ep["no_obj_loss"] / 4)
-            if self.verbose:
+            if self.verbose and rank0:
                 print("  EPOCH NR: ", epoch)
                 print("EPOCH LOSS: ", ep["loss"])
                 print("  NPS LOSS: ", ep["nps_loss"])
@@ -281,8 +414,14 @@ class PatchTrainer(object):
                 print("  NO_CLS LOSS: ", ep["no_cls_loss"])
                 print("  COLORFUL LOSS: ", ep["colorful_loss"])
                 print("EPOCH TIME: ", time.time() - et0)
-            if epoch % 20 == 0 and save_dir:
-                save_patch_png(adv_patch.detach(), os.path.join(save_dir, "%d_patch.png" % epoch))
+            if epoch % 20 == 0 and save_dir and rank0:
+                path = os.path.join(save_dir, "%d_patch.png" % epoch)
+                save_patch_png(adv_patch.detach(), path)
+                if self.verbose:
+                    print("saved patch dir : ", save_dir)
+                if epoch > 0 and self.verbose:
+                    prev = os.path.join(save_dir, "%d_patch.png" % (epoch - 20))
+                    print("MSE-loss between adjacent patch : ", patch_mse(prev, path))
         return adv_patch.detach(), ep_loss_list
 
     # ------------------------------------------------------------------
@@ -330,6 +469,13 @@ def save_patch_png(patch, path):
     os.makedirs(os.path.dirname(os.path.abspath(path)), exist_ok=True)
     arr = patch.detach().float().cpu().mul(255).byte().permute(1, 2, 0).numpy()
     Image.fromarray(arr, "RGB").save(path)
+
+
+def patch_mse(path0, path1):
+    """MSE between two saved patches read back as ToTensor floats
+    (utils_self.patch_MSE_calsulator, utils_self.py:205-220)."""
+    a, b = _read_image(path0), _read_image(path1)
+    return float(((a - b) ** 2).mean())
 
 
 def main():

@@ -6,10 +6,15 @@ YOLOv3-DOTA forward -> cell loss + NPS/TV/colour -> backward (dgrad) ->
 [all-reduce of the patch gradient over RCCL when N > 1] -> Adam(amsgrad) + clamp.
 Inputs (frames, labels, patch) are resident in HBM before the timed region.
 
-    python bench.py [--gpus N --steps K --warmup W --batch B --config yolov3|tiny]
+    python bench.py [--gpus N --steps K --warmup W --batch B --config yolov3|tiny --prec both|fp32|fp16x3]
 
+``value`` is measured with exact fp32 convolutions (v_mfma_f32_32x32x2_f32,
+the reference's arithmetic); the fp16x3 split-precision path is timed in the
+same run and reported beside it (``value_fp16x3``, ``roofline_fp16x3``).
 N > 1 is launched by torchrun (one process per GPU, RCCL over xGMI); the
-global batch is N*B (weak scaling).
+global batch is N*B (weak scaling), each rank runs its contiguous shard of one
+seeded global batch with draws keyed by global image index, and one
+all-reduce(SUM) of the weighted patch gradient per step.
 """
 import argparse
 import json
@@ -63,13 +68,42 @@ def conv_macs(net):
     return total
 
 
-def cpu_baseline(cfg, S, P, seconds_budget=25.0):
-    """The oracle (PyTorch-CPU restatement, weight grads on as in the
-    reference, no detect_anomaly) on the host cores: 1 warm-up + timed
-    iterations of a 1-image batch for ~10 s (at most seconds_budget)."""
+def _usable_cpus():
+    """CPUs this process may actually use: the cgroup CPU quota (cpu.max) and
+    the affinity mask bound it; os.cpu_count() reports the whole machine."""
+    n = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            quota, period = f.read().split()[:2]
+        if quota != "max":
+            n = min(n, max(1, int(int(quota) // int(period))))
+    except (OSError, ValueError):
+        pass
+    return n
+
+
+def _cpu_model():
+    cpu = platform.processor() or platform.machine()
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return cpu
+
+
+def cpu_baseline(cfg, S, P, B=16, warmup=1, iters=3):
+    """the oracle (PyTorch-CPU fp32 restatement of the
+    reference step, weight gradients ON as in the reference, no
+    detect_anomaly) on the host cores, batch B, 1 warm-up + 3 timed steps.
+    Threads: every CPU the process may use (the cgroup quota; on the GPU
+    box os.cpu_count() shows the whole 256-CPU machine while the job's quota
+    is 16, and oversubscribing a quota only slows torch down)."""
     import oracle
     sy, W, G, ld = ge._pkg("synthetic"), ge._pkg("weights"), ge._pkg("cfg_gen"), ge._pkg("load_data")
-    cores = min(16, os.cpu_count() or 1)
+    cores = _usable_cpus()
     torch.set_num_threads(cores)
     stream = W.synthesize(cfg, seed=4)
     net = oracle.OracleDarknet(G.cfg_text(cfg), None, requires_grad=True)
@@ -80,29 +114,92 @@ def cpu_baseline(cfg, S, P, seconds_budget=25.0):
                 if k in p:
                     p[k].requires_grad_(True)
     colors = ld.load_printability_colors("builtin:30values")
-    B = 1
     img, lab, patch, dr = sy.frames(B, S, seed=100), sy.labels(B, seed=101), sy.patch(P, seed=102), sy.draws(B, P, seed=103)
-    oracle.train_step(patch, img, lab, dr, net, colors)           # warm-up
-    n, t0 = 0, time.time()
-    while True:
+    for _ in range(warmup):
         oracle.train_step(patch, img, lab, dr, net, colors)
-        n += 1
-        el = time.time() - t0
-        if el > seconds_budget or (el > 10.0 and n >= 3):     # ~10 s of CPU work, at least 3 steps
-            break
+    t0 = time.time()
+    for _ in range(iters):
+        oracle.train_step(patch, img, lab, dr, net, colors)
     el = time.time() - t0
-    cpu = platform.processor() or platform.machine()
-    try:
-        with open("/proc/cpuinfo") as f:
-            for line in f:
-                if line.startswith("model name"):
-                    cpu = line.split(":", 1)[1].strip()
-                    break
-    except OSError:
-        pass
-    return {"value": n * B / el, "unit": "images/s", "cores": cores, "kind": "port",
-            "sample": "oracle train_step (PyTorch-CPU fp32, weight grads on), batch 1 @%d, %d timed iters "
-                      "after 1 warm-up, %.1fs, %d threads of %s" % (S, n, el, cores, cpu)}
+    return {"value": iters * B / el, "unit": "images/s", "cores": cores, "kind": "port",
+            "sample": "oracle train_step (PyTorch-CPU fp32, weight grads on, no detect_anomaly), batch %d @%d, "
+                      "%d timed steps after %d warm-up, %.1fs, %d threads (cgroup quota; os.cpu_count()=%d) of %s"
+                      % (B, S, iters, warmup, el, cores, os.cpu_count() or 0, _cpu_model())}
+
+
+def measure(tr, prec, patch, img, lab, B, world, rank, steps, warmup, weights):
+    """Warm-up, K timed steps (barrier + synchronize on both sides, max over
+    ranks), then K instrumented steps with HIP events around every po_conv
+    launch (the roofline pass; kept out of the timed region because each
+    event pair adds a ~10 us dispatch gap, profiles/r01)."""
+    net = tr.darknet_model
+    net.conv_prec = prec
+    opt = tr.make_optimizer(patch)
+    pt = tr.patch_transformer
+    pt.draw_b0 = rank * B                 # draws keyed by global image index (po_draws)
+
+    def step():
+        return tr.step(patch, opt, img, lab, weights=weights)
+
+    for _ in range(warmup):
+        step()
+    torch.cuda.synchronize()
+    if getattr(tr, "last_plan", None) is None or tr.last_plan.prec != (1 if prec == "fp16x3" else 0):
+        tr.losses(patch, img, lab, weights=weights)      # --warmup 0: build the plan outside the timed region
+        torch.cuda.synchronize()
+    plan = tr.last_plan
+    if world > 1:
+        torch.distributed.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        terms = step()
+    torch.cuda.synchronize()
+    if world > 1:
+        torch.distributed.barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], device=img.device)
+        torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
+        elapsed = float(t)
+    plan.conv_timer = []
+    torch.cuda.synchronize()
+    t1 = time.perf_counter()
+    for _ in range(steps):
+        step()
+    torch.cuda.synchronize()
+    instrumented_ms = (time.perf_counter() - t1) * 1000.0 / steps
+    timer, plan.conv_timer = plan.conv_timer, None
+    conv_ms = sum(e0.elapsed_time(e1) for e0, e1, _, _ in timer) / steps
+    # MACs actually computed: a boxed dgrad (gradient cones) counts its boxes only
+    conv_flops = 2.0 * sum(plan.launch_macs(d, c) for _, _, d, c in timer) / steps
+    tr.check_flags()
+    return {"elapsed": elapsed, "ms_per_step": elapsed * 1000.0 / steps, "value": world * B * steps / elapsed,
+            "conv_ms": conv_ms, "conv_flops": conv_flops, "launches": len(timer) // steps,
+            "instrumented_ms": instrumented_ms, "loss": float(terms["loss"].detach()), "plan": plan}
+
+
+def roofline(cfg_name, B, prec, m, ref_flops_step):
+    traffic = None
+    tfile = os.path.join(ROOT, "profiles", "traffic_%s_b%d_%s.json" % (cfg_name, B, prec))
+    if os.path.exists(tfile):
+        with open(tfile) as f:
+            traffic = json.load(f).get("conv_hbm_bytes_per_step")
+    achieved = m["conv_flops"] / (m["conv_ms"] * 1e-3) / 1e12
+    peak = PEAK_CONV[prec]
+    return {"bound": "mfma",
+            "kernel": "po_conv implicit GEMM (%s): every Darknet fwd + dgrad launch of a step" % (
+                "conv_h3*_k, fp16x3 split operands" if prec == "fp16x3" else "conv_k, exact fp32 v_mfma_f32_32x32x2_f32"),
+            "achieved": achieved, "peak": peak, "unit": "TFLOP/s", "frac": achieved / peak, "traffic": traffic,
+            "traffic_per": "step: HBM bytes of all conv launches + split-K reduces (rocprofv3 FETCH_SIZE/WRITE_SIZE "
+                           "passes, profiles/traffic_*.json)",
+            "peak_note": "fp32-equivalent: fp16 dense 2500 / 3 products" if prec == "fp16x3" else "fp32 dense MFMA",
+            "flops_per_step": m["conv_flops"], "conv_ms_per_step": m["conv_ms"],
+            "conv_launches_per_step": m["launches"],
+            "measured_on": "a second pass of K steps with per-launch HIP events (%.3f ms/step instrumented vs %.3f "
+                           "plain)" % (m["instrumented_ms"], m["ms_per_step"]),
+            "reference_dense_flops_per_step": ref_flops_step,
+            "receptive_field_windows": bool(m["plan"].windowed)}
 
 
 def main():
@@ -112,8 +209,11 @@ def main():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--batch", type=int, default=None, help="per-GPU batch")
     ap.add_argument("--config", default="yolov3", choices=sorted(CONFIGS))
+    ap.add_argument("--prec", default="both", choices=("both", "fp32", "fp16x3"),
+                    help="conv operand precision(s) timed: value is exact fp32; fp16x3 is reported beside it")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--dist-backend", default="nccl", help="nccl (= RCCL); gloo only to rehearse ranks on one GPU")
+    ap.add_argument("--tile-cache", default=None, help="conv tile cache (default: the committed tiles/ file)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -129,7 +229,11 @@ def main():
     dev = torch.device("cuda", local % ndev)
     cfg, S, P, Bdef = CONFIGS[args.config]
     B = args.batch or Bdef
-    os.environ.setdefault("ADVPATCH_TUNE_CACHE", os.path.join(ROOT, "weights", "conv_tiles_%s_b%d.json" % (args.config, B)))
+    # conv tile choices: the committed per-(config, batch) cache keeps runs
+    # reproducible (same tiles -> same summation order); shapes it lacks are
+    # autotuned on first use
+    os.environ["ADVPATCH_TUNE_CACHE"] = args.tile_cache or os.path.join(
+        ge.PKG_DIR, "tiles", "conv_tiles_%s_b%d.json" % (args.config, B))
 
     tp, pc, sy, W = ge._pkg("train_patch"), ge._pkg("patch_config"), ge._pkg("synthetic"), ge._pkg("weights")
     wpath = pc.synthetic_weights_path(cfg.split(":")[-1])
@@ -143,99 +247,47 @@ def main():
             super().__init__()
             self.cfgfile = cfg
             self.weightfile = wpath
-            self.batch_size = B
+            self.batch_size = B * world
 
     pc.patch_configs["_bench"] = _Cfg
     tr = tp.PatchTrainer("_bench", device=dev, verbose=False, distributed=world > 1)
 
-    img = sy.frames(B, S, seed=1000 + rank).to(dev)
-    lab = sy.labels(B, seed=2000 + rank).to(dev)
+    # this rank's contiguous shard of one seeded global batch
+    img = sy.frames_slice(rank * B, B, S, seed=1000).to(dev)
+    lab = sy.labels_slice(rank * B, B, seed=2000).to(dev)
     patch = sy.patch(P, seed=2).to(dev).requires_grad_(True)
-    opt = tr.make_optimizer(patch)
-    gen = torch.Generator(device=dev)
-    gen.manual_seed(3 + rank)
-    tr.patch_transformer.generator = gen
+    weights = tp.shard_weights(B, B * world, world, tr.objective) if world > 1 else None
+    ref_flops_step = 4.0 * conv_macs(tr.darknet_model) * B      # reference algorithm: dense fwd + dgrad (§8d)
 
-    net = tr.darknet_model
-    ref_flops_per_img = 4.0 * conv_macs(net)      # reference algorithm: dense fwd + dgrad
-
-    for _ in range(args.warmup):
-        tr.step(patch, opt, img, lab)
-    torch.cuda.synchronize()
-    if getattr(tr, "last_plan", None) is None:       # --warmup 0: build the plan outside the timed region
-        tr.losses(patch, img, lab)
-        torch.cuda.synchronize()
-    plan = tr.last_plan
-    # timed region: K plain steps (no per-launch instrumentation)
-    if world > 1:
-        torch.distributed.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        terms = tr.step(patch, opt, img, lab)
-    torch.cuda.synchronize()
-    if world > 1:
-        torch.distributed.barrier()
-    elapsed = time.perf_counter() - t0
-    if world > 1:
-        t = torch.tensor([elapsed], device=dev)
-        torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
-        elapsed = float(t)
-    # roofline pass: the same K steps again with HIP events around every
-    # po_conv launch (the kernels run on torch's current stream, where the
-    # events are recorded).  Kept out of the timed region: each event pair
-    # adds a ~10 us dispatch gap in front of its launch (profiles/r01).
-    plan.conv_timer = []
-    torch.cuda.synchronize()
-    t1 = time.perf_counter()
-    for _ in range(args.steps):
-        tr.step(patch, opt, img, lab)
-    torch.cuda.synchronize()
-    instrumented_ms = (time.perf_counter() - t1) * 1000.0 / args.steps
-    timer, plan.conv_timer = plan.conv_timer, None
-    conv_ms = sum(e0.elapsed_time(e1) for e0, e1, _, _ in timer) / args.steps
-    # MACs actually computed: a boxed dgrad (gradient cones) counts its boxes only
-    conv_flops = 2.0 * sum(plan.launch_macs(d, c) for _, _, d, c in timer) / args.steps
-    ms_per_step = elapsed * 1000.0 / args.steps
-    value = world * B * args.steps / elapsed
-    achieved = conv_flops / (conv_ms * 1e-3) / 1e12
+    precs = ["fp32", "fp16x3"] if args.prec == "both" else [args.prec]
+    res = {p: measure(tr, p, patch, img, lab, B, world, rank, args.steps, args.warmup, weights) for p in precs}
 
     if rank == 0:
-        traffic = None
-        prec = net.conv_prec
-        tfile = os.path.join(ROOT, "profiles", "traffic_%s_b%d_%s.json" % (args.config, B, prec))
-        if os.path.exists(tfile):
-            with open(tfile) as f:
-                traffic = json.load(f).get("conv_hbm_bytes_per_step")
-        peak = PEAK_CONV[prec]
+        head = precs[0]
+        m = res[head]
         line = {
             "metric": "patch-opt images/sec (608x608, YOLOv3-DOTA) at 1/2/4/8 MI355X" if args.config == "yolov3"
             else "patch-opt images/sec (416x416, YOLOv3-tiny-15)",
-            "value": value, "unit": "images/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
-            "ms_per_step": ms_per_step, "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
-            "dtype": "fp32" if prec == "fp32" else "fp32 (fp16x3 split MFMA, fp32 accumulate)", "data": "synthetic (seeded DOTA-shaped frames/labels, synthetic calibrated weights)",
+            "value": m["value"], "unit": "images/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+            "ms_per_step": m["ms_per_step"], "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+            "dtype": "fp32" if head == "fp32" else "fp32 (fp16x3 split MFMA, fp32 accumulate)",
+            "data": "synthetic (seeded DOTA-shaped frames/labels, synthetic calibrated weights)",
             "config": {"workload": "%s S=%d P=%d batch=%d per GPU, global %d" % (cfg, S, P, B, B * world),
                        "global_batch": B * world, "per_gpu_batch": B, "image_size": S, "patch_size": P,
-                       "parallelism": "dp%d" % world},
-            "roofline": {"bound": "mfma", "kernel": "po_conv implicit GEMM (%s): every Darknet fwd + dgrad launch "
-                                                    "of a step" % ("conv_h3_k/conv_h3d_k, fp16x3" if prec == "fp16x3"
-                                                                   else "conv_k, fp32"),
-                         "achieved": achieved, "peak": peak, "unit": "TFLOP/s",
-                         "frac": achieved / peak, "traffic": traffic,
-                         "traffic_per": "step: HBM bytes of all conv launches + split-K reduces (rocprofv3 FETCH_SIZE/WRITE_SIZE passes, profiles/traffic_*.json)",
-                         "peak_note": "fp32-equivalent: fp16 dense 2500 / 3 products" if prec == "fp16x3"
-                                      else "fp32 dense MFMA",
-                         "frac_of_fp32_mfma_peak": achieved / PEAK_FP32_MFMA_TFLOPS,
-                         "flops_per_step": conv_flops, "conv_ms_per_step": conv_ms,
-                         "conv_launches_per_step": len(timer) // args.steps,
-                         "measured_on": "a second pass of K steps with per-launch HIP events "
-                                        "(%.3f ms/step instrumented vs %.3f plain)" % (instrumented_ms, elapsed * 1000.0 / args.steps),
-                         "reference_dense_flops_per_step": ref_flops_per_img * B,
-                         "receptive_field_windows": bool(plan.windowed)},
-            "loss": float(terms["loss"].detach()),
+                       "parallelism": "dp%d" % world, "conv_precision": head},
+            "roofline": roofline(args.config, B, head, m, ref_flops_step),
+            "loss": m["loss"],
         }
+        if "fp16x3" in res and head != "fp16x3":
+            f = res["fp16x3"]
+            line["value_fp16x3"] = f["value"]
+            line["ms_per_step_fp16x3"] = f["ms_per_step"]
+            line["dtype_fp16x3"] = ("fp32 operands held as two fp16 pieces (~22 significant bits) under a "
+                                    "power-of-two scale, three fp16 MFMA products, fp32 accumulate")
+            line["roofline_fp16x3"] = roofline(args.config, B, "fp16x3", f, ref_flops_step)
+            line["loss_fp16x3"] = f["loss"]
         if world == 1 and not args.no_cpu_baseline:
-            line["cpu_baseline"] = cpu_baseline(cfg, S, P)
+            line["cpu_baseline"] = cpu_baseline(cfg, S, P, B=16)
         print(json.dumps(line))
     if world > 1:
         torch.distributed.destroy_process_group()

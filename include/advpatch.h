@@ -33,7 +33,7 @@ typedef void* po_stream_t;
 #define PO_EHIP -2     /* HIP runtime error */
 #define PO_EDEVICE -3  /* device is not gfx950 */
 
-#define PO_ABI_VERSION 8
+#define PO_ABI_VERSION 9
 #define PO_AMAX_SUB 64  /* sub-slots per max|x| slot (see po_conv_desc) */
 
 int po_abi_version(void);
@@ -54,12 +54,31 @@ int po_median7_bwd(const float* dy, const int32_t* argidx, int C, int H, int W, 
 /* Per-image patch placement (load_data.py:453-509 lab_transform,
  * 654-743 target_size/scale/theta, 693-715 target_x/y and patch_center).
  * lab [B,L,5]; angle,ux,uy [B]; theta out [B,6]; center out [B,2]
- * (column,row) pixels; target_size out [B] (may be NULL); roi out [B,4] int32
+ * (column,row) pixels, fp32 exactly as the reference (the loss cell index is
+ * derived from it); target_size out [B] (may be NULL); roi out [B,4] int32
  * (may be NULL) = {x0,y0,x1,y1} bounding box (+2 px margin, clipped to the
- * image) of the output pixels the warped patch can touch. */
+ * image) of the output pixels the warped patch can touch; affine out [B,6]
+ * float64 (may be NULL) = the pixel-space sampling map of affine_grid +
+ * grid_sample (align_corners=False): output pixel (i,j) samples the padded
+ * patch at column ix = a0*j + a1*i + a2, row iy = a3*j + a4*i + a5.  theta,
+ * target_size, roi and affine are evaluated in float64 from the fp32 inputs
+ * (theta rounded to fp32 on output); po_warp_* take `affine`. */
 int po_patch_params(const float* lab, int B, int L, const float* angle, const float* ux,
                     const float* uy, int do_rotate, int S, int P, float* theta, float* center,
-                    float* target_size, int32_t* roi, po_stream_t s);
+                    float* target_size, int32_t* roi, double* affine, po_stream_t s);
+
+/* Random draws of the patch transformer for images b0 .. b0+B-1 of a global
+ * batch (load_data.py:548-574 contrast U(0.8,1.2), brightness U(-0.1,0.1),
+ * noise U(-1,1) [B,3,P,P]; 607-614 angle U(-pi,pi); 693-707 ux, uy U(0,1)).
+ * Counter-based (Philox4x32-10, key = seed, counter = {element group, global
+ * image index, step counter}): a rank drawing its shard gets exactly the rows a
+ * single process draws for the whole batch.  Any output may be NULL. */
+int po_draws(uint64_t seed, uint64_t counter, int b0, int B, int P, float* contrast, float* bright,
+             float* noise, float* angle, float* ux, float* uy, po_stream_t s);
+
+/* NaN/Inf guard (replaces torch.autograd.detect_anomaly, train_patch.py:158):
+ * flags[0] |= bit if any of x[0..n) is not finite.  No host synchronisation. */
+int po_check_finite(const float* x, int64_t n, int32_t bit, int32_t* flags, po_stream_t s);
 
 /* Augment (contrast/brightness/noise/clamp, load_data.py:548-574) + affine
  * bilinear warp of patch and mask (affine_grid + grid_sample, align_corners
@@ -68,16 +87,16 @@ int po_patch_params(const float* lab, int B, int L, const float* angle, const fl
  * mode 1: also composite, out = where(adv_t==0, img, adv_t) (PatchApplier,
  *         load_data.py:820) into `out` [B,3,S,S]; `img` required.
  * patch_mp [3,P,P] (median-pooled patch), noise [B,3,P,P] U(-1,1) (x0.1 inside),
- * contrast/bright [B], theta [B,6]. */
+ * contrast/bright [B], affine [B,6] float64 (po_patch_params). */
 int po_warp_fwd(const float* img, const float* patch_mp, const float* noise, const float* contrast,
-                const float* bright, const float* theta, int B, int S, int P, int mode,
+                const float* bright, const double* affine, int B, int S, int P, int mode,
                 float* out, po_stream_t s);
 /* Backward of po_warp_fwd w.r.t. patch_mp: d_patch_mp [3,P,P] (overwritten).
  * d_out [B,3,S,S] is dL/d(out).  mode as in fwd (mode 1 applies the where()
  * routing).  Deterministic: one thread per patch element gathers over images
  * and over the output pixels whose bilinear footprint covers it. */
 int po_warp_bwd(const float* d_out, const float* patch_mp, const float* noise, const float* contrast,
-                const float* bright, const float* theta, int B, int S, int P, int mode,
+                const float* bright, const double* affine, int B, int S, int P, int mode,
                 float* work /* [B,3,S,S] scratch, may alias d_out */, float* d_patch_mp,
                 po_stream_t s);
 
@@ -116,8 +135,9 @@ int po_regularisers(const float* patch, int P, const float* colors, int ncol, co
  * (each may be NULL).  d_heads (may be NULL, same layout as heads): gradient of
  * g2[0]*no_obj + g2[1]*no_cls (g2: DEVICE pointer, 2 floats)
  * written at the selected cells only (other elements untouched — caller zeroes).
- * flags: bit0 set if any cell index was out of range (clamped), bit1 if a
- * cell fell outside its head window (clamped; a planning error). */
+ * flags (may be NULL): OR-ed with bit0 if any cell index was out of range
+ * (clamped), bit1 if a cell fell outside its head window (clamped; a
+ * planning error) — an accumulator the caller checks when it chooses. */
 int po_cell_loss(const float* const* heads, const int* hw, const int* win, const int32_t* const* org,
                  int nheads, int Cp, int B, int S, const float* center, int target, int objective,
                  const float* g2, float* const* d_heads, float* out2, float* obj_out, float* cls_out,
@@ -243,9 +263,16 @@ typedef struct po_conv_desc {
    * block (nb, tap, c) is W[32 nb + (l & 31)][tap][16 c + 8 (l >> 5) + e].
    * Needs N % 32 == 0; NULL: those tiles do not apply. */
   const void* Wfrag;
+  /* Optional (prec 0, tile 61): Winograd F(2x2,3x3) weights of this launch,
+   * U = G g G^T in float64 rounded to fp32 (g = the launch's 3x3 taps mapped
+   * onto the canonical offsets -1..1), stored in MFMA fragment order
+   * [N/32][Cin_p/16][16 components][64 lanes][8]: element (lane l, s) of
+   * block (nb, kc, xi) is U[xi][16 kc + 8 (l >> 5) + s][32 nb + (l & 31)].
+   * NULL: tile 61 does not apply. */
+  const float* Wwino;
 } po_conv_desc;
 
-#define PO_CONV_NTILES 60
+#define PO_CONV_NTILES 61
 /* Tile `t` (1-based): block rows BM (output pixels), block columns BN (output
  * channels), k-step BK (input channels).  Tiles 1..10 stage operands through
  * registers, 11..20 are the same shapes staged by LDS-DMA, 21..28 are
@@ -255,7 +282,10 @@ typedef struct po_conv_desc {
  * 3x3 convs (53..54); 55..56 are the 2-D tile halo kernel (8 x 16 output
  * pixels per tile) for 3x3 convs of input step 1 or 2 on full maps without
  * split-K or boxes; 57..60 the same 2-D tiles (and 16 x 16-pixel ones at input
- * step 1) reading the weights as MFMA fragments from Wfrag.  A tile that does not apply to a launch makes po_conv
+ * step 1) reading the weights as MFMA fragments from Wfrag.  61 is the exact-fp32
+ * Winograd F(2x2,3x3) kernel (64 2x2-tiles x 32 channels x 16 input channels
+ * per k-step) for stride-1 3x3 convs and their input gradients on full maps,
+ * without split-K (needs Wwino).  A tile that does not apply to a launch makes po_conv
  * return PO_EINVAL.  Returns PO_EINVAL for a bad index. */
 int po_conv_tile_info(int t, int* bm, int* bn, int* bk, int* prec);
 

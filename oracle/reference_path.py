@@ -64,6 +64,14 @@ def parse_model_config(text):
 # --------------------------------------------------------------------------
 # median_pool.py:19-52 MedianPool2d(7, same=True)
 # --------------------------------------------------------------------------
+# Tie rule of the median's backward.  "torch": torch.median's own index
+# (implementation-defined when several window values equal the median, SURVEY
+# Q8) — the reference.  "first": the first window position (row-major) that
+# holds the median value — the rule po_median7 documents; tests of tied
+# windows select it so both sides route the gradient identically.
+MEDIAN_TIE_RULE = "torch"
+
+
 def median_pool7(x, k=7):
     """reflect pad per `_padding` (median_pool.py:26-44: stride 1 -> ph=pw=k-1,
     split pl=pw//2, pr=pw-pl), 7x7 unfold, median over the 49 window values
@@ -73,6 +81,10 @@ def median_pool7(x, k=7):
     xp = F.pad(x, (pl, pr, pl, pr), mode="reflect")
     win = xp.unfold(2, k, 1).unfold(3, k, 1)
     win = win.contiguous().view(win.size()[:4] + (-1,))
+    if MEDIAN_TIE_RULE == "first":
+        med = win.detach().median(dim=-1)[0]
+        first = (win.detach() == med.unsqueeze(-1)).int().argmax(dim=-1, keepdim=True)
+        return torch.gather(win, -1, first).squeeze(-1)
     return win.median(dim=-1)[0]
 
 
@@ -527,7 +539,7 @@ def max_prob_extractor(outputs, cls_id, num_cls, anchors_per_head, sigmoid_mode=
 # train_patch.py:157-330 one iteration of the batch loop
 # --------------------------------------------------------------------------
 def train_step(patch, img_batch, lab_batch, draws, net, colors, target_id=TARGET_ID,
-               objective="ce", weight_grad=False, branch=None, record=None):
+               objective="ce", weight_grad=False, branch=None, record=None, combine=None):
     """One iteration of PatchTrainer.train's batch body (train_patch.py:164-327).
 
     ``patch`` is the [3,P,P] leaf.  Returns a dict of loss terms (float
@@ -536,7 +548,9 @@ def train_step(patch, img_batch, lab_batch, draws, net, colors, target_id=TARGET
     ``objective``: "ce" (active, train_patch.py:253), "targeted"
     (noCLS_loss_targeted, train_patch.py:262) or "untargeted"
     (train_patch.py:305-307).  ``branch``, ``record``: see OracleDarknet.forward
-    (recorded pre-activations keep their gradients).
+    (recorded pre-activations keep their gradients).  ``combine`` (tests of
+    the data-parallel weighting): f(no_obj_loss, no_cls_loss, nps, tv,
+    colorful) -> (loss, terms) replaces the loss formula of 312-314.
     """
     leaf = patch.detach().clone().requires_grad_(True)
     img_size = net.height
@@ -560,9 +574,14 @@ def train_step(patch, img_batch, lab_batch, draws, net, colors, target_id=TARGET
     nps_loss = nps * NPS_FACTOR
     tv_loss = tv * TV_FACTOR
     colorful = colorful_loss(leaf)                                                 # 311
-    loss = nps_loss + torch.max(tv_loss, torch.tensor(0.1)) + no_obj_loss + colorful  # 312-314
-    if objective != "untargeted":
-        loss = loss + no_cls_loss
+    if combine is None:
+        loss = nps_loss + torch.max(tv_loss, torch.tensor(0.1)) + no_obj_loss + colorful  # 312-314
+        if objective != "untargeted":
+            loss = loss + no_cls_loss
+    else:
+        loss, t = combine(no_obj_loss, no_cls_loss, nps, tv, colorful)
+        nps_loss, tv_loss, no_obj_loss, no_cls_loss, colorful = (
+            t["nps_loss"], t["tv_loss"], t["no_obj_loss"], t["no_cls_loss"], t["colorful_loss"])
     loss.backward()                                                                # 327
     return {
         "loss": loss.detach(), "nps_loss": nps_loss.detach(), "tv_loss": tv_loss.detach(),

@@ -78,7 +78,15 @@ def test_warp_fwd_quad_kernel_bit_identical(mode):
     theta = torch.tensor([[1.6, 0.4, 0.1, -0.4, 1.6, -0.2],      # scaled, rotated, inside
                           [0.9, -1.1, 0.9, 1.1, 0.9, -0.8],      # large, partly outside
                           [2.0, 0.0, 3.5, 0.0, 2.0, 3.5]],       # off the frame
-                         dtype=torch.float32, device=dev)
+                         dtype=torch.float64)
+    # po_warp_* take the pixel-space sampling map (po_patch_params' affine):
+    # ix = a0 j + a1 i + a2, iy = a3 j + a4 i + a5 (affine_grid + unnormalize folded)
+    half = 0.5 - 0.5 * S
+    affine = torch.stack([theta[:, 0], theta[:, 1],
+                          (theta[:, 0] + theta[:, 1]) * half + 0.5 * S * theta[:, 2] + 0.5 * (S - 1),
+                          theta[:, 3], theta[:, 4],
+                          (theta[:, 3] + theta[:, 4]) * half + 0.5 * S * theta[:, 5] + 0.5 * (S - 1)], 1)
+    affine = affine.contiguous().to(dev)
     outs = []
     for v1 in (False, True):
         out = torch.full((B, 3, S, S), float("nan"), device=dev)
@@ -87,7 +95,8 @@ def test_warp_fwd_quad_kernel_bit_identical(mode):
             if v1:
                 os.environ["PO_WARP_V1"] = "1"
             nat.call("po_warp_fwd", nat.ptr(img) if mode == 1 else None, nat.ptr(mp), nat.ptr(noise),
-                     nat.ptr(contrast), nat.ptr(bright), nat.ptr(theta), B, S, P, mode, nat.ptr(out), nat.stream())
+                     nat.ptr(contrast), nat.ptr(bright), nat.ptr(affine, torch.float64), B, S, P, mode, nat.ptr(out),
+                     nat.stream())
             torch.cuda.synchronize()
         finally:
             os.environ.pop("PO_WARP_V1", None)

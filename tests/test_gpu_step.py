@@ -1,12 +1,18 @@
 """GPU parity of one full training iteration (train_patch.py:164-330) against
 the oracle: loss terms, bit-exact cell indices, objectness/class extraction,
 and the fp32 patch gradient within 1e-4 relative (north_star tolerance:
-max|g_hip - g_ref| / max|g_ref| <= 1e-4)."""
+max|g_hip - g_ref| / max|g_ref| <= 1e-4).
+
+On yolov3-dota@608 the comparison is branch-aligned: the oracle runs on the
+LeakyReLU/maxpool decisions the HIP forward took, and every decision where
+the two disagree must be a rounding tie (assert_branch_ties_only) — a kernel
+that flips a real branch fails.  The yardstick is the float64 evaluation of
+the same ops on those branches; the bound is a fixed 1e-4."""
 import pytest
 import torch
 
 import oracle
-from conftest import pkg_mod, plan_branches
+from conftest import assert_branch_ties_only, pkg_mod, plan_branches
 
 pytestmark = pytest.mark.gpu
 DEV = torch.device("cuda", 0)
@@ -72,32 +78,60 @@ def test_step_mini3_objectives(tmp_path, objective):
     _compare(*_run("builtin:mini3", 4, 32, tmp_path, objective=objective))
 
 
-@pytest.mark.parametrize("prec", ["fp16x3", "fp32"])
-def test_step_yolov3_dota_608(tmp_path, prec):
-    """yolov3-dota, two 608x608 frames, 224x224 patch.  Through 75 layers two
-    fp32 implementations differ by more than 1e-4 even on aligned branches
-    (different summation orders), so both are measured against a float64
-    evaluation of the same ops: the HIP gradient must be within 1e-4 of it,
-    or no further from it than 2x the fp32 oracle is."""
+# A LeakyReLU decision the HIP forward took differently from the oracle must
+# sit within the forward's rounding of zero: |pre-activation| <= TIE_TOL *
+# max|pre-activation of the layer|.  fp32 operands carry 24 bits; fp16x3
+# operands ~22 bits, and their error compounds over the 75 layers.
+TIE_TOL = {"fp32": 1e-5, "fp16x3": 1e-4}
+
+
+def branch_aligned_608(tr, ref_net, B, seed, objective="ce"):
+    """One HIP step on B 608x608 frames and the oracle on its branches: the
+    fp32 oracle (with the tie check) and the float64 yardstick.  Returns
+    (terms, hip grad, fp32 oracle result, err_hip, err_fp32)."""
     sy, ld = pkg_mod("synthetic"), pkg_mod("load_data")
-    tr, ref_net = _trainer("builtin:yolov3-dota", tmp_path, prec=prec)
-    B, P, S = 2, 224, 608
-    img, lab = sy.frames(B, S, seed=40), sy.labels(B, seed=41)
-    patch, dr = sy.patch(P, seed=42), sy.draws(B, P, seed=43)
+    P, S = 224, 608
+    img, lab = sy.frames(B, S, seed=seed), sy.labels(B, seed=seed + 1)
+    patch, dr = sy.patch(P, seed=seed + 2), sy.draws(B, P, seed=seed + 3)
     colors = ld.load_printability_colors("builtin:30values")
     pg = patch.to(DEV).requires_grad_(True)
     loss, terms = tr.losses(pg, img.to(DEV), lab.to(DEV), {k: v.to(DEV) for k, v in dr.items()})
     br = plan_branches(tr.last_plan)
     loss.backward()
-    ref32 = oracle.train_step(patch, img, lab, dr, ref_net, colors, branch=br)
-    ref64 = oracle.train_step_f64(patch, img, lab, dr, ref_net, colors, branch=br)
-    _compare(ref32, terms, pg.grad.cpu(), grad_check=False)
+    rec = {}
+    ref32 = oracle.train_step(patch, img, lab, dr, ref_net, colors, objective=objective, branch=br, record=rec)
+    assert_branch_ties_only(br, rec, TIE_TOL[tr.darknet_model.conv_prec])   # differing branches are ties
+    del rec
+    ref64 = oracle.train_step_f64(patch, img, lab, dr, ref_net, colors, objective=objective, branch=br)
     g64 = ref64["grad"]
     scale = g64.abs().max()
-    err_hip = float((pg.grad.cpu().double() - g64).abs().max() / scale)
+    g = pg.grad.cpu()
+    err_hip = float((g.double() - g64).abs().max() / scale)
     err_32 = float((ref32["grad"].double() - g64).abs().max() / scale)
+    return terms, g, ref32, err_hip, err_32
+
+
+@pytest.mark.parametrize("prec", ["fp16x3", "fp32"])
+def test_step_yolov3_dota_608(tmp_path, prec):
+    """yolov3-dota, two 608x608 frames, 224x224 patch: patch gradient within
+    1e-4 (max-abs relative) of the float64 evaluation, branch-aligned with
+    ties asserted; the fp32 oracle's own distance is printed beside."""
+    tr, ref_net = _trainer("builtin:yolov3-dota", tmp_path, prec=prec)
+    terms, g, ref32, err_hip, err_32 = branch_aligned_608(tr, ref_net, 2, 40)
+    _compare(ref32, terms, g, grad_check=False)
     print("yolov3 (%s) patch grad vs float64: hip %.3g, fp32 oracle %.3g" % (prec, err_hip, err_32))
-    assert err_hip <= max(1e-4, 2.0 * err_32), (err_hip, err_32)
+    assert err_hip <= 1e-4, (err_hip, err_32)
+
+
+def test_step_yolov3_targeted(tmp_path):
+    """BASELINE config 4's per-rank workload: the targeted class objective
+    (noCLS_loss_targeted, a batch SUM, train_patch.py:550-577) + NPS + TV on
+    yolov3-dota@608, exact fp32 convolutions."""
+    tr, ref_net = _trainer("builtin:yolov3-dota", tmp_path, objective="targeted", prec="fp32")
+    terms, g, ref32, err_hip, err_32 = branch_aligned_608(tr, ref_net, 3, 140, objective="targeted")
+    _compare(ref32, terms, g, grad_check=False)
+    print("yolov3 targeted patch grad vs float64: hip %.3g, fp32 oracle %.3g" % (err_hip, err_32))
+    assert err_hip <= 1e-4, (err_hip, err_32)
 
 
 def test_two_adam_steps_yolov3(tmp_path):
