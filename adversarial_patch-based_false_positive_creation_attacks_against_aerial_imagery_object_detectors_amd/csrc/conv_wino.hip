@@ -158,16 +158,16 @@ __global__ __launch_bounds__(256) void conv_wino_k(const ConvArgs a, const float
     }
   };
 
-  // ---- B operand: U in fragment order [nb][kc][xi][lane][8]
+  // ---- B operand: U in fragment order [nb][kc][xi][2 halves][lane][4]
   const int kc_n = a.Cin_p / WK;
-  const float* Ub = U + ((size_t)tn * kc_n * 16) * 512 + (size_t)lane * 8;
+  const float* Ub = U + ((size_t)tn * kc_n * 16) * 512 + (size_t)lane * 4;
   float4 bc[4][2], bn[4][2];
   auto bload = [&](float4 (&dst)[4][2], int ks) {
 #pragma unroll
     for (int c = 0; c < 4; ++c) {
       const float* p = Ub + ((size_t)ks * 16 + wave * 4 + c) * 512;
       dst[c][0] = *reinterpret_cast<const float4*>(p);
-      dst[c][1] = *reinterpret_cast<const float4*>(p + 4);
+      dst[c][1] = *reinterpret_cast<const float4*>(p + 256);
     }
   };
 
@@ -274,6 +274,214 @@ __global__ __launch_bounds__(256) void conv_wino_k(const ConvArgs a, const float
   if (a.sum_amax) po::amax_commit(a.sum_amax, mx.s);
   if (a.y2_amax) po::amax_commit(a.y2_amax, mx.y2);
 }
+
+// ---------------------------------------------------------------------------
+// Tile 62: 32 tiles x 64 output channels per workgroup, LDS-DMA input.
+//
+// The input patches arrive by LDS-DMA (buffer_load ... lds: no VGPR staging)
+// as coalesced rows: one instruction loads patch pixel p of 16 tiles, 64 B
+// (the k-step's 16 channels) per tile, into R[buf][p][tile][16 ch].  A thread
+// transforms (tile, channel pair) from LDS into V[buf][xi][tile][16 ch]
+// (chunks swizzled by tile).  R and V are both double-buffered: during the
+// MFMAs of step k the transform of step k+1 and the DMA of step k+2 run;
+// one barrier per step.  B fragments (U) come from global memory, in the
+// layout [N/32][Cin_p/16][16][2 halves][64 lanes][4] (two contiguous 1 KB
+// loads per component and 32-channel block), one step ahead.
+constexpr int T2 = 32, N2 = 64;
+constexpr int R2_FLOATS = 16 * T2 * WK;                 // one raw buffer: 32 KB
+constexpr int V2_FLOATS = 16 * T2 * WK;                 // one transformed buffer: 32 KB
+constexpr int M2_ROW = N2 + 8;                          // epilogue rows padded: conflict-free C writes
+
+// 16-byte LDS-DMA: lane l's 16 bytes from rsrc + voff + soff land at lds + 16*l
+// (soff: wave-uniform, scalar; an out-of-range voff stays out of range)
+__device__ __forceinline__ void lds_dma16(__amdgpu_buffer_rsrc_t rs, float* lds, uint32_t voff, uint32_t soff) {
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (__attribute__((address_space(3))) void*)lds, 16, voff, soff, 0, 0);
+}
+typedef float f2v __attribute__((ext_vector_type(2)));       // packed pairs: v_pk_add_f32
+__device__ __forceinline__ int v2idx(int xi, int t, int ch) { return ((xi * T2 + t) * WK) + ((ch ^ ((t >> 2) & 3)) << 2); }
+
+__global__ __launch_bounds__(256) void conv_wino2_k(const ConvArgs a, const float* __restrict__ U, int Ht, int Wt) {
+  __shared__ __attribute__((aligned(16))) float smem[16 * T2 * M2_ROW];     // 144 KB (k-loop: 2R + 2V = 128 KB)
+  __shared__ int s_live;
+  float* R = smem;                       // [2][16 p][T2][WK]
+  float* V = smem + 2 * R2_FLOATS;       // [2][16 xi][T2][WK] (swizzled chunks)
+  const int wgid = po::xcd_remap();
+  const int tn = wgid % a.ntiles_n, tm = wgid / a.ntiles_n;
+  const int m0 = tm * T2, n0 = tn * N2;
+  const int tid = threadIdx.x & 255, lane = tid & 63, wave = tid >> 6;
+  const int wave_u = __builtin_amdgcn_readfirstlane(wave);
+  const int h = lane >> 5;
+
+  if (tid == 0) s_live = 0;
+  __syncthreads();
+  if (tid < T2) {
+    int b, ti, tj;
+    if (tile_point(a, Ht, Wt, m0 + tid, b, ti, tj)) s_live = 1;
+  }
+  __syncthreads();
+  if (!s_live) return;
+
+  // ---- DMA source offsets: wave w loads patch row u = w (pixels p = 4w + v)
+  // for both 16-tile halves; lane L -> tile 16*half + (L >> 2), chunk L & 3
+  const uint32_t in_bytes = (uint32_t)__builtin_amdgcn_readfirstlane(a.in_bytes);
+  const __amdgpu_buffer_rsrc_t in_rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(a.in), 0, in_bytes, 0x00020000);
+  const uint32_t pix_bytes = (uint32_t)a.Cin_p * 4u;
+  uint32_t doff[2][4];
+#pragma unroll
+  for (int half = 0; half < 2; ++half) {
+    int b, ti, tj;
+    const bool ok_t = tile_point(a, Ht, Wt, m0 + 16 * half + (lane >> 2), b, ti, tj);
+#pragma unroll
+    for (int v = 0; v < 4; ++v) {
+      const int y = 2 * ti - 1 + wave_u, x = 2 * tj - 1 + v;
+      const bool ok = ok_t && (unsigned)y < (unsigned)a.Hin && (unsigned)x < (unsigned)a.Win;
+      doff[half][v] = ok ? (((uint32_t)b * a.Hin + y) * a.Win + x) * pix_bytes + 16u * (lane & 3) : kOOB;
+    }
+  }
+  auto dma = [&](int ks, float* Rb) {
+    const uint32_t cb = (uint32_t)__builtin_amdgcn_readfirstlane(ks * (WK * 4));
+#pragma unroll
+    for (int v = 0; v < 4; ++v)
+#pragma unroll
+      for (int half = 0; half < 2; ++half) lds_dma16(in_rs, Rb + ((wave_u * 4 + v) * T2 + 16 * half) * WK, doff[half][v], cb);
+  };
+  // ---- transform: thread -> tile r, channel pair qq (a half-wave covers 4
+  // tiles x 8 pairs: conflict-free 8-byte LDS reads and writes)
+  const int qq = lane & 7, r = wave * 8 + (lane >> 3);
+  auto transform = [&](const float* Rb, float* Vb) {
+    f2v d[16];
+#pragma unroll
+    for (int p = 0; p < 16; ++p) d[p] = *reinterpret_cast<const f2v*>(Rb + (p * T2 + r) * WK + 2 * qq);
+    f2v t[4][4];
+#pragma unroll
+    for (int v = 0; v < 4; ++v) {
+      const f2v d0 = d[v], d1 = d[4 + v], d2 = d[8 + v], d3 = d[12 + v];
+      t[0][v] = d0 - d2;
+      t[1][v] = d1 + d2;
+      t[2][v] = d2 - d1;
+      t[3][v] = d1 - d3;
+    }
+    const int sub = (qq & 1) * 2;
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const f2v e[4] = {t[u][0] - t[u][2], t[u][1] + t[u][2], t[u][2] - t[u][1], t[u][1] - t[u][3]};
+#pragma unroll
+      for (int v = 0; v < 4; ++v) *reinterpret_cast<f2v*>(Vb + v2idx(u * 4 + v, r, qq >> 1) + sub) = e[v];
+    }
+  };
+
+  // ---- B operand
+  const int kc_n = a.Cin_p / WK;
+  const float* Ub = U + (size_t)lane * 4;
+  float4 bc[4][2][2], bn[4][2][2];
+  auto bload = [&](float4 (&dst)[4][2][2], int ks) {
+#pragma unroll
+    for (int c = 0; c < 4; ++c)
+#pragma unroll
+      for (int nb = 0; nb < 2; ++nb) {
+        const float* p = Ub + ((((size_t)(2 * tn + nb) * kc_n + ks) * 16 + wave_u * 4 + c) * 512);
+        dst[c][nb][0] = *reinterpret_cast<const float4*>(p);
+        dst[c][nb][1] = *reinterpret_cast<const float4*>(p + 256);
+      }
+  };
+
+  floatx16 acc[4][2];
+#pragma unroll
+  for (int c = 0; c < 4; ++c)
+#pragma unroll
+    for (int nb = 0; nb < 2; ++nb)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) acc[c][nb][e] = 0.f;
+
+  dma(0, R);
+  if (kc_n > 1) dma(1, R + R2_FLOATS);
+  bload(bc, 0);
+  __syncthreads();                         // raw(0), raw(1) landed
+  transform(R, V);
+  __syncthreads();
+  // one k-step on V[buf] with B fragments bcur, prefetching step ks+1 into bnxt
+  auto kstep = [&](int ks, float4 (&bcur)[4][2][2], float4 (&bnxt)[4][2][2]) {
+    const int buf = ks & 1;
+    if (ks + 2 < kc_n) dma(ks + 2, R + buf * R2_FLOATS);
+    if (ks + 1 < kc_n) bload(bnxt, ks + 1);
+    const float* Vb = V + buf * V2_FLOATS;
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      const int xi = wave_u * 4 + c;
+      const int t = lane & 31;
+      const float4 a0 = *reinterpret_cast<const float4*>(Vb + v2idx(xi, t, 2 * h));
+      const float4 a1 = *reinterpret_cast<const float4*>(Vb + v2idx(xi, t, 2 * h + 1));
+      const float av[8] = {a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w};
+#pragma unroll
+      for (int nb = 0; nb < 2; ++nb) {
+        const float bv[8] = {bcur[c][nb][0].x, bcur[c][nb][0].y, bcur[c][nb][0].z, bcur[c][nb][0].w,
+                             bcur[c][nb][1].x, bcur[c][nb][1].y, bcur[c][nb][1].z, bcur[c][nb][1].w};
+#pragma unroll
+        for (int s8 = 0; s8 < 8; ++s8)        // MFMA step s, half h <-> channel 8h + s
+          acc[c][nb] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[s8], bv[s8], acc[c][nb], 0, 0, 0);
+      }
+    }
+    if (ks + 1 < kc_n) transform(R + (buf ^ 1) * R2_FLOATS, V + (buf ^ 1) * V2_FLOATS);
+    __syncthreads();
+  };
+  for (int ks = 0; ks < kc_n; ks += 2) {    // two steps per trip: the B registers swap roles, no copies
+    kstep(ks, bc, bn);
+    if (ks + 1 < kc_n) kstep(ks + 1, bn, bc);
+  }
+
+  // ---- epilogue: M[xi][tile][64 ch] (rows padded), then A^T M A per (tile, channel)
+  float* M = smem;
+#pragma unroll
+  for (int c = 0; c < 4; ++c)
+#pragma unroll
+    for (int nb = 0; nb < 2; ++nb)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) {
+        const int t = (e & 3) + 8 * (e >> 2) + 4 * h;
+        M[((wave * 4 + c) * T2 + t) * M2_ROW + nb * 32 + (lane & 31)] = acc[c][nb][e];
+      }
+  __syncthreads();
+  EpiMax mx;
+  const int n = n0 + lane;
+  const int wpp = a.Cout_p >> 5;
+#pragma unroll 1
+  for (int it = 0; it < T2 / 4; ++it) {
+    const int t = wave + 4 * it;
+    int bb, tti, ttj;
+    const bool tl = tile_point(a, Ht, Wt, m0 + t, bb, tti, ttj);
+    float m[16];
+#pragma unroll
+    for (int xi = 0; xi < 16; ++xi) m[xi] = M[(xi * T2 + t) * M2_ROW + lane];
+    float s0[4], s1[4];
+#pragma unroll
+    for (int v = 0; v < 4; ++v) {
+      s0[v] = m[0 * 4 + v] + m[1 * 4 + v] + m[2 * 4 + v];
+      s1[v] = m[1 * 4 + v] - m[2 * 4 + v] - m[3 * 4 + v];
+    }
+    const float yv[2][2] = {{s0[0] + s0[1] + s0[2], s0[1] - s0[2] - s0[3]},
+                            {s1[0] + s1[1] + s1[2], s1[1] - s1[2] - s1[3]}};
+    int4 bx = make_int4(0, 0, 1 << 30, 1 << 30);
+    if (a.gbox && tl) bx = reinterpret_cast<const int4*>(a.gbox)[bb];
+#pragma unroll
+    for (int di = 0; di < 2; ++di)
+#pragma unroll
+      for (int dj = 0; dj < 2; ++dj) {
+        const int i = 2 * tti + di, j = 2 * ttj + dj;
+        const bool ok = tl && n < a.N && i < a.Hout && j < a.Wout && i >= bx.x && i < bx.z && j >= bx.y && j < bx.w;
+        const size_t pix = ((size_t)bb * a.Hout + i) * a.Wout + j;
+        float out = 0.f;
+        if (ok) out = epi_store(a, pix, n, yv[di][dj], mx);
+        if (a.ybits) {
+          // 64 lanes = channels n0 .. n0+63 of one pixel: two sign-bit words
+          const uint64_t bits = __ballot(ok && out > 0.f);
+          if (ok && (lane & 31) == 0) a.ybits[pix * wpp + (n >> 5)] = (uint32_t)(bits >> (lane & 32));
+        }
+      }
+  }
+  if (a.y_amax) po::amax_commit(a.y_amax, mx.y);
+  if (a.sum_amax) po::amax_commit(a.sum_amax, mx.s);
+  if (a.y2_amax) po::amax_commit(a.y2_amax, mx.y2);
+}
 }  // namespace
 
 namespace po {
@@ -281,7 +489,7 @@ namespace po {
 // correlation over the full 3x3 neighbourhood on full maps (no windows, no
 // split-K, destination = source grid) with N % 32 == 0, Cin_p % 16 == 0 and
 // the transformed weights (po_conv_desc.Wwino).
-int launch_wino(const ConvArgs& a, const float* U, hipStream_t st) {
+int launch_wino(const ConvArgs& a, const float* U, hipStream_t st, int bm) {
   PO_REQUIRE(U, "po_conv: Winograd tile needs the transformed weights (Wwino)");
   PO_REQUIRE(a.prec == 0 && a.ntaps == 9 && a.tkw == 3 && (a.sdh == 1 || a.sdh == -1) && (a.sdw == 1 || a.sdw == -1) &&
                  a.dh0 == -a.sdh && a.dw0 == -a.sdw,
@@ -294,6 +502,14 @@ int launch_wino(const ConvArgs& a, const float* U, hipStream_t st) {
   PO_REQUIRE(a.N % WN == 0 && a.Cin_p % WK == 0, "po_conv: Winograd tile needs N %% 32 == 0 and Cin_p %% 16 == 0");
   const int Ht = (a.Hout + 1) / 2, Wt = (a.Wout + 1) / 2;
   PO_REQUIRE((int64_t)a.B * Ht * Wt < (1LL << 31), "po_conv: too many tiles");
+  if (bm == T2) {
+    PO_REQUIRE(a.N % N2 == 0, "po_conv: Winograd tile 62 needs N %% 64 == 0");
+    ConvArgs b = a;
+    b.ntiles_n = a.N / N2;
+    const int ntm = ceil_div((int64_t)a.B * Ht * Wt, T2);
+    hipLaunchKernelGGL(conv_wino2_k, dim3(ntm * b.ntiles_n), dim3(256), 0, st, b, U, Ht, Wt);
+    return check_launch("po_conv (winograd 32x64)");
+  }
   ConvArgs b = a;
   b.ntiles_n = a.N / WN;
   const int ntm = ceil_div((int64_t)a.B * Ht * Wt, WT);

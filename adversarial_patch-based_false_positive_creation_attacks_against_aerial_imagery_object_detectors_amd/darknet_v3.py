@@ -1179,8 +1179,9 @@ def wino_transform(w, offs):
     """po_conv_desc.Wwino of launch weights w [N][9][Cin_p] (fp32) whose tap t
     reads source offset offs[t] = (dh, dw) in {-1,0,1}^2: U = G g G^T in
     float64, rounded once to fp32, in MFMA fragment order
-    [N/32][Cin_p/16][16][64 lanes][8], element (lane l, s) of block (nb, kc, xi)
-    = U[xi][16 kc + 8 (l >> 5) + s][32 nb + (l & 31)]."""
+    [N/32][Cin_p/16][16][2][64 lanes][4]: element (lane l, s) of block
+    (nb, kc, xi) = U[xi][16 kc + 8 (l >> 5) + s][32 nb + (l & 31)] sits at
+    [nb][kc][xi][s >> 2][l][s & 3] (a wave reads each half as 1 KB)."""
     N, T, C = w.shape
     assert T == 9 and N % 32 == 0 and C % 16 == 0
     g = torch.zeros(N, C, 3, 3, dtype=torch.float64, device=w.device)
@@ -1188,7 +1189,7 @@ def wino_transform(w, offs):
         g[:, :, dh + 1, dw + 1] = w[:, t, :].double()
     G = torch.tensor(_WINO_G, dtype=torch.float64, device=w.device)
     U = torch.einsum("xa,ncab,yb->xycn", G, g, G).reshape(16, C, N).float()        # [xi][c][n]
-    return U.view(16, C // 16, 2, 8, N // 32, 32).permute(4, 1, 0, 2, 5, 3).contiguous()
+    return U.view(16, C // 16, 2, 2, 4, N // 32, 32).permute(5, 1, 0, 3, 2, 6, 4).contiguous()
 
 
 class _DarknetFn(torch.autograd.Function):

@@ -266,13 +266,13 @@ typedef struct po_conv_desc {
   /* Optional (prec 0, tile 61): Winograd F(2x2,3x3) weights of this launch,
    * U = G g G^T in float64 rounded to fp32 (g = the launch's 3x3 taps mapped
    * onto the canonical offsets -1..1), stored in MFMA fragment order
-   * [N/32][Cin_p/16][16 components][64 lanes][8]: element (lane l, s) of
-   * block (nb, kc, xi) is U[xi][16 kc + 8 (l >> 5) + s][32 nb + (l & 31)].
-   * NULL: tile 61 does not apply. */
+   * [N/32][Cin_p/16][16 components][2][64 lanes][4]: element (lane l, s) of
+   * block (nb, kc, xi), U[xi][16 kc + 8 (l >> 5) + s][32 nb + (l & 31)], sits
+   * at [nb][kc][xi][s >> 2][l][s & 3].  NULL: tiles 61-62 do not apply. */
   const float* Wwino;
 } po_conv_desc;
 
-#define PO_CONV_NTILES 61
+#define PO_CONV_NTILES 62
 /* Tile `t` (1-based): block rows BM (output pixels), block columns BN (output
  * channels), k-step BK (input channels).  Tiles 1..10 stage operands through
  * registers, 11..20 are the same shapes staged by LDS-DMA, 21..28 are
@@ -282,10 +282,11 @@ typedef struct po_conv_desc {
  * 3x3 convs (53..54); 55..56 are the 2-D tile halo kernel (8 x 16 output
  * pixels per tile) for 3x3 convs of input step 1 or 2 on full maps without
  * split-K or boxes; 57..60 the same 2-D tiles (and 16 x 16-pixel ones at input
- * step 1) reading the weights as MFMA fragments from Wfrag.  61 is the exact-fp32
- * Winograd F(2x2,3x3) kernel (64 2x2-tiles x 32 channels x 16 input channels
- * per k-step) for stride-1 3x3 convs and their input gradients on full maps,
- * without split-K (needs Wwino).  A tile that does not apply to a launch makes po_conv
+ * step 1) reading the weights as MFMA fragments from Wfrag.  61 and 62 are the
+ * exact-fp32 Winograd F(2x2,3x3) kernels (64 2x2-tiles x 32 channels, and 32
+ * tiles x 64 channels with LDS-DMA input; 16 input channels per k-step) for
+ * stride-1 3x3 convs and their input gradients on full maps, without split-K
+ * (needs Wwino; 62 needs N % 64 == 0).  A tile that does not apply to a launch makes po_conv
  * return PO_EINVAL.  Returns PO_EINVAL for a bad index. */
 int po_conv_tile_info(int t, int* bm, int* bn, int* bk, int* prec);
 

@@ -80,9 +80,12 @@ def test_step_mini3_objectives(tmp_path, objective):
 
 # A LeakyReLU decision the HIP forward took differently from the oracle must
 # sit within the forward's rounding of zero: |pre-activation| <= TIE_TOL *
-# max|pre-activation of the layer|.  fp32 operands carry 24 bits; fp16x3
-# operands ~22 bits, and their error compounds over the 75 layers.
-TIE_TOL = {"fp32": 1e-5, "fp16x3": 1e-4}
+# max|pre-activation of the layer|.  Two fp32 evaluations of the 75-layer
+# forward (folded vs unfolded BN, different summation orders) differ by up
+# to ~5e-5 of a layer's maximum (test_gpu_darknet's forward bound); fp16x3
+# operands carry ~22 bits instead of 24.  A kernel that flips a real
+# branch misses by O(max).
+TIE_TOL = {"fp32": 5e-5, "fp16x3": 1e-4}
 
 
 def branch_aligned_608(tr, ref_net, B, seed, objective="ce"):

@@ -156,7 +156,7 @@ def test_headline_plan_b16_608(yolo_weights, monkeypatch, prec):
     colors = ld.load_printability_colors("builtin:30values")
     rec = {}
     ref32 = oracle.train_step(patch, img, lab, dr, ref_net, colors, branch=br, record=rec)
-    assert_branch_ties_only(br, rec, {"fp32": 1e-5, "fp16x3": 1e-4}[prec])
+    assert_branch_ties_only(br, rec, {"fp32": 5e-5, "fp16x3": 1e-4}[prec])
     del rec
     assert terms["cells"].cpu().tolist() == ref32["cells"]
     torch.testing.assert_close(terms["obj"].cpu(), ref32["obj"], rtol=0, atol=2e-5)

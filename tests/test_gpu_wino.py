@@ -15,7 +15,7 @@ from conftest import pkg_mod
 
 pytestmark = pytest.mark.gpu
 DEV = torch.device("cuda", 0)
-WINO = 61
+WINO_TILES = [61, 62]       # 64 tiles x 32 channels; 32 tiles x 64 channels (LDS-DMA input, N % 64 == 0)
 
 
 def _rel(a, b):
@@ -48,10 +48,13 @@ def _setup(B, H, Cin, Cout, flip, seed):
     return x, w, bias, wd, U
 
 
-@pytest.mark.parametrize("B,H,Cin,Cout,flip", [(3, 7, 96, 96, False), (3, 7, 96, 96, True), (2, 38, 256, 512, False),
+@pytest.mark.parametrize("WINO", WINO_TILES)
+@pytest.mark.parametrize("B,H,Cin,Cout,flip", [(3, 7, 96, 128, False), (3, 7, 96, 128, True), (2, 38, 256, 512, False),
                                                (4, 19, 512, 256, True), (1, 76, 128, 64, False),
                                                (2, 9, 16, 32, False)])
-def test_wino_matches_float64_conv(B, H, Cin, Cout, flip):
+def test_wino_matches_float64_conv(B, H, Cin, Cout, flip, WINO):
+    if WINO == 62 and Cout % 64:
+        pytest.skip("tile 62 takes N % 64 == 0")
     nat = pkg_mod("_native")
     x, w, bias, wd, U = _setup(B, H, Cin, Cout, flip, seed=H * Cin + flip)
     ref = F.conv2d(x.double(), w.double(), bias.double(), padding=1)
@@ -70,13 +73,14 @@ def test_wino_matches_float64_conv(B, H, Cin, Cout, flip):
     assert e_w < 1e-5 and e_w < 4 * e_d + 1e-7, (e_w, e_d)
 
 
+@pytest.mark.parametrize("WINO", WINO_TILES)
 @pytest.mark.parametrize("mode", ["fwd_bits", "fwd_shortcut", "dgrad_acc_bits", "dgrad_dual"])
-def test_wino_epilogues_match_direct(mode):
+def test_wino_epilogues_match_direct(mode, WINO):
     """The training plan's epilogue combinations: identical semantics to the
     direct kernel (values within fp32 class, sign bits of the written
     values, max|x| slots bounding them)."""
     nat = pkg_mod("_native")
-    B, H, Cin, Cout = 2, 11, 64, 96
+    B, H, Cin, Cout = 2, 11, 64, 128
     flip = mode.startswith("dgrad")
     x, w, bias, wd, U = _setup(B, H, Cin, Cout, flip, seed=7)
     gen = torch.Generator().manual_seed(3)
@@ -127,7 +131,8 @@ def test_wino_epilogues_match_direct(mode):
         assert torch.equal(got, yw > 0)
 
 
-def test_wino_gradient_cone_box():
+@pytest.mark.parametrize("WINO", WINO_TILES)
+def test_wino_gradient_cone_box(WINO):
     """A boxed launch (gbox) writes exactly the box and matches the full launch there."""
     nat = pkg_mod("_native")
     B, H, Cin, Cout = 2, 38, 64, 64
@@ -151,10 +156,11 @@ def test_wino_gradient_cone_box():
     assert torch.isnan(bx[~inside]).all()
 
 
-def test_wino_refuses_what_it_cannot_run():
+@pytest.mark.parametrize("WINO", WINO_TILES)
+def test_wino_refuses_what_it_cannot_run(WINO):
     import ctypes as C
     nat = pkg_mod("_native")
-    B, H, Cin, Cout = 1, 8, 32, 32
+    B, H, Cin, Cout = 1, 8, 32, 64
     x, w, bias, wd, U = _setup(B, H, Cin, Cout, False, seed=9)
     xd = x.permute(0, 2, 3, 1).contiguous().to(DEV)
     y = torch.zeros(B, H, H, Cout, device=DEV)

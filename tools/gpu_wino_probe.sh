@@ -1,9 +1,9 @@
 set -o pipefail
-mkdir -p gpurun_out/w1
-timeout -k 10 300 python3 -u -m pytest tests/test_gpu_wino.py -x -v -s --timeout 200 --timeout-method thread > gpurun_out/w1/wino.log 2>&1
+mkdir -p gpurun_out/w3
+timeout -k 10 300 python3 -u -m pytest tests/test_gpu_wino.py -x -q --timeout 200 --timeout-method thread > gpurun_out/w3/wino.log 2>&1
 rc=$?
-grep -E "winograd|passed|failed|Error" gpurun_out/w1/wino.log | tail -30
+tail -3 gpurun_out/w3/wino.log
 [ $rc -eq 0 ] || exit $rc
-timeout -k 10 600 python3 -u bench.py --prec fp32 --no-cpu-baseline > gpurun_out/w1/bench.json 2> gpurun_out/w1/bench.err || { tail -20 gpurun_out/w1/bench.err; exit 1; }
-python3 -c "import json;d=json.loads(open('gpurun_out/w1/bench.json').read().strip().splitlines()[-1]);print('fp32', d['value'], d['roofline']['conv_ms_per_step'], d['roofline']['frac'])"
-mkdir -p gpurun_out/w1/tiles && cp adversarial_patch-based_false_positive_creation_attacks_against_aerial_imagery_object_detectors_amd/tiles/*.json gpurun_out/w1/tiles/
+for shp in "16 38 512 256" "16 76 256 128" "16 19 1024 512" "16 76 128 256" "16 152 128 64"; do
+  echo -n "62: "; MICRO_TILE=62 timeout -k 5 60 python3 tools/conv_micro.py $shp 3 1 20 2>&1 | tail -1
+done
