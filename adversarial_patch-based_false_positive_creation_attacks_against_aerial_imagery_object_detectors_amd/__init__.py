@@ -11,7 +11,8 @@ include/advpatch.h); see DESIGN.md.
 import importlib
 import sys
 
-DROPIN_MODULES = ("cfg", "median_pool", "load_data", "darknet_v3", "patch_config", "train_patch")
+DROPIN_MODULES = ("cfg", "median_pool", "load_data", "darknet_v3", "patch_config", "train_patch", "utils",
+                  "utils_self")
 
 
 def install_dropin():

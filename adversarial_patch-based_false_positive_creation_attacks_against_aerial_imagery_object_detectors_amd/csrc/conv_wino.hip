@@ -300,7 +300,15 @@ __device__ __forceinline__ void lds_dma16(__amdgpu_buffer_rsrc_t rs, float* lds,
 typedef float f2v __attribute__((ext_vector_type(2)));       // packed pairs: v_pk_add_f32
 __device__ __forceinline__ int v2idx(int xi, int t, int ch) { return ((xi * T2 + t) * WK) + ((ch ^ ((t >> 2) & 3)) << 2); }
 
-__global__ __launch_bounds__(256) void conv_wino2_k(const ConvArgs a, const float* __restrict__ U, int Ht, int Wt) {
+// NW = 4 waves (wave w owns components 4w..4w+3, a thread transforms a
+// channel pair) or NW = 8 waves (two waves per SIMD for latency hiding; wave
+// w owns components 2w, 2w+1, a thread transforms one channel).
+template <int NW>
+__global__ __launch_bounds__(64 * NW) void conv_wino2_k(const ConvArgs a, const float* __restrict__ U, int Ht, int Wt) {
+  constexpr int NT = 64 * NW;            // threads
+  constexpr int CPW = 16 / NW;           // components per wave
+  constexpr int DPW = 32 / NW;           // DMA instructions per wave per k-step (16 pixels x 2 tile halves)
+  constexpr int CPT = 16 * T2 / NT;      // channels per thread in the transform (2 or 1)
   __shared__ __attribute__((aligned(16))) float smem[16 * T2 * M2_ROW];     // 144 KB (k-loop: 2R + 2V = 128 KB)
   __shared__ int s_live;
   float* R = smem;                       // [2][16 p][T2][WK]
@@ -308,7 +316,7 @@ __global__ __launch_bounds__(256) void conv_wino2_k(const ConvArgs a, const floa
   const int wgid = po::xcd_remap();
   const int tn = wgid % a.ntiles_n, tm = wgid / a.ntiles_n;
   const int m0 = tm * T2, n0 = tn * N2;
-  const int tid = threadIdx.x & 255, lane = tid & 63, wave = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wave_u = __builtin_amdgcn_readfirstlane(wave);
   const int h = lane >> 5;
 
@@ -321,73 +329,95 @@ __global__ __launch_bounds__(256) void conv_wino2_k(const ConvArgs a, const floa
   __syncthreads();
   if (!s_live) return;
 
-  // ---- DMA source offsets: wave w loads patch row u = w (pixels p = 4w + v)
-  // for both 16-tile halves; lane L -> tile 16*half + (L >> 2), chunk L & 3
+  // ---- DMA source offsets: instruction j of wave w loads pixel p of one
+  // 16-tile half: (p, half) = ((w*DPW + j) >> 1, (w*DPW + j) & 1); lane L ->
+  // tile 16*half + (L >> 2), 16-byte chunk L & 3
   const uint32_t in_bytes = (uint32_t)__builtin_amdgcn_readfirstlane(a.in_bytes);
   const __amdgpu_buffer_rsrc_t in_rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(a.in), 0, in_bytes, 0x00020000);
   const uint32_t pix_bytes = (uint32_t)a.Cin_p * 4u;
-  uint32_t doff[2][4];
+  uint32_t doff[DPW];
 #pragma unroll
-  for (int half = 0; half < 2; ++half) {
+  for (int j = 0; j < DPW; ++j) {
+    const int idx = wave_u * DPW + j, p = idx >> 1, half = idx & 1;
     int b, ti, tj;
     const bool ok_t = tile_point(a, Ht, Wt, m0 + 16 * half + (lane >> 2), b, ti, tj);
-#pragma unroll
-    for (int v = 0; v < 4; ++v) {
-      const int y = 2 * ti - 1 + wave_u, x = 2 * tj - 1 + v;
-      const bool ok = ok_t && (unsigned)y < (unsigned)a.Hin && (unsigned)x < (unsigned)a.Win;
-      doff[half][v] = ok ? (((uint32_t)b * a.Hin + y) * a.Win + x) * pix_bytes + 16u * (lane & 3) : kOOB;
-    }
+    const int y = 2 * ti - 1 + (p >> 2), x = 2 * tj - 1 + (p & 3);
+    const bool ok = ok_t && (unsigned)y < (unsigned)a.Hin && (unsigned)x < (unsigned)a.Win;
+    doff[j] = ok ? (((uint32_t)b * a.Hin + y) * a.Win + x) * pix_bytes + 16u * (lane & 3) : kOOB;
   }
   auto dma = [&](int ks, float* Rb) {
     const uint32_t cb = (uint32_t)__builtin_amdgcn_readfirstlane(ks * (WK * 4));
 #pragma unroll
-    for (int v = 0; v < 4; ++v)
-#pragma unroll
-      for (int half = 0; half < 2; ++half) lds_dma16(in_rs, Rb + ((wave_u * 4 + v) * T2 + 16 * half) * WK, doff[half][v], cb);
-  };
-  // ---- transform: thread -> tile r, channel pair qq (a half-wave covers 4
-  // tiles x 8 pairs: conflict-free 8-byte LDS reads and writes)
-  const int qq = lane & 7, r = wave * 8 + (lane >> 3);
-  auto transform = [&](const float* Rb, float* Vb) {
-    f2v d[16];
-#pragma unroll
-    for (int p = 0; p < 16; ++p) d[p] = *reinterpret_cast<const f2v*>(Rb + (p * T2 + r) * WK + 2 * qq);
-    f2v t[4][4];
-#pragma unroll
-    for (int v = 0; v < 4; ++v) {
-      const f2v d0 = d[v], d1 = d[4 + v], d2 = d[8 + v], d3 = d[12 + v];
-      t[0][v] = d0 - d2;
-      t[1][v] = d1 + d2;
-      t[2][v] = d2 - d1;
-      t[3][v] = d1 - d3;
+    for (int j = 0; j < DPW; ++j) {
+      const int idx = wave_u * DPW + j;
+      lds_dma16(in_rs, Rb + ((idx >> 1) * T2 + 16 * (idx & 1)) * WK, doff[j], cb);
     }
-    const int sub = (qq & 1) * 2;
+  };
+  // ---- transform: a half-wave covers 4 tiles (conflict-free LDS access)
+  const int tc = (CPT == 2) ? (lane & 7) : (lane & 15);                 // channel pair / channel
+  const int r = (CPT == 2) ? wave * 8 + (lane >> 3) : wave * 4 + (lane >> 4);
+  auto transform = [&](const float* Rb, float* Vb) {
+    if constexpr (CPT == 2) {
+      f2v d[16];
 #pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      const f2v e[4] = {t[u][0] - t[u][2], t[u][1] + t[u][2], t[u][2] - t[u][1], t[u][1] - t[u][3]};
+      for (int p = 0; p < 16; ++p) d[p] = *reinterpret_cast<const f2v*>(Rb + (p * T2 + r) * WK + 2 * tc);
+      f2v t[4][4];
 #pragma unroll
-      for (int v = 0; v < 4; ++v) *reinterpret_cast<f2v*>(Vb + v2idx(u * 4 + v, r, qq >> 1) + sub) = e[v];
+      for (int v = 0; v < 4; ++v) {
+        const f2v d0 = d[v], d1 = d[4 + v], d2 = d[8 + v], d3 = d[12 + v];
+        t[0][v] = d0 - d2;
+        t[1][v] = d1 + d2;
+        t[2][v] = d2 - d1;
+        t[3][v] = d1 - d3;
+      }
+      const int sub = (tc & 1) * 2;
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const f2v e[4] = {t[u][0] - t[u][2], t[u][1] + t[u][2], t[u][2] - t[u][1], t[u][1] - t[u][3]};
+#pragma unroll
+        for (int v = 0; v < 4; ++v) *reinterpret_cast<f2v*>(Vb + v2idx(u * 4 + v, r, tc >> 1) + sub) = e[v];
+      }
+    } else {
+      float d[16];
+#pragma unroll
+      for (int p = 0; p < 16; ++p) d[p] = Rb[(p * T2 + r) * WK + tc];
+      float t[4][4];
+#pragma unroll
+      for (int v = 0; v < 4; ++v) {
+        const float d0 = d[v], d1 = d[4 + v], d2 = d[8 + v], d3 = d[12 + v];
+        t[0][v] = d0 - d2;
+        t[1][v] = d1 + d2;
+        t[2][v] = d2 - d1;
+        t[3][v] = d1 - d3;
+      }
+      const int sub = tc & 3;
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const float e[4] = {t[u][0] - t[u][2], t[u][1] + t[u][2], t[u][2] - t[u][1], t[u][1] - t[u][3]};
+#pragma unroll
+        for (int v = 0; v < 4; ++v) Vb[v2idx(u * 4 + v, r, tc >> 2) + sub] = e[v];
+      }
     }
   };
 
   // ---- B operand
   const int kc_n = a.Cin_p / WK;
   const float* Ub = U + (size_t)lane * 4;
-  float4 bc[4][2][2], bn[4][2][2];
-  auto bload = [&](float4 (&dst)[4][2][2], int ks) {
+  float4 bc[CPW][2][2], bn[CPW][2][2];
+  auto bload = [&](float4 (&dst)[CPW][2][2], int ks) {
 #pragma unroll
-    for (int c = 0; c < 4; ++c)
+    for (int c = 0; c < CPW; ++c)
 #pragma unroll
       for (int nb = 0; nb < 2; ++nb) {
-        const float* p = Ub + ((((size_t)(2 * tn + nb) * kc_n + ks) * 16 + wave_u * 4 + c) * 512);
+        const float* p = Ub + ((((size_t)(2 * tn + nb) * kc_n + ks) * 16 + wave_u * CPW + c) * 512);
         dst[c][nb][0] = *reinterpret_cast<const float4*>(p);
         dst[c][nb][1] = *reinterpret_cast<const float4*>(p + 256);
       }
   };
 
-  floatx16 acc[4][2];
+  floatx16 acc[CPW][2];
 #pragma unroll
-  for (int c = 0; c < 4; ++c)
+  for (int c = 0; c < CPW; ++c)
 #pragma unroll
     for (int nb = 0; nb < 2; ++nb)
 #pragma unroll
@@ -399,15 +429,14 @@ __global__ __launch_bounds__(256) void conv_wino2_k(const ConvArgs a, const floa
   __syncthreads();                         // raw(0), raw(1) landed
   transform(R, V);
   __syncthreads();
-  // one k-step on V[buf] with B fragments bcur, prefetching step ks+1 into bnxt
-  auto kstep = [&](int ks, float4 (&bcur)[4][2][2], float4 (&bnxt)[4][2][2]) {
+  auto kstep = [&](int ks, float4 (&bcur)[CPW][2][2], float4 (&bnxt)[CPW][2][2]) {
     const int buf = ks & 1;
     if (ks + 2 < kc_n) dma(ks + 2, R + buf * R2_FLOATS);
     if (ks + 1 < kc_n) bload(bnxt, ks + 1);
     const float* Vb = V + buf * V2_FLOATS;
 #pragma unroll
-    for (int c = 0; c < 4; ++c) {
-      const int xi = wave_u * 4 + c;
+    for (int c = 0; c < CPW; ++c) {
+      const int xi = wave_u * CPW + c;
       const int t = lane & 31;
       const float4 a0 = *reinterpret_cast<const float4*>(Vb + v2idx(xi, t, 2 * h));
       const float4 a1 = *reinterpret_cast<const float4*>(Vb + v2idx(xi, t, 2 * h + 1));
@@ -432,21 +461,21 @@ __global__ __launch_bounds__(256) void conv_wino2_k(const ConvArgs a, const floa
   // ---- epilogue: M[xi][tile][64 ch] (rows padded), then A^T M A per (tile, channel)
   float* M = smem;
 #pragma unroll
-  for (int c = 0; c < 4; ++c)
+  for (int c = 0; c < CPW; ++c)
 #pragma unroll
     for (int nb = 0; nb < 2; ++nb)
 #pragma unroll
       for (int e = 0; e < 16; ++e) {
         const int t = (e & 3) + 8 * (e >> 2) + 4 * h;
-        M[((wave * 4 + c) * T2 + t) * M2_ROW + nb * 32 + (lane & 31)] = acc[c][nb][e];
+        M[((wave * CPW + c) * T2 + t) * M2_ROW + nb * 32 + (lane & 31)] = acc[c][nb][e];
       }
   __syncthreads();
   EpiMax mx;
   const int n = n0 + lane;
   const int wpp = a.Cout_p >> 5;
 #pragma unroll 1
-  for (int it = 0; it < T2 / 4; ++it) {
-    const int t = wave + 4 * it;
+  for (int it = 0; it < T2 / NW; ++it) {
+    const int t = wave + NW * it;
     int bb, tti, ttj;
     const bool tl = tile_point(a, Ht, Wt, m0 + t, bb, tti, ttj);
     float m[16];
@@ -489,7 +518,7 @@ namespace po {
 // correlation over the full 3x3 neighbourhood on full maps (no windows, no
 // split-K, destination = source grid) with N % 32 == 0, Cin_p % 16 == 0 and
 // the transformed weights (po_conv_desc.Wwino).
-int launch_wino(const ConvArgs& a, const float* U, hipStream_t st, int bm) {
+int launch_wino(const ConvArgs& a, const float* U, hipStream_t st, int bm, int waves) {
   PO_REQUIRE(U, "po_conv: Winograd tile needs the transformed weights (Wwino)");
   PO_REQUIRE(a.prec == 0 && a.ntaps == 9 && a.tkw == 3 && (a.sdh == 1 || a.sdh == -1) && (a.sdw == 1 || a.sdw == -1) &&
                  a.dh0 == -a.sdh && a.dw0 == -a.sdw,
@@ -503,11 +532,14 @@ int launch_wino(const ConvArgs& a, const float* U, hipStream_t st, int bm) {
   const int Ht = (a.Hout + 1) / 2, Wt = (a.Wout + 1) / 2;
   PO_REQUIRE((int64_t)a.B * Ht * Wt < (1LL << 31), "po_conv: too many tiles");
   if (bm == T2) {
-    PO_REQUIRE(a.N % N2 == 0, "po_conv: Winograd tile 62 needs N %% 64 == 0");
+    PO_REQUIRE(a.N % N2 == 0, "po_conv: Winograd tiles 62/63 need N %% 64 == 0");
     ConvArgs b = a;
     b.ntiles_n = a.N / N2;
     const int ntm = ceil_div((int64_t)a.B * Ht * Wt, T2);
-    hipLaunchKernelGGL(conv_wino2_k, dim3(ntm * b.ntiles_n), dim3(256), 0, st, b, U, Ht, Wt);
+    if (waves == 8)
+      hipLaunchKernelGGL(conv_wino2_k<8>, dim3(ntm * b.ntiles_n), dim3(512), 0, st, b, U, Ht, Wt);
+    else
+      hipLaunchKernelGGL(conv_wino2_k<4>, dim3(ntm * b.ntiles_n), dim3(256), 0, st, b, U, Ht, Wt);
     return check_launch("po_conv (winograd 32x64)");
   }
   ConvArgs b = a;

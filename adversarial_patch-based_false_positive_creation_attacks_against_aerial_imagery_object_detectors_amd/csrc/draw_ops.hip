@@ -37,8 +37,12 @@ __device__ __forceinline__ u4 philox4x32_10(u4 c, uint32_t k0, uint32_t k1) {
 }
 
 __device__ __forceinline__ float unif(uint32_t x) { return (float)(x >> 8) * 0x1p-24f; }
-// from + u * span, rounded as two separate fp32 operations (no fma)
-__device__ __forceinline__ float affine(float u, float span, float from) { return __fadd_rn(__fmul_rn(u, span), from); }
+// from + u * span for fp32 u, span, from: the product is exact in float64
+// (24 + 24 bits), so the float64 sum is rounded once and then to fp32 — the
+// same bits whether or not the compiler fuses the multiply-add
+__device__ __forceinline__ float affine(float u, float span, float from) {
+  return (float)((double)u * (double)span + (double)from);
+}
 
 constexpr float kPi = 3.14159265358979323846f;
 

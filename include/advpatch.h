@@ -192,6 +192,32 @@ int po_cell_windows(const float* center, int B, int S, int nheads, const int* hw
 int po_grad_boxes(const int32_t* roi, int B, int S, const int32_t* prog, int nprog, int nbox, int32_t* boxes,
                   po_stream_t s);
 
+/* ---------------- patch evaluation (reference utils.py:93-245, 450-519) ---------------- */
+
+/* get_region_boxes (utils.py:125-245) for one YOLO head, NCHW [B, A*(5+C), h, w]:
+ * candidates enumerated per image in the reference's loop order (cy, cx,
+ * anchor i); a candidate is kept when conf = sigmoid(obj) * max_c sigmoid(cls_c)
+ * (only_objectness: sigmoid(obj)) > conf_thresh, as the 8-float record
+ *   {cx, cy, w, h, det_conf, cls_max_conf, cls_max_id, 0}
+ * with cx = (sigmoid(tx) + x) * stride_w, w = (exp(tw) * anchor_w) * stride_w
+ * (anchors_scaled = HOST [A][2] fp32 anchor / stride), divided by norm_w /
+ * norm_h unless 1 (do_detect's normalisation, utils.py:511-515).  Records are
+ * appended in order at boxes[b][counts[b] ...] and counts[b] advanced (so the
+ * heads of do_detect append one after another); records past `cap` are
+ * dropped and *overflow is set to 1. */
+int po_region_boxes(const float* head, int B, int A, int C, int h, int w, const float* anchors_scaled,
+                    float stride_w, float stride_h, float norm_w, float norm_h, float conf_thresh,
+                    int only_objectness, int cap, float* boxes, int32_t* counts, int32_t* overflow, po_stream_t s);
+/* nms (utils.py:93-112) per image over boxes[b][0 .. min(counts[b], cap)):
+ * sort by fp32(1 - det_conf) ascending (ties: record index), then keep a box
+ * unless a kept box before it has bbox_iou (centre form, fp32, utils.py:37-57)
+ * > nms_thresh with it, and only if det_conf > 0.  keep [B][cap] = record
+ * indices in kept order, nkeep [B].  nmax >= every counts[b] (<= cap, <= 65536);
+ * workspaces keys / mask sized by po_nms_workspace. */
+int po_nms(const float* boxes, const int32_t* counts, int B, int cap, int nmax, float nms_thresh, uint64_t* keys,
+           uint64_t* mask, int32_t* keep, int32_t* nkeep, po_stream_t s);
+int po_nms_workspace(int B, int nmax, int64_t* key_words, int64_t* mask_words);
+
 /* ---------------- network ops (reference darknet_v3.py:37-100, 195-220) ---------------- */
 
 /* Tap list of an implicit-GEMM convolution launch.  For output pixel (b,i,j)
@@ -272,7 +298,7 @@ typedef struct po_conv_desc {
   const float* Wwino;
 } po_conv_desc;
 
-#define PO_CONV_NTILES 62
+#define PO_CONV_NTILES 63
 /* Tile `t` (1-based): block rows BM (output pixels), block columns BN (output
  * channels), k-step BK (input channels).  Tiles 1..10 stage operands through
  * registers, 11..20 are the same shapes staged by LDS-DMA, 21..28 are
@@ -282,11 +308,11 @@ typedef struct po_conv_desc {
  * 3x3 convs (53..54); 55..56 are the 2-D tile halo kernel (8 x 16 output
  * pixels per tile) for 3x3 convs of input step 1 or 2 on full maps without
  * split-K or boxes; 57..60 the same 2-D tiles (and 16 x 16-pixel ones at input
- * step 1) reading the weights as MFMA fragments from Wfrag.  61 and 62 are the
- * exact-fp32 Winograd F(2x2,3x3) kernels (64 2x2-tiles x 32 channels, and 32
- * tiles x 64 channels with LDS-DMA input; 16 input channels per k-step) for
- * stride-1 3x3 convs and their input gradients on full maps, without split-K
- * (needs Wwino; 62 needs N % 64 == 0).  A tile that does not apply to a launch makes po_conv
+ * step 1) reading the weights as MFMA fragments from Wfrag.  61..63 are the
+ * exact-fp32 Winograd F(2x2,3x3) kernels (64 2x2-tiles x 32 channels; 32
+ * tiles x 64 channels with LDS-DMA input, 4 or 8 waves; 16 input channels per
+ * k-step) for stride-1 3x3 convs and their input gradients on full maps,
+ * without split-K (needs Wwino; 62 and 63 need N % 64 == 0).  A tile that does not apply to a launch makes po_conv
  * return PO_EINVAL.  Returns PO_EINVAL for a bad index. */
 int po_conv_tile_info(int t, int* bm, int* bn, int* bk, int* prec);
 

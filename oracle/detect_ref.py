@@ -60,22 +60,38 @@ def bbox_iou(box1, box2, x1y1x2y2=True):                               # utils.p
 
 def nms(boxes, nms_thresh):                                              # utils.py:93-112
     """Greedy NMS over boxes [x,y,w,h,det_conf,...] (0-dim fp32 tensors);
-    suppressed boxes get det_conf = 0 in place, as in the reference."""
+    suppressed boxes get det_conf = 0 in place, as in the reference.  The
+    inner loop over j (utils.py:107-110) is evaluated as one fp32 vector
+    expression per kept box: the same elementwise operations in the same
+    order as bbox_iou(x1y1x2y2=False) on 0-dim tensors."""
     if len(boxes) == 0:
         return boxes
-    det_confs = torch.zeros(len(boxes))
-    for i in range(len(boxes)):
+    n = len(boxes)
+    det_confs = torch.zeros(n)
+    for i in range(n):
         det_confs[i] = 1 - boxes[i][4]
     _, sortIds = torch.sort(det_confs, stable=True)
+    sb = torch.stack([torch.stack([torch.as_tensor(boxes[k][q], dtype=torch.float32) for q in range(5)])
+                      for k in sortIds.tolist()])                   # [n,5] in sorted order
+    alive = sb[:, 4].clone()
     out_boxes = []
-    for i in range(len(boxes)):
-        box_i = boxes[sortIds[i]]
-        if box_i[4] > 0:
-            out_boxes.append(box_i)
-            for j in range(i + 1, len(boxes)):
-                box_j = boxes[sortIds[j]]
-                if bbox_iou(box_i, box_j, x1y1x2y2=False) > nms_thresh:
-                    box_j[4] = 0
+    for i in range(n):
+        if alive[i] > 0:
+            out_boxes.append(boxes[sortIds[i]])
+            b1, b2 = sb[i], sb[i + 1:]
+            mx = torch.minimum(b1[0] - b1[2] / 2.0, b2[:, 0] - b2[:, 2] / 2.0)
+            Mx = torch.maximum(b1[0] + b1[2] / 2.0, b2[:, 0] + b2[:, 2] / 2.0)
+            my = torch.minimum(b1[1] - b1[3] / 2.0, b2[:, 1] - b2[:, 3] / 2.0)
+            My = torch.maximum(b1[1] + b1[3] / 2.0, b2[:, 1] + b2[:, 3] / 2.0)
+            cw = b1[2] + b2[:, 2] - (Mx - mx)
+            ch = b1[3] + b2[:, 3] - (My - my)
+            carea = cw * ch
+            iou = carea / (b1[2] * b1[3] + b2[:, 2] * b2[:, 3] - carea)
+            hit = (cw > 0) & (ch > 0) & (iou > nms_thresh)
+            alive[i + 1:][hit] = 0
+    for s_, k in enumerate(sortIds.tolist()):
+        if alive[s_] == 0 and not (float(boxes[k][4]) == 0):
+            boxes[k][4] = 0
     return out_boxes
 
 

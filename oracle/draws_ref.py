@@ -43,8 +43,9 @@ def _unif(x):
 
 
 def _affine(u, span, frm):
-    # fp32: u * span rounded, then + from rounded (po_draws: no fma)
-    return (u * np.float32(span)).astype(np.float32) + np.float32(frm)
+    # po_draws: float64(u) * float64(fp32 span) is exact; + float64(fp32 from)
+    # rounds once in float64, then to fp32
+    return (u.astype(np.float64) * np.float64(np.float32(span)) + np.float64(np.float32(frm))).astype(np.float32)
 
 
 def draws(seed, counter, b0, B, P):
@@ -65,7 +66,7 @@ def draws(seed, counter, b0, B, P):
         "contrast": _affine(_unif(s[0]), 0.4, 0.8),
         "bright": _affine(_unif(s[1]), 0.2, -0.1),
         "noise": noise.reshape(B, 3, P, P).astype(np.float32),
-        "angle": (_unif(s[2]) * (np.float32(2.0) * pi)).astype(np.float32) - pi,
+        "angle": _affine(_unif(s[2]), np.float32(2.0) * pi, -pi),
         "ux": _unif(s[3]),
         "uy": _unif(t[0]),
     }

@@ -54,13 +54,13 @@ def _run(cfg, B, P, tmp_path, objective="ce", seed=0):
     return ref, terms, pg.grad.cpu()
 
 
-def _compare(ref, terms, grad, loss_tol=2e-5, grad_check=True):
+def _compare(ref, terms, grad, loss_tol=2e-5, grad_check=True, obj_tol=2e-5):
     assert int(terms["flags"].item()) == 0
     torch.testing.assert_close(terms["patch_center"].cpu(), ref["patch_center"], rtol=0, atol=0)
     cells = terms["cells"].cpu().tolist()
     assert cells == ref["cells"]                                   # bit-exact cell indices
-    torch.testing.assert_close(terms["obj"].cpu(), ref["obj"], rtol=0, atol=2e-5)
-    torch.testing.assert_close(terms["cls"].cpu(), ref["cls"], rtol=0, atol=2e-5)
+    torch.testing.assert_close(terms["obj"].cpu(), ref["obj"], rtol=0, atol=obj_tol)
+    torch.testing.assert_close(terms["cls"].cpu(), ref["cls"], rtol=0, atol=obj_tol)
     for k in ("loss", "nps_loss", "tv_loss", "no_obj_loss", "no_cls_loss", "colorful_loss"):
         a, b = float(terms[k]), float(ref[k])
         assert abs(a - b) <= loss_tol * max(1.0, abs(b)), (k, a, b)
@@ -86,6 +86,9 @@ def test_step_mini3_objectives(tmp_path, objective):
 # operands carry ~22 bits instead of 24.  A kernel that flips a real
 # branch misses by O(max).
 TIE_TOL = {"fp32": 5e-5, "fp16x3": 1e-4}
+# objectness / class probabilities at the loss cells after 75 layers: two fp32
+# evaluations agree to the forward's 5e-5 (test_gpu_darknet), sigmoid' <= 1/4
+OBJ_TOL_608 = 5e-5
 
 
 def branch_aligned_608(tr, ref_net, B, seed, objective="ce"):
@@ -121,7 +124,7 @@ def test_step_yolov3_dota_608(tmp_path, prec):
     ties asserted; the fp32 oracle's own distance is printed beside."""
     tr, ref_net = _trainer("builtin:yolov3-dota", tmp_path, prec=prec)
     terms, g, ref32, err_hip, err_32 = branch_aligned_608(tr, ref_net, 2, 40)
-    _compare(ref32, terms, g, grad_check=False)
+    _compare(ref32, terms, g, grad_check=False, obj_tol=OBJ_TOL_608)
     print("yolov3 (%s) patch grad vs float64: hip %.3g, fp32 oracle %.3g" % (prec, err_hip, err_32))
     assert err_hip <= 1e-4, (err_hip, err_32)
 
@@ -132,7 +135,7 @@ def test_step_yolov3_targeted(tmp_path):
     yolov3-dota@608, exact fp32 convolutions."""
     tr, ref_net = _trainer("builtin:yolov3-dota", tmp_path, objective="targeted", prec="fp32")
     terms, g, ref32, err_hip, err_32 = branch_aligned_608(tr, ref_net, 3, 140, objective="targeted")
-    _compare(ref32, terms, g, grad_check=False)
+    _compare(ref32, terms, g, grad_check=False, obj_tol=OBJ_TOL_608)
     print("yolov3 targeted patch grad vs float64: hip %.3g, fp32 oracle %.3g" % (err_hip, err_32))
     assert err_hip <= 1e-4, (err_hip, err_32)
 
