@@ -68,7 +68,7 @@ def main():
                     "hbm_GBps": None if hbm is None or ms == 0 else hbm / (ms * 1e-3) / 1e9}
     pdir = os.path.join(ROOT, "profiles", rnd)
     os.makedirs(pdir, exist_ok=True)
-    tag = "%s_b%d" % (cfg, batch)
+    tag = "%s_b%d_%s" % (cfg, batch, prec)
     for f in glob.glob(os.path.join(outdir, "trace", "**", "*kernel_stats.csv"), recursive=True):
         shutil.copy(f, os.path.join(pdir, "kernel_stats_%s.csv" % tag))
     lines = ["# rocprofv3 summary, %s, bench.py --config %s --batch %d (%d identical steps incl. warm-up)" %
@@ -96,7 +96,7 @@ def main():
         fh.write("\n".join(lines) + "\n")
     conv = [table[k] for k in table if k.startswith("conv_") and k.endswith("_k")]
     hb = [t["hbm_bytes_per_step"] for t in conv]
-    with open(os.path.join(ROOT, "profiles", "traffic_%s_%s.json" % (tag, prec)), "w") as fh:
+    with open(os.path.join(ROOT, "profiles", "traffic_%s.json" % tag), "w") as fh:
         json.dump({"round": rnd, "prec": prec,
                    "kernel": "po_conv launches of one step (conv_k / conv_h3*_k tile families + split-K reduce)",
                    "conv_hbm_bytes_per_step": None if None in hb else sum(hb),

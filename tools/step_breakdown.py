@@ -22,7 +22,7 @@ ap.add_argument("--windows", type=int, default=1)
 args = ap.parse_args()
 cfg, S, P, Bdef = bench.CONFIGS[args.config]
 B = args.batch or Bdef
-os.environ.setdefault("ADVPATCH_TUNE_CACHE", os.path.join(ROOT, "weights", "conv_tiles_%s_b%d.json" % (args.config, B)))
+os.environ.setdefault("ADVPATCH_TUNE_CACHE", os.path.join(ge.PKG_DIR, "tiles", "conv_tiles_%s_b%d.json" % (args.config, B)))
 tp, pc, sy, W = ge._pkg("train_patch"), ge._pkg("patch_config"), ge._pkg("synthetic"), ge._pkg("weights")
 dev = torch.device("cuda", 0)
 wpath = pc.synthetic_weights_path(cfg.split(":")[-1])
