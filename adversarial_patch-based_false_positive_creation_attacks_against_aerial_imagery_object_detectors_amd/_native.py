@@ -13,7 +13,7 @@ LIB_PATH = os.path.join(_HERE, "libadvpatch_hip.so")
 
 c_int, c_float, c_int64, c_void_p = ctypes.c_int, ctypes.c_float, ctypes.c_int64, ctypes.c_void_p
 
-PO_ABI_VERSION = 9    # include/advpatch.h
+PO_ABI_VERSION = 10   # include/advpatch.h
 PO_CONV_NTILES = 63   # include/advpatch.h
 PO_AMAX_SUB = 64      # sub-slots per max|x| slot
 
@@ -44,6 +44,14 @@ _SIGS = {
                         c_float, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p],
     "po_nms": [c_void_p, c_void_p, c_int, c_int, c_int, c_float, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p],
     "po_nms_workspace": [c_int, c_int, ctypes.POINTER(c_int64), ctypes.POINTER(c_int64)],
+    "po_place_test_mode": [c_void_p, c_int, c_void_p, c_void_p, c_int, c_int, c_int, c_float, c_void_p, c_void_p,
+                           c_void_p, c_void_p, c_void_p, c_void_p, c_void_p],
+    "po_place_workspace": [c_int, c_int, c_int, ctypes.POINTER(c_int64), ctypes.POINTER(c_int64)],
+    "po_place_free_map": [c_void_p, c_void_p, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p],
+    "po_vanishing_params": [c_void_p, c_int, c_int, c_int, c_int, c_float, c_void_p, c_void_p, c_void_p, c_int,
+                            c_void_p, c_void_p, c_void_p],
+    "po_warp_composite_multi": [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int,
+                                c_int, c_int, c_void_p, c_void_p],
     "po_warp_fwd": [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int,
                     c_int, c_void_p, c_void_p],
     "po_warp_bwd": [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int,

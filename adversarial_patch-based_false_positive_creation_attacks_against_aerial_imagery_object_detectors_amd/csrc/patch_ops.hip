@@ -7,6 +7,7 @@
 // masks route gradients like the reference.
 #pragma clang fp contract(off)
 #include "common.h"
+#include "warp_geom.h"
 #include <math.h>
 #include <string.h>
 
@@ -192,43 +193,15 @@ __global__ __launch_bounds__(64) void patch_params_k(const float* __restrict__ l
   const double tx = (-txd + 0.5) * 2.0;                      // load_data.py:726
   const double ty = (-tyd + 0.5) * 2.0;                      // load_data.py:727
   const double a = do_rotate ? (double)angle[b] : 0.0;
-  const double sn = sin(a), cs = cos(a);
-  const double th[6] = {cs / scale, sn / scale, tx * cs / scale + ty * sn / scale,      // load_data.py:738-743
-                        -sn / scale, cs / scale, -tx * sn / scale + ty * cs / scale};
+  double th[6], af[6];
+  po::placement_theta(a, scale, tx, ty, th);                   // load_data.py:738-743
   float* tho = theta + 6 * b;
   for (int k = 0; k < 6; ++k) tho[k] = (float)th[k];
   if (tsize) tsize[b] = (float)ts;
-  // pixel-space affine of affine_grid + grid_sample (align_corners=False):
-  // ix = A00 j + A01 i + A02, iy = A10 j + A11 i + A12 for output pixel (i, j)
-  const double half = 0.5 - 0.5 * dS;
-  const double A00 = th[0], A01 = th[1], A10 = th[3], A11 = th[4];
-  const double A02 = (th[0] + th[1]) * half + 0.5 * dS * th[2] + 0.5 * (dS - 1.0);
-  const double A12 = (th[3] + th[4]) * half + 0.5 * dS * th[5] + 0.5 * (dS - 1.0);
-  if (affine) {
-    double* af = affine + 6 * b;
-    af[0] = A00; af[1] = A01; af[2] = A02; af[3] = A10; af[4] = A11; af[5] = A12;
-  }
-  if (roi) {
-    // output pixels whose bilinear sample can touch the padded patch region:
-    // preimage of [pad-1, pad+P) x [pad-1, pad+P) under the pixel-space affine
-    const double det = A00 * A11 - A01 * A10;
-    const int padL = (int)((S - P) / 2.0 + 0.5);
-    double jlo = 1e30, jhi = -1e30, ilo = 1e30, ihi = -1e30;
-    for (int k = 0; k < 4; ++k) {
-      const double X = (double)((k & 1) ? padL + P : padL - 1) - A02;
-      const double Y = (double)((k & 2) ? padL + P : padL - 1) - A12;
-      const double jj = (A11 * X - A01 * Y) / det, ii = (-A10 * X + A00 * Y) / det;
-      jlo = fmin(jlo, jj); jhi = fmax(jhi, jj);
-      ilo = fmin(ilo, ii); ihi = fmax(ihi, ii);
-    }
-    const double lo = -4.0, hi = dS + 4.0;      // clamp before the int conversion
-    jlo = fmin(fmax(jlo, lo), hi); jhi = fmin(fmax(jhi, lo), hi);
-    ilo = fmin(fmax(ilo, lo), hi); ihi = fmin(fmax(ihi, lo), hi);
-    roi[4 * b + 0] = max(0, (int)floor(jlo) - 2);
-    roi[4 * b + 1] = max(0, (int)floor(ilo) - 2);
-    roi[4 * b + 2] = min(S, (int)ceil(jhi) + 3);
-    roi[4 * b + 3] = min(S, (int)ceil(ihi) + 3);
-  }
+  po::theta_pixel_affine(th, dS, af);
+  if (affine)
+    for (int k = 0; k < 6; ++k) affine[6 * b + k] = af[k];
+  if (roi) po::footprint_roi(af, S, P, roi + 4 * b);
 }
 }  // namespace
 
@@ -282,6 +255,7 @@ __device__ __forceinline__ float aug_value(const float* __restrict__ mp, const f
 
 // Forward of one output pixel: adv_t[3] (clamped) and msk_t.  Returns false
 // if no neighbour lies inside the padded patch region (output exactly 0).
+template <bool AUG = true>
 __device__ __forceinline__ bool warp_pixel(const double* af, const WarpGeom& g, const float* mp,
                                            const float* nz, float contrast, float bright, int i, int j,
                                            float adv[3], float& msk, bool raw_in_range[3]) {
@@ -301,9 +275,16 @@ __device__ __forceinline__ bool warp_pixel(const double* af, const WarpGeom& g, 
   for (int k = 0; k < 4; ++k) {
     const int pr = cy[k] - g.padT, pc = cx[k] - g.padL;
     if (pr >= 0 && pr < g.P && pc >= 0 && pc < g.P) {
-      a0 += aug_value(mp, nz, contrast, bright, 0, pr, pc, g.P) * w[k];
-      a1 += aug_value(mp, nz, contrast, bright, 1, pr, pc, g.P) * w[k];
-      a2 += aug_value(mp, nz, contrast, bright, 2, pr, pc, g.P) * w[k];
+      if (AUG) {
+        a0 += aug_value(mp, nz, contrast, bright, 0, pr, pc, g.P) * w[k];
+        a1 += aug_value(mp, nz, contrast, bright, 1, pr, pc, g.P) * w[k];
+        a2 += aug_value(mp, nz, contrast, bright, 2, pr, pc, g.P) * w[k];
+      } else {                                // test_real: clamp(patch) only (load_data.py:1070-1076)
+        const size_t o = (size_t)pr * g.P + pc, pp = (size_t)g.P * g.P;
+        a0 += fminf(fmaxf(mp[o], 0.f), 1.f) * w[k];
+        a1 += fminf(fmaxf(mp[o + pp], 0.f), 1.f) * w[k];
+        a2 += fminf(fmaxf(mp[o + 2 * pp], 0.f), 1.f) * w[k];
+      }
       m += 1.f * w[k];
     }
   }
@@ -496,6 +477,49 @@ __global__ __launch_bounds__(256) void warp_bwd_b_k(const float* __restrict__ gf
   }
 }
 
+// L patches per image composited in slot order (PatchApplier, load_data.py:
+// 808-833, over the [B,L,3,S,S] output of PatchTransformer_vanishing): per
+// element the value of the last slot whose clamp(adv)*msk is non-zero, else
+// the image.  Slots are visited last to first and a pixel outside a slot's
+// footprint box skips it; the per-slot value is warp_pixel's, so the result
+// equals L sequential po_warp_fwd + po_apply_fwd passes bit for bit.
+template <bool AUG>
+__global__ __launch_bounds__(256) void warp_multi_k(const float* __restrict__ img, const float* __restrict__ mp,
+                                                    const float* __restrict__ noise,
+                                                    const float* __restrict__ contrast,
+                                                    const float* __restrict__ bright,
+                                                    const double* __restrict__ affine,
+                                                    const int32_t* __restrict__ roi, int L, WarpGeom g,
+                                                    float* __restrict__ out) {
+  const int b = blockIdx.y;
+  const int q = blockIdx.x * 256 + threadIdx.x;
+  if (q >= g.S * g.S) return;
+  const int i = q / g.S, j = q - i * g.S;
+  const size_t plane = (size_t)g.S * g.S;
+  const size_t o = (size_t)b * 3 * plane + q;
+  float v[3] = {0.f, 0.f, 0.f};
+  bool set[3] = {false, false, false};
+  for (int l = L - 1; l >= 0; --l) {
+    const int t = b * L + l;
+    const int32_t* r = roi + 4 * t;
+    if (j < r[0] || j >= r[2] || i < r[1] || i >= r[3]) continue;
+    float adv[3], msk;
+    bool rng[3];
+    const float* nz = AUG ? noise + (size_t)t * 3 * g.P * g.P : nullptr;
+    if (!warp_pixel<AUG>(affine + 6 * t, g, mp, nz, AUG ? contrast[t] : 1.f, AUG ? bright[t] : 0.f, i, j, adv,
+                         msk, rng))
+      continue;
+#pragma unroll
+    for (int ch = 0; ch < 3; ++ch) {
+      const float val = adv[ch] * msk;                  // load_data.py:1227-1230
+      if (!set[ch] && val != 0.f) { v[ch] = val; set[ch] = true; }
+    }
+    if (set[0] && set[1] && set[2]) break;
+  }
+#pragma unroll
+  for (int ch = 0; ch < 3; ++ch) out[o + ch * plane] = set[ch] ? v[ch] : img[o + ch * plane];
+}
+
 WarpGeom make_geom(int S, int P) {
   WarpGeom g;
   g.S = S;
@@ -540,6 +564,23 @@ extern "C" int po_warp_bwd(const float* d_out, const float* patch_mp, const floa
   hipLaunchKernelGGL(warp_bwd_b_k, dim3(po::ceil_div(P * P, WB_EL)), dim3(256), 0, po::stream_of(s),
                      work, patch_mp, noise, contrast, bright, affine, g, B, d_patch_mp);
   return po::check_launch("po_warp_bwd(b)");
+}
+
+extern "C" int po_warp_composite_multi(const float* img, const float* patch_mp, const float* noise,
+                                       const float* contrast, const float* bright, const double* affine,
+                                       const int32_t* roi, int B, int L, int S, int P, float* out, po_stream_t s) {
+  PO_REQUIRE(img && patch_mp && affine && roi && out, "po_warp_composite_multi: null pointer");
+  PO_REQUIRE(!noise || (contrast && bright), "po_warp_composite_multi: noise needs contrast and bright");
+  PO_REQUIRE(B > 0 && L > 0 && S > 1 && P > 0 && P <= S, "po_warp_composite_multi: bad shape B=%d L=%d S=%d P=%d",
+             B, L, S, P);
+  dim3 grid(po::ceil_div((int64_t)S * S, 256), B);
+  if (noise)
+    hipLaunchKernelGGL(warp_multi_k<true>, grid, dim3(256), 0, po::stream_of(s), img, patch_mp, noise, contrast,
+                       bright, affine, roi, L, make_geom(S, P), out);
+  else
+    hipLaunchKernelGGL(warp_multi_k<false>, grid, dim3(256), 0, po::stream_of(s), img, patch_mp, noise, contrast,
+                       bright, affine, roi, L, make_geom(S, P), out);
+  return po::check_launch("po_warp_composite_multi");
 }
 
 // ------------------------------------------------------------------------

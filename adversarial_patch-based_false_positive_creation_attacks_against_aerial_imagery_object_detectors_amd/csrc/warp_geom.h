@@ -1,0 +1,66 @@
+// Float64 placement geometry shared by the training placement (po_patch_params)
+// and the test-time placements (po_place_test_mode, po_vanishing_params).
+// Include after `#pragma clang fp contract(off)`: the expressions are the
+// reference formulas evaluated in float64, operation by operation.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <math.h>
+#include <stdint.h>
+
+namespace po {
+
+// Pixel-space form of affine_grid + grid_sample (align_corners=False) on an
+// S x S output: output pixel (i, j) samples the input at column
+// ix = af0 j + af1 i + af2 and row iy = af3 j + af4 i + af5.
+__device__ __forceinline__ void theta_pixel_affine(const double th[6], double dS, double af[6]) {
+  const double half = 0.5 - 0.5 * dS;
+  af[0] = th[0];
+  af[1] = th[1];
+  af[2] = (th[0] + th[1]) * half + 0.5 * dS * th[2] + 0.5 * (dS - 1.0);
+  af[3] = th[3];
+  af[4] = th[4];
+  af[5] = (th[3] + th[4]) * half + 0.5 * dS * th[5] + 0.5 * (dS - 1.0);
+}
+
+// The single-stage theta of PatchTransformer (load_data.py:733-743) and
+// PatchTransformer_vanishing (1171-1178): rotation by `a`, scale 1/scale,
+// translation (tx, ty) in affine_grid units.
+__device__ __forceinline__ void placement_theta(double a, double scale, double tx, double ty, double th[6]) {
+  const double sn = sin(a), cs = cos(a);
+  th[0] = cs / scale;
+  th[1] = sn / scale;
+  th[2] = tx * cs / scale + ty * sn / scale;
+  th[3] = -sn / scale;
+  th[4] = cs / scale;
+  th[5] = -tx * sn / scale + ty * cs / scale;
+}
+
+// Bounding box {x0, y0, x1, y1} (+2 px margin, clipped to the image) of the
+// output pixels whose bilinear sample can touch the padded patch region
+// [pad-1, pad+P)^2: the preimage of its corners under the pixel-space affine.
+__device__ __forceinline__ void footprint_roi(const double af[6], int S, int P, int32_t* roi) {
+  const double A00 = af[0], A01 = af[1], A02 = af[2], A10 = af[3], A11 = af[4], A12 = af[5];
+  const double det = A00 * A11 - A01 * A10;
+  const int padL = (int)((S - P) / 2.0 + 0.5);
+  double jlo = 1e30, jhi = -1e30, ilo = 1e30, ihi = -1e30;
+  for (int k = 0; k < 4; ++k) {
+    const double X = (double)((k & 1) ? padL + P : padL - 1) - A02;
+    const double Y = (double)((k & 2) ? padL + P : padL - 1) - A12;
+    const double jj = (A11 * X - A01 * Y) / det, ii = (-A10 * X + A00 * Y) / det;
+    jlo = fmin(jlo, jj); jhi = fmax(jhi, jj);
+    ilo = fmin(ilo, ii); ihi = fmax(ihi, ii);
+  }
+  if (!(det != 0.0) || !(jlo <= jhi) || !(ilo <= ihi)) {    // degenerate or non-finite map: empty box
+    roi[0] = roi[1] = roi[2] = roi[3] = 0;
+    return;
+  }
+  const double dS = (double)S, lo = -4.0, hi = dS + 4.0;      // clamp before the int conversion
+  jlo = fmin(fmax(jlo, lo), hi); jhi = fmin(fmax(jhi, lo), hi);
+  ilo = fmin(fmax(ilo, lo), hi); ihi = fmin(fmax(ihi, lo), hi);
+  roi[0] = max(0, (int)floor(jlo) - 2);
+  roi[1] = max(0, (int)floor(ilo) - 2);
+  roi[2] = min(S, (int)ceil(jhi) + 3);
+  roi[3] = min(S, (int)ceil(ihi) + 3);
+}
+
+}  // namespace po

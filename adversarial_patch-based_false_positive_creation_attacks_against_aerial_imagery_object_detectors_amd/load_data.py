@@ -9,6 +9,10 @@ TotalVariation         load_data.py:392-411                        po_regularise
 PatchTransformer       load_data.py:414-794 (training placement)   po_median7_*, po_patch_params,
                                                                    po_warp_fwd / po_warp_bwd
 PatchApplier           load_data.py:797-833                        po_apply_fwd / po_apply_bwd
+PatchTransformer_      load_data.py:985-1230 (one patch per        po_vanishing_params, po_warp_fwd,
+  vanishing            label, evaluation)                          po_warp_composite_multi
+PatchTransformer_      load_data.py:1233-1722 (placement away      po_place_test_mode,
+  test_mode            from the detections, evaluation)            po_place_free_map
 HasSusRGB              load_data.py:1724-1754                      po_regularisers
 DotaDataset            load_data.py:859-978 (host data loader)     (PIL / numpy, no GPU)
 =====================  ==========================================  =========================
@@ -292,6 +296,237 @@ class PatchApplier(nn.Module):
                 img_batch = img_batch.expand_as(adv)
             img_batch = _Apply.apply(img_batch, adv)
         return img_batch
+
+
+# ---------------------------------------------------------------------------
+# Test-time placements (load_data.py:985-1722)
+# ---------------------------------------------------------------------------
+PLACE_FLAG_MASK, PLACE_FLAG_NOFREE, PLACE_FLAG_PICK = 1, 2, 4
+PLACE_INFO = ("flags", "x", "y", "semi_edge2", "M", "n_free", "pick", "mask_ones")
+
+
+def _place_workspace(B, L, S, dev):
+    fw, iw = nat.c_int64(), nat.c_int64()
+    nat.call("po_place_workspace", B, L, S, nat.ctypes.byref(fw), nat.ctypes.byref(iw))
+    return (torch.empty(fw.value, device=dev), torch.empty(iw.value, dtype=torch.int32, device=dev))
+
+
+def _label_rows(lab_batch, nlab, ncols):
+    nat.ensure_device(lab_batch)
+    lab = lab_batch.contiguous().float()
+    if lab.dim() != 3 or lab.size(2) != ncols:
+        raise ValueError("expected labels [B, L, %d], got %s" % (ncols, tuple(lab.shape)))
+    B, L = lab.size(0), lab.size(1)
+    if L < 1:
+        raise RuntimeError("no label rows (the reference's torch.max over an empty label set fails)")
+    if nlab is None:
+        nlab = torch.full((B,), L, dtype=torch.int32, device=lab.device)
+    else:
+        nlab = torch.as_tensor(nlab, dtype=torch.int32).to(lab.device)
+    return lab, nlab
+
+
+def place_test_mode(mp, lab_batch, img_size, angle, upick, nlab=None, scale_factor=SCALE_FACTOR):
+    """po_place_test_mode: median-pooled patch [3,P,P], labels [B,L,7] (the
+    first nlab[b] rows used; all L by default), angle / upick [B] ->
+    (out [B,3,S,S], info [B,8] int32 with the PLACE_INFO fields)."""
+    nat.ensure_device(mp)
+    lab, nlab = _label_rows(lab_batch, nlab, 7)
+    B, L, S, P = lab.size(0), lab.size(1), int(img_size), mp.size(-1)
+    dev = lab.device
+    fw, iw = _place_workspace(B, L, S, dev)
+    out = torch.empty(B, 3, S, S, device=dev)
+    info = torch.empty(B, 8, dtype=torch.int32, device=dev)
+    nat.call("po_place_test_mode", nat.ptr(mp.contiguous()), P, nat.ptr(lab), nat.ptr(nlab, torch.int32), B, L, S,
+             float(scale_factor), nat.ptr(None if angle is None else angle.contiguous().float()),
+             nat.ptr(upick.contiguous().float()), nat.ptr(fw), nat.ptr(iw, torch.int32), nat.ptr(out),
+             nat.ptr(info, torch.int32), nat.stream())
+    return out, info
+
+
+def check_place_info(info):
+    """Raise as the reference does on the conditions po_place_test_mode flags."""
+    for b, row in enumerate(info.cpu().tolist()):
+        f = row[0]
+        if f & PLACE_FLAG_MASK:
+            raise RuntimeError("image %d: fewer than two mask==1 pixels after scale/rotate (the reference fails in "
+                               "torch.min / the squeeze, load_data.py:1655-1662)" % b)
+        if f & PLACE_FLAG_NOFREE:
+            raise IndexError("image %d: no free position (position_available is empty, load_data.py:1684)" % b)
+        if f & PLACE_FLAG_PICK:
+            raise IndexError("image %d: random.randint(0, %d) drew %d == len(position_available) "
+                             "(load_data.py:1682-1684)" % (b, row[5], row[6]))
+
+
+class PatchTransformer_test_mode(nn.Module):
+    """Test-time placement that avoids the detections (load_data.py:1233-1722):
+    scale from the (max-area + min-area)/2 detection, rotation (U(-pi/2, pi/2)
+    with test_mode=True, else U(-pi, pi)), the inter_axis_cal occupancy map,
+    a random free position, translation there.  The contrast/brightness/noise
+    the reference draws are not applied (1464-1490), so they are not drawn.
+
+    lab_batch [B, n, 7] rows {x, y, w, h, obj_conf, cls_conf, id} (the
+    0.01-threshold detections, 1295-1297); the reference runs B = 1.  Every
+    image uses all n rows unless ``nlab`` [B] gives per-image counts.
+    Randomness: ``draws`` = {"angle": [B], "upick": [B]} or the on-device
+    counter-based draws (po_draws, seed ``draw_seed``, counter ``draw_step``).
+    """
+
+    def __init__(self, test_mode=False):
+        super().__init__()
+        self.min_contrast = 0.8
+        self.max_contrast = 1.2
+        self.min_brightness = -0.1
+        self.max_brightness = 0.1
+        self.noise_factor = NOISE_FACTOR
+        self.minangle = -180 / 180 * math.pi
+        self.maxangle = 180 / 180 * math.pi
+        if test_mode:                                     # load_data.py:1254-1259
+            self.maxangle = 90 / 180 * math.pi
+            self.minangle = -90 / 180 * math.pi
+        self.test_mode = bool(test_mode)
+        self.medianpooler = MedianPool2d(7, same=True)
+        self.draw_seed = 5
+        self.draw_step = 0
+        self.last_info = None
+
+    def lab_transform(self, lab_batch_origin):
+        """[B,n,7] -> [B,1,7] (load_data.py:1262-1320): (max-area row +
+        min-area row)/2 over cols 2,3; 0.25 everywhere for a single row or a
+        max area above 0.99."""
+        area = lab_batch_origin[:, :, 2] * lab_batch_origin[:, :, 3]
+        imax, imin = torch.argmax(area, 1), torch.argmin(area, 1)
+        ar = torch.arange(lab_batch_origin.size(0), device=lab_batch_origin.device)
+        sel = (lab_batch_origin[ar, imax, :] + lab_batch_origin[ar, imin, :]) / 2.
+        flat = (area.max(1).values > 0.99) | torch.tensor(lab_batch_origin.size(1) == 1, device=area.device)
+        sel = torch.where(flat[:, None], torch.full_like(sel, 0.25), sel)
+        return sel.unsqueeze(1)
+
+    def inter_axis_cal(self, lab_batch, semi_edge, img_size, nlab=None):
+        """The occupancy map of load_data.py:1322-1430 (po_place_free_map):
+        [S,S] (lab_batch [1,n,7]) or [B,S,S], indexed [x][y] as the
+        reference's; 0 exactly where the reference's map is 0 (its layer
+        counts are not reproduced: only its zeros are read, 1678)."""
+        lab, nlab = _label_rows(lab_batch if lab_batch.dim() == 3 else lab_batch.unsqueeze(0), nlab, 7)
+        B, L, S = lab.size(0), lab.size(1), int(img_size)
+        semi = torch.as_tensor(semi_edge, dtype=torch.float32).reshape(-1).to(lab.device)
+        if semi.numel() == 1 and B > 1:
+            semi = semi.expand(B).contiguous()
+        fw, iw = _place_workspace(B, L, S, lab.device)
+        layout = torch.empty(B, S, S, dtype=torch.int32, device=lab.device)
+        nat.call("po_place_free_map", nat.ptr(lab), nat.ptr(nlab, torch.int32), B, L, S, nat.ptr(semi), nat.ptr(fw),
+                 nat.ptr(iw, torch.int32), nat.ptr(layout, torch.int32), nat.stream())
+        return layout[0] if lab_batch.size(0) == 1 else layout
+
+    def make_draws(self, B, device):
+        d = synthetic.draws_device(self.draw_seed, self.draw_step, 0, B, 1, device, keys=("angle", "ux"))
+        self.draw_step += 1
+        # po_draws' angle is U(-pi, pi); test_mode halves it (exact) to U(-pi/2, pi/2)
+        angle = d["angle"] * 0.5 if self.test_mode else d["angle"]
+        return {"angle": angle, "upick": d["ux"]}
+
+    def forward(self, adv_patch, lab_batch, img_size, do_rotate=True, rand_loc=False, draws=None, nlab=None):
+        """-> adv_patch_mask [B, 1, 3, S, S] (load_data.py:1432-1722).  Raises
+        where the reference raises (see check_place_info); ``rand_loc`` is
+        accepted and unused, as in the reference."""
+        nat.ensure_device(adv_patch)
+        mp = self.medianpooler(adv_patch.unsqueeze(0))[0]                 # load_data.py:1451-1452
+        if draws is None:
+            draws = self.make_draws(lab_batch.size(0), adv_patch.device)
+        angle = draws["angle"] if do_rotate else None
+        out, info = place_test_mode(mp, lab_batch, img_size, angle, draws["upick"], nlab=nlab)
+        self.last_info = info
+        check_place_info(info)
+        return out.unsqueeze(1)
+
+
+class PatchTransformer_vanishing(nn.Module):
+    """One patch per label row (load_data.py:985-1230): contrast/brightness/
+    noise (not with test_real), clamp, rotation U(-pi, pi), size
+    sqrt((w S/8)^2 + (h S/8)^2), centre at the label (+-0.2 w/h with
+    rand_loc, -+w/6 with orient "left"/"right"), single-stage theta, clamp *
+    mask.  lab_batch [B, n, 5] rows {cls, x, y, w, h}.
+
+    ``forward`` returns the reference's [B, n, 3, S, S] (po_vanishing_params
+    + po_warp_fwd over the B*n patches; differentiable in adv_patch);
+    ``forward_composite`` fuses the PatchApplier loop over the n slots
+    (po_warp_composite_multi) without materialising them (evaluation only).
+    Randomness as PatchTransformer (po_draws over the B*n patches)."""
+
+    PRE_SCALE = 8.0                                       # load_data.py:1116
+
+    def __init__(self):
+        super().__init__()
+        self.min_contrast = 0.8
+        self.max_contrast = 1.2
+        self.min_brightness = -0.1
+        self.max_brightness = 0.1
+        self.noise_factor = NOISE_FACTOR
+        self.minangle = -180 / 180 * math.pi
+        self.maxangle = 180 / 180 * math.pi
+        self.medianpooler = MedianPool2d(7, same=True)
+        self.draw_seed = 7
+        self.draw_step = 0
+
+    def make_draws(self, n, P, device):
+        d = synthetic.draws_device(self.draw_seed, self.draw_step, 0, n, P, device)
+        self.draw_step += 1
+        return d
+
+    def _prep(self, adv_patch, lab_batch, img_size, do_rotate, rand_loc, orient, test_real, draws):
+        nat.ensure_device(adv_patch)
+        lab, _ = _label_rows(lab_batch, None, 5)
+        mp = self.medianpooler(adv_patch.unsqueeze(0))[0]                 # load_data.py:1041-1042
+        B, L, S, P = lab.size(0), lab.size(1), int(img_size), mp.size(-1)
+        if draws is None:
+            draws = self.make_draws(B * L, P, adv_patch.device)
+        dev = adv_patch.device
+        if orient not in (None, "left", "right"):
+            orient_code = 0                               # any other value: no shift (load_data.py:1158-1162)
+        else:
+            orient_code = {None: 0, "left": 1, "right": 2}[orient]
+        angle = draws["angle"].contiguous().float() if do_rotate else None
+        offx = offy = None
+        if rand_loc:                                      # U(-0.2, 0.2) from the U[0,1) draws
+            offx = (draws["ux"].double() * 0.4 - 0.2).float().contiguous()
+            offy = (draws["uy"].double() * 0.4 - 0.2).float().contiguous()
+        affine = torch.empty(B * L, 6, dtype=torch.float64, device=dev)
+        roi = torch.empty(B * L, 4, dtype=torch.int32, device=dev)
+        nat.call("po_vanishing_params", nat.ptr(lab), B, L, S, P, float(self.PRE_SCALE), nat.ptr(angle),
+                 nat.ptr(offx), nat.ptr(offy), orient_code, nat.ptr(affine, torch.float64), nat.ptr(roi, torch.int32),
+                 nat.stream())
+        if test_real:                                     # load_data.py:1070-1071: no augmentation
+            aug = None
+        else:
+            aug = (draws["noise"].contiguous().float(), draws["contrast"].contiguous().float(),
+                   draws["bright"].contiguous().float())
+        return mp, aug, affine, roi, (B, L, S, P)
+
+    def forward(self, adv_patch, lab_batch, img_size, do_rotate=True, rand_loc=False, orient=None,
+                test_real=False, draws=None):
+        mp, aug, affine, roi, (B, L, S, P) = self._prep(adv_patch, lab_batch, img_size, do_rotate, rand_loc,
+                                                        orient, test_real, draws)
+        if aug is None:
+            dev = mp.device
+            aug = (torch.zeros(B * L, 3, P, P, device=dev), torch.ones(B * L, device=dev),
+                   torch.zeros(B * L, device=dev))
+        out = _Warp.apply(mp, aug[0], aug[1], aug[2], affine, None, S, 0)
+        return out.view(B, L, 3, S, S)
+
+    def forward_composite(self, adv_patch, lab_batch, img_batch, img_size, do_rotate=True, rand_loc=False,
+                          orient=None, test_real=False, draws=None):
+        """PatchApplier(img_batch, forward(...)) in one pass (no autograd)."""
+        mp, aug, affine, roi, (B, L, S, P) = self._prep(adv_patch, lab_batch, img_size, do_rotate, rand_loc,
+                                                        orient, test_real, draws)
+        img = img_batch.contiguous().float()
+        if tuple(img.shape) != (B, 3, S, S):
+            raise ValueError("img_batch must be [%d,3,%d,%d], got %s" % (B, S, S, tuple(img.shape)))
+        out = torch.empty_like(img)
+        noise, contrast, bright = aug if aug is not None else (None, None, None)
+        nat.call("po_warp_composite_multi", nat.ptr(img), nat.ptr(mp.detach().contiguous()), nat.ptr(noise),
+                 nat.ptr(contrast), nat.ptr(bright), nat.ptr(affine, torch.float64), nat.ptr(roi, torch.int32), B, L,
+                 S, P, nat.ptr(out), nat.stream())
+        return out
 
 
 # ---------------------------------------------------------------------------

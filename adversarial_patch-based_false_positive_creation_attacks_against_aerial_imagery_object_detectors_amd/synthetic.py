@@ -65,16 +65,21 @@ def draws(B, P, seed=3):
     }
 
 
-def draws_device(seed, counter, b0, B, P, device):
+DRAW_KEYS = ("contrast", "bright", "noise", "angle", "ux", "uy")
+
+
+def draws_device(seed, counter, b0, B, P, device, keys=DRAW_KEYS):
     """On-device counter-based draws (po_draws, csrc/draw_ops.hip) for images
     b0 .. b0+B-1 of a global batch at step ``counter``: the rows do not depend
-    on how the global batch is split over ranks."""
+    on how the global batch is split over ranks.  ``keys``: the outputs to
+    make (the others are not drawn)."""
     from . import _native as nat
     dev = torch.device(device)
     f = lambda *shape: torch.empty(*shape, device=dev)
-    d = {"contrast": f(B), "bright": f(B), "noise": f(B, 3, P, P), "angle": f(B), "ux": f(B), "uy": f(B)}
+    shapes = {"noise": (B, 3, P, P)}
+    d = {k: f(*shapes.get(k, (B,))) for k in keys}
     nat.call("po_draws", int(seed) & 0xFFFFFFFFFFFFFFFF, int(counter) & 0xFFFFFFFFFFFFFFFF, int(b0), int(B), int(P),
-             *(nat.ptr(d[k]) for k in ("contrast", "bright", "noise", "angle", "ux", "uy")), nat.stream())
+             *(nat.ptr(d.get(k)) for k in DRAW_KEYS), nat.stream())
     return d
 
 

@@ -33,7 +33,7 @@ typedef void* po_stream_t;
 #define PO_EHIP -2     /* HIP runtime error */
 #define PO_EDEVICE -3  /* device is not gfx950 */
 
-#define PO_ABI_VERSION 9
+#define PO_ABI_VERSION 10
 #define PO_AMAX_SUB 64  /* sub-slots per max|x| slot (see po_conv_desc) */
 
 int po_abi_version(void);
@@ -217,6 +217,66 @@ int po_region_boxes(const float* head, int B, int A, int C, int h, int w, const 
 int po_nms(const float* boxes, const int32_t* counts, int B, int cap, int nmax, float nms_thresh, uint64_t* keys,
            uint64_t* mask, int32_t* keep, int32_t* nkeep, po_stream_t s);
 int po_nms_workspace(int B, int nmax, int64_t* key_words, int64_t* mask_words);
+
+/* ---------------- test-time placement (reference load_data.py:985-1722) ---------------- */
+
+/* PatchTransformer_test_mode.forward (load_data.py:1432-1722) for B images at
+ * once (the reference runs one image; lab_batch [1, n, 7]):
+ *   lab [B, L, 7] fp32 rows {x, y, w, h, obj_conf, cls_conf, id} (normalised),
+ *   nlab [B] (DEVICE int32) rows in use per image (1 <= nlab[b] <= L);
+ *   patch_mp [3,P,P] the median-pooled patch (clamped to [0,1] here; the
+ *   contrast/brightness/noise the reference draws are not applied there);
+ *   angle [B] (DEVICE, radians; NULL = 0), upick [B] (DEVICE, U[0,1)) the
+ *   draw behind random.randint(0, len(position_available)).
+ * Steps: lab_transform (1262-1320: (max-area row + min-area row)/2 over cols
+ * 2,3; 0.25 when nlab == 1 or max area > 0.99); theta1 = rotation + scale
+ * sqrt((w S/sf)^2 + (h S/sf)^2)/P about the centre, warp of the padded patch
+ * and its mask (1617-1635); semi_edge = (max - min)/2 of the rows holding
+ * mask == 1 (1650-1664); inter_axis_cal's occupancy map (1322-1430: border
+ * of int(semi_edge), label boxes grown by semi_edge in area order, the early
+ * exit and its temp_lab[0:i-1] sum, Python slice semantics of the int()
+ * bounds; the map is indexed [x][y]); position = the upick-th free cell in
+ * torch.nonzero order (1678-1687); theta2 = translation to it and a second
+ * bilinear resampling of the warped patch and mask (1689-1706); out =
+ * clamp(adv) * msk (1714-1715).  Sampling geometry in float64, each resampled
+ * value rounded once to fp32; msk == 1 is tested on that fp32 value.
+ *   out [B,3,S,S]; info [B,8] int32 (DEVICE) = {flags, x, y, semi_edge*2,
+ *   M, n_free, pick, rows_eq1}; flags bit 1: fewer than two mask==1 pixels
+ *   (the reference fails in torch.min / the squeeze), 2: no free cell (its
+ *   position_available[0] raises), 4: the pick equals n_free (its randint's
+ *   inclusive bound: IndexError).  Flagged images get a zero output.
+ * Workspace (po_place_workspace): fwork >= 4*B*S*S + 16*B floats (8-byte
+ * aligned), iwork >= B*(S*S + 5*L + 16) int32 (16-byte aligned). */
+int po_place_test_mode(const float* patch_mp, int P, const float* lab, const int32_t* nlab, int B, int L, int S,
+                       float scale_factor, const float* angle, const float* upick, float* fwork, int32_t* iwork,
+                       float* out, int32_t* info, po_stream_t s);
+int po_place_workspace(int B, int L, int S, int64_t* fwords, int64_t* iwords);
+/* inter_axis_cal alone (load_data.py:1322-1430) for a given semi_edge [B]
+ * (DEVICE fp32): layout [B,S,S] int32 indexed [x][y] as the reference's map,
+ * 0 where its returned sum is 0 (the free cells), 1 elsewhere (the layer
+ * count itself is not reproduced; the reference only reads its zeros).
+ * Workspaces as po_place_test_mode. */
+int po_place_free_map(const float* lab, const int32_t* nlab, int B, int L, int S, const float* semi_edge,
+                      float* fwork, int32_t* iwork, int32_t* layout, po_stream_t s);
+
+/* PatchTransformer_vanishing placement (load_data.py:1095-1180): one patch
+ * per label row, lab [B, L, 5] {cls, x, y, w, h}; target size
+ * sqrt((w S/pre)^2 + (h S/pre)^2) (pre_scale 8, 1116-1120), centre (x, y)
+ * (+ w*offx, h*offy with rand_loc, 1131-1147; x -/+ w/6 for orient 1 left /
+ * 2 right, 1158-1162), rotation angle[B*L] (NULL = 0); single-stage theta
+ * (1164-1178).  affine [B*L, 6] float64 pixel-space sampling maps for
+ * po_warp_fwd / po_warp_composite_multi; roi [B*L, 4] footprint boxes. */
+int po_vanishing_params(const float* lab, int B, int L, int S, int P, float pre_scale, const float* angle,
+                        const float* offx, const float* offy, int orient, double* affine, int32_t* roi,
+                        po_stream_t s);
+/* Fused po_warp_fwd (mode 0) of L patches per image + PatchApplier's
+ * sequential composite (load_data.py:808-833): out[b] = img[b] with, per
+ * element, the value of the LAST patch l whose clamp(adv)*msk there is
+ * non-zero.  noise [B*L,3,P,P], contrast/bright [B*L], affine/roi from
+ * po_vanishing_params; noise == NULL: no augmentation (test_real). */
+int po_warp_composite_multi(const float* img, const float* patch_mp, const float* noise, const float* contrast,
+                            const float* bright, const double* affine, const int32_t* roi, int B, int L, int S,
+                            int P, float* out, po_stream_t s);
 
 /* ---------------- network ops (reference darknet_v3.py:37-100, 195-220) ---------------- */
 

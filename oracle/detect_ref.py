@@ -139,8 +139,12 @@ def get_region_boxes(output, conf_thresh, num_classes, anchors, num_anchors, img
                     det_conf = det_confs[ind]
                     conf = det_confs[ind] if only_objectness else det_confs[ind] * cls_max_confs[ind]
                     if conf > conf_thresh:
+                        # 8th element (test-side only): the class ids whose probability is within
+                        # 1e-6 relative of the max -- the device's and the CPU's sigmoid may
+                        # order such near-ties differently by an ulp
+                        near = set(torch.nonzero(cls_confs[ind] >= cls_max_confs[ind] * (1 - 1e-6)).view(-1).tolist())
                         boxes.append([xs[ind], ys[ind], ws[ind], hs[ind], det_conf, cls_max_confs[ind],
-                                      cls_max_ids[ind]])
+                                      cls_max_ids[ind], near])
         all_boxes.append(boxes)
     return all_boxes
 
