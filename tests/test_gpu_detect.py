@@ -117,5 +117,6 @@ def test_detect_batch_end_to_end(tmp_path):
     want = ref.detect_postprocess(heads, 608, 608, ut.get_anchors(None), 15, 0.4, 0.4)
     assert len(boxes) == len(want)
     _assert_boxes_equal(boxes, want, sat_ties=True)
-    us.write_labels(boxes, str(tmp_path / "a.txt"))
-    assert us.txt_len_read(str(tmp_path))[0] == len(boxes)
+    (tmp_path / "labels").mkdir()
+    us.write_labels(boxes, str(tmp_path / "labels" / "a.txt"))
+    assert us.txt_len_read(str(tmp_path / "labels"))[0] == len(boxes)
