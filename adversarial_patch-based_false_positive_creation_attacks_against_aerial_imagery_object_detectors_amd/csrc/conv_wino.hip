@@ -99,6 +99,52 @@ __device__ __forceinline__ float epi_store(const ConvArgs& a, size_t pix, int n,
   return out;
 }
 
+// The epilogue's per-element inputs, loaded ahead: the shortcut operand, the
+// accumulated destination, and the first / second leaky masks (sign-bit word
+// or fp32 mask bits).
+struct EpiIn {
+  float res = 0.f, yold = 0.f;
+  uint32_t m = 0u, m2 = 0u;
+};
+
+__device__ __forceinline__ EpiIn epi_load(const ConvArgs& a, size_t pix, int n) {
+  const size_t o = pix * (size_t)a.Cout_p + n;
+  const size_t wo = pix * (size_t)(a.Cout_p >> 5) + (n >> 5);
+  EpiIn e;
+  if (a.res) e.res = a.res[o];
+  if (a.accumulate) e.yold = a.y[o];
+  if (a.mbits) e.m = a.mbits[wo];
+  else if (a.mask) e.m = __float_as_uint(a.mask[o]);
+  if (a.y2) e.m2 = a.m2bits ? a.m2bits[wo] : __float_as_uint(a.mask2[o]);
+  return e;
+}
+
+// epi_store with the inputs of epi_load (same arithmetic, same order)
+__device__ __forceinline__ float epi_store_in(const ConvArgs& a, size_t pix, int n, float v, const EpiIn& e,
+                                              EpiMax& mx) {
+  const size_t o = pix * (size_t)a.Cout_p + n;
+  float x = v + (a.bias ? a.bias[n] : 0.f);
+  if (a.act) x = po::leaky(x);
+  if (a.accumulate) x += e.yold;
+  float out = x;
+  if (a.mbits) out = x * (((e.m >> (n & 31)) & 1u) ? 1.f : 0.1f);
+  else if (a.mask) out = x * po::leaky_grad(__uint_as_float(e.m));
+  if (a.y) a.y[o] = out;
+  mx.y = fmaxf(mx.y, fabsf(out));
+  if (a.res) {
+    const float sm = x + e.res;
+    a.sum[o] = sm;
+    mx.s = fmaxf(mx.s, fabsf(sm));
+  }
+  if (a.y2) {
+    const float g = a.m2bits ? (((e.m2 >> (n & 31)) & 1u) ? 1.f : 0.1f) : po::leaky_grad(__uint_as_float(e.m2));
+    const float o2 = x * g;
+    a.y2[o] = o2;
+    mx.y2 = fmaxf(mx.y2, fabsf(o2));
+  }
+  return out;
+}
+
 __global__ __launch_bounds__(256) void conv_wino_k(const ConvArgs a, const float* __restrict__ U, int Ht, int Wt) {
   __shared__ __attribute__((aligned(16))) float smem[2 * 16 * WT * WK];     // 128 KB
   __shared__ int s_live;
@@ -303,7 +349,12 @@ __device__ __forceinline__ int v2idx(int xi, int t, int ch) { return ((xi * T2 +
 // NW = 4 waves (wave w owns components 4w..4w+3, a thread transforms a
 // channel pair) or NW = 8 waves (two waves per SIMD for latency hiding; wave
 // w owns components 2w, 2w+1, a thread transforms one channel).
-template <int NW>
+// SCHED (tile 64): the MFMAs of step k and the transform of step k+1 form one
+// basic block (the transform runs unconditionally; on the last step it
+// rewrites a V buffer nobody reads) whose instructions are interleaved by
+// scheduling-group barriers, so the wave keeps the matrix pipe fed while it
+// transforms instead of transforming after its last MFMA.
+template <int NW, bool SCHED = false>
 __global__ __launch_bounds__(64 * NW) void conv_wino2_k(const ConvArgs a, const float* __restrict__ U, int Ht, int Wt) {
   constexpr int NT = 64 * NW;            // threads
   constexpr int CPW = 16 / NW;           // components per wave
@@ -450,7 +501,29 @@ __global__ __launch_bounds__(64 * NW) void conv_wino2_k(const ConvArgs a, const 
           acc[c][nb] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[s8], bv[s8], acc[c][nb], 0, 0, 0);
       }
     }
-    if (ks + 1 < kc_n) transform(R + (buf ^ 1) * R2_FLOATS, V + (buf ^ 1) * V2_FLOATS);
+    if constexpr (SCHED) {
+      transform(R + (buf ^ 1) * R2_FLOATS, V + (buf ^ 1) * V2_FLOATS);
+      // A fragments, then MFMAs paced against the transform's LDS reads,
+      // its VALU arithmetic and its LDS writes
+      __builtin_amdgcn_sched_group_barrier(0x100, 2 * CPW, 0);
+#pragma unroll
+      for (int g = 0; g < 4 * CPW; ++g) {
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+        __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
+      }
+#pragma unroll
+      for (int g = 0; g < 8 * CPW; ++g) {
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+        __builtin_amdgcn_sched_group_barrier(0x002, 4, 0);
+      }
+#pragma unroll
+      for (int g = 0; g < 4 * CPW; ++g) {
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+        __builtin_amdgcn_sched_group_barrier(0x200, 2, 0);
+      }
+    } else if (ks + 1 < kc_n) {
+      transform(R + (buf ^ 1) * R2_FLOATS, V + (buf ^ 1) * V2_FLOATS);
+    }
     __syncthreads();
   };
   for (int ks = 0; ks < kc_n; ks += 2) {    // two steps per trip: the B registers swap roles, no copies
@@ -469,15 +542,34 @@ __global__ __launch_bounds__(64 * NW) void conv_wino2_k(const ConvArgs a, const 
         const int t = (e & 3) + 8 * (e >> 2) + 4 * h;
         M[((wave * CPW + c) * T2 + t) * M2_ROW + nb * 32 + (lane & 31)] = acc[c][nb][e];
       }
-  __syncthreads();
   EpiMax mx;
   const int n = n0 + lane;
   const int wpp = a.Cout_p >> 5;
-#pragma unroll 1
-  for (int it = 0; it < T2 / NW; ++it) {
+  // the wave's tiles and their per-element epilogue inputs, all loads in
+  // flight at once (they overlap the barrier and the M reads below instead of
+  // one dependent round trip per tile)
+  constexpr int IT = T2 / NW;
+  int tb[IT], tti_[IT], ttj_[IT];
+  bool tl_[IT];
+  EpiIn pre[IT][4];
+  const bool pre_any = a.res || a.accumulate || a.mbits || a.mask || a.y2;
+#pragma unroll
+  for (int it = 0; it < IT; ++it) {
+    tl_[it] = tile_point(a, Ht, Wt, m0 + wave + NW * it, tb[it], tti_[it], ttj_[it]);
+    if (pre_any)
+#pragma unroll
+      for (int p = 0; p < 4; ++p) {
+        const int i = 2 * tti_[it] + (p >> 1), j = 2 * ttj_[it] + (p & 1);
+        if (tl_[it] && n < a.N && i < a.Hout && j < a.Wout)
+          pre[it][p] = epi_load(a, ((size_t)tb[it] * a.Hout + i) * a.Wout + j, n);
+      }
+  }
+  __syncthreads();
+#pragma unroll
+  for (int it = 0; it < IT; ++it) {
     const int t = wave + NW * it;
-    int bb, tti, ttj;
-    const bool tl = tile_point(a, Ht, Wt, m0 + t, bb, tti, ttj);
+    const int bb = tb[it], tti = tti_[it], ttj = ttj_[it];
+    const bool tl = tl_[it];
     float m[16];
 #pragma unroll
     for (int xi = 0; xi < 16; ++xi) m[xi] = M[(xi * T2 + t) * M2_ROW + lane];
@@ -499,7 +591,7 @@ __global__ __launch_bounds__(64 * NW) void conv_wino2_k(const ConvArgs a, const 
         const bool ok = tl && n < a.N && i < a.Hout && j < a.Wout && i >= bx.x && i < bx.z && j >= bx.y && j < bx.w;
         const size_t pix = ((size_t)bb * a.Hout + i) * a.Wout + j;
         float out = 0.f;
-        if (ok) out = epi_store(a, pix, n, yv[di][dj], mx);
+        if (ok) out = epi_store_in(a, pix, n, yv[di][dj], pre[it][2 * di + dj], mx);
         if (a.ybits) {
           // 64 lanes = channels n0 .. n0+63 of one pixel: two sign-bit words
           const uint64_t bits = __ballot(ok && out > 0.f);
@@ -518,7 +610,7 @@ namespace po {
 // correlation over the full 3x3 neighbourhood on full maps (no windows, no
 // split-K, destination = source grid) with N % 32 == 0, Cin_p % 16 == 0 and
 // the transformed weights (po_conv_desc.Wwino).
-int launch_wino(const ConvArgs& a, const float* U, hipStream_t st, int bm, int waves) {
+int launch_wino(const ConvArgs& a, const float* U, hipStream_t st, int bm, int waves, bool sched) {
   PO_REQUIRE(U, "po_conv: Winograd tile needs the transformed weights (Wwino)");
   PO_REQUIRE(a.prec == 0 && a.ntaps == 9 && a.tkw == 3 && (a.sdh == 1 || a.sdh == -1) && (a.sdw == 1 || a.sdw == -1) &&
                  a.dh0 == -a.sdh && a.dw0 == -a.sdw,
@@ -536,7 +628,9 @@ int launch_wino(const ConvArgs& a, const float* U, hipStream_t st, int bm, int w
     ConvArgs b = a;
     b.ntiles_n = a.N / N2;
     const int ntm = ceil_div((int64_t)a.B * Ht * Wt, T2);
-    if (waves == 8)
+    if (waves == 8 && sched)
+      hipLaunchKernelGGL((conv_wino2_k<8, true>), dim3(ntm * b.ntiles_n), dim3(512), 0, st, b, U, Ht, Wt);
+    else if (waves == 8)
       hipLaunchKernelGGL(conv_wino2_k<8>, dim3(ntm * b.ntiles_n), dim3(512), 0, st, b, U, Ht, Wt);
     else
       hipLaunchKernelGGL(conv_wino2_k<4>, dim3(ntm * b.ntiles_n), dim3(256), 0, st, b, U, Ht, Wt);

@@ -1,8 +1,9 @@
 // Loss head: per-anchor objectness/class extraction at the patch cell and the
 // creation-attack losses (reference train_patch.py:428-548, 230-253), forward
-// and the sparse gradient into the head tensors.  One workgroup; one thread per
-// (image, anchor), per-image reductions in anchor order, and the batch means
-// summed by thread 0 in image order (deterministic).
+// and the sparse gradient into the head tensors.  One thread per (image,
+// anchor), per-image reductions in anchor order, and the batch means summed by
+// one thread in image order (deterministic); chunks of 16 images run on one
+// workgroup each when the caller gives a scratch buffer.
 #pragma clang fp contract(off)
 #include "common.h"
 #include <math.h>
@@ -29,10 +30,14 @@ __device__ __forceinline__ float sigm(float x) { return 1.f / (1.f + expf(-x)); 
 // the chunk takes the first-index max objectness and sums the class terms in
 // anchor order, as the one-thread-per-image form did (same values, same order).
 constexpr int CL_IMG = 16;
+// With a scratch buffer the chunks are spread over workgroups (one per chunk)
+// and each image's (max objectness, class term) goes to scratch[b],
+// scratch[B + b]; cell_final_k then sums them in image order, so the result
+// is bit-identical to the one-workgroup form.
 __global__ __launch_bounds__(256) void cell_loss_k(LossArgs a, const float* __restrict__ center,
                                                    float* __restrict__ out2, float* __restrict__ obj_out,
                                                    float* __restrict__ cls_out, int32_t* __restrict__ cells,
-                                                   int32_t* __restrict__ flags) {
+                                                   int32_t* __restrict__ flags, float* __restrict__ scratch) {
   __shared__ float s_max[MAXB];
   __shared__ float s_cls[MAXB];
   __shared__ float c_obj[CL_IMG][3 * MAXH];
@@ -44,7 +49,7 @@ __global__ __launch_bounds__(256) void cell_loss_k(LossArgs a, const float* __re
   const int A = 3 * a.nheads;
   const float invB = 1.f / (float)a.B;
   const float g_obj = a.g2 ? a.g2[0] : 0.f, g_cls = a.g2 ? a.g2[1] : 0.f;
-  for (int b0 = 0; b0 < a.B; b0 += CL_IMG) {
+  for (int b0 = blockIdx.x * CL_IMG; b0 < a.B; b0 += gridDim.x * CL_IMG) {
     const int lb = threadIdx.x / A, k = threadIdx.x - lb * A;
     const int b = b0 + lb;
     if (lb < CL_IMG && b < a.B) {
@@ -121,8 +126,14 @@ __global__ __launch_bounds__(256) void cell_loss_k(LossArgs a, const float* __re
         if (kbest < 0 || o > best) { best = o; kbest = kk; }          // torch.max: first index
         cls_term += c_cls[lb2][kk];
       }
-      s_max[fb] = best;
-      s_cls[fb] = cls_term / (a.objective == 0 ? (float)A : (a.objective == 1 ? (float)A : 1.f));
+      const float ct = cls_term / (a.objective == 0 ? (float)A : (a.objective == 1 ? (float)A : 1.f));
+      if (scratch) {
+        scratch[fb] = best;
+        scratch[a.B + fb] = ct;
+      } else {
+        s_max[fb] = best;
+        s_cls[fb] = ct;
+      }
       // objectness gradient: d/d obj[kbest] of 4*(1 - mean_b max_k obj) = -4/B
       const int h = kbest / 3, an = kbest % 3;
       if (a.dheads[h]) {
@@ -133,15 +144,37 @@ __global__ __launch_bounds__(256) void cell_loss_k(LossArgs a, const float* __re
     __syncthreads();
   }
   if (threadIdx.x == 0) {
-    float sm = 0.f, sc = 0.f;
-    for (int b = 0; b < a.B; ++b) {
-      sm += s_max[b];
-      sc += s_cls[b];
+    if (!scratch) {
+      float sm = 0.f, sc = 0.f;
+      for (int b = 0; b < a.B; ++b) {
+        sm += s_max[b];
+        sc += s_cls[b];
+      }
+      out2[0] = 4.f * (1.f - sm / (float)a.B);                       // train_patch.py:236-239
+      out2[1] = a.objective == 0 ? sc / (float)a.B : (a.objective == 1 ? sc : 0.f);
     }
-    out2[0] = 4.f * (1.f - sm / (float)a.B);                       // train_patch.py:236-239
-    out2[1] = a.objective == 0 ? sc / (float)a.B : (a.objective == 1 ? sc : 0.f);
     if (flags && s_flag) atomicOr(flags, s_flag);       // accumulates over calls
   }
+}
+
+// batch means of the per-image terms, summed in image order (as cell_loss_k's one-workgroup form)
+__global__ __launch_bounds__(256) void cell_final_k(const float* __restrict__ scratch, int B, int objective,
+                                                    float* __restrict__ out2) {
+  __shared__ float s_max[MAXB];
+  __shared__ float s_cls[MAXB];
+  for (int b = threadIdx.x; b < B; b += 256) {
+    s_max[b] = scratch[b];
+    s_cls[b] = scratch[B + b];
+  }
+  __syncthreads();
+  if (threadIdx.x != 0) return;
+  float sm = 0.f, sc = 0.f;
+  for (int b = 0; b < B; ++b) {
+    sm += s_max[b];
+    sc += s_cls[b];
+  }
+  out2[0] = 4.f * (1.f - sm / (float)B);                           // train_patch.py:236-239
+  out2[1] = objective == 0 ? sc / (float)B : (objective == 1 ? sc : 0.f);
 }
 }  // namespace
 
@@ -149,7 +182,7 @@ extern "C" int po_cell_loss(const float* const* heads, const int* hw, const int*
                             const int32_t* const* org, int nheads, int Cp, int B, int S,
                             const float* center, int target, int objective, const float* g2,
                             float* const* d_heads, float* out2, float* obj_out, float* cls_out,
-                            int32_t* cells, int32_t* flags, po_stream_t s) {
+                            int32_t* cells, int32_t* flags, float* scratch, po_stream_t s) {
   PO_REQUIRE(heads && hw && center && out2, "po_cell_loss: null pointer");
   PO_REQUIRE(nheads >= 1 && nheads <= MAXH, "po_cell_loss: 1..%d heads supported, got %d", MAXH, nheads);
   PO_REQUIRE(Cp >= 3 * NF, "po_cell_loss: head channel stride %d < 60 (3 anchors x (5+15))", Cp);
@@ -178,8 +211,11 @@ extern "C" int po_cell_loss(const float* const* heads, const int* hw, const int*
   a.target = target;
   a.objective = objective;
   a.g2 = g2;
-  hipLaunchKernelGGL(cell_loss_k, dim3(1), dim3(256), 0, po::stream_of(s), a, center, out2, obj_out,
-                     cls_out, cells, flags);
+  const int nchunk = scratch ? po::ceil_div(B, CL_IMG) : 1;
+  hipLaunchKernelGGL(cell_loss_k, dim3(nchunk), dim3(256), 0, po::stream_of(s), a, center, out2, obj_out,
+                     cls_out, cells, flags, scratch);
+  if (scratch)
+    hipLaunchKernelGGL(cell_final_k, dim3(1), dim3(256), 0, po::stream_of(s), scratch, B, objective, out2);
   return po::check_launch("po_cell_loss");
 }
 

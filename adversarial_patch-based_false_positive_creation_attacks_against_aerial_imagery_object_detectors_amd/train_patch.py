@@ -84,9 +84,11 @@ class _CellLoss(torch.autograd.Function):
         if flags is None:
             flags = torch.zeros(1, dtype=torch.int32, device=dev)
         hwa, wina, orga = _head_args(hw, views)
+        scratch = torch.empty(2 * B, device=dev)
         nat.call("po_cell_loss", nat.ptr_array(heads), hwa, wina, orga, len(heads), Cp, B, S,
                  nat.ptr(center.contiguous()), target, objective, None, None, nat.ptr(out2), nat.ptr(obj),
-                 nat.ptr(cls), nat.ptr(cells, torch.int32), nat.ptr(flags, torch.int32), nat.stream())
+                 nat.ptr(cls), nat.ptr(cells, torch.int32), nat.ptr(flags, torch.int32), nat.ptr(scratch),
+                 nat.stream())
         ctx.save_for_backward(center, *heads)
         ctx.meta = (S, target, objective, tuple(hw), Cp, views)
         ctx.mark_non_differentiable(obj, cls, cells, flags)
@@ -99,9 +101,10 @@ class _CellLoss(torch.autograd.Function):
         d_heads = [torch.zeros_like(h) for h in heads]
         out2 = torch.empty(2, device=center.device)
         hwa, wina, orga = _head_args(hw, views)
+        scratch = torch.empty(2 * center.size(0), device=center.device)
         nat.call("po_cell_loss", nat.ptr_array(heads), hwa, wina, orga, len(heads), Cp, center.size(0), S,
                  nat.ptr(center.contiguous()), target, objective, nat.ptr(g2.contiguous().float()),
-                 nat.ptr_array(d_heads), nat.ptr(out2), None, None, None, None, nat.stream())
+                 nat.ptr_array(d_heads), nat.ptr(out2), None, None, None, None, nat.ptr(scratch), nat.stream())
         return (None, None, None, None, None, None, None, None) + tuple(d_heads)
 
 

@@ -137,11 +137,13 @@ int po_regularisers(const float* patch, int P, const float* colors, int ncol, co
  * written at the selected cells only (other elements untouched — caller zeroes).
  * flags (may be NULL): OR-ed with bit0 if any cell index was out of range
  * (clamped), bit1 if a cell fell outside its head window (clamped; a
- * planning error) — an accumulator the caller checks when it chooses. */
+ * planning error) — an accumulator the caller checks when it chooses.
+ * scratch (may be NULL): 2*B floats; with it the images run on one workgroup
+ * per 16 (the same results, bit for bit), without it on one workgroup. */
 int po_cell_loss(const float* const* heads, const int* hw, const int* win, const int32_t* const* org,
                  int nheads, int Cp, int B, int S, const float* center, int target, int objective,
                  const float* g2, float* const* d_heads, float* out2, float* obj_out, float* cls_out,
-                 int32_t* cells, int32_t* flags, po_stream_t s);
+                 int32_t* cells, int32_t* flags, float* scratch /* >= 2*B floats, or NULL */, po_stream_t s);
 
 /* MaxProbExtractor.forward (load_data.py:125-311; bbox_decode 63-122 rewrites
  * only the box fields, so it is not run): per image b, the max over every head
@@ -358,7 +360,7 @@ typedef struct po_conv_desc {
   const float* Wwino;
 } po_conv_desc;
 
-#define PO_CONV_NTILES 63
+#define PO_CONV_NTILES 64
 /* Tile `t` (1-based): block rows BM (output pixels), block columns BN (output
  * channels), k-step BK (input channels).  Tiles 1..10 stage operands through
  * registers, 11..20 are the same shapes staged by LDS-DMA, 21..28 are

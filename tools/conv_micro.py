@@ -33,11 +33,18 @@ if os.environ.get("MICRO_PREC", "0") == "1":          # fp16x3 operands
     wf._frag = {}
     d.Wfrag = wf._frag16(w)                             # fragment-ordered copy (tiles 57..60)
 d.tile = int(os.environ.get("MICRO_TILE", "0"))
-if d.tile in (61, 62, 63):                                        # Winograd F(2x2,3x3): transformed weights
+if d.tile in (61, 62, 63, 64):                                     # Winograd F(2x2,3x3): transformed weights
     offs = [(d.dh[t], d.dw[t]) for t in range(9)]
     U = ge._pkg("darknet_v3").wino_transform(w, offs)
     d.Wwino = U.data_ptr()
-args = (ctypes.byref(d), nat.ptr(x), nat.ptr(w, w.dtype), nat.ptr(b), nat.ptr(y), None, None, None, None, None)
+res = sm = None
+if os.environ.get("MICRO_RES") == "1":                 # fused shortcut epilogue (res + sum_out) and sign bits
+    res = torch.randn(B, Ho, Ho, Cout, device=dev)
+    sm = torch.empty_like(res)
+    bits = torch.empty(B * Ho * Ho * (Cout // 32), dtype=torch.int32, device=dev)
+    d.ybits = bits.data_ptr()
+args = (ctypes.byref(d), nat.ptr(x), nat.ptr(w, w.dtype), nat.ptr(b), nat.ptr(y), nat.ptr(res), nat.ptr(sm), None,
+        None, None)
 st = nat.stream()
 for _ in range(3):
     nat.call("po_conv", *args, st)
