@@ -107,19 +107,7 @@ struct EpiIn {
   uint32_t m = 0u, m2 = 0u;
 };
 
-__device__ __forceinline__ EpiIn epi_load(const ConvArgs& a, size_t pix, int n) {
-  const size_t o = pix * (size_t)a.Cout_p + n;
-  const size_t wo = pix * (size_t)(a.Cout_p >> 5) + (n >> 5);
-  EpiIn e;
-  if (a.res) e.res = a.res[o];
-  if (a.accumulate) e.yold = a.y[o];
-  if (a.mbits) e.m = a.mbits[wo];
-  else if (a.mask) e.m = __float_as_uint(a.mask[o]);
-  if (a.y2) e.m2 = a.m2bits ? a.m2bits[wo] : __float_as_uint(a.mask2[o]);
-  return e;
-}
-
-// epi_store with the inputs of epi_load (same arithmetic, same order)
+// epi_store with the inputs loaded ahead (same arithmetic, same order)
 __device__ __forceinline__ float epi_store_in(const ConvArgs& a, size_t pix, int n, float v, const EpiIn& e,
                                               EpiMax& mx) {
   const size_t o = pix * (size_t)a.Cout_p + n;
@@ -354,7 +342,11 @@ __device__ __forceinline__ int v2idx(int xi, int t, int ch) { return ((xi * T2 +
 // rewrites a V buffer nobody reads) whose instructions are interleaved by
 // scheduling-group barriers, so the wave keeps the matrix pipe fed while it
 // transforms instead of transforming after its last MFMA.
-template <int NW, bool SCHED = false>
+// PRE (tile 64): the epilogue inputs loaded before the k-loop, so their HBM
+// latency hides behind it: 1 = the shortcut operand (forward residual
+// launches), 2 = the accumulated destination and the two leaky-mask words
+// (dgrad launches); 0 = loaded at the start of the epilogue.
+template <int NW, bool SCHED = false, int PRE = 0>
 __global__ __launch_bounds__(64 * NW) void conv_wino2_k(const ConvArgs a, const float* __restrict__ U, int Ht, int Wt) {
   constexpr int NT = 64 * NW;            // threads
   constexpr int CPW = 16 / NW;           // components per wave
@@ -451,6 +443,42 @@ __global__ __launch_bounds__(64 * NW) void conv_wino2_k(const ConvArgs a, const 
     }
   };
 
+  // ---- the wave's epilogue tiles, and (PRE) epilogue inputs of its outputs
+  // loaded now: their HBM latency hides behind the whole k-loop
+  constexpr int IT = T2 / NW;
+  const int n = n0 + lane;
+  int tb[IT], tti_[IT], ttj_[IT];
+  bool tl_[IT];
+  EpiIn pre[IT][4];
+  auto tiles_meta = [&]() {
+#pragma unroll
+    for (int it = 0; it < IT; ++it) tl_[it] = tile_point(a, Ht, Wt, m0 + wave + NW * it, tb[it], tti_[it], ttj_[it]);
+  };
+  auto pre_load = [&](bool early) {
+#pragma unroll
+    for (int it = 0; it < IT; ++it)
+#pragma unroll
+      for (int p = 0; p < 4; ++p) {
+        const int i = 2 * tti_[it] + (p >> 1), j = 2 * ttj_[it] + (p & 1);
+        if (!(tl_[it] && n < a.N && i < a.Hout && j < a.Wout)) continue;
+        const size_t pix = ((size_t)tb[it] * a.Hout + i) * a.Wout + j;
+        const size_t o = pix * (size_t)a.Cout_p + n;
+        const size_t wo = pix * (size_t)(a.Cout_p >> 5) + (n >> 5);
+        EpiIn& e = pre[it][p];
+        if (early == (PRE == 1) && a.res) e.res = a.res[o];
+        if (early == (PRE == 2)) {
+          if (a.accumulate) e.yold = a.y[o];
+          if (a.mbits) e.m = a.mbits[wo];
+          else if (a.mask) e.m = __float_as_uint(a.mask[o]);
+          if (a.y2) e.m2 = a.m2bits ? a.m2bits[wo] : __float_as_uint(a.mask2[o]);
+        }
+      }
+  };
+  if constexpr (PRE != 0) {
+    tiles_meta();
+    pre_load(true);
+  }
+
   // ---- B operand
   const int kc_n = a.Cin_p / WK;
   const float* Ub = U + (size_t)lane * 4;
@@ -543,27 +571,12 @@ __global__ __launch_bounds__(64 * NW) void conv_wino2_k(const ConvArgs a, const 
         M[((wave * CPW + c) * T2 + t) * M2_ROW + nb * 32 + (lane & 31)] = acc[c][nb][e];
       }
   EpiMax mx;
-  const int n = n0 + lane;
   const int wpp = a.Cout_p >> 5;
-  // the wave's tiles and their per-element epilogue inputs, all loads in
-  // flight at once (they overlap the barrier and the M reads below instead of
-  // one dependent round trip per tile)
-  constexpr int IT = T2 / NW;
-  int tb[IT], tti_[IT], ttj_[IT];
-  bool tl_[IT];
-  EpiIn pre[IT][4];
-  const bool pre_any = a.res || a.accumulate || a.mbits || a.mask || a.y2;
-#pragma unroll
-  for (int it = 0; it < IT; ++it) {
-    tl_[it] = tile_point(a, Ht, Wt, m0 + wave + NW * it, tb[it], tti_[it], ttj_[it]);
-    if (pre_any)
-#pragma unroll
-      for (int p = 0; p < 4; ++p) {
-        const int i = 2 * tti_[it] + (p >> 1), j = 2 * ttj_[it] + (p & 1);
-        if (tl_[it] && n < a.N && i < a.Hout && j < a.Wout)
-          pre[it][p] = epi_load(a, ((size_t)tb[it] * a.Hout + i) * a.Wout + j, n);
-      }
-  }
+  // the per-element epilogue inputs of the wave's tiles, all loads in flight
+  // at once (they overlap the barrier and the M reads below instead of one
+  // dependent round trip per tile)
+  if constexpr (PRE == 0) tiles_meta();
+  pre_load(false);
   __syncthreads();
 #pragma unroll
   for (int it = 0; it < IT; ++it) {
@@ -628,7 +641,11 @@ int launch_wino(const ConvArgs& a, const float* U, hipStream_t st, int bm, int w
     ConvArgs b = a;
     b.ntiles_n = a.N / N2;
     const int ntm = ceil_div((int64_t)a.B * Ht * Wt, T2);
-    if (waves == 8 && sched)
+    if (waves == 8 && sched && a.res)
+      hipLaunchKernelGGL((conv_wino2_k<8, true, 1>), dim3(ntm * b.ntiles_n), dim3(512), 0, st, b, U, Ht, Wt);
+    else if (waves == 8 && sched && (a.accumulate || a.mbits || a.mask || a.y2))
+      hipLaunchKernelGGL((conv_wino2_k<8, true, 2>), dim3(ntm * b.ntiles_n), dim3(512), 0, st, b, U, Ht, Wt);
+    else if (waves == 8 && sched)
       hipLaunchKernelGGL((conv_wino2_k<8, true>), dim3(ntm * b.ntiles_n), dim3(512), 0, st, b, U, Ht, Wt);
     else if (waves == 8)
       hipLaunchKernelGGL(conv_wino2_k<8>, dim3(ntm * b.ntiles_n), dim3(512), 0, st, b, U, Ht, Wt);
