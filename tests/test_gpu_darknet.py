@@ -273,7 +273,7 @@ def test_quad_halo_tiles_match_row_tiles(quad, row, step, H, flip):
         run(quad, box)
 
 
-@pytest.mark.parametrize("stride,H,W,C,Cp", [(2, 13, 10, 12, 16), (1, 9, 7, 16, 16), (2, 416 // 8, 52, 30, 32)])
+@pytest.mark.parametrize("stride,H,W,C,Cp", [(2, 13, 10, 12, 16), (1, 9, 7, 16, 16), (2, 416 // 8, 52, 30, 32), (2, 7, 7, 3, 4)])
 def test_maxpool_ops_match_torch(stride, H, W, C, Cp):
     """po_maxpool2_fwd/bwd (darknet_v3.py:61-69: MaxPool2d(2,2), or
     ZeroPad2d((0,1,0,1)) + MaxPool2d(2,1)) against torch on NHWC buffers with
