@@ -136,6 +136,119 @@ extern "C" int po_median7_bwd(const float* dy, const int32_t* argidx, int C, int
 }
 
 // ------------------------------------------------------------------------
+// General median pool (median_pool.py:8-52 for any kernel, stride and
+// padding): reflect pad (l, r, t, b), kh x kw windows at stride (sh, sw), the
+// lower median (torch.median: rank (n-1)/2), argument = the first window
+// position (row-major) holding it.  Not on the training path (the patch
+// transformer uses the 7x7 kernels above); rank by counting, O(n^2) per
+// output from the L1/L2-resident plane.
+// ------------------------------------------------------------------------
+namespace {
+struct MedGeom {
+  int H, W, kh, kw, sh, sw, pl, pt, Ho, Wo;
+};
+
+__global__ __launch_bounds__(256) void median_fwd_k(const float* __restrict__ x, int C, MedGeom g,
+                                                    float* __restrict__ y, int32_t* __restrict__ arg) {
+  const int64_t q = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (q >= (int64_t)C * g.Ho * g.Wo) return;
+  const int c = (int)(q / ((int64_t)g.Ho * g.Wo));
+  const int rem = (int)(q - (int64_t)c * g.Ho * g.Wo);
+  const int i = rem / g.Wo, j = rem - (rem / g.Wo) * g.Wo;
+  const float* xc = x + (size_t)c * g.H * g.W;
+  const int n = g.kh * g.kw, r = (n - 1) / 2;
+  auto val = [&](int a) {
+    const int rr = reflect_idx(i * g.sh + a / g.kw - g.pt, g.H), cc = reflect_idx(j * g.sw + a % g.kw - g.pl, g.W);
+    return xc[(size_t)rr * g.W + cc];
+  };
+  int found = 0;
+  float med = 0.f;
+  for (int a = 0; a < n; ++a) {
+    const float va = val(a);
+    int less = 0, leq = 0;
+    for (int b2 = 0; b2 < n; ++b2) {
+      const float vb = val(b2);
+      less += vb < va;
+      leq += vb <= va;
+    }
+    if (less <= r && leq > r) { found = a; med = va; break; }     // first position holding the median
+  }
+  const int rr = reflect_idx(i * g.sh + found / g.kw - g.pt, g.H), cc = reflect_idx(j * g.sw + found % g.kw - g.pl, g.W);
+  y[q] = med;
+  arg[q] = (int32_t)((size_t)c * g.H * g.W + (size_t)rr * g.W + cc);
+}
+
+// dx[p] = sum, in output order, of dy[o] over the outputs o whose argument
+// is p.  Candidate outputs: those whose window covers one of the padded
+// positions reflecting onto p's row and column (up to 3 each); each output is
+// visited once (the union of the ranges is scanned), so a window holding two
+// reflections of p still routes its gradient once, as torch's unfold + pad
+// backward does.
+__global__ __launch_bounds__(256) void median_bwd_k(const float* __restrict__ dy, const int32_t* __restrict__ arg,
+                                                    int C, MedGeom g, int pb, int pr, float* __restrict__ dx) {
+  const int64_t p = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (p >= (int64_t)C * g.H * g.W) return;
+  const int c = (int)(p / ((int64_t)g.H * g.W));
+  const int rem = (int)(p - (int64_t)c * g.H * g.W);
+  const int r0 = rem / g.W, c0 = rem - (rem / g.W) * g.W;
+  // padded coordinates (from the padded origin) that reflect onto r0 / c0
+  int us[3], nu = 0, vs[3], nv = 0;
+  us[nu++] = r0 + g.pt;
+  if (r0 > 0 && r0 <= g.pt) us[nu++] = g.pt - r0;                                   // u = -r0
+  if (r0 < g.H - 1 && g.H - 1 - r0 <= pb) us[nu++] = 2 * (g.H - 1) - r0 + g.pt;     // u = 2(H-1) - r0
+  vs[nv++] = c0 + g.pl;
+  if (c0 > 0 && c0 <= g.pl) vs[nv++] = g.pl - c0;
+  if (c0 < g.W - 1 && g.W - 1 - c0 <= pr) vs[nv++] = 2 * (g.W - 1) - c0 + g.pl;
+  int i0 = g.Ho, i1 = -1, j0 = g.Wo, j1 = -1;
+  for (int a = 0; a < nu; ++a) {
+    i0 = min(i0, max(0, (us[a] - g.kh + g.sh) / g.sh));
+    i1 = max(i1, min(g.Ho - 1, us[a] / g.sh));
+  }
+  for (int b = 0; b < nv; ++b) {
+    j0 = min(j0, max(0, (vs[b] - g.kw + g.sw) / g.sw));
+    j1 = max(j1, min(g.Wo - 1, vs[b] / g.sw));
+  }
+  const int32_t want = (int32_t)p;
+  const size_t base = (size_t)c * g.Ho * g.Wo;
+  float acc = 0.f;
+  for (int i = i0; i <= i1; ++i)
+    for (int j = j0; j <= j1; ++j)
+      if (arg[base + (size_t)i * g.Wo + j] == want) acc += dy[base + (size_t)i * g.Wo + j];
+  dx[p] = acc;
+}
+}  // namespace
+
+extern "C" int po_median_fwd(const float* x, int C, int H, int W, int kh, int kw, int sh, int sw, int pl, int pr,
+                             int pt, int pb, float* y, int32_t* argidx, po_stream_t s) {
+  PO_REQUIRE(x && y && argidx, "po_median_fwd: null pointer");
+  PO_REQUIRE(C > 0 && H > 0 && W > 0 && kh > 0 && kw > 0 && sh > 0 && sw > 0, "po_median_fwd: bad shape");
+  PO_REQUIRE(kh * kw <= 1024, "po_median_fwd: window of %d elements (max 1024)", kh * kw);
+  PO_REQUIRE(pl >= 0 && pr >= 0 && pt >= 0 && pb >= 0 && pl < W && pr < W && pt < H && pb < H,
+             "po_median_fwd: reflect padding must be smaller than the input (F.pad mode='reflect')");
+  const int Hp = H + pt + pb, Wp = W + pl + pr;
+  PO_REQUIRE(Hp >= kh && Wp >= kw, "po_median_fwd: window larger than the padded input");
+  MedGeom g{H, W, kh, kw, sh, sw, pl, pt, (Hp - kh) / sh + 1, (Wp - kw) / sw + 1};
+  const int64_t n = (int64_t)C * g.Ho * g.Wo;
+  hipLaunchKernelGGL(median_fwd_k, dim3(po::ceil_div(n, 256)), dim3(256), 0, po::stream_of(s), x, C, g, y, argidx);
+  return po::check_launch("po_median_fwd");
+}
+
+extern "C" int po_median_bwd(const float* dy, const int32_t* argidx, int C, int H, int W, int kh, int kw, int sh,
+                             int sw, int pl, int pr, int pt, int pb, float* dx, po_stream_t s) {
+  PO_REQUIRE(dy && argidx && dx, "po_median_bwd: null pointer");
+  PO_REQUIRE(C > 0 && H > 0 && W > 0 && kh > 0 && kw > 0 && sh > 0 && sw > 0 && pl >= 0 && pr >= 0 && pt >= 0 &&
+                 pb >= 0 && pl < W && pr < W && pt < H && pb < H,
+             "po_median_bwd: bad shape");
+  const int Hp = H + pt + pb, Wp = W + pl + pr;
+  PO_REQUIRE(Hp >= kh && Wp >= kw, "po_median_bwd: window larger than the padded input");
+  MedGeom g{H, W, kh, kw, sh, sw, pl, pt, (Hp - kh) / sh + 1, (Wp - kw) / sw + 1};
+  const int64_t n = (int64_t)C * H * W;
+  hipLaunchKernelGGL(median_bwd_k, dim3(po::ceil_div(n, 256)), dim3(256), 0, po::stream_of(s), dy, argidx, C, g,
+                     pb, pr, dx);
+  return po::check_launch("po_median_bwd");
+}
+
+// ------------------------------------------------------------------------
 // Placement parameters (load_data.py:453-509, 654-743)
 // ------------------------------------------------------------------------
 namespace {

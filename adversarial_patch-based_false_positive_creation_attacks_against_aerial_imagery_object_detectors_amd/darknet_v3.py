@@ -997,16 +997,25 @@ class NetPlan:
             self.ws = torch.empty(floats, device=self.device)
         return self.ws
 
-    def tune(self, cache, iters=4):
+    def tune(self, cache, iters=4, time_missing=True):
         """Time every candidate (tile, split-K) of po_conv for each distinct
         launch shape of this plan on the current GPU and keep the fastest
         (wave quantisation over the 256 CUs, the k-step size and, for launches
         with few tiles — the receptive-field windows — splitting K over more
         workgroups decide it per shape).  ``cache`` maps a launch signature
-        to (tile, ksplit) and is shared between plans."""
+        to (tile, ksplit) and is shared between plans.  ``time_missing``
+        False (ADVPATCH_TUNE=cache): shapes not in the cache keep the
+        built-in heuristic instead of being timed, so a run is bit-for-bit
+        reproducible from the committed cache alone."""
         lib = self.lib
         st = nat.stream()
         convs = [(args, desc) for name, args, desc in self.fwd_ops + self.bwd_ops if name == "po_conv"]
+        if not time_missing:
+            for args, desc in convs:
+                key = self._tune_key(args, desc)
+                if key in cache:
+                    self._set_tile(desc, cache[key])
+            return
         if all(self._tune_key(args, desc) in cache for args, desc in convs):
             for args, desc in convs:                 # every shape already tuned: no launches
                 self._set_tile(desc, cache[self._tune_key(args, desc)])
@@ -1431,7 +1440,8 @@ class Darknet(nn.Module):
     def plan(self, B, H, W, device, windowed=False):
         """The execution plan for a batch shape (built, and its conv tiles
         autotuned on the device, on first use; ADVPATCH_TUNE=0 keeps the
-        built-in tile heuristic).  ``windowed``: blocks past the last
+        built-in tile heuristic, ADVPATCH_TUNE=cache takes the tiles of
+        ADVPATCH_TUNE_CACHE and times nothing).  ``windowed``: blocks past the last
         full-map dependency run on receptive-field windows around the loss
         cells (NetPlan._plan_windows); only the training path uses it."""
         self._prepare(device)
@@ -1445,7 +1455,7 @@ class Darknet(nn.Module):
                     with open(path) as f:
                         self._tile_cache.update({tuple(json.loads(k)): v for k, v in json.load(f).items()})
                 n0 = len(self._tile_cache)
-                p.tune(self._tile_cache)
+                p.tune(self._tile_cache, time_missing=os.environ.get("ADVPATCH_TUNE", "1") != "cache")
                 if path and len(self._tile_cache) != n0:
                     import json
                     os.makedirs(os.path.dirname(os.path.abspath(path)), exist_ok=True)

@@ -2,8 +2,9 @@
 
 The training path uses ``MedianPool2d(7, same=True)`` on the [1,3,P,P] patch
 (load_data.py:439, 531).  That configuration (k=7, stride 1, 'same' reflect
-padding) runs as ``po_median7_fwd``/``po_median7_bwd``; other configurations
-are not on the hot path and raise NotImplementedError.
+padding) runs as ``po_median7_fwd``/``po_median7_bwd`` (49 values in
+registers); every other kernel size / stride / padding runs as the general
+``po_median_fwd``/``po_median_bwd`` (the reference module's full surface).
 
 Tie rule (the reference's is implementation-defined): the
 gradient goes to the first window position, row-major, holding the median.
@@ -40,6 +41,33 @@ class _Median7(torch.autograd.Function):
         return dx
 
 
+class _MedianGeneral(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, k, stride, pad):
+        nat.ensure_device(x)
+        x = x.contiguous()
+        N, C, H, W = x.shape
+        (kh, kw), (sh, sw), (pl, pr, pt, pb) = k, stride, pad
+        Ho, Wo = (H + pt + pb - kh) // sh + 1, (W + pl + pr - kw) // sw + 1
+        y = torch.empty(N, C, Ho, Wo, device=x.device)
+        arg = torch.empty(N, C, Ho, Wo, dtype=torch.int32, device=x.device)
+        nat.call("po_median_fwd", nat.ptr(x), N * C, H, W, kh, kw, sh, sw, pl, pr, pt, pb, nat.ptr(y),
+                 nat.ptr(arg, torch.int32), nat.stream())
+        ctx.save_for_backward(arg)
+        ctx.meta = (x.shape, k, stride, pad)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        (arg,) = ctx.saved_tensors
+        shape, (kh, kw), (sh, sw), (pl, pr, pt, pb) = ctx.meta
+        N, C, H, W = shape
+        dx = torch.empty(shape, device=dy.device)
+        nat.call("po_median_bwd", nat.ptr(dy.contiguous()), nat.ptr(arg, torch.int32), N * C, H, W, kh, kw, sh, sw,
+                 pl, pr, pt, pb, nat.ptr(dx), nat.stream())
+        return dx, None, None, None
+
+
 def median_pool7(x):
     """[N,C,H,W] -> [N,C,H,W], 7x7 median with reflect 'same' padding."""
     return _Median7.apply(x)
@@ -72,8 +100,9 @@ class MedianPool2d(nn.Module):
         return self.padding
 
     def forward(self, x):
-        if self.k == (7, 7) and self.stride == (1, 1) and self._padding(x) == (3, 3, 3, 3):
+        """reflect pad, kh x kw windows at the stride, lower median
+        (median_pool.py:46-52); the 7x7 'same' case takes the fast kernels."""
+        pad = tuple(int(v) for v in self._padding(x))
+        if self.k == (7, 7) and self.stride == (1, 1) and pad == (3, 3, 3, 3):
             return median_pool7(x)
-        raise NotImplementedError("HIP MedianPool2d implements kernel 7, stride 1, same padding "
-                                  "(the training path); got k=%s stride=%s padding=%s"
-                                  % (self.k, self.stride, self._padding(x)))
+        return _MedianGeneral.apply(x, tuple(self.k), tuple(self.stride), pad)

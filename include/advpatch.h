@@ -50,6 +50,15 @@ int po_device_check(int device);
 int po_median7_fwd(const float* x, int C, int H, int W, float* y, int32_t* argidx, po_stream_t s);
 /* dx = scatter-add of dy through argidx (deterministic gather form). */
 int po_median7_bwd(const float* dy, const int32_t* argidx, int C, int H, int W, float* dx, po_stream_t s);
+/* MedianPool2d for any kernel (kh, kw), stride (sh, sw) and reflect padding
+ * (pl, pr, pt, pb) (median_pool.py:8-52; the 'same' rule is the caller's):
+ * y [C,Ho,Wo] = the lower median (rank (n-1)/2) of each window, argidx = the
+ * flat source index of the first window position holding it; bwd: dx [C,H,W]
+ * = sum of dy over the outputs whose argument is each pixel. */
+int po_median_fwd(const float* x, int C, int H, int W, int kh, int kw, int sh, int sw, int pl, int pr, int pt,
+                  int pb, float* y, int32_t* argidx, po_stream_t s);
+int po_median_bwd(const float* dy, const int32_t* argidx, int C, int H, int W, int kh, int kw, int sh, int sw,
+                  int pl, int pr, int pt, int pb, float* dx, po_stream_t s);
 
 /* Per-image patch placement (load_data.py:453-509 lab_transform,
  * 654-743 target_size/scale/theta, 693-715 target_x/y and patch_center).

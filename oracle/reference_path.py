@@ -21,7 +21,7 @@ import torch
 import torch.nn.functional as F
 
 __all__ = [
-    "parse_model_config", "median_pool7", "lab_transform", "patch_transformer",
+    "parse_model_config", "median_pool7", "median_pool2d", "lab_transform", "patch_transformer",
     "patch_applier", "load_printability", "nps_score", "total_variation",
     "colorful_loss", "OracleDarknet", "read_darknet_weights", "obj_cls_conf_find",
     "no_obj_reshape", "no_cls_reshape", "noCLS_Loss_CE", "noCLS_loss_targeted",
@@ -80,6 +80,19 @@ def median_pool7(x, k=7):
     pl, pr = pw // 2, pw - pw // 2
     xp = F.pad(x, (pl, pr, pl, pr), mode="reflect")
     win = xp.unfold(2, k, 1).unfold(3, k, 1)
+    win = win.contiguous().view(win.size()[:4] + (-1,))
+    if MEDIAN_TIE_RULE == "first":
+        med = win.detach().median(dim=-1)[0]
+        first = (win.detach() == med.unsqueeze(-1)).int().argmax(dim=-1, keepdim=True)
+        return torch.gather(win, -1, first).squeeze(-1)
+    return win.median(dim=-1)[0]
+
+
+def median_pool2d(x, k, stride, padding):
+    """MedianPool2d.forward for any configuration (median_pool.py:46-52):
+    reflect pad (l, r, t, b), unfold, lower median; MEDIAN_TIE_RULE as above."""
+    xp = F.pad(x, padding, mode="reflect")
+    win = xp.unfold(2, k[0], stride[0]).unfold(3, k[1], stride[1])
     win = win.contiguous().view(win.size()[:4] + (-1,))
     if MEDIAN_TIE_RULE == "first":
         med = win.detach().median(dim=-1)[0]

@@ -209,3 +209,35 @@ def test_nps_tv_kats_on_gpu():
     r = ld.regularisers(patch, colors.to(_dev())).cpu()
     assert abs(float(r[0]) - math.sqrt(1e-6 + 3e-12) / 3) < 1e-9
     assert abs(float(r[1]) - 2 * (P - 1) / P * 1e-6) < 1e-10
+
+
+@pytest.mark.parametrize("k,stride,padding,same,shape", [
+    (3, 1, 0, True, (2, 3, 17, 19)),
+    ((3, 5), (2, 1), (1, 2, 0, 1), False, (1, 3, 20, 23)),
+    (4, 2, 0, False, (1, 2, 16, 16)),              # even window: the lower median
+    (5, 3, 0, True, (1, 3, 31, 29)),               # 'same' with stride 3 (uneven padding)
+    (2, 1, (1, 0, 1, 0), False, (1, 1, 9, 9)),
+])
+def test_median_pool_general_matches_oracle(monkeypatch, k, stride, padding, same, shape):
+    """MedianPool2d beyond the 7x7 training configuration (median_pool.py:8-52):
+    values bit-exact; gradient on random (tie-free) data and on quantised
+    data with ties (first window position, the oracle's 'first' rule)."""
+    mp = pkg_mod("median_pool")
+    mod = mp.MedianPool2d(k, stride, padding, same)
+    for quant in (False, True):
+        monkeypatch.setattr(oracle.reference_path, "MEDIAN_TIE_RULE", "first" if quant else "torch")
+        g = torch.Generator().manual_seed(sum(shape) + quant)
+        x = torch.rand(*shape, generator=g)
+        if quant:
+            x = (x * 4).floor() / 4
+        pad = mod._padding(x)
+        xr = x.clone().requires_grad_(True)
+        ref = oracle.median_pool2d(xr, mod.k, mod.stride, pad)
+        xg = x.to(_dev()).requires_grad_(True)
+        y = mod(xg)
+        assert y.shape == ref.shape
+        assert torch.equal(y.detach().cpu(), ref.detach())
+        dy = torch.randn(ref.shape, generator=g)
+        ref.backward(dy)
+        y.backward(dy.to(_dev()))
+        torch.testing.assert_close(xg.grad.cpu(), xr.grad, rtol=0, atol=1e-6)

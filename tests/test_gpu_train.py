@@ -135,6 +135,7 @@ def test_headline_plan_b16_608(yolo_weights, monkeypatch, prec):
     terms, objectness/class at the cells, and the patch gradient against the
     branch-aligned oracle (ties asserted), fixed 1e-4 against float64."""
     monkeypatch.setenv("ADVPATCH_TUNE_CACHE", TILES)
+    monkeypatch.setenv("ADVPATCH_TUNE", "cache")          # the committed tiles, nothing timed
     sy, ld = pkg_mod("synthetic"), pkg_mod("load_data")
     tr = _trainer("builtin:yolov3-dota", yolo_weights, prec=prec)
     net = tr.darknet_model
@@ -234,3 +235,25 @@ def test_dropin_train_writes_reference_png_layout(tmp_path, capsys, monkeypatch)
     want = (patch.detach().float().cpu() * 255).to(torch.uint8).permute(1, 2, 0).numpy()
     assert np.array_equal(arr, want)
     assert float(patch.min()) >= 0.0 and float(patch.max()) <= 1.0
+
+
+def test_cache_mode_runs_are_bit_reproducible(yolo_weights, monkeypatch):
+    """ADVPATCH_TUNE=cache: two trainers built from scratch take the same
+    committed tiles (no timing), so the same inputs give the same patch
+    gradient and loss terms bit for bit."""
+    monkeypatch.setenv("ADVPATCH_TUNE_CACHE", TILES)
+    monkeypatch.setenv("ADVPATCH_TUNE", "cache")
+    sy = pkg_mod("synthetic")
+    B, S, P = 16, 608, 224
+    img, lab = sy.frames_slice(0, B, S, seed=7), sy.labels_slice(0, B, seed=8)
+    patch = sy.patch(P, seed=9)
+    dr = {k: v.cpu() for k, v in sy.draws_device(3, 5, 0, B, P, DEV).items()}
+    outs = []
+    for _ in range(2):
+        tr = _trainer("builtin:yolov3-dota", yolo_weights)
+        pg = patch.to(DEV).requires_grad_(True)
+        loss, terms = tr.losses(pg, img.to(DEV), lab.to(DEV), {k: v.to(DEV) for k, v in dr.items()})
+        loss.backward()
+        outs.append((pg.grad.cpu(), float(loss)))
+    assert torch.equal(outs[0][0], outs[1][0])
+    assert outs[0][1] == outs[1][1]
