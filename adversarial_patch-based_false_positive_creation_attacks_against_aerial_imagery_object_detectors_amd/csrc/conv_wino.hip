@@ -108,10 +108,12 @@ struct EpiIn {
 };
 
 // epi_store with the inputs loaded ahead (same arithmetic, same order)
-__device__ __forceinline__ float epi_store_in(const ConvArgs& a, size_t pix, int n, float v, const EpiIn& e,
-                                              EpiMax& mx) {
+// (bias_n = the channel's bias, loaded once per thread: a load here would be
+// re-issued after every store, which may alias it)
+__device__ __forceinline__ float epi_store_in(const ConvArgs& a, size_t pix, int n, float v, float bias_n,
+                                              const EpiIn& e, EpiMax& mx) {
   const size_t o = pix * (size_t)a.Cout_p + n;
-  float x = v + (a.bias ? a.bias[n] : 0.f);
+  float x = v + bias_n;
   if (a.act) x = po::leaky(x);
   if (a.accumulate) x += e.yold;
   float out = x;
@@ -449,10 +451,24 @@ __global__ __launch_bounds__(64 * NW) void conv_wino2_k(const ConvArgs a, const 
   const int n = n0 + lane;
   int tb[IT], tti_[IT], ttj_[IT];
   bool tl_[IT];
+  uint32_t okm[IT];                      // bit p: output pixel p of the tile is written (image, map, box, channel)
   EpiIn pre[IT][4];
+  // (all of it before the first epilogue store: a load between stores would
+  // make the wave wait for every store issued before it)
   auto tiles_meta = [&]() {
 #pragma unroll
-    for (int it = 0; it < IT; ++it) tl_[it] = tile_point(a, Ht, Wt, m0 + wave + NW * it, tb[it], tti_[it], ttj_[it]);
+    for (int it = 0; it < IT; ++it) {
+      tl_[it] = tile_point(a, Ht, Wt, m0 + wave + NW * it, tb[it], tti_[it], ttj_[it]);
+      int4 bx = make_int4(0, 0, 1 << 30, 1 << 30);
+      if (a.gbox && tl_[it]) bx = reinterpret_cast<const int4*>(a.gbox)[tb[it]];
+      okm[it] = 0u;
+#pragma unroll
+      for (int p = 0; p < 4; ++p) {
+        const int i = 2 * tti_[it] + (p >> 1), j = 2 * ttj_[it] + (p & 1);
+        if (tl_[it] && n < a.N && i < a.Hout && j < a.Wout && i >= bx.x && i < bx.z && j >= bx.y && j < bx.w)
+          okm[it] |= 1u << p;
+      }
+    }
   };
   auto pre_load = [&](bool early) {
 #pragma unroll
@@ -460,7 +476,7 @@ __global__ __launch_bounds__(64 * NW) void conv_wino2_k(const ConvArgs a, const 
 #pragma unroll
       for (int p = 0; p < 4; ++p) {
         const int i = 2 * tti_[it] + (p >> 1), j = 2 * ttj_[it] + (p & 1);
-        if (!(tl_[it] && n < a.N && i < a.Hout && j < a.Wout)) continue;
+        if (!((okm[it] >> p) & 1u)) continue;
         const size_t pix = ((size_t)tb[it] * a.Hout + i) * a.Wout + j;
         const size_t o = pix * (size_t)a.Cout_p + n;
         const size_t wo = pix * (size_t)(a.Cout_p >> 5) + (n >> 5);
@@ -524,9 +540,13 @@ __global__ __launch_bounds__(64 * NW) void conv_wino2_k(const ConvArgs a, const 
       for (int nb = 0; nb < 2; ++nb) {
         const float bv[8] = {bcur[c][nb][0].x, bcur[c][nb][0].y, bcur[c][nb][0].z, bcur[c][nb][0].w,
                              bcur[c][nb][1].x, bcur[c][nb][1].y, bcur[c][nb][1].z, bcur[c][nb][1].w};
+#ifdef PO_ABLATE_WINO_NOMFMA
+        acc[c][nb][0] += av[0] * bv[0];       // ablation build: staging without the MFMAs
+#else
 #pragma unroll
         for (int s8 = 0; s8 < 8; ++s8)        // MFMA step s, half h <-> channel 8h + s
           acc[c][nb] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[s8], bv[s8], acc[c][nb], 0, 0, 0);
+#endif
       }
     }
     if constexpr (SCHED) {
@@ -559,6 +579,20 @@ __global__ __launch_bounds__(64 * NW) void conv_wino2_k(const ConvArgs a, const 
     if (ks + 1 < kc_n) kstep(ks + 1, bn, bc);
   }
 
+#ifdef PO_ABLATE_WINO_NOEPI
+  // ablation build (tools/build_ablate.sh): prologue + k-loop only
+  {
+    float t = 0.f;
+#pragma unroll
+    for (int c = 0; c < CPW; ++c)
+#pragma unroll
+      for (int nb = 0; nb < 2; ++nb)
+#pragma unroll
+        for (int e = 0; e < 16; ++e) t += acc[c][nb][e];
+    if (t == 1234.5f) a.y[m0] = 1.f;
+    return;
+  }
+#endif
   // ---- epilogue: M[xi][tile][64 ch] (rows padded), then A^T M A per (tile, channel)
   float* M = smem;
 #pragma unroll
@@ -575,14 +609,14 @@ __global__ __launch_bounds__(64 * NW) void conv_wino2_k(const ConvArgs a, const 
   // the per-element epilogue inputs of the wave's tiles, all loads in flight
   // at once (they overlap the barrier and the M reads below instead of one
   // dependent round trip per tile)
-  if constexpr (PRE == 0) tiles_meta();
+  tiles_meta();            // (recomputed after the k-loop: nothing but the prefetched values lives across it)
   pre_load(false);
+  const float bias_n = (a.bias && n < a.N) ? a.bias[n] : 0.f;
   __syncthreads();
 #pragma unroll
   for (int it = 0; it < IT; ++it) {
     const int t = wave + NW * it;
     const int bb = tb[it], tti = tti_[it], ttj = ttj_[it];
-    const bool tl = tl_[it];
     float m[16];
 #pragma unroll
     for (int xi = 0; xi < 16; ++xi) m[xi] = M[(xi * T2 + t) * M2_ROW + lane];
@@ -594,17 +628,20 @@ __global__ __launch_bounds__(64 * NW) void conv_wino2_k(const ConvArgs a, const 
     }
     const float yv[2][2] = {{s0[0] + s0[1] + s0[2], s0[1] - s0[2] - s0[3]},
                             {s1[0] + s1[1] + s1[2], s1[1] - s1[2] - s1[3]}};
-    int4 bx = make_int4(0, 0, 1 << 30, 1 << 30);
-    if (a.gbox && tl) bx = reinterpret_cast<const int4*>(a.gbox)[bb];
 #pragma unroll
     for (int di = 0; di < 2; ++di)
 #pragma unroll
       for (int dj = 0; dj < 2; ++dj) {
         const int i = 2 * tti + di, j = 2 * ttj + dj;
-        const bool ok = tl && n < a.N && i < a.Hout && j < a.Wout && i >= bx.x && i < bx.z && j >= bx.y && j < bx.w;
+        const bool ok = (okm[it] >> (2 * di + dj)) & 1u;
         const size_t pix = ((size_t)bb * a.Hout + i) * a.Wout + j;
         float out = 0.f;
-        if (ok) out = epi_store_in(a, pix, n, yv[di][dj], pre[it][2 * di + dj], mx);
+#ifdef PO_ABLATE_WINO_NOSTORE
+        out = yv[di][dj] + bias_n;             // ablation build: epilogue without global traffic
+        if (out == 1234.5f) a.y[0] = out;
+        continue;
+#endif
+        if (ok) out = epi_store_in(a, pix, n, yv[di][dj], bias_n, pre[it][2 * di + dj], mx);
         if (a.ybits) {
           // 64 lanes = channels n0 .. n0+63 of one pixel: two sign-bit words
           const uint64_t bits = __ballot(ok && out > 0.f);

@@ -660,9 +660,13 @@ class NetPlan:
         return self.bits[t.data_ptr()].data_ptr()
 
     def slot(self, t):
-        """Device address of tensor t's max|x| slot (None for None)."""
+        """Device address of tensor t's max|x| slot (None for None, and for
+        every tensor of an exact-fp32 plan: only the fp16x3 splits read the
+        bounds, and a kernel that commits one waits for its own stores)."""
         if t is None:
             return None
+        if self.prec != 1:
+            return nat.c_void_p(None)
         return nat.c_void_p(self.amax.data_ptr() + 4 * nat.PO_AMAX_SUB * self._slot_idx[t.data_ptr()])
 
     def _conv_prec(self, desc, src, wts_or_j, taps=None, cin_p=None):

@@ -8,8 +8,9 @@ SRC=$ROOT/adversarial_patch-based_false_positive_creation_attacks_against_aerial
 OUT=$ROOT/tools/bin
 TMP=$(mktemp -d)
 mkdir -p "$OUT"
-for f in patch_ops loss_ops conv_first conv_igemm conv_h3 net_ops; do
-  /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -fPIC -std=c++17 -munsafe-fp-atomics -Wno-inline-asm "$@" -c "$SRC/$f.hip" -o "$TMP/$f.o" &
+for f in "$SRC"/*.hip; do
+  b=$(basename "$f" .hip)
+  /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -fPIC -std=c++17 -munsafe-fp-atomics -Wno-inline-asm "$@" -c "$f" -o "$TMP/$b.o" &
 done
 wait
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o "$OUT/libadvpatch_$TAG.so" "$TMP"/*.o

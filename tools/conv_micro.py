@@ -5,7 +5,7 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import torch
 import __graft_entry__ as ge
 nat = ge._pkg("_native")
-if os.environ.get("MICRO_LIB"):          # ablation builds (tools/bin)
+if os.environ.get("MICRO_LIB"):             # ablation builds (tools/bin)
     nat.LIB_PATH = os.environ["MICRO_LIB"]
 B, H, Cin, Cout, k, s = (int(x) for x in sys.argv[1:7])
 iters = int(sys.argv[7]) if len(sys.argv) > 7 else 50
