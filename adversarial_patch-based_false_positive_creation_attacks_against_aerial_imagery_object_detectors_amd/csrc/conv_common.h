@@ -184,16 +184,35 @@ __device__ __forceinline__ void conv_epilogue(const ConvArgs& a, const floatx16 
       float4 bv = make_float4(0.f, 0.f, 0.f, 0.f);
       if (a.bias && n < a.N) bv = *reinterpret_cast<const float4*>(a.bias + n);
       const int wpp = a.Cout_p >> 5;            // sign-bit words per pixel (bits need Cout_p % 32 == 0)
+      // load phase: the rows' shortcut operand, accumulated destination and
+      // mask words, all before the first store (gfx9 counts stores and loads
+      // on one counter: a load issued after a store waits for that store)
+      int pixq[4];
+      float4 pres[4], pold[4];
+      uint32_t pmw[4], pm2w[4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        pixq[q] = dst_pix[wm * TM * 32 + i * 32 + rr + 8 * q];
+        pres[q] = pold[q] = make_float4(0.f, 0.f, 0.f, 0.f);
+        pmw[q] = pm2w[q] = 0u;
+        if (pixq[q] >= 0 && n < a.N) {
+          const size_t o = (size_t)pixq[q] * a.Cout_p + n;
+          const size_t wo = (size_t)pixq[q] * wpp + (n >> 5);
+          if (a.res) pres[q] = *reinterpret_cast<const float4*>(a.res + o);
+          if (a.accumulate) pold[q] = *reinterpret_cast<const float4*>(a.y + o);
+          if (a.mbits) pmw[q] = a.mbits[wo];
+          if (a.y2 && a.m2bits) pm2w[q] = a.m2bits[wo];
+        }
+      }
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
         const int row = rr + 8 * q;
         const float4 v = *reinterpret_cast<const float4*>(scr + row * 32 + cc);
-        const int pix = dst_pix[wm * TM * 32 + i * 32 + row];
+        const int pix = pixq[q];
         const bool live = pix >= 0 && n < a.N;
         uint32_t nib = 0;
         if (live) {
           const size_t o = (size_t)pix * a.Cout_p + n;
-          const size_t wo = (size_t)pix * wpp + (n >> 5);
           float x[4] = {__builtin_ldexpf(v.x, -sh) + bv.x, __builtin_ldexpf(v.y, -sh) + bv.y,
                         __builtin_ldexpf(v.z, -sh) + bv.z, __builtin_ldexpf(v.w, -sh) + bv.w};
           if (a.act) {
@@ -201,12 +220,12 @@ __device__ __forceinline__ void conv_epilogue(const ConvArgs& a, const floatx16 
             for (int c = 0; c < 4; ++c) x[c] = leaky(x[c]);
           }
           if (a.accumulate) {
-            const float4 p = *reinterpret_cast<const float4*>(a.y + o);
+            const float4 p = pold[q];
             x[0] += p.x; x[1] += p.y; x[2] += p.z; x[3] += p.w;
           }
           float4 out = make_float4(x[0], x[1], x[2], x[3]);
           if (a.mbits) {
-            const float4 g = leaky_grad_bits(a.mbits[wo], n);
+            const float4 g = leaky_grad_bits(pmw[q], n);
             out = make_float4(x[0] * g.x, x[1] * g.y, x[2] * g.z, x[3] * g.w);
           } else if (a.mask) {
             const float4 mk = *reinterpret_cast<const float4*>(a.mask + o);
@@ -217,7 +236,7 @@ __device__ __forceinline__ void conv_epilogue(const ConvArgs& a, const floatx16 
           nib = (out.x > 0.f ? 1u : 0u) | (out.y > 0.f ? 2u : 0u) | (out.z > 0.f ? 4u : 0u) | (out.w > 0.f ? 8u : 0u);
           my = fmaxf(my, fmaxf(fmaxf(fabsf(out.x), fabsf(out.y)), fmaxf(fabsf(out.z), fabsf(out.w))));
           if (a.res) {
-            const float4 r = *reinterpret_cast<const float4*>(a.res + o);
+            const float4 r = pres[q];
             const float4 sm = make_float4(x[0] + r.x, x[1] + r.y, x[2] + r.z, x[3] + r.w);
             *reinterpret_cast<float4*>(a.sum + o) = sm;
             ms = fmaxf(ms, fmaxf(fmaxf(fabsf(sm.x), fabsf(sm.y)), fmaxf(fabsf(sm.z), fabsf(sm.w))));
@@ -225,7 +244,7 @@ __device__ __forceinline__ void conv_epilogue(const ConvArgs& a, const floatx16 
           if (a.y2) {
             float4 g;
             if (a.m2bits) {
-              g = leaky_grad_bits(a.m2bits[wo], n);
+              g = leaky_grad_bits(pm2w[q], n);
             } else {
               const float4 mk = *reinterpret_cast<const float4*>(a.mask2 + o);
               g = make_float4(leaky_grad(mk.x), leaky_grad(mk.y), leaky_grad(mk.z), leaky_grad(mk.w));
