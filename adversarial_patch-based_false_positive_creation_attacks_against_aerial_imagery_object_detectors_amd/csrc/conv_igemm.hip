@@ -389,7 +389,8 @@ bool forced_tile(int& bm, int& bn, int& bk, int& gl) {
 // 61, 62: prec 0 Winograd F(2x2,3x3) (staging 5, conv_wino.hip; BM counts
 // 2x2 output tiles): 64 tiles x 32 channels, and 32 tiles x 64 channels with
 // LDS-DMA input (62: 4 waves; 63, staging 6: 8 waves, two per SIMD; 64,
-// staging 7: 63 with the transform interleaved into the MFMA stream).
+// staging 7: 63 with the transform interleaved into the MFMA stream; 65,
+// staging 8: 64 with the 16-byte (4-channel) epilogue).
 constexpr int kTiles[PO_CONV_NTILES][5] = {
     {128, 128, 16, 0, 0}, {128, 128, 32, 0, 0}, {64, 128, 16, 0, 0}, {64, 128, 32, 0, 0}, {128, 64, 16, 0, 0},
     {128, 64, 32, 0, 0},  {64, 64, 16, 0, 0},   {64, 64, 32, 0, 0},  {128, 32, 16, 0, 0}, {128, 32, 32, 0, 0},
@@ -405,7 +406,7 @@ constexpr int kTiles[PO_CONV_NTILES][5] = {
     {128, 128, 16, 1, 1}, {256, 128, 16, 1, 1}, {128, 128, 16, 2, 1}, {128, 64, 16, 2, 1},
     {128, 128, 16, 3, 1}, {128, 64, 16, 3, 1},
     {128, 128, 16, 4, 1}, {128, 64, 16, 4, 1}, {256, 128, 16, 4, 1}, {256, 64, 16, 4, 1},
-    {64, 32, 16, 5, 0}, {32, 64, 16, 5, 0}, {32, 64, 16, 6, 0}, {32, 64, 16, 7, 0}};
+    {64, 32, 16, 5, 0}, {32, 64, 16, 5, 0}, {32, 64, 16, 6, 0}, {32, 64, 16, 7, 0}, {32, 64, 16, 8, 0}};
 }  // namespace
 
 extern "C" int po_conv_tile_info(int t, int* bm, int* bn, int* bk, int* prec) {
@@ -524,7 +525,7 @@ extern "C" int po_conv(const po_conv_desc* d, const float* in, const float* W, c
     }
     return rc;
   }
-  if (gl >= 5 && gl <= 7) return po::launch_wino(a, d->Wwino, st, bm, gl >= 6 ? 8 : 4, gl == 7);
+  if (gl >= 5 && gl <= 8) return po::launch_wino(a, d->Wwino, st, bm, gl >= 6 ? 8 : 4, gl >= 7, gl == 8);
   if (bk > 32) bk = 32;
   if (gl) return bk == 32 ? dispatch<32, true>(a, st, bm, bn) : dispatch<16, true>(a, st, bm, bn);
   return bk == 32 ? dispatch<32, false>(a, st, bm, bn) : dispatch<16, false>(a, st, bm, bn);

@@ -135,6 +135,53 @@ __device__ __forceinline__ float epi_store_in(const ConvArgs& a, size_t pix, int
   return out;
 }
 
+// Four consecutive channels n..n+3 of one destination element (VEC epilogue):
+// the arithmetic of epi_store_in per channel, 16-byte loads and stores.
+struct EpiIn4 {
+  float4 res = make_float4(0.f, 0.f, 0.f, 0.f), yold = make_float4(0.f, 0.f, 0.f, 0.f);
+  uint32_t m = 0u, m2 = 0u;
+};
+
+__device__ __forceinline__ float4 epi_store4(const ConvArgs& a, size_t pix, int n, float4 v, float4 bias_n,
+                                             const EpiIn4& e, EpiMax& mx) {
+  const size_t o = pix * (size_t)a.Cout_p + n;
+  float x[4] = {v.x + bias_n.x, v.y + bias_n.y, v.z + bias_n.z, v.w + bias_n.w};
+  if (a.act) {
+#pragma unroll
+    for (int c = 0; c < 4; ++c) x[c] = po::leaky(x[c]);
+  }
+  if (a.accumulate) { x[0] += e.yold.x; x[1] += e.yold.y; x[2] += e.yold.z; x[3] += e.yold.w; }
+  float4 out = make_float4(x[0], x[1], x[2], x[3]);
+  if (a.mbits) {
+    const float4 g = po::leaky_grad_bits(e.m, n);
+    out = make_float4(x[0] * g.x, x[1] * g.y, x[2] * g.z, x[3] * g.w);
+  } else if (a.mask) {
+    const float4 mk = *reinterpret_cast<const float4*>(a.mask + o);
+    out = make_float4(x[0] * po::leaky_grad(mk.x), x[1] * po::leaky_grad(mk.y), x[2] * po::leaky_grad(mk.z),
+                      x[3] * po::leaky_grad(mk.w));
+  }
+  if (a.y) *reinterpret_cast<float4*>(a.y + o) = out;
+  mx.y = fmaxf(mx.y, fmaxf(fmaxf(fabsf(out.x), fabsf(out.y)), fmaxf(fabsf(out.z), fabsf(out.w))));
+  if (a.res) {
+    const float4 sm = make_float4(x[0] + e.res.x, x[1] + e.res.y, x[2] + e.res.z, x[3] + e.res.w);
+    *reinterpret_cast<float4*>(a.sum + o) = sm;
+    mx.s = fmaxf(mx.s, fmaxf(fmaxf(fabsf(sm.x), fabsf(sm.y)), fmaxf(fabsf(sm.z), fabsf(sm.w))));
+  }
+  if (a.y2) {
+    float4 g;
+    if (a.m2bits) {
+      g = po::leaky_grad_bits(e.m2, n);
+    } else {
+      const float4 mk = *reinterpret_cast<const float4*>(a.mask2 + o);
+      g = make_float4(po::leaky_grad(mk.x), po::leaky_grad(mk.y), po::leaky_grad(mk.z), po::leaky_grad(mk.w));
+    }
+    const float4 o2 = make_float4(x[0] * g.x, x[1] * g.y, x[2] * g.z, x[3] * g.w);
+    *reinterpret_cast<float4*>(a.y2 + o) = o2;
+    mx.y2 = fmaxf(mx.y2, fmaxf(fmaxf(fabsf(o2.x), fabsf(o2.y)), fmaxf(fabsf(o2.z), fabsf(o2.w))));
+  }
+  return out;
+}
+
 __global__ __launch_bounds__(256) void conv_wino_k(const ConvArgs a, const float* __restrict__ U, int Ht, int Wt) {
   __shared__ __attribute__((aligned(16))) float smem[2 * 16 * WT * WK];     // 128 KB
   __shared__ int s_live;
@@ -348,7 +395,10 @@ __device__ __forceinline__ int v2idx(int xi, int t, int ch) { return ((xi * T2 +
 // latency hides behind it: 1 = the shortcut operand (forward residual
 // launches), 2 = the accumulated destination and the two leaky-mask words
 // (dgrad launches); 0 = loaded at the start of the epilogue.
-template <int NW, bool SCHED = false, int PRE = 0>
+// VEC (tile 65, NW = 8): in the epilogue a lane owns 4 consecutive channels
+// of one of the wave's 4 tiles (16 lanes per tile), so M is read, and the
+// destination written, 16 bytes at a time (a quarter of the instructions).
+template <int NW, bool SCHED = false, int PRE = 0, bool VEC = false>
 __global__ __launch_bounds__(64 * NW) void conv_wino2_k(const ConvArgs a, const float* __restrict__ U, int Ht, int Wt) {
   constexpr int NT = 64 * NW;            // threads
   constexpr int CPW = 16 / NW;           // components per wave
@@ -490,9 +540,46 @@ __global__ __launch_bounds__(64 * NW) void conv_wino2_k(const ConvArgs a, const 
         }
       }
   };
+  // VEC epilogue lane roles: tile it4 of the wave, channels n4 .. n4+3
+  const int it4 = lane >> 4, n4 = n0 + 4 * (lane & 15);
+  int vb = 0, vti = 0, vtj = 0;
+  uint32_t vok = 0u;
+  EpiIn4 pre4[4];
+  auto vec_meta = [&]() {
+    const bool tl = tile_point(a, Ht, Wt, m0 + wave + NW * it4, vb, vti, vtj);
+    int4 bx = make_int4(0, 0, 1 << 30, 1 << 30);
+    if (a.gbox && tl) bx = reinterpret_cast<const int4*>(a.gbox)[vb];
+    vok = 0u;
+#pragma unroll
+    for (int p = 0; p < 4; ++p) {
+      const int i = 2 * vti + (p >> 1), j = 2 * vtj + (p & 1);
+      if (tl && n4 < a.N && i < a.Hout && j < a.Wout && i >= bx.x && i < bx.z && j >= bx.y && j < bx.w)
+        vok |= 1u << p;
+    }
+  };
+  auto vec_load = [&](bool early) {
+#pragma unroll
+    for (int p = 0; p < 4; ++p) {
+      if (!((vok >> p) & 1u)) continue;
+      const size_t pix = ((size_t)vb * a.Hout + 2 * vti + (p >> 1)) * a.Wout + 2 * vtj + (p & 1);
+      const size_t o = pix * (size_t)a.Cout_p + n4;
+      const size_t wo = pix * (size_t)(a.Cout_p >> 5) + (n4 >> 5);
+      if (early == (PRE == 1) && a.res) pre4[p].res = *reinterpret_cast<const float4*>(a.res + o);
+      if (early == (PRE == 2)) {
+        if (a.accumulate) pre4[p].yold = *reinterpret_cast<const float4*>(a.y + o);
+        if (a.mbits) pre4[p].m = a.mbits[wo];
+        if (a.y2 && a.m2bits) pre4[p].m2 = a.m2bits[wo];
+      }
+    }
+  };
   if constexpr (PRE != 0) {
-    tiles_meta();
-    pre_load(true);
+    if constexpr (VEC) {
+      vec_meta();
+      vec_load(true);
+    } else {
+      tiles_meta();
+      pre_load(true);
+    }
   }
 
   // ---- B operand
@@ -606,6 +693,43 @@ __global__ __launch_bounds__(64 * NW) void conv_wino2_k(const ConvArgs a, const 
       }
   EpiMax mx;
   const int wpp = a.Cout_p >> 5;
+  if constexpr (VEC) {
+    vec_meta();
+    vec_load(false);
+    const float4 bias4 = (a.bias && n4 < a.N) ? *reinterpret_cast<const float4*>(a.bias + n4)
+                                              : make_float4(0.f, 0.f, 0.f, 0.f);
+    __syncthreads();
+    const int t = wave + NW * it4;
+    float4 m[16];
+#pragma unroll
+    for (int xi = 0; xi < 16; ++xi) m[xi] = *reinterpret_cast<const float4*>(M + (xi * T2 + t) * M2_ROW + 4 * (lane & 15));
+    float4 s0[4], s1[4];
+#pragma unroll
+    for (int v = 0; v < 4; ++v) {
+      s0[v] = f4add(f4add(m[0 * 4 + v], m[1 * 4 + v]), m[2 * 4 + v]);
+      s1[v] = f4sub(f4sub(m[1 * 4 + v], m[2 * 4 + v]), m[3 * 4 + v]);
+    }
+    const float4 yv[2][2] = {{f4add(f4add(s0[0], s0[1]), s0[2]), f4sub(f4sub(s0[1], s0[2]), s0[3])},
+                             {f4add(f4add(s1[0], s1[1]), s1[2]), f4sub(f4sub(s1[1], s1[2]), s1[3])}};
+#pragma unroll
+    for (int p = 0; p < 4; ++p) {
+      const bool ok = (vok >> p) & 1u;
+      const size_t pix = ((size_t)vb * a.Hout + 2 * vti + (p >> 1)) * a.Wout + 2 * vtj + (p & 1);
+      uint32_t nib = 0u;
+      if (ok) {
+        const float4 out = epi_store4(a, pix, n4, yv[p >> 1][p & 1], bias4, pre4[p], mx);
+        nib = (out.x > 0.f ? 1u : 0u) | (out.y > 0.f ? 2u : 0u) | (out.z > 0.f ? 4u : 0u) | (out.w > 0.f ? 8u : 0u);
+      }
+      if (a.ybits) {
+        // 8 lanes hold the 32 channels of one sign-bit word: OR their nibbles
+        uint32_t w = nib << (4 * (lane & 7));
+        w |= (uint32_t)__shfl_xor((int)w, 1);
+        w |= (uint32_t)__shfl_xor((int)w, 2);
+        w |= (uint32_t)__shfl_xor((int)w, 4);
+        if (ok && (lane & 7) == 0) a.ybits[pix * wpp + (n4 >> 5)] = w;
+      }
+    }
+  } else {
   // the per-element epilogue inputs of the wave's tiles, all loads in flight
   // at once (they overlap the barrier and the M reads below instead of one
   // dependent round trip per tile)
@@ -649,6 +773,7 @@ __global__ __launch_bounds__(64 * NW) void conv_wino2_k(const ConvArgs a, const 
         }
       }
   }
+  }
   if (a.y_amax) po::amax_commit(a.y_amax, mx.y);
   if (a.sum_amax) po::amax_commit(a.sum_amax, mx.s);
   if (a.y2_amax) po::amax_commit(a.y2_amax, mx.y2);
@@ -660,7 +785,7 @@ namespace po {
 // correlation over the full 3x3 neighbourhood on full maps (no windows, no
 // split-K, destination = source grid) with N % 32 == 0, Cin_p % 16 == 0 and
 // the transformed weights (po_conv_desc.Wwino).
-int launch_wino(const ConvArgs& a, const float* U, hipStream_t st, int bm, int waves, bool sched) {
+int launch_wino(const ConvArgs& a, const float* U, hipStream_t st, int bm, int waves, bool sched, bool vec) {
   PO_REQUIRE(U, "po_conv: Winograd tile needs the transformed weights (Wwino)");
   PO_REQUIRE(a.prec == 0 && a.ntaps == 9 && a.tkw == 3 && (a.sdh == 1 || a.sdh == -1) && (a.sdw == 1 || a.sdw == -1) &&
                  a.dh0 == -a.sdh && a.dw0 == -a.sdw,
@@ -678,7 +803,13 @@ int launch_wino(const ConvArgs& a, const float* U, hipStream_t st, int bm, int w
     ConvArgs b = a;
     b.ntiles_n = a.N / N2;
     const int ntm = ceil_div((int64_t)a.B * Ht * Wt, T2);
-    if (waves == 8 && sched && a.res)
+    if (waves == 8 && sched && vec && a.res)
+      hipLaunchKernelGGL((conv_wino2_k<8, true, 1, true>), dim3(ntm * b.ntiles_n), dim3(512), 0, st, b, U, Ht, Wt);
+    else if (waves == 8 && sched && vec && (a.accumulate || a.mbits || a.mask || a.y2))
+      hipLaunchKernelGGL((conv_wino2_k<8, true, 2, true>), dim3(ntm * b.ntiles_n), dim3(512), 0, st, b, U, Ht, Wt);
+    else if (waves == 8 && sched && vec)
+      hipLaunchKernelGGL((conv_wino2_k<8, true, 0, true>), dim3(ntm * b.ntiles_n), dim3(512), 0, st, b, U, Ht, Wt);
+    else if (waves == 8 && sched && a.res)
       hipLaunchKernelGGL((conv_wino2_k<8, true, 1>), dim3(ntm * b.ntiles_n), dim3(512), 0, st, b, U, Ht, Wt);
     else if (waves == 8 && sched && (a.accumulate || a.mbits || a.mask || a.y2))
       hipLaunchKernelGGL((conv_wino2_k<8, true, 2>), dim3(ntm * b.ntiles_n), dim3(512), 0, st, b, U, Ht, Wt);

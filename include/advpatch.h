@@ -369,7 +369,7 @@ typedef struct po_conv_desc {
   const float* Wwino;
 } po_conv_desc;
 
-#define PO_CONV_NTILES 64
+#define PO_CONV_NTILES 65
 /* Tile `t` (1-based): block rows BM (output pixels), block columns BN (output
  * channels), k-step BK (input channels).  Tiles 1..10 stage operands through
  * registers, 11..20 are the same shapes staged by LDS-DMA, 21..28 are
