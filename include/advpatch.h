@@ -33,7 +33,7 @@ typedef void* po_stream_t;
 #define PO_EHIP -2     /* HIP runtime error */
 #define PO_EDEVICE -3  /* device is not gfx950 */
 
-#define PO_ABI_VERSION 10
+#define PO_ABI_VERSION 11
 #define PO_AMAX_SUB 64  /* sub-slots per max|x| slot (see po_conv_desc) */
 
 int po_abi_version(void);
