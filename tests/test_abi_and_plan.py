@@ -149,3 +149,12 @@ def test_plan_structure_yolov3_on_cpu_buffers():
     for i, d in enumerate(net.blocks):
         if d["type"] == "convolutional" and plan._leaky(i) and plan.has_grad[i] and i > 0:
             assert plan.ncons[i] >= 1
+
+
+def test_graft_entry_build_runs():
+    """__graft_entry__.build() (the driver's build check): make, import, and the
+    library's ABI equals the package's."""
+    import __graft_entry__
+    __graft_entry__.build()
+    nat = pkg_mod("_native")
+    assert nat.load().po_abi_version() == nat.PO_ABI_VERSION
