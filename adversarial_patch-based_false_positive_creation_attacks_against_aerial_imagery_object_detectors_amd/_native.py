@@ -13,7 +13,7 @@ LIB_PATH = os.path.join(_HERE, "libadvpatch_hip.so")
 
 c_int, c_float, c_int64, c_void_p = ctypes.c_int, ctypes.c_float, ctypes.c_int64, ctypes.c_void_p
 
-PO_ABI_VERSION = 11   # include/advpatch.h
+PO_ABI_VERSION = 12   # include/advpatch.h
 PO_CONV_NTILES = 65   # include/advpatch.h
 PO_AMAX_SUB = 64      # sub-slots per max|x| slot
 
@@ -78,6 +78,8 @@ _SIGS = {
                           ctypes.POINTER(c_int)],
     "po_conv_first_fwd": [c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_int, c_int,
                           c_int, c_void_p, c_void_p, c_void_p],
+    "po_conv_first_pool_fwd": [c_void_p, c_int, c_int, c_int, c_void_p, c_void_p, c_int, c_int, c_int, c_void_p,
+                               c_void_p, c_void_p, c_void_p],
     "po_conv_first_dgrad": [c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_int, c_int, c_void_p,
                             c_void_p, c_void_p],
     "po_slice_accum": [c_void_p, c_int, c_int, c_void_p, c_int, c_int, c_int64, c_int, c_int,

@@ -151,6 +151,117 @@ __global__ __launch_bounds__(256) void first_fwd2_k(const float* __restrict__ im
   }
 }
 
+// First conv (stride 1) with the k=2 stride-2 max pool that follows it fused
+// into the epilogue (yolov3-tiny: conv 3->16 @416 then maxpool,
+// darknet_v3.py:61-69).  The conv output is never stored: the pool backward
+// needs only the window argmax and leaky'(y) at the argmax, which equals
+// leaky'(pooled max) (same value).  One thread per pooled pixel: the 4x4x3
+// input patch of its 2x2 conv outputs (zero outside the image through the
+// buffer range check), the two output rows as packed pairs (v_pk_fma_f32,
+// weights from the scalar cache), per output the summation order of
+// first_fwd2_k (bit-identical conv values), and po_maxpool2_fwd's window rule
+// (first position on ties, NaN wins).  Argmax byte: bits 0-1 window position,
+// bit 3 "LeakyReLU mask encoded", bit 2 set when the max is not positive
+// (slope 0.1 in the backward).  Pooled floats are staged through LDS for
+// fully coalesced 16-byte stores; each thread's CO argmax bytes are one or two
+// contiguous 16-byte stores.
+template <int CO>
+__global__ __launch_bounds__(256) void first_pool_fwd_k(const float* __restrict__ img, int B, int H, int W,
+                                                        int Hp, int Wp, const float* __restrict__ Wt,
+                                                        const float* __restrict__ bias, int Cout, int act,
+                                                        float* __restrict__ y, int8_t* __restrict__ am,
+                                                        uint32_t* __restrict__ amax) {
+  constexpr int LS = CO + 1;
+  __shared__ float ys[256 * LS];
+  const int npix = B * Hp * Wp;                     // < 2^31 (host check)
+  const int pbase = (int)blockIdx.x * 256;
+  const int tid = threadIdx.x;
+  const int p0 = pbase + tid;
+  const bool live = p0 < npix;
+  const int p = live ? p0 : 0;
+  const int b = p / (Hp * Wp);
+  const int rem = p - b * Hp * Wp;
+  const int py = rem / Wp, px = rem - py * Wp;
+  const uint32_t img_bytes = (uint32_t)((int64_t)B * 3 * H * W * 4);
+  const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(img), 0, img_bytes, 0x00020000);
+  constexpr uint32_t kOOB = 0x80000000u;
+  const uint32_t plane = (uint32_t)H * W * 4u;
+  const uint32_t ib = (uint32_t)b * 3u * plane;
+  // xp[c][r][q] = {x(row 2py-1+r, col 2px-1+q), x(row, col + 1)}: the operand
+  // pair of the two outputs (dx = 0, 1) of one output row at tap column q
+  f2_t xp[3][4][3];
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const int hi = 2 * py - 1 + r;
+    float xr[3][4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int wi = 2 * px - 1 + q;
+      const bool ok = live && (unsigned)hi < (unsigned)H && (unsigned)wi < (unsigned)W;
+      const uint32_t o = ib + ((uint32_t)hi * W + wi) * 4u;
+#pragma unroll
+      for (int c = 0; c < 3; ++c)
+        xr[c][q] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rs, ok ? o + c * plane : kOOB, 0, 0));
+    }
+#pragma unroll
+    for (int c = 0; c < 3; ++c)
+#pragma unroll
+      for (int q = 0; q < 3; ++q) xp[c][r][q] = (f2_t){xr[c][q], xr[c][q + 1]};
+  }
+  float vmax = 0.f;
+  uint32_t aw[CO / 4];
+#pragma unroll
+  for (int i = 0; i < CO / 4; ++i) aw[i] = 0u;
+#pragma unroll
+  for (int co = 0; co < CO; ++co) {
+    float bv = 0.f;
+    uint32_t code = 0u;
+    if (co < Cout) {                                 // wave-uniform
+      f2_t s0 = {0.f, 0.f}, s1 = {0.f, 0.f};
+#pragma unroll
+      for (int c = 0; c < 3; ++c)
+#pragma unroll
+        for (int kh = 0; kh < 3; ++kh)
+#pragma unroll
+          for (int kw = 0; kw < 3; ++kw) {
+            const f2_t w = (f2_t)(Wt[co * 27 + c * 9 + kh * 3 + kw]);
+            s0 = __builtin_elementwise_fma(w, xp[c][kh][kw], s0);
+            s1 = __builtin_elementwise_fma(w, xp[c][kh + 1][kw], s1);
+          }
+      const f2_t bb = (f2_t)(bias ? bias[co] : 0.f);
+      s0 += bb;
+      s1 += bb;
+      float v[4] = {s0[0], s0[1], s1[0], s1[1]};     // window positions k = 2 dy + dx
+      if (act) {
+#pragma unroll
+        for (int k = 0; k < 4; ++k) v[k] = po::leaky(v[k]);
+      }
+      bv = v[0];
+#pragma unroll
+      for (int k = 1; k < 4; ++k)
+        if (v[k] > bv || isnan(v[k])) { bv = v[k]; code = (uint32_t)k; }
+      if (act) code |= 8u | (bv > 0.f ? 0u : 4u);   // linear conv: no slope to apply
+    }
+    vmax = fmaxf(vmax, fabsf(bv));
+    ys[tid * LS + co] = bv;
+    aw[co >> 2] |= code << (8 * (co & 3));
+  }
+  if (amax) po::amax_commit(amax, live ? vmax : 0.f);
+  if (live) {
+    uint4* ap = reinterpret_cast<uint4*>(am + (int64_t)p0 * CO);
+#pragma unroll
+    for (int i = 0; i < CO / 16; ++i) ap[i] = make_uint4(aw[4 * i], aw[4 * i + 1], aw[4 * i + 2], aw[4 * i + 3]);
+  }
+  __syncthreads();
+  const int nlive = min(256, npix - pbase);
+  float* yb = y + (int64_t)pbase * CO;
+  for (int f = tid; f < nlive * (CO / 4); f += 256) {
+    const int q = f / (CO / 4), ch = (f % (CO / 4)) * 4;
+    const float* r = ys + q * LS + ch;
+    *reinterpret_cast<float4*>(yb + (int64_t)f * 4) = make_float4(r[0], r[1], r[2], r[3]);
+  }
+}
+
 template <int CO>
 __global__ __launch_bounds__(256) void first_dgrad_k(const float* __restrict__ D, int B, int H, int W,
                                                      int stride, int Ho, int Wo,
@@ -246,6 +357,28 @@ extern "C" int po_conv_first_fwd(const float* img, int B, int H, int W, int stri
   else
     hipLaunchKernelGGL(first_fwd_k<64>, grid, dim3(256), 0, st, img, B, H, W, stride, Ho, Wo, Wt, bias, Cout, Cout_p, act, y, amax);
   return po::check_launch("po_conv_first_fwd");
+}
+
+extern "C" int po_conv_first_pool_fwd(const float* img, int B, int H, int W, const float* Wt, const float* bias,
+                                      int Cout, int Cout_p, int act, float* y, int8_t* argmax, uint32_t* amax,
+                                      po_stream_t s) {
+  PO_REQUIRE(img && Wt && y && argmax, "po_conv_first_pool_fwd: null pointer");
+  PO_REQUIRE((Cout_p == 16 || Cout_p == 32) && Cout > 0 && Cout <= Cout_p,
+             "po_conv_first_pool_fwd: Cout_p must be 16 or 32 (got %d, Cout %d)", Cout_p, Cout);
+  PO_REQUIRE(B > 0 && H >= 2 && W >= 2, "po_conv_first_pool_fwd: bad size B=%d H=%d W=%d", B, H, W);
+  const int Hp = H / 2, Wp = W / 2;
+  const int64_t n = (int64_t)B * Hp * Wp;
+  PO_REQUIRE((int64_t)B * 3 * H * W * 4 < (1LL << 31) && n + 256 < (1LL << 31),
+             "po_conv_first_pool_fwd: image batch must be < 2 GiB");
+  hipStream_t st = po::stream_of(s);
+  dim3 grid(po::ceil_div(n, 256));
+  if (Cout_p == 16)
+    hipLaunchKernelGGL(first_pool_fwd_k<16>, grid, dim3(256), 0, st, img, B, H, W, Hp, Wp, Wt, bias, Cout, act, y,
+                       argmax, amax);
+  else
+    hipLaunchKernelGGL(first_pool_fwd_k<32>, grid, dim3(256), 0, st, img, B, H, W, Hp, Wp, Wt, bias, Cout, act, y,
+                       argmax, amax);
+  return po::check_launch("po_conv_first_pool_fwd");
 }
 
 extern "C" int po_conv_first_dgrad(const float* D, int B, int H, int W, int stride, const float* Wt,

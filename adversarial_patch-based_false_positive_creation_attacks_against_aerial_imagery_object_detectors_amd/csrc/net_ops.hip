@@ -153,6 +153,9 @@ __device__ __forceinline__ float mp_bwd_px(const float* __restrict__ dd, const i
                                            int x, int c, int H, int W, int C, int Cp, int stride, int Ho, int Wo,
                                            float* __restrict__ ds, int acc, const float* __restrict__ my) {
   float v[4] = {0.f, 0.f, 0.f, 0.f};
+  // argmax bytes of po_conv_first_pool_fwd carry the LeakyReLU slope of the
+  // (unstored) pool input at the argmax: bit 3 set, bit 2 = slope 0.1
+  float lg[4] = {1.f, 1.f, 1.f, 1.f};
 #pragma unroll
   for (int k = 0; k < 4; ++k) {
     const int ty = y - (k >> 1), tx = x - (k & 1);
@@ -162,10 +165,14 @@ __device__ __forceinline__ float mp_bwd_px(const float* __restrict__ dd, const i
     const int64_t o = (((int64_t)b * Ho + oy) * Wo + ox) * Cp + c;
     const char4 a = *reinterpret_cast<const char4*>(am + o);
     const float4 g = *reinterpret_cast<const float4*>(dd + o);
-    if (a.x == k) v[0] += g.x;
-    if (a.y == k) v[1] += g.y;
-    if (a.z == k) v[2] += g.z;
-    if (a.w == k) v[3] += g.w;
+    const int ak[4] = {a.x, a.y, a.z, a.w};
+    const float gk[4] = {g.x, g.y, g.z, g.w};
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+      if ((ak[u] & 3) == k) {
+        v[u] += gk[u];
+        if (ak[u] & 8) lg[u] = (ak[u] & 4) ? 0.1f : 1.f;
+      }
   }
 #pragma unroll
   for (int u = 0; u < 4; ++u)
@@ -179,6 +186,9 @@ __device__ __forceinline__ float mp_bwd_px(const float* __restrict__ dd, const i
     const float4 m = *reinterpret_cast<const float4*>(my + t);
     v[0] *= po::leaky_grad(m.x); v[1] *= po::leaky_grad(m.y);
     v[2] *= po::leaky_grad(m.z); v[3] *= po::leaky_grad(m.w);
+  } else {
+#pragma unroll
+    for (int u = 0; u < 4; ++u) v[u] *= lg[u];
   }
   *reinterpret_cast<float4*>(ds + t) = make_float4(v[0], v[1], v[2], v[3]);
   return fmaxf(fmaxf(fabsf(v[0]), fabsf(v[1])), fmaxf(fabsf(v[2]), fabsf(v[3])));

@@ -244,6 +244,14 @@ class NetPlan:
         self.first_direct = (first["type"] == "convolutional" and net._conv_meta[0]["k"] == 3
                              and net._conv_meta[0]["cin"] == 3 and net._conv_meta[0]["cout"] <= 64)
         self.in_nhwc = None if self.first_direct else torch.zeros(B, H, W, 16, device=dev)
+        # first conv (stride 1) whose only consumer is a k=2 stride-2 max pool
+        # (yolov3-tiny): one fused launch writes the pool output and its argmax
+        # (with the LeakyReLU slope encoded); the conv output is never stored
+        self.first_pool = (self.first_direct and n > 1 and net._conv_meta[0]["stride"] == 1
+                           and blocks[1]["type"] == "maxpool" and int(blocks[1]["stride"]) == 2
+                           and self.cp[0] in (16, 32) and self.win[0] is None and self.win[1] is None
+                           and [j for j in range(n) if 0 in srcs[j]] == [1]
+                           and os.environ.get("ADVPATCH_FIRST_POOL", "1") != "0")
         self._build_grad_plan()
         self.prec = 1 if net.conv_prec == "fp16x3" else 0
         self._build_slots()
@@ -646,6 +654,8 @@ class NetPlan:
         """bool [B, h, w, C]: output of leaky conv i > 0 — from the fp32
         activation, or from its sign bits when it is not stored."""
         C = self.shp[i][2]
+        if i == 0 and self.first_pool:
+            return None                         # not stored (fused into the pool: its argmax bytes)
         if i in self.y_dropped:
             bits = self.bits[self.act[i].data_ptr()]
             sh = torch.arange(32, device=bits.device, dtype=torch.int32)
@@ -714,6 +724,12 @@ class NetPlan:
                 y = self.act[i] if i not in self.fused else None
                 fuse_next = (i + 1) in self.fused
                 y_out = self.act[i]
+                if i == 0 and self.first_pool:
+                    args = (None, B, self.H, self.W, P(wts["w27"]), P(wts["bias"]), m["cout"], self.cp[i],
+                            1 if m["act"] == "leaky" else 0, P(self.act[1]), P(self.argmax[1]), self.slot(self.act[1]))
+                    fwd.append(("po_conv_first_pool_fwd", args, "img0"))
+                    assert not fuse_next
+                    continue
                 if i == 0 and self.first_direct:
                     args = (None, B, self.H, self.W, m["stride"], P(wts["w27"]), P(wts["bias"]), m["cout"],
                             self.cp[i], 1 if m["act"] == "leaky" else 0, P(y_out), self.slot(y_out))
@@ -789,6 +805,8 @@ class NetPlan:
                     fwd.append(("po_view_move", self._move(self.act[s], s, 0, self.act[i], i, 0, cs, 1, 0, None),
                                 None))
             elif t == "maxpool":
+                if i == 1 and self.first_pool:
+                    continue                    # fused into po_conv_first_pool_fwd
                 s = self.srcs[i][0]
                 hs, ws_, cs = self.shp[s]
                 fwd.append(("po_maxpool2_fwd", (P(self.act[s]), B, hs, ws_, cs, self.cp[s], int(d["stride"]),
@@ -910,6 +928,10 @@ class NetPlan:
             elif t == "maxpool":
                 s_ = self.srcs[j][0]
                 acc, mask, final = contrib(s_)
+                if j == 1 and self.first_pool:
+                    # the LeakyReLU slopes come from the argmax bytes (the conv output is not stored)
+                    assert acc == 0 and final
+                    mask = None
                 hs, ws_, cs = self.shp[s_]
                 # on a gradient-cone source only its per-image boxes are written
                 cone = self._cone_ptr(s_, 0)
@@ -1136,7 +1158,7 @@ class NetPlan:
         if not self.first_direct:
             nat.call("po_nchw_to_nhwc", xp, self.B, self.H, self.W, 3, 16, nat.c_void_p(self.in_nhwc.data_ptr()), st)
         for name, args, desc in self.fwd_ops:
-            if name == "po_conv_first_fwd":
+            if name in ("po_conv_first_fwd", "po_conv_first_pool_fwd"):
                 args = (xp,) + args[1:]
             self._launch(lib, name, args, desc, st)
         return [self.act[h] for h in self.heads]

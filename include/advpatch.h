@@ -33,7 +33,7 @@ typedef void* po_stream_t;
 #define PO_EHIP -2     /* HIP runtime error */
 #define PO_EDEVICE -3  /* device is not gfx950 */
 
-#define PO_ABI_VERSION 11
+#define PO_ABI_VERSION 12
 #define PO_AMAX_SUB 64  /* sub-slots per max|x| slot (see po_conv_desc) */
 
 int po_abi_version(void);
@@ -409,6 +409,16 @@ int po_conv(const po_conv_desc* d, const float* in, const float* W, const float*
 int po_conv_first_fwd(const float* img, int B, int H, int W, int stride, const float* Wt,
                       const float* bias, int Cout, int Cout_p, int act, float* y, uint32_t* amax,
                       po_stream_t s);
+/* po_conv_first_fwd (stride 1) followed by the k=2 stride-2 max pool, fused
+ * (yolov3-tiny's conv 3->16 + maxpool, darknet_v3.py:61-69; reference ops
+ * nn.Conv2d + nn.LeakyReLU + nn.MaxPool2d).  y [B,H/2,W/2,Cout_p] is the pool
+ * output and argmax [B,H/2,W/2,Cout_p] its window position (bits 0-1) as in
+ * po_maxpool2_fwd, plus (act = leaky) bit 3 set and bit 2 = (max <= 0): the conv output is
+ * not stored, and po_maxpool2_bwd / _bwd_box with mask_y == NULL apply the
+ * LeakyReLU slope encoded there (valid when the pool is the conv's only
+ * consumer).  Cout_p 16 or 32. */
+int po_conv_first_pool_fwd(const float* img, int B, int H, int W, const float* Wt, const float* bias, int Cout,
+                           int Cout_p, int act, float* y, int8_t* argmax, uint32_t* amax, po_stream_t s);
 /* Its input gradient: d_img[b,c,h,w] (NCHW) from D [B,Ho,Wo,Cout_p] (already
  * multiplied by leaky'), W [Cout][27].  roi (may be NULL) [B,4] int32
  * {x0,y0,x1,y1}: only pixels x0<=w<x1, y0<=h<y1 of image b are computed (the

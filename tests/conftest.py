@@ -54,7 +54,10 @@ def plan_branches(plan):
     for i, d in enumerate(plan.net.blocks):
         C = plan.shp[i][2]
         if d["type"] == "convolutional" and plan._leaky(i):
-            pos = plan.leaky_signs(i).permute(0, 3, 1, 2).cpu()
+            sg = plan.leaky_signs(i)
+            if sg is None:          # not stored (first conv fused into its max pool): the oracle decides
+                continue
+            pos = sg.permute(0, 3, 1, 2).cpu()
             if plan.win[i] is not None:
                 H, W = plan.shp[i][:2]
                 full = torch.full((plan.B, C, H, W), -1, dtype=torch.int8)
@@ -66,7 +69,8 @@ def plan_branches(plan):
             br[i] = ("leaky", pos)
         elif d["type"] == "maxpool":
             assert plan.win[i] is None
-            br[i] = ("maxpool", plan.argmax[i][..., :C].permute(0, 3, 1, 2).long().cpu())
+            # bits 0-1: window position (bits 2-3 of a fused first conv + pool: its LeakyReLU slope)
+            br[i] = ("maxpool", (plan.argmax[i][..., :C].long() & 3).permute(0, 3, 1, 2).cpu())
     return br
 
 

@@ -105,3 +105,53 @@ def test_warp_fwd_quad_kernel_bit_identical(mode):
         outs.append(out)
     assert torch.equal(outs[0], outs[1])
     assert (outs[0] != (img if mode == 1 else 0)).any()      # the patch landed somewhere
+
+
+@pytest.mark.parametrize("B,H,W,cout", [(2, 38, 54, 32), (3, 29, 31, 16), (1, 64, 64, 16), (2, 17, 20, 13)])
+def test_first_pool_fused_matches_conv_then_pool(B, H, W, cout):
+    """po_conv_first_pool_fwd (yolov3-tiny's conv 3->16 + maxpool 2/2,
+    darknet_v3.py:61-69) writes the pool output po_conv_first_fwd +
+    po_maxpool2_fwd write, bit for bit, and the same window positions; its
+    argmax bytes carry the LeakyReLU slope, so po_maxpool2_bwd without the
+    conv output gives the gradient that the unfused backward (mask = conv
+    output) gives.  Odd sizes (the last row/column in no window), a ragged
+    last workgroup and Cout < Cout_p are covered."""
+    nat = pkg_mod("_native")
+    dev = torch.device("cuda", 0)
+    g = torch.Generator().manual_seed(B * 100 + H + W)
+    cp = 16 if cout <= 16 else 32
+    img = torch.rand(B, 3, H, W, generator=g).to(dev)
+    w27 = (torch.randn(cout, 27, generator=g) * 0.3).to(dev)
+    b = (torch.randn(cout, generator=g) * 0.1).to(dev)
+    Hp, Wp = H // 2, W // 2
+    for act in (0, 1):
+        y, _ = _run(img, w27, b, 1, cp, act)
+        pooled = torch.full((B, Hp, Wp, cp), float("nan"), device=dev)
+        am = torch.full((B, Hp, Wp, cp), -1, dtype=torch.int8, device=dev)
+        nat.call("po_maxpool2_fwd", nat.ptr(y), B, H, W, cout, cp, 2, nat.ptr(pooled), nat.ptr(am, torch.int8), None,
+                 nat.stream())
+        fp = torch.full_like(pooled, float("nan"))
+        fam = torch.full_like(am, -1)
+        amax = torch.zeros(nat.PO_AMAX_SUB, dtype=torch.int32, device=dev)
+        nat.call("po_conv_first_pool_fwd", nat.ptr(img), B, H, W, nat.ptr(w27), nat.ptr(b), cout, cp, act,
+                 nat.ptr(fp), nat.ptr(fam, torch.int8), nat.ptr(amax, torch.int32), nat.stream())
+        torch.cuda.synchronize()
+        assert torch.equal(fp, pooled), "fused pool output differs from conv + po_maxpool2_fwd"
+        assert torch.equal(fam.long()[..., :cout] & 3, am.long()[..., :cout])
+        code = fam.long()[..., :cout]
+        if act:
+            assert bool(((code & 8) == 8).all())
+            assert torch.equal((code & 4) == 4, pooled[..., :cout] <= 0)
+        else:
+            assert bool((code < 4).all())
+        assert amax.view(torch.float32).max().item() == pooled.abs().max().item()
+        # backward: leaky' from the argmax bytes == leaky' from the stored conv output
+        dd = torch.randn(B, Hp, Wp, cp, generator=g).to(dev)
+        d_ref = torch.full((B, H, W, cp), float("nan"), device=dev)
+        d_fus = torch.full_like(d_ref, float("nan"))
+        nat.call("po_maxpool2_bwd", nat.ptr(dd), nat.ptr(am, torch.int8), B, H, W, cout, cp, 2, nat.ptr(d_ref), 0,
+                 nat.ptr(y) if act else None, None, nat.stream())
+        nat.call("po_maxpool2_bwd", nat.ptr(dd), nat.ptr(fam, torch.int8), B, H, W, cout, cp, 2, nat.ptr(d_fus), 0,
+                 None, None, nat.stream())
+        torch.cuda.synchronize()
+        assert torch.equal(d_fus, d_ref)

@@ -26,7 +26,7 @@ def rows(sub, pattern):
 
 
 def is_main(name):
-    return ("conv_k" in name or "conv_h3" in name) and "reduce" not in name
+    return ("conv_k" in name or "conv_h3" in name or "conv_wino" in name) and "reduce" not in name
 
 
 def conv_dispatches(rs, key):
@@ -34,7 +34,7 @@ def conv_dispatches(rs, key):
     seen = {}
     for r in rs:
         nm = r["Kernel_Name"]
-        if "conv_" in nm and ("conv_k" in nm or "conv_h3" in nm or "conv_reduce_k" in nm):
+        if "conv_" in nm and ("conv_k" in nm or "conv_h3" in nm or "conv_wino" in nm or "conv_reduce_k" in nm):
             seen[int(r[key])] = nm
     return sorted(seen.items())
 
