@@ -537,7 +537,7 @@ class DotaDataset(torch.utils.data.Dataset):
     ``imgsize``, labels ``cls x y w h`` normalised and padded to ``max_lab``
     rows with 1e-6; an empty label file becomes one row of ones(5)."""
 
-    def __init__(self, img_dir, lab_dir, max_lab, imgsize, shuffle=True):
+    def __init__(self, img_dir, lab_dir, max_lab, imgsize, shuffle=True, as_uint8=False):
         names = fnmatch.filter(os.listdir(img_dir), "*.png") + fnmatch.filter(os.listdir(img_dir), "*.jpg")
         n_labels = len(fnmatch.filter(os.listdir(lab_dir), "*.txt"))
         assert len(names) == n_labels, "Number of images and number of labels does't match"
@@ -548,6 +548,10 @@ class DotaDataset(torch.utils.data.Dataset):
         self.img_paths = [os.path.join(img_dir, n) for n in names]
         self.lab_paths = [os.path.join(lab_dir, n).replace(".jpg", ".txt").replace(".png", ".txt") for n in names]
         self.max_n_labels = max_lab
+        # as_uint8: images come out as uint8 [3,S,S] (a quarter of the bytes through the
+        # worker queues, pinning and the PCIe copy); DevicePrefetcher divides by 255 on
+        # the device, which gives the same floats as ToTensor's division on the host
+        self.as_uint8 = as_uint8
 
     def __len__(self):
         return self.len
@@ -565,7 +569,11 @@ class DotaDataset(torch.utils.data.Dataset):
         if label.dim() == 1:
             label = label.unsqueeze(0)
         image, label = self.pad_and_scale(image, label)
-        image = torch.from_numpy(np.asarray(image, dtype=np.uint8).copy()).permute(2, 0, 1).float().div_(255.0)
+        image = torch.from_numpy(np.asarray(image, dtype=np.uint8).copy()).permute(2, 0, 1)
+        if not self.as_uint8:
+            image = image.float().div_(255.0)
+        else:
+            image = image.contiguous()
         return image, self.pad_lab(label)
 
     def pad_and_scale(self, img, lab):
@@ -593,3 +601,110 @@ class DotaDataset(torch.utils.data.Dataset):
         if pad_size > 0:
             return F.pad(lab, (0, 0, 0, pad_size), value=1e-6)
         return lab
+
+
+class DevicePrefetcher:
+    """Host->device feed of the training loop (the reference copies each batch
+    with a blocking ``.cuda()``, train_patch.py:164-166).  The copy of batch
+    k+1 (pinned source, non-blocking, on a side stream) is issued before batch
+    k is handed out, so it overlaps batch k's step instead of sitting between
+    two steps on the compute stream; the compute stream waits on an event only
+    when it takes the batch.  uint8 image batches (DotaDataset(as_uint8=True))
+    become float32 / 255 on the device, bit-identical to ToTensor on the host
+    (both are one correctly rounded fp32 division).  Batches that are already
+    on the device pass through; without a GPU it only applies the conversion."""
+
+    def __init__(self, loader, device):
+        self.loader, self.device = loader, torch.device(device)
+
+    def __len__(self):
+        return len(self.loader)
+
+    @staticmethod
+    def _to_float(img):
+        return img.float().div_(255.0) if img.dtype == torch.uint8 else img
+
+    def __iter__(self):
+        if self.device.type != "cuda":
+            for img, lab in self.loader:
+                yield self._to_float(img.to(self.device)), lab.to(self.device)
+            return
+        side = torch.cuda.Stream(self.device)
+        main = torch.cuda.current_stream(self.device)
+        it = iter(self.loader)
+
+        def issue():
+            try:
+                img, lab = next(it)
+            except StopIteration:
+                return None
+            side.wait_stream(main)        # buffers freed by earlier steps are reusable on the side stream
+            with torch.cuda.stream(side):
+                img = self._to_float(img.to(self.device, non_blocking=True))
+                lab = lab.to(self.device, non_blocking=True)
+                ev = torch.cuda.Event()
+                ev.record(side)
+            return img, lab, ev
+
+        nxt = issue()
+        while nxt is not None:
+            img, lab, ev = nxt
+            main.wait_event(ev)
+            img.record_stream(main)
+            lab.record_stream(main)
+            nxt = issue()
+            yield img, lab
+
+
+
+class FrameCache:
+    """Decoded training frames resident in device memory.  DotaDataset's
+    transform (PNG decode, grey pad, bilinear resize, label padding;
+    load_data.py:910-978) is deterministic and every augmentation happens later
+    on the GPU (PatchTransformer), so each frame is decoded ONCE — by a
+    DataLoader over the host workers — and kept as uint8 [N,3,S,S] plus float
+    labels [N,L,5] in HBM (1.1 MB per 608x608 frame: a 20k-frame set is 22 GB of
+    a MI355X's 288 GB).  Every epoch after that gathers its batches on the
+    device (index_select + /255, the same floats as ToTensor), so the host
+    decode rate (tens of frames/s per core) no longer bounds the step rate."""
+
+    def __init__(self, dataset, device, num_workers=8, batch=32):
+        ds = dataset
+        if not getattr(ds, "as_uint8", False):
+            raise ValueError("FrameCache needs DotaDataset(..., as_uint8=True)")
+        self.device = torch.device(device)
+        n, S, L = len(ds), ds.imgsize, ds.max_n_labels
+        self.frames = torch.empty(n, 3, S, S, dtype=torch.uint8, device=self.device)
+        self.labels = torch.empty(n, L, 5, dtype=torch.float32, device=self.device)
+        dl = torch.utils.data.DataLoader(ds, batch_size=batch, shuffle=False, num_workers=num_workers,
+                                         pin_memory=self.device.type == "cuda")
+        k = 0
+        for img, lab in dl:
+            m = img.size(0)
+            self.frames[k:k + m].copy_(img, non_blocking=True)
+            self.labels[k:k + m].copy_(lab, non_blocking=True)
+            k += m
+        assert k == n
+        if self.device.type == "cuda":
+            torch.cuda.current_stream(self.device).synchronize()
+
+    def __len__(self):
+        return self.frames.size(0)
+
+    def batch(self, indices):
+        """(img [b,3,S,S] float32 in [0,1], lab [b,L,5]) of dataset rows ``indices``, on the device."""
+        idx = torch.as_tensor(indices, dtype=torch.long).to(self.device, non_blocking=True)
+        return self.frames.index_select(0, idx).float().div_(255.0), self.labels.index_select(0, idx)
+
+    def loader(self, batch_sampler):
+        """Iterable of device batches in ``batch_sampler``'s order (a fresh pass per iter())."""
+        cache = self
+
+        class _It:
+            def __len__(self):
+                return len(batch_sampler)
+
+            def __iter__(self):
+                for b in batch_sampler:
+                    yield cache.batch(b)
+        return _It()

@@ -49,8 +49,8 @@ from . import patch_config
 from . import synthetic
 from . import weights as synth_weights
 from .darknet_v3 import Darknet
-from .load_data import (DotaDataset, HasSusRGB, NPSCalculator, PatchApplier, PatchTransformer,
-                        TotalVariation, read_image as _read_image, regularisers)
+from .load_data import (DevicePrefetcher, DotaDataset, FrameCache, HasSusRGB, NPSCalculator, PatchApplier,
+                        PatchTransformer, TotalVariation, read_image as _read_image, regularisers)
 
 TV_FACTOR = 2.5      # train_patch.py:25
 NPS_FACTOR = 0.01    # train_patch.py:26
@@ -346,13 +346,15 @@ class PatchTrainer(object):
 
     # ------------------------------------------------------------------
     def train(self, max_n_epochs=401, save_dir="training_patches_saves/trained_patches", num_workers=10,
-              data=None, seed=0):
+              data=None, seed=0, cache_frames=None):
         """Optimise a patch on the configured dataset (train_patch.py:85-389).
         ``config.batch_size`` is the GLOBAL batch, as in the reference; under
         torchrun every rank loads its contiguous shard of each global batch
         (GlobalBatchSampler).  ``data``: optional iterable of (img_batch,
         lab_batch) replacing the DataLoader (under torchrun: this rank's
-        equal shards)."""
+        equal shards).  ``cache_frames``: decode the dataset once into device
+        memory (FrameCache) instead of every epoch; None = when the uint8
+        frames take at most a quarter of the free device memory."""
         img_size = self.darknet_model.height
         batch_size = self.config.batch_size
         max_lab = 252
@@ -365,12 +367,19 @@ class PatchTrainer(object):
                 len(fnmatch.filter(os.listdir(self.config.img_dir), "*.jpg"))
             if self.verbose and rank0:
                 print("Total images in TrainSet : ", n_images)
-            ds = DotaDataset(self.config.img_dir, self.config.lab_dir, max_lab, img_size, shuffle=True)
+            ds = DotaDataset(self.config.img_dir, self.config.lab_dir, max_lab, img_size, shuffle=True, as_uint8=True)
             sampler = GlobalBatchSampler(len(ds), batch_size, self.rank, self.world, shuffle=True, seed=seed)
-            loader = torch.utils.data.DataLoader(ds, batch_sampler=sampler, num_workers=num_workers,
-                                                 pin_memory=True, persistent_workers=num_workers > 0)
+            if cache_frames is None:
+                need = len(ds) * (3 * img_size * img_size + max_lab * 5 * 4)
+                cache_frames = self.device.type == "cuda" and need <= torch.cuda.mem_get_info(self.device)[0] // 4
+            if cache_frames:
+                loader = FrameCache(ds, self.device, num_workers=num_workers).loader(sampler)
+            else:
+                loader = DevicePrefetcher(torch.utils.data.DataLoader(
+                    ds, batch_sampler=sampler, num_workers=num_workers, pin_memory=True,
+                    persistent_workers=num_workers > 0), self.device)
         else:
-            loader = data
+            loader = DevicePrefetcher(data, self.device)
         optimizer = self.make_optimizer(adv_patch)
         scheduler = self.config.scheduler_factory(optimizer)
         ep_loss_list = []
@@ -384,8 +393,6 @@ class PatchTrainer(object):
             nb = 0
             et0 = time.time()
             for k, (img_batch, lab_batch) in enumerate(loader):
-                img_batch = img_batch.to(self.device, non_blocking=True)
-                lab_batch = lab_batch.to(self.device, non_blocking=True)
                 weights = None
                 if sampler is not None:
                     lo, hi, ng = sampler.shard_of(k)

@@ -126,3 +126,41 @@ def test_dota_dataset_padding_and_labels(tmp_path):
     dl = torch.utils.data.DataLoader(ds, batch_size=3, shuffle=False)
     ib, lb = next(iter(dl))
     assert ib.shape == (3, 3, S, S) and lb.shape == (3, L, 5)
+
+
+def test_dota_uint8_loader_and_prefetcher_match_float_path(tmp_path):
+    """The training loader's uint8 path (DotaDataset(as_uint8=True) through a
+    2-worker DataLoader with GlobalBatchSampler, then DevicePrefetcher's /255)
+    yields exactly the float batches of the reference path
+    (load_data.py:910-978: ToTensor on the host)."""
+    ld, tp = pkg_mod("load_data"), pkg_mod("train_patch")
+    img_dir, lab_dir = tmp_path / "images", tmp_path / "labels"
+    img_dir.mkdir()
+    lab_dir.mkdir()
+    rng = np.random.default_rng(3)
+    for k in range(7):
+        h, w = int(rng.integers(20, 50)), int(rng.integers(20, 50))
+        _write(str(img_dir / ("im%d.png" % k)), rng.integers(0, 256, (h, w, 3), dtype=np.uint8))
+        (lab_dir / ("im%d.txt" % k)).write_text("%d 0.5 0.5 0.2 0.1\n" % k if k % 3 else "")
+    S, L = 48, 252
+    ref = ld.DotaDataset(str(img_dir), str(lab_dir), L, S, shuffle=False)
+    u8 = ld.DotaDataset(str(img_dir), str(lab_dir), L, S, shuffle=False, as_uint8=True)
+    smp = tp.GlobalBatchSampler(len(u8), 3, shuffle=True, seed=5)
+    loader = torch.utils.data.DataLoader(u8, batch_sampler=smp, num_workers=2)
+    got = list(ld.DevicePrefetcher(loader, "cpu"))
+    order = [i for b in smp for i in b]
+    assert len(got) == 3 and sum(g[0].size(0) for g in got) == 7
+    flat_img = torch.cat([g[0] for g in got])
+    flat_lab = torch.cat([g[1] for g in got])
+    assert flat_img.dtype == torch.float32
+    for row, i in enumerate(order):
+        img, lab = ref[i]
+        assert torch.equal(flat_img[row], img)
+        assert torch.equal(flat_lab[row], lab)
+    # the decoded-once frame cache gives the same batches, every pass
+    cache = ld.FrameCache(u8, "cpu", num_workers=2, batch=4)
+    for _ in range(2):
+        again = list(cache.loader(smp))
+        assert len(again) == len(got)
+        for (a, b), (c, d) in zip(again, got):
+            assert torch.equal(a, c) and torch.equal(b, d)

@@ -257,3 +257,42 @@ def test_cache_mode_runs_are_bit_reproducible(yolo_weights, monkeypatch):
         outs.append((pg.grad.cpu(), float(loss)))
     assert torch.equal(outs[0][0], outs[1][0])
     assert outs[0][1] == outs[1][1]
+
+
+def test_train_on_disk_loader_matches_data_iterable(tmp_path, yolo_weights, monkeypatch):
+    """PatchTrainer.train() on a DOTA-style folder, two epochs: the device
+    frame cache (decoded once, batches gathered in HBM) and the streaming path
+    (DotaDataset(as_uint8=True), 2 DataLoader workers, pinned batches,
+    DevicePrefetcher side-stream copies, on-device /255) end at the same patch
+    and epoch losses bit for bit; the first epoch equals train() fed the
+    reference path's float batches (load_data.py:910-978) in the sampler's
+    order through ``data=``."""
+    from PIL import Image
+    monkeypatch.setenv("ADVPATCH_TUNE", "0")        # built-in tiles: the same summation order in every run
+    ld, tp = pkg_mod("load_data"), pkg_mod("train_patch")
+    img_dir, lab_dir = tmp_path / "images", tmp_path / "labels"
+    img_dir.mkdir()
+    lab_dir.mkdir()
+    rng = np.random.default_rng(11)
+    for k in range(10):
+        h, w = int(rng.integers(40, 90)), int(rng.integers(40, 90))
+        Image.fromarray(rng.integers(0, 256, (h, w, 3), dtype=np.uint8), "RGB").save(str(img_dir / ("f%d.png" % k)))
+        (lab_dir / ("f%d.txt" % k)).write_text("1 0.5 0.5 0.3 0.2\n4 0.3 0.6 0.1 0.1\n" if k % 4 else "")
+    runs = []
+    for mode in ("cache", "disk", "iterable"):
+        tr = _trainer("builtin:mini3", yolo_weights + ".mini3", batch=4)
+        tr.config.img_dir, tr.config.lab_dir = str(img_dir), str(lab_dir)
+        tr.config.patch_size = 32                  # mini3 frames are 64x64
+        data = None
+        if mode == "iterable":
+            S = tr.darknet_model.height
+            ref = ld.DotaDataset(str(img_dir), str(lab_dir), 252, S, shuffle=False)
+            smp = tp.GlobalBatchSampler(len(ref), 4, shuffle=True, seed=0)
+            data = [(torch.stack([ref[i][0] for i in b]), torch.stack([ref[i][1] for i in b])) for b in smp]
+        patch, losses = tr.train(max_n_epochs=2, data=data, save_dir=None,
+                                 num_workers=2, cache_frames=(mode == "cache"))
+        runs.append((patch, losses))
+    # epoch 2 of the iterable run repeats epoch 1's order; the loaders reshuffle (set_epoch):
+    # compare the first epoch's loss and run the disk loaders against each other over both
+    assert runs[0][1] == runs[1][1] and torch.equal(runs[0][0], runs[1][0])
+    assert runs[0][1][0] == runs[2][1][0]
