@@ -506,13 +506,75 @@ __global__ __launch_bounds__(256) void warp_bwd_a_k(const float* __restrict__ d_
   }
 }
 
+// Phase A with four consecutive pixels of a row per thread (S % 4 == 0), as
+// warp_fwd4_k: a quarter of the threads of warp_bwd_a_k over the full frame;
+// a quad with a footprint pixel loads d_out and stores gfac as 16-byte
+// vectors (0 at its non-footprint pixels, which phase B never reads).  The
+// per-pixel arithmetic is warp_bwd_a_k's (bit-identical factors).
+__global__ __launch_bounds__(256) void warp_bwd_a4_k(const float* __restrict__ d_out,
+                                                     const float* __restrict__ mp,
+                                                     const float* __restrict__ noise,
+                                                     const float* __restrict__ contrast,
+                                                     const float* __restrict__ bright,
+                                                     const double* __restrict__ affine, WarpGeom g,
+                                                     int mode, float* __restrict__ gfac) {
+  const int b = blockIdx.y;
+  const int sq = g.S >> 2;
+  const int q = blockIdx.x * 256 + threadIdx.x;
+  if (q >= g.S * sq) return;
+  const int i = q / sq, j0 = (q - i * sq) * 4;
+  const size_t plane = (size_t)g.S * g.S;
+  const size_t o = (size_t)b * 3 * plane + (size_t)i * g.S + j0;
+  const double* th = affine + 6 * b;
+  const float* nz = noise + (size_t)b * 3 * g.P * g.P;
+  const float cb = contrast[b], bb = bright[b];
+  float adv[4][3], msk[4];
+  bool rng[4][3], hit[4];
+  bool any = false;
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {
+    hit[u] = warp_pixel(th, g, mp, nz, cb, bb, i, j0 + u, adv[u], msk[u], rng[u]);
+    any |= hit[u];
+  }
+  if (!any) return;
+#pragma unroll
+  for (int ch = 0; ch < 3; ++ch) {
+    const float4 d4 = *reinterpret_cast<const float4*>(d_out + o + ch * plane);
+    const float dv[4] = {d4.x, d4.y, d4.z, d4.w};
+    float gv[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const float out = adv[u][ch] * msk[u];
+      float t = dv[u];
+      if (mode == 1 && out == 0.f) t = 0.f;
+      t = t * msk[u];
+      if (!rng[u][ch]) t = 0.f;
+      gv[u] = hit[u] ? t : 0.f;
+    }
+    *reinterpret_cast<float4*>(gfac + o + ch * plane) = make_float4(gv[0], gv[1], gv[2], gv[3]);
+  }
+}
+
 // Backward phase B: per patch element (pr, pc), gather over images and over the
 // output pixels whose bilinear footprint covers padded-input pixel (pr+padT, pc+padL).
 // A workgroup holds WB_EL patch elements x WB_G image groups: group q sums the
 // images q, q + WB_G, ... in increasing order, then the WB_G partials are added
 // in group order through LDS (deterministic, no atomics, no workspace); the
 // batch is spread over WB_G x more workgroups than one thread per element.
+// SCAN 1: only the output pixels whose sample point lies in [c-1, c+1) x
+// [r-1, r+1) can have (r, c) as a corner, so the scan covers the integer
+// points of that square's preimage box (from the inverse map with one
+// division per image; +-1e-6 px against its rounding) instead of the box
+// widened by one pixel on each side (SCAN 0, PO_WARP_BWD_WIDE=1): for a
+// down-scaled patch (an output pixel spans several patch pixels) that is ~0-1
+// candidate pixels per (element, image) instead of >= 9.  The skipped pixels
+// fail the corner test anyway, so the contributions and their order (rows,
+// then columns) are unchanged: bit-identical to the wide scan.  (A fused
+// single pass that recomputes phase A at each candidate instead of reading
+// gfac measured 477 us against 165 + 159 us on tiny B=256: each footprint
+// pixel is the candidate of 4 corners, and warp_pixel's 24 gathers dominate.)
 constexpr int WB_EL = 32, WB_G = 8;
+template <int SCAN>
 __global__ __launch_bounds__(256) void warp_bwd_b_k(const float* __restrict__ gfac,
                                                     const float* __restrict__ mp,
                                                     const float* __restrict__ noise,
@@ -536,18 +598,38 @@ __global__ __launch_bounds__(256) void warp_bwd_b_k(const float* __restrict__ gf
     const double A00 = af[0], A01 = af[1], A02 = af[2], A10 = af[3], A11 = af[4], A12 = af[5];
     const double det = A00 * A11 - A01 * A10;
     double jlo = 1e30, jhi = -1e30, ilo = 1e30, ihi = -1e30;
+    if (SCAN == 1) {
+      const double inv = 1.0 / det;
+      const double m00 = A11 * inv, m01 = -A01 * inv, m10 = -A10 * inv, m11 = A00 * inv;
+      const double X = (double)c - A02, Y = (double)r - A12;
+      const double jc = m00 * X + m01 * Y, ic = m10 * X + m11 * Y;
+      const double hj = fabs(m00) + fabs(m01), hi_ = fabs(m10) + fabs(m11);
+      jlo = jc - hj; jhi = jc + hj;
+      ilo = ic - hi_; ihi = ic + hi_;
+    } else {
 #pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      const double X = (double)c + ((k & 1) ? 1.0 : -1.0) - A02;
-      const double Y = (double)r + ((k & 2) ? 1.0 : -1.0) - A12;
-      const double jj = (A11 * X - A01 * Y) / det;
-      const double ii = (-A10 * X + A00 * Y) / det;
-      jlo = fmin(jlo, jj); jhi = fmax(jhi, jj);
-      ilo = fmin(ilo, ii); ihi = fmax(ihi, ii);
+      for (int k = 0; k < 4; ++k) {
+        const double X = (double)c + ((k & 1) ? 1.0 : -1.0) - A02;
+        const double Y = (double)r + ((k & 2) ? 1.0 : -1.0) - A12;
+        const double jj = (A11 * X - A01 * Y) / det;
+        const double ii = (-A10 * X + A00 * Y) / det;
+        jlo = fmin(jlo, jj); jhi = fmax(jhi, jj);
+        ilo = fmin(ilo, ii); ihi = fmax(ihi, ii);
+      }
     }
     if (!(jhi >= -1.0 && jlo <= (double)g.S && ihi >= -1.0 && ilo <= (double)g.S)) continue;
-    const int j0 = max(0, (int)floor(jlo) - 1), j1 = min(g.S - 1, (int)ceil(jhi) + 1);
-    const int i0 = max(0, (int)floor(ilo) - 1), i1 = min(g.S - 1, (int)ceil(ihi) + 1);
+    int j0, j1, i0, i1;
+    const double hiS = (double)(g.S - 1);
+    if (SCAN > 0) {
+      constexpr double eps = 1e-6;
+      j0 = (int)fmax(0.0, ceil(jlo - eps)); j1 = (int)fmin(hiS, floor(jhi + eps));
+      i0 = (int)fmax(0.0, ceil(ilo - eps)); i1 = (int)fmin(hiS, floor(ihi + eps));
+    } else {
+      j0 = (int)fmax(0.0, floor(jlo) - 1.0); j1 = (int)fmin(hiS, ceil(jhi) + 1.0);
+      i0 = (int)fmax(0.0, floor(ilo) - 1.0); i1 = (int)fmin(hiS, ceil(ihi) + 1.0);
+    }
+    const float cb = contrast[b], bb = bright[b];
+    const float* nz = noise + (size_t)b * 3 * g.P * g.P;
     float a0 = 0.f, a1 = 0.f, a2 = 0.f;
     const float* gb = gfac + (size_t)b * 3 * plane;
     for (int i = i0; i <= i1; ++i)
@@ -561,13 +643,12 @@ __global__ __launch_bounds__(256) void warp_bwd_b_k(const float* __restrict__ gf
         if (dx < 0 || dx > 1 || dy < 0 || dy > 1) continue;
         const float w = wb[2 * dy + dx];
         const size_t o = (size_t)i * g.S + j;
-        a0 += w * gb[o];
-        a1 += w * gb[o + plane];
-        a2 += w * gb[o + 2 * plane];
+        const float gv[3] = {gb[o], gb[o + plane], gb[o + 2 * plane]};
+        a0 += w * gv[0];
+        a1 += w * gv[1];
+        a2 += w * gv[2];
       }
     // through clamp(adv*contrast + bright + noise) and * contrast, summed over images
-    const float cb = contrast[b], bb = bright[b];
-    const float* nz = noise + (size_t)b * 3 * g.P * g.P;
     const float av[3] = {a0, a1, a2};
     float dd[3];
 #pragma unroll
@@ -669,13 +750,25 @@ extern "C" int po_warp_bwd(const float* d_out, const float* patch_mp, const floa
   PO_REQUIRE(mode == 0 || mode == 1, "po_warp_bwd: mode must be 0 or 1");
   PO_REQUIRE(B > 0 && S > 1 && P > 0 && P <= S, "po_warp_bwd: bad shape");
   WarpGeom g = make_geom(S, P);
-  dim3 grid(po::ceil_div(S, 256), S, B);
-  hipLaunchKernelGGL(warp_bwd_a_k, grid, dim3(256), 0, po::stream_of(s), d_out, patch_mp, noise,
-                     contrast, bright, affine, g, mode, work);
+  const bool quad = S % 4 == 0 && ((uintptr_t)d_out | (uintptr_t)work) % 16 == 0 && work != d_out &&
+                    !getenv("PO_WARP_V1");
+  if (quad) {
+    hipLaunchKernelGGL(warp_bwd_a4_k, dim3(po::ceil_div(S * (S / 4), 256), B), dim3(256), 0, po::stream_of(s), d_out,
+                       patch_mp, noise, contrast, bright, affine, g, mode, work);
+  } else {
+    dim3 grid(po::ceil_div(S, 256), S, B);
+    hipLaunchKernelGGL(warp_bwd_a_k, grid, dim3(256), 0, po::stream_of(s), d_out, patch_mp, noise,
+                       contrast, bright, affine, g, mode, work);
+  }
   int rc = po::check_launch("po_warp_bwd(a)");
   if (rc) return rc;
-  hipLaunchKernelGGL(warp_bwd_b_k, dim3(po::ceil_div(P * P, WB_EL)), dim3(256), 0, po::stream_of(s),
-                     work, patch_mp, noise, contrast, bright, affine, g, B, d_patch_mp);
+  dim3 gridb(po::ceil_div(P * P, WB_EL));
+  if (getenv("PO_WARP_BWD_WIDE"))
+    hipLaunchKernelGGL(warp_bwd_b_k<0>, gridb, dim3(256), 0, po::stream_of(s), work, patch_mp, noise, contrast,
+                       bright, affine, g, B, d_patch_mp);
+  else
+    hipLaunchKernelGGL(warp_bwd_b_k<1>, gridb, dim3(256), 0, po::stream_of(s), work, patch_mp, noise, contrast,
+                       bright, affine, g, B, d_patch_mp);
   return po::check_launch("po_warp_bwd(b)");
 }
 
