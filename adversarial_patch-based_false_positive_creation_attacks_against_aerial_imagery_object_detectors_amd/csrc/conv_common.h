@@ -42,6 +42,8 @@ struct ConvArgs {
   int in_step, out_step, out_oy, out_ox;
   int ntaps, N, act, accumulate;
   int M, ntiles_n;
+  int mrows;                    // GEMM rows per image: Hg*Wg, or fewer with gbox (a compact grid over each
+                                // image's box of at most mrows points: see grid_point)
   uint32_t in_bytes, w_bytes;   // buffer-resource extents (< 2^31)
   // taps form a rectangular grid: tap t = th*tkw + tw -> (dh0 + th*sdh, dw0 + tw*sdw)
   int tkw, dh0, dw0, sdh, sdw;
@@ -58,10 +60,11 @@ __device__ __forceinline__ int input_shift(const ConvArgs& a) {
   return min(max(13 - e, -120), 120);
 }
 
-// ---- launch-grid enumeration.  GEMM row m is image b = m / (Hg*Wg) and, in
-// that image, grid point l = m % (Hg*Wg): row-major over the whole Hg x Wg
-// grid, or (a.gbox set) row-major over the image's box only, the rows past the
-// box's area computing nothing.  Grid point (i, j) writes destination pixel
+// ---- launch-grid enumeration.  GEMM row m is image b = m / mrows and, in
+// that image, grid point l = m % mrows: row-major over the whole Hg x Wg grid
+// (mrows = Hg*Wg), or (a.gbox set) row-major over the image's box only, the
+// rows past the box's area computing nothing (mrows < Hg*Wg when every box is
+// known to hold at most mrows points: the launch has no dead rows to spare).  Grid point (i, j) writes destination pixel
 // (i*out_step + out_oy, j*out_step + out_ox).
 struct GridBox {
   int i0, j0, h, w;
@@ -83,7 +86,7 @@ __device__ __forceinline__ GridBox grid_box(const ConvArgs& a, int b) {
 }
 // GEMM row m -> image b and grid point (i, j); false: the row computes nothing
 __device__ __forceinline__ bool grid_point(const ConvArgs& a, int m, int& b, int& i, int& j) {
-  const int HgWg = a.Hg * a.Wg;
+  const int HgWg = a.mrows;
   if (m >= a.M) {
     b = i = j = 0;
     return false;
@@ -108,7 +111,7 @@ __device__ __forceinline__ bool grid_point(const ConvArgs& a, int m, int& b, int
 // does the tile of GEMM rows [m0, m0 + rows) hold a row that computes something?
 __device__ __forceinline__ bool tile_live(const ConvArgs& a, int m0, int rows) {
   if (!a.gbox) return true;
-  const int HgWg = a.Hg * a.Wg;
+  const int HgWg = a.mrows;
   const int m1 = min(m0 + rows, a.M);
   for (int b = m0 / HgWg; b * HgWg < m1; ++b) {
     const GridBox g = grid_box(a, b);

@@ -467,7 +467,10 @@ extern "C" int po_conv(const po_conv_desc* d, const float* in, const float* W, c
   a.Hout = d->Hout; a.Wout = d->Wout; a.Cout_p = d->Cout_p; a.Hg = d->Hg; a.Wg = d->Wg;
   a.in_step = d->in_step; a.out_step = d->out_step; a.out_oy = d->out_oy; a.out_ox = d->out_ox;
   a.ntaps = d->ntaps; a.N = d->N; a.act = d->act; a.accumulate = d->accumulate;
-  a.M = d->B * d->Hg * d->Wg;
+  a.mrows = d->mrows > 0 ? d->mrows : d->Hg * d->Wg;
+  PO_REQUIRE(a.mrows <= d->Hg * d->Wg && (a.mrows == d->Hg * d->Wg || d->gbox),
+             "po_conv: mrows %d needs gbox and at most Hg*Wg = %d rows", a.mrows, d->Hg * d->Wg);
+  a.M = d->B * a.mrows;
   a.ntiles_n = 1;
   const int64_t in_bytes = (int64_t)d->B * d->Hin * d->Win * d->Cin_p * 4;
   // prec 1: w_bytes is one fp16 plane (the lo plane follows it)
@@ -514,6 +517,7 @@ extern "C" int po_conv(const po_conv_desc* d, const float* in, const float* W, c
   }
   while (bk > 16 && a.Cin_p % bk != 0) bk /= 2;
   int rc;
+  PO_REQUIRE(a.mrows == a.Hg * a.Wg || gl <= 1, "po_conv: a compact box grid (mrows) runs on the generic tiles only");
   if (a.prec == 1) {
     ConvArgs b = a;
     b.ntiles_n = po::ceil_div(a.N, bn);

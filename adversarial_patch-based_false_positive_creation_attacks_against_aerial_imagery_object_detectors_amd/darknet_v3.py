@@ -257,6 +257,7 @@ class NetPlan:
         self._build_slots()
         self._build_bits()
         self._build_cones()
+        self.support = []             # compact dgrad grids over window supports (_support_grid)
         self._build_ops()
         self._drop_mask_only_outputs()
 
@@ -509,6 +510,10 @@ class NetPlan:
         """MACs one po_conv launch computes: desc.macs for a full grid; for a
         boxed launch (cones = the step's po_grad_boxes output) only its
         per-image boxes' grid points, counted as the kernels enumerate them."""
+        if getattr(desc, "support", None) is not None:
+            bx = desc.support.cpu().tolist()
+            pts = sum(max(r1 - r0, 0) * max(c1 - c0, 0) for r0, c0, r1, c1 in bx)
+            return desc.macs * pts / (desc.B * desc.mrows)
         if cones is None or not desc.gbox:
             return desc.macs
 
@@ -873,9 +878,12 @@ class NetPlan:
                 acc, mask, final = contrib(src)
                 y2, m2 = dual_of(src, final)
                 for desc, wd, b0 in self._dgrad_descs(j, src, acc, G, self.grad[src], y2):
+                    if desc.mrows:
+                        bwd.append(("zero", (self.grad[src],), None))
                     Pb = lambda t: self._img_ptr(t, b0)
-                    desc.gbox = self._cone_ptr(src, b0)
-                    desc.cone_block, desc.cone_b0 = src, b0
+                    if not desc.mrows:
+                        desc.gbox = self._cone_ptr(src, b0)
+                        desc.cone_block, desc.cone_b0 = src, b0
                     mb, m2b = self._img_ptr(self.bits_of(mask), b0), self._img_ptr(self.bits_of(m2), b0)
                     desc.mbits = mb.value if mb is not None else None
                     desc.m2bits = m2b.value if m2b is not None else None
@@ -1006,8 +1014,55 @@ class NetPlan:
             desc.accumulate = acc
             desc.macs = nb * Hg * Wg * m["cin"] * len(taps) * m["cout"]
             desc.block, desc.kind = j, "dgrad"
+            self._support_grid(desc, j, src, acc, dst, dst2, b0)
             out.append((desc, wd, b0))
         return out
+
+    def _support_grid(self, desc, j, src, acc, dst, dst2, b0):
+        """A dgrad from a receptive-field window (G_j lives on a window of side
+        w) into a full map is nonzero only on the window dilated by the taps:
+        rows [org - max(dh), org + w - min(dh)), columns likewise.  Such a
+        launch runs over that box only — a compact grid of mrows points per
+        image with per-step boxes (po_conv gbox, ∩ the gradient cone), the
+        destination zero-filled first (its consumers read the whole map).
+        Only first contributions (acc = 0) without a dual output.  Off with
+        ADVPATCH_SUPPORT_BOX=0."""
+        if (os.environ.get("ADVPATCH_SUPPORT_BOX", "1") == "0" or src == INPUT or self.win[j] is None
+                or self.win[src] is not None or acc or dst2 is not None or desc.in_step != 1
+                or desc.out_step != 1 or desc.Wwino):
+            return
+        if sum(1 for g in self.grad if g is not None and g.data_ptr() == dst.data_ptr()) > 1:
+            return                              # a shared (residual) gradient buffer: no zero fill
+        dh = [desc.dh[t] for t in range(desc.ntaps)]
+        dw = [desc.dw[t] for t in range(desc.ntaps)]
+        w = self.win[j]
+        hr, wc = min(w + max(dh) - min(dh), desc.Hg), min(w + max(dw) - min(dw), desc.Wg)
+        if hr * wc >= desc.Hg * desc.Wg:
+            return
+        box = torch.zeros(desc.B, 4, dtype=torch.int32, device=self.device)
+        self.support.append((box, j, src, b0, desc.B, (max(dh), min(dh), max(dw), min(dw)), dst))
+        desc.gbox = box.data_ptr()
+        desc.mrows = hr * wc
+        desc.macs = desc.macs * desc.mrows // (desc.Hg * desc.Wg)
+        desc.cone_block = None                  # launch_macs: counted over the support boxes
+        desc.support = box
+
+    def set_support_boxes(self):
+        """Per-step support boxes of the compact dgrad grids (after set_cones):
+        the window dilated by the taps, clipped to the map, ∩ the cone box."""
+        for box, j, src, b0, nb, (dh1, dh0, dw1, dw0), _ in self.support:
+            org = self.org_of(j)[b0:b0 + nb]
+            H, W = self.shp[src][:2]
+            w = self.win[j]
+            r0 = (org[:, 0] - dh1).clamp(0, H)
+            c0 = (org[:, 1] - dw1).clamp(0, W)
+            r1 = (org[:, 0] + w - dh0).clamp(0, H)
+            c1 = (org[:, 1] + w - dw0).clamp(0, W)
+            bx = torch.stack([r0, c0, r1, c1], 1)
+            if self.cone_boxes is not None and src in self.cone_blocks:
+                cb = self.cone_boxes[src, b0:b0 + nb]
+                bx = torch.cat([torch.maximum(bx[:, :2], cb[:, :2]), torch.minimum(bx[:, 2:], cb[:, 2:])], 1)
+            box.copy_(bx)
 
     def conv_macs(self):
         """MACs (logical channels) of the po_conv launches of one forward +
@@ -1060,6 +1115,7 @@ class NetPlan:
             a = self.H // 3
             roi = torch.tensor([[a, a, self.H - a, self.H - a]] * self.B, dtype=torch.int32, device=self.device)
             self.set_cones(roi)
+        self.set_support_boxes()                # compact dgrad grids: boxes at the current window origins
         tiles = []
         for t in range(1, nat.PO_CONV_NTILES + 1):
             bm, bn, bk, pr = nat.c_int(), nat.c_int(), nat.c_int(), nat.c_int()
@@ -1135,9 +1191,10 @@ class NetPlan:
 
     @staticmethod
     def _tune_key(args, desc):
-        return (desc.B, desc.Hin, desc.Win, desc.Cin_p, desc.Hg, desc.Wg, desc.in_step, desc.ntaps, desc.N,
-                desc.accumulate, args[6] is not None, args[7] is not None or bool(desc.mbits),
-                args[8] is not None, desc.prec, bool(desc.ybits), bool(desc.gbox))
+        key = (desc.B, desc.Hin, desc.Win, desc.Cin_p, desc.Hg, desc.Wg, desc.in_step, desc.ntaps, desc.N,
+               desc.accumulate, args[6] is not None, args[7] is not None or bool(desc.mbits),
+               args[8] is not None, desc.prec, bool(desc.ybits), bool(desc.gbox))
+        return key + ("mrows", desc.mrows) if desc.mrows else key
 
     def _set_tile(self, desc, choice):
         t, ks = (choice, 1) if isinstance(choice, int) else choice
@@ -1194,9 +1251,13 @@ class NetPlan:
         dxp = nat.c_void_p(d_x.data_ptr())
         roip = nat.c_void_p(roi.data_ptr()) if roi is not None else None
         self.set_cones(roi)
+        self.set_support_boxes()
         if self.conv_timer is not None and self.cone_boxes is not None:
             self._cone_snap = self.cone_boxes.clone()        # this step's cones, for launch_macs
         for name, args, desc in self.bwd_ops:
+            if name == "zero":
+                args[0].zero_()
+                continue
             if args and args[-1] == "dimg":
                 if name == "po_conv_first_dgrad":
                     args = args[:-2] + (roip, dxp)

@@ -33,7 +33,7 @@ typedef void* po_stream_t;
 #define PO_EHIP -2     /* HIP runtime error */
 #define PO_EDEVICE -3  /* device is not gfx950 */
 
-#define PO_ABI_VERSION 12
+#define PO_ABI_VERSION 13
 #define PO_AMAX_SUB 64  /* sub-slots per max|x| slot (see po_conv_desc) */
 
 int po_abi_version(void);
@@ -367,6 +367,12 @@ typedef struct po_conv_desc {
    * block (nb, kc, xi), U[xi][16 kc + 8 (l >> 5) + s][32 nb + (l & 31)], sits
    * at [nb][kc][xi][s >> 2][l][s & 3].  NULL: tiles 61-62 do not apply. */
   const float* Wwino;
+  /* GEMM rows per image (0: Hg*Wg).  With gbox, mrows < Hg*Wg enumerates each
+   * image's box compactly when every box holds at most mrows grid points: a
+   * dgrad from a receptive-field window (nonzero only on the window dilated by
+   * the taps) runs over that box instead of the whole map.  Generic tiles only
+   * (staging 0/1). */
+  int mrows;
 } po_conv_desc;
 
 #define PO_CONV_NTILES 65

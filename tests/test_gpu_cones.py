@@ -178,3 +178,39 @@ def test_halo_tiles_refuse_boxes():
     y = torch.zeros(2, 9, 9, 32, device=DEV)
     with pytest.raises(RuntimeError, match="halo"):
         _conv(nat, x, wt, shift, slot, torch.zeros(32, device=DEV), y, box, 1, 53, 1, (9, 9, 9, 1, 0, 0))
+
+
+@pytest.mark.parametrize("prec", ["fp32", "fp16x3"])
+def test_support_box_grid_leaves_the_patch_gradient_unchanged(tmp_path, monkeypatch, prec):
+    """yolov3-tiny's dgrad from the 13x13 head window into the full 13x13 map
+    of block 11 runs over the window dilated by the taps only (po_conv mrows +
+    per-step gbox, destination zero-filled): the same patch gradient as the
+    full-map launch (ADVPATCH_SUPPORT_BOX=0) — bit for bit with exact fp32
+    operands, within the operand-scale effect for fp16x3."""
+    from test_gpu_step import _trainer
+    sy = pkg_mod("synthetic")
+    B, P, S = 5, 224, 416
+    monkeypatch.setenv("ADVPATCH_TUNE", "0")
+    out = []
+    for sup in ("1", "0"):
+        monkeypatch.setenv("ADVPATCH_SUPPORT_BOX", sup)
+        tr, _ = _trainer("builtin:yolov3-tiny-dota", tmp_path, prec=prec)
+        img, lab = sy.frames(B, S, seed=70).to(DEV), sy.labels(B, seed=71).to(DEV)
+        dr = {k: v.to(DEV) for k, v in sy.draws(B, P, seed=73).items()}
+        pg = sy.patch(P, seed=72).to(DEV).requires_grad_(True)
+        loss, terms = tr.losses(pg, img, lab, dr)
+        loss.backward()
+        plan = tr.last_plan
+        assert bool(plan.support) == (sup == "1")
+        if sup == "1":
+            for box, j, src, b0, nb, _, _ in plan.support:
+                bx = box.cpu()
+                assert bool(((bx[:, 2] - bx[:, 0]) * (bx[:, 3] - bx[:, 1]) <= 25).all())
+        out.append((float(loss.detach()), pg.grad.detach().clone()))
+    (l1, g1), (l0, g0) = out
+    assert l1 == l0
+    if prec == "fp32":
+        assert torch.equal(g1, g0)
+    else:
+        rel = float((g1 - g0).abs().max() / g0.abs().max())
+        assert rel < 1e-5, rel
