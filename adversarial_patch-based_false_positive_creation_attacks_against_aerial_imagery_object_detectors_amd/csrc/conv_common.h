@@ -44,6 +44,8 @@ struct ConvArgs {
   int M, ntiles_n;
   int mrows;                    // GEMM rows per image: Hg*Wg, or fewer with gbox (a compact grid over each
                                 // image's box of at most mrows points: see grid_point)
+  float* pool_y;                // optional: k=2 stride-2 max pool of the output fused into the epilogue
+  int8_t* pool_am;              //   (pool output, argmax bytes); the grid runs in pool order
   uint32_t in_bytes, w_bytes;   // buffer-resource extents (< 2^31)
   // taps form a rectangular grid: tap t = th*tkw + tw -> (dh0 + th*sdh, dw0 + tw*sdw)
   int tkw, dh0, dw0, sdh, sdw;
@@ -93,6 +95,13 @@ __device__ __forceinline__ bool grid_point(const ConvArgs& a, int m, int& b, int
   }
   b = m / HgWg;
   const int l = m - b * HgWg;
+  if (a.pool_y) {          // pool order: rows 4w .. 4w+3 are the 2x2 window w (row-major windows)
+    const int w = l >> 2, k = l & 3, wp = a.Wg >> 1;
+    const int i2 = w / wp;
+    i = 2 * i2 + (k >> 1);
+    j = 2 * (w - i2 * wp) + (k & 1);
+    return true;
+  }
   if (!a.gbox) {
     i = l / a.Wg;
     j = l - i * a.Wg;
@@ -152,6 +161,81 @@ __device__ __forceinline__ float4 leaky_grad_bits(uint32_t w, int n) {
   return make_float4((b & 1) ? 1.f : 0.1f, (b & 2) ? 1.f : 0.1f, (b & 4) ? 1.f : 0.1f, (b & 8) ? 1.f : 0.1f);
 }
 
+// Epilogue of a conv with its k=2 stride-2 max pool fused (ConvArgs.pool_y;
+// pool-order grid: GEMM rows 4w..4w+3 are the 2x2 window w).  Each wave stages
+// one 32x32 accumulator tile through its LDS slot as conv_epilogue does; the
+// lane whose rows are window position 0 (row & 3 == 0) reads the window's four
+// rows, applies bias + activation to each exactly as conv_epilogue would, then
+// po_maxpool2_fwd's rule (first position on ties, NaN wins), and writes the
+// pooled value and the argmax byte (bit 3 set and bit 2 = max <= 0 for a leaky
+// conv: the LeakyReLU slope of the unstored output, see
+// po_conv_first_pool_fwd).  The conv output itself is not stored.
+template <int BM, int TM, int TN>
+__device__ __forceinline__ void conv_pool_epilogue(const ConvArgs& a, const floatx16 (&acc)[TM][TN], float* smem,
+                                                   int* dst_pix, int m0, int n0, int wm, int wn, int sh,
+                                                   bool active) {
+  const int tid = threadIdx.x, lane = tid & 63, wave = (tid >> 6) & 3;
+  if (tid < BM) {
+    int b, i, j;
+    dst_pix[tid] = grid_point(a, m0 + tid, b, i, j) ? (b * a.Hout + i) * a.Wout + j : -1;
+  }
+  __syncthreads();
+  float* scr = smem + wave * 1024;
+  const int rr = lane >> 3, cc = (lane & 7) * 4;
+  float my = 0.f;
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      if (!active) break;
+#pragma unroll
+      for (int e = 0; e < 16; ++e)
+        scr[((e & 3) + 8 * (e >> 2) + 4 * (lane >> 5)) * 32 + (lane & 31)] = acc[i][j][e];
+      __builtin_amdgcn_wave_barrier();
+      const int n = n0 + wn * TN * 32 + j * 32 + cc;
+      float4 bv = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (a.bias && n < a.N) bv = *reinterpret_cast<const float4*>(a.bias + n);
+      if ((rr & 3) == 0) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const int row = rr + 8 * q;
+          const int pix = dst_pix[wm * TM * 32 + i * 32 + row];
+          if (pix < 0 || n >= a.N) continue;
+          float pv[4] = {0.f, 0.f, 0.f, 0.f};
+          uint32_t arg[4] = {0u, 0u, 0u, 0u};
+#pragma unroll
+          for (int k = 0; k < 4; ++k) {
+            const float4 vk = *reinterpret_cast<const float4*>(scr + (row + k) * 32 + cc);
+            float x[4] = {__builtin_ldexpf(vk.x, -sh) + bv.x, __builtin_ldexpf(vk.y, -sh) + bv.y,
+                          __builtin_ldexpf(vk.z, -sh) + bv.z, __builtin_ldexpf(vk.w, -sh) + bv.w};
+#pragma unroll
+            for (int c = 0; c < 4; ++c) {
+              if (a.act) x[c] = leaky(x[c]);
+              if (k == 0 || x[c] > pv[c] || isnan(x[c])) { pv[c] = x[c]; arg[c] = (uint32_t)k; }
+            }
+          }
+          uint32_t code = 0u;
+#pragma unroll
+          for (int c = 0; c < 4; ++c) {
+            if (a.act) arg[c] |= 8u | (pv[c] > 0.f ? 0u : 4u);
+            if (n + c >= a.N) { pv[c] = 0.f; arg[c] = 0u; }
+            code |= arg[c] << (8 * c);
+            my = fmaxf(my, fabsf(pv[c]));
+          }
+          // pixel (b, i, j) of window position 0 (i, j even) -> pooled pixel (b, i/2, j/2)
+          const int Wo = a.Wout, Ho = a.Hout;
+          const int bimg = pix / (Ho * Wo), rem = pix - bimg * Ho * Wo;
+          const int pi = rem / Wo, pj = rem - pi * Wo;
+          const size_t po = (((size_t)bimg * (Ho >> 1) + (pi >> 1)) * (Wo >> 1) + (pj >> 1)) * a.Cout_p + n;
+          *reinterpret_cast<float4*>(a.pool_y + po) = make_float4(pv[0], pv[1], pv[2], pv[3]);
+          *reinterpret_cast<uint32_t*>(a.pool_am + po) = code;
+        }
+      }
+      __builtin_amdgcn_wave_barrier();
+    }
+  if (a.y_amax) amax_commit(a.y_amax, my);
+}
+
 // Epilogue.  Each wave stages one 32x32 accumulator tile at a time through a
 // private 4 KB slot of `smem` (the k-loop buffers are free by now), then every
 // lane handles 4 consecutive channels of a row: 16-byte loads of
@@ -163,6 +247,12 @@ template <int BM, int TM, int TN>
 __device__ __forceinline__ void conv_epilogue(const ConvArgs& a, const floatx16 (&acc)[TM][TN], float* smem,
                                               int* dst_pix, int m0, int n0, int wm, int wn, int sh,
                                               bool active = true, bool fill_dst = true) {
+  if constexpr (TM * TN <= 4) {     // pooled launches: tiles up to 128x128 (host check)
+    if (a.pool_y) {
+      conv_pool_epilogue<BM, TM, TN>(a, acc, smem, dst_pix, m0, n0, wm, wn, sh, active);
+      return;
+    }
+  }
   const int tid = threadIdx.x, lane = tid & 63, wave = (tid >> 6) & 3;
   if (fill_dst && tid < BM) {     // else the caller has written dst_pix (2-D tiles)
     int b, i, j;

@@ -424,8 +424,13 @@ extern "C" int po_conv(const po_conv_desc* d, const float* in, const float* W, c
   PO_REQUIRE(d && in && W, "po_conv: null pointer");
   // y_out may be NULL only when the launch still writes something: the shortcut
   // sum or the sign bits (a forward activation used only as a LeakyReLU mask)
-  PO_REQUIRE(y_out || ((sum_out || d->ybits) && !d->accumulate && !mask_y && !d->mbits && !y2_out),
-             "po_conv: y_out may be NULL only for a plain forward conv that writes sum_out or ybits");
+  PO_REQUIRE(y_out || ((sum_out || d->ybits || d->pool_y) && !d->accumulate && !mask_y && !d->mbits && !y2_out),
+             "po_conv: y_out may be NULL only for a plain forward conv that writes sum_out, ybits or pool_y");
+  PO_REQUIRE(!d->pool_y || (d->pool_argmax && !y_out && !res && !d->accumulate && !mask_y && !d->mbits && !y2_out &&
+                            !d->ybits && !d->gbox && !d->in_org && !d->out_org && d->out_step == 1 &&
+                            d->out_oy == 0 && d->out_ox == 0 && d->Hg == d->Hout && d->Wg == d->Wout &&
+                            d->Hg % 2 == 0 && d->Wg % 2 == 0 && d->ksplit <= 1 && d->N % 4 == 0),
+             "po_conv: pool_y needs a plain full-map forward conv (even grid, no split-K, no other outputs)");
   PO_REQUIRE((res == nullptr) == (sum_out == nullptr), "po_conv: res and sum_out must both be set or both NULL");
   PO_REQUIRE((y2_out == nullptr) == (mask2 == nullptr && d->m2bits == nullptr),
              "po_conv: y2_out needs mask2 or m2bits (and neither without y2_out)");
@@ -467,6 +472,8 @@ extern "C" int po_conv(const po_conv_desc* d, const float* in, const float* W, c
   a.Hout = d->Hout; a.Wout = d->Wout; a.Cout_p = d->Cout_p; a.Hg = d->Hg; a.Wg = d->Wg;
   a.in_step = d->in_step; a.out_step = d->out_step; a.out_oy = d->out_oy; a.out_ox = d->out_ox;
   a.ntaps = d->ntaps; a.N = d->N; a.act = d->act; a.accumulate = d->accumulate;
+  a.pool_y = d->pool_y;
+  a.pool_am = d->pool_argmax;
   a.mrows = d->mrows > 0 ? d->mrows : d->Hg * d->Wg;
   PO_REQUIRE(a.mrows <= d->Hg * d->Wg && (a.mrows == d->Hg * d->Wg || d->gbox),
              "po_conv: mrows %d needs gbox and at most Hg*Wg = %d rows", a.mrows, d->Hg * d->Wg);
@@ -517,7 +524,10 @@ extern "C" int po_conv(const po_conv_desc* d, const float* in, const float* W, c
   }
   while (bk > 16 && a.Cin_p % bk != 0) bk /= 2;
   int rc;
-  PO_REQUIRE(a.mrows == a.Hg * a.Wg || gl <= 1, "po_conv: a compact box grid (mrows) runs on the generic tiles only");
+  PO_REQUIRE((a.mrows == a.Hg * a.Wg && !a.pool_y) || gl <= 1,
+             "po_conv: a compact box grid (mrows) or a fused pool runs on the generic tiles only");
+  PO_REQUIRE(!a.pool_y || bm * bn <= 128 * 128,
+             "po_conv: a fused pool needs a generic tile of at most 128x128 (got %dx%d)", bm, bn);
   if (a.prec == 1) {
     ConvArgs b = a;
     b.ntiles_n = po::ceil_div(a.N, bn);

@@ -252,6 +252,21 @@ class NetPlan:
                            and self.cp[0] in (16, 32) and self.win[0] is None and self.win[1] is None
                            and [j for j in range(n) if 0 in srcs[j]] == [1]
                            and os.environ.get("ADVPATCH_FIRST_POOL", "1") != "0")
+        # later conv + k=2 stride-2 pool pairs (yolov3-tiny blocks 2/3, 4/5): the pool
+        # runs in the conv epilogue (po_conv_desc.pool_y, pool-order grid) when the
+        # conv's only consumer is the pool and it runs on the generic tiles anyway
+        # (Cin_p <= 32, where the tuner never picks Winograd); ADVPATCH_CONV_POOL=0: off
+        self.conv_pool = set()
+        if os.environ.get("ADVPATCH_CONV_POOL", "1") != "0":
+            for i in range(1, n - 1):
+                if (blocks[i]["type"] == "convolutional" and root[i] == i and blocks[i + 1]["type"] == "maxpool"
+                        and int(blocks[i + 1]["stride"]) == 2 and root[i + 1] == i + 1
+                        and [j for j in range(n) if i in srcs[j]] == [i + 1]
+                        and self.win[i] is None and self.win[i + 1] is None
+                        and shp[i][0] % 2 == 0 and shp[i][1] % 2 == 0 and self.cp[i] % 16 == 0
+                        and srcs[i][0] != INPUT and self.cp[srcs[i][0]] <= 32
+                        and not (i - 1 == 0 and self.first_pool)):
+                    self.conv_pool.add(i)
         self._build_grad_plan()
         self.prec = 1 if net.conv_prec == "fp16x3" else 0
         self._build_slots()
@@ -617,7 +632,7 @@ class NetPlan:
             return
         for i, d in enumerate(self.net.blocks):
             if (d["type"] == "convolutional" and self.root[i] == i and self._leaky(i) and self.has_grad[i]
-                    and self.cp[i] % 32 == 0 and not (i == 0 and self.first_direct)):
+                    and self.cp[i] % 32 == 0 and not (i == 0 and self.first_direct) and i not in self.conv_pool):
                 self.bits[self.act[i].data_ptr()] = torch.zeros(self.B, self.dims[i][0], self.dims[i][1],
                                                                 self.cp[i] // 32, dtype=torch.int32,
                                                                 device=self.device)
@@ -659,7 +674,7 @@ class NetPlan:
         """bool [B, h, w, C]: output of leaky conv i > 0 — from the fp32
         activation, or from its sign bits when it is not stored."""
         C = self.shp[i][2]
-        if i == 0 and self.first_pool:
+        if (i == 0 and self.first_pool) or i in self.conv_pool:
             return None                         # not stored (fused into the pool: its argmax bytes)
         if i in self.y_dropped:
             bits = self.bits[self.act[i].data_ptr()]
@@ -771,7 +786,13 @@ class NetPlan:
                 desc.y_amax = self.slot(y_out).value
                 desc.sum_amax = self.slot(sum_out).value if sum_out is not None else None
                 desc.ybits = self.bits_of(y_out)
-                args = (nat.ctypes.byref(desc), P(inp), P(wptr), P(wts["bias"]), P(y_out), P(res),
+                y_ptr = P(y_out)
+                if i in self.conv_pool:               # the pool output instead of the conv output
+                    desc.pool_y, desc.pool_argmax = self.act[i + 1].data_ptr(), self.argmax[i + 1].data_ptr()
+                    desc.y_amax = self.slot(self.act[i + 1]).value
+                    desc.ybits = None
+                    y_ptr = None
+                args = (nat.ctypes.byref(desc), P(inp), P(wptr), P(wts["bias"]), y_ptr, P(res),
                         P(sum_out), None, None, None)
                 desc.macs = B * desc.Hg * desc.Wg * m["cout"] * m["cin"] * k * k      # logical channels
                 desc.block, desc.kind = i, "fwd"
@@ -810,8 +831,8 @@ class NetPlan:
                     fwd.append(("po_view_move", self._move(self.act[s], s, 0, self.act[i], i, 0, cs, 1, 0, None),
                                 None))
             elif t == "maxpool":
-                if i == 1 and self.first_pool:
-                    continue                    # fused into po_conv_first_pool_fwd
+                if (i == 1 and self.first_pool) or (i - 1) in self.conv_pool:
+                    continue                    # fused into the producing conv
                 s = self.srcs[i][0]
                 hs, ws_, cs = self.shp[s]
                 fwd.append(("po_maxpool2_fwd", (P(self.act[s]), B, hs, ws_, cs, self.cp[s], int(d["stride"]),
@@ -936,7 +957,7 @@ class NetPlan:
             elif t == "maxpool":
                 s_ = self.srcs[j][0]
                 acc, mask, final = contrib(s_)
-                if j == 1 and self.first_pool:
+                if (j == 1 and self.first_pool) or s_ in self.conv_pool:
                     # the LeakyReLU slopes come from the argmax bytes (the conv output is not stored)
                     assert acc == 0 and final
                     mask = None
@@ -1194,6 +1215,8 @@ class NetPlan:
         key = (desc.B, desc.Hin, desc.Win, desc.Cin_p, desc.Hg, desc.Wg, desc.in_step, desc.ntaps, desc.N,
                desc.accumulate, args[6] is not None, args[7] is not None or bool(desc.mbits),
                args[8] is not None, desc.prec, bool(desc.ybits), bool(desc.gbox))
+        if desc.pool_y:
+            key = key + ("pool", 1)
         return key + ("mrows", desc.mrows) if desc.mrows else key
 
     def _set_tile(self, desc, choice):

@@ -549,8 +549,8 @@ class DotaDataset(torch.utils.data.Dataset):
         self.lab_paths = [os.path.join(lab_dir, n).replace(".jpg", ".txt").replace(".png", ".txt") for n in names]
         self.max_n_labels = max_lab
         # as_uint8: images come out as uint8 [3,S,S] (a quarter of the bytes through the
-        # worker queues, pinning and the PCIe copy); DevicePrefetcher divides by 255 on
-        # the device, which gives the same floats as ToTensor's division on the host
+        # worker queues, pinning and the PCIe copy); DevicePrefetcher / FrameCache turn
+        # them into ToTensor's floats on the device (u8_to_float)
         self.as_uint8 = as_uint8
 
     def __len__(self):
@@ -603,6 +603,21 @@ class DotaDataset(torch.utils.data.Dataset):
         return lab
 
 
+_U8_LUT = {}
+
+
+def u8_to_float(img):
+    """uint8 -> float32 / 255 exactly as ToTensor computes it on the host.
+    (On the GPU ``x.float() / 255.0`` is x * (1/255), which differs from the
+    host's correctly rounded division in the last bit for some values: the
+    256 host-computed quotients are gathered instead.)"""
+    lut = _U8_LUT.get(img.device)
+    if lut is None:
+        lut = torch.arange(256, dtype=torch.uint8).float().div_(255.0).to(img.device)
+        _U8_LUT[img.device] = lut
+    return lut[img.long()]
+
+
 class DevicePrefetcher:
     """Host->device feed of the training loop (the reference copies each batch
     with a blocking ``.cuda()``, train_patch.py:164-166).  The copy of batch
@@ -611,7 +626,7 @@ class DevicePrefetcher:
     two steps on the compute stream; the compute stream waits on an event only
     when it takes the batch.  uint8 image batches (DotaDataset(as_uint8=True))
     become float32 / 255 on the device, bit-identical to ToTensor on the host
-    (both are one correctly rounded fp32 division).  Batches that are already
+    (u8_to_float).  Batches that are already
     on the device pass through; without a GPU it only applies the conversion."""
 
     def __init__(self, loader, device):
@@ -622,7 +637,7 @@ class DevicePrefetcher:
 
     @staticmethod
     def _to_float(img):
-        return img.float().div_(255.0) if img.dtype == torch.uint8 else img
+        return u8_to_float(img) if img.dtype == torch.uint8 else img
 
     def __iter__(self):
         if self.device.type != "cuda":
@@ -665,7 +680,7 @@ class FrameCache:
     DataLoader over the host workers — and kept as uint8 [N,3,S,S] plus float
     labels [N,L,5] in HBM (1.1 MB per 608x608 frame: a 20k-frame set is 22 GB of
     a MI355X's 288 GB).  Every epoch after that gathers its batches on the
-    device (index_select + /255, the same floats as ToTensor), so the host
+    device (index_select + u8_to_float, the same floats as ToTensor), so the host
     decode rate (tens of frames/s per core) no longer bounds the step rate."""
 
     def __init__(self, dataset, device, num_workers=8, batch=32):
@@ -694,7 +709,7 @@ class FrameCache:
     def batch(self, indices):
         """(img [b,3,S,S] float32 in [0,1], lab [b,L,5]) of dataset rows ``indices``, on the device."""
         idx = torch.as_tensor(indices, dtype=torch.long).to(self.device, non_blocking=True)
-        return self.frames.index_select(0, idx).float().div_(255.0), self.labels.index_select(0, idx)
+        return u8_to_float(self.frames.index_select(0, idx)), self.labels.index_select(0, idx)
 
     def loader(self, batch_sampler):
         """Iterable of device batches in ``batch_sampler``'s order (a fresh pass per iter())."""

@@ -33,7 +33,7 @@ typedef void* po_stream_t;
 #define PO_EHIP -2     /* HIP runtime error */
 #define PO_EDEVICE -3  /* device is not gfx950 */
 
-#define PO_ABI_VERSION 13
+#define PO_ABI_VERSION 14
 #define PO_AMAX_SUB 64  /* sub-slots per max|x| slot (see po_conv_desc) */
 
 int po_abi_version(void);
@@ -373,6 +373,14 @@ typedef struct po_conv_desc {
    * the taps) runs over that box instead of the whole map.  Generic tiles only
    * (staging 0/1). */
   int mrows;
+  /* Optional fused k=2 stride-2 max pool of a plain forward conv (y_out NULL,
+   * full even grid, no split-K, generic tiles): pool_y [B,Hout/2,Wout/2,Cout_p]
+   * and pool_argmax (int8, same shape) as po_maxpool2_fwd writes them, the
+   * argmax bytes of a leaky conv also carrying its LeakyReLU slope (bit 3
+   * set, bit 2 = max <= 0; see po_conv_first_pool_fwd); the conv output
+   * itself is not stored (darknet_v3.py:61-69 conv + maxpool pairs). */
+  float* pool_y;
+  int8_t* pool_argmax;
 } po_conv_desc;
 
 #define PO_CONV_NTILES 65

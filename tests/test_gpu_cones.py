@@ -214,3 +214,39 @@ def test_support_box_grid_leaves_the_patch_gradient_unchanged(tmp_path, monkeypa
     else:
         rel = float((g1 - g0).abs().max() / g0.abs().max())
         assert rel < 1e-5, rel
+
+
+@pytest.mark.parametrize("prec", ["fp32", "fp16x3"])
+def test_conv_pool_fusion_leaves_the_step_unchanged(tmp_path, monkeypatch, prec):
+    """yolov3-tiny's conv + 2x2/2 max pool pairs (blocks 2/3 and 4/5,
+    darknet_v3.py:61-69) with the pool in the conv epilogue (po_conv_desc.pool_y,
+    pool-order grid; the conv output is never stored, the argmax bytes carry
+    the LeakyReLU slope): the same loss, pool outputs, window positions and
+    patch gradient as the separate po_maxpool2_fwd (ADVPATCH_CONV_POOL=0) — bit
+    for bit with exact fp32 operands."""
+    from test_gpu_step import _trainer
+    sy = pkg_mod("synthetic")
+    B, P, S = 3, 224, 416
+    monkeypatch.setenv("ADVPATCH_TUNE", "0")
+    out = []
+    for fuse in ("1", "0"):
+        monkeypatch.setenv("ADVPATCH_CONV_POOL", fuse)
+        tr, _ = _trainer("builtin:yolov3-tiny-dota", tmp_path, prec=prec)
+        img, lab = sy.frames(B, S, seed=60).to(DEV), sy.labels(B, seed=61).to(DEV)
+        dr = {k: v.to(DEV) for k, v in sy.draws(B, P, seed=63).items()}
+        pg = sy.patch(P, seed=62).to(DEV).requires_grad_(True)
+        loss, terms = tr.losses(pg, img, lab, dr)
+        loss.backward()
+        plan = tr.last_plan
+        assert sorted(plan.conv_pool) == ([2, 4] if fuse == "1" else [])
+        pools = {j: (plan.act[j].clone(), plan.argmax[j].long() & 3) for j in (3, 5)}
+        out.append((float(loss.detach()), pools, pg.grad.detach().clone()))
+    (l1, p1, g1), (l0, p0, g0) = out
+    if prec == "fp32":
+        assert l1 == l0
+        for j in (3, 5):
+            assert torch.equal(p1[j][0], p0[j][0]) and torch.equal(p1[j][1], p0[j][1])
+        assert torch.equal(g1, g0)
+    else:
+        rel = float((g1 - g0).abs().max() / g0.abs().max())
+        assert rel < 1e-5, rel
