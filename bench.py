@@ -199,6 +199,11 @@ def roofline(cfg_name, B, prec, m, ref_flops_step):
             "measured_on": "a second pass of K steps with per-launch HIP events (%.3f ms/step instrumented vs %.3f "
                            "plain)" % (m["instrumented_ms"], m["ms_per_step"]),
             "reference_dense_flops_per_step": ref_flops_step,
+            # SURVEY §8d's algorithmic rate: the reference's dense fwd + dgrad FLOPs of the
+            # images processed, over the whole step's wall time (windows, cones and Winograd
+            # skip part of that work, so this can exceed the MFMA peak)
+            "achieved_algorithmic": ref_flops_step / (m["ms_per_step"] * 1e-3) / 1e12,
+            "frac_algorithmic": ref_flops_step / (m["ms_per_step"] * 1e-3) / 1e12 / peak,
             "receptive_field_windows": bool(m["plan"].windowed)}
 
 
