@@ -374,6 +374,6 @@ int launch_h3(const ConvArgs& a, hipStream_t st, int bm, int bn, int bk, int sta
 // conv_wino.hip: the exact-fp32 Winograd F(2x2,3x3) kernel (tile 61); U =
 // the launch's transformed weights (po_conv_desc.Wwino)
 int launch_wino(const ConvArgs& a, const float* U, hipStream_t st, int bm, int waves, bool sched = false,
-                bool vec = false);
+                bool vec = false, bool small_lds = false);
 
 }  // namespace po

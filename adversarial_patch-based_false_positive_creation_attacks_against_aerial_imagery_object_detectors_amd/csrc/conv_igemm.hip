@@ -390,7 +390,8 @@ bool forced_tile(int& bm, int& bn, int& bk, int& gl) {
 // 2x2 output tiles): 64 tiles x 32 channels, and 32 tiles x 64 channels with
 // LDS-DMA input (62: 4 waves; 63, staging 6: 8 waves, two per SIMD; 64,
 // staging 7: 63 with the transform interleaved into the MFMA stream; 65,
-// staging 8: 64 with the 16-byte (4-channel) epilogue).
+// staging 8: 64 with the 16-byte (4-channel) epilogue; 66, staging 11: 65's
+// work as 4-wave workgroups in 72 KB of LDS, two per CU).
 constexpr int kTiles[PO_CONV_NTILES][5] = {
     {128, 128, 16, 0, 0}, {128, 128, 32, 0, 0}, {64, 128, 16, 0, 0}, {64, 128, 32, 0, 0}, {128, 64, 16, 0, 0},
     {128, 64, 32, 0, 0},  {64, 64, 16, 0, 0},   {64, 64, 32, 0, 0},  {128, 32, 16, 0, 0}, {128, 32, 32, 0, 0},
@@ -406,7 +407,8 @@ constexpr int kTiles[PO_CONV_NTILES][5] = {
     {128, 128, 16, 1, 1}, {256, 128, 16, 1, 1}, {128, 128, 16, 2, 1}, {128, 64, 16, 2, 1},
     {128, 128, 16, 3, 1}, {128, 64, 16, 3, 1},
     {128, 128, 16, 4, 1}, {128, 64, 16, 4, 1}, {256, 128, 16, 4, 1}, {256, 64, 16, 4, 1},
-    {64, 32, 16, 5, 0}, {32, 64, 16, 5, 0}, {32, 64, 16, 6, 0}, {32, 64, 16, 7, 0}, {32, 64, 16, 8, 0}};
+    {64, 32, 16, 5, 0}, {32, 64, 16, 5, 0}, {32, 64, 16, 6, 0}, {32, 64, 16, 7, 0}, {32, 64, 16, 8, 0},
+    {32, 64, 16, 11, 0}};
 }  // namespace
 
 extern "C" int po_conv_tile_info(int t, int* bm, int* bn, int* bk, int* prec) {
@@ -540,6 +542,7 @@ extern "C" int po_conv(const po_conv_desc* d, const float* in, const float* W, c
     return rc;
   }
   if (gl >= 5 && gl <= 8) return po::launch_wino(a, d->Wwino, st, bm, gl >= 6 ? 8 : 4, gl >= 7, gl == 8);
+  if (gl == 11) return po::launch_wino(a, d->Wwino, st, bm, 4, false, true, true);
   if (bk > 32) bk = 32;
   if (gl) return bk == 32 ? dispatch<32, true>(a, st, bm, bn) : dispatch<16, true>(a, st, bm, bn);
   return bk == 32 ? dispatch<32, false>(a, st, bm, bn) : dispatch<16, false>(a, st, bm, bn);

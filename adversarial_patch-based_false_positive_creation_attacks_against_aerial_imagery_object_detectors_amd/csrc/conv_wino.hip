@@ -778,6 +778,221 @@ __global__ __launch_bounds__(64 * NW) void conv_wino2_k(const ConvArgs a, const 
   if (a.sum_amax) po::amax_commit(a.sum_amax, mx.s);
   if (a.y2_amax) po::amax_commit(a.y2_amax, mx.y2);
 }
+
+// ---------------------------------------------------------------------------
+// Tile 66 (staging 11): tile 65's work (32 tiles x 64 channels, VEC epilogue)
+// as 4-wave workgroups in 72 KB of LDS instead of 8 waves in 144 KB, so that
+// two workgroups share a CU (2 waves per SIMD, as tile 65) and one
+// workgroup's prologue/epilogue overlaps the other's k-loop: tile 65 spends
+// 6-36% of a launch outside its k-loop with nothing else on the CU
+// (profiles/r02/wino_epilogue_share.txt).  One raw buffer R and one
+// transformed buffer V (32 KB each): per k-step the transform runs between two
+// barriers, then the next step's DMA and this step's B fragments go out and
+// the MFMAs run.  The epilogue stages M in two passes of 16 tiles.  Same
+// transforms, MFMA order and epilogue arithmetic as tile 65 (bit-identical).
+__global__ __launch_bounds__(256, 2) void conv_wino3_k(const ConvArgs a, const float* __restrict__ U, int Ht, int Wt) {
+  constexpr int NW = 4;
+  constexpr int CPW = 16 / NW;           // components per wave (4)
+  constexpr int DPW = 32 / NW;           // DMA instructions per wave per k-step (8)
+  constexpr int TH = T2 / 2;             // tiles per epilogue pass
+  __shared__ __attribute__((aligned(16))) float smem[16 * TH * M2_ROW];   // 72 KB (k-loop: R + V = 64 KB)
+  __shared__ int s_live;
+  float* R = smem;                       // [16 p][T2][WK]
+  float* V = smem + R2_FLOATS;           // [16 xi][T2][WK] (swizzled chunks)
+  const int wgid = po::xcd_remap();
+  const int tn = wgid % a.ntiles_n, tm = wgid / a.ntiles_n;
+  const int m0 = tm * T2, n0 = tn * N2;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wave_u = __builtin_amdgcn_readfirstlane(wave);
+  const int h = lane >> 5;
+
+  if (tid == 0) s_live = 0;
+  __syncthreads();
+  if (tid < T2) {
+    int b, ti, tj;
+    if (tile_point(a, Ht, Wt, m0 + tid, b, ti, tj)) s_live = 1;
+  }
+  __syncthreads();
+  if (!s_live) return;
+
+  const uint32_t in_bytes = (uint32_t)__builtin_amdgcn_readfirstlane(a.in_bytes);
+  const __amdgpu_buffer_rsrc_t in_rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(a.in), 0, in_bytes, 0x00020000);
+  const uint32_t pix_bytes = (uint32_t)a.Cin_p * 4u;
+  uint32_t doff[DPW];
+#pragma unroll
+  for (int j = 0; j < DPW; ++j) {
+    const int idx = wave_u * DPW + j, p = idx >> 1, half = idx & 1;
+    int b, ti, tj;
+    const bool ok_t = tile_point(a, Ht, Wt, m0 + 16 * half + (lane >> 2), b, ti, tj);
+    const int y = 2 * ti - 1 + (p >> 2), x = 2 * tj - 1 + (p & 3);
+    const bool ok = ok_t && (unsigned)y < (unsigned)a.Hin && (unsigned)x < (unsigned)a.Win;
+    doff[j] = ok ? (((uint32_t)b * a.Hin + y) * a.Win + x) * pix_bytes + 16u * (lane & 3) : kOOB;
+  }
+  auto dma = [&](int ks) {
+    const uint32_t cb = (uint32_t)__builtin_amdgcn_readfirstlane(ks * (WK * 4));
+#pragma unroll
+    for (int j = 0; j < DPW; ++j) {
+      const int idx = wave_u * DPW + j;
+      lds_dma16(in_rs, R + ((idx >> 1) * T2 + 16 * (idx & 1)) * WK, doff[j], cb);
+    }
+  };
+  // transform: one (tile, channel pair) per thread, packed pairs (as tile 62/63 with 4 waves)
+  const int tc = lane & 7;
+  const int r = wave * 8 + (lane >> 3);
+  auto transform = [&]() {
+    f2v d[16];
+#pragma unroll
+    for (int p = 0; p < 16; ++p) d[p] = *reinterpret_cast<const f2v*>(R + (p * T2 + r) * WK + 2 * tc);
+    f2v t[4][4];
+#pragma unroll
+    for (int v = 0; v < 4; ++v) {
+      const f2v d0 = d[v], d1 = d[4 + v], d2 = d[8 + v], d3 = d[12 + v];
+      t[0][v] = d0 - d2;
+      t[1][v] = d1 + d2;
+      t[2][v] = d2 - d1;
+      t[3][v] = d1 - d3;
+    }
+    const int sub = (tc & 1) * 2;
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const f2v e[4] = {t[u][0] - t[u][2], t[u][1] + t[u][2], t[u][2] - t[u][1], t[u][1] - t[u][3]};
+#pragma unroll
+      for (int v = 0; v < 4; ++v) *reinterpret_cast<f2v*>(V + v2idx(u * 4 + v, r, tc >> 1) + sub) = e[v];
+    }
+  };
+
+  // ---- B operand (fragment-ordered U), loaded after each step's transform
+  const int kc_n = a.Cin_p / WK;
+  const float* Ub = U + (size_t)lane * 4;
+  float4 bc[CPW][2][2];
+  auto bload = [&](int ks) {
+#pragma unroll
+    for (int c = 0; c < CPW; ++c)
+#pragma unroll
+      for (int nb = 0; nb < 2; ++nb) {
+        const float* p = Ub + ((((size_t)(2 * tn + nb) * kc_n + ks) * 16 + wave_u * CPW + c) * 512);
+        bc[c][nb][0] = *reinterpret_cast<const float4*>(p);
+        bc[c][nb][1] = *reinterpret_cast<const float4*>(p + 256);
+      }
+  };
+
+  floatx16 acc[CPW][2];
+#pragma unroll
+  for (int c = 0; c < CPW; ++c)
+#pragma unroll
+    for (int nb = 0; nb < 2; ++nb)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) acc[c][nb][e] = 0.f;
+
+  dma(0);
+  for (int ks = 0; ks < kc_n; ++ks) {
+    __syncthreads();                       // R(ks) landed everywhere; V free
+    transform();
+    __syncthreads();                       // V(ks) complete; R free
+    bload(ks);
+    if (ks + 1 < kc_n) dma(ks + 1);
+#pragma unroll
+    for (int c = 0; c < CPW; ++c) {
+      const int xi = wave_u * CPW + c;
+      const int t = lane & 31;
+      const float4 a0 = *reinterpret_cast<const float4*>(V + v2idx(xi, t, 2 * h));
+      const float4 a1 = *reinterpret_cast<const float4*>(V + v2idx(xi, t, 2 * h + 1));
+      const float av[8] = {a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w};
+#pragma unroll
+      for (int nb = 0; nb < 2; ++nb) {
+        const float bv[8] = {bc[c][nb][0].x, bc[c][nb][0].y, bc[c][nb][0].z, bc[c][nb][0].w,
+                             bc[c][nb][1].x, bc[c][nb][1].y, bc[c][nb][1].z, bc[c][nb][1].w};
+#pragma unroll
+        for (int s8 = 0; s8 < 8; ++s8)        // MFMA step s, half h <-> channel 8h + s
+          acc[c][nb] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[s8], bv[s8], acc[c][nb], 0, 0, 0);
+      }
+    }
+  }
+
+  // ---- epilogue, two passes of 16 tiles: M[xi][tile - 16 pass][64 ch] (rows padded);
+  // lane roles as tile 65's VEC epilogue: tile wave + 4 it4 of the pass, channels n4 .. n4+3
+  float* M = smem;
+  EpiMax mx;
+  const int wpp = a.Cout_p >> 5;
+  const int it4 = lane >> 4, n4 = n0 + 4 * (lane & 15);
+  const float4 bias4 = (a.bias && n4 < a.N) ? *reinterpret_cast<const float4*>(a.bias + n4)
+                                            : make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+  for (int pass = 0; pass < 2; ++pass) {
+    // this pass's tile of the lane, its output mask and epilogue inputs (loads before any store)
+    int vb = 0, vti = 0, vtj = 0;
+    uint32_t vok = 0u;
+    EpiIn4 pre4[4];
+    {
+      const bool tl = tile_point(a, Ht, Wt, m0 + TH * pass + wave + NW * it4, vb, vti, vtj);
+      int4 bx = make_int4(0, 0, 1 << 30, 1 << 30);
+      if (a.gbox && tl) bx = reinterpret_cast<const int4*>(a.gbox)[vb];
+#pragma unroll
+      for (int p = 0; p < 4; ++p) {
+        const int i = 2 * vti + (p >> 1), j = 2 * vtj + (p & 1);
+        if (tl && n4 < a.N && i < a.Hout && j < a.Wout && i >= bx.x && i < bx.z && j >= bx.y && j < bx.w)
+          vok |= 1u << p;
+      }
+#pragma unroll
+      for (int p = 0; p < 4; ++p) {
+        if (!((vok >> p) & 1u)) continue;
+        const size_t pix = ((size_t)vb * a.Hout + 2 * vti + (p >> 1)) * a.Wout + 2 * vtj + (p & 1);
+        const size_t o = pix * (size_t)a.Cout_p + n4;
+        const size_t wo = pix * (size_t)(a.Cout_p >> 5) + (n4 >> 5);
+        if (a.res) pre4[p].res = *reinterpret_cast<const float4*>(a.res + o);
+        if (a.accumulate) pre4[p].yold = *reinterpret_cast<const float4*>(a.y + o);
+        if (a.mbits) pre4[p].m = a.mbits[wo];
+        if (a.y2 && a.m2bits) pre4[p].m2 = a.m2bits[wo];
+      }
+    }
+    __syncthreads();                       // the k-loop's (or the previous pass's) LDS reads are done
+#pragma unroll
+    for (int c = 0; c < CPW; ++c)
+#pragma unroll
+      for (int nb = 0; nb < 2; ++nb)
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const int ee = 8 * pass + e;
+          const int t = (ee & 3) + 8 * (ee >> 2) + 4 * h - TH * pass;
+          M[((wave * CPW + c) * TH + t) * M2_ROW + nb * 32 + (lane & 31)] = acc[c][nb][ee];
+        }
+    __syncthreads();
+    const int t = wave + NW * it4;
+    float4 s0[4], s1[4];
+#pragma unroll
+    for (int v = 0; v < 4; ++v) {
+      float4 m[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+        m[u] = *reinterpret_cast<const float4*>(M + ((u * 4 + v) * TH + t) * M2_ROW + 4 * (lane & 15));
+      s0[v] = f4add(f4add(m[0], m[1]), m[2]);
+      s1[v] = f4sub(f4sub(m[1], m[2]), m[3]);
+    }
+    const float4 yv[2][2] = {{f4add(f4add(s0[0], s0[1]), s0[2]), f4sub(f4sub(s0[1], s0[2]), s0[3])},
+                             {f4add(f4add(s1[0], s1[1]), s1[2]), f4sub(f4sub(s1[1], s1[2]), s1[3])}};
+#pragma unroll
+    for (int p = 0; p < 4; ++p) {
+      const bool ok = (vok >> p) & 1u;
+      const size_t pix = ((size_t)vb * a.Hout + 2 * vti + (p >> 1)) * a.Wout + 2 * vtj + (p & 1);
+      uint32_t nib = 0u;
+      if (ok) {
+        const float4 out = epi_store4(a, pix, n4, yv[p >> 1][p & 1], bias4, pre4[p], mx);
+        nib = (out.x > 0.f ? 1u : 0u) | (out.y > 0.f ? 2u : 0u) | (out.z > 0.f ? 4u : 0u) | (out.w > 0.f ? 8u : 0u);
+      }
+      if (a.ybits) {
+        // 8 lanes hold the 32 channels of one sign-bit word: OR their nibbles
+        uint32_t w = nib << (4 * (lane & 7));
+        w |= (uint32_t)__shfl_xor((int)w, 1);
+        w |= (uint32_t)__shfl_xor((int)w, 2);
+        w |= (uint32_t)__shfl_xor((int)w, 4);
+        if (ok && (lane & 7) == 0) a.ybits[pix * wpp + (n4 >> 5)] = w;
+      }
+    }
+  }
+  if (a.y_amax) po::amax_commit(a.y_amax, mx.y);
+  if (a.sum_amax) po::amax_commit(a.sum_amax, mx.s);
+  if (a.y2_amax) po::amax_commit(a.y2_amax, mx.y2);
+}
 }  // namespace
 
 namespace po {
@@ -785,7 +1000,8 @@ namespace po {
 // correlation over the full 3x3 neighbourhood on full maps (no windows, no
 // split-K, destination = source grid) with N % 32 == 0, Cin_p % 16 == 0 and
 // the transformed weights (po_conv_desc.Wwino).
-int launch_wino(const ConvArgs& a, const float* U, hipStream_t st, int bm, int waves, bool sched, bool vec) {
+int launch_wino(const ConvArgs& a, const float* U, hipStream_t st, int bm, int waves, bool sched, bool vec,
+                bool small_lds) {
   PO_REQUIRE(U, "po_conv: Winograd tile needs the transformed weights (Wwino)");
   PO_REQUIRE(a.prec == 0 && a.ntaps == 9 && a.tkw == 3 && (a.sdh == 1 || a.sdh == -1) && (a.sdw == 1 || a.sdw == -1) &&
                  a.dh0 == -a.sdh && a.dw0 == -a.sdw,
@@ -803,7 +1019,9 @@ int launch_wino(const ConvArgs& a, const float* U, hipStream_t st, int bm, int w
     ConvArgs b = a;
     b.ntiles_n = a.N / N2;
     const int ntm = ceil_div((int64_t)a.B * Ht * Wt, T2);
-    if (waves == 8 && sched && vec && a.res)
+    if (small_lds)
+      hipLaunchKernelGGL(conv_wino3_k, dim3(ntm * b.ntiles_n), dim3(256), 0, st, b, U, Ht, Wt);
+    else if (waves == 8 && sched && vec && a.res)
       hipLaunchKernelGGL((conv_wino2_k<8, true, 1, true>), dim3(ntm * b.ntiles_n), dim3(512), 0, st, b, U, Ht, Wt);
     else if (waves == 8 && sched && vec && (a.accumulate || a.mbits || a.mask || a.y2))
       hipLaunchKernelGGL((conv_wino2_k<8, true, 2, true>), dim3(ntm * b.ntiles_n), dim3(512), 0, st, b, U, Ht, Wt);

@@ -33,7 +33,7 @@ typedef void* po_stream_t;
 #define PO_EHIP -2     /* HIP runtime error */
 #define PO_EDEVICE -3  /* device is not gfx950 */
 
-#define PO_ABI_VERSION 14
+#define PO_ABI_VERSION 15
 #define PO_AMAX_SUB 64  /* sub-slots per max|x| slot (see po_conv_desc) */
 
 int po_abi_version(void);
@@ -383,7 +383,7 @@ typedef struct po_conv_desc {
   int8_t* pool_argmax;
 } po_conv_desc;
 
-#define PO_CONV_NTILES 65
+#define PO_CONV_NTILES 66
 /* Tile `t` (1-based): block rows BM (output pixels), block columns BN (output
  * channels), k-step BK (input channels).  Tiles 1..10 stage operands through
  * registers, 11..20 are the same shapes staged by LDS-DMA, 21..28 are
@@ -393,11 +393,14 @@ typedef struct po_conv_desc {
  * 3x3 convs (53..54); 55..56 are the 2-D tile halo kernel (8 x 16 output
  * pixels per tile) for 3x3 convs of input step 1 or 2 on full maps without
  * split-K or boxes; 57..60 the same 2-D tiles (and 16 x 16-pixel ones at input
- * step 1) reading the weights as MFMA fragments from Wfrag.  61..63 are the
- * exact-fp32 Winograd F(2x2,3x3) kernels (64 2x2-tiles x 32 channels; 32
- * tiles x 64 channels with LDS-DMA input, 4 or 8 waves; 16 input channels per
+ * step 1) reading the weights as MFMA fragments from Wfrag.  61..66 are the
+ * exact-fp32 Winograd F(2x2,3x3) kernels (61: 64 2x2-tiles x 32 channels;
+ * 62..66: 32 tiles x 64 channels with LDS-DMA input -- 62/63 4 or 8 waves,
+ * 64 scheduled, 65 with the vector epilogue, 66 as 65 in 4-wave workgroups
+ * with 72 KB of LDS, two per CU, bit-identical to 65; 16 input channels per
  * k-step) for stride-1 3x3 convs and their input gradients on full maps,
- * without split-K (needs Wwino; 62 and 63 need N % 64 == 0).  A tile that does not apply to a launch makes po_conv
+ * without split-K (needs Wwino; 62..66 need N % 64 == 0).  A tile that does
+ * not apply to a launch makes po_conv
  * return PO_EINVAL.  Returns PO_EINVAL for a bad index. */
 int po_conv_tile_info(int t, int* bm, int* bn, int* bk, int* prec);
 

@@ -15,7 +15,8 @@ from conftest import pkg_mod
 
 pytestmark = pytest.mark.gpu
 DEV = torch.device("cuda", 0)
-WINO_TILES = [61, 62, 63, 64, 65]   # 64 tiles x 32 ch; 32 tiles x 64 ch (LDS-DMA input, N % 64 == 0), 4 / 8 waves, 8 scheduled
+WINO_TILES = [61, 62, 63, 64, 65, 66]   # 64 tiles x 32 ch; 32 tiles x 64 ch (LDS-DMA input, N % 64 == 0), 4 / 8 waves,
+                                        # 8 scheduled, 4 waves in 72 KB of LDS
 
 
 def _rel(a, b):
@@ -53,7 +54,7 @@ def _setup(B, H, Cin, Cout, flip, seed):
                                                (4, 19, 512, 256, True), (1, 76, 128, 64, False),
                                                (2, 9, 16, 32, False)])
 def test_wino_matches_float64_conv(B, H, Cin, Cout, flip, WINO):
-    if WINO in (62, 63, 64, 65) and Cout % 64:
+    if WINO in (62, 63, 64, 65, 66) and Cout % 64:
         pytest.skip("tiles 62/63 take N % 64 == 0")
     nat = pkg_mod("_native")
     x, w, bias, wd, U = _setup(B, H, Cin, Cout, flip, seed=H * Cin + flip)
@@ -181,3 +182,53 @@ def test_wino_refuses_what_it_cannot_run(WINO):
     d.in_step = 2
     d.Hg = d.Wg = d.Hout = d.Wout = 4
     assert call(d) != 0                                             # stride 2
+
+
+@pytest.mark.parametrize("mode", ["fwd_bits", "fwd_shortcut", "dgrad_acc_bits", "dgrad_dual"])
+@pytest.mark.parametrize("B,H,Cin,Cout", [(2, 11, 64, 128), (3, 38, 256, 512), (1, 19, 512, 64)])
+def test_wino_tile66_bit_identical_to_65(mode, B, H, Cin, Cout):
+    """Tile 66 (4-wave workgroups in 72 KB of LDS, two per CU) runs tile 65's
+    transforms, MFMA order and epilogue arithmetic: the same bits in every
+    epilogue combination the training plan uses (sign bits and max|x| slots
+    included), ragged tile counts."""
+    nat = pkg_mod("_native")
+    flip = mode.startswith("dgrad")
+    x, w, bias, wd, U = _setup(B, H, Cin, Cout, flip, seed=H + Cin)
+    gen = torch.Generator().manual_seed(5)
+    xd = x.permute(0, 2, 3, 1).contiguous().to(DEV)
+    prev = torch.randn(B, H, H, Cout, generator=gen).to(DEV)
+    res = torch.randn(B, H, H, Cout, generator=gen).to(DEV)
+    mbits = torch.randint(-2 ** 31, 2 ** 31 - 1, (B, H, H, Cout // 32), generator=gen, dtype=torch.int32).to(DEV)
+    m2bits = torch.randint(-2 ** 31, 2 ** 31 - 1, (B, H, H, Cout // 32), generator=gen, dtype=torch.int32).to(DEV)
+    runs = []
+    for tile in (66, 65):
+        d = _desc(nat, B, H, Cin, Cout, tile, flip)
+        d.Wwino = U.data_ptr()
+        y = prev.clone()
+        ssum = torch.full_like(prev, float("nan"))
+        y2 = torch.full_like(prev, float("nan"))
+        bits = torch.zeros(B, H, H, Cout // 32, dtype=torch.int32, device=DEV)
+        slots = [torch.zeros(64, dtype=torch.int32, device=DEV) for _ in range(3)]
+        args = dict(bias=None, res=None, sum=None, y2=None)
+        if mode == "fwd_bits":
+            d.act, d.ybits = 1, bits.data_ptr()
+            args["bias"] = bias.to(DEV)
+        elif mode == "fwd_shortcut":
+            d.act, d.ybits = 1, bits.data_ptr()
+            args.update(bias=bias.to(DEV), res=res, sum=ssum)
+            d.sum_amax = slots[1].data_ptr()
+        elif mode == "dgrad_acc_bits":
+            d.accumulate, d.mbits = 1, mbits.data_ptr()
+        else:
+            d.mbits, d.m2bits = mbits.data_ptr(), m2bits.data_ptr()
+            args["y2"] = y2
+            d.y2_amax = slots[2].data_ptr()
+        d.y_amax = slots[0].data_ptr()
+        nat.call("po_conv", ctypes.byref(d), nat.ptr(xd), nat.ptr(wd), nat.ptr(args["bias"]), nat.ptr(y),
+                 nat.ptr(args["res"]), nat.ptr(args["sum"]), None, nat.ptr(args["y2"]), None, nat.stream())
+        torch.cuda.synchronize()
+        runs.append((y, ssum, y2, bits, [sl.max() for sl in slots]))
+    for a, b in zip(runs[0][:4], runs[1][:4]):
+        assert torch.equal(a.nan_to_num(7.0), b.nan_to_num(7.0))
+    assert [int(v) for v in runs[0][4]] == [int(v) for v in runs[1][4]]
+

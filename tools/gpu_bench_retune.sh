@@ -9,5 +9,5 @@ import json, sys
 d = json.loads(open("gpurun_out/%s/bench.json" % sys.argv[1]).read().strip().splitlines()[-1])
 print("fp32", d["value"], d["roofline"]["conv_ms_per_step"], d["roofline"]["frac"], "| fp16x3", d.get("value_fp16x3"))
 c = json.load(open("gpurun_out/%s/tiles/conv_tiles_yolov3_b16.json" % sys.argv[1]))
-print("winograd launches:", sum(1 for v in c.values() if v[0] in (61, 62, 63, 64)), "of", len(c))
+print("winograd launches:", sum(1 for v in c.values() if v[0] in (61, 62, 63, 64, 65, 66)), "of", len(c))
 PY
