@@ -970,22 +970,54 @@ __global__ __launch_bounds__(256, 2) void conv_wino3_k(const ConvArgs a, const f
     }
     const float4 yv[2][2] = {{f4add(f4add(s0[0], s0[1]), s0[2]), f4sub(f4sub(s0[1], s0[2]), s0[3])},
                              {f4add(f4add(s1[0], s1[1]), s1[2]), f4sub(f4sub(s1[1], s1[2]), s1[3])}};
+    if (a.pool_y) {
+      // fused k=2 stride-2 max pool (even map, no boxes: host checks): the
+      // lane's 2x2 Winograd tile is pool window (vti, vtj).  Bias + activation
+      // per element as epi_store4, then conv_pool_epilogue's rule and codes
+      // (first window position on ties, NaN wins; bit 3 | bit 2 = max <= 0 for
+      // a leaky conv); the conv output itself is not stored.
+      if (vok == 0xFu) {
+        float pv[4] = {0.f, 0.f, 0.f, 0.f};
+        uint32_t arg[4] = {0u, 0u, 0u, 0u};
 #pragma unroll
-    for (int p = 0; p < 4; ++p) {
-      const bool ok = (vok >> p) & 1u;
-      const size_t pix = ((size_t)vb * a.Hout + 2 * vti + (p >> 1)) * a.Wout + 2 * vtj + (p & 1);
-      uint32_t nib = 0u;
-      if (ok) {
-        const float4 out = epi_store4(a, pix, n4, yv[p >> 1][p & 1], bias4, pre4[p], mx);
-        nib = (out.x > 0.f ? 1u : 0u) | (out.y > 0.f ? 2u : 0u) | (out.z > 0.f ? 4u : 0u) | (out.w > 0.f ? 8u : 0u);
+        for (int k = 0; k < 4; ++k) {
+          const float4 v = yv[k >> 1][k & 1];
+          float x[4] = {v.x + bias4.x, v.y + bias4.y, v.z + bias4.z, v.w + bias4.w};
+#pragma unroll
+          for (int c = 0; c < 4; ++c) {
+            if (a.act) x[c] = po::leaky(x[c]);
+            if (k == 0 || x[c] > pv[c] || isnan(x[c])) { pv[c] = x[c]; arg[c] = (uint32_t)k; }
+          }
+        }
+        uint32_t code = 0u;
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+          if (a.act) arg[c] |= 8u | (pv[c] > 0.f ? 0u : 4u);
+          code |= arg[c] << (8 * c);
+          mx.y = fmaxf(mx.y, fabsf(pv[c]));
+        }
+        const size_t po = (((size_t)vb * (a.Hout >> 1) + vti) * (a.Wout >> 1) + vtj) * a.Cout_p + n4;
+        *reinterpret_cast<float4*>(a.pool_y + po) = make_float4(pv[0], pv[1], pv[2], pv[3]);
+        *reinterpret_cast<uint32_t*>(a.pool_am + po) = code;
       }
-      if (a.ybits) {
-        // 8 lanes hold the 32 channels of one sign-bit word: OR their nibbles
-        uint32_t w = nib << (4 * (lane & 7));
-        w |= (uint32_t)__shfl_xor((int)w, 1);
-        w |= (uint32_t)__shfl_xor((int)w, 2);
-        w |= (uint32_t)__shfl_xor((int)w, 4);
-        if (ok && (lane & 7) == 0) a.ybits[pix * wpp + (n4 >> 5)] = w;
+    } else {
+#pragma unroll
+      for (int p = 0; p < 4; ++p) {
+        const bool ok = (vok >> p) & 1u;
+        const size_t pix = ((size_t)vb * a.Hout + 2 * vti + (p >> 1)) * a.Wout + 2 * vtj + (p & 1);
+        uint32_t nib = 0u;
+        if (ok) {
+          const float4 out = epi_store4(a, pix, n4, yv[p >> 1][p & 1], bias4, pre4[p], mx);
+          nib = (out.x > 0.f ? 1u : 0u) | (out.y > 0.f ? 2u : 0u) | (out.z > 0.f ? 4u : 0u) | (out.w > 0.f ? 8u : 0u);
+        }
+        if (a.ybits) {
+          // 8 lanes hold the 32 channels of one sign-bit word: OR their nibbles
+          uint32_t w = nib << (4 * (lane & 7));
+          w |= (uint32_t)__shfl_xor((int)w, 1);
+          w |= (uint32_t)__shfl_xor((int)w, 2);
+          w |= (uint32_t)__shfl_xor((int)w, 4);
+          if (ok && (lane & 7) == 0) a.ybits[pix * wpp + (n4 >> 5)] = w;
+        }
       }
     }
   }
@@ -1012,6 +1044,8 @@ int launch_wino(const ConvArgs& a, const float* U, hipStream_t st, int bm, int w
   PO_REQUIRE(a.Hg == a.Hout && a.Wg == a.Wout && a.Hin == a.Hout && a.Win == a.Wout,
              "po_conv: Winograd tile needs source, grid and destination of one size");
   PO_REQUIRE(a.N % WN == 0 && a.Cin_p % WK == 0, "po_conv: Winograd tile needs N %% 32 == 0 and Cin_p %% 16 == 0");
+  PO_REQUIRE(!a.pool_y || (small_lds && a.N % N2 == 0 && a.Hout % 2 == 0 && a.Wout % 2 == 0 && !a.gbox),
+             "po_conv: a fused pool runs on Winograd tile 66 only (even map, no boxes)");
   const int Ht = (a.Hout + 1) / 2, Wt = (a.Wout + 1) / 2;
   PO_REQUIRE((int64_t)a.B * Ht * Wt < (1LL << 31), "po_conv: too many tiles");
   if (bm == T2) {

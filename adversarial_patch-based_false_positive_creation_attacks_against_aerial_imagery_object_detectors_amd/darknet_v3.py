@@ -254,8 +254,10 @@ class NetPlan:
                            and os.environ.get("ADVPATCH_FIRST_POOL", "1") != "0")
         # later conv + k=2 stride-2 pool pairs (yolov3-tiny blocks 2/3, 4/5): the pool
         # runs in the conv epilogue (po_conv_desc.pool_y, pool-order grid) when the
-        # conv's only consumer is the pool and it runs on the generic tiles anyway
-        # (Cin_p <= 32, where the tuner never picks Winograd); ADVPATCH_CONV_POOL=0: off
+        # conv's only consumer is the pool: with exact fp32 operands at any width
+        # (the generic tiles and Winograd tile 66 carry the pool epilogue), with
+        # fp16x3 operands at Cin_p <= 32 (generic tiles only, where the halo tiles
+        # do not win anyway); ADVPATCH_CONV_POOL=0: off
         self.conv_pool = set()
         if os.environ.get("ADVPATCH_CONV_POOL", "1") != "0":
             for i in range(1, n - 1):
@@ -264,7 +266,7 @@ class NetPlan:
                         and [j for j in range(n) if i in srcs[j]] == [i + 1]
                         and self.win[i] is None and self.win[i + 1] is None
                         and shp[i][0] % 2 == 0 and shp[i][1] % 2 == 0 and self.cp[i] % 16 == 0
-                        and srcs[i][0] != INPUT and self.cp[srcs[i][0]] <= 32
+                        and srcs[i][0] != INPUT and (self.cp[srcs[i][0]] <= 32 or net.conv_prec != "fp16x3")
                         and not (i - 1 == 0 and self.first_pool)):
                     self.conv_pool.add(i)
         self._build_grad_plan()

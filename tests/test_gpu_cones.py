@@ -218,8 +218,8 @@ def test_support_box_grid_leaves_the_patch_gradient_unchanged(tmp_path, monkeypa
 
 @pytest.mark.parametrize("prec", ["fp32", "fp16x3"])
 def test_conv_pool_fusion_leaves_the_step_unchanged(tmp_path, monkeypatch, prec):
-    """yolov3-tiny's conv + 2x2/2 max pool pairs (blocks 2/3 and 4/5,
-    darknet_v3.py:61-69) with the pool in the conv epilogue (po_conv_desc.pool_y,
+    """yolov3-tiny's conv + 2x2/2 max pool pairs (blocks 2/3, 4/5, 6/7 with exact
+    fp32 operands, 2/3 and 4/5 with fp16x3; darknet_v3.py:61-69) with the pool in the conv epilogue (po_conv_desc.pool_y,
     pool-order grid; the conv output is never stored, the argmax bytes carry
     the LeakyReLU slope): the same loss, pool outputs, window positions and
     patch gradient as the separate po_maxpool2_fwd (ADVPATCH_CONV_POOL=0) — bit
@@ -238,13 +238,14 @@ def test_conv_pool_fusion_leaves_the_step_unchanged(tmp_path, monkeypatch, prec)
         loss, terms = tr.losses(pg, img, lab, dr)
         loss.backward()
         plan = tr.last_plan
-        assert sorted(plan.conv_pool) == ([2, 4] if fuse == "1" else [])
-        pools = {j: (plan.act[j].clone(), plan.argmax[j].long() & 3) for j in (3, 5)}
+        fused = ([2, 4, 6] if prec == "fp32" else [2, 4]) if fuse == "1" else []
+        assert sorted(plan.conv_pool) == fused
+        pools = {j: (plan.act[j].clone(), plan.argmax[j].long() & 3) for j in (3, 5, 7)}
         out.append((float(loss.detach()), pools, pg.grad.detach().clone()))
     (l1, p1, g1), (l0, p0, g0) = out
     if prec == "fp32":
         assert l1 == l0
-        for j in (3, 5):
+        for j in (3, 5, 7):
             assert torch.equal(p1[j][0], p0[j][0]) and torch.equal(p1[j][1], p0[j][1])
         assert torch.equal(g1, g0)
     else:

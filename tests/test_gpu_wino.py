@@ -232,3 +232,45 @@ def test_wino_tile66_bit_identical_to_65(mode, B, H, Cin, Cout):
         assert torch.equal(a.nan_to_num(7.0), b.nan_to_num(7.0))
     assert [int(v) for v in runs[0][4]] == [int(v) for v in runs[1][4]]
 
+
+
+@pytest.mark.parametrize("act", [0, 1])
+@pytest.mark.parametrize("B,H,Cin,Cout", [(2, 12, 64, 128), (3, 26, 128, 256), (2, 104, 32, 64)])
+def test_wino_tile66_fused_pool(act, B, H, Cin, Cout):
+    """Tile 66 with the k=2 stride-2 max pool in its epilogue (po_conv_desc.pool_y):
+    pooled values, window positions and slope codes bit-identical to pooling
+    tile 66's own unpooled output by po_maxpool2_fwd's rule (first position on
+    ties), max|x| slot of the pooled map; tile 65 refuses a pooled launch."""
+    nat = pkg_mod("_native")
+    x, w, bias, wd, U = _setup(B, H, Cin, Cout, False, seed=H + Cout)
+    xd = x.permute(0, 2, 3, 1).contiguous().to(DEV)
+    bd = bias.to(DEV)
+    y = torch.full((B, H, H, Cout), float("nan"), device=DEV)
+    d = _desc(nat, B, H, Cin, Cout, 66)
+    d.Wwino, d.act = U.data_ptr(), act
+    nat.call("po_conv", ctypes.byref(d), nat.ptr(xd), nat.ptr(wd), nat.ptr(bd), nat.ptr(y), None, None, None, None,
+             None, nat.stream())
+    h = H // 2
+    py = torch.full((B, h, h, Cout), float("nan"), device=DEV)
+    pam = torch.full((B, h, h, Cout), -1, dtype=torch.int8, device=DEV)
+    slot = torch.zeros(64, dtype=torch.int32, device=DEV)
+    d = _desc(nat, B, H, Cin, Cout, 66)
+    d.Wwino, d.act = U.data_ptr(), act
+    d.pool_y, d.pool_argmax, d.y_amax = py.data_ptr(), pam.data_ptr(), slot.data_ptr()
+    nat.call("po_conv", ctypes.byref(d), nat.ptr(xd), nat.ptr(wd), nat.ptr(bd), None, None, None, None, None,
+             None, nat.stream())
+    torch.cuda.synchronize()
+    win = y.view(B, h, 2, h, 2, Cout)
+    pv, arg = win[:, :, 0, :, 0], torch.zeros(B, h, h, Cout, dtype=torch.int64, device=DEV)
+    for k in range(1, 4):
+        v = win[:, :, k >> 1, :, k & 1]
+        upd = (v > pv) | torch.isnan(v)
+        pv, arg = torch.where(upd, v, pv), torch.where(upd, torch.full_like(arg, k), arg)
+    if act:
+        arg = arg | 8 | torch.where(pv > 0, 0, 4)
+    assert torch.equal(py, pv)
+    assert torch.equal(pam.long(), arg)
+    assert int(slot.max()) == int(pv.abs().max().view(torch.int32))
+    d.tile = 65
+    assert nat.load().po_conv(ctypes.byref(d), nat.ptr(xd), nat.ptr(wd), nat.ptr(bd), None, None, None, None, None,
+                              None, nat.stream()) != 0
