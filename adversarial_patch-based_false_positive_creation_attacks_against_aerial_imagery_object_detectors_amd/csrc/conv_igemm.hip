@@ -526,8 +526,8 @@ extern "C" int po_conv(const po_conv_desc* d, const float* in, const float* W, c
   }
   while (bk > 16 && a.Cin_p % bk != 0) bk /= 2;
   int rc;
-  PO_REQUIRE((a.mrows == a.Hg * a.Wg && !a.pool_y) || gl <= 1 || (gl == 11 && a.mrows == a.Hg * a.Wg),
-             "po_conv: a compact box grid (mrows) runs on the generic tiles only, a fused pool on those and tile 66");
+  PO_REQUIRE((a.mrows == a.Hg * a.Wg && !a.pool_y) || gl <= 1 || ((gl == 5 || gl == 11) && a.mrows == a.Hg * a.Wg),
+             "po_conv: a compact box grid (mrows) runs on the generic tiles only, a fused pool on those and tiles 61/66");
   PO_REQUIRE(!a.pool_y || bm * bn <= 128 * 128,
              "po_conv: a fused pool needs a generic tile of at most 128x128 (got %dx%d)", bm, bn);
   if (a.prec == 1) {

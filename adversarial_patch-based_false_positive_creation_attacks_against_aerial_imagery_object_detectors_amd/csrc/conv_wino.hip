@@ -334,6 +334,27 @@ __global__ __launch_bounds__(256) void conv_wino_k(const ConvArgs a, const float
     }
     const float yv[2][2] = {{s0[0] + s0[1] + s0[2], s0[1] - s0[2] - s0[3]},
                             {s1[0] + s1[1] + s1[2], s1[1] - s1[2] - s1[3]}};
+    if (a.pool_y) {
+      // fused k=2 stride-2 max pool (even map, no boxes: host checks): the
+      // tile is pool window (tti, ttj); epi_store's bias + activation, then
+      // conv_pool_epilogue's rule and codes; the conv output is not stored
+      if (tl && n < a.N) {
+        float pv = 0.f;
+        uint32_t arg = 0u;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          float x = yv[k >> 1][k & 1] + (a.bias ? a.bias[n] : 0.f);
+          if (a.act) x = po::leaky(x);
+          if (k == 0 || x > pv || isnan(x)) { pv = x; arg = (uint32_t)k; }
+        }
+        if (a.act) arg |= 8u | (pv > 0.f ? 0u : 4u);
+        mx.y = fmaxf(mx.y, fabsf(pv));
+        const size_t po = (((size_t)bb * (a.Hout >> 1) + tti) * (a.Wout >> 1) + ttj) * a.Cout_p + n;
+        a.pool_y[po] = pv;
+        a.pool_am[po] = (int8_t)arg;
+      }
+      continue;
+    }
     int4 bx = make_int4(0, 0, 1 << 30, 1 << 30);
     if (a.gbox && tl) bx = reinterpret_cast<const int4*>(a.gbox)[bb];
 #pragma unroll
@@ -1044,8 +1065,8 @@ int launch_wino(const ConvArgs& a, const float* U, hipStream_t st, int bm, int w
   PO_REQUIRE(a.Hg == a.Hout && a.Wg == a.Wout && a.Hin == a.Hout && a.Win == a.Wout,
              "po_conv: Winograd tile needs source, grid and destination of one size");
   PO_REQUIRE(a.N % WN == 0 && a.Cin_p % WK == 0, "po_conv: Winograd tile needs N %% 32 == 0 and Cin_p %% 16 == 0");
-  PO_REQUIRE(!a.pool_y || (small_lds && a.N % N2 == 0 && a.Hout % 2 == 0 && a.Wout % 2 == 0 && !a.gbox),
-             "po_conv: a fused pool runs on Winograd tile 66 only (even map, no boxes)");
+  PO_REQUIRE(!a.pool_y || ((small_lds || bm == WT) && a.Hout % 2 == 0 && a.Wout % 2 == 0 && !a.gbox),
+             "po_conv: a fused pool runs on Winograd tiles 61 and 66 only (even map, no boxes)");
   const int Ht = (a.Hout + 1) / 2, Wt = (a.Wout + 1) / 2;
   PO_REQUIRE((int64_t)a.B * Ht * Wt < (1LL << 31), "po_conv: too many tiles");
   if (bm == T2) {

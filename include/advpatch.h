@@ -374,8 +374,8 @@ typedef struct po_conv_desc {
    * (staging 0/1). */
   int mrows;
   /* Optional fused k=2 stride-2 max pool of a plain forward conv (y_out NULL,
-   * full even grid, no split-K; generic tiles, or Winograd tile 66 without
-   * gbox -- its 2x2 output tiles are the windows): pool_y [B,Hout/2,Wout/2,Cout_p]
+   * full even grid, no split-K; generic tiles, or Winograd tiles 61/66
+   * without gbox -- their 2x2 output tiles are the windows): pool_y [B,Hout/2,Wout/2,Cout_p]
    * and pool_argmax (int8, same shape) as po_maxpool2_fwd writes them, the
    * argmax bytes of a leaky conv also carrying its LeakyReLU slope (bit 3
    * set, bit 2 = max <= 0; see po_conv_first_pool_fwd); the conv output

@@ -234,19 +234,23 @@ def test_wino_tile66_bit_identical_to_65(mode, B, H, Cin, Cout):
 
 
 
+@pytest.mark.parametrize("tile", [61, 66])
 @pytest.mark.parametrize("act", [0, 1])
-@pytest.mark.parametrize("B,H,Cin,Cout", [(2, 12, 64, 128), (3, 26, 128, 256), (2, 104, 32, 64)])
-def test_wino_tile66_fused_pool(act, B, H, Cin, Cout):
-    """Tile 66 with the k=2 stride-2 max pool in its epilogue (po_conv_desc.pool_y):
-    pooled values, window positions and slope codes bit-identical to pooling
-    tile 66's own unpooled output by po_maxpool2_fwd's rule (first position on
-    ties), max|x| slot of the pooled map; tile 65 refuses a pooled launch."""
+@pytest.mark.parametrize("B,H,Cin,Cout", [(2, 12, 64, 128), (3, 26, 128, 256), (2, 104, 32, 64), (2, 52, 16, 32)])
+def test_wino_fused_pool(act, B, H, Cin, Cout, tile):
+    """Tiles 61 and 66 with the k=2 stride-2 max pool in the epilogue
+    (po_conv_desc.pool_y): pooled values, window positions and slope codes
+    bit-identical to pooling the tile's own unpooled output by
+    po_maxpool2_fwd's rule (first position on ties), max|x| slot of the pooled
+    map; tile 65 refuses a pooled launch."""
+    if tile == 66 and Cout % 64:
+        pytest.skip("tile 66 takes N % 64 == 0")
     nat = pkg_mod("_native")
     x, w, bias, wd, U = _setup(B, H, Cin, Cout, False, seed=H + Cout)
     xd = x.permute(0, 2, 3, 1).contiguous().to(DEV)
     bd = bias.to(DEV)
     y = torch.full((B, H, H, Cout), float("nan"), device=DEV)
-    d = _desc(nat, B, H, Cin, Cout, 66)
+    d = _desc(nat, B, H, Cin, Cout, tile)
     d.Wwino, d.act = U.data_ptr(), act
     nat.call("po_conv", ctypes.byref(d), nat.ptr(xd), nat.ptr(wd), nat.ptr(bd), nat.ptr(y), None, None, None, None,
              None, nat.stream())
@@ -254,7 +258,7 @@ def test_wino_tile66_fused_pool(act, B, H, Cin, Cout):
     py = torch.full((B, h, h, Cout), float("nan"), device=DEV)
     pam = torch.full((B, h, h, Cout), -1, dtype=torch.int8, device=DEV)
     slot = torch.zeros(64, dtype=torch.int32, device=DEV)
-    d = _desc(nat, B, H, Cin, Cout, 66)
+    d = _desc(nat, B, H, Cin, Cout, tile)
     d.Wwino, d.act = U.data_ptr(), act
     d.pool_y, d.pool_argmax, d.y_amax = py.data_ptr(), pam.data_ptr(), slot.data_ptr()
     nat.call("po_conv", ctypes.byref(d), nat.ptr(xd), nat.ptr(wd), nat.ptr(bd), None, None, None, None, None,
