@@ -542,7 +542,14 @@ extern "C" int po_conv(const po_conv_desc* d, const float* in, const float* W, c
     return rc;
   }
   if (gl >= 5 && gl <= 8) return po::launch_wino(a, d->Wwino, st, bm, gl >= 6 ? 8 : 4, gl >= 7, gl == 8);
-  if (gl == 11) return po::launch_wino(a, d->Wwino, st, bm, 4, false, true, true);
+  if (gl == 11) {
+    rc = po::launch_wino(a, d->Wwino, st, bm, 4, false, true, true);
+    if (rc == PO_OK && a.ksplit > 1) {
+      hipLaunchKernelGGL(conv_reduce_k, dim3(po::ceil_div((int64_t)a.M * (a.N / (4 * RQ)), 256)), dim3(256), 0, st, a);
+      rc = po::check_launch("po_conv (winograd split-K reduce)");
+    }
+    return rc;
+  }
   if (bk > 32) bk = 32;
   if (gl) return bk == 32 ? dispatch<32, true>(a, st, bm, bn) : dispatch<16, true>(a, st, bm, bn);
   return bk == 32 ? dispatch<32, false>(a, st, bm, bn) : dispatch<16, false>(a, st, bm, bn);

@@ -905,13 +905,15 @@ __global__ __launch_bounds__(256, 2) void conv_wino3_k(const ConvArgs a, const f
 #pragma unroll
       for (int e = 0; e < 16; ++e) acc[c][nb][e] = 0.f;
 
-  dma(0);
-  for (int ks = 0; ks < kc_n; ++ks) {
+  // split-K (blockIdx.y = slice): input-channel steps [ks0, ks1) of kc_n
+  const int ks0 = (int)((int64_t)blockIdx.y * kc_n / a.ksplit), ks1 = (int)((int64_t)(blockIdx.y + 1) * kc_n / a.ksplit);
+  dma(ks0);
+  for (int ks = ks0; ks < ks1; ++ks) {
     __syncthreads();                       // R(ks) landed everywhere; V free
     transform();
     __syncthreads();                       // V(ks) complete; R free
     bload(ks);
-    if (ks + 1 < kc_n) dma(ks + 1);
+    if (ks + 1 < ks1) dma(ks + 1);
 #pragma unroll
     for (int c = 0; c < CPW; ++c) {
       const int xi = wave_u * CPW + c;
@@ -956,7 +958,7 @@ __global__ __launch_bounds__(256, 2) void conv_wino3_k(const ConvArgs a, const f
       }
 #pragma unroll
       for (int p = 0; p < 4; ++p) {
-        if (!((vok >> p) & 1u)) continue;
+        if (!((vok >> p) & 1u) || a.ksplit > 1) continue;
         const size_t pix = ((size_t)vb * a.Hout + 2 * vti + (p >> 1)) * a.Wout + 2 * vtj + (p & 1);
         const size_t o = pix * (size_t)a.Cout_p + n4;
         const size_t wo = pix * (size_t)(a.Cout_p >> 5) + (n4 >> 5);
@@ -991,7 +993,23 @@ __global__ __launch_bounds__(256, 2) void conv_wino3_k(const ConvArgs a, const f
     }
     const float4 yv[2][2] = {{f4add(f4add(s0[0], s0[1]), s0[2]), f4sub(f4sub(s0[1], s0[2]), s0[3])},
                              {f4add(f4add(s1[0], s1[1]), s1[2]), f4sub(f4sub(s1[1], s1[2]), s1[3])}};
-    if (a.pool_y) {
+    if (a.ksplit > 1) {
+      // split-K slice: the raw inverse-transformed partial sums at the GEMM rows
+      // conv_reduce_k enumerates (grid_point: row-major over the map, or over
+      // the image's box), which applies the epilogue
+      float* ws = a.ws + (size_t)blockIdx.y * a.M * a.N;
+      int i0 = 0, j0 = 0, gw = a.Wg;
+      if (a.gbox) {
+        const po::GridBox g = po::grid_box(a, vb);
+        i0 = g.i0, j0 = g.j0, gw = g.w;
+      }
+#pragma unroll
+      for (int p = 0; p < 4; ++p) {
+        if (!((vok >> p) & 1u)) continue;
+        const int l = (2 * vti + (p >> 1) - i0) * gw + 2 * vtj + (p & 1) - j0;
+        *reinterpret_cast<float4*>(ws + ((size_t)vb * a.mrows + l) * a.N + n4) = yv[p >> 1][p & 1];
+      }
+    } else if (a.pool_y) {
       // fused k=2 stride-2 max pool (even map, no boxes: host checks): the
       // lane's 2x2 Winograd tile is pool window (vti, vtj).  Bias + activation
       // per element as epi_store4, then conv_pool_epilogue's rule and codes
@@ -1042,6 +1060,7 @@ __global__ __launch_bounds__(256, 2) void conv_wino3_k(const ConvArgs a, const f
       }
     }
   }
+  if (a.ksplit > 1) return;                // conv_reduce_k commits the max|x| slots
   if (a.y_amax) po::amax_commit(a.y_amax, mx.y);
   if (a.sum_amax) po::amax_commit(a.sum_amax, mx.s);
   if (a.y2_amax) po::amax_commit(a.y2_amax, mx.y2);
@@ -1061,7 +1080,9 @@ int launch_wino(const ConvArgs& a, const float* U, hipStream_t st, int bm, int w
              "po_conv: Winograd tile needs a full 3x3 neighbourhood of taps");
   PO_REQUIRE(a.in_step == 1 && a.out_step == 1 && a.out_oy == 0 && a.out_ox == 0 && !a.in_org && !a.out_org,
              "po_conv: Winograd tile needs stride 1 on full maps");
-  PO_REQUIRE(a.ksplit == 1, "po_conv: Winograd tile has no split-K");
+  PO_REQUIRE(a.ksplit == 1 || (small_lds && !a.pool_y && a.ws && a.ksplit <= a.Cin_p / WK &&
+                                (int64_t)a.M * a.N < (1LL << 31)),
+             "po_conv: split-K runs on Winograd tile 66 only (ksplit <= Cin_p / 16, with a workspace)");
   PO_REQUIRE(a.Hg == a.Hout && a.Wg == a.Wout && a.Hin == a.Hout && a.Win == a.Wout,
              "po_conv: Winograd tile needs source, grid and destination of one size");
   PO_REQUIRE(a.N % WN == 0 && a.Cin_p % WK == 0, "po_conv: Winograd tile needs N %% 32 == 0 and Cin_p %% 16 == 0");
@@ -1075,7 +1096,7 @@ int launch_wino(const ConvArgs& a, const float* U, hipStream_t st, int bm, int w
     b.ntiles_n = a.N / N2;
     const int ntm = ceil_div((int64_t)a.B * Ht * Wt, T2);
     if (small_lds)
-      hipLaunchKernelGGL(conv_wino3_k, dim3(ntm * b.ntiles_n), dim3(256), 0, st, b, U, Ht, Wt);
+      hipLaunchKernelGGL(conv_wino3_k, dim3(ntm * b.ntiles_n, a.ksplit), dim3(256), 0, st, b, U, Ht, Wt);
     else if (waves == 8 && sched && vec && a.res)
       hipLaunchKernelGGL((conv_wino2_k<8, true, 1, true>), dim3(ntm * b.ntiles_n), dim3(512), 0, st, b, U, Ht, Wt);
     else if (waves == 8 && sched && vec && (a.accumulate || a.mbits || a.mask || a.y2))

@@ -1095,6 +1095,7 @@ class NetPlan:
     # ---------------- autotuning ----------------
     SPLITS = (2, 4, 8, 16, 32)
     WS_FLOATS = 64 << 20          # split-K workspace cap (256 MB)
+    WINO_SPLIT_TILES = (66,)      # Winograd tiles with split-K (conv_wino3_k)
 
     def _ensure_ws(self, floats):
         if self.ws is None or self.ws.numel() < floats:
@@ -1167,6 +1168,10 @@ class NetPlan:
                 if ntiles < 256:
                     cands += [k for k in self.SPLITS if k * ntiles <= 2048 and nks // k >= 4
                               and k * M * desc.N <= self.WS_FLOATS]
+                elif t in self.WINO_SPLIT_TILES and not desc.pool_y:
+                    # input-channel slices re-quantise a Winograd launch whose
+                    # workgroup count fills the 512 slots badly (19x19 maps: 800)
+                    cands += [k for k in (2, 3) if desc.Cin_p // bk // k >= 8 and k * M * desc.N <= self.WS_FLOATS]
                 for ks in cands:
                     self._set_tile(desc, (t, ks))
                     if lib.po_conv(*args, st) != 0:      # tile not applicable to this launch

@@ -400,8 +400,8 @@ typedef struct po_conv_desc {
  * 64 scheduled, 65 with the vector epilogue, 66 as 65 in 4-wave workgroups
  * with 72 KB of LDS, two per CU, bit-identical to 65; 16 input channels per
  * k-step) for stride-1 3x3 convs and their input gradients on full maps,
- * without split-K (needs Wwino; 62..66 need N % 64 == 0).  A tile that does
- * not apply to a launch makes po_conv
+ * without split-K except on 66 (needs Wwino; 62..66 need N % 64 == 0).  A
+ * tile that does not apply to a launch makes po_conv
  * return PO_EINVAL.  Returns PO_EINVAL for a bad index. */
 int po_conv_tile_info(int t, int* bm, int* bn, int* bk, int* prec);
 

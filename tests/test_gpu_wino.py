@@ -176,7 +176,9 @@ def test_wino_refuses_what_it_cannot_run(WINO):
     assert call(d) == 0
     ws = torch.empty(4 * B * H * H * Cout, device=DEV)
     d.ksplit, d.workspace = 2, ws.data_ptr()
-    assert call(d) != 0                                             # no split-K
+    assert (call(d) == 0) == (WINO == 66)                           # split-K: tile 66 only
+    d.ksplit = 3
+    assert call(d) != 0                                             # more slices than 16-channel steps
     d = _desc(nat, B, H, Cin, Cout, WINO)
     d.Wwino = U.data_ptr()
     d.in_step = 2
@@ -278,3 +280,75 @@ def test_wino_fused_pool(act, B, H, Cin, Cout, tile):
     d.tile = 65
     assert nat.load().po_conv(ctypes.byref(d), nat.ptr(xd), nat.ptr(wd), nat.ptr(bd), None, None, None, None, None,
                               None, nat.stream()) != 0
+
+
+@pytest.mark.parametrize("ks", [2, 3])
+@pytest.mark.parametrize("boxed", [False, True])
+@pytest.mark.parametrize("mode", ["fwd_bits", "fwd_shortcut", "dgrad_acc_bits", "dgrad_dual"])
+def test_wino_tile66_split_k(mode, boxed, ks):
+    """Tile 66 with input-channel slices (blockIdx.y) writing raw partial
+    sums at conv_reduce_k's GEMM rows (the box's compact rows with gbox), the
+    reduction applying the epilogue: the unsplit launch's values within the
+    fp32 summation-order class, untouched pixels outside the box, sign bits of
+    the written values and max|x| slots bounding them; odd map side."""
+    nat = pkg_mod("_native")
+    B, H, Cin, Cout = 3, 19, 256, 128
+    flip = mode.startswith("dgrad")
+    x, w, bias, wd, U = _setup(B, H, Cin, Cout, flip, seed=11)
+    gen = torch.Generator().manual_seed(12)
+    xd = x.permute(0, 2, 3, 1).contiguous().to(DEV)
+    prev = torch.randn(B, H, H, Cout, generator=gen).to(DEV)
+    res = torch.randn(B, H, H, Cout, generator=gen).to(DEV)
+    mbits = torch.randint(-2 ** 31, 2 ** 31 - 1, (B, H, H, Cout // 32), generator=gen, dtype=torch.int32).to(DEV)
+    m2bits = torch.randint(-2 ** 31, 2 ** 31 - 1, (B, H, H, Cout // 32), generator=gen, dtype=torch.int32).to(DEV)
+    box = torch.tensor([[3, 5, 14, 18], [0, 0, 19, 19], [11, 0, 12, 19]], dtype=torch.int32, device=DEV)
+    ws = torch.full((ks * B * H * H * Cout,), float("nan"), device=DEV)
+    runs = []
+    for split in (1, ks):
+        d = _desc(nat, B, H, Cin, Cout, 66, flip)
+        d.Wwino = U.data_ptr()
+        if split > 1:
+            d.ksplit, d.workspace = split, ws.data_ptr()
+        d.gbox = box.data_ptr() if boxed else None
+        y = prev.clone()
+        ssum = torch.full_like(prev, float("nan"))
+        y2 = torch.full_like(prev, float("nan"))
+        bits = torch.zeros(B, H, H, Cout // 32, dtype=torch.int32, device=DEV)
+        slots = [torch.zeros(64, dtype=torch.int32, device=DEV) for _ in range(3)]
+        args = dict(bias=None, res=None, sum=None, y2=None)
+        if mode == "fwd_bits":
+            d.act, d.ybits = 1, bits.data_ptr()
+            args["bias"] = bias.to(DEV)
+        elif mode == "fwd_shortcut":
+            d.act, d.ybits = 1, bits.data_ptr()
+            args.update(bias=bias.to(DEV), res=res, sum=ssum)
+            d.sum_amax = slots[1].data_ptr()
+        elif mode == "dgrad_acc_bits":
+            d.accumulate, d.mbits = 1, mbits.data_ptr()
+        else:
+            d.mbits, d.m2bits = mbits.data_ptr(), m2bits.data_ptr()
+            args["y2"] = y2
+            d.y2_amax = slots[2].data_ptr()
+        d.y_amax = slots[0].data_ptr()
+        nat.call("po_conv", ctypes.byref(d), nat.ptr(xd), nat.ptr(wd), nat.ptr(args["bias"]), nat.ptr(y),
+                 nat.ptr(args["res"]), nat.ptr(args["sum"]), None, nat.ptr(args["y2"]), None, nat.stream())
+        torch.cuda.synchronize()
+        runs.append((y.cpu(), ssum.cpu(), y2.cpu(), bits.cpu(), [sl.cpu().view(torch.float32).max() for sl in slots]))
+    (y1, s1, z1, b1, sl1), (yk, sk, zk, bk, slk) = runs
+    inside = torch.ones(B, H, H, dtype=torch.bool)
+    if boxed:
+        inside[:] = False
+        for b, (r0, c0, r1, c1) in enumerate(box.cpu().tolist()):
+            inside[b, r0:r1, c0:c1] = True
+    assert torch.equal(yk[~inside], prev.cpu()[~inside])
+    assert _rel(yk[inside], y1[inside]) < 1e-5
+    if mode.startswith("fwd"):
+        sh = torch.arange(32, dtype=torch.int32)
+        got = ((bk.unsqueeze(-1) >> sh) & 1).reshape(B, H, H, Cout).bool()
+        assert torch.equal(got[inside], yk[inside] > 0)
+    if mode == "fwd_shortcut":
+        assert _rel(sk[inside], s1[inside]) < 1e-5 and float(slk[1]) >= float(sk[inside].abs().max())
+    if mode == "dgrad_dual":
+        assert _rel(zk[inside], z1[inside]) < 1e-5 and float(slk[2]) >= float(zk[inside].abs().max())
+    assert float(slk[0]) >= float(yk[inside].abs().max()) * (1 - 1e-7)
+

@@ -37,6 +37,11 @@ if d.tile in (61, 62, 63, 64, 65, 66):                                     # Win
     offs = [(d.dh[t], d.dw[t]) for t in range(9)]
     U = ge._pkg("darknet_v3").wino_transform(w, offs)
     d.Wwino = U.data_ptr()
+ws = None
+if int(os.environ.get("MICRO_KSPLIT", "1")) > 1:        # split-K slices + conv_reduce_k
+    d.ksplit = int(os.environ["MICRO_KSPLIT"])
+    ws = torch.empty(d.ksplit * B * Ho * Ho * Cout, device=dev)
+    d.workspace = ws.data_ptr()
 res = sm = None
 if os.environ.get("MICRO_RES") == "1":                 # fused shortcut epilogue (res + sum_out) and sign bits
     res = torch.randn(B, Ho, Ho, Cout, device=dev)
