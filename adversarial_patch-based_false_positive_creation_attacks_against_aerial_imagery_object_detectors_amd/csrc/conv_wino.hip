@@ -802,7 +802,7 @@ __global__ __launch_bounds__(64 * NW) void conv_wino2_k(const ConvArgs a, const 
 
 // ---------------------------------------------------------------------------
 // Tile 66 (staging 11): tile 65's work (32 tiles x 64 channels, VEC epilogue)
-// as 4-wave workgroups in 72 KB of LDS instead of 8 waves in 144 KB, so that
+// as 4-wave workgroups in 64 KB of LDS instead of 8 waves in 144 KB, so that
 // two workgroups share a CU (2 waves per SIMD, as tile 65) and one
 // workgroup's prologue/epilogue overlaps the other's k-loop: tile 65 spends
 // 6-36% of a launch outside its k-loop with nothing else on the CU
@@ -816,7 +816,8 @@ __global__ __launch_bounds__(256, 2) void conv_wino3_k(const ConvArgs a, const f
   constexpr int CPW = 16 / NW;           // components per wave (4)
   constexpr int DPW = 32 / NW;           // DMA instructions per wave per k-step (8)
   constexpr int TH = T2 / 2;             // tiles per epilogue pass
-  __shared__ __attribute__((aligned(16))) float smem[16 * TH * M2_ROW];   // 72 KB (k-loop: R + V = 64 KB)
+  constexpr int M3_ROW = N2;             // epilogue rows unpadded: 64 KB, the k-loop's R + V
+  __shared__ __attribute__((aligned(16))) float smem[16 * TH * M3_ROW];
   __shared__ int s_live;
   float* R = smem;                       // [16 p][T2][WK]
   float* V = smem + R2_FLOATS;           // [16 xi][T2][WK] (swizzled chunks)
@@ -977,7 +978,7 @@ __global__ __launch_bounds__(256, 2) void conv_wino3_k(const ConvArgs a, const f
         for (int e = 0; e < 8; ++e) {
           const int ee = 8 * pass + e;
           const int t = (ee & 3) + 8 * (ee >> 2) + 4 * h - TH * pass;
-          M[((wave * CPW + c) * TH + t) * M2_ROW + nb * 32 + (lane & 31)] = acc[c][nb][ee];
+          M[((wave * CPW + c) * TH + t) * M3_ROW + nb * 32 + (lane & 31)] = acc[c][nb][ee];
         }
     __syncthreads();
     const int t = wave + NW * it4;
@@ -987,7 +988,7 @@ __global__ __launch_bounds__(256, 2) void conv_wino3_k(const ConvArgs a, const f
       float4 m[4];
 #pragma unroll
       for (int u = 0; u < 4; ++u)
-        m[u] = *reinterpret_cast<const float4*>(M + ((u * 4 + v) * TH + t) * M2_ROW + 4 * (lane & 15));
+        m[u] = *reinterpret_cast<const float4*>(M + ((u * 4 + v) * TH + t) * M3_ROW + 4 * (lane & 15));
       s0[v] = f4add(f4add(m[0], m[1]), m[2]);
       s1[v] = f4sub(f4sub(m[1], m[2]), m[3]);
     }

@@ -398,7 +398,7 @@ typedef struct po_conv_desc {
  * exact-fp32 Winograd F(2x2,3x3) kernels (61: 64 2x2-tiles x 32 channels;
  * 62..66: 32 tiles x 64 channels with LDS-DMA input -- 62/63 4 or 8 waves,
  * 64 scheduled, 65 with the vector epilogue, 66 as 65 in 4-wave workgroups
- * with 72 KB of LDS, two per CU, bit-identical to 65; 16 input channels per
+ * with 64 KB of LDS, two per CU, bit-identical to 65; 16 input channels per
  * k-step) for stride-1 3x3 convs and their input gradients on full maps,
  * without split-K except on 66 (needs Wwino; 62..66 need N % 64 == 0).  A
  * tile that does not apply to a launch makes po_conv

@@ -16,7 +16,7 @@ from conftest import pkg_mod
 pytestmark = pytest.mark.gpu
 DEV = torch.device("cuda", 0)
 WINO_TILES = [61, 62, 63, 64, 65, 66]   # 64 tiles x 32 ch; 32 tiles x 64 ch (LDS-DMA input, N % 64 == 0), 4 / 8 waves,
-                                        # 8 scheduled, 4 waves in 72 KB of LDS
+                                        # 8 scheduled, 4 waves in 64 KB of LDS
 
 
 def _rel(a, b):
@@ -189,7 +189,7 @@ def test_wino_refuses_what_it_cannot_run(WINO):
 @pytest.mark.parametrize("mode", ["fwd_bits", "fwd_shortcut", "dgrad_acc_bits", "dgrad_dual"])
 @pytest.mark.parametrize("B,H,Cin,Cout", [(2, 11, 64, 128), (3, 38, 256, 512), (1, 19, 512, 64)])
 def test_wino_tile66_bit_identical_to_65(mode, B, H, Cin, Cout):
-    """Tile 66 (4-wave workgroups in 72 KB of LDS, two per CU) runs tile 65's
+    """Tile 66 (4-wave workgroups in 64 KB of LDS, two per CU) runs tile 65's
     transforms, MFMA order and epilogue arithmetic: the same bits in every
     epilogue combination the training plan uses (sign bits and max|x| slots
     included), ragged tile counts."""
