@@ -138,8 +138,21 @@ def last_error():
     return load().po_last_error().decode(errors="replace")
 
 
+# Per-entry HIP-event timing for bench.py's roofline pass: {entry name: [(e0, e1), ...]}
+# (events recorded on the current torch stream, the stream every entry is launched on), or None.
+TIMERS = None
+
+
 def call(name, *args):
-    rc = getattr(load(), name)(*args)
+    timers = TIMERS
+    if timers is not None and name in timers:
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        rc = getattr(load(), name)(*args)
+        e1.record()
+        timers[name].append((e0, e1))
+    else:
+        rc = getattr(load(), name)(*args)
     if rc != 0:
         raise RuntimeError("%s failed (%d): %s" % (name, rc, last_error()))
 

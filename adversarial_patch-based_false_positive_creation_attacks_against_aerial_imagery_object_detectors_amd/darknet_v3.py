@@ -544,6 +544,83 @@ class NetPlan:
                   for r0, c0, r1, c1 in bx)
         return desc.macs * pts / (desc.B * desc.Hg * desc.Wg)
 
+    # Winograd tiles of po_conv: (tiles = GEMM rows, output channels) per workgroup
+    WINO_TILES = {61: (64, 32), 62: (32, 64), 63: (32, 64), 64: (32, 64), 65: (32, 64), 66: (32, 64)}
+    _tile_shapes = {}
+
+    @classmethod
+    def tile_shape(cls, t):
+        """(BM, BN, BK) of po_conv tile t (po_conv_tile_info)."""
+        if t not in cls._tile_shapes:
+            bm, bn, bk, pr = nat.c_int(), nat.c_int(), nat.c_int(), nat.c_int()
+            nat.call("po_conv_tile_info", t, nat.ctypes.byref(bm), nat.ctypes.byref(bn), nat.ctypes.byref(bk),
+                     nat.ctypes.byref(pr))
+            cls._tile_shapes[t] = (bm.value, bn.value, bk.value)
+        return cls._tile_shapes[t]
+
+    @classmethod
+    def launch_mfma_flops(cls, desc, cones=None):
+        """FLOPs the matrix cores EXECUTE for one exact-fp32 po_conv launch
+        (v_mfma_f32_32x32x2_f32, 4096 FLOP each), as the kernels enumerate
+        their work: every workgroup that holds a live row runs its whole
+        BM x BN tile over every k-step (padded channels, ragged tile rows and
+        the dead rows of a boxed workgroup included; a workgroup whose rows
+        are all dead exits before its first MFMA).
+
+        * direct tiles: 2 * live M-tiles * BM * ceil(N/BN)*BN * ntaps * Cin_p;
+        * Winograd F(2x2,3x3) tiles (61-66): 2 * 16 * live workgroups * WT
+          * Cin_p * N — 16 transform-domain GEMMs over the 2x2 output tiles,
+          4/9 of the direct-conv MFMA work of the same launch.
+        Boxed launches (gbox) count the live rows of this step's boxes
+        (conv_common.h grid_point / conv_wino.hip tile_point)."""
+        if desc.prec != 0:
+            return None
+        t = desc.tile
+        boxes = None
+        if getattr(desc, "support", None) is not None:
+            boxes = desc.support.cpu().tolist()
+        elif desc.gbox and cones is not None:
+            boxes = cones[desc.cone_block, desc.cone_b0:desc.cone_b0 + desc.B].cpu().tolist()
+        if t in cls.WINO_TILES:
+            WT, WN = cls.WINO_TILES[t]
+            Ht, Wt = (desc.Hg + 1) // 2, (desc.Wg + 1) // 2
+            per = Ht * Wt
+            if boxes is None:
+                live = [per] * desc.B
+            else:
+                live = []
+                for r0, c0, r1, c1 in boxes:
+                    h = max(((r1 + 1) >> 1) - (r0 >> 1), 0)
+                    w = max(((c1 + 1) >> 1) - (c0 >> 1), 0)
+                    live.append(min(h * w, per))
+            nwg = cls._live_groups(live, per, WT, desc.B)
+            return 2.0 * 16 * nwg * WT * desc.Cin_p * desc.N
+        BM, BN, BK = cls.tile_shape(t)
+        mrows = desc.mrows or desc.Hg * desc.Wg
+        if boxes is None:
+            live = [mrows] * desc.B
+        else:
+            def span(lo, hi, off, step, n):
+                a = 0 if lo - off <= 0 else -(-(lo - off) // step)
+                b = 0 if hi - 1 - off < 0 else min(n, (hi - 1 - off) // step + 1)
+                return max(b - a, 0)
+            live = [min(span(r0, r1, desc.out_oy, desc.out_step, desc.Hg) *
+                        span(c0, c1, desc.out_ox, desc.out_step, desc.Wg), mrows) for r0, c0, r1, c1 in boxes]
+        ntm = cls._live_groups(live, mrows, BM, desc.B)
+        return 2.0 * ntm * BM * (-(-desc.N // BN) * BN) * desc.ntaps * desc.Cin_p
+
+    @staticmethod
+    def _live_groups(live, per, rows, B):
+        """Workgroups of ``rows`` consecutive GEMM rows (image b owns rows
+        [b*per, b*per + per), its first live[b] of them live) holding a live row."""
+        if all(n == per for n in live):
+            return -(-(B * per) // rows)
+        ids = set()
+        for b, n in enumerate(live):
+            if n > 0:
+                ids.update(range((b * per) // rows, (b * per + n - 1) // rows + 1))
+        return len(ids)
+
     def _cone_ptr(self, s, b0):
         """po_conv gbox of a dgrad writing block s's gradient (images from b0)."""
         if s == INPUT or s not in self.cone_blocks:

@@ -127,11 +127,15 @@ def cpu_baseline(cfg, S, P, B=16, warmup=1, iters=3):
                       % (B, S, iters, warmup, el, cores, os.cpu_count() or 0, _cpu_model())}
 
 
+WARP_ENTRIES = ("po_warp_fwd", "po_warp_bwd")
+
+
 def measure(tr, prec, patch, img, lab, B, world, rank, steps, warmup, weights):
     """Warm-up, K timed steps (barrier + synchronize on both sides, max over
     ranks), then K instrumented steps with HIP events around every po_conv
-    launch (the roofline pass; kept out of the timed region because each
-    event pair adds a ~10 us dispatch gap, profiles/r01)."""
+    launch and every warp entry (the roofline pass; kept out of the timed
+    region because each event pair adds a ~10 us dispatch gap, profiles/r01)."""
+    nat = ge._pkg("_native")
     net = tr.darknet_model
     net.conv_prec = prec
     opt = tr.make_optimizer(patch)
@@ -163,6 +167,7 @@ def measure(tr, prec, patch, img, lab, B, world, rank, steps, warmup, weights):
         torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
         elapsed = float(t)
     plan.conv_timer = []
+    nat.TIMERS = {k: [] for k in WARP_ENTRIES}
     torch.cuda.synchronize()
     t1 = time.perf_counter()
     for _ in range(steps):
@@ -170,13 +175,37 @@ def measure(tr, prec, patch, img, lab, B, world, rank, steps, warmup, weights):
     torch.cuda.synchronize()
     instrumented_ms = (time.perf_counter() - t1) * 1000.0 / steps
     timer, plan.conv_timer = plan.conv_timer, None
+    warp, nat.TIMERS = nat.TIMERS, None
     conv_ms = sum(e0.elapsed_time(e1) for e0, e1, _, _ in timer) / steps
     # MACs actually computed: a boxed dgrad (gradient cones) counts its boxes only
     conv_flops = 2.0 * sum(plan.launch_macs(d, c) for _, _, d, c in timer) / steps
+    # per tile family: time, dense-equivalent FLOPs and the FLOPs the matrix cores execute
+    fam = {}
+    for e0, e1, d, c in timer:
+        key = "winograd" if d.tile in plan.WINO_TILES else "direct"
+        f = fam.setdefault(key, {"ms": 0.0, "flops": 0.0, "mfma_flops": 0.0, "launches": 0, "tiles": {}})
+        ms = e0.elapsed_time(e1)
+        mf = plan.launch_mfma_flops(d, c)
+        f["ms"] += ms
+        f["flops"] += 2.0 * plan.launch_macs(d, c)
+        f["mfma_flops"] += mf or 0.0
+        f["launches"] += 1
+        tt = f["tiles"].setdefault(int(d.tile), {"ms": 0.0, "mfma_flops": 0.0, "launches": 0})
+        tt["ms"] += ms
+        tt["mfma_flops"] += mf or 0.0
+        tt["launches"] += 1
+    for f in fam.values():
+        for key in ("ms", "flops", "mfma_flops", "launches"):
+            f[key] /= steps
+        for tt in f["tiles"].values():
+            for key in ("ms", "mfma_flops", "launches"):
+                tt[key] /= steps
+    warp_ms = {k: sum(e0.elapsed_time(e1) for e0, e1 in v) / steps for k, v in warp.items()}
     tr.check_flags()
     return {"elapsed": elapsed, "ms_per_step": elapsed * 1000.0 / steps, "value": world * B * steps / elapsed,
-            "conv_ms": conv_ms, "conv_flops": conv_flops, "launches": len(timer) // steps,
-            "instrumented_ms": instrumented_ms, "loss": float(terms["loss"].detach()), "plan": plan}
+            "conv_ms": conv_ms, "conv_flops": conv_flops, "launches": len(timer) // steps, "families": fam,
+            "warp_ms": warp_ms, "instrumented_ms": instrumented_ms, "loss": float(terms["loss"].detach()),
+            "plan": plan}
 
 
 def roofline(cfg_name, B, prec, m, ref_flops_step):
@@ -187,24 +216,115 @@ def roofline(cfg_name, B, prec, m, ref_flops_step):
             traffic = json.load(f).get("conv_hbm_bytes_per_step")
     achieved = m["conv_flops"] / (m["conv_ms"] * 1e-3) / 1e12
     peak = PEAK_CONV[prec]
-    return {"bound": "mfma",
-            "kernel": "po_conv implicit GEMM (%s): every Darknet fwd + dgrad launch of a step" % (
-                "conv_h3*_k, fp16x3 split operands" if prec == "fp16x3" else "conv_k, exact fp32 v_mfma_f32_32x32x2_f32"),
-            "achieved": achieved, "peak": peak, "unit": "TFLOP/s", "frac": achieved / peak, "traffic": traffic,
-            "traffic_per": "step: HBM bytes of all conv launches + split-K reduces (rocprofv3 FETCH_SIZE/WRITE_SIZE "
-                           "passes, profiles/traffic_*.json)",
-            "peak_note": "fp32-equivalent: fp16 dense 2500 / 3 products" if prec == "fp16x3" else "fp32 dense MFMA",
-            "flops_per_step": m["conv_flops"], "conv_ms_per_step": m["conv_ms"],
-            "conv_launches_per_step": m["launches"],
-            "measured_on": "a second pass of K steps with per-launch HIP events (%.3f ms/step instrumented vs %.3f "
-                           "plain)" % (m["instrumented_ms"], m["ms_per_step"]),
-            "reference_dense_flops_per_step": ref_flops_step,
-            # SURVEY §8d's algorithmic rate: the reference's dense fwd + dgrad FLOPs of the
-            # images processed, over the whole step's wall time (windows, cones and Winograd
-            # skip part of that work, so this can exceed the MFMA peak)
-            "achieved_algorithmic": ref_flops_step / (m["ms_per_step"] * 1e-3) / 1e12,
-            "frac_algorithmic": ref_flops_step / (m["ms_per_step"] * 1e-3) / 1e12 / peak,
-            "receptive_field_windows": bool(m["plan"].windowed)}
+    r = {"bound": "mfma",
+         "kernel": "po_conv implicit GEMM (%s): every Darknet fwd + dgrad launch of a step" % (
+             "conv_h3*_k, fp16x3 split operands" if prec == "fp16x3" else
+             "conv_k + Winograd conv_wino*_k, exact fp32 v_mfma_f32_32x32x2_f32"),
+         "achieved": achieved, "peak": peak, "unit": "TFLOP/s", "frac": achieved / peak, "traffic": traffic,
+         "achieved_is": "dense-equivalent: 2 x the direct-conv MACs of every launch (Winograd launches counted at "
+                        "their direct-conv FLOPs) / conv time; the matrix-core utilisation is frac_mfma",
+         "traffic_per": "step: HBM bytes of all conv launches + split-K reduces (rocprofv3 FETCH_SIZE/WRITE_SIZE "
+                        "passes, profiles/traffic_*.json)",
+         "peak_note": "fp32-equivalent: fp16 dense 2500 / 3 products" if prec == "fp16x3" else "fp32 dense MFMA",
+         "flops_per_step": m["conv_flops"], "conv_ms_per_step": m["conv_ms"],
+         "conv_launches_per_step": m["launches"],
+         "measured_on": "a second pass of K steps with per-launch HIP events (%.3f ms/step instrumented vs %.3f "
+                        "plain)" % (m["instrumented_ms"], m["ms_per_step"]),
+         "reference_dense_flops_per_step": ref_flops_step,
+         # SURVEY §8d's algorithmic rate: the reference's dense fwd + dgrad FLOPs of the
+         # images processed, over the whole step's wall time (windows, cones and Winograd
+         # skip part of that work, so this can exceed the MFMA peak)
+         "achieved_algorithmic": ref_flops_step / (m["ms_per_step"] * 1e-3) / 1e12,
+         "frac_algorithmic": ref_flops_step / (m["ms_per_step"] * 1e-3) / 1e12 / peak,
+         "frac_algorithmic_is": "the reference's dense fwd+dgrad FLOPs over the step's wall time: includes the work "
+                                "removed by receptive-field windows, gradient cones and Winograd (not a utilisation)",
+         "receptive_field_windows": bool(m["plan"].windowed)}
+    if prec == "fp32":
+        fam = m["families"]
+        mf = sum(f["mfma_flops"] for f in fam.values())
+        r["mfma_flops_per_step"] = mf
+        r["achieved_mfma"] = mf / (m["conv_ms"] * 1e-3) / 1e12
+        r["frac_mfma"] = r["achieved_mfma"] / peak
+        r["frac_mfma_is"] = ("FLOPs the matrix cores execute (v_mfma_f32_32x32x2_f32: padded tiles, Winograd at "
+                             "16 GEMMs per 2x2 tile = 4/9 of the direct work; NetPlan.launch_mfma_flops) / conv time "
+                             "/ the 157.3 TFLOP/s peak at 2.4 GHz")
+        r["families"] = {k: {"ms_per_step": f["ms"], "launches_per_step": f["launches"],
+                             "mfma_tflops": f["mfma_flops"] / (f["ms"] * 1e-3) / 1e12 if f["ms"] else None,
+                             "frac_mfma": f["mfma_flops"] / (f["ms"] * 1e-3) / 1e12 / peak if f["ms"] else None,
+                             "dense_equiv_tflops": f["flops"] / (f["ms"] * 1e-3) / 1e12 if f["ms"] else None}
+                         for k, f in fam.items()}
+        # the dominant kernel: the tile with the most time per step
+        best = max(((t, tt, k) for k, f in fam.items() for t, tt in f["tiles"].items()), key=lambda x: x[1]["ms"])
+        t, tt, k = best
+        name = {66: "conv_wino3_k", 65: "conv_wino2_k", 64: "conv_wino2_k", 63: "conv_wino2_k", 62: "conv_wino2_k",
+                61: "conv_wino_k"}.get(t, "conv_k")
+        r["dominant_kernel"] = {"kernel": "%s (po_conv tile %d, %s)" % (name, t, k), "ms_per_step": tt["ms"],
+                                "launches_per_step": tt["launches"],
+                                "avg_launch_us": 1000.0 * tt["ms"] / max(tt["launches"], 1e-9),
+                                "mfma_tflops": tt["mfma_flops"] / (tt["ms"] * 1e-3) / 1e12,
+                                "frac_mfma": tt["mfma_flops"] / (tt["ms"] * 1e-3) / 1e12 / peak}
+    return r
+
+
+def warp_roofline(m, B, S, P):
+    """HBM fractions of the fused augment/warp/composite kernels (SURVEY §8d
+    algorithmic bytes: forward reads the frame and writes the composite,
+    2*3*S^2*4 B per image, plus the 3*P^2*4 B patch once; backward reads
+    dL/dp_img, 3*S^2*4 B per image), per call, HIP events on the launch stream."""
+    out = {}
+    for name, per_img, extra in (("po_warp_fwd", 2 * 3 * S * S * 4, 3 * P * P * 4),
+                                 ("po_warp_bwd", 3 * S * S * 4, 0)):
+        ms = m["warp_ms"].get(name)
+        if not ms:
+            continue
+        byts = B * per_img + extra
+        gbs = byts / (ms * 1e-3) / 1e9
+        out[name] = {"bound": "hbm", "algorithmic_bytes": byts, "us_per_call": ms * 1000.0, "achieved": gbs,
+                     "peak": PEAK_HBM_GBS, "unit": "GB/s", "frac": gbs / PEAK_HBM_GBS}
+    return out
+
+
+def build_trainer(tp, pc, W, cfg, B, world, dev, name):
+    wpath = pc.synthetic_weights_path(cfg.split(":")[-1])
+
+    class _Cfg(pc.ReproducePaperObj):
+        def __init__(self):
+            super().__init__()
+            self.cfgfile = cfg
+            self.weightfile = wpath
+            self.batch_size = B * world
+
+    pc.patch_configs[name] = _Cfg
+    return tp.PatchTrainer(name, device=dev, verbose=False, distributed=world > 1)
+
+
+def measure_tiny(args, dev):
+    """Config 5 (yolov3-tiny-15 @416, B=256, 1 GPU) in the same run: exact
+    fp32 value, conv roofline with frac_mfma, and the warp kernels' HBM
+    fractions (the bandwidth-bound stress this config exists for)."""
+    tp, pc, sy, W = ge._pkg("train_patch"), ge._pkg("patch_config"), ge._pkg("synthetic"), ge._pkg("weights")
+    cfg, S, P, B = CONFIGS["tiny"]
+    old = os.environ.get("ADVPATCH_TUNE_CACHE")
+    os.environ["ADVPATCH_TUNE_CACHE"] = os.path.join(ge.PKG_DIR, "tiles", "conv_tiles_tiny_b%d.json" % B)
+    try:
+        W.ensure_synthetic(cfg, pc.synthetic_weights_path(cfg.split(":")[-1]))
+        tr = build_trainer(tp, pc, W, cfg, B, 1, dev, "_bench_tiny")
+        img = sy.frames_slice(0, B, S, seed=1000).to(dev)
+        lab = sy.labels_slice(0, B, seed=2000).to(dev)
+        patch = sy.patch(P, seed=2).to(dev).requires_grad_(True)
+        m = measure(tr, "fp32", patch, img, lab, B, 1, 0, args.steps, args.warmup, None)
+    finally:
+        if old is None:
+            os.environ.pop("ADVPATCH_TUNE_CACHE", None)
+        else:
+            os.environ["ADVPATCH_TUNE_CACHE"] = old
+    ref = 4.0 * conv_macs(tr.darknet_model) * B
+    return {"value_tiny": m["value"], "ms_per_step_tiny": m["ms_per_step"],
+            "config_tiny": {"workload": "%s S=%d P=%d batch=%d (BASELINE config 5)" % (cfg, S, P, B),
+                            "global_batch": B, "image_size": S, "patch_size": P, "parallelism": "dp1",
+                            "conv_precision": "fp32"},
+            "roofline_tiny": roofline("tiny", B, "fp32", m, ref), "warp_roofline_tiny": warp_roofline(m, B, S, P),
+            "loss_tiny": m["loss"]}
 
 
 def main():
@@ -217,6 +337,7 @@ def main():
     ap.add_argument("--prec", default="both", choices=("both", "fp32", "fp16x3"),
                     help="conv operand precision(s) timed: value is exact fp32; fp16x3 is reported beside it")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-tiny", action="store_true", help="skip config 5 (timed beside the yolov3 line at N=1)")
     ap.add_argument("--dist-backend", default="nccl", help="nccl (= RCCL); gloo only to rehearse ranks on one GPU")
     ap.add_argument("--tile-cache", default=None, help="conv tile cache (default: the committed tiles/ file)")
     args = ap.parse_args()
@@ -246,16 +367,7 @@ def main():
         W.ensure_synthetic(cfg, wpath)
     if world > 1:
         torch.distributed.barrier()
-
-    class _Cfg(pc.ReproducePaperObj):
-        def __init__(self):
-            super().__init__()
-            self.cfgfile = cfg
-            self.weightfile = wpath
-            self.batch_size = B * world
-
-    pc.patch_configs["_bench"] = _Cfg
-    tr = tp.PatchTrainer("_bench", device=dev, verbose=False, distributed=world > 1)
+    tr = build_trainer(tp, pc, W, cfg, B, world, dev, "_bench")
 
     # this rank's contiguous shard of one seeded global batch
     img = sy.frames_slice(rank * B, B, S, seed=1000).to(dev)
@@ -281,6 +393,7 @@ def main():
                        "global_batch": B * world, "per_gpu_batch": B, "image_size": S, "patch_size": P,
                        "parallelism": "dp%d" % world, "conv_precision": head},
             "roofline": roofline(args.config, B, head, m, ref_flops_step),
+            "warp_roofline": warp_roofline(m, B, S, P),
             "loss": m["loss"],
         }
         if "fp16x3" in res and head != "fp16x3":
@@ -291,6 +404,8 @@ def main():
                                     "power-of-two scale, three fp16 MFMA products, fp32 accumulate")
             line["roofline_fp16x3"] = roofline(args.config, B, "fp16x3", f, ref_flops_step)
             line["loss_fp16x3"] = f["loss"]
+        if world == 1 and args.config == "yolov3" and not args.no_tiny:
+            line.update(measure_tiny(args, dev))
         if world == 1 and not args.no_cpu_baseline:
             line["cpu_baseline"] = cpu_baseline(cfg, S, P, B=16)
         print(json.dumps(line))

@@ -24,7 +24,7 @@ __all__ = [
     "parse_model_config", "median_pool7", "median_pool2d", "lab_transform", "patch_transformer",
     "patch_applier", "load_printability", "nps_score", "total_variation",
     "colorful_loss", "OracleDarknet", "read_darknet_weights", "obj_cls_conf_find",
-    "no_obj_reshape", "no_cls_reshape", "noCLS_Loss_CE", "noCLS_loss_targeted",
+    "no_obj_reshape", "no_cls_reshape", "no_obj_reshape3", "no_cls_reshape3", "noCLS_Loss_CE", "noCLS_loss_targeted",
     "train_step", "train_step_f64", "adam_amsgrad_steps", "patch_theta", "cell_indices", "TV_FACTOR", "NPS_FACTOR",
     "TARGET_ID", "bbox_decode", "max_prob_extractor",
 ]
@@ -121,9 +121,18 @@ def lab_transform(lab_batch):
 # --------------------------------------------------------------------------
 # load_data.py:512-794 PatchTransformer.forward (training placement)
 # --------------------------------------------------------------------------
-def patch_transformer(adv_patch, lab_batch, img_size, draws, do_rotate=True):
+def patch_transformer(adv_patch, lab_batch, img_size, draws, do_rotate=True, geometry="fp32"):
     """Returns (adv_batch_t [B,1,3,S,S], patch_center [B,2]).  patch_center is
-    (column, row) in pixels = (target_x*S, target_y*S) (load_data.py:712-715)."""
+    (column, row) in pixels = (target_x*S, target_y*S) (load_data.py:712-715).
+
+    ``geometry`` (tests only): "fp32" is the reference (theta, affine_grid and
+    grid_sample in fp32).  "f64" evaluates theta, the grid and the bilinear
+    sampling in float64 from the same fp32 inputs and rounds each sampled
+    value to fp32 once — the HIP path's deliberate deviation:
+    the fp32 affine_grid leaves ~1e-4 px in the sampling coordinates (its
+    translation terms cancel), i.e. up to ~1.5e-4 relative in the patch
+    gradient, so an fp32 comparison of two implementations at 1e-4 needs the
+    geometry taken out of the rounding noise."""
     adv = median_pool7(adv_patch.unsqueeze(0))                    # 531-532
     P = adv.size(-1)
     pad = (img_size - P) / 2                                     # 534
@@ -159,11 +168,14 @@ def patch_transformer(adv_patch, lab_batch, img_size, draws, do_rotate=True):
     s = adv_batch.size()
     adv_batch = adv_batch.reshape(s[0] * s[1], s[2], s[3], s[4])
     msk_batch = msk_batch.reshape(s[0] * s[1], s[2], s[3], s[4])
+    if geometry == "f64":
+        adv_batch, msk_batch = adv_batch.double(), msk_batch.double()
+        angle, target_x, target_y, scale = angle.double(), target_x.double(), target_y.double(), scale.double()
     tx = (-target_x + 0.5) * 2                                   # 726
     ty = (-target_y + 0.5) * 2                                   # 727
     sin = torch.sin(angle)
     cos = torch.cos(angle)
-    theta = torch.zeros(B, 2, 3)                                 # 733-743
+    theta = torch.zeros(B, 2, 3, dtype=adv_batch.dtype)          # 733-743
     theta[:, 0, 0] = cos / scale
     theta[:, 0, 1] = sin / scale
     theta[:, 0, 2] = tx * cos / scale + ty * sin / scale
@@ -176,7 +188,10 @@ def patch_transformer(adv_patch, lab_batch, img_size, draws, do_rotate=True):
     adv_t = adv_t.view(s[0], s[1], s[2], s[3], s[4])
     msk_t = msk_t.view(s[0], s[1], s[2], s[3], s[4])
     adv_t = torch.clamp(adv_t, 0.0, 1.)                          # 791
-    return adv_t * msk_t, patch_center                          # 792-794
+    out = adv_t * msk_t                                          # 792-794
+    if geometry == "f64":
+        out = out.float()
+    return out, patch_center
 
 
 def patch_theta(lab_batch, img_size, P, draws, do_rotate=True):
@@ -350,7 +365,8 @@ class OracleDarknet:
         given ones — used to compare gradients of two fp32 implementations
         on identical branches (a pre-activation within rounding of 0 can
         take either LeakyReLU slope).  ``record``: dict filled with the
-        pre-activations of leaky convs."""
+        pre-activations of leaky convs (key: block) and the windows of every
+        max pool, [B,C,Ho,Wo,k*k] (key: ("maxpool", block))."""
         outs, yolo = [], []
         for i, (d, p) in enumerate(zip(self.blocks, self.params)):
             t = d["type"]
@@ -378,6 +394,9 @@ class OracleDarknet:
                 k, s = int(d["size"]), int(d["stride"])
                 if k == 2 and s == 1:
                     x = F.pad(x, (0, 1, 0, 1))
+                if record is not None:                             # the pool windows (branch tie checks)
+                    w_ = x.detach().unfold(2, k, s).unfold(3, k, s)
+                    record[("maxpool", i)] = w_.reshape(w_.shape[:4] + (k * k,))
                 if br is not None:
                     win = x.unfold(2, k, s).unfold(3, k, s)        # [B,C,Ho,Wo,k,k]
                     win = win.reshape(win.shape[:4] + (k * k,))
@@ -415,26 +434,33 @@ class OracleDarknet:
 
 
 # --------------------------------------------------------------------------
-# train_patch.py:428-548 loss head
+# train_patch.py:428-548 loss head (generalised to (nheads, 5+C))
 # --------------------------------------------------------------------------
 def obj_cls_conf_find(outputs, img_size, patch_center):
     """train_patch.py:428-486, including the transposed cell index
-    `index = ix*w + iy` (train_patch.py:467)."""
+    `index = ix*w + iy` (train_patch.py:467).
+
+    Generalised to any number of heads and C classes per
+    anchor: the reference hard-codes 3 anchors x (5 + 15) = 60 channels
+    (``view(batch, 3, 5 + 15, h*w)`` at 459, ``4:20`` / ``1:16`` at 470-483);
+    here C = channels / 3 - 5, which is exactly that form for the reference's
+    heads (C = 15) and also covers the two-head yolov3-tiny-15 (config 5)."""
     obj_all, cls_all = [], []
     for output in outputs:
         obj_inner, cls_inner = [], []
         batch, h, w = output.size(0), output.size(2), output.size(3)
+        nc = output.size(1) // 3 - 5                             # 15 in the reference (459)
         feature_size = output.size(-1)
         feature_scale = img_size / feature_size
         axis = torch.div(patch_center, feature_scale, rounding_mode="floor")
-        output = output.view(batch, 3, 5 + 15, h * w)
+        output = output.view(batch, 3, 5 + nc, h * w)
         for i in range(batch):
             index_x = int(axis[i, 0])
             index_y = int(axis[i, 1])
             index = int(index_x * feature_size + index_y)
-            cells = torch.sigmoid(output[i, :, 4:20, index])
+            cells = torch.sigmoid(output[i, :, 4:5 + nc, index])
             obj_inner.append(cells[:, 0].view(-1, 3))
-            cls_inner.append(cells[:, 1:16])
+            cls_inner.append(cells[:, 1:1 + nc])
         obj_all.append(obj_inner)
         cls_all.append(cls_inner)
     return obj_all, cls_all
@@ -450,7 +476,37 @@ def cell_indices(heads_hw, img_size, patch_center):
     return res
 
 
-def no_obj_reshape(index_obj_conf):                                # train_patch.py:488-503
+def no_obj_reshape(index_obj_conf):
+    """train_patch.py:488-503: stack the heads' [1,3] objectness rows to
+    [nheads, B, 3], transpose to [B, nheads, 3] and flatten to [B, 3*nheads]
+    (anchor k = head*3 + a).  The reference allocates ``zeros(3, B, 3)`` (492):
+    nheads = 3; the generalised form (SURVEY.md Q10, config 5's two tiny
+    heads) takes nheads = len(index_obj_conf).  ``no_obj_reshape3`` below
+    keeps the literal 3-head statement the generalisation is tested against."""
+    H = len(index_obj_conf)
+    B = len(index_obj_conf[0])
+    t = torch.zeros(H, B, 3)
+    for i, obj in enumerate(index_obj_conf):
+        t[i, :, :] = torch.cat(obj, 0)
+    return t.transpose(0, 1).reshape(B, 3 * H)
+
+
+def no_cls_reshape(index_cls_conf):
+    """train_patch.py:505-524 generalised as no_obj_reshape: [nheads, B, 3, C]
+    -> [B, 3*nheads, C] (the reference: ``zeros(3, B, 3, 15)``, 509-513)."""
+    H = len(index_cls_conf)
+    B = len(index_cls_conf[0])
+    C = index_cls_conf[0][0].size(-1)
+    t = torch.zeros(H, B, 3, C)
+    for i, cls in enumerate(index_cls_conf):
+        inner = torch.zeros(B, 3, C)
+        for j, c in enumerate(cls):
+            inner[j, :, :] = c
+        t[i, :, :, :] = inner
+    return t.transpose(0, 1).reshape(B, 3 * H, C)
+
+
+def no_obj_reshape3(index_obj_conf):                               # train_patch.py:488-503, literal
     B = len(index_obj_conf[0])
     t = torch.zeros(3, B, 3)
     for i, obj in enumerate(index_obj_conf):
@@ -458,7 +514,7 @@ def no_obj_reshape(index_obj_conf):                                # train_patch
     return t.transpose(0, 1).reshape(B, 9)
 
 
-def no_cls_reshape(index_cls_conf):                                # train_patch.py:505-524
+def no_cls_reshape3(index_cls_conf):                               # train_patch.py:505-524, literal
     B = len(index_cls_conf[0])
     t = torch.zeros(3, B, 3, 15)
     for i, cls in enumerate(index_cls_conf):
@@ -552,22 +608,25 @@ def max_prob_extractor(outputs, cls_id, num_cls, anchors_per_head, sigmoid_mode=
 # train_patch.py:157-330 one iteration of the batch loop
 # --------------------------------------------------------------------------
 def train_step(patch, img_batch, lab_batch, draws, net, colors, target_id=TARGET_ID,
-               objective="ce", weight_grad=False, branch=None, record=None, combine=None):
+               objective="ce", weight_grad=False, branch=None, record=None, combine=None, geometry="fp32"):
     """One iteration of PatchTrainer.train's batch body (train_patch.py:164-327).
 
     ``patch`` is the [3,P,P] leaf.  Returns a dict of loss terms (float
     tensors), the patch gradient, and the intermediates the parity tests
-    check (patch_center, cell indices, obj [B,9], cls [B,9,15]).
+    check (patch_center, cell indices, obj [B,3*nheads], cls [B,3*nheads,C];
+    [B,9] and [B,9,15] for the reference's three heads).
     ``objective``: "ce" (active, train_patch.py:253), "targeted"
     (noCLS_loss_targeted, train_patch.py:262) or "untargeted"
     (train_patch.py:305-307).  ``branch``, ``record``: see OracleDarknet.forward
     (recorded pre-activations keep their gradients).  ``combine`` (tests of
     the data-parallel weighting): f(no_obj_loss, no_cls_loss, nps, tv,
     colorful) -> (loss, terms) replaces the loss formula of 312-314.
+    ``geometry``: see patch_transformer ("f64": the placement geometry in
+    float64, as the HIP path evaluates it).
     """
     leaf = patch.detach().clone().requires_grad_(True)
     img_size = net.height
-    adv_batch_t, patch_center = patch_transformer(leaf, lab_batch, img_size, draws)  # 173-174
+    adv_batch_t, patch_center = patch_transformer(leaf, lab_batch, img_size, draws, geometry=geometry)  # 173-174
     p_img = patch_applier(img_batch, adv_batch_t)                                  # 183
     p_img = F.interpolate(p_img, (net.height, net.width))                         # 186-187
     outputs = net(p_img, branch=branch, record=record)                             # 197

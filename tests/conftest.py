@@ -55,7 +55,23 @@ def plan_branches(plan):
         C = plan.shp[i][2]
         if d["type"] == "convolutional" and plan._leaky(i):
             sg = plan.leaky_signs(i)
-            if sg is None:          # not stored (first conv fused into its max pool): the oracle decides
+            if sg is None:
+                # not stored: the conv runs fused into its 2x2/2 max pool (first conv + pool,
+                # conv + pool epilogue).  The pool's argmax byte carries the slope taken at the
+                # window's maximum (bit 3 = encoded, bit 2 = slope 0.1), the only conv pixel of
+                # the window the gradient reaches; elsewhere (-1) the oracle decides.
+                a = plan.argmax[i + 1][..., :C].to(torch.int32).permute(0, 3, 1, 2).cpu()
+                H, W = plan.shp[i][:2]
+                full = torch.full((plan.B, C, H, W), -1, dtype=torch.int8)
+                known = (a & 8) != 0
+                val = ((a & 4) == 0).to(torch.int8)
+                pos = a & 3
+                for dy in range(2):
+                    for dx in range(2):
+                        sel = known & (pos == 2 * dy + dx)
+                        view = full[:, :, dy:2 * (a.shape[2]) :2, dx:2 * (a.shape[3]):2]
+                        view[sel] = val[sel]
+                br[i] = ("leaky", full)
                 continue
             pos = sg.permute(0, 3, 1, 2).cpu()
             if plan.win[i] is not None:
@@ -77,8 +93,23 @@ def plan_branches(plan):
 def assert_branch_ties_only(br, record, tol=1e-5, max_frac=1e-4):
     """Every LeakyReLU branch where the HIP forward and the oracle disagree
     must be a near-tie: |pre-activation| <= tol * max|pre-activation| of the
-    layer; and such ties must be rare (<= max_frac of the layer's elements)."""
+    layer; every max-pool window where they disagree likewise (the gap to
+    the window's maximum <= tol * the layer's max); and such ties must be
+    rare (<= max_frac of the layer's elements / windows)."""
     for i, (kind, val) in br.items():
+        if kind == "maxpool" and ("maxpool", i) in record:
+            # the window element the HIP pool took must be a maximum of the oracle's
+            # window up to rounding: a max pool routes the whole gradient to one
+            # element, so a near-tie taken the other way moves it (the tiny net)
+            win = record[("maxpool", i)]
+            chosen = torch.gather(win, -1, val.long().unsqueeze(-1)).squeeze(-1)
+            gap = win.max(-1).values - chosen
+            if bool((gap > 0).any()):
+                worst = float(gap.max() / win.abs().max())
+                assert worst <= tol, "block %d: pool argmax differs at gap/max=%.3g (not a rounding tie)" % (i, worst)
+                frac = float((gap > 0).float().mean())
+                assert frac <= max_frac, "block %d: %.3g of the pool windows differ" % (i, frac)
+            continue
         if kind != "leaky" or i not in record:
             continue
         pre = record[i].detach()

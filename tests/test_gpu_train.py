@@ -11,11 +11,13 @@ import pytest
 import torch
 
 import oracle
-from conftest import ROOT, pkg_mod, plan_branches, assert_branch_ties_only
+from conftest import ROOT, pkg_mod
+from test_gpu_step import assert_north_star, assert_tiny_parity, branch_aligned
 
 pytestmark = pytest.mark.gpu
 DEV = torch.device("cuda", 0)
 TILES = os.path.join(ROOT, pkg_mod().__name__, "tiles", "conv_tiles_yolov3_b16.json")
+TILES_TINY = os.path.join(ROOT, pkg_mod().__name__, "tiles", "conv_tiles_tiny_b256.json")
 
 
 def _trainer(cfg, wpath, prec="fp32", objective="ce", batch=16):
@@ -133,45 +135,69 @@ def test_headline_plan_b16_608(yolo_weights, monkeypatch, prec):
     receptive-field windows and gradient cones on, conv tiles and split-K
     factors from the committed cache the bench uses.  Cells bit-exact, loss
     terms, objectness/class at the cells, and the patch gradient against the
-    branch-aligned oracle (ties asserted), fixed 1e-4 against float64."""
+    branch-aligned oracle (ties asserted): within 1e-4 of the fp32 oracle
+    (north_star) and of the float64 evaluation."""
     monkeypatch.setenv("ADVPATCH_TUNE_CACHE", TILES)
     monkeypatch.setenv("ADVPATCH_TUNE", "cache")          # the committed tiles, nothing timed
-    sy, ld = pkg_mod("synthetic"), pkg_mod("load_data")
+    sy, G = pkg_mod("synthetic"), pkg_mod("cfg_gen")
     tr = _trainer("builtin:yolov3-dota", yolo_weights, prec=prec)
-    net = tr.darknet_model
-    assert net.window_heads
+    assert tr.darknet_model.window_heads
     B, S, P = 16, 608, 224
     img, lab = sy.frames_slice(0, B, S, seed=1000), sy.labels_slice(0, B, seed=2000)
     patch = sy.patch(P, seed=2)
     dr = {k: v.cpu() for k, v in sy.draws_device(3, 0, 0, B, P, DEV).items()}      # the bench's step-0 draws
-    pg = patch.to(DEV).requires_grad_(True)
-    loss, terms = tr.losses(pg, img.to(DEV), lab.to(DEV), {k: v.to(DEV) for k, v in dr.items()})
+    ref_net = oracle.OracleDarknet(G.cfg_text("builtin:yolov3-dota"), yolo_weights)
+    terms, g, ref32, errs = branch_aligned(tr, ref_net, img, lab, patch, dr)
     plan = tr.last_plan
     assert plan.windowed and plan.cone_blocks
     tuned = [d for name, _, d in plan.fwd_ops + plan.bwd_ops if name == "po_conv"]
     assert all(d.tile > 0 for d in tuned)                  # every launch runs a tuned/cached tile
-    br = plan_branches(plan)
-    loss.backward()
-    W, G = pkg_mod("weights"), pkg_mod("cfg_gen")
-    ref_net = oracle.OracleDarknet(G.cfg_text("builtin:yolov3-dota"), yolo_weights)
-    colors = ld.load_printability_colors("builtin:30values")
-    rec = {}
-    ref32 = oracle.train_step(patch, img, lab, dr, ref_net, colors, branch=br, record=rec)
-    assert_branch_ties_only(br, rec, {"fp32": 5e-5, "fp16x3": 1e-4}[prec])
-    del rec
     assert terms["cells"].cpu().tolist() == ref32["cells"]
     torch.testing.assert_close(terms["obj"].cpu(), ref32["obj"], rtol=0, atol=5e-5)
     torch.testing.assert_close(terms["cls"].cpu(), ref32["cls"], rtol=0, atol=5e-5)
     for k in ("loss", "nps_loss", "tv_loss", "no_obj_loss", "no_cls_loss", "colorful_loss"):
         a, b = float(terms[k]), float(ref32[k])
         assert abs(a - b) <= 2e-5 * max(1.0, abs(b)), (k, a, b)
-    ref64 = oracle.train_step_f64(patch, img, lab, dr, ref_net, colors, branch=br)
-    g64 = ref64["grad"]
-    scale = g64.abs().max()
-    err_hip = float((pg.grad.cpu().double() - g64).abs().max() / scale)
-    err_32 = float((ref32["grad"].double() - g64).abs().max() / scale)
-    print("headline plan (%s) B=16 patch grad vs float64: hip %.3g, fp32 oracle %.3g" % (prec, err_hip, err_32))
-    assert err_hip <= 1e-4, (err_hip, err_32)
+    assert_north_star(errs, "headline plan (%s) B=16" % prec)
+    tr.check_flags()
+
+
+@pytest.mark.timeout(900)
+def test_tiny_bench_plan_b256_416(tmp_path_factory, monkeypatch):
+    """Config 5 as bench.py times it: yolov3-tiny-15 @416, B=256, P=224, the
+    committed tiny tile cache in ADVPATCH_TUNE=cache (nothing timed), with
+    every plan feature the tiny number depends on asserted on: the first conv
+    fused with its max pool, the conv + pool epilogues (Winograd pool on tile
+    66 where the cache picks it), the support grid of the head-window dgrad,
+    receptive-field windows and gradient cones.  Against the oracle's
+    generalised two-head loss, branch-aligned (LeakyReLU signs,
+    max-pool argmaxes; ties asserted): cells bit-exact, loss terms within
+    2e-5, objectness/class within 5e-5, the gradient per assert_tiny_parity."""
+    monkeypatch.setenv("ADVPATCH_TUNE_CACHE", TILES_TINY)
+    monkeypatch.setenv("ADVPATCH_TUNE", "cache")
+    sy, G = pkg_mod("synthetic"), pkg_mod("cfg_gen")
+    cfg = "builtin:yolov3-tiny-dota"
+    wpath = str(tmp_path_factory.mktemp("wt") / "tiny.weights")
+    tr = _trainer(cfg, wpath, prec="fp32", batch=256)
+    B, S, P = 256, 416, 224
+    img, lab = sy.frames_slice(0, B, S, seed=1000), sy.labels_slice(0, B, seed=2000)
+    patch = sy.patch(P, seed=2)
+    dr = {k: v.cpu() for k, v in sy.draws_device(3, 0, 0, B, P, DEV).items()}      # the bench's step-0 draws
+    ref_net = oracle.OracleDarknet(G.cfg_text(cfg), wpath)
+    terms, g, ref32, errs = branch_aligned(tr, ref_net, img, lab, patch, dr, geometry32=True)
+    plan = tr.last_plan
+    assert plan.first_pool and plan.conv_pool and plan.support and plan.windowed and plan.cone_blocks
+    convs = [d for name, _, d in plan.fwd_ops + plan.bwd_ops if name == "po_conv"]
+    assert all(d.tile > 0 for d in convs)
+    assert any(d.pool_y and d.tile == 66 for d in convs)   # Winograd with the fused pool
+    assert terms["obj"].shape == (B, 6) and terms["cls"].shape == (B, 6, 15)
+    assert terms["cells"].cpu().tolist() == ref32["cells"]
+    torch.testing.assert_close(terms["obj"].cpu(), ref32["obj"], rtol=0, atol=5e-5)
+    torch.testing.assert_close(terms["cls"].cpu(), ref32["cls"], rtol=0, atol=5e-5)
+    for k in ("loss", "nps_loss", "tv_loss", "no_obj_loss", "no_cls_loss", "colorful_loss"):
+        a, b = float(terms[k]), float(ref32[k])
+        assert abs(a - b) <= 2e-5 * max(1.0, abs(b)), (k, a, b)
+    assert_tiny_parity(errs, "tiny bench plan B=256")
     tr.check_flags()
 
 

@@ -118,3 +118,52 @@ def test_max_prob_extractor_reads_the_logit_fields():
     so, sc, _, _ = oracle.max_prob_extractor(heads, 7, 15, anchors, sigmoid_mode=True)
     torch.testing.assert_close(so, torch.sigmoid(mo), rtol=0, atol=0)
     torch.testing.assert_close(sc, torch.sigmoid(mc), rtol=0, atol=0)
+
+
+def test_generalised_loss_head_equals_reference_form_at_three_heads():
+    """the (nheads, 5+C) head of obj_cls_conf_find / no_obj_reshape /
+    no_cls_reshape is, at the reference's 3 heads x (5+15), the literal
+    statement of train_patch.py:488-524 (no_obj_reshape3 / no_cls_reshape3)
+    bit for bit."""
+    gen = torch.Generator().manual_seed(3)
+    B = 5
+    heads = [torch.randn(B, 60, s, s, generator=gen) for s in (19, 38, 76)]
+    center = torch.rand(B, 2, generator=gen) * 608
+    obj_l, cls_l = oracle.obj_cls_conf_find(heads, 608, center)
+    assert torch.equal(oracle.no_obj_reshape(obj_l), oracle.no_obj_reshape3(obj_l))
+    assert torch.equal(oracle.no_cls_reshape(cls_l), oracle.no_cls_reshape3(cls_l))
+
+
+def test_generalised_loss_head_two_tiny_heads():
+    """Config 5 (yolov3-tiny-15, two heads at 13/26 for S=416): anchors are
+    k = head*3 + a over 6 anchors, each read at the transposed cell (Q1) of its
+    head; a head of C=15 classes reads channels a*20 + 4 .. a*20 + 19."""
+    B, S = 3, 416
+    heads = [torch.zeros(B, 60, 13, 13), torch.zeros(B, 60, 26, 26)]
+    center = torch.tensor([[100.0, 300.0], [5.0, 410.0], [250.0, 17.0]])
+    cells = oracle.cell_indices([13, 26], S, center)
+    for h, hw in enumerate((13, 26)):
+        st = S / hw
+        for b in range(B):
+            ix, iy = int(center[b, 0] // st), int(center[b, 1] // st)
+            assert cells[h][b] == ix * hw + iy
+            r, c = divmod(cells[h][b], hw)
+            for a in range(3):
+                heads[h][b, a * 20 + 4, r, c] = 10.0 * h + a + b / 10.0      # objectness logit
+                heads[h][b, a * 20 + 5 + 14, r, c] = -(a + 1.0)              # class-14 logit
+    obj_l, cls_l = oracle.obj_cls_conf_find(heads, S, center)
+    no_obj, no_cls = oracle.no_obj_reshape(obj_l), oracle.no_cls_reshape(cls_l)
+    assert no_obj.shape == (B, 6) and no_cls.shape == (B, 6, 15)
+    for b in range(B):
+        for h in range(2):
+            for a in range(3):
+                assert float(no_obj[b, 3 * h + a]) == float(torch.sigmoid(torch.tensor(10.0 * h + a + b / 10.0)))
+                assert float(no_cls[b, 3 * h + a, 14]) == float(torch.sigmoid(torch.tensor(-(a + 1.0))))
+                assert torch.all(no_cls[b, 3 * h + a, :14] == 0.5)
+    # CE of probabilities treated as logits (Q7), target 14, mean over 6 anchors then over B
+    want = 0.0
+    for b in range(B):
+        row = [math.log(14 * math.exp(0.5) + math.exp(float(no_cls[b, k, 14]))) - float(no_cls[b, k, 14])
+               for k in range(6)]
+        want += sum(row) / 6
+    assert abs(float(oracle.noCLS_Loss_CE(no_cls, 14)) - want / B) < 1e-6

@@ -18,7 +18,7 @@ OUT=gpurun_out/prof_${ROUND}_${CFG}_${PREC}
 mkdir -p "$OUT"
 STEPS=10
 WARM=2
-BENCH="bench.py --config $CFG --batch $BATCH --steps $STEPS --warmup $WARM --no-cpu-baseline --prec $PREC"
+BENCH="bench.py --config $CFG --batch $BATCH --steps $STEPS --warmup $WARM --no-cpu-baseline --no-tiny --prec $PREC"
 timeout -k 10 300 python $BENCH > "$OUT/bench_plain.json" 2> "$OUT/bench_plain.err"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/trace" -o run -- python $BENCH \
     > "$OUT/bench_trace.json" 2> "$OUT/trace.err"
