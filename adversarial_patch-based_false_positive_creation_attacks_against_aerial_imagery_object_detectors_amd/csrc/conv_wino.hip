@@ -362,7 +362,7 @@ __global__ __launch_bounds__(256) void conv_wino_k(const ConvArgs a, const float
 #pragma unroll
       for (int dj = 0; dj < 2; ++dj) {
         const int i = 2 * tti + di, j = 2 * ttj + dj;
-        const bool ok = tl && n < a.N && i < a.Hout && j < a.Wout && i >= bx.x && i < bx.z && j >= bx.y && j < bx.w;
+        const bool ok = tl && n < a.N && i >= 0 && j >= 0 && i < a.Hout && j < a.Wout && i >= bx.x && i < bx.z && j >= bx.y && j < bx.w;
         const size_t pix = ((size_t)bb * a.Hout + i) * a.Wout + j;
         float out = 0.f;
         if (ok) out = epi_store(a, pix, n, yv[di][dj], mx);
@@ -536,7 +536,7 @@ __global__ __launch_bounds__(64 * NW) void conv_wino2_k(const ConvArgs a, const 
 #pragma unroll
       for (int p = 0; p < 4; ++p) {
         const int i = 2 * tti_[it] + (p >> 1), j = 2 * ttj_[it] + (p & 1);
-        if (tl_[it] && n < a.N && i < a.Hout && j < a.Wout && i >= bx.x && i < bx.z && j >= bx.y && j < bx.w)
+        if (tl_[it] && n < a.N && i >= 0 && j >= 0 && i < a.Hout && j < a.Wout && i >= bx.x && i < bx.z && j >= bx.y && j < bx.w)
           okm[it] |= 1u << p;
       }
     }
@@ -574,7 +574,7 @@ __global__ __launch_bounds__(64 * NW) void conv_wino2_k(const ConvArgs a, const 
 #pragma unroll
     for (int p = 0; p < 4; ++p) {
       const int i = 2 * vti + (p >> 1), j = 2 * vtj + (p & 1);
-      if (tl && n4 < a.N && i < a.Hout && j < a.Wout && i >= bx.x && i < bx.z && j >= bx.y && j < bx.w)
+      if (tl && n4 < a.N && i >= 0 && j >= 0 && i < a.Hout && j < a.Wout && i >= bx.x && i < bx.z && j >= bx.y && j < bx.w)
         vok |= 1u << p;
     }
   };
@@ -954,7 +954,7 @@ __global__ __launch_bounds__(256, 2) void conv_wino3_k(const ConvArgs a, const f
 #pragma unroll
       for (int p = 0; p < 4; ++p) {
         const int i = 2 * vti + (p >> 1), j = 2 * vtj + (p & 1);
-        if (tl && n4 < a.N && i < a.Hout && j < a.Wout && i >= bx.x && i < bx.z && j >= bx.y && j < bx.w)
+        if (tl && n4 < a.N && i >= 0 && j >= 0 && i < a.Hout && j < a.Wout && i >= bx.x && i < bx.z && j >= bx.y && j < bx.w)
           vok |= 1u << p;
       }
 #pragma unroll

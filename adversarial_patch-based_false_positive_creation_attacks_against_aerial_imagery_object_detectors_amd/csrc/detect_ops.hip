@@ -94,9 +94,9 @@ __global__ __launch_bounds__(256) void region_boxes_k(const RegionArgs a, const 
 
 // ---- NMS (1): per image, sort packed keys (fp32 bits of 1 - det) << 32 | index
 __global__ __launch_bounds__(1024) void nms_sort_k(const float* __restrict__ boxes, const int32_t* __restrict__ counts,
-                                                   int cap, int n2, uint64_t* __restrict__ keys) {
+                                                   int cap, int nmax, int n2, uint64_t* __restrict__ keys) {
   const int b = blockIdx.x;
-  const int n = min(counts[b], cap);
+  const int n = min(counts[b], nmax);   // keys / mask / LDS are sized for nmax
   uint64_t* kb = keys + (size_t)b * n2;
   for (int j = threadIdx.x; j < n2; j += 1024) {
     uint64_t v = ~0ull;
@@ -138,11 +138,11 @@ __device__ __forceinline__ bool iou_over(const float* b1, const float* b2, float
 
 // ---- NMS (2): suppression matrix, block (row block rb, word wd) of 64 x 64
 __global__ __launch_bounds__(64) void nms_mask_k(const float* __restrict__ boxes, const int32_t* __restrict__ counts,
-                                                 const uint64_t* __restrict__ keys, int cap, int n2, int nwords,
+                                                 const uint64_t* __restrict__ keys, int cap, int nmax, int n2, int nwords,
                                                  float thresh, uint64_t* __restrict__ mask) {
   __shared__ float cb[64][BOXF];
   const int b = blockIdx.z, rb = blockIdx.y, wd = blockIdx.x, t = threadIdx.x;
-  const int n = min(counts[b], cap);
+  const int n = min(counts[b], nmax);   // keys / mask / LDS are sized for nmax
   if (rb * 64 >= n || wd * 64 >= n || wd < rb) {
     // blocks below the diagonal hold no bit (t > s only); rows past n are never read
     if (rb * 64 < n && wd < rb) mask[((size_t)b * n2 + rb * 64 + t) * nwords + wd] = 0ull;
@@ -175,11 +175,11 @@ __global__ __launch_bounds__(64) void nms_mask_k(const float* __restrict__ boxes
 // ---- NMS (3): one wave per image scans the sorted boxes
 __global__ __launch_bounds__(64) void nms_scan_k(const float* __restrict__ boxes, const int32_t* __restrict__ counts,
                                                  const uint64_t* __restrict__ keys, const uint64_t* __restrict__ mask,
-                                                 int cap, int n2, int nwords, int32_t* __restrict__ keep,
+                                                 int cap, int nmax, int n2, int nwords, int32_t* __restrict__ keep,
                                                  int32_t* __restrict__ nkeep) {
   extern __shared__ uint64_t removed[];
   const int b = blockIdx.x, lane = threadIdx.x;
-  const int n = min(counts[b], cap);
+  const int n = min(counts[b], nmax);   // keys / mask / LDS are sized for nmax
   for (int w = lane; w < nwords; w += 64) removed[w] = 0ull;
   __syncthreads();
   const uint64_t* kb = keys + (size_t)b * n2;
@@ -226,15 +226,15 @@ extern "C" int po_nms(const float* boxes, const int32_t* counts, int B, int cap,
   while (n2 < nmax) n2 <<= 1;
   const int nwords = (nmax + 63) / 64;
   hipStream_t st = po::stream_of(s);
-  hipLaunchKernelGGL(nms_sort_k, dim3(B), dim3(1024), 0, st, boxes, counts, cap, n2, keys);
+  hipLaunchKernelGGL(nms_sort_k, dim3(B), dim3(1024), 0, st, boxes, counts, cap, nmax, n2, keys);
   int rc = po::check_launch("po_nms (sort)");
   if (rc) return rc;
-  hipLaunchKernelGGL(nms_mask_k, dim3(nwords, nwords, B), dim3(64), 0, st, boxes, counts, keys, cap, n2, nwords,
+  hipLaunchKernelGGL(nms_mask_k, dim3(nwords, nwords, B), dim3(64), 0, st, boxes, counts, keys, cap, nmax, n2, nwords,
                      nms_thresh, mask);
   rc = po::check_launch("po_nms (mask)");
   if (rc) return rc;
-  hipLaunchKernelGGL(nms_scan_k, dim3(B), dim3(64), nwords * sizeof(uint64_t), st, boxes, counts, keys, mask, cap, n2,
-                     nwords, keep, nkeep);
+  hipLaunchKernelGGL(nms_scan_k, dim3(B), dim3(64), nwords * sizeof(uint64_t), st, boxes, counts, keys, mask, cap,
+                     nmax, n2, nwords, keep, nkeep);
   return po::check_launch("po_nms (scan)");
 }
 

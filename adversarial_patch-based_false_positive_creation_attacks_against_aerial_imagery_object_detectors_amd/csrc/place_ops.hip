@@ -38,6 +38,11 @@ struct TmWork {
   int32_t* st;      // [B,TM_ST]
 };
 
+// int32 sub-buffer offsets rounded up to 4 words: every sub-buffer of the
+// (16-byte aligned) int workspace starts 16-byte aligned, so tm_cover_k's int4
+// loads of w.rect are aligned for any B, L, S
+__host__ __device__ constexpr size_t up4(size_t n) { return (n + 3) & ~(size_t)3; }
+
 TmWork carve(float* fwork, int32_t* iwork, int B, int L, int S) {
   TmWork w;
   const size_t plane = (size_t)S * S;
@@ -45,8 +50,8 @@ TmWork carve(float* fwork, int32_t* iwork, int B, int L, int S) {
   w.msk1 = fwork + (size_t)B * 3 * plane;
   w.aff = reinterpret_cast<double*>(fwork + (size_t)B * 4 * plane);
   w.cover = iwork;
-  w.order = iwork + (size_t)B * plane;
-  w.rect = w.order + (size_t)B * L;
+  w.order = iwork + up4((size_t)B * plane);
+  w.rect = w.order + up4((size_t)B * L);
   w.st = w.rect + (size_t)B * L * 4;
   return w;
 }
@@ -402,7 +407,8 @@ __global__ __launch_bounds__(256) void vanish_params_k(const float* __restrict__
 extern "C" int po_place_workspace(int B, int L, int S, int64_t* fwords, int64_t* iwords) {
   PO_REQUIRE(B > 0 && L > 0 && S > 0 && fwords && iwords, "po_place_workspace: bad argument");
   *fwords = (int64_t)4 * B * S * S + 16 * (int64_t)B;
-  *iwords = (int64_t)B * ((int64_t)S * S + 5 * (int64_t)L + TM_ST);
+  // carve(): cover [B*S*S] | order [B*L] | rect [B*L*4] | st [B*TM_ST], the first two rounded up to 4 words
+  *iwords = (int64_t)up4((size_t)B * S * S) + (int64_t)up4((size_t)B * L) + 4 * (int64_t)B * L + (int64_t)B * TM_ST;
   return PO_OK;
 }
 

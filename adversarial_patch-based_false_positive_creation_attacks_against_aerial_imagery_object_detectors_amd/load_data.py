@@ -618,6 +618,21 @@ def u8_to_float(img):
     return lut[img.long()]
 
 
+class DotaCollate:
+    """DataLoader collate of DotaDataset items that also forms the EMPTY batch
+    of a rank whose shard of a ragged last global batch is empty
+    (GlobalBatchSampler): uint8/float [0,3,S,S] frames and [0,L,5] labels."""
+
+    def __init__(self, imgsize, max_n_labels, as_uint8=False):
+        self.S, self.L, self.u8 = int(imgsize), int(max_n_labels), bool(as_uint8)
+
+    def __call__(self, batch):
+        if not batch:
+            return (torch.empty(0, 3, self.S, self.S, dtype=torch.uint8 if self.u8 else torch.float32),
+                    torch.empty(0, self.L, 5))
+        return torch.utils.data.default_collate(batch)
+
+
 class DevicePrefetcher:
     """Host->device feed of the training loop (the reference copies each batch
     with a blocking ``.cuda()``, train_patch.py:164-166).  The copy of batch

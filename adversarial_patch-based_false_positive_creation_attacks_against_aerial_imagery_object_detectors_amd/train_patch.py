@@ -49,7 +49,7 @@ from . import patch_config
 from . import synthetic
 from . import weights as synth_weights
 from .darknet_v3 import Darknet
-from .load_data import (DevicePrefetcher, DotaDataset, FrameCache, HasSusRGB, NPSCalculator, PatchApplier,
+from .load_data import (DevicePrefetcher, DotaCollate, DotaDataset, FrameCache, HasSusRGB, NPSCalculator, PatchApplier,
                         PatchTransformer, TotalVariation, read_image as _read_image, regularisers)
 
 TV_FACTOR = 2.5      # train_patch.py:25
@@ -198,8 +198,11 @@ class GlobalBatchSampler(torch.utils.data.Sampler):
     yields its CONTIGUOUS slice [lo, hi) of each global batch, so the images of
     global step k are the same for any number of ranks and so are their
     transformer draws (keyed by the global index lo + i).  A ragged last batch
-    is split as evenly as possible (the loss weights account for it); a
-    final batch with fewer images than ranks is dropped when world > 1."""
+    is split as evenly as possible (the loss weights account for it); when it
+    holds fewer images than there are ranks, the surplus ranks get EMPTY
+    shards and contribute only their share of the patch terms (PatchTrainer.
+    losses on an empty batch), so the epoch trains on the same images in the
+    same steps as one process whatever the world size."""
 
     def __init__(self, n_items, global_batch, rank=0, world=1, shuffle=True, seed=0):
         self.n, self.G, self.rank, self.world = int(n_items), int(global_batch), int(rank), int(world)
@@ -209,10 +212,7 @@ class GlobalBatchSampler(torch.utils.data.Sampler):
         self.epoch = int(epoch)
 
     def __len__(self):
-        nb = -(-self.n // self.G)
-        if self.world > 1 and nb and self.n - (nb - 1) * self.G < self.world:
-            nb -= 1
-        return nb
+        return -(-self.n // self.G)
 
     def shard_of(self, k):
         """(lo, hi, n_global) of this rank's slice of global batch k."""
@@ -263,6 +263,7 @@ class PatchTrainer(object):
         self.flags = torch.zeros(1, dtype=torch.int32, device=self.device)
         # NaN/Inf guard on the patch gradient (replaces detect_anomaly, train_patch.py:158)
         self.check_finite = os.environ.get("ADVPATCH_CHECK_FINITE", "1") != "0"
+        self._found_inf = None
 
     # ------------------------------------------------------------------
     def generate_patch(self, type):
@@ -288,6 +289,8 @@ class PatchTrainer(object):
         yields adv_patch.grad."""
         objective = objective or self.objective
         img_size = self.darknet_model.height
+        if img_batch.size(0) == 0:
+            return self._patch_terms_only(adv_patch, objective, weights)
         p_img, center = self.patch_transformer.forward_composite(adv_patch, lab_batch, img_batch, img_size,
                                                                  do_rotate=True, draws=draws)
         roi = self.patch_transformer.last_roi
@@ -307,6 +310,23 @@ class PatchTrainer(object):
         terms.update({"patch_center": center, "obj": obj, "cls": cls, "cells": cells, "flags": flags})
         return loss, terms
 
+    def _patch_terms_only(self, adv_patch, objective, weights):
+        """The loss of a rank whose shard of a global batch is empty (a ragged
+        last batch with fewer images than ranks, GlobalBatchSampler): no image
+        terms, its 1/world share of NPS/TV/colour, so the SUM all-reduce still
+        yields the global-batch loss and gradient."""
+        dev = adv_patch.device
+        reg = regularisers(adv_patch, self.nps_calculator.colors)
+        if self._tv_floor is None or self._tv_floor.device != dev:
+            self._tv_floor = torch.tensor(0.1, device=dev)
+        z = torch.zeros((), device=dev)
+        loss, terms = combine_terms(z, z, reg[0], reg[1], reg[2], objective, weights, self._tv_floor)
+        terms.update({"patch_center": torch.empty(0, 2, device=dev), "obj": torch.empty(0, 0, device=dev),
+                      "cls": torch.empty(0, 0, 15, device=dev), "cells": torch.empty(0, 0, dtype=torch.int32,
+                                                                                   device=dev),
+                      "flags": self.flags})
+        return loss, terms
+
     def allreduce_grad(self, adv_patch, terms):
         """One all-reduce(SUM) of [patch grad | weighted loss scalars] over all ranks."""
         if self.dist:
@@ -318,9 +338,19 @@ class PatchTrainer(object):
         loss.backward()
         self.allreduce_grad(adv_patch, terms)
         if self.check_finite:
+            # after the all-reduce: a NaN/Inf on any rank reaches every rank's reduced
+            # gradient, so all ranks raise the same bit and skip the same updates
             g = adv_patch.grad
             nat.call("po_check_finite", nat.ptr(g), g.numel(), FLAG_NONFINITE, nat.ptr(self.flags, torch.int32),
                      nat.stream())
+            if optimizer.defaults.get("fused"):
+                # once the bit is up the fused Adam skips its update (found_inf, as under
+                # GradScaler): the patch stays at its last finite value until check_flags
+                # raises at the end of the epoch, instead of being corrupted by the NaN
+                if self._found_inf is None or self._found_inf.device != g.device:
+                    self._found_inf = torch.zeros(1, device=g.device)
+                self._found_inf.copy_(self.flags & FLAG_NONFINITE).clamp_(max=1.0)
+                optimizer.found_inf = self._found_inf
         optimizer.step()
         optimizer.zero_grad()
         adv_patch.data.clamp_(0, 1)
@@ -368,6 +398,7 @@ class PatchTrainer(object):
             if self.verbose and rank0:
                 print("Total images in TrainSet : ", n_images)
             ds = DotaDataset(self.config.img_dir, self.config.lab_dir, max_lab, img_size, shuffle=True, as_uint8=True)
+            collate = DotaCollate(img_size, max_lab, as_uint8=True)
             sampler = GlobalBatchSampler(len(ds), batch_size, self.rank, self.world, shuffle=True, seed=seed)
             if cache_frames is None:
                 need = len(ds) * (3 * img_size * img_size + max_lab * 5 * 4)
@@ -377,7 +408,7 @@ class PatchTrainer(object):
             else:
                 loader = DevicePrefetcher(torch.utils.data.DataLoader(
                     ds, batch_sampler=sampler, num_workers=num_workers, pin_memory=True,
-                    persistent_workers=num_workers > 0), self.device)
+                    persistent_workers=num_workers > 0, collate_fn=collate), self.device)
         else:
             loader = DevicePrefetcher(data, self.device)
         optimizer = self.make_optimizer(adv_patch)

@@ -224,7 +224,9 @@ int po_region_boxes(const float* head, int B, int A, int C, int h, int w, const 
  * unless a kept box before it has bbox_iou (centre form, fp32, utils.py:37-57)
  * > nms_thresh with it, and only if det_conf > 0.  keep [B][cap] = record
  * indices in kept order, nkeep [B].  nmax >= every counts[b] (<= cap, <= 65536);
- * workspaces keys / mask sized by po_nms_workspace. */
+ * workspaces keys / mask sized by po_nms_workspace(B, nmax).  An image with
+ * counts[b] > nmax is processed on its first nmax records only (the
+ * workspaces hold nmax), never beyond. */
 int po_nms(const float* boxes, const int32_t* counts, int B, int cap, int nmax, float nms_thresh, uint64_t* keys,
            uint64_t* mask, int32_t* keep, int32_t* nkeep, po_stream_t s);
 int po_nms_workspace(int B, int nmax, int64_t* key_words, int64_t* mask_words);

@@ -58,11 +58,22 @@ def _worker(rank, world, port, B, objective, out_q):
     net, (img, lab, patch, dr), colors = _case(B)
     lo, hi = _bounds(B, rank, world)
     w = tp.shard_weights(hi - lo, B, world, objective)
-    r = oracle.train_step(patch, img[lo:hi], lab[lo:hi], {k: v[lo:hi] for k, v in dr.items()}, net, colors,
-                          objective=objective,
-                          combine=lambda *t: tp.combine_terms(*t, objective=objective, weights=w))
-    terms = {k: r[k] for k in tp.LOSS_KEYS}
-    g = r["grad"].clone()
+    if hi > lo:
+        r = oracle.train_step(patch, img[lo:hi], lab[lo:hi], {k: v[lo:hi] for k, v in dr.items()}, net, colors,
+                              objective=objective,
+                              combine=lambda *t: tp.combine_terms(*t, objective=objective, weights=w))
+        terms = {k: r[k] for k in tp.LOSS_KEYS}
+        g = r["grad"].clone()
+    else:
+        # an empty shard (fewer images than ranks): PatchTrainer._patch_terms_only —
+        # no image terms, this rank's 1/world share of NPS/TV/colour
+        leaf = patch.detach().clone().requires_grad_(True)
+        z = torch.zeros(())
+        loss, terms = tp.combine_terms(z, z, oracle.nps_score(leaf, colors), oracle.total_variation(leaf),
+                                       oracle.colorful_loss(leaf), objective=objective, weights=w)
+        loss.backward()
+        terms = {k: v.detach() for k, v in terms.items()}
+        g = leaf.grad.clone()
     tp.allreduce_patch_grad(g, terms)
     if rank == 0:
         out_q.put((g.numpy(), {k: float(v) for k, v in terms.items()}))
@@ -71,9 +82,11 @@ def _worker(rank, world, port, B, objective, out_q):
 
 
 @pytest.mark.parametrize("world,B,objective", [(2, 8, "ce"), (4, 8, "ce"), (2, 8, "targeted"), (4, 8, "targeted"),
-                                               (3, 8, "ce"), (3, 8, "targeted")])
+                                               (3, 8, "ce"), (3, 8, "targeted"), (4, 3, "ce"), (3, 2, "targeted")])
 def test_sharded_allreduce_equals_full_batch(world, B, objective):
-    """world 3 with B=8 gives ragged shards (2, 3, 3)."""
+    """world 3 with B=8 gives ragged shards (2, 3, 3); world 4 with B=3 and
+    world 3 with B=2 give EMPTY shards (a ragged last global batch with fewer
+    images than ranks), which contribute only their share of the patch terms."""
     import oracle
     net, (img, lab, patch, dr), colors = _case(B)
     full = oracle.train_step(patch, img, lab, dr, net, colors, objective=objective)
@@ -94,7 +107,7 @@ def test_sharded_allreduce_equals_full_batch(world, B, objective):
         assert abs(v - float(full[k])) <= 1e-5 * max(1.0, abs(float(full[k]))), (k, v, float(full[k]))
 
 
-@pytest.mark.parametrize("n,G", [(37, 8), (32, 8), (9, 4)])
+@pytest.mark.parametrize("n,G", [(37, 8), (32, 8), (9, 4), (10, 4)])
 def test_global_batch_sampler_is_rank_count_independent(n, G):
     """For every world size, the union of the ranks' slices of global batch k
     (concatenated in rank order) is the single-process batch k, and the shard
@@ -111,8 +124,8 @@ def test_global_batch_sampler_is_rank_count_independent(n, G):
             for r in range(world):
                 lo, hi, ng = samplers[r].shard_of(k)
                 assert ng == len(one[k]) and per[r][k] == one[k][lo:hi]
-        # a final batch smaller than the world is dropped, nothing else
-        assert len(samplers[0]) in (len(one), len(one) - 1)
+        # nothing is dropped: a final batch smaller than the world leaves some ranks an empty shard
+        assert len(samplers[0]) == len(one)
     # set_epoch reshuffles, identically on every rank
     s0, s1 = tp.GlobalBatchSampler(n, G, 0, 2, seed=5), tp.GlobalBatchSampler(n, G, 1, 2, seed=5)
     s0.set_epoch(3)

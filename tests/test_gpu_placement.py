@@ -59,6 +59,7 @@ TM_CASES = [
     (608, 224, 1, 3, 0.2, 0.9, 0.05),          # single detection: the 0.25 row
     (416, 96, 12, 4, 0.45, 1.45, 0.5),         # large boxes: crowded map
     (97, 32, 5, 5, 0.3, -0.7, 0.999),          # odd size: half-pixel translation
+    (101, 32, 3, 6, 0.2, 0.2, 0.3),            # B*S*S and B*L not multiples of 4 (workspace sub-buffer alignment)
 ]
 
 

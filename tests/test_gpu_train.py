@@ -90,6 +90,19 @@ def test_nonfinite_guard_and_flags(yolo_weights):
     tr.step(patch, opt, sy.frames(2, 64, seed=2).to(DEV), sy.labels(2, seed=3).to(DEV))
     with pytest.raises(RuntimeError):
         tr.check_flags()
+    # once the bit is up, the fused Adam skips its update (found_inf): the patch
+    # keeps its last finite value instead of taking the NaN gradient's step
+    good = sy.patch(32, seed=4).to(DEV).requires_grad_(True)
+    opt = tr.make_optimizer(good)
+    frames, labels = sy.frames(2, 64, seed=2).to(DEV), sy.labels(2, seed=3).to(DEV)
+    tr.flags.fill_(tp.FLAG_NONFINITE)
+    before = good.detach().clone()
+    tr.step(good, opt, frames, labels)
+    assert torch.equal(good.detach(), before)
+    assert float(opt.state[good]["step"]) == 0.0
+    tr.flags.zero_()
+    tr.step(good, opt, frames, labels)
+    assert not torch.equal(good.detach(), before) and float(opt.state[good]["step"]) == 1.0
 
 
 @pytest.mark.parametrize("prec,tol", [("fp32", 1e-5), ("fp16x3", 1e-4)])
@@ -125,6 +138,35 @@ def test_two_half_steps_equal_one_full_step(yolo_weights, monkeypatch, prec, tol
     assert rel < tol, rel
     for k in tp.LOSS_KEYS:
         assert abs(tsum[k] - float(tf[k])) <= 1e-5 * max(1.0, abs(float(tf[k]))), (k, tsum[k], float(tf[k]))
+    tr.check_flags()
+
+
+@pytest.mark.parametrize("objective", ["ce", "targeted"])
+def test_empty_shard_adds_only_its_patch_terms(yolo_weights, objective):
+    """A ragged last global batch with fewer images than ranks leaves a rank
+    an EMPTY shard (GlobalBatchSampler): PatchTrainer.losses on the empty
+    batch contributes its 1/world share of NPS/TV/colour and no image term, so
+    the SUM of the two ranks' weighted steps is the one-process step."""
+    tp, sy = pkg_mod("train_patch"), pkg_mod("synthetic")
+    tr = _trainer("builtin:mini3", yolo_weights + ".mini3", objective=objective, batch=1)
+    img, lab = sy.frames(1, 64, seed=21).to(DEV), sy.labels(1, seed=22).to(DEV)
+    patch = sy.patch(32, seed=23).to(DEV)
+    dr = {k: v.to(DEV) for k, v in sy.draws(1, 32, seed=24).items()}
+    pf = patch.clone().requires_grad_(True)
+    loss, tf = tr.losses(pf, img, lab, dr)
+    loss.backward()
+    gsum, tsum = torch.zeros_like(patch), {k: 0.0 for k in tp.LOSS_KEYS}
+    for lo, hi in ((0, 0), (0, 1)):                   # shard_of for world 2, one image: rank 0 is empty
+        ph = patch.clone().requires_grad_(True)
+        w = tp.shard_weights(hi - lo, 1, 2, objective)
+        loss, th = tr.losses(ph, img[lo:hi], lab[lo:hi], {k: v[lo:hi] for k, v in dr.items()}, weights=w)
+        loss.backward()
+        gsum += ph.grad
+        for k in tp.LOSS_KEYS:
+            tsum[k] += float(th[k])
+    assert float((gsum - pf.grad).abs().max() / pf.grad.abs().max()) < 1e-6
+    for k in tp.LOSS_KEYS:
+        assert abs(tsum[k] - float(tf[k])) <= 1e-6 * max(1.0, abs(float(tf[k]))), (k, tsum[k], float(tf[k]))
     tr.check_flags()
 
 
