@@ -1066,6 +1066,311 @@ __global__ __launch_bounds__(256, 2) void conv_wino3_k(const ConvArgs a, const f
   if (a.sum_amax) po::amax_commit(a.sum_amax, mx.s);
   if (a.y2_amax) po::amax_commit(a.y2_amax, mx.y2);
 }
+
+// ---------------------------------------------------------------------------
+// Tile 67 (staging 12): Winograd F(2x2,3x3) with 64 tiles x 64 output
+// channels per 512-thread workgroup (8 waves, one workgroup per CU) and a
+// software-pipelined k-loop with ONE barrier per k-step.
+//
+// On gfx950 the fp32 MFMA (v_mfma_f32_32x32x2_f32) never co-executes with
+// VALU work (SQ_VALU_MFMA_COEXEC_CYCLES = 0 on tiles 65/66): the matrix pipe
+// is fed only while some wave of the SIMD has an MFMA ready.  Tile 66 runs, per
+// k-step, barrier -> transform -> barrier -> B-fragment loads -> MFMAs, so every
+// wave exposes the LDS-DMA wait, two barriers and the L2 latency of its B
+// fragments once per step, and with 32 tiles per workgroup every B fragment
+// feeds one MFMA.  Here:
+//   * the input patches come to REGISTERS (16 buffer_load_dwordx2 per thread:
+//     tile tid >> 3, channel pair tid & 7), one k-step ahead; the transform of
+//     step k+1 runs between the two MFMA groups of step k and writes the other
+//     half of a double-buffered V (2 x 64 KB);
+//   * wave w owns components 2w, 2w+1 for BOTH 32-tile M-blocks: each B
+//     fragment register feeds two MFMAs (half the U traffic per MFMA of tile
+//     66), and the B fragments of component c for step k+1 are loaded into
+//     c's registers right after c's MFMAs of step k have been issued;
+//   * one barrier per k-step (V of step k+1 complete; V of step k free).
+// Same transforms, per-accumulator MFMA order (k-steps, then channels
+// 8h + s) and epilogue arithmetic as tiles 65/66: bit-identical outputs.
+// Split-K (blockIdx.y = slice) and the fused pool epilogue as tile 66.
+constexpr int T4 = 64, N4 = 64;
+constexpr int V4_FLOATS = 16 * T4 * WK;                 // one transformed buffer: 64 KB
+__device__ __forceinline__ int v4idx(int xi, int t, int ch) { return ((xi * T4 + t) * WK) + ((ch ^ ((t >> 2) & 3)) << 2); }
+
+__global__ __launch_bounds__(512, 1) void conv_wino4_k(const ConvArgs a, const float* __restrict__ U, int Ht, int Wt) {
+  constexpr int CPW = 2;                 // components per wave
+  constexpr int TH = 32;                 // tiles per epilogue pass (one M-block)
+  __shared__ __attribute__((aligned(16))) float smem[2 * V4_FLOATS];
+  __shared__ int s_live;
+  const int wgid = po::xcd_remap();
+  const int tn = wgid % a.ntiles_n, tm = wgid / a.ntiles_n;
+  const int m0 = tm * T4, n0 = tn * N4;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wave_u = __builtin_amdgcn_readfirstlane(wave);
+  const int h = lane >> 5;
+
+  if (tid == 0) s_live = 0;
+  __syncthreads();
+  if (tid < T4) {
+    int b, ti, tj;
+    if (tile_point(a, Ht, Wt, m0 + tid, b, ti, tj)) s_live = 1;
+  }
+  __syncthreads();
+  if (!s_live) return;
+
+  // ---- input staging: thread (tile r, channel pair tc) loads its 4x4 patch, 2 channels
+  const uint32_t in_bytes = (uint32_t)__builtin_amdgcn_readfirstlane(a.in_bytes);
+  const __amdgpu_buffer_rsrc_t in_rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(a.in), 0, in_bytes, 0x00020000);
+  const int r = tid >> 3, tc = tid & 7;
+  uint32_t off[16];
+  {
+    int b, ti, tj;
+    const bool ok_t = tile_point(a, Ht, Wt, m0 + r, b, ti, tj);
+    const uint32_t pix_bytes = (uint32_t)a.Cin_p * 4u;
+#pragma unroll
+    for (int p = 0; p < 16; ++p) {
+      const int y = 2 * ti - 1 + (p >> 2), x = 2 * tj - 1 + (p & 3);
+      const bool ok = ok_t && (unsigned)y < (unsigned)a.Hin && (unsigned)x < (unsigned)a.Win;
+      off[p] = ok ? (((uint32_t)b * a.Hin + y) * a.Win + x) * pix_bytes + 8u * tc : kOOB;
+    }
+  }
+  f2v d[16];
+  auto gload = [&](int ks) {
+    const uint32_t cb = (uint32_t)__builtin_amdgcn_readfirstlane(ks * (WK * 4));
+#pragma unroll
+    for (int p = 0; p < 16; ++p) d[p] = __builtin_bit_cast(f2v, __builtin_amdgcn_raw_buffer_load_b64(in_rs, off[p], cb, 0));
+  };
+  // B^T d B of the thread's (tile, channel pair) into V buffer vb (tile 66's arithmetic)
+  auto transform = [&](float* Vb) {
+    f2v t[4][4];
+#pragma unroll
+    for (int v = 0; v < 4; ++v) {
+      const f2v d0 = d[v], d1 = d[4 + v], d2 = d[8 + v], d3 = d[12 + v];
+      t[0][v] = d0 - d2;
+      t[1][v] = d1 + d2;
+      t[2][v] = d2 - d1;
+      t[3][v] = d1 - d3;
+    }
+    const int sub = (tc & 1) * 2;
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const f2v e[4] = {t[u][0] - t[u][2], t[u][1] + t[u][2], t[u][2] - t[u][1], t[u][1] - t[u][3]};
+#pragma unroll
+      for (int v = 0; v < 4; ++v) *reinterpret_cast<f2v*>(Vb + v4idx(u * 4 + v, r, tc >> 1) + sub) = e[v];
+    }
+  };
+
+  // ---- B operand (fragment-ordered U) per component, one k-step ahead
+  const int kc_n = a.Cin_p / WK;
+  const float* Ub = U + (size_t)lane * 4;
+  float4 bq[CPW][2][2];
+  auto bload = [&](int c, int ks) {
+#pragma unroll
+    for (int nb = 0; nb < 2; ++nb) {
+      const float* p = Ub + ((((size_t)(2 * tn + nb) * kc_n + ks) * 16 + wave_u * CPW + c) * 512);
+      bq[c][nb][0] = *reinterpret_cast<const float4*>(p);
+      bq[c][nb][1] = *reinterpret_cast<const float4*>(p + 256);
+    }
+  };
+  floatx16 acc[CPW][2][2];
+#pragma unroll
+  for (int c = 0; c < CPW; ++c)
+#pragma unroll
+    for (int mb = 0; mb < 2; ++mb)
+#pragma unroll
+      for (int nb = 0; nb < 2; ++nb)
+#pragma unroll
+        for (int e = 0; e < 16; ++e) acc[c][mb][nb][e] = 0.f;
+  // the MFMAs of component c of one k-step on V buffer Vb
+  auto mfma_c = [&](int c, const float* Vb) {
+    const int xi = wave_u * CPW + c;
+#pragma unroll
+    for (int mb = 0; mb < 2; ++mb) {
+      const int t = 32 * mb + (lane & 31);
+      const float4 a0 = *reinterpret_cast<const float4*>(Vb + v4idx(xi, t, 2 * h));
+      const float4 a1 = *reinterpret_cast<const float4*>(Vb + v4idx(xi, t, 2 * h + 1));
+      const float av[8] = {a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w};
+#pragma unroll
+      for (int nb = 0; nb < 2; ++nb) {
+        const float bv[8] = {bq[c][nb][0].x, bq[c][nb][0].y, bq[c][nb][0].z, bq[c][nb][0].w,
+                             bq[c][nb][1].x, bq[c][nb][1].y, bq[c][nb][1].z, bq[c][nb][1].w};
+#pragma unroll
+        for (int s8 = 0; s8 < 8; ++s8)        // MFMA step s, half h <-> channel 8h + s
+          acc[c][mb][nb] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[s8], bv[s8], acc[c][mb][nb], 0, 0, 0);
+      }
+    }
+  };
+
+  // split-K (blockIdx.y = slice): input-channel steps [ks0, ks1) of kc_n
+  const int ks0 = (int)((int64_t)blockIdx.y * kc_n / a.ksplit), ks1 = (int)((int64_t)(blockIdx.y + 1) * kc_n / a.ksplit);
+  // prologue in the loop body's issue order (B0, inputs, B1): the loop header's
+  // waitcnt state then equals the back edge's and stays a partial wait
+  gload(ks0);
+  transform(smem);
+  __builtin_amdgcn_sched_barrier(0);
+  bload(0, ks0);
+  __builtin_amdgcn_sched_barrier(0);
+  gload(min(ks0 + 1, ks1 - 1));
+  __builtin_amdgcn_sched_barrier(0);
+  bload(1, ks0);
+  __builtin_amdgcn_sched_barrier(0);
+  __syncthreads();
+  int ks = ks0;
+  do {                                       // ks1 > ks0: every slice has a k-step (host check); no
+    float* Vc = smem + ((ks - ks0) & 1) * V4_FLOATS;      // zero-trip test to sink the prologue loads into
+    float* Vn = smem + (((ks - ks0) & 1) ^ 1) * V4_FLOATS;
+    // branch-free body (a branch around the prefetches would merge the waitcnt
+    // states of both paths into a full vmcnt(0) drain): on the last steps the
+    // prefetches re-read the last k-step and the transform rewrites the V
+    // buffer nobody reads any more
+    const int k1 = min(ks + 1, ks1 - 1), k2 = min(ks + 2, ks1 - 1);
+    // phases kept in this order (sched_barrier): live ranges stay within the
+    // 256-VGPR budget of two waves per SIMD
+    mfma_c(0, Vc);
+    __builtin_amdgcn_sched_barrier(0);
+    bload(0, k1);                            // component 0's registers are free once its MFMAs are issued
+    __builtin_amdgcn_sched_barrier(0);
+    transform(Vn);                           // step ks+1 (d landed one step ago)
+    __builtin_amdgcn_sched_barrier(0);
+    gload(k2);
+    __builtin_amdgcn_sched_barrier(0);
+    mfma_c(1, Vc);
+    __builtin_amdgcn_sched_barrier(0);
+    bload(1, k1);
+    __syncthreads();                         // V(ks+1) complete everywhere; V(ks) free
+  } while (++ks < ks1);
+
+
+  // ---- epilogue, two passes of 32 tiles (pass = M-block mb): M[xi][tile - 32 pass][64 ch]
+  // in the 128 KB of the V buffers; thread tid owns tile tid >> 4 of the pass, channels n4 .. n4+3
+  float* M = smem;
+  EpiMax mx;
+  const int wpp = a.Cout_p >> 5;
+  const int n4 = n0 + 4 * (lane & 15);
+  const float4 bias4 = (a.bias && n4 < a.N) ? *reinterpret_cast<const float4*>(a.bias + n4)
+                                            : make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+  for (int pass = 0; pass < 2; ++pass) {
+    // this pass's tile of the lane, its output mask and epilogue inputs (loads before any store)
+    int vb = 0, vti = 0, vtj = 0;
+    uint32_t vok = 0u;
+    EpiIn4 pre4[4];
+    {
+      const bool tl = tile_point(a, Ht, Wt, m0 + TH * pass + (tid >> 4), vb, vti, vtj);
+      int4 bx = make_int4(0, 0, 1 << 30, 1 << 30);
+      if (a.gbox && tl) bx = reinterpret_cast<const int4*>(a.gbox)[vb];
+#pragma unroll
+      for (int p = 0; p < 4; ++p) {
+        const int i = 2 * vti + (p >> 1), j = 2 * vtj + (p & 1);
+        if (tl && n4 < a.N && i >= 0 && j >= 0 && i < a.Hout && j < a.Wout && i >= bx.x && i < bx.z && j >= bx.y && j < bx.w)
+          vok |= 1u << p;
+      }
+#pragma unroll
+      for (int p = 0; p < 4; ++p) {
+        if (!((vok >> p) & 1u) || a.ksplit > 1) continue;
+        const size_t pix = ((size_t)vb * a.Hout + 2 * vti + (p >> 1)) * a.Wout + 2 * vtj + (p & 1);
+        const size_t o = pix * (size_t)a.Cout_p + n4;
+        const size_t wo = pix * (size_t)(a.Cout_p >> 5) + (n4 >> 5);
+        if (a.res) pre4[p].res = *reinterpret_cast<const float4*>(a.res + o);
+        if (a.accumulate) pre4[p].yold = *reinterpret_cast<const float4*>(a.y + o);
+        if (a.mbits) pre4[p].m = a.mbits[wo];
+        if (a.y2 && a.m2bits) pre4[p].m2 = a.m2bits[wo];
+      }
+    }
+    __syncthreads();                       // the k-loop's (or the previous pass's) LDS reads are done
+#pragma unroll
+    for (int c = 0; c < CPW; ++c)
+#pragma unroll
+      for (int nb = 0; nb < 2; ++nb)
+#pragma unroll
+        for (int e = 0; e < 16; ++e) {
+          const int t = (e & 3) + 8 * (e >> 2) + 4 * h;
+          M[((wave * CPW + c) * TH + t) * N4 + nb * 32 + (lane & 31)] = acc[c][pass][nb][e];
+        }
+    __syncthreads();
+    const int t = tid >> 4;
+    float4 s0[4], s1[4];
+#pragma unroll
+    for (int v = 0; v < 4; ++v) {
+      float4 m[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+        m[u] = *reinterpret_cast<const float4*>(M + ((u * 4 + v) * TH + t) * N4 + 4 * (lane & 15));
+      s0[v] = f4add(f4add(m[0], m[1]), m[2]);
+      s1[v] = f4sub(f4sub(m[1], m[2]), m[3]);
+    }
+    const float4 yv[2][2] = {{f4add(f4add(s0[0], s0[1]), s0[2]), f4sub(f4sub(s0[1], s0[2]), s0[3])},
+                             {f4add(f4add(s1[0], s1[1]), s1[2]), f4sub(f4sub(s1[1], s1[2]), s1[3])}};
+    if (a.ksplit > 1) {
+      // split-K slice: the raw inverse-transformed partial sums at the GEMM rows
+      // conv_reduce_k enumerates (grid_point: row-major over the map, or over
+      // the image's box), which applies the epilogue
+      float* ws = a.ws + (size_t)blockIdx.y * a.M * a.N;
+      int i0 = 0, j0 = 0, gw = a.Wg;
+      if (a.gbox) {
+        const po::GridBox g = po::grid_box(a, vb);
+        i0 = g.i0, j0 = g.j0, gw = g.w;
+      }
+#pragma unroll
+      for (int p = 0; p < 4; ++p) {
+        if (!((vok >> p) & 1u)) continue;
+        const int l = (2 * vti + (p >> 1) - i0) * gw + 2 * vtj + (p & 1) - j0;
+        *reinterpret_cast<float4*>(ws + ((size_t)vb * a.mrows + l) * a.N + n4) = yv[p >> 1][p & 1];
+      }
+    } else if (a.pool_y) {
+      // fused k=2 stride-2 max pool (even map, no boxes: host checks): the
+      // lane's 2x2 Winograd tile is pool window (vti, vtj).  Bias + activation
+      // per element as epi_store4, then conv_pool_epilogue's rule and codes
+      // (first window position on ties, NaN wins; bit 3 | bit 2 = max <= 0 for
+      // a leaky conv); the conv output itself is not stored.
+      if (vok == 0xFu) {
+        float pv[4] = {0.f, 0.f, 0.f, 0.f};
+        uint32_t arg[4] = {0u, 0u, 0u, 0u};
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          const float4 v = yv[k >> 1][k & 1];
+          float x[4] = {v.x + bias4.x, v.y + bias4.y, v.z + bias4.z, v.w + bias4.w};
+#pragma unroll
+          for (int c = 0; c < 4; ++c) {
+            if (a.act) x[c] = po::leaky(x[c]);
+            if (k == 0 || x[c] > pv[c] || isnan(x[c])) { pv[c] = x[c]; arg[c] = (uint32_t)k; }
+          }
+        }
+        uint32_t code = 0u;
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+          if (a.act) arg[c] |= 8u | (pv[c] > 0.f ? 0u : 4u);
+          code |= arg[c] << (8 * c);
+          mx.y = fmaxf(mx.y, fabsf(pv[c]));
+        }
+        const size_t po = (((size_t)vb * (a.Hout >> 1) + vti) * (a.Wout >> 1) + vtj) * a.Cout_p + n4;
+        *reinterpret_cast<float4*>(a.pool_y + po) = make_float4(pv[0], pv[1], pv[2], pv[3]);
+        *reinterpret_cast<uint32_t*>(a.pool_am + po) = code;
+      }
+    } else {
+#pragma unroll
+      for (int p = 0; p < 4; ++p) {
+        const bool ok = (vok >> p) & 1u;
+        const size_t pix = ((size_t)vb * a.Hout + 2 * vti + (p >> 1)) * a.Wout + 2 * vtj + (p & 1);
+        uint32_t nib = 0u;
+        if (ok) {
+          const float4 out = epi_store4(a, pix, n4, yv[p >> 1][p & 1], bias4, pre4[p], mx);
+          nib = (out.x > 0.f ? 1u : 0u) | (out.y > 0.f ? 2u : 0u) | (out.z > 0.f ? 4u : 0u) | (out.w > 0.f ? 8u : 0u);
+        }
+        if (a.ybits) {
+          // 8 lanes hold the 32 channels of one sign-bit word: OR their nibbles
+          uint32_t w = nib << (4 * (lane & 7));
+          w |= (uint32_t)__shfl_xor((int)w, 1);
+          w |= (uint32_t)__shfl_xor((int)w, 2);
+          w |= (uint32_t)__shfl_xor((int)w, 4);
+          if (ok && (lane & 7) == 0) a.ybits[pix * wpp + (n4 >> 5)] = w;
+        }
+      }
+    }
+  }
+  if (a.ksplit > 1) return;                // conv_reduce_k commits the max|x| slots
+  if (a.y_amax) po::amax_commit(a.y_amax, mx.y);
+  if (a.sum_amax) po::amax_commit(a.sum_amax, mx.s);
+  if (a.y2_amax) po::amax_commit(a.y2_amax, mx.y2);
+}
 }  // namespace
 
 namespace po {
@@ -1121,5 +1426,30 @@ int launch_wino(const ConvArgs& a, const float* U, hipStream_t st, int bm, int w
   const int ntm = ceil_div((int64_t)a.B * Ht * Wt, WT);
   hipLaunchKernelGGL(conv_wino_k, dim3(ntm * b.ntiles_n), dim3(256), 0, st, b, U, Ht, Wt);
   return check_launch("po_conv (winograd)");
+}
+
+// po_conv tile staging 12 (tile 67): conv_wino4_k, 64 tiles x 64 channels per
+// 512-thread workgroup, register-staged input, pipelined k-loop (see above).
+int launch_wino4(const ConvArgs& a, const float* U, hipStream_t st) {
+  PO_REQUIRE(U, "po_conv: Winograd tile needs the transformed weights (Wwino)");
+  PO_REQUIRE(a.prec == 0 && a.ntaps == 9 && a.tkw == 3 && (a.sdh == 1 || a.sdh == -1) && (a.sdw == 1 || a.sdw == -1) &&
+                 a.dh0 == -a.sdh && a.dw0 == -a.sdw,
+             "po_conv: Winograd tile needs a full 3x3 neighbourhood of taps");
+  PO_REQUIRE(a.in_step == 1 && a.out_step == 1 && a.out_oy == 0 && a.out_ox == 0 && !a.in_org && !a.out_org,
+             "po_conv: Winograd tile needs stride 1 on full maps");
+  PO_REQUIRE(a.Hg == a.Hout && a.Wg == a.Wout && a.Hin == a.Hout && a.Win == a.Wout,
+             "po_conv: Winograd tile needs source, grid and destination of one size");
+  PO_REQUIRE(a.N % N4 == 0 && a.Cin_p % WK == 0, "po_conv: tile 67 needs N %% 64 == 0 and Cin_p %% 16 == 0");
+  PO_REQUIRE(a.ksplit == 1 || (!a.pool_y && a.ws && a.ksplit <= a.Cin_p / WK && (int64_t)a.M * a.N < (1LL << 31)),
+             "po_conv: tile 67 split-K needs ksplit <= Cin_p / 16 and a workspace");
+  PO_REQUIRE(!a.pool_y || (a.Hout % 2 == 0 && a.Wout % 2 == 0 && !a.gbox),
+             "po_conv: a fused pool needs an even map and no boxes");
+  const int Ht = (a.Hout + 1) / 2, Wt = (a.Wout + 1) / 2;
+  PO_REQUIRE((int64_t)a.B * Ht * Wt < (1LL << 31), "po_conv: too many tiles");
+  ConvArgs b = a;
+  b.ntiles_n = a.N / N4;
+  const int ntm = ceil_div((int64_t)a.B * Ht * Wt, T4);
+  hipLaunchKernelGGL(conv_wino4_k, dim3(ntm * b.ntiles_n, a.ksplit), dim3(512), 0, st, b, U, Ht, Wt);
+  return check_launch("po_conv (winograd 64x64)");
 }
 }  // namespace po

@@ -514,6 +514,26 @@ class NetPlan:
         self.cone_prog = torch.tensor(prog, dtype=torch.int32, device=self.device).contiguous()
         self.cone_boxes = torch.zeros(self.n, self.B, 4, dtype=torch.int32, device=self.device)
 
+    def tuning_rois(self):
+        """[B,4] patch footprints (x0, y0, x1, y1) the tuner times boxed
+        launches on: square footprints with sides spread over 0.10-0.30 S
+        across the batch at positions spread over the frame — the range of
+        the training placement (target size S/4 * sqrt(y^2 + w^2) of the
+        selected label, SURVEY Q2, times the rotation's up to sqrt(2);
+        ~0.16 S on the synthetic DOTA labels).  A centred S/3 footprint (the
+        round-2 choice) gives boxes ~4x the typical area, and the tuner then
+        leaves the real, smaller boxed launches with too few workgroups."""
+        S, B = self.H, self.B
+        rows = []
+        for b in range(B):
+            f = b / max(B - 1, 1)
+            side = int(S * (0.10 + 0.20 * ((7 * b) % B) / max(B - 1, 1)))
+            cx = int(S * (0.25 + 0.5 * f))
+            cy = int(S * (0.25 + 0.5 * ((3 * b) % B) / max(B - 1, 1)))
+            x0, y0 = max(cx - side // 2, 0), max(cy - side // 2, 0)
+            rows.append([x0, y0, min(x0 + side, S), min(y0 + side, S)])
+        return torch.tensor(rows, dtype=torch.int32, device=self.device)
+
     def set_cones(self, roi):
         """Evaluate the gradient cones of roi [B,4] (None: the whole image)."""
         if self.cone_boxes is None:
@@ -545,7 +565,7 @@ class NetPlan:
         return desc.macs * pts / (desc.B * desc.Hg * desc.Wg)
 
     # Winograd tiles of po_conv: (tiles = GEMM rows, output channels) per workgroup
-    WINO_TILES = {61: (64, 32), 62: (32, 64), 63: (32, 64), 64: (32, 64), 65: (32, 64), 66: (32, 64)}
+    WINO_TILES = {61: (64, 32), 62: (32, 64), 63: (32, 64), 64: (32, 64), 65: (32, 64), 66: (32, 64), 67: (64, 64)}
     _tile_shapes = {}
 
     @classmethod
@@ -576,38 +596,40 @@ class NetPlan:
         if desc.prec != 0:
             return None
         t = desc.tile
+        if t in cls.WINO_TILES:
+            WT = cls.WINO_TILES[t][0]
+            return 2.0 * 16 * cls._live_tiles(desc, t, WT, cones) * WT * desc.Cin_p * desc.N
+        BM, BN, BK = cls.tile_shape(t)
+        return 2.0 * cls._live_tiles(desc, t, BM, cones) * BM * (-(-desc.N // BN) * BN) * desc.ntaps * desc.Cin_p
+
+    @classmethod
+    def _live_tiles(cls, desc, t, bm, cones=None):
+        """GEMM-row workgroups of tile t (bm rows; Winograd: WT 2x2 tiles)
+        that hold a live row (all of them for a full grid)."""
         boxes = None
         if getattr(desc, "support", None) is not None:
             boxes = desc.support.cpu().tolist()
         elif desc.gbox and cones is not None:
-            boxes = cones[desc.cone_block, desc.cone_b0:desc.cone_b0 + desc.B].cpu().tolist()
+            boxes = cones[desc.cone_block, desc.cone_b0:desc.cone_b0 + desc.B].tolist()
         if t in cls.WINO_TILES:
-            WT, WN = cls.WINO_TILES[t]
+            WT = cls.WINO_TILES[t][0]
             Ht, Wt = (desc.Hg + 1) // 2, (desc.Wg + 1) // 2
             per = Ht * Wt
-            if boxes is None:
-                live = [per] * desc.B
-            else:
-                live = []
-                for r0, c0, r1, c1 in boxes:
-                    h = max(((r1 + 1) >> 1) - (r0 >> 1), 0)
-                    w = max(((c1 + 1) >> 1) - (c0 >> 1), 0)
-                    live.append(min(h * w, per))
-            nwg = cls._live_groups(live, per, WT, desc.B)
-            return 2.0 * 16 * nwg * WT * desc.Cin_p * desc.N
-        BM, BN, BK = cls.tile_shape(t)
+            live = [per] * desc.B if boxes is None else [
+                min(max(((r1 + 1) >> 1) - (r0 >> 1), 0) * max(((c1 + 1) >> 1) - (c0 >> 1), 0), per)
+                for r0, c0, r1, c1 in boxes]
+            return cls._live_groups(live, per, WT, desc.B)
         mrows = desc.mrows or desc.Hg * desc.Wg
         if boxes is None:
-            live = [mrows] * desc.B
-        else:
-            def span(lo, hi, off, step, n):
-                a = 0 if lo - off <= 0 else -(-(lo - off) // step)
-                b = 0 if hi - 1 - off < 0 else min(n, (hi - 1 - off) // step + 1)
-                return max(b - a, 0)
-            live = [min(span(r0, r1, desc.out_oy, desc.out_step, desc.Hg) *
-                        span(c0, c1, desc.out_ox, desc.out_step, desc.Wg), mrows) for r0, c0, r1, c1 in boxes]
-        ntm = cls._live_groups(live, mrows, BM, desc.B)
-        return 2.0 * ntm * BM * (-(-desc.N // BN) * BN) * desc.ntaps * desc.Cin_p
+            return -(-(desc.B * mrows) // bm)
+
+        def span(lo, hi, off, step, n):
+            a = 0 if lo - off <= 0 else -(-(lo - off) // step)
+            b = 0 if hi - 1 - off < 0 else min(n, (hi - 1 - off) // step + 1)
+            return max(b - a, 0)
+        live = [min(span(r0, r1, desc.out_oy, desc.out_step, desc.Hg) * span(c0, c1, desc.out_ox, desc.out_step, desc.Wg),
+                    mrows) for r0, c0, r1, c1 in boxes]
+        return cls._live_groups(live, mrows, bm, desc.B)
 
     @staticmethod
     def _live_groups(live, per, rows, B):
@@ -1172,7 +1194,7 @@ class NetPlan:
     # ---------------- autotuning ----------------
     SPLITS = (2, 4, 8, 16, 32)
     WS_FLOATS = 64 << 20          # split-K workspace cap (256 MB)
-    WINO_SPLIT_TILES = (66,)      # Winograd tiles with split-K (conv_wino3_k)
+    WINO_SPLIT_TILES = (66, 67)   # Winograd tiles with split-K (conv_wino3_k, conv_wino4_k)
 
     def _ensure_ws(self, floats):
         if self.ws is None or self.ws.numel() < floats:
@@ -1212,10 +1234,8 @@ class NetPlan:
             for t in bufs.values():
                 t.uniform_(-1.0, 1.0)           # time on random data, not zeros (clock)
         self.amax.fill_(0x3F800000)             # max|x| = 1.0 for the U(-1,1) buffers
-        if self.cone_boxes is not None:         # boxed dgrads: time them on a centred S/3 footprint
-            a = self.H // 3
-            roi = torch.tensor([[a, a, self.H - a, self.H - a]] * self.B, dtype=torch.int32, device=self.device)
-            self.set_cones(roi)
+        if self.cone_boxes is not None:         # boxed dgrads: time them on training-like footprints
+            self.set_cones(self.tuning_rois())
         self.set_support_boxes()                # compact dgrad grids: boxes at the current window origins
         tiles = []
         for t in range(1, nat.PO_CONV_NTILES + 1):
@@ -1223,6 +1243,7 @@ class NetPlan:
             nat.call("po_conv_tile_info", t, nat.ctypes.byref(bm), nat.ctypes.byref(bn), nat.ctypes.byref(bk),
                      nat.ctypes.byref(pr))
             tiles.append((t, bm.value, bn.value, bk.value, pr.value))
+        cones_host = self.cone_boxes.cpu() if self.cone_boxes is not None else None
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         for name, args, desc in self.fwd_ops + self.bwd_ops:
             if name != "po_conv":
@@ -1231,7 +1252,7 @@ class NetPlan:
             if key in cache:
                 self._set_tile(desc, cache[key])
                 continue
-            M = desc.B * desc.Hg * desc.Wg
+            M = desc.B * (desc.mrows or desc.Hg * desc.Wg)
             best = None
             timed = []
             for t, bm, bn, bk, pr in tiles:
@@ -1239,16 +1260,21 @@ class NetPlan:
                     continue
                 if bn > max(32, desc.N):
                     continue
-                ntiles = -(-M // bm) * -(-desc.N // bn)
+                # workgroups that hold live rows (a boxed launch: those of the tuning boxes)
+                live = self._live_tiles(desc, t, bm, cones_host)
+                ntiles = live * -(-desc.N // bn)
                 nks = desc.ntaps * desc.Cin_p // bk
                 cands = [1]
-                if ntiles < 256:
+                if t in self.WINO_TILES:
+                    if t in self.WINO_SPLIT_TILES and not desc.pool_y:
+                        # input-channel slices re-quantise a Winograd launch whose
+                        # workgroup count fills the 512 slots badly (19x19 maps: 800)
+                        # or that has few live workgroups (small gradient-cone boxes)
+                        ks_ok = (2, 3, 4, 6, 8) if ntiles < 512 else (2, 3)
+                        cands += [k for k in ks_ok if desc.Cin_p // bk // k >= 4 and k * M * desc.N <= self.WS_FLOATS]
+                elif ntiles < 256:
                     cands += [k for k in self.SPLITS if k * ntiles <= 2048 and nks // k >= 4
                               and k * M * desc.N <= self.WS_FLOATS]
-                elif t in self.WINO_SPLIT_TILES and not desc.pool_y:
-                    # input-channel slices re-quantise a Winograd launch whose
-                    # workgroup count fills the 512 slots badly (19x19 maps: 800)
-                    cands += [k for k in (2, 3) if desc.Cin_p // bk // k >= 8 and k * M * desc.N <= self.WS_FLOATS]
                 for ks in cands:
                     self._set_tile(desc, (t, ks))
                     if lib.po_conv(*args, st) != 0:      # tile not applicable to this launch

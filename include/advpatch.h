@@ -33,7 +33,7 @@ typedef void* po_stream_t;
 #define PO_EHIP -2     /* HIP runtime error */
 #define PO_EDEVICE -3  /* device is not gfx950 */
 
-#define PO_ABI_VERSION 15
+#define PO_ABI_VERSION 16
 #define PO_AMAX_SUB 64  /* sub-slots per max|x| slot (see po_conv_desc) */
 
 int po_abi_version(void);
@@ -376,7 +376,7 @@ typedef struct po_conv_desc {
    * (staging 0/1). */
   int mrows;
   /* Optional fused k=2 stride-2 max pool of a plain forward conv (y_out NULL,
-   * full even grid, no split-K; generic tiles, or Winograd tiles 61/66
+   * full even grid, no split-K; generic tiles, or Winograd tiles 61/66/67
    * without gbox -- their 2x2 output tiles are the windows): pool_y [B,Hout/2,Wout/2,Cout_p]
    * and pool_argmax (int8, same shape) as po_maxpool2_fwd writes them, the
    * argmax bytes of a leaky conv also carrying its LeakyReLU slope (bit 3
@@ -386,7 +386,7 @@ typedef struct po_conv_desc {
   int8_t* pool_argmax;
 } po_conv_desc;
 
-#define PO_CONV_NTILES 66
+#define PO_CONV_NTILES 67
 /* Tile `t` (1-based): block rows BM (output pixels), block columns BN (output
  * channels), k-step BK (input channels).  Tiles 1..10 stage operands through
  * registers, 11..20 are the same shapes staged by LDS-DMA, 21..28 are
@@ -400,9 +400,11 @@ typedef struct po_conv_desc {
  * exact-fp32 Winograd F(2x2,3x3) kernels (61: 64 2x2-tiles x 32 channels;
  * 62..66: 32 tiles x 64 channels with LDS-DMA input -- 62/63 4 or 8 waves,
  * 64 scheduled, 65 with the vector epilogue, 66 as 65 in 4-wave workgroups
- * with 64 KB of LDS, two per CU, bit-identical to 65; 16 input channels per
- * k-step) for stride-1 3x3 convs and their input gradients on full maps,
- * without split-K except on 66 (needs Wwino; 62..66 need N % 64 == 0).  A
+ * with 64 KB of LDS, two per CU, bit-identical to 65; 67: 64 tiles x 64
+ * channels per 512-thread workgroup, register-staged input and a pipelined
+ * k-loop, bit-identical to 65/66; 16 input channels per k-step) for stride-1
+ * 3x3 convs and their input gradients on full maps, without split-K except on
+ * 66/67 (needs Wwino; 62..67 need N % 64 == 0).  A
  * tile that does not apply to a launch makes po_conv
  * return PO_EINVAL.  Returns PO_EINVAL for a bad index. */
 int po_conv_tile_info(int t, int* bm, int* bn, int* bk, int* prec);

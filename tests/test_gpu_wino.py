@@ -15,8 +15,8 @@ from conftest import pkg_mod
 
 pytestmark = pytest.mark.gpu
 DEV = torch.device("cuda", 0)
-WINO_TILES = [61, 62, 63, 64, 65, 66]   # 64 tiles x 32 ch; 32 tiles x 64 ch (LDS-DMA input, N % 64 == 0), 4 / 8 waves,
-                                        # 8 scheduled, 4 waves in 64 KB of LDS
+WINO_TILES = [61, 62, 63, 64, 65, 66, 67]   # 64 tiles x 32 ch; 32 tiles x 64 ch (LDS-DMA input, N % 64 == 0), 4 / 8
+                                            # waves, 8 scheduled, 4 waves in 64 KB of LDS; 64 tiles x 64 ch pipelined
 
 
 def _rel(a, b):
@@ -54,7 +54,7 @@ def _setup(B, H, Cin, Cout, flip, seed):
                                                (4, 19, 512, 256, True), (1, 76, 128, 64, False),
                                                (2, 9, 16, 32, False)])
 def test_wino_matches_float64_conv(B, H, Cin, Cout, flip, WINO):
-    if WINO in (62, 63, 64, 65, 66) and Cout % 64:
+    if WINO in (62, 63, 64, 65, 66, 67) and Cout % 64:
         pytest.skip("tiles 62/63 take N % 64 == 0")
     nat = pkg_mod("_native")
     x, w, bias, wd, U = _setup(B, H, Cin, Cout, flip, seed=H * Cin + flip)
@@ -176,7 +176,7 @@ def test_wino_refuses_what_it_cannot_run(WINO):
     assert call(d) == 0
     ws = torch.empty(4 * B * H * H * Cout, device=DEV)
     d.ksplit, d.workspace = 2, ws.data_ptr()
-    assert (call(d) == 0) == (WINO == 66)                           # split-K: tile 66 only
+    assert (call(d) == 0) == (WINO in (66, 67))                     # split-K: tiles 66 and 67 only
     d.ksplit = 3
     assert call(d) != 0                                             # more slices than 16-channel steps
     d = _desc(nat, B, H, Cin, Cout, WINO)
@@ -186,13 +186,15 @@ def test_wino_refuses_what_it_cannot_run(WINO):
     assert call(d) != 0                                             # stride 2
 
 
+@pytest.mark.parametrize("tile", [66, 67])
 @pytest.mark.parametrize("mode", ["fwd_bits", "fwd_shortcut", "dgrad_acc_bits", "dgrad_dual"])
-@pytest.mark.parametrize("B,H,Cin,Cout", [(2, 11, 64, 128), (3, 38, 256, 512), (1, 19, 512, 64)])
-def test_wino_tile66_bit_identical_to_65(mode, B, H, Cin, Cout):
-    """Tile 66 (4-wave workgroups in 64 KB of LDS, two per CU) runs tile 65's
-    transforms, MFMA order and epilogue arithmetic: the same bits in every
-    epilogue combination the training plan uses (sign bits and max|x| slots
-    included), ragged tile counts."""
+@pytest.mark.parametrize("B,H,Cin,Cout", [(2, 11, 64, 128), (3, 38, 256, 512), (1, 19, 512, 64), (2, 7, 16, 64)])
+def test_wino_tile66_bit_identical_to_65(mode, B, H, Cin, Cout, tile):
+    """Tile 66 (4-wave workgroups in 64 KB of LDS, two per CU) and tile 67
+    (64 tiles x 64 channels, register-staged input, pipelined k-loop) run tile
+    65's transforms, per-accumulator MFMA order and epilogue arithmetic: the
+    same bits in every epilogue combination the training plan uses (sign bits
+    and max|x| slots included), ragged tile counts, a single k-step."""
     nat = pkg_mod("_native")
     flip = mode.startswith("dgrad")
     x, w, bias, wd, U = _setup(B, H, Cin, Cout, flip, seed=H + Cin)
@@ -203,8 +205,8 @@ def test_wino_tile66_bit_identical_to_65(mode, B, H, Cin, Cout):
     mbits = torch.randint(-2 ** 31, 2 ** 31 - 1, (B, H, H, Cout // 32), generator=gen, dtype=torch.int32).to(DEV)
     m2bits = torch.randint(-2 ** 31, 2 ** 31 - 1, (B, H, H, Cout // 32), generator=gen, dtype=torch.int32).to(DEV)
     runs = []
-    for tile in (66, 65):
-        d = _desc(nat, B, H, Cin, Cout, tile, flip)
+    for t_ in (tile, 65):
+        d = _desc(nat, B, H, Cin, Cout, t_, flip)
         d.Wwino = U.data_ptr()
         y = prev.clone()
         ssum = torch.full_like(prev, float("nan"))
@@ -236,7 +238,7 @@ def test_wino_tile66_bit_identical_to_65(mode, B, H, Cin, Cout):
 
 
 
-@pytest.mark.parametrize("tile", [61, 66])
+@pytest.mark.parametrize("tile", [61, 66, 67])
 @pytest.mark.parametrize("act", [0, 1])
 @pytest.mark.parametrize("B,H,Cin,Cout", [(2, 12, 64, 128), (3, 26, 128, 256), (2, 104, 32, 64), (2, 52, 16, 32)])
 def test_wino_fused_pool(act, B, H, Cin, Cout, tile):
@@ -245,8 +247,8 @@ def test_wino_fused_pool(act, B, H, Cin, Cout, tile):
     bit-identical to pooling the tile's own unpooled output by
     po_maxpool2_fwd's rule (first position on ties), max|x| slot of the pooled
     map; tile 65 refuses a pooled launch."""
-    if tile == 66 and Cout % 64:
-        pytest.skip("tile 66 takes N % 64 == 0")
+    if tile in (66, 67) and Cout % 64:
+        pytest.skip("tiles 66/67 take N % 64 == 0")
     nat = pkg_mod("_native")
     x, w, bias, wd, U = _setup(B, H, Cin, Cout, False, seed=H + Cout)
     xd = x.permute(0, 2, 3, 1).contiguous().to(DEV)
@@ -282,10 +284,11 @@ def test_wino_fused_pool(act, B, H, Cin, Cout, tile):
                               None, nat.stream()) != 0
 
 
+@pytest.mark.parametrize("tile", [66, 67])
 @pytest.mark.parametrize("ks", [2, 3])
 @pytest.mark.parametrize("boxed", [False, True])
 @pytest.mark.parametrize("mode", ["fwd_bits", "fwd_shortcut", "dgrad_acc_bits", "dgrad_dual"])
-def test_wino_tile66_split_k(mode, boxed, ks):
+def test_wino_tile66_split_k(mode, boxed, ks, tile):
     """Tile 66 with input-channel slices (blockIdx.y) writing raw partial
     sums at conv_reduce_k's GEMM rows (the box's compact rows with gbox), the
     reduction applying the epilogue: the unsplit launch's values within the
@@ -305,7 +308,7 @@ def test_wino_tile66_split_k(mode, boxed, ks):
     ws = torch.full((ks * B * H * H * Cout,), float("nan"), device=DEV)
     runs = []
     for split in (1, ks):
-        d = _desc(nat, B, H, Cin, Cout, 66, flip)
+        d = _desc(nat, B, H, Cin, Cout, tile, flip)
         d.Wwino = U.data_ptr()
         if split > 1:
             d.ksplit, d.workspace = split, ws.data_ptr()
