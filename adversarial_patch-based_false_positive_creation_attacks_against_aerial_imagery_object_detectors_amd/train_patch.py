@@ -348,8 +348,8 @@ class PatchTrainer(object):
                 # GradScaler): the patch stays at its last finite value until check_flags
                 # raises at the end of the epoch, instead of being corrupted by the NaN
                 if self._found_inf is None or self._found_inf.device != g.device:
-                    self._found_inf = torch.zeros(1, device=g.device)
-                self._found_inf.copy_(self.flags & FLAG_NONFINITE).clamp_(max=1.0)
+                    self._found_inf = torch.zeros((), device=g.device)     # 0-dim, as Adam's step counters
+                self._found_inf.copy_(self.flags[0] & FLAG_NONFINITE).clamp_(max=1.0)
                 optimizer.found_inf = self._found_inf
         optimizer.step()
         optimizer.zero_grad()

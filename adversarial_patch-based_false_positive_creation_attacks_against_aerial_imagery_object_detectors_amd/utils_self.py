@@ -6,6 +6,7 @@ metric block as one function.
 * per_img_conf_sum        utils_self.py:180-196  sum of objectness (column 5)
 * instances_per_class_cal utils_self.py:230-257  instances per class id (last column)
 * patch_MSE_calsulator    utils_self.py:205-220  MSE of two saved patches
+* load_image_file         utils_self.py:151-166  PIL open + EXIF transpose + RGB
 * creation_metrics        test_patch_DOTA_metrics.py:301-371: M1 (instances
   created per image at conf 0.4 and 0.01), M2 (objectness created per new
   instance), M4 (instance gap per class)
@@ -16,6 +17,7 @@ Label files are the evaluation's ``cx cy w h det_conf cls_conf cls_id`` lines
 import math
 import os
 
+from .eval_patch import load_image_file  # noqa: F401  (utils_self.load_image_file)
 from .train_patch import patch_mse
 
 
