@@ -169,21 +169,12 @@ __global__ __launch_bounds__(256) void conv_k(const ConvArgs a) {
   // chunk re-read the same (shifted) pixels while they are still in L1/L2
   int tap = ks0 % a.ntaps, c0 = (ks0 / a.ntaps) * BK;
   int th = tap / a.tkw, tw = tap - th * a.tkw;
-  if constexpr (GL) {
-    gload_lds(0, tap, a.dh0 + th * a.sdh, a.dw0 + tw * a.sdw, c0);
-  } else {
-    gload(tap, a.dh0 + th * a.sdh, a.dw0 + tw * a.sdw, c0);
-    sstore(0);
-  }
-  __syncthreads();
   const int arow = wm * TM * 32 + (lane & 31);
   const int brow = wn * TN * 32 + (lane & 31);
   const int h = lane >> 5;
-  for (int ks = 0; ks < nks; ++ks) {
-    const int buf = ks & 1;
-    const bool more = ks + 1 < nks;
-    const float* Ab = As + buf * BM * BK;
-    const float* Bb = Bs + buf * BN * BK;
+  // the MFMAs of one k-step from LDS buffer (Ab, Bb); `load` runs after the
+  // first fragment group's reads
+  auto kstep = [&](const float* Ab, const float* Bb, auto&& load) {
 #pragma unroll
     for (int g = 0; g < BK / 8; ++g) {
       float4 af[TM], bf[TN];
@@ -197,24 +188,7 @@ __global__ __launch_bounds__(256) void conv_k(const ConvArgs a) {
         const int row = brow + j * 32;
         bf[j] = *reinterpret_cast<const float4*>(&Bb[row * BK + swz(row, 2 * g + h)]);
       }
-#ifdef PO_ABLATE_NOLOAD
-      if (false) {      // ablation build (tools/): k-steps without staging loads
-#else
-      if (g == 0 && more) {
-#endif
-        // issue the next k-step's staging loads behind this group's fragment reads
-        if (++tap == a.ntaps) {
-          tap = th = tw = 0;
-          c0 += BK;
-        } else if (++tw == a.tkw) {
-          tw = 0;
-          ++th;
-        }
-        if constexpr (GL)
-          gload_lds(buf ^ 1, tap, a.dh0 + th * a.sdh, a.dw0 + tw * a.sdw, c0);
-        else
-          gload(tap, a.dh0 + th * a.sdh, a.dw0 + tw * a.sdw, c0);
-      }
+      if (g == 0) load();
 #pragma unroll
       for (int i = 0; i < TM; ++i)
 #pragma unroll
@@ -225,12 +199,83 @@ __global__ __launch_bounds__(256) void conv_k(const ConvArgs a) {
           acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(af[i].w, bf[j].w, acc[i][j], 0, 0, 0);
         }
     }
-#ifndef PO_ABLATE_NOLOAD
-    if constexpr (!GL) {
-      if (more) sstore(buf ^ 1);
+  };
+  auto advance = [&]() {
+    if (++tap == a.ntaps) {
+      tap = th = tw = 0;
+      c0 += BK;
+    } else if (++tw == a.tkw) {
+      tw = 0;
+      ++th;
     }
-#endif
+  };
+  if constexpr (GL) {
+    gload_lds(0, tap, a.dh0 + th * a.sdh, a.dw0 + tw * a.sdw, c0);
     __syncthreads();
+    for (int ks = 0; ks < nks; ++ks) {
+      const int buf = ks & 1;
+      const bool more = ks + 1 < nks;
+      kstep(As + buf * BM * BK, Bs + buf * BN * BK, [&]() {
+#ifndef PO_ABLATE_NOLOAD
+        if (more) {
+          // issue the next k-step's staging loads behind this group's fragment reads
+          advance();
+          gload_lds(buf ^ 1, tap, a.dh0 + th * a.sdh, a.dw0 + tw * a.sdw, c0);
+        }
+#endif
+      });
+      __syncthreads();
+    }
+  } else {
+    // Register staging with TWO k-steps of loads in flight: set p of the staging
+    // registers holds the k-step of parity p, the loads of step ks+2 are issued
+    // during step ks (behind its first fragment reads) and step ks+1 goes to
+    // LDS at its end, so a load has a whole k-step of MFMAs more to land than
+    // with one set.  The loop is unrolled by two (compile-time set index) and
+    // branch-free (loads of steps past the slice read nothing: out-of-range
+    // buffer offsets), so the waits stay partial (vmcnt of one set).
+    float4 ra2[2][AL], rb2[2][BL];
+    int issued = 0;                              // k-steps of this slice whose loads are issued
+    auto gload2 = [&](float4 (&ra_)[AL], float4 (&rb_)[BL]) {
+      const uint32_t oob = issued < nks ? 0u : kOOB;
+      const uint32_t cb = (uint32_t)c0 * 4u;
+      const int dh = a.dh0 + th * a.sdh, dw = a.dw0 + tw * a.sdw;
+#pragma unroll
+      for (int r = 0; r < AL; ++r)
+        ra_[r] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(in_rs, a_offset(r, dh, dw, cb) | oob, 0, 0));
+      const uint32_t tb = (uint32_t)tap * pix_bytes + cb;
+#pragma unroll
+      for (int r = 0; r < BL; ++r)
+        rb_[r] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(w_rs, (b_off[r] + tb) | oob, 0, 0));
+      ++issued;
+      advance();
+    };
+    auto sstore2 = [&](int buf, const float4 (&ra_)[AL], const float4 (&rb_)[BL]) {
+#pragma unroll
+      for (int r = 0; r < AL; ++r) {
+        const int row = rth + RPP * r;
+        if (row < BM) *reinterpret_cast<float4*>(&As[(buf * BM + row) * BK + swz(row, cth)]) = ra_[r];
+      }
+#pragma unroll
+      for (int r = 0; r < BL; ++r) {
+        const int row = rth + RPP * r;
+        if (row < BN) *reinterpret_cast<float4*>(&Bs[(buf * BN + row) * BK + swz(row, cth)]) = rb_[r];
+      }
+    };
+    gload2(ra2[0], rb2[0]);
+    gload2(ra2[1], rb2[1]);
+    sstore2(0, ra2[0], rb2[0]);
+    __syncthreads();
+    int ks = 0;
+    for (; ks + 1 < nks; ks += 2) {
+      kstep(As, Bs, [&]() { gload2(ra2[0], rb2[0]); });
+      sstore2(1, ra2[1], rb2[1]);
+      __syncthreads();
+      kstep(As + BM * BK, Bs + BN * BK, [&]() { gload2(ra2[1], rb2[1]); });
+      sstore2(0, ra2[0], rb2[0]);
+      __syncthreads();
+    }
+    if (ks < nks) kstep(As, Bs, [&]() {});
   }
 
   if (a.ksplit > 1) {

@@ -1,20 +1,24 @@
 #!/bin/bash
-# PMC of Winograd tiles 67 vs 66 at a long-K shape; the new train/eval tests;
-# re-tune (boxed + Winograd entries) and bench.
+# PMC of Winograd tiles 67 vs 66 at a long-K shape; the conv / train / eval
+# tests; direct conv_k old vs new (two-step register prefetch); re-tune
+# (boxed + Winograd entries) and bench.
 cd "$GRAFT_REPO_ROOT"
 OUT=gpurun_out/r03d
 mkdir -p $OUT/tiles
+timeout -k 10 900 python -u -m pytest -x -q --timeout 300 --timeout-method thread tests/test_gpu_darknet.py \
+    tests/test_gpu_cones.py tests/test_gpu_first_conv.py tests/test_gpu_eval_folder.py \
+    "tests/test_gpu_train.py::test_nonfinite_guard_and_flags" tests/test_gpu_train.py::test_empty_shard_adds_only_its_patch_terms \
+    tests/test_gpu_placement.py > $OUT/tests.log 2>&1
+rc=$?; echo "pytest rc=$rc" >> $OUT/tests.log; tail -5 $OUT/tests.log
+if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then exit $rc; fi
+OUT=$OUT/direct_cmp.txt bash tools/direct_cmp.sh || exit 1
 for t in 67 66; do
   bash tools/pmc_conv.sh $OUT/pmc_w$t "16 38 256 512 3 1 30" $t || exit 1
   python3 tools/pmc_read.py $OUT/pmc_w$t > $OUT/pmc_w$t/summary.txt
 done
 paste $OUT/pmc_w67/summary.txt $OUT/pmc_w66/summary.txt | awk '{print $1, $2, $5}' > $OUT/pmc_67_vs_66.txt
 cat $OUT/pmc_w67/plain.txt $OUT/pmc_w66/plain.txt >> $OUT/pmc_67_vs_66.txt
-timeout -k 10 600 python -u -m pytest -x -v --timeout 300 --timeout-method thread tests/test_gpu_eval_folder.py \
-    "tests/test_gpu_train.py::test_nonfinite_guard_and_flags" tests/test_gpu_train.py::test_empty_shard_adds_only_its_patch_terms \
-    tests/test_gpu_placement.py > $OUT/tests.log 2>&1
-rc=$?; echo "pytest rc=$rc" >> $OUT/tests.log
-if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then exit $rc; fi
+[ $rc -eq 0 ] || exit 1
 T=adversarial_patch-based_false_positive_creation_attacks_against_aerial_imagery_object_detectors_amd/tiles
 python tools/retune_boxed.py --wino $T/conv_tiles_yolov3_b16.json $T/conv_tiles_tiny_b256.json > $OUT/retune.log
 timeout -k 10 600 python -u bench.py --no-cpu-baseline > $OUT/bench_tune.json 2> $OUT/bench_tune.err || exit $?
