@@ -102,21 +102,10 @@ __global__ __launch_bounds__(256) void conv_k(const ConvArgs a) {
     b_off[r] = ok ? (uint32_t)(n0 + row) * wrow_bytes + a_chunk(row) * 16u : kOOB;
   }
 
-  float4 ra[GL ? 1 : AL], rb[GL ? 1 : BL];
   auto a_offset = [&](int r, int dh, int dw, uint32_t cb) {
     const int hi = a_hi[r] + dh, wi = a_wi[r] + dw;
     const bool ok = (unsigned)hi < (unsigned)a.Hin && (unsigned)wi < (unsigned)a.Win;
     return ok ? a_off[r] + ((uint32_t)hi * a.Win + wi) * pix_bytes + cb : kOOB;
-  };
-  auto gload = [&](int tap, int dh, int dw, int c0) {
-    const uint32_t cb = (uint32_t)c0 * 4u;
-#pragma unroll
-    for (int r = 0; r < AL; ++r)
-      ra[r] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(in_rs, a_offset(r, dh, dw, cb), 0, 0));
-    const uint32_t tb = (uint32_t)tap * pix_bytes + cb;
-#pragma unroll
-    for (int r = 0; r < BL; ++r)
-      rb[r] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(w_rs, b_off[r] + tb, 0, 0));
   };
   auto gload_lds = [&](int buf, int tap, int dh, int dw, int c0) {
     const uint32_t cb = (uint32_t)c0 * 4u;
@@ -135,21 +124,6 @@ __global__ __launch_bounds__(256) void conv_k(const ConvArgs a) {
     }
   };
   auto swz = [](int row, int chunk) { return (chunk ^ ((row >> SW) & (CPR - 1))) * 4; };
-  auto sstore = [&](int buf) {
-#pragma unroll
-    for (int r = 0; r < AL; ++r) {
-      const int row = rth + RPP * r;
-      if (row < BM)
-        *reinterpret_cast<float4*>(&As[(buf * BM + row) * BK + swz(row, cth)]) = ra[r];
-    }
-#pragma unroll
-    for (int r = 0; r < BL; ++r) {
-      const int row = rth + RPP * r;
-      if (row < BN)
-        *reinterpret_cast<float4*>(&Bs[(buf * BN + row) * BK + swz(row, cth)]) = rb[r];
-    }
-  };
-
   floatx16 acc[TM][TN];
 #pragma unroll
   for (int i = 0; i < TM; ++i)

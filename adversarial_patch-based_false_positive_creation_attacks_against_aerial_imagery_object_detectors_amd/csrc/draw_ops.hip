@@ -16,33 +16,14 @@
 // angle, ux} and 0xFFFFFFFE {uy}.  oracle/draws_ref.py restates it in numpy.
 #pragma clang fp contract(off)
 #include "common.h"
+#include "philox.h"
 
 namespace {
 
-struct u4 {
-  uint32_t x, y, z, w;
-};
-
-__device__ __forceinline__ u4 philox4x32_10(u4 c, uint32_t k0, uint32_t k1) {
-  constexpr uint32_t M0 = 0xD2511F53u, M1 = 0xCD9E8D57u, W0 = 0x9E3779B9u, W1 = 0xBB67AE85u;
-#pragma unroll
-  for (int r = 0; r < 10; ++r) {
-    const uint32_t lo0 = M0 * c.x, hi0 = __umulhi(M0, c.x);
-    const uint32_t lo1 = M1 * c.z, hi1 = __umulhi(M1, c.z);
-    c = u4{hi1 ^ c.y ^ k0, lo1, hi0 ^ c.w ^ k1, lo0};
-    k0 += W0;
-    k1 += W1;
-  }
-  return c;
-}
-
-__device__ __forceinline__ float unif(uint32_t x) { return (float)(x >> 8) * 0x1p-24f; }
-// from + u * span for fp32 u, span, from: the product is exact in float64
-// (24 + 24 bits), so the float64 sum is rounded once and then to fp32 — the
-// same bits whether or not the compiler fuses the multiply-add
-__device__ __forceinline__ float affine(float u, float span, float from) {
-  return (float)((double)u * (double)span + (double)from);
-}
+using po::u4;
+using po::philox4x32_10;
+__device__ __forceinline__ float unif(uint32_t x) { return po::philox_unif(x); }
+__device__ __forceinline__ float affine(float u, float span, float from) { return po::philox_affine(u, span, from); }
 
 constexpr float kPi = 3.14159265358979323846f;
 

@@ -7,6 +7,7 @@
 // masks route gradients like the reference.
 #pragma clang fp contract(off)
 #include "common.h"
+#include "philox.h"
 #include "warp_geom.h"
 #include <math.h>
 #include <string.h>
@@ -336,7 +337,29 @@ extern "C" int po_patch_params(const float* lab, int B, int L, const float* angl
 namespace {
 struct WarpGeom {
   int S, P, padL, padT;
+  // noise key (po_warp_*_keyed): with no noise tensor the kernels regenerate
+  // element e of image b as po_draws does (philox_noise, global image nb0 + b)
+  uint32_t nk0, nk1, nc_lo, nc_hi;
+  int nb0;
 };
+
+// The transformer noise of one image: the explicit tensor [3][P][P], or (nz
+// NULL) regenerated in-kernel from the po_draws key — bit-identical values,
+// without the B*3*P*P*4-byte noise tensor being written and gathered.
+struct NoiseSrc {
+  const float* nz;
+  uint32_t k0, k1, c_lo, c_hi, gb;
+  __device__ __forceinline__ float at(size_t e) const {
+    return nz ? nz[e] : po::philox_noise(k0, k1, c_lo, c_hi, gb, (uint32_t)e);
+  }
+};
+__device__ __forceinline__ NoiseSrc noise_src(const float* noise, const WarpGeom& g, int b) {
+  NoiseSrc ns;
+  ns.nz = noise ? noise + (size_t)b * 3 * g.P * g.P : nullptr;
+  ns.k0 = g.nk0; ns.k1 = g.nk1; ns.c_lo = g.nc_lo; ns.c_hi = g.nc_hi;
+  ns.gb = (uint32_t)(g.nb0 + b);
+  return ns;
+}
 
 // Source coordinate (ix: column, iy: row) in the padded patch of output pixel
 // (i, j): affine_grid (align_corners=False) + grid_sampler_unnormalize folded
@@ -359,10 +382,10 @@ __device__ __forceinline__ void bilinear(double ix, double iy, int& x0, int& y0,
   w[3] = (float)(ex * ey);
 }
 
-__device__ __forceinline__ float aug_value(const float* __restrict__ mp, const float* __restrict__ nz,
+__device__ __forceinline__ float aug_value(const float* __restrict__ mp, const NoiseSrc& ns,
                                            float contrast, float bright, int ch, int pr, int pc, int P) {
   const size_t o = ((size_t)ch * P + pr) * P + pc;
-  float v = mp[o] * contrast + bright + nz[o] * 0.1f;    // load_data.py:566-571
+  float v = mp[o] * contrast + bright + ns.at(o) * 0.1f;    // load_data.py:566-571
   return fminf(fmaxf(v, 0.f), 1.f);                      // load_data.py:574
 }
 
@@ -370,7 +393,7 @@ __device__ __forceinline__ float aug_value(const float* __restrict__ mp, const f
 // if no neighbour lies inside the padded patch region (output exactly 0).
 template <bool AUG = true>
 __device__ __forceinline__ bool warp_pixel(const double* af, const WarpGeom& g, const float* mp,
-                                           const float* nz, float contrast, float bright, int i, int j,
+                                           const NoiseSrc& nz, float contrast, float bright, int i, int j,
                                            float adv[3], float& msk, bool raw_in_range[3]) {
   double ix, iy;
   sample_coord(af, i, j, ix, iy);
@@ -425,7 +448,7 @@ __global__ __launch_bounds__(256) void warp_fwd_k(const float* __restrict__ img,
   const size_t o = (size_t)b * 3 * plane + (size_t)i * g.S + j;
   float adv[3], msk;
   bool rng[3];
-  const bool hit = warp_pixel(affine + 6 * b, g, mp, noise + (size_t)b * 3 * g.P * g.P, contrast[b],
+  const bool hit = warp_pixel(affine + 6 * b, g, mp, noise_src(noise, g, b), contrast[b],
                               bright[b], i, j, adv, msk, rng);
 #pragma unroll
   for (int ch = 0; ch < 3; ++ch) {
@@ -453,7 +476,7 @@ __global__ __launch_bounds__(256) void warp_fwd4_k(const float* __restrict__ img
   const size_t plane = (size_t)g.S * g.S;
   const size_t o = (size_t)b * 3 * plane + (size_t)i * g.S + j0;
   const double* th = affine + 6 * b;
-  const float* nz = noise + (size_t)b * 3 * g.P * g.P;
+  const NoiseSrc nz = noise_src(noise, g, b);
   const float cb = contrast[b], bb = bright[b];
   float v[3][4];
 #pragma unroll
@@ -492,7 +515,7 @@ __global__ __launch_bounds__(256) void warp_bwd_a_k(const float* __restrict__ d_
   const size_t o = (size_t)b * 3 * plane + (size_t)i * g.S + j;
   float adv[3], msk;
   bool rng[3];
-  if (!warp_pixel(affine + 6 * b, g, mp, noise + (size_t)b * 3 * g.P * g.P, contrast[b], bright[b],
+  if (!warp_pixel(affine + 6 * b, g, mp, noise_src(noise, g, b), contrast[b], bright[b],
                   i, j, adv, msk, rng))
     return;   // never read by phase B
 #pragma unroll
@@ -526,7 +549,7 @@ __global__ __launch_bounds__(256) void warp_bwd_a4_k(const float* __restrict__ d
   const size_t plane = (size_t)g.S * g.S;
   const size_t o = (size_t)b * 3 * plane + (size_t)i * g.S + j0;
   const double* th = affine + 6 * b;
-  const float* nz = noise + (size_t)b * 3 * g.P * g.P;
+  const NoiseSrc nz = noise_src(noise, g, b);
   const float cb = contrast[b], bb = bright[b];
   float adv[4][3], msk[4];
   bool rng[4][3], hit[4];
@@ -629,7 +652,7 @@ __global__ __launch_bounds__(256) void warp_bwd_b_k(const float* __restrict__ gf
       i0 = (int)fmax(0.0, floor(ilo) - 1.0); i1 = (int)fmin(hiS, ceil(ihi) + 1.0);
     }
     const float cb = contrast[b], bb = bright[b];
-    const float* nz = noise + (size_t)b * 3 * g.P * g.P;
+    const NoiseSrc nz = noise_src(noise, g, b);
     float a0 = 0.f, a1 = 0.f, a2 = 0.f;
     const float* gb = gfac + (size_t)b * 3 * plane;
     for (int i = i0; i <= i1; ++i)
@@ -654,7 +677,7 @@ __global__ __launch_bounds__(256) void warp_bwd_b_k(const float* __restrict__ gf
 #pragma unroll
     for (int ch = 0; ch < 3; ++ch) {
       const size_t po_ = ((size_t)ch * g.P + pr) * g.P + pc;
-      const float pre = mp[po_] * cb + bb + nz[po_] * 0.1f;
+      const float pre = mp[po_] * cb + bb + nz.at(po_) * 0.1f;
       dd[ch] = (pre >= 0.f && pre <= 1.f) ? av[ch] * cb : 0.f;
     }
     d0 += dd[0]; d1 += dd[1]; d2 += dd[2];
@@ -699,7 +722,7 @@ __global__ __launch_bounds__(256) void warp_multi_k(const float* __restrict__ im
     if (j < r[0] || j >= r[2] || i < r[1] || i >= r[3]) continue;
     float adv[3], msk;
     bool rng[3];
-    const float* nz = AUG ? noise + (size_t)t * 3 * g.P * g.P : nullptr;
+    const NoiseSrc nz = noise_src(AUG ? noise : nullptr, g, t);     // !AUG: never read
     if (!warp_pixel<AUG>(affine + 6 * t, g, mp, nz, AUG ? contrast[t] : 1.f, AUG ? bright[t] : 0.f, i, j, adv,
                          msk, rng))
       continue;
@@ -714,14 +737,34 @@ __global__ __launch_bounds__(256) void warp_multi_k(const float* __restrict__ im
   for (int ch = 0; ch < 3; ++ch) out[o + ch * plane] = set[ch] ? v[ch] : img[o + ch * plane];
 }
 
-WarpGeom make_geom(int S, int P) {
+WarpGeom make_geom(int S, int P, uint64_t seed = 0, uint64_t counter = 0, int b0 = 0) {
   WarpGeom g;
   g.S = S;
   g.P = P;
+  g.nk0 = (uint32_t)seed;
+  g.nk1 = (uint32_t)(seed >> 32);
+  g.nc_lo = (uint32_t)counter;
+  g.nc_hi = (uint32_t)(counter >> 32);
+  g.nb0 = b0;
   const double pad = (S - P) / 2.0;      // load_data.py:534
   g.padL = (int)(pad + 0.5);            // ConstantPad2d((int(pad+.5), int(pad), int(pad+.5), int(pad)))
   g.padT = (int)(pad + 0.5);
   return g;
+}
+}  // namespace
+
+namespace {
+int warp_fwd(const float* img, const float* patch_mp, const float* noise, const float* contrast, const float* bright,
+             const double* affine, int B, int S, int mode, float* out, const WarpGeom& g, po_stream_t s) {
+  if (S % 4 == 0 && ((uintptr_t)img | (uintptr_t)out) % 16 == 0 && !getenv("PO_WARP_V1")) {
+    hipLaunchKernelGGL(warp_fwd4_k, dim3(po::ceil_div(S * (S / 4), 256), B), dim3(256), 0, po::stream_of(s), img,
+                       patch_mp, noise, contrast, bright, affine, g, mode, out);
+    return po::check_launch("po_warp_fwd");
+  }
+  dim3 grid(po::ceil_div(S, 256), S, B);
+  hipLaunchKernelGGL(warp_fwd_k, grid, dim3(256), 0, po::stream_of(s), img, patch_mp, noise, contrast,
+                     bright, affine, g, mode, out);
+  return po::check_launch("po_warp_fwd");
 }
 }  // namespace
 
@@ -731,25 +774,24 @@ extern "C" int po_warp_fwd(const float* img, const float* patch_mp, const float*
   PO_REQUIRE(patch_mp && noise && contrast && bright && affine && out, "po_warp_fwd: null pointer");
   PO_REQUIRE(mode == 0 || (mode == 1 && img), "po_warp_fwd: mode must be 0 or 1 (1 needs img)");
   PO_REQUIRE(B > 0 && S > 1 && P > 0 && P <= S, "po_warp_fwd: bad shape B=%d S=%d P=%d", B, S, P);
-  if (S % 4 == 0 && ((uintptr_t)img | (uintptr_t)out) % 16 == 0 && !getenv("PO_WARP_V1")) {
-    hipLaunchKernelGGL(warp_fwd4_k, dim3(po::ceil_div(S * (S / 4), 256), B), dim3(256), 0, po::stream_of(s), img,
-                       patch_mp, noise, contrast, bright, affine, make_geom(S, P), mode, out);
-    return po::check_launch("po_warp_fwd");
-  }
-  dim3 grid(po::ceil_div(S, 256), S, B);
-  hipLaunchKernelGGL(warp_fwd_k, grid, dim3(256), 0, po::stream_of(s), img, patch_mp, noise, contrast,
-                     bright, affine, make_geom(S, P), mode, out);
-  return po::check_launch("po_warp_fwd");
+  return warp_fwd(img, patch_mp, noise, contrast, bright, affine, B, S, mode, out, make_geom(S, P), s);
 }
 
-extern "C" int po_warp_bwd(const float* d_out, const float* patch_mp, const float* noise,
-                           const float* contrast, const float* bright, const double* affine, int B,
-                           int S, int P, int mode, float* work, float* d_patch_mp, po_stream_t s) {
-  PO_REQUIRE(d_out && patch_mp && noise && contrast && bright && affine && work && d_patch_mp,
-             "po_warp_bwd: null pointer");
-  PO_REQUIRE(mode == 0 || mode == 1, "po_warp_bwd: mode must be 0 or 1");
-  PO_REQUIRE(B > 0 && S > 1 && P > 0 && P <= S, "po_warp_bwd: bad shape");
-  WarpGeom g = make_geom(S, P);
+extern "C" int po_warp_fwd_keyed(const float* img, const float* patch_mp, uint64_t seed, uint64_t counter, int b0,
+                                 const float* contrast, const float* bright, const double* affine, int B, int S, int P,
+                                 int mode, float* out, po_stream_t s) {
+  PO_REQUIRE(patch_mp && contrast && bright && affine && out, "po_warp_fwd_keyed: null pointer");
+  PO_REQUIRE(mode == 0 || (mode == 1 && img), "po_warp_fwd_keyed: mode must be 0 or 1 (1 needs img)");
+  PO_REQUIRE(B > 0 && S > 1 && P > 0 && P <= S && b0 >= 0, "po_warp_fwd_keyed: bad shape B=%d S=%d P=%d", B, S, P);
+  PO_REQUIRE(3LL * P * P < (1LL << 31), "po_warp_fwd_keyed: patch too large");
+  return warp_fwd(img, patch_mp, nullptr, contrast, bright, affine, B, S, mode, out, make_geom(S, P, seed, counter, b0),
+                  s);
+}
+
+namespace {
+int warp_bwd(const float* d_out, const float* patch_mp, const float* noise, const float* contrast, const float* bright,
+             const double* affine, int B, int S, int P, int mode, float* work, float* d_patch_mp, const WarpGeom& g,
+             po_stream_t s) {
   const bool quad = S % 4 == 0 && ((uintptr_t)d_out | (uintptr_t)work) % 16 == 0 && work != d_out &&
                     !getenv("PO_WARP_V1");
   if (quad) {
@@ -770,6 +812,30 @@ extern "C" int po_warp_bwd(const float* d_out, const float* patch_mp, const floa
     hipLaunchKernelGGL(warp_bwd_b_k<1>, gridb, dim3(256), 0, po::stream_of(s), work, patch_mp, noise, contrast,
                        bright, affine, g, B, d_patch_mp);
   return po::check_launch("po_warp_bwd(b)");
+}
+}  // namespace
+
+extern "C" int po_warp_bwd(const float* d_out, const float* patch_mp, const float* noise,
+                           const float* contrast, const float* bright, const double* affine, int B,
+                           int S, int P, int mode, float* work, float* d_patch_mp, po_stream_t s) {
+  PO_REQUIRE(d_out && patch_mp && noise && contrast && bright && affine && work && d_patch_mp,
+             "po_warp_bwd: null pointer");
+  PO_REQUIRE(mode == 0 || mode == 1, "po_warp_bwd: mode must be 0 or 1");
+  PO_REQUIRE(B > 0 && S > 1 && P > 0 && P <= S, "po_warp_bwd: bad shape");
+  return warp_bwd(d_out, patch_mp, noise, contrast, bright, affine, B, S, P, mode, work, d_patch_mp, make_geom(S, P),
+                  s);
+}
+
+extern "C" int po_warp_bwd_keyed(const float* d_out, const float* patch_mp, uint64_t seed, uint64_t counter, int b0,
+                                 const float* contrast, const float* bright, const double* affine, int B, int S, int P,
+                                 int mode, float* work, float* d_patch_mp, po_stream_t s) {
+  PO_REQUIRE(d_out && patch_mp && contrast && bright && affine && work && d_patch_mp,
+             "po_warp_bwd_keyed: null pointer");
+  PO_REQUIRE(mode == 0 || mode == 1, "po_warp_bwd_keyed: mode must be 0 or 1");
+  PO_REQUIRE(B > 0 && S > 1 && P > 0 && P <= S && b0 >= 0, "po_warp_bwd_keyed: bad shape");
+  PO_REQUIRE(3LL * P * P < (1LL << 31), "po_warp_bwd_keyed: patch too large");
+  return warp_bwd(d_out, patch_mp, nullptr, contrast, bright, affine, B, S, P, mode, work, d_patch_mp,
+                  make_geom(S, P, seed, counter, b0), s);
 }
 
 extern "C" int po_warp_composite_multi(const float* img, const float* patch_mp, const float* noise,

@@ -173,26 +173,47 @@ class _Warp(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, mp, noise, contrast, bright, affine, img, S, mode):
+        """``noise``: the [B,3,P,P] tensor, or a po_draws key (seed, counter,
+        b0) — the kernels then regenerate the same values in-kernel
+        (po_warp_fwd_keyed) and no noise tensor exists."""
         mp = mp.contiguous()
         B = affine.size(0)
         P = mp.size(-1)
         out = torch.empty(B, 3, S, S, device=mp.device)
-        nat.call("po_warp_fwd", nat.ptr(img.contiguous() if img is not None else None), nat.ptr(mp),
-                 nat.ptr(noise), nat.ptr(contrast), nat.ptr(bright), nat.ptr(affine, torch.float64), B, S, P, mode,
-                 nat.ptr(out), nat.stream())
-        ctx.save_for_backward(mp, noise, contrast, bright, affine)
+        imgp = nat.ptr(img.contiguous() if img is not None else None)
+        if isinstance(noise, tuple):
+            seed, counter, b0 = noise
+            nat.call("po_warp_fwd_keyed", imgp, nat.ptr(mp), int(seed) & 0xFFFFFFFFFFFFFFFF,
+                     int(counter) & 0xFFFFFFFFFFFFFFFF, int(b0), nat.ptr(contrast), nat.ptr(bright),
+                     nat.ptr(affine, torch.float64), B, S, P, mode, nat.ptr(out), nat.stream())
+            ctx.key = noise
+            ctx.save_for_backward(mp, contrast, bright, affine)
+        else:
+            nat.call("po_warp_fwd", imgp, nat.ptr(mp), nat.ptr(noise), nat.ptr(contrast), nat.ptr(bright),
+                     nat.ptr(affine, torch.float64), B, S, P, mode, nat.ptr(out), nat.stream())
+            ctx.key = None
+            ctx.save_for_backward(mp, contrast, bright, affine, noise)
         ctx.S, ctx.mode = S, mode
         return out
 
     @staticmethod
     def backward(ctx, d_out):
-        mp, noise, contrast, bright, affine = ctx.saved_tensors
+        mp, contrast, bright, affine = ctx.saved_tensors[:4]
         d_out = d_out.contiguous()
         work = torch.empty_like(d_out)
         d_mp = torch.empty_like(mp)
-        nat.call("po_warp_bwd", nat.ptr(d_out), nat.ptr(mp), nat.ptr(noise), nat.ptr(contrast),
-                 nat.ptr(bright), nat.ptr(affine, torch.float64), affine.size(0), ctx.S, mp.size(-1), ctx.mode,
-                 nat.ptr(work), nat.ptr(d_mp), nat.stream())
+        B, P = affine.size(0), mp.size(-1)
+        if ctx.key is not None:
+            seed, counter, b0 = ctx.key
+            nat.call("po_warp_bwd_keyed", nat.ptr(d_out), nat.ptr(mp), int(seed) & 0xFFFFFFFFFFFFFFFF,
+                     int(counter) & 0xFFFFFFFFFFFFFFFF, int(b0), nat.ptr(contrast), nat.ptr(bright),
+                     nat.ptr(affine, torch.float64), B, ctx.S, P, ctx.mode, nat.ptr(work), nat.ptr(d_mp),
+                     nat.stream())
+        else:
+            noise = ctx.saved_tensors[4]
+            nat.call("po_warp_bwd", nat.ptr(d_out), nat.ptr(mp), nat.ptr(noise), nat.ptr(contrast),
+                     nat.ptr(bright), nat.ptr(affine, torch.float64), B, ctx.S, P, ctx.mode,
+                     nat.ptr(work), nat.ptr(d_mp), nat.stream())
         return d_mp, None, None, None, None, None, None, None
 
 
@@ -218,6 +239,7 @@ class PatchTransformer(nn.Module):
         self.draw_seed = 3
         self.draw_step = 0
         self.draw_b0 = 0
+        self.keyed_noise = os.environ.get("ADVPATCH_NOISE_KEYED", "1") != "0"
         self.last_roi = None     # [B,4] int32 footprint boxes of the last placement
 
     def lab_transform(self, lab_batch_origin):
@@ -234,10 +256,21 @@ class PatchTransformer(nn.Module):
 
     def make_draws(self, B, P, device):
         """This step's draws for images draw_b0 .. draw_b0+B-1 of the global
-        batch; advances the step counter."""
-        d = synthetic.draws_device(self.draw_seed, self.draw_step, self.draw_b0, B, P, device)
+        batch; advances the step counter.  With ``keyed_noise`` (default;
+        ADVPATCH_NOISE_KEYED=0: off) the noise is not drawn: ``noise_key``
+        (seed, step, b0) lets the warp kernels regenerate po_draws' values."""
+        if self.keyed_noise:
+            d = synthetic.draws_device(self.draw_seed, self.draw_step, self.draw_b0, B, P, device,
+                                       keys=tuple(k for k in synthetic.DRAW_KEYS if k != "noise"))
+            d["noise_key"] = (self.draw_seed, self.draw_step, self.draw_b0)
+        else:
+            d = synthetic.draws_device(self.draw_seed, self.draw_step, self.draw_b0, B, P, device)
         self.draw_step += 1
         return d
+
+    @staticmethod
+    def _noise(d):
+        return d["noise"].contiguous() if "noise" in d else d["noise_key"]
 
     def _prep(self, adv_patch, lab_batch, img_size, do_rotate, draws):
         nat.ensure_device(adv_patch)
@@ -252,7 +285,7 @@ class PatchTransformer(nn.Module):
     def forward(self, adv_patch, lab_batch, img_size, do_rotate=True, rand_loc=False, draws=None):
         """-> (adv_batch_t [B,1,3,S,S], patch_center [B,2] = (x*S, y*S))."""
         mp, d, affine, center = self._prep(adv_patch, lab_batch, img_size, do_rotate, draws)
-        out = _Warp.apply(mp, d["noise"].contiguous(), d["contrast"].contiguous(),
+        out = _Warp.apply(mp, self._noise(d), d["contrast"].contiguous(),
                           d["bright"].contiguous(), affine, None, int(img_size), 0)
         return out.unsqueeze(1), center
 
@@ -261,7 +294,7 @@ class PatchTransformer(nn.Module):
         -> (p_img_batch [B,3,S,S], patch_center [B,2]) without materialising
         adv_batch_t."""
         mp, d, affine, center = self._prep(adv_patch, lab_batch, img_size, do_rotate, draws)
-        out = _Warp.apply(mp, d["noise"].contiguous(), d["contrast"].contiguous(),
+        out = _Warp.apply(mp, self._noise(d), d["contrast"].contiguous(),
                           d["bright"].contiguous(), affine, img_batch.contiguous(), int(img_size), 1)
         return out, center
 

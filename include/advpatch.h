@@ -33,7 +33,7 @@ typedef void* po_stream_t;
 #define PO_EHIP -2     /* HIP runtime error */
 #define PO_EDEVICE -3  /* device is not gfx950 */
 
-#define PO_ABI_VERSION 16
+#define PO_ABI_VERSION 17
 #define PO_AMAX_SUB 64  /* sub-slots per max|x| slot (see po_conv_desc) */
 
 int po_abi_version(void);
@@ -108,6 +108,17 @@ int po_warp_bwd(const float* d_out, const float* patch_mp, const float* noise, c
                 const float* bright, const double* affine, int B, int S, int P, int mode,
                 float* work /* [B,3,S,S] scratch, may alias d_out */, float* d_patch_mp,
                 po_stream_t s);
+/* po_warp_fwd / po_warp_bwd with the noise regenerated in the kernels instead
+ * of read from a [B,3,P,P] tensor: element e (flat over [3][P][P]) of image b
+ * is po_draws(seed, counter, b0, ...)'s noise value of global image b0 + b,
+ * bit for bit (lane e % 4 of Philox group e / 4).  The B*3*P*P*4 bytes of
+ * noise are then neither written by po_draws nor gathered by the warp. */
+int po_warp_fwd_keyed(const float* img, const float* patch_mp, uint64_t seed, uint64_t counter, int b0,
+                      const float* contrast, const float* bright, const double* affine, int B, int S, int P,
+                      int mode, float* out, po_stream_t s);
+int po_warp_bwd_keyed(const float* d_out, const float* patch_mp, uint64_t seed, uint64_t counter, int b0,
+                      const float* contrast, const float* bright, const double* affine, int B, int S, int P,
+                      int mode, float* work, float* d_patch_mp, po_stream_t s);
 
 /* PatchApplier for an explicit adv tensor: out = where(adv==0, img, adv)
  * (load_data.py:820); n elements. bwd: d_img = d_out*(adv==0), d_adv = d_out*(adv!=0). */

@@ -15,6 +15,7 @@ import oracle
 from conftest import pkg_mod
 
 pytestmark = pytest.mark.gpu
+DEV = torch.device("cuda", 0)
 
 
 def _dev():
@@ -273,3 +274,40 @@ def test_warp_bwd_tight_scan_bit_identical(monkeypatch, S, P, B, big):
         grads.append(pg.grad.detach().clone())
     assert bool((grads[0] != 0).any())
     assert torch.equal(grads[0], grads[1]) and torch.equal(grads[0], grads[2])
+
+
+@pytest.mark.parametrize("B,S,P,b0", [(6, 608, 224, 0), (5, 416, 224, 37), (3, 97, 33, 2)])
+def test_keyed_noise_warp_bit_identical(B, S, P, b0):
+    """po_warp_fwd_keyed / po_warp_bwd_keyed regenerate po_draws' noise in the
+    kernels: the composite, the warp-only output and the patch gradient equal
+    the tensor path fed po_draws' own noise tensor bit for bit (global image
+    index b0 + b, odd S and P included)."""
+    ld, sy = pkg_mod("load_data"), pkg_mod("synthetic")
+    seed, step = 0x5EED1234ABCD, 9
+    full = sy.draws_device(seed, step, b0, B, P, DEV)
+    keyed = {k: v for k, v in full.items() if k != "noise"}
+    keyed["noise_key"] = (seed, step, b0)
+    img = sy.frames(B, S, seed=3).to(DEV)
+    lab = sy.labels(B, seed=4).to(DEV)
+    patch = sy.patch(P, seed=5).to(DEV)
+    outs = []
+    for dr in (full, keyed):
+        pt = ld.PatchTransformer()
+        pg = patch.clone().requires_grad_(True)
+        comp, _ = pt.forward_composite(pg, lab, img, S, draws=dr)
+        g = torch.randn_like(comp)
+        comp.backward(g)
+        adv, _ = pt(patch, lab, S, draws=dr)
+        outs.append((comp.detach(), pg.grad.clone(), adv))
+    for a, b in zip(outs[0], outs[1]):
+        assert torch.equal(a, b)
+    assert (outs[0][0] != img).any()                   # the patch landed somewhere
+
+
+def test_trainer_draws_are_keyed():
+    """The training placement draws no noise tensor by default (keyed noise);
+    ADVPATCH_NOISE_KEYED=0 restores the tensor."""
+    ld = pkg_mod("load_data")
+    pt = ld.PatchTransformer()
+    d = pt.make_draws(4, 32, DEV)
+    assert "noise" not in d and d["noise_key"] == (pt.draw_seed, 0, 0)

@@ -5,7 +5,7 @@
 cd "$GRAFT_REPO_ROOT"
 OUT=gpurun_out/r03d
 mkdir -p $OUT/tiles
-timeout -k 10 900 python -u -m pytest -x -q --timeout 300 --timeout-method thread tests/test_gpu_darknet.py \
+timeout -k 10 900 python -u -m pytest -x -q --timeout 300 --timeout-method thread tests/test_gpu_darknet.py tests/test_gpu_patch_ops.py tests/test_gpu_step.py \
     tests/test_gpu_cones.py tests/test_gpu_first_conv.py tests/test_gpu_eval_folder.py \
     "tests/test_gpu_train.py::test_nonfinite_guard_and_flags" tests/test_gpu_train.py::test_empty_shard_adds_only_its_patch_terms \
     tests/test_gpu_placement.py > $OUT/tests.log 2>&1
