@@ -291,11 +291,11 @@ def test_keyed_noise_warp_bit_identical(B, S, P, b0):
     lab = sy.labels(B, seed=4).to(DEV)
     patch = sy.patch(P, seed=5).to(DEV)
     outs = []
+    g = torch.randn(B, 3, S, S, generator=torch.Generator().manual_seed(6)).to(DEV)
     for dr in (full, keyed):
         pt = ld.PatchTransformer()
         pg = patch.clone().requires_grad_(True)
         comp, _ = pt.forward_composite(pg, lab, img, S, draws=dr)
-        g = torch.randn_like(comp)
         comp.backward(g)
         adv, _ = pt(patch, lab, S, draws=dr)
         outs.append((comp.detach(), pg.grad.clone(), adv))
