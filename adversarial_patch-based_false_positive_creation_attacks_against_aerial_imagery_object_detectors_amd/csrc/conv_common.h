@@ -375,7 +375,8 @@ int launch_h3(const ConvArgs& a, hipStream_t st, int bm, int bn, int bk, int sta
 // the launch's transformed weights (po_conv_desc.Wwino)
 int launch_wino(const ConvArgs& a, const float* U, hipStream_t st, int bm, int waves, bool sched = false,
                 bool vec = false, bool small_lds = false);
-// tile 67: 64 tiles x 64 channels per 512-thread workgroup, pipelined k-loop
-int launch_wino4(const ConvArgs& a, const float* U, hipStream_t st);
+// tiles 67/68: 64 tiles x 64 channels per 512-thread workgroup, pipelined k-loop
+// (68: the two waves of a SIMD staggered)
+int launch_wino4(const ConvArgs& a, const float* U, hipStream_t st, bool stagger);
 
 }  // namespace po

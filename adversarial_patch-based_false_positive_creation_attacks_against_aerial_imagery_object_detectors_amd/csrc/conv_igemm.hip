@@ -427,7 +427,7 @@ constexpr int kTiles[PO_CONV_NTILES][5] = {
     {128, 128, 16, 3, 1}, {128, 64, 16, 3, 1},
     {128, 128, 16, 4, 1}, {128, 64, 16, 4, 1}, {256, 128, 16, 4, 1}, {256, 64, 16, 4, 1},
     {64, 32, 16, 5, 0}, {32, 64, 16, 5, 0}, {32, 64, 16, 6, 0}, {32, 64, 16, 7, 0}, {32, 64, 16, 8, 0},
-    {32, 64, 16, 11, 0}, {64, 64, 16, 12, 0}};
+    {32, 64, 16, 11, 0}, {64, 64, 16, 12, 0}, {64, 64, 16, 13, 0}};
 }  // namespace
 
 extern "C" int po_conv_tile_info(int t, int* bm, int* bn, int* bk, int* prec) {
@@ -546,7 +546,7 @@ extern "C" int po_conv(const po_conv_desc* d, const float* in, const float* W, c
   while (bk > 16 && a.Cin_p % bk != 0) bk /= 2;
   int rc;
   PO_REQUIRE((a.mrows == a.Hg * a.Wg && !a.pool_y) || gl <= 1 ||
-                 ((gl == 5 || gl == 11 || gl == 12) && a.mrows == a.Hg * a.Wg),
+                 ((gl == 5 || gl == 11 || gl == 12 || gl == 13) && a.mrows == a.Hg * a.Wg),
              "po_conv: a compact box grid (mrows) runs on the generic tiles only, a fused pool on those and tiles "
              "61/66/67");
   PO_REQUIRE(!a.pool_y || bm * bn <= 128 * 128,
@@ -563,8 +563,9 @@ extern "C" int po_conv(const po_conv_desc* d, const float* in, const float* W, c
     return rc;
   }
   if (gl >= 5 && gl <= 8) return po::launch_wino(a, d->Wwino, st, bm, gl >= 6 ? 8 : 4, gl >= 7, gl == 8);
-  if (gl == 11 || gl == 12) {
-    rc = gl == 12 ? po::launch_wino4(a, d->Wwino, st) : po::launch_wino(a, d->Wwino, st, bm, 4, false, true, true);
+  if (gl >= 11 && gl <= 13) {
+    rc = gl >= 12 ? po::launch_wino4(a, d->Wwino, st, gl == 13)
+                  : po::launch_wino(a, d->Wwino, st, bm, 4, false, true, true);
     if (rc == PO_OK && a.ksplit > 1) {
       hipLaunchKernelGGL(conv_reduce_k, dim3(po::ceil_div((int64_t)a.M * (a.N / (4 * RQ)), 256)), dim3(256), 0, st, a);
       rc = po::check_launch("po_conv (winograd split-K reduce)");

@@ -1095,6 +1095,7 @@ constexpr int T4 = 64, N4 = 64;
 constexpr int V4_FLOATS = 16 * T4 * WK;                 // one transformed buffer: 64 KB
 __device__ __forceinline__ int v4idx(int xi, int t, int ch) { return ((xi * T4 + t) * WK) + ((ch ^ ((t >> 2) & 3)) << 2); }
 
+template <bool STAG>
 __global__ __launch_bounds__(512, 1) void conv_wino4_k(const ConvArgs a, const float* __restrict__ U, int Ht, int Wt) {
   constexpr int CPW = 2;                 // components per wave
   constexpr int TH = 32;                 // tiles per epilogue pass (one M-block)
@@ -1206,37 +1207,70 @@ __global__ __launch_bounds__(512, 1) void conv_wino4_k(const ConvArgs a, const f
   gload(ks0);
   transform(smem);
   __builtin_amdgcn_sched_barrier(0);
-  bload(0, ks0);
-  __builtin_amdgcn_sched_barrier(0);
-  gload(min(ks0 + 1, ks1 - 1));
-  __builtin_amdgcn_sched_barrier(0);
-  bload(1, ks0);
-  __builtin_amdgcn_sched_barrier(0);
-  __syncthreads();
-  int ks = ks0;
-  do {                                       // ks1 > ks0: every slice has a k-step (host check); no
-    float* Vc = smem + ((ks - ks0) & 1) * V4_FLOATS;      // zero-trip test to sink the prologue loads into
-    float* Vn = smem + (((ks - ks0) & 1) ^ 1) * V4_FLOATS;
-    // branch-free body (a branch around the prefetches would merge the waitcnt
-    // states of both paths into a full vmcnt(0) drain): on the last steps the
-    // prefetches re-read the last k-step and the transform rewrites the V
-    // buffer nobody reads any more
-    const int k1 = min(ks + 1, ks1 - 1), k2 = min(ks + 2, ks1 - 1);
-    // phases kept in this order (sched_barrier): live ranges stay within the
-    // 256-VGPR budget of two waves per SIMD
-    mfma_c(0, Vc);
+  if (STAG && wave_u >= 4) {
+    // tile 68: waves 4-7 (the second wave of every SIMD) transform the next
+    // step BEFORE their MFMAs, waves 0-3 between their two components: on each
+    // SIMD one wave's transform and load issue run beside the other's MFMAs
+    // instead of both waves leaving the matrix pipe idle together (issue
+    // order inputs, B0, B1 in prologue and loop alike)
+    gload(min(ks0 + 1, ks1 - 1));
     __builtin_amdgcn_sched_barrier(0);
-    bload(0, k1);                            // component 0's registers are free once its MFMAs are issued
+    bload(0, ks0);
     __builtin_amdgcn_sched_barrier(0);
-    transform(Vn);                           // step ks+1 (d landed one step ago)
+    bload(1, ks0);
     __builtin_amdgcn_sched_barrier(0);
-    gload(k2);
+    __syncthreads();
+    int ks = ks0;
+    do {
+      float* Vc = smem + ((ks - ks0) & 1) * V4_FLOATS;
+      float* Vn = smem + (((ks - ks0) & 1) ^ 1) * V4_FLOATS;
+      const int k1 = min(ks + 1, ks1 - 1), k2 = min(ks + 2, ks1 - 1);
+      transform(Vn);
+      __builtin_amdgcn_sched_barrier(0);
+      gload(k2);
+      __builtin_amdgcn_sched_barrier(0);
+      mfma_c(0, Vc);
+      __builtin_amdgcn_sched_barrier(0);
+      bload(0, k1);
+      __builtin_amdgcn_sched_barrier(0);
+      mfma_c(1, Vc);
+      __builtin_amdgcn_sched_barrier(0);
+      bload(1, k1);
+      __syncthreads();
+    } while (++ks < ks1);
+  } else {
+    bload(0, ks0);
     __builtin_amdgcn_sched_barrier(0);
-    mfma_c(1, Vc);
+    gload(min(ks0 + 1, ks1 - 1));
     __builtin_amdgcn_sched_barrier(0);
-    bload(1, k1);
-    __syncthreads();                         // V(ks+1) complete everywhere; V(ks) free
-  } while (++ks < ks1);
+    bload(1, ks0);
+    __builtin_amdgcn_sched_barrier(0);
+    __syncthreads();
+    int ks = ks0;
+    do {                                     // ks1 > ks0: every slice has a k-step (host check); no
+      float* Vc = smem + ((ks - ks0) & 1) * V4_FLOATS;    // zero-trip test to sink the prologue loads into
+      float* Vn = smem + (((ks - ks0) & 1) ^ 1) * V4_FLOATS;
+      // branch-free body (a branch around the prefetches would merge the waitcnt
+      // states of both paths into a full vmcnt(0) drain): on the last steps the
+      // prefetches re-read the last k-step and the transform rewrites the V
+      // buffer nobody reads any more
+      const int k1 = min(ks + 1, ks1 - 1), k2 = min(ks + 2, ks1 - 1);
+      // phases kept in this order (sched_barrier): live ranges stay within the
+      // 256-VGPR budget of two waves per SIMD
+      mfma_c(0, Vc);
+      __builtin_amdgcn_sched_barrier(0);
+      bload(0, k1);                          // component 0's registers are free once its MFMAs are issued
+      __builtin_amdgcn_sched_barrier(0);
+      transform(Vn);                         // step ks+1 (d landed one step ago)
+      __builtin_amdgcn_sched_barrier(0);
+      gload(k2);
+      __builtin_amdgcn_sched_barrier(0);
+      mfma_c(1, Vc);
+      __builtin_amdgcn_sched_barrier(0);
+      bload(1, k1);
+      __syncthreads();                       // V(ks+1) complete everywhere; V(ks) free
+    } while (++ks < ks1);
+  }
 
 
   // ---- epilogue, two passes of 32 tiles (pass = M-block mb): M[xi][tile - 32 pass][64 ch]
@@ -1430,7 +1464,7 @@ int launch_wino(const ConvArgs& a, const float* U, hipStream_t st, int bm, int w
 
 // po_conv tile staging 12 (tile 67): conv_wino4_k, 64 tiles x 64 channels per
 // 512-thread workgroup, register-staged input, pipelined k-loop (see above).
-int launch_wino4(const ConvArgs& a, const float* U, hipStream_t st) {
+int launch_wino4(const ConvArgs& a, const float* U, hipStream_t st, bool stagger) {
   PO_REQUIRE(U, "po_conv: Winograd tile needs the transformed weights (Wwino)");
   PO_REQUIRE(a.prec == 0 && a.ntaps == 9 && a.tkw == 3 && (a.sdh == 1 || a.sdh == -1) && (a.sdw == 1 || a.sdw == -1) &&
                  a.dh0 == -a.sdh && a.dw0 == -a.sdw,
@@ -1449,7 +1483,10 @@ int launch_wino4(const ConvArgs& a, const float* U, hipStream_t st) {
   ConvArgs b = a;
   b.ntiles_n = a.N / N4;
   const int ntm = ceil_div((int64_t)a.B * Ht * Wt, T4);
-  hipLaunchKernelGGL(conv_wino4_k, dim3(ntm * b.ntiles_n, a.ksplit), dim3(512), 0, st, b, U, Ht, Wt);
+  if (stagger)
+    hipLaunchKernelGGL(conv_wino4_k<true>, dim3(ntm * b.ntiles_n, a.ksplit), dim3(512), 0, st, b, U, Ht, Wt);
+  else
+    hipLaunchKernelGGL(conv_wino4_k<false>, dim3(ntm * b.ntiles_n, a.ksplit), dim3(512), 0, st, b, U, Ht, Wt);
   return check_launch("po_conv (winograd 64x64)");
 }
 }  // namespace po

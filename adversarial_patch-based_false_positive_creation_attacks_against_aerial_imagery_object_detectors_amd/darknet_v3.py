@@ -565,7 +565,7 @@ class NetPlan:
         return desc.macs * pts / (desc.B * desc.Hg * desc.Wg)
 
     # Winograd tiles of po_conv: (tiles = GEMM rows, output channels) per workgroup
-    WINO_TILES = {61: (64, 32), 62: (32, 64), 63: (32, 64), 64: (32, 64), 65: (32, 64), 66: (32, 64), 67: (64, 64)}
+    WINO_TILES = {61: (64, 32), 62: (32, 64), 63: (32, 64), 64: (32, 64), 65: (32, 64), 66: (32, 64), 67: (64, 64), 68: (64, 64)}
     _tile_shapes = {}
 
     @classmethod
@@ -1194,7 +1194,7 @@ class NetPlan:
     # ---------------- autotuning ----------------
     SPLITS = (2, 4, 8, 16, 32)
     WS_FLOATS = 64 << 20          # split-K workspace cap (256 MB)
-    WINO_SPLIT_TILES = (66, 67)   # Winograd tiles with split-K (conv_wino3_k, conv_wino4_k)
+    WINO_SPLIT_TILES = (66, 67, 68)   # Winograd tiles with split-K (conv_wino3_k, conv_wino4_k)
 
     def _ensure_ws(self, floats):
         if self.ws is None or self.ws.numel() < floats:

@@ -256,7 +256,7 @@ def roofline(cfg_name, B, prec, m, ref_flops_step):
         # the dominant kernel: the tile with the most time per step
         best = max(((t, tt, k) for k, f in fam.items() for t, tt in f["tiles"].items()), key=lambda x: x[1]["ms"])
         t, tt, k = best
-        name = {67: "conv_wino4_k", 66: "conv_wino3_k", 65: "conv_wino2_k", 64: "conv_wino2_k", 63: "conv_wino2_k", 62: "conv_wino2_k",
+        name = {68: "conv_wino4_k<stagger>", 67: "conv_wino4_k", 66: "conv_wino3_k", 65: "conv_wino2_k", 64: "conv_wino2_k", 63: "conv_wino2_k", 62: "conv_wino2_k",
                 61: "conv_wino_k"}.get(t, "conv_k")
         r["dominant_kernel"] = {"kernel": "%s (po_conv tile %d, %s)" % (name, t, k), "ms_per_step": tt["ms"],
                                 "launches_per_step": tt["launches"],

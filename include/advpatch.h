@@ -387,7 +387,7 @@ typedef struct po_conv_desc {
    * (staging 0/1). */
   int mrows;
   /* Optional fused k=2 stride-2 max pool of a plain forward conv (y_out NULL,
-   * full even grid, no split-K; generic tiles, or Winograd tiles 61/66/67
+   * full even grid, no split-K; generic tiles, or Winograd tiles 61/66/67/68
    * without gbox -- their 2x2 output tiles are the windows): pool_y [B,Hout/2,Wout/2,Cout_p]
    * and pool_argmax (int8, same shape) as po_maxpool2_fwd writes them, the
    * argmax bytes of a leaky conv also carrying its LeakyReLU slope (bit 3
@@ -397,7 +397,7 @@ typedef struct po_conv_desc {
   int8_t* pool_argmax;
 } po_conv_desc;
 
-#define PO_CONV_NTILES 67
+#define PO_CONV_NTILES 68
 /* Tile `t` (1-based): block rows BM (output pixels), block columns BN (output
  * channels), k-step BK (input channels).  Tiles 1..10 stage operands through
  * registers, 11..20 are the same shapes staged by LDS-DMA, 21..28 are
@@ -413,9 +413,10 @@ typedef struct po_conv_desc {
  * 64 scheduled, 65 with the vector epilogue, 66 as 65 in 4-wave workgroups
  * with 64 KB of LDS, two per CU, bit-identical to 65; 67: 64 tiles x 64
  * channels per 512-thread workgroup, register-staged input and a pipelined
- * k-loop, bit-identical to 65/66; 16 input channels per k-step) for stride-1
+ * k-loop, bit-identical to 65/66; 68: 67 with the two waves of every SIMD
+ * staggered; 16 input channels per k-step) for stride-1
  * 3x3 convs and their input gradients on full maps, without split-K except on
- * 66/67 (needs Wwino; 62..67 need N % 64 == 0).  A
+ * 66/67/68 (needs Wwino; 62..68 need N % 64 == 0).  A
  * tile that does not apply to a launch makes po_conv
  * return PO_EINVAL.  Returns PO_EINVAL for a bad index. */
 int po_conv_tile_info(int t, int* bm, int* bn, int* bk, int* prec);

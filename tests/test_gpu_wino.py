@@ -15,7 +15,7 @@ from conftest import pkg_mod
 
 pytestmark = pytest.mark.gpu
 DEV = torch.device("cuda", 0)
-WINO_TILES = [61, 62, 63, 64, 65, 66, 67]   # 64 tiles x 32 ch; 32 tiles x 64 ch (LDS-DMA input, N % 64 == 0), 4 / 8
+WINO_TILES = [61, 62, 63, 64, 65, 66, 67, 68]   # 64 tiles x 32 ch; 32 tiles x 64 ch (LDS-DMA input, N % 64 == 0), 4 / 8
                                             # waves, 8 scheduled, 4 waves in 64 KB of LDS; 64 tiles x 64 ch pipelined
 
 
@@ -54,7 +54,7 @@ def _setup(B, H, Cin, Cout, flip, seed):
                                                (4, 19, 512, 256, True), (1, 76, 128, 64, False),
                                                (2, 9, 16, 32, False)])
 def test_wino_matches_float64_conv(B, H, Cin, Cout, flip, WINO):
-    if WINO in (62, 63, 64, 65, 66, 67) and Cout % 64:
+    if WINO in (62, 63, 64, 65, 66, 67, 68) and Cout % 64:
         pytest.skip("tiles 62/63 take N % 64 == 0")
     nat = pkg_mod("_native")
     x, w, bias, wd, U = _setup(B, H, Cin, Cout, flip, seed=H * Cin + flip)
@@ -176,7 +176,7 @@ def test_wino_refuses_what_it_cannot_run(WINO):
     assert call(d) == 0
     ws = torch.empty(4 * B * H * H * Cout, device=DEV)
     d.ksplit, d.workspace = 2, ws.data_ptr()
-    assert (call(d) == 0) == (WINO in (66, 67))                     # split-K: tiles 66 and 67 only
+    assert (call(d) == 0) == (WINO in (66, 67, 68))                 # split-K: tiles 66, 67, 68 only
     d.ksplit = 3
     assert call(d) != 0                                             # more slices than 16-channel steps
     d = _desc(nat, B, H, Cin, Cout, WINO)
@@ -186,7 +186,7 @@ def test_wino_refuses_what_it_cannot_run(WINO):
     assert call(d) != 0                                             # stride 2
 
 
-@pytest.mark.parametrize("tile", [66, 67])
+@pytest.mark.parametrize("tile", [66, 67, 68])
 @pytest.mark.parametrize("mode", ["fwd_bits", "fwd_shortcut", "dgrad_acc_bits", "dgrad_dual"])
 @pytest.mark.parametrize("B,H,Cin,Cout", [(2, 11, 64, 128), (3, 38, 256, 512), (1, 19, 512, 64), (2, 7, 16, 64)])
 def test_wino_tile66_bit_identical_to_65(mode, B, H, Cin, Cout, tile):
@@ -238,7 +238,7 @@ def test_wino_tile66_bit_identical_to_65(mode, B, H, Cin, Cout, tile):
 
 
 
-@pytest.mark.parametrize("tile", [61, 66, 67])
+@pytest.mark.parametrize("tile", [61, 66, 67, 68])
 @pytest.mark.parametrize("act", [0, 1])
 @pytest.mark.parametrize("B,H,Cin,Cout", [(2, 12, 64, 128), (3, 26, 128, 256), (2, 104, 32, 64), (2, 52, 16, 32)])
 def test_wino_fused_pool(act, B, H, Cin, Cout, tile):
@@ -247,7 +247,7 @@ def test_wino_fused_pool(act, B, H, Cin, Cout, tile):
     bit-identical to pooling the tile's own unpooled output by
     po_maxpool2_fwd's rule (first position on ties), max|x| slot of the pooled
     map; tile 65 refuses a pooled launch."""
-    if tile in (66, 67) and Cout % 64:
+    if tile in (66, 67, 68) and Cout % 64:
         pytest.skip("tiles 66/67 take N % 64 == 0")
     nat = pkg_mod("_native")
     x, w, bias, wd, U = _setup(B, H, Cin, Cout, False, seed=H + Cout)
@@ -284,7 +284,7 @@ def test_wino_fused_pool(act, B, H, Cin, Cout, tile):
                               None, nat.stream()) != 0
 
 
-@pytest.mark.parametrize("tile", [66, 67])
+@pytest.mark.parametrize("tile", [66, 67, 68])
 @pytest.mark.parametrize("ks", [2, 3])
 @pytest.mark.parametrize("boxed", [False, True])
 @pytest.mark.parametrize("mode", ["fwd_bits", "fwd_shortcut", "dgrad_acc_bits", "dgrad_dual"])

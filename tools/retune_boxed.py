@@ -17,7 +17,7 @@ for path in [a for a in sys.argv[1:] if not a.startswith("--")]:
         key = json.loads(k)
         boxed = bool(key[15]) or "mrows" in key
         tile = v[0] if isinstance(v, list) else v
-        if not boxed and not (wino and 61 <= tile <= 67):
+        if not boxed and not (wino and 61 <= tile <= 68):
             keep[k] = v
     with open(path, "w") as f:
         json.dump(keep, f)
