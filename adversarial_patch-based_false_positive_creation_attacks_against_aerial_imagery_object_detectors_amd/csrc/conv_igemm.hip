@@ -102,10 +102,21 @@ __global__ __launch_bounds__(256) void conv_k(const ConvArgs a) {
     b_off[r] = ok ? (uint32_t)(n0 + row) * wrow_bytes + a_chunk(row) * 16u : kOOB;
   }
 
+  float4 ra[GL ? 1 : AL], rb[GL ? 1 : BL];
   auto a_offset = [&](int r, int dh, int dw, uint32_t cb) {
     const int hi = a_hi[r] + dh, wi = a_wi[r] + dw;
     const bool ok = (unsigned)hi < (unsigned)a.Hin && (unsigned)wi < (unsigned)a.Win;
     return ok ? a_off[r] + ((uint32_t)hi * a.Win + wi) * pix_bytes + cb : kOOB;
+  };
+  auto gload = [&](int tap, int dh, int dw, int c0) {
+    const uint32_t cb = (uint32_t)c0 * 4u;
+#pragma unroll
+    for (int r = 0; r < AL; ++r)
+      ra[r] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(in_rs, a_offset(r, dh, dw, cb), 0, 0));
+    const uint32_t tb = (uint32_t)tap * pix_bytes + cb;
+#pragma unroll
+    for (int r = 0; r < BL; ++r)
+      rb[r] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(w_rs, b_off[r] + tb, 0, 0));
   };
   auto gload_lds = [&](int buf, int tap, int dh, int dw, int c0) {
     const uint32_t cb = (uint32_t)c0 * 4u;
@@ -124,6 +135,21 @@ __global__ __launch_bounds__(256) void conv_k(const ConvArgs a) {
     }
   };
   auto swz = [](int row, int chunk) { return (chunk ^ ((row >> SW) & (CPR - 1))) * 4; };
+  auto sstore = [&](int buf) {
+#pragma unroll
+    for (int r = 0; r < AL; ++r) {
+      const int row = rth + RPP * r;
+      if (row < BM)
+        *reinterpret_cast<float4*>(&As[(buf * BM + row) * BK + swz(row, cth)]) = ra[r];
+    }
+#pragma unroll
+    for (int r = 0; r < BL; ++r) {
+      const int row = rth + RPP * r;
+      if (row < BN)
+        *reinterpret_cast<float4*>(&Bs[(buf * BN + row) * BK + swz(row, cth)]) = rb[r];
+    }
+  };
+
   floatx16 acc[TM][TN];
 #pragma unroll
   for (int i = 0; i < TM; ++i)
@@ -143,12 +169,21 @@ __global__ __launch_bounds__(256) void conv_k(const ConvArgs a) {
   // chunk re-read the same (shifted) pixels while they are still in L1/L2
   int tap = ks0 % a.ntaps, c0 = (ks0 / a.ntaps) * BK;
   int th = tap / a.tkw, tw = tap - th * a.tkw;
+  if constexpr (GL) {
+    gload_lds(0, tap, a.dh0 + th * a.sdh, a.dw0 + tw * a.sdw, c0);
+  } else {
+    gload(tap, a.dh0 + th * a.sdh, a.dw0 + tw * a.sdw, c0);
+    sstore(0);
+  }
+  __syncthreads();
   const int arow = wm * TM * 32 + (lane & 31);
   const int brow = wn * TN * 32 + (lane & 31);
   const int h = lane >> 5;
-  // the MFMAs of one k-step from LDS buffer (Ab, Bb); `load` runs after the
-  // first fragment group's reads
-  auto kstep = [&](const float* Ab, const float* Bb, auto&& load) {
+  for (int ks = 0; ks < nks; ++ks) {
+    const int buf = ks & 1;
+    const bool more = ks + 1 < nks;
+    const float* Ab = As + buf * BM * BK;
+    const float* Bb = Bs + buf * BN * BK;
 #pragma unroll
     for (int g = 0; g < BK / 8; ++g) {
       float4 af[TM], bf[TN];
@@ -162,7 +197,24 @@ __global__ __launch_bounds__(256) void conv_k(const ConvArgs a) {
         const int row = brow + j * 32;
         bf[j] = *reinterpret_cast<const float4*>(&Bb[row * BK + swz(row, 2 * g + h)]);
       }
-      if (g == 0) load();
+#ifdef PO_ABLATE_NOLOAD
+      if (false) {      // ablation build (tools/): k-steps without staging loads
+#else
+      if (g == 0 && more) {
+#endif
+        // issue the next k-step's staging loads behind this group's fragment reads
+        if (++tap == a.ntaps) {
+          tap = th = tw = 0;
+          c0 += BK;
+        } else if (++tw == a.tkw) {
+          tw = 0;
+          ++th;
+        }
+        if constexpr (GL)
+          gload_lds(buf ^ 1, tap, a.dh0 + th * a.sdh, a.dw0 + tw * a.sdw, c0);
+        else
+          gload(tap, a.dh0 + th * a.sdh, a.dw0 + tw * a.sdw, c0);
+      }
 #pragma unroll
       for (int i = 0; i < TM; ++i)
 #pragma unroll
@@ -173,83 +225,12 @@ __global__ __launch_bounds__(256) void conv_k(const ConvArgs a) {
           acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(af[i].w, bf[j].w, acc[i][j], 0, 0, 0);
         }
     }
-  };
-  auto advance = [&]() {
-    if (++tap == a.ntaps) {
-      tap = th = tw = 0;
-      c0 += BK;
-    } else if (++tw == a.tkw) {
-      tw = 0;
-      ++th;
-    }
-  };
-  if constexpr (GL) {
-    gload_lds(0, tap, a.dh0 + th * a.sdh, a.dw0 + tw * a.sdw, c0);
-    __syncthreads();
-    for (int ks = 0; ks < nks; ++ks) {
-      const int buf = ks & 1;
-      const bool more = ks + 1 < nks;
-      kstep(As + buf * BM * BK, Bs + buf * BN * BK, [&]() {
 #ifndef PO_ABLATE_NOLOAD
-        if (more) {
-          // issue the next k-step's staging loads behind this group's fragment reads
-          advance();
-          gload_lds(buf ^ 1, tap, a.dh0 + th * a.sdh, a.dw0 + tw * a.sdw, c0);
-        }
+    if constexpr (!GL) {
+      if (more) sstore(buf ^ 1);
+    }
 #endif
-      });
-      __syncthreads();
-    }
-  } else {
-    // Register staging with TWO k-steps of loads in flight: set p of the staging
-    // registers holds the k-step of parity p, the loads of step ks+2 are issued
-    // during step ks (behind its first fragment reads) and step ks+1 goes to
-    // LDS at its end, so a load has a whole k-step of MFMAs more to land than
-    // with one set.  The loop is unrolled by two (compile-time set index) and
-    // branch-free (loads of steps past the slice read nothing: out-of-range
-    // buffer offsets), so the waits stay partial (vmcnt of one set).
-    float4 ra2[2][AL], rb2[2][BL];
-    int issued = 0;                              // k-steps of this slice whose loads are issued
-    auto gload2 = [&](float4 (&ra_)[AL], float4 (&rb_)[BL]) {
-      const uint32_t oob = issued < nks ? 0u : kOOB;
-      const uint32_t cb = (uint32_t)c0 * 4u;
-      const int dh = a.dh0 + th * a.sdh, dw = a.dw0 + tw * a.sdw;
-#pragma unroll
-      for (int r = 0; r < AL; ++r)
-        ra_[r] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(in_rs, a_offset(r, dh, dw, cb) | oob, 0, 0));
-      const uint32_t tb = (uint32_t)tap * pix_bytes + cb;
-#pragma unroll
-      for (int r = 0; r < BL; ++r)
-        rb_[r] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(w_rs, (b_off[r] + tb) | oob, 0, 0));
-      ++issued;
-      advance();
-    };
-    auto sstore2 = [&](int buf, const float4 (&ra_)[AL], const float4 (&rb_)[BL]) {
-#pragma unroll
-      for (int r = 0; r < AL; ++r) {
-        const int row = rth + RPP * r;
-        if (row < BM) *reinterpret_cast<float4*>(&As[(buf * BM + row) * BK + swz(row, cth)]) = ra_[r];
-      }
-#pragma unroll
-      for (int r = 0; r < BL; ++r) {
-        const int row = rth + RPP * r;
-        if (row < BN) *reinterpret_cast<float4*>(&Bs[(buf * BN + row) * BK + swz(row, cth)]) = rb_[r];
-      }
-    };
-    gload2(ra2[0], rb2[0]);
-    gload2(ra2[1], rb2[1]);
-    sstore2(0, ra2[0], rb2[0]);
     __syncthreads();
-    int ks = 0;
-    for (; ks + 1 < nks; ks += 2) {
-      kstep(As, Bs, [&]() { gload2(ra2[0], rb2[0]); });
-      sstore2(1, ra2[1], rb2[1]);
-      __syncthreads();
-      kstep(As + BM * BK, Bs + BN * BK, [&]() { gload2(ra2[1], rb2[1]); });
-      sstore2(0, ra2[0], rb2[0]);
-      __syncthreads();
-    }
-    if (ks < nks) kstep(As, Bs, [&]() {});
   }
 
   if (a.ksplit > 1) {
@@ -548,7 +529,7 @@ extern "C" int po_conv(const po_conv_desc* d, const float* in, const float* W, c
   PO_REQUIRE((a.mrows == a.Hg * a.Wg && !a.pool_y) || gl <= 1 ||
                  ((gl == 5 || gl == 11 || gl == 12 || gl == 13) && a.mrows == a.Hg * a.Wg),
              "po_conv: a compact box grid (mrows) runs on the generic tiles only, a fused pool on those and tiles "
-             "61/66/67");
+             "61/66/67/68");
   PO_REQUIRE(!a.pool_y || bm * bn <= 128 * 128,
              "po_conv: a fused pool needs a generic tile of at most 128x128 (got %dx%d)", bm, bn);
   if (a.prec == 1) {

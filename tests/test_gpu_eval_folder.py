@@ -86,7 +86,12 @@ def test_evaluate_folder_matches_oracle(tmp_path):
     assert sorted(res) == ["im0", "im1", "im2", "im3"]
     anchors = ut.get_anchors(None)
     for k, stem in enumerate(sorted(res)):
-        assert torch.equal(frames[stem], frames2[stem]) and res[stem] == res2[stem]      # batching changes nothing
+        # batching changes nothing: same frames, same boxes (the Darknet launches of
+        # the two batch sizes may run other tuned tiles: values agree to fp32 rounding)
+        assert torch.equal(frames[stem], frames2[stem])
+        assert len(res[stem]) == len(res2[stem])
+        for b1, b2 in zip(res[stem], res2[stem]):
+            assert b1[6] == b2[6] and max(abs(float(x) - float(y)) for x, y in zip(b1[:6], b2[:6])) <= 1e-5
         # oracle: pad/resize, placement (draws of image k), composite, quantisation
         base = _reference_frame(str(img_dir / (stem + ".png")), S)
         lab = ev.load_eval_labels(str(lab_dir / (stem + ".txt"))).unsqueeze(0)
