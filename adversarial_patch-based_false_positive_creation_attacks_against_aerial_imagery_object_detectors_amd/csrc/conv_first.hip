@@ -346,14 +346,10 @@ extern "C" int po_conv_first_fwd(const float* img, int B, int H, int W, int stri
   PO_REQUIRE((int64_t)B * 3 * H * W * 4 < (1LL << 31) && n + 512 < (1LL << 31),
              "po_conv_first_fwd: image batch must be < 2 GiB");
   dim3 grid2(po::ceil_div(n, 512));
-  if (CO == 16 && !getenv("PO_FIRST_V1"))
+  if (CO == 16)
     hipLaunchKernelGGL(first_fwd2_k<16>, grid2, dim3(256), 0, st, img, B, H, W, stride, Ho, Wo, Wt, bias, Cout, act, y, amax);
-  else if (CO == 32 && !getenv("PO_FIRST_V1"))
-    hipLaunchKernelGGL(first_fwd2_k<32>, grid2, dim3(256), 0, st, img, B, H, W, stride, Ho, Wo, Wt, bias, Cout, act, y, amax);
-  else if (CO == 16)
-    hipLaunchKernelGGL(first_fwd_k<16>, grid, dim3(256), 0, st, img, B, H, W, stride, Ho, Wo, Wt, bias, Cout, Cout_p, act, y, amax);
   else if (CO == 32)
-    hipLaunchKernelGGL(first_fwd_k<32>, grid, dim3(256), 0, st, img, B, H, W, stride, Ho, Wo, Wt, bias, Cout, Cout_p, act, y, amax);
+    hipLaunchKernelGGL(first_fwd2_k<32>, grid2, dim3(256), 0, st, img, B, H, W, stride, Ho, Wo, Wt, bias, Cout, act, y, amax);
   else
     hipLaunchKernelGGL(first_fwd_k<64>, grid, dim3(256), 0, st, img, B, H, W, stride, Ho, Wo, Wt, bias, Cout, Cout_p, act, y, amax);
   return po::check_launch("po_conv_first_fwd");

@@ -360,8 +360,8 @@ int dispatch(const ConvArgs& a, hipStream_t st, int bm, int bn) {
   if (bm == 128 && bn == 64) return launch<128, 64, 4, BK, GL>(a, st);
   if (bm == 64 && bn == 64) return launch<64, 64, 2, BK, GL>(a, st);
   if (bm == 128 && bn == 32) return launch<128, 32, 4, BK, GL>(a, st);
-  if (bm == 256 && bn == 128) return launch<256, 128, 2, BK, GL>(a, st);
-  if (bm == 128 && bn == 256) return launch<128, 256, 2, BK, GL>(a, st);
+  if constexpr (BK == 16 && GL)
+    if (bm == 128 && bn == 256) return launch<128, 256, 2, BK, GL>(a, st);
   po::set_error("po_conv: no %dx%d tile", bm, bn);
   return PO_EINVAL;
 }
@@ -391,7 +391,10 @@ bool forced_tile(int& bm, int& bn, int& bk, int& gl) {
 // LDS-DMA input (62: 4 waves; 63, staging 6: 8 waves, two per SIMD; 64,
 // staging 7: 63 with the transform interleaved into the MFMA stream; 65,
 // staging 8: 64 with the 16-byte (4-channel) epilogue; 66, staging 11: 65's
-// work as 4-wave workgroups in 72 KB of LDS, two per CU).
+// work as 4-wave workgroups in 72 KB of LDS, two per CU; 67, staging 12:
+// conv_wino4_k, 64 tiles x 64 channels per 8-wave workgroup with
+// register-staged input; 68, staging 13: 67 with the two waves of each SIMD
+// staggered by half a k-step).  Retired (see retired()): 21..26, 28, 62..64.
 constexpr int kTiles[PO_CONV_NTILES][5] = {
     {128, 128, 16, 0, 0}, {128, 128, 32, 0, 0}, {64, 128, 16, 0, 0}, {64, 128, 32, 0, 0}, {128, 64, 16, 0, 0},
     {128, 64, 32, 0, 0},  {64, 64, 16, 0, 0},   {64, 64, 32, 0, 0},  {128, 32, 16, 0, 0}, {128, 32, 32, 0, 0},
@@ -409,6 +412,11 @@ constexpr int kTiles[PO_CONV_NTILES][5] = {
     {128, 128, 16, 4, 1}, {128, 64, 16, 4, 1}, {256, 128, 16, 4, 1}, {256, 64, 16, 4, 1},
     {64, 32, 16, 5, 0}, {32, 64, 16, 5, 0}, {32, 64, 16, 6, 0}, {32, 64, 16, 7, 0}, {32, 64, 16, 8, 0},
     {32, 64, 16, 11, 0}, {64, 64, 16, 12, 0}, {64, 64, 16, 13, 0}};
+// Tiles no tuned cache or tuner run selected over rounds 1-3 (the 256x128
+// shapes, the register-staged and BK-32 128x256 ones, the 32x64 Winograd
+// kernels before tile 65); their numbers stay reserved so cached choices keep
+// their meaning.
+constexpr bool retired(int t) { return (t >= 21 && t <= 26) || t == 28 || (t >= 62 && t <= 64); }
 }  // namespace
 
 extern "C" int po_conv_tile_info(int t, int* bm, int* bn, int* bk, int* prec) {
@@ -416,7 +424,7 @@ extern "C" int po_conv_tile_info(int t, int* bm, int* bn, int* bk, int* prec) {
   *bm = kTiles[t - 1][0];
   *bn = kTiles[t - 1][1];
   *bk = kTiles[t - 1][2];
-  if (prec) *prec = kTiles[t - 1][4];
+  if (prec) *prec = retired(t) ? -1 : kTiles[t - 1][4];
   return PO_OK;
 }
 
@@ -506,6 +514,7 @@ extern "C" int po_conv(const po_conv_desc* d, const float* in, const float* W, c
   int bm, bn, bk, gl = 0;
   PO_REQUIRE(d->tile >= 0 && d->tile <= PO_CONV_NTILES, "po_conv: tile %d out of range", d->tile);
   if (d->tile > 0) {
+    PO_REQUIRE(!retired(d->tile), "po_conv: tile %d is retired", d->tile);
     bm = kTiles[d->tile - 1][0];
     bn = kTiles[d->tile - 1][1];
     bk = kTiles[d->tile - 1][2];

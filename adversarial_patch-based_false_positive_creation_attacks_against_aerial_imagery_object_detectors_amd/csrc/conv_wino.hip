@@ -1435,24 +1435,15 @@ int launch_wino(const ConvArgs& a, const float* U, hipStream_t st, int bm, int w
     ConvArgs b = a;
     b.ntiles_n = a.N / N2;
     const int ntm = ceil_div((int64_t)a.B * Ht * Wt, T2);
+    PO_REQUIRE(small_lds || (waves == 8 && sched && vec), "po_conv: retired Winograd variant");
     if (small_lds)
       hipLaunchKernelGGL(conv_wino3_k, dim3(ntm * b.ntiles_n, a.ksplit), dim3(256), 0, st, b, U, Ht, Wt);
-    else if (waves == 8 && sched && vec && a.res)
+    else if (a.res)
       hipLaunchKernelGGL((conv_wino2_k<8, true, 1, true>), dim3(ntm * b.ntiles_n), dim3(512), 0, st, b, U, Ht, Wt);
-    else if (waves == 8 && sched && vec && (a.accumulate || a.mbits || a.mask || a.y2))
+    else if (a.accumulate || a.mbits || a.mask || a.y2)
       hipLaunchKernelGGL((conv_wino2_k<8, true, 2, true>), dim3(ntm * b.ntiles_n), dim3(512), 0, st, b, U, Ht, Wt);
-    else if (waves == 8 && sched && vec)
-      hipLaunchKernelGGL((conv_wino2_k<8, true, 0, true>), dim3(ntm * b.ntiles_n), dim3(512), 0, st, b, U, Ht, Wt);
-    else if (waves == 8 && sched && a.res)
-      hipLaunchKernelGGL((conv_wino2_k<8, true, 1>), dim3(ntm * b.ntiles_n), dim3(512), 0, st, b, U, Ht, Wt);
-    else if (waves == 8 && sched && (a.accumulate || a.mbits || a.mask || a.y2))
-      hipLaunchKernelGGL((conv_wino2_k<8, true, 2>), dim3(ntm * b.ntiles_n), dim3(512), 0, st, b, U, Ht, Wt);
-    else if (waves == 8 && sched)
-      hipLaunchKernelGGL((conv_wino2_k<8, true>), dim3(ntm * b.ntiles_n), dim3(512), 0, st, b, U, Ht, Wt);
-    else if (waves == 8)
-      hipLaunchKernelGGL(conv_wino2_k<8>, dim3(ntm * b.ntiles_n), dim3(512), 0, st, b, U, Ht, Wt);
     else
-      hipLaunchKernelGGL(conv_wino2_k<4>, dim3(ntm * b.ntiles_n), dim3(256), 0, st, b, U, Ht, Wt);
+      hipLaunchKernelGGL((conv_wino2_k<8, true, 0, true>), dim3(ntm * b.ntiles_n), dim3(512), 0, st, b, U, Ht, Wt);
     return check_launch("po_conv (winograd 32x64)");
   }
   ConvArgs b = a;

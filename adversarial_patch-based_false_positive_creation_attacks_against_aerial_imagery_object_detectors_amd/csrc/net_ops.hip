@@ -344,8 +344,7 @@ extern "C" int po_view_move(const float* src, int Hs, int Ws, int src_stride, in
   if (!tot) return PO_OK;
   const bool v4 = C % 4 == 0 && src_stride % 4 == 0 && src_off % 4 == 0 && dst_stride % 4 == 0 && dst_off % 4 == 0 &&
                   (!mask_y || mask_stride % 4 == 0) && ((uintptr_t)src | (uintptr_t)dst | (uintptr_t)mask_y) % 16 == 0 &&
-                  tot + 1024 < (1LL << 31) && (int64_t)B * Hs * Ws * src_stride < (1LL << 31) &&
-                  !getenv("PO_VIEW_MOVE_V1");
+                  tot + 1024 < (1LL << 31) && (int64_t)B * Hs * Ws * src_stride < (1LL << 31);
   if (v4) {
     hipLaunchKernelGGL(view_move4_k, dim3(po::ceil_div(tot / 4, 256)), dim3(256), 0, po::stream_of(s), src, Hs, Ws,
                        src_stride, src_off, src_org, dst, Hd, Wd, dst_stride, dst_off, dst_org, B, C / 4, mode,

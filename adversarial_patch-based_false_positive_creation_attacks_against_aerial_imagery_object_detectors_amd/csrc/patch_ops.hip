@@ -584,20 +584,18 @@ __global__ __launch_bounds__(256) void warp_bwd_a4_k(const float* __restrict__ d
 // images q, q + WB_G, ... in increasing order, then the WB_G partials are added
 // in group order through LDS (deterministic, no atomics, no workspace); the
 // batch is spread over WB_G x more workgroups than one thread per element.
-// SCAN 1: only the output pixels whose sample point lies in [c-1, c+1) x
-// [r-1, r+1) can have (r, c) as a corner, so the scan covers the integer
-// points of that square's preimage box (from the inverse map with one
-// division per image; +-1e-6 px against its rounding) instead of the box
-// widened by one pixel on each side (SCAN 0, PO_WARP_BWD_WIDE=1): for a
-// down-scaled patch (an output pixel spans several patch pixels) that is ~0-1
-// candidate pixels per (element, image) instead of >= 9.  The skipped pixels
-// fail the corner test anyway, so the contributions and their order (rows,
-// then columns) are unchanged: bit-identical to the wide scan.  (A fused
+// Only the output pixels whose sample point lies in [c-1, c+1) x [r-1, r+1)
+// can have (r, c) as a corner, so the scan covers the integer points of that
+// square's preimage box (from the inverse map with one division per image;
+// +-1e-6 px against its rounding) instead of the box widened by one pixel on
+// each side (the round-2 scan): for a down-scaled patch (an output pixel spans
+// several patch pixels) that is ~0-1 candidate pixels per (element, image)
+// instead of >= 9.  The skipped pixels fail the corner test anyway, so the
+// contributions and their order (rows, then columns) are unchanged.  (A fused
 // single pass that recomputes phase A at each candidate instead of reading
 // gfac measured 477 us against 165 + 159 us on tiny B=256: each footprint
 // pixel is the candidate of 4 corners, and warp_pixel's 24 gathers dominate.)
 constexpr int WB_EL = 32, WB_G = 8;
-template <int SCAN>
 __global__ __launch_bounds__(256) void warp_bwd_b_k(const float* __restrict__ gfac,
                                                     const float* __restrict__ mp,
                                                     const float* __restrict__ noise,
@@ -620,37 +618,17 @@ __global__ __launch_bounds__(256) void warp_bwd_b_k(const float* __restrict__ gf
     // the preimage of (c-1, c+1) x (r-1, r+1) under the pixel-space affine
     const double A00 = af[0], A01 = af[1], A02 = af[2], A10 = af[3], A11 = af[4], A12 = af[5];
     const double det = A00 * A11 - A01 * A10;
-    double jlo = 1e30, jhi = -1e30, ilo = 1e30, ihi = -1e30;
-    if (SCAN == 1) {
-      const double inv = 1.0 / det;
-      const double m00 = A11 * inv, m01 = -A01 * inv, m10 = -A10 * inv, m11 = A00 * inv;
-      const double X = (double)c - A02, Y = (double)r - A12;
-      const double jc = m00 * X + m01 * Y, ic = m10 * X + m11 * Y;
-      const double hj = fabs(m00) + fabs(m01), hi_ = fabs(m10) + fabs(m11);
-      jlo = jc - hj; jhi = jc + hj;
-      ilo = ic - hi_; ihi = ic + hi_;
-    } else {
-#pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        const double X = (double)c + ((k & 1) ? 1.0 : -1.0) - A02;
-        const double Y = (double)r + ((k & 2) ? 1.0 : -1.0) - A12;
-        const double jj = (A11 * X - A01 * Y) / det;
-        const double ii = (-A10 * X + A00 * Y) / det;
-        jlo = fmin(jlo, jj); jhi = fmax(jhi, jj);
-        ilo = fmin(ilo, ii); ihi = fmax(ihi, ii);
-      }
-    }
+    const double inv = 1.0 / det;
+    const double m00 = A11 * inv, m01 = -A01 * inv, m10 = -A10 * inv, m11 = A00 * inv;
+    const double X = (double)c - A02, Y = (double)r - A12;
+    const double jc = m00 * X + m01 * Y, ic = m10 * X + m11 * Y;
+    const double hj = fabs(m00) + fabs(m01), hi_ = fabs(m10) + fabs(m11);
+    const double jlo = jc - hj, jhi = jc + hj, ilo = ic - hi_, ihi = ic + hi_;
     if (!(jhi >= -1.0 && jlo <= (double)g.S && ihi >= -1.0 && ilo <= (double)g.S)) continue;
-    int j0, j1, i0, i1;
+    constexpr double eps = 1e-6;
     const double hiS = (double)(g.S - 1);
-    if (SCAN > 0) {
-      constexpr double eps = 1e-6;
-      j0 = (int)fmax(0.0, ceil(jlo - eps)); j1 = (int)fmin(hiS, floor(jhi + eps));
-      i0 = (int)fmax(0.0, ceil(ilo - eps)); i1 = (int)fmin(hiS, floor(ihi + eps));
-    } else {
-      j0 = (int)fmax(0.0, floor(jlo) - 1.0); j1 = (int)fmin(hiS, ceil(jhi) + 1.0);
-      i0 = (int)fmax(0.0, floor(ilo) - 1.0); i1 = (int)fmin(hiS, ceil(ihi) + 1.0);
-    }
+    const int j0 = (int)fmax(0.0, ceil(jlo - eps)), j1 = (int)fmin(hiS, floor(jhi + eps));
+    const int i0 = (int)fmax(0.0, ceil(ilo - eps)), i1 = (int)fmin(hiS, floor(ihi + eps));
     const float cb = contrast[b], bb = bright[b];
     const NoiseSrc nz = noise_src(noise, g, b);
     float a0 = 0.f, a1 = 0.f, a2 = 0.f;
@@ -756,7 +734,7 @@ WarpGeom make_geom(int S, int P, uint64_t seed = 0, uint64_t counter = 0, int b0
 namespace {
 int warp_fwd(const float* img, const float* patch_mp, const float* noise, const float* contrast, const float* bright,
              const double* affine, int B, int S, int mode, float* out, const WarpGeom& g, po_stream_t s) {
-  if (S % 4 == 0 && ((uintptr_t)img | (uintptr_t)out) % 16 == 0 && !getenv("PO_WARP_V1")) {
+  if (S % 4 == 0 && ((uintptr_t)img | (uintptr_t)out) % 16 == 0) {
     hipLaunchKernelGGL(warp_fwd4_k, dim3(po::ceil_div(S * (S / 4), 256), B), dim3(256), 0, po::stream_of(s), img,
                        patch_mp, noise, contrast, bright, affine, g, mode, out);
     return po::check_launch("po_warp_fwd");
@@ -792,8 +770,7 @@ namespace {
 int warp_bwd(const float* d_out, const float* patch_mp, const float* noise, const float* contrast, const float* bright,
              const double* affine, int B, int S, int P, int mode, float* work, float* d_patch_mp, const WarpGeom& g,
              po_stream_t s) {
-  const bool quad = S % 4 == 0 && ((uintptr_t)d_out | (uintptr_t)work) % 16 == 0 && work != d_out &&
-                    !getenv("PO_WARP_V1");
+  const bool quad = S % 4 == 0 && ((uintptr_t)d_out | (uintptr_t)work) % 16 == 0 && work != d_out;
   if (quad) {
     hipLaunchKernelGGL(warp_bwd_a4_k, dim3(po::ceil_div(S * (S / 4), 256), B), dim3(256), 0, po::stream_of(s), d_out,
                        patch_mp, noise, contrast, bright, affine, g, mode, work);
@@ -805,12 +782,8 @@ int warp_bwd(const float* d_out, const float* patch_mp, const float* noise, cons
   int rc = po::check_launch("po_warp_bwd(a)");
   if (rc) return rc;
   dim3 gridb(po::ceil_div(P * P, WB_EL));
-  if (getenv("PO_WARP_BWD_WIDE"))
-    hipLaunchKernelGGL(warp_bwd_b_k<0>, gridb, dim3(256), 0, po::stream_of(s), work, patch_mp, noise, contrast,
-                       bright, affine, g, B, d_patch_mp);
-  else
-    hipLaunchKernelGGL(warp_bwd_b_k<1>, gridb, dim3(256), 0, po::stream_of(s), work, patch_mp, noise, contrast,
-                       bright, affine, g, B, d_patch_mp);
+  hipLaunchKernelGGL(warp_bwd_b_k, gridb, dim3(256), 0, po::stream_of(s), work, patch_mp, noise, contrast, bright,
+                     affine, g, B, d_patch_mp);
   return po::check_launch("po_warp_bwd(b)");
 }
 }  // namespace

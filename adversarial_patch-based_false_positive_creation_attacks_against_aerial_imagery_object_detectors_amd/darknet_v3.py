@@ -565,7 +565,7 @@ class NetPlan:
         return desc.macs * pts / (desc.B * desc.Hg * desc.Wg)
 
     # Winograd tiles of po_conv: (tiles = GEMM rows, output channels) per workgroup
-    WINO_TILES = {61: (64, 32), 62: (32, 64), 63: (32, 64), 64: (32, 64), 65: (32, 64), 66: (32, 64), 67: (64, 64), 68: (64, 64)}
+    WINO_TILES = {61: (64, 32), 65: (32, 64), 66: (32, 64), 67: (64, 64), 68: (64, 64)}   # 62-64 retired
     _tile_shapes = {}
 
     @classmethod

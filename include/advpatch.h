@@ -378,7 +378,7 @@ typedef struct po_conv_desc {
    * onto the canonical offsets -1..1), stored in MFMA fragment order
    * [N/32][Cin_p/16][16 components][2][64 lanes][4]: element (lane l, s) of
    * block (nb, kc, xi), U[xi][16 kc + 8 (l >> 5) + s][32 nb + (l & 31)], sits
-   * at [nb][kc][xi][s >> 2][l][s & 3].  NULL: tiles 61-62 do not apply. */
+   * at [nb][kc][xi][s >> 2][l][s & 3].  NULL: the Winograd tiles do not apply. */
   const float* Wwino;
   /* GEMM rows per image (0: Hg*Wg).  With gbox, mrows < Hg*Wg enumerates each
    * image's box compactly when every box holds at most mrows grid points: a
@@ -400,25 +400,25 @@ typedef struct po_conv_desc {
 #define PO_CONV_NTILES 68
 /* Tile `t` (1-based): block rows BM (output pixels), block columns BN (output
  * channels), k-step BK (input channels).  Tiles 1..10 stage operands through
- * registers, 11..20 are the same shapes staged by LDS-DMA, 21..28 are
- * 256x128 / 128x256 blocks (register, then LDS-DMA staging); these are the
- * exact-fp32 (prec 0) tiles.  29..54 are fp16x3 (prec 1) tiles: register
- * staging, LDS-DMA multi-stage (46..52) and the row halo kernel for stride-1
- * 3x3 convs (53..54); 55..56 are the 2-D tile halo kernel (8 x 16 output
- * pixels per tile) for 3x3 convs of input step 1 or 2 on full maps without
- * split-K or boxes; 57..60 the same 2-D tiles (and 16 x 16-pixel ones at input
- * step 1) reading the weights as MFMA fragments from Wfrag.  61..66 are the
- * exact-fp32 Winograd F(2x2,3x3) kernels (61: 64 2x2-tiles x 32 channels;
- * 62..66: 32 tiles x 64 channels with LDS-DMA input -- 62/63 4 or 8 waves,
- * 64 scheduled, 65 with the vector epilogue, 66 as 65 in 4-wave workgroups
- * with 64 KB of LDS, two per CU, bit-identical to 65; 67: 64 tiles x 64
- * channels per 512-thread workgroup, register-staged input and a pipelined
- * k-loop, bit-identical to 65/66; 68: 67 with the two waves of every SIMD
- * staggered; 16 input channels per k-step) for stride-1
- * 3x3 convs and their input gradients on full maps, without split-K except on
- * 66/67/68 (needs Wwino; 62..68 need N % 64 == 0).  A
- * tile that does not apply to a launch makes po_conv
- * return PO_EINVAL.  Returns PO_EINVAL for a bad index. */
+ * registers, 11..20 are the same shapes staged by LDS-DMA, 27 a 128x256
+ * LDS-DMA block; these are the exact-fp32 (prec 0) tiles.  29..54 are fp16x3
+ * (prec 1) tiles: register staging, LDS-DMA multi-stage (46..52) and the row
+ * halo kernel for stride-1 3x3 convs (53..54); 55..56 are the 2-D tile halo
+ * kernel (8 x 16 output pixels per tile) for 3x3 convs of input step 1 or 2 on
+ * full maps without split-K or boxes; 57..60 the same 2-D tiles (and 16 x
+ * 16-pixel ones at input step 1) reading the weights as MFMA fragments from
+ * Wfrag.  61, 65..68 are the exact-fp32 Winograd F(2x2,3x3) kernels (61: 64
+ * 2x2-tiles x 32 channels; 65/66: 32 tiles x 64 channels with LDS-DMA input,
+ * 65 in 8 scheduled waves, 66 in 4-wave workgroups with 64 KB of LDS, two per
+ * CU, bit-identical to 65; 67: 64 tiles x 64 channels per 512-thread
+ * workgroup, register-staged input and a pipelined k-loop, bit-identical to
+ * 65/66; 68: 67 with the two waves of every SIMD staggered; 16 input channels
+ * per k-step) for stride-1 3x3 convs and their input gradients on full maps,
+ * without split-K except on 66/67/68 (needs Wwino; 65..68 need N % 64 == 0).
+ * Retired tiles (21..26, 28, 62..64: never selected by a tuner run) keep their
+ * numbers; po_conv_tile_info reports them with *prec = -1 and po_conv refuses
+ * them.  A tile that does not apply to a launch makes po_conv return
+ * PO_EINVAL.  Returns PO_EINVAL for a bad index. */
 int po_conv_tile_info(int t, int* bm, int* bn, int* bk, int* prec);
 
 /* v[m][n] = act(sum_k A[m][k] * W[n][k] + bias[n]) (+ y_out[m][n] if accumulate);

@@ -182,8 +182,8 @@ def test_split_k_matches_single_pass(B, H, Cin, Cout, k, prec, tile):
 
 @pytest.mark.parametrize("tile", list(range(1, 61)))
 def test_every_conv_tile(tile):
-    """Every po_conv tile (exact fp32: register-staged 1..10 and 21..24,
-    LDS-DMA-staged 11..20 and 25..28; fp16x3: 29..45, LDS-DMA 46..52, halo 53..54,
+    """Every po_conv tile (exact fp32: register-staged 1..10, LDS-DMA-staged
+    11..20 and 27 — the retired 21..26 and 28 are refused; fp16x3: 29..45, LDS-DMA 46..52, halo 53..54,
     2-D halo 55..56, fragment-weight 2-D halo 57..60) on a 3x3 conv with zero
     padding, a ragged pixel count and a ragged channel count, against a
     float64 torch conv2d."""
@@ -191,6 +191,8 @@ def test_every_conv_tile(tile):
     nat = pkg_mod("_native")
     bm, bn, bk, pr = (ctypes.c_int() for _ in range(4))
     nat.call("po_conv_tile_info", tile, ctypes.byref(bm), ctypes.byref(bn), ctypes.byref(bk), ctypes.byref(pr))
+    retired = pr.value < 0
+    pr.value = max(pr.value, 0)
     B, H, Cin, Cout, k = 3, 7, 128 if bk.value == 64 else 96, 96, 3
     gen = torch.Generator().manual_seed(tile)
     x = torch.randn(B, Cin, H, H, generator=gen)
@@ -211,8 +213,13 @@ def test_every_conv_tile(tile):
     d.in_amax = slot.data_ptr() if slot is not None else None
     wf = _frag(wt) if pr.value == 1 else None
     d.Wfrag = wf.data_ptr() if wf is not None else None
-    nat.call("po_conv", ctypes.byref(d), nat.ptr(xd), nat.ptr(wt, wt.dtype), nat.ptr(bias.to(DEV)), nat.ptr(y),
-             None, None, None, None, None, nat.stream())
+    args = (ctypes.byref(d), nat.ptr(xd), nat.ptr(wt, wt.dtype), nat.ptr(bias.to(DEV)), nat.ptr(y),
+            None, None, None, None, None, nat.stream())
+    if retired:                 # po_conv refuses a retired tile
+        with pytest.raises(RuntimeError, match="retired"):
+            nat.call("po_conv", *args)
+        return
+    nat.call("po_conv", *args)
     assert _rel(y.permute(0, 3, 1, 2).cpu().double(), ref) < 3e-6     # fp32-class error either way
 
 

@@ -1,13 +1,11 @@
-"""HBM-bound producer kernels vs their one-element-per-thread forms.
+"""HBM-bound producer kernels: first conv, warp, fused conv + pool.
 
 po_conv_first_fwd (the 3-channel first Darknet conv, darknet_v3.py:9-100
 conv + BN-folded bias + LeakyReLU 0.1, cfg.py:37-56) on the GPU: the packed
-two-pixel kernel (first_fwd2_k) is bit-identical to the one-pixel kernel
-(first_fwd_k, PO_FIRST_V1=1) and matches a PyTorch fp32 conv within fp32
-rounding; ragged pixel counts (not a multiple of the 512-pixel block) and
+two-pixel kernel (first_fwd2_k, Cout_p 16 / 32) and the one-pixel kernel
+(first_fwd_k, Cout_p 64) match a PyTorch fp32 conv within fp32 rounding; ragged pixel counts (not a multiple of the 512-pixel block) and
 image borders (zero padding) are covered."""
 import ctypes
-import os
 
 import pytest
 import torch
@@ -17,55 +15,57 @@ from conftest import pkg_mod
 pytestmark = pytest.mark.gpu
 
 
-def _run(img, w, b, stride, cout_p, act, v1=False):
+def _run(img, w, b, stride, cout_p, act):
     nat = pkg_mod("_native")
     B, _, H, W = img.shape
     Ho, Wo = (H - 1) // stride + 1, (W - 1) // stride + 1
     y = torch.full((B, Ho, Wo, cout_p), float("nan"), device=img.device)
     amax = torch.zeros(nat.PO_AMAX_SUB, dtype=torch.int32, device=img.device)
-    old = os.environ.pop("PO_FIRST_V1", None)
-    try:
-        if v1:
-            os.environ["PO_FIRST_V1"] = "1"
-        nat.call("po_conv_first_fwd", nat.ptr(img), B, H, W, stride, nat.ptr(w), nat.ptr(b), w.size(0), cout_p,
-                 act, nat.ptr(y), nat.ptr(amax, torch.int32), nat.stream())
-        torch.cuda.synchronize()
-    finally:
-        os.environ.pop("PO_FIRST_V1", None)
-        if old is not None:
-            os.environ["PO_FIRST_V1"] = old
+    nat.call("po_conv_first_fwd", nat.ptr(img), B, H, W, stride, nat.ptr(w), nat.ptr(b), w.size(0), cout_p,
+             act, nat.ptr(y), nat.ptr(amax, torch.int32), nat.stream())
+    torch.cuda.synchronize()
     amax_f = amax.view(torch.float32).max().item()
     return y, amax_f
 
 
 @pytest.mark.parametrize("B,H,W,stride,cout", [(2, 37, 53, 1, 32), (3, 29, 31, 2, 32), (1, 64, 64, 1, 16),
-                                              (1, 41, 23, 2, 16)])
-def test_first_fwd_packed_matches_v1_and_torch(B, H, W, stride, cout):
+                                              (1, 41, 23, 2, 16), (2, 19, 22, 1, 64), (1, 17, 30, 2, 40)])
+def test_first_fwd_matches_torch(B, H, W, stride, cout):
+    """Cout_p 16 / 32: the packed two-pixel kernel; 64: the one-pixel kernel."""
     dev = torch.device("cuda", 0)
     g = torch.Generator().manual_seed(B * 1000 + H)
     img = torch.rand(B, 3, H, W, generator=g).to(dev)
     w = (torch.randn(cout, 3, 3, 3, generator=g) * 0.3).to(dev)
     b = (torch.randn(cout, generator=g) * 0.1).to(dev)
     w27 = w.reshape(cout, 27).contiguous()
+    cp = 16 if cout <= 16 else (32 if cout <= 32 else 64)
     for act in (0, 1):
-        y2, m2 = _run(img, w27, b, stride, cout, act)
-        y1, m1 = _run(img, w27, b, stride, cout, act, v1=True)
-        assert torch.equal(y2, y1), "packed kernel differs from the one-pixel kernel"
-        assert m2 == m1
+        y2, m2 = _run(img, w27, b, stride, cp, act)
         ref = torch.nn.functional.conv2d(img.cpu().double(), w.cpu().double(), b.cpu().double(), stride, 1)
         if act:
             ref = torch.nn.functional.leaky_relu(ref, 0.1)
         ref = ref.permute(0, 2, 3, 1).float()
-        torch.testing.assert_close(y2.cpu(), ref, rtol=1e-5, atol=1e-5)
+        torch.testing.assert_close(y2[..., :cout].cpu(), ref, rtol=1e-5, atol=1e-5)
         assert abs(m2 - ref.abs().max().item()) <= 1e-5 * max(1.0, m2)
 
 
+def _shifted(shape, shift, dev, fill=float("nan")):
+    """A tensor of ``shape`` starting ``shift`` floats into a fresh buffer:
+    shift 1 breaks the 16-byte alignment the vector kernels dispatch on."""
+    n = 1
+    for d in shape:
+        n *= d
+    return torch.full((n + 4,), fill, device=dev)[shift:shift + n].view(shape)
+
+
 @pytest.mark.parametrize("mode", [0, 1])
-def test_warp_fwd_quad_kernel_bit_identical(mode):
-    """po_warp_fwd (PatchTransformer affine warp + composite, load_data.py:
-    726-792, 820): the four-pixels-per-thread kernel writes the same bits as
-    the one-pixel kernel (PO_WARP_V1=1), patch inside, partly outside and
-    fully outside the frame."""
+def test_warp_quad_kernels_bit_identical(mode):
+    """po_warp_fwd / po_warp_bwd (PatchTransformer affine warp + composite,
+    load_data.py:726-792, 820, and its gather-form backward): the
+    four-pixels-per-thread kernels (16-byte aligned buffers) write the same
+    bits as the one-pixel kernels (the dispatch's fallback for unaligned
+    buffers or S % 4 != 0, taken here by a buffer one float off alignment),
+    patch magnified, partly outside and fully outside the frame."""
     nat = pkg_mod("_native")
     dev = torch.device("cuda", 0)
     g = torch.Generator().manual_seed(7 + mode)
@@ -75,6 +75,7 @@ def test_warp_fwd_quad_kernel_bit_identical(mode):
     noise = (torch.rand(B, 3, P, P, generator=g) * 2 - 1).to(dev)
     contrast = (torch.rand(B, generator=g) * 0.4 + 0.8).to(dev)
     bright = (torch.rand(B, generator=g) * 0.2 - 0.1).to(dev)
+    d_out = torch.randn(B, 3, S, S, generator=g).to(dev)
     theta = torch.tensor([[1.6, 0.4, 0.1, -0.4, 1.6, -0.2],      # scaled, rotated, inside
                           [0.9, -1.1, 0.9, 1.1, 0.9, -0.8],      # large, partly outside
                           [2.0, 0.0, 3.5, 0.0, 2.0, 3.5]],       # off the frame
@@ -87,24 +88,24 @@ def test_warp_fwd_quad_kernel_bit_identical(mode):
                           theta[:, 3], theta[:, 4],
                           (theta[:, 3] + theta[:, 4]) * half + 0.5 * S * theta[:, 5] + 0.5 * (S - 1)], 1)
     affine = affine.contiguous().to(dev)
-    outs = []
-    for v1 in (False, True):
-        out = torch.full((B, 3, S, S), float("nan"), device=dev)
-        old = os.environ.pop("PO_WARP_V1", None)
-        try:
-            if v1:
-                os.environ["PO_WARP_V1"] = "1"
-            nat.call("po_warp_fwd", nat.ptr(img) if mode == 1 else None, nat.ptr(mp), nat.ptr(noise),
-                     nat.ptr(contrast), nat.ptr(bright), nat.ptr(affine, torch.float64), B, S, P, mode, nat.ptr(out),
-                     nat.stream())
-            torch.cuda.synchronize()
-        finally:
-            os.environ.pop("PO_WARP_V1", None)
-            if old is not None:
-                os.environ["PO_WARP_V1"] = old
-        outs.append(out)
+    outs, grads = [], []
+    for shift in (0, 1):
+        out = _shifted((B, 3, S, S), shift, dev)
+        nat.call("po_warp_fwd", nat.ptr(img) if mode == 1 else None, nat.ptr(mp), nat.ptr(noise),
+                 nat.ptr(contrast), nat.ptr(bright), nat.ptr(affine, torch.float64), B, S, P, mode, nat.ptr(out),
+                 nat.stream())
+        dsh = _shifted((B, 3, S, S), shift, dev)
+        dsh.copy_(d_out)
+        work = _shifted((B, 3, S, S), shift, dev)
+        dmp = torch.full((3, P, P), float("nan"), device=dev)
+        nat.call("po_warp_bwd", nat.ptr(dsh), nat.ptr(mp), nat.ptr(noise), nat.ptr(contrast), nat.ptr(bright),
+                 nat.ptr(affine, torch.float64), B, S, P, mode, nat.ptr(work), nat.ptr(dmp), nat.stream())
+        torch.cuda.synchronize()
+        outs.append(out.clone())
+        grads.append(dmp)
     assert torch.equal(outs[0], outs[1])
     assert (outs[0] != (img if mode == 1 else 0)).any()      # the patch landed somewhere
+    assert torch.equal(grads[0], grads[1]) and bool((grads[0] != 0).any())
 
 
 @pytest.mark.parametrize("B,H,W,cout", [(2, 38, 54, 32), (3, 29, 31, 16), (1, 64, 64, 16), (2, 17, 20, 13)])

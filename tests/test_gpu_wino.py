@@ -15,8 +15,8 @@ from conftest import pkg_mod
 
 pytestmark = pytest.mark.gpu
 DEV = torch.device("cuda", 0)
-WINO_TILES = [61, 62, 63, 64, 65, 66, 67, 68]   # 64 tiles x 32 ch; 32 tiles x 64 ch (LDS-DMA input, N % 64 == 0), 4 / 8
-                                            # waves, 8 scheduled, 4 waves in 64 KB of LDS; 64 tiles x 64 ch pipelined
+WINO_TILES = [61, 65, 66, 67, 68]   # 64 tiles x 32 ch; 32 tiles x 64 ch (LDS-DMA input, N % 64 == 0) in 8
+                                    # scheduled waves / 4 waves in 64 KB of LDS; 64 tiles x 64 ch pipelined (68: staggered)
 
 
 def _rel(a, b):
@@ -54,8 +54,8 @@ def _setup(B, H, Cin, Cout, flip, seed):
                                                (4, 19, 512, 256, True), (1, 76, 128, 64, False),
                                                (2, 9, 16, 32, False)])
 def test_wino_matches_float64_conv(B, H, Cin, Cout, flip, WINO):
-    if WINO in (62, 63, 64, 65, 66, 67, 68) and Cout % 64:
-        pytest.skip("tiles 62/63 take N % 64 == 0")
+    if WINO in (65, 66, 67, 68) and Cout % 64:
+        pytest.skip("tiles 65-68 take N % 64 == 0")
     nat = pkg_mod("_native")
     x, w, bias, wd, U = _setup(B, H, Cin, Cout, flip, seed=H * Cin + flip)
     ref = F.conv2d(x.double(), w.double(), bias.double(), padding=1)
