@@ -127,7 +127,7 @@ def cpu_baseline(cfg, S, P, B=16, warmup=1, iters=3):
                       % (B, S, iters, warmup, el, cores, os.cpu_count() or 0, _cpu_model())}
 
 
-WARP_ENTRIES = ("po_warp_fwd", "po_warp_bwd")
+WARP_ENTRIES = ("po_warp_fwd", "po_warp_bwd", "po_warp_fwd_keyed", "po_warp_bwd_keyed")
 
 
 def measure(tr, prec, patch, img, lab, B, world, rank, steps, warmup, weights):
@@ -201,6 +201,20 @@ def measure(tr, prec, patch, img, lab, B, world, rank, steps, warmup, weights):
             for key in ("ms", "mfma_flops", "launches"):
                 tt[key] /= steps
     warp_ms = {k: sum(e0.elapsed_time(e1) for e0, e1 in v) / steps for k, v in warp.items()}
+    dump = os.environ.get("ADVPATCH_LAUNCH_DUMP")
+    if dump:
+        # per-launch table (launch order of one step, averaged over the K steps)
+        n = len(timer) // steps
+        with open(dump, "w") as f:
+            for k in range(n):
+                _, _, d, c = timer[k]
+                us = 1000.0 * sum(timer[s * n + k][0].elapsed_time(timer[s * n + k][1]) for s in range(steps)) / steps
+                mf = plan.launch_mfma_flops(d, c) or 0.0
+                f.write(json.dumps({"k": k, "tile": int(d.tile), "ksplit": int(d.ksplit), "B": d.B, "Hg": d.Hg,
+                                    "Wg": d.Wg, "Hin": d.Hin, "Cin_p": d.Cin_p, "N": d.N, "ntaps": d.ntaps,
+                                    "in_step": d.in_step, "mrows": d.mrows, "boxed": bool(d.gbox),
+                                    "pool": bool(d.pool_y), "us": us, "mfma_tflops": mf / us / 1e6,
+                                    "frac_mfma": mf / us / 1e6 / PEAK_CONV[prec]}) + "\n")
     tr.check_flags()
     return {"elapsed": elapsed, "ms_per_step": elapsed * 1000.0 / steps, "value": world * B * steps / elapsed,
             "conv_ms": conv_ms, "conv_flops": conv_flops, "launches": len(timer) // steps, "families": fam,
@@ -272,8 +286,10 @@ def warp_roofline(m, B, S, P):
     2*3*S^2*4 B per image, plus the 3*P^2*4 B patch once; backward reads
     dL/dp_img, 3*S^2*4 B per image), per call, HIP events on the launch stream."""
     out = {}
-    for name, per_img, extra in (("po_warp_fwd", 2 * 3 * S * S * 4, 3 * P * P * 4),
+    for base, per_img, extra in (("po_warp_fwd", 2 * 3 * S * S * 4, 3 * P * P * 4),
                                  ("po_warp_bwd", 3 * S * S * 4, 0)):
+        # the trainer's keyed entries (noise regenerated in-kernel), else the tensor-noise ones
+        name = base + "_keyed" if m["warp_ms"].get(base + "_keyed") else base
         ms = m["warp_ms"].get(name)
         if not ms:
             continue

@@ -90,8 +90,14 @@ def test_evaluate_folder_matches_oracle(tmp_path):
         # the two batch sizes may run other tuned tiles: values agree to fp32 rounding)
         assert torch.equal(frames[stem], frames2[stem])
         assert len(res[stem]) == len(res2[stem])
-        for b1, b2 in zip(res[stem], res2[stem]):
-            assert max(abs(float(x) - float(y)) for x, y in zip(b1[:6], b2[:6])) <= 1e-5, (b1, b2)
+        # boxes whose confidences tie to fp32 rounding may swap places in the sorted list:
+        # match each box to its nearest in the other run
+        rest = list(res2[stem])
+        for b1 in res[stem]:
+            dist = [max(abs(float(x) - float(y)) for x, y in zip(b1[:6], c[:6])) for c in rest]
+            j = min(range(len(rest)), key=dist.__getitem__)
+            b2 = rest.pop(j)
+            assert dist[j] <= 1e-5, (b1, b2)
             # class ids agree unless the winning class probability saturates (ties: first index wins
             # on the last sigmoid bit, which the two launch tilings may round differently)
             assert b1[6] == b2[6] or float(b1[5]) >= 1 - 1e-6, (b1, b2)
