@@ -3,7 +3,8 @@ tang-agui/Adversarial_patch-based_false_positive_creation_attacks_against_aerial
 
 Modules mirror the reference's module names so existing code can switch by
 import: ``load_data``, ``median_pool``, ``darknet_v3``, ``cfg``,
-``patch_config``, ``train_patch``.  ``install_dropin()`` registers them under
+``patch_config``, ``train_patch`` (plus ``eval_patch``, the folder
+evaluation of test_patch_DOTA.py).  ``install_dropin()`` registers them under
 those top-level names in ``sys.modules`` (``import load_data`` then resolves
 here).  The compute runs in ``libadvpatch_hip.so`` (csrc/, C ABI in
 include/advpatch.h); see DESIGN.md.
@@ -12,7 +13,7 @@ import importlib
 import sys
 
 DROPIN_MODULES = ("cfg", "median_pool", "load_data", "darknet_v3", "patch_config", "train_patch", "utils",
-                  "utils_self")
+                  "utils_self", "eval_patch")
 
 
 def install_dropin():
