@@ -18,12 +18,14 @@ Per image of ``imgdir`` (``.png`` / ``.jpg``), as the reference loop does:
 The reference runs one image at a time on the host; here the frames are
 decoded and padded on the host (PIL, as DotaDataset) and everything after —
 median pool, placement, warp + composite, the uint8 quantisation, the Darknet
-forward, decode and NMS — runs on the GPU in batches.  Batching changes
-nothing: the placement draws are keyed by the image's index in the folder
-(po_draws, seed ``seed``, step 0), and an image's labels are padded to the
-batch's row count by repeating its own first row, which leaves
-lab_transform's max-area / min-area picks (first index on ties) where the
-reference's unpadded [1, n, 5] labels put them.  Files are visited in sorted
+forward, decode and NMS — runs on the GPU in batches.  The patched frames
+do not depend on the batch size: the placement draws are keyed by the image's
+index in the folder (po_draws, seed ``seed``, step 0), and an image's labels
+are padded to the batch's row count by repeating its own first row, which
+leaves lab_transform's max-area / min-area picks (first index on ties) where
+the reference's unpadded [1, n, 5] labels put them.  The detections may differ
+between batch sizes at fp32 rounding (the conv tiles are tuned per batch
+shape): a box whose confidence sits at the threshold can come and go.  Files are visited in sorted
 order (the reference's os.listdir order is the filesystem's)."""
 import math
 import os

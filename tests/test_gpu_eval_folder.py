@@ -85,24 +85,15 @@ def test_evaluate_folder_matches_oracle(tmp_path):
     (res, frames, out), (res2, frames2, _) = runs
     assert sorted(res) == ["im0", "im1", "im2", "im3"]
     anchors = ut.get_anchors(None)
-    x4 = ld.u8_to_float(torch.stack([frames[st] for st in sorted(res)]).to(DEV))
+    stems = sorted(res)
+    x4 = ld.u8_to_float(torch.stack([frames[st] for st in stems]).to(DEV))
     heads4 = [h.cpu() for h in net.forward(x4)]
+    heads2 = [torch.cat(hs) for hs in zip(*[[h.cpu() for h in net.forward(x4[i:i + 2].contiguous())]
+                                            for i in (0, 2)])]
     for k, stem in enumerate(sorted(res)):
-        # batching changes nothing: same frames, same boxes (the Darknet launches of
-        # the two batch sizes may run other tuned tiles: values agree to fp32 rounding)
+        # the frames do not depend on the batch size (draws keyed by the image's index); the
+        # detections of each run are checked against the oracle decode of that run's own heads
         assert torch.equal(frames[stem], frames2[stem])
-        assert len(res[stem]) == len(res2[stem])
-        # boxes whose confidences tie to fp32 rounding may swap places in the sorted list:
-        # match each box to its nearest in the other run
-        rest = list(res2[stem])
-        for b1 in res[stem]:
-            dist = [max(abs(float(x) - float(y)) for x, y in zip(b1[:6], c[:6])) for c in rest]
-            j = min(range(len(rest)), key=dist.__getitem__)
-            b2 = rest.pop(j)
-            assert dist[j] <= 1e-5, (b1, b2)
-            # class ids agree unless the winning class probability saturates (ties: first index wins
-            # on the last sigmoid bit, which the two launch tilings may round differently)
-            assert b1[6] == b2[6] or float(b1[5]) >= 1 - 1e-6, (b1, b2)
         # oracle: pad/resize, placement (draws of image k), composite, quantisation
         base = _reference_frame(str(img_dir / (stem + ".png")), S)
         lab = ev.load_eval_labels(str(lab_dir / (stem + ".txt"))).unsqueeze(0)
@@ -117,6 +108,8 @@ def test_evaluate_folder_matches_oracle(tmp_path):
         # batch the bs=4 run detected in, so the same launches) through the oracle post-process
         want_boxes = ref.detect_postprocess([h[k:k + 1] for h in heads4], S, S, anchors, 15, 0.4, 0.4)
         _assert_boxes_equal(res[stem], want_boxes, sat_ties=True)
+        want2 = ref.detect_postprocess([h[k:k + 1] for h in heads2], S, S, anchors, 15, 0.4, 0.4)
+        _assert_boxes_equal(res2[stem], want2, sat_ties=True)
         lines = (out / "yolo-labels" / (stem + ".txt")).read_text().splitlines()
         assert lines == ["%s %s %s %s %s %s %s" % tuple(b) for b in res[stem]]
         assert (out / "pre_patched" / (stem + ".png")).exists()
