@@ -13,7 +13,7 @@ LIB_PATH = os.path.join(_HERE, "libadvpatch_hip.so")
 
 c_int, c_float, c_int64, c_void_p = ctypes.c_int, ctypes.c_float, ctypes.c_int64, ctypes.c_void_p
 
-PO_ABI_VERSION = 17   # include/advpatch.h
+PO_ABI_VERSION = 18   # include/advpatch.h
 PO_CONV_NTILES = 68   # include/advpatch.h
 PO_AMAX_SUB = 64      # sub-slots per max|x| slot
 
@@ -61,6 +61,11 @@ _SIGS = {
                     c_int, c_void_p, c_void_p, c_void_p],
     "po_warp_fwd_keyed": [c_void_p, c_void_p, ctypes.c_uint64, ctypes.c_uint64, c_int, c_void_p, c_void_p, c_void_p,
                           c_int, c_int, c_int, c_int, c_void_p, c_void_p],
+    "po_augment_patch": [c_void_p, ctypes.c_uint64, ctypes.c_uint64, c_int, c_void_p, c_void_p, c_int, c_int, c_void_p,
+                         c_void_p],
+    "po_warp_fwd_pre": [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_void_p],
+    "po_warp_bwd_pre": [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_void_p,
+                        c_void_p],
     "po_warp_bwd_keyed": [c_void_p, c_void_p, ctypes.c_uint64, ctypes.c_uint64, c_int, c_void_p, c_void_p, c_void_p,
                           c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p],
     "po_apply_fwd": [c_void_p, c_void_p, c_int64, c_void_p, c_void_p],

@@ -341,6 +341,10 @@ struct WarpGeom {
   // element e of image b as po_draws does (philox_noise, global image nb0 + b)
   uint32_t nk0, nk1, nc_lo, nc_hi;
   int nb0;
+  // pre-augmented patches (po_warp_*_pre): [B][3][P][P] values mp*contrast +
+  // bright + 0.1*noise before the clamp (po_augment_patch); the kernels then
+  // read them instead of forming them from mp, the draws and the noise
+  const float* pre;
 };
 
 // The transformer noise of one image: the explicit tensor [3][P][P], or (nz
@@ -348,6 +352,7 @@ struct WarpGeom {
 // without the B*3*P*P*4-byte noise tensor being written and gathered.
 struct NoiseSrc {
   const float* nz;
+  const float* pre;       // this image's pre-augmented values, or NULL
   uint32_t k0, k1, c_lo, c_hi, gb;
   __device__ __forceinline__ float at(size_t e) const {
     return nz ? nz[e] : po::philox_noise(k0, k1, c_lo, c_hi, gb, (uint32_t)e);
@@ -356,6 +361,7 @@ struct NoiseSrc {
 __device__ __forceinline__ NoiseSrc noise_src(const float* noise, const WarpGeom& g, int b) {
   NoiseSrc ns;
   ns.nz = noise ? noise + (size_t)b * 3 * g.P * g.P : nullptr;
+  ns.pre = g.pre ? g.pre + (size_t)b * 3 * g.P * g.P : nullptr;
   ns.k0 = g.nk0; ns.k1 = g.nk1; ns.c_lo = g.nc_lo; ns.c_hi = g.nc_hi;
   ns.gb = (uint32_t)(g.nb0 + b);
   return ns;
@@ -385,7 +391,7 @@ __device__ __forceinline__ void bilinear(double ix, double iy, int& x0, int& y0,
 __device__ __forceinline__ float aug_value(const float* __restrict__ mp, const NoiseSrc& ns,
                                            float contrast, float bright, int ch, int pr, int pc, int P) {
   const size_t o = ((size_t)ch * P + pr) * P + pc;
-  float v = mp[o] * contrast + bright + ns.at(o) * 0.1f;    // load_data.py:566-571
+  const float v = ns.pre ? ns.pre[o] : mp[o] * contrast + bright + ns.at(o) * 0.1f;    // load_data.py:566-571
   return fminf(fmaxf(v, 0.f), 1.f);                      // load_data.py:574
 }
 
@@ -448,8 +454,8 @@ __global__ __launch_bounds__(256) void warp_fwd_k(const float* __restrict__ img,
   const size_t o = (size_t)b * 3 * plane + (size_t)i * g.S + j;
   float adv[3], msk;
   bool rng[3];
-  const bool hit = warp_pixel(affine + 6 * b, g, mp, noise_src(noise, g, b), contrast[b],
-                              bright[b], i, j, adv, msk, rng);
+  const bool hit = warp_pixel(affine + 6 * b, g, mp, noise_src(noise, g, b), g.pre ? 1.f : contrast[b],
+                              g.pre ? 0.f : bright[b], i, j, adv, msk, rng);
 #pragma unroll
   for (int ch = 0; ch < 3; ++ch) {
     float v = hit ? adv[ch] * msk : 0.f;          // load_data.py:791-792
@@ -477,7 +483,7 @@ __global__ __launch_bounds__(256) void warp_fwd4_k(const float* __restrict__ img
   const size_t o = (size_t)b * 3 * plane + (size_t)i * g.S + j0;
   const double* th = affine + 6 * b;
   const NoiseSrc nz = noise_src(noise, g, b);
-  const float cb = contrast[b], bb = bright[b];
+  const float cb = g.pre ? 1.f : contrast[b], bb = g.pre ? 0.f : bright[b];
   float v[3][4];
 #pragma unroll
   for (int u = 0; u < 4; ++u) {
@@ -515,7 +521,7 @@ __global__ __launch_bounds__(256) void warp_bwd_a_k(const float* __restrict__ d_
   const size_t o = (size_t)b * 3 * plane + (size_t)i * g.S + j;
   float adv[3], msk;
   bool rng[3];
-  if (!warp_pixel(affine + 6 * b, g, mp, noise_src(noise, g, b), contrast[b], bright[b],
+  if (!warp_pixel(affine + 6 * b, g, mp, noise_src(noise, g, b), contrast[b], g.pre ? 0.f : bright[b],
                   i, j, adv, msk, rng))
     return;   // never read by phase B
 #pragma unroll
@@ -550,7 +556,7 @@ __global__ __launch_bounds__(256) void warp_bwd_a4_k(const float* __restrict__ d
   const size_t o = (size_t)b * 3 * plane + (size_t)i * g.S + j0;
   const double* th = affine + 6 * b;
   const NoiseSrc nz = noise_src(noise, g, b);
-  const float cb = contrast[b], bb = bright[b];
+  const float cb = contrast[b], bb = g.pre ? 0.f : bright[b];
   float adv[4][3], msk[4];
   bool rng[4][3], hit[4];
   bool any = false;
@@ -629,7 +635,7 @@ __global__ __launch_bounds__(256) void warp_bwd_b_k(const float* __restrict__ gf
     const double hiS = (double)(g.S - 1);
     const int j0 = (int)fmax(0.0, ceil(jlo - eps)), j1 = (int)fmin(hiS, floor(jhi + eps));
     const int i0 = (int)fmax(0.0, ceil(ilo - eps)), i1 = (int)fmin(hiS, floor(ihi + eps));
-    const float cb = contrast[b], bb = bright[b];
+    const float cb = contrast[b], bb = g.pre ? 0.f : bright[b];
     const NoiseSrc nz = noise_src(noise, g, b);
     float a0 = 0.f, a1 = 0.f, a2 = 0.f;
     const float* gb = gfac + (size_t)b * 3 * plane;
@@ -655,7 +661,7 @@ __global__ __launch_bounds__(256) void warp_bwd_b_k(const float* __restrict__ gf
 #pragma unroll
     for (int ch = 0; ch < 3; ++ch) {
       const size_t po_ = ((size_t)ch * g.P + pr) * g.P + pc;
-      const float pre = mp[po_] * cb + bb + nz.at(po_) * 0.1f;
+      const float pre = nz.pre ? nz.pre[po_] : mp[po_] * cb + bb + nz.at(po_) * 0.1f;
       dd[ch] = (pre >= 0.f && pre <= 1.f) ? av[ch] * cb : 0.f;
     }
     d0 += dd[0]; d1 += dd[1]; d2 += dd[2];
@@ -724,6 +730,7 @@ WarpGeom make_geom(int S, int P, uint64_t seed = 0, uint64_t counter = 0, int b0
   g.nc_lo = (uint32_t)counter;
   g.nc_hi = (uint32_t)(counter >> 32);
   g.nb0 = b0;
+  g.pre = nullptr;
   const double pad = (S - P) / 2.0;      // load_data.py:534
   g.padL = (int)(pad + 0.5);            // ConstantPad2d((int(pad+.5), int(pad), int(pad+.5), int(pad)))
   g.padT = (int)(pad + 0.5);
@@ -809,6 +816,69 @@ extern "C" int po_warp_bwd_keyed(const float* d_out, const float* patch_mp, uint
   PO_REQUIRE(3LL * P * P < (1LL << 31), "po_warp_bwd_keyed: patch too large");
   return warp_bwd(d_out, patch_mp, nullptr, contrast, bright, affine, B, S, P, mode, work, d_patch_mp,
                   make_geom(S, P, seed, counter, b0), s);
+}
+
+namespace {
+// The transformer's augmentation of the median-pooled patch for each image,
+// before the clamp (load_data.py:548-571): pre[b][e] = mp[e] * contrast[b] +
+// bright[b] + 0.1 * noise(b, e), the noise regenerated from the po_draws key
+// (philox_noise's values: one Philox call per group of 4 elements, so a
+// thread forms 4 consecutive elements).  The warp kernels then gather these
+// values (po_warp_*_pre) instead of forming them at every bilinear corner:
+// one Philox call per 4 patch elements instead of one per corner read.
+__global__ __launch_bounds__(256) void augment_k(const float* __restrict__ mp, const float* __restrict__ contrast,
+                                                 const float* __restrict__ bright, WarpGeom g, int n,
+                                                 float* __restrict__ pre) {
+  const int b = blockIdx.y;
+  const int t = blockIdx.x * 256 + threadIdx.x;
+  const int e0 = 4 * t;
+  if (e0 >= n) return;
+  const po::u4 r = po::philox4x32_10(po::u4{(uint32_t)t, (uint32_t)(g.nb0 + b), g.nc_lo, g.nc_hi}, g.nk0, g.nk1);
+  const uint32_t x[4] = {r.x, r.y, r.z, r.w};
+  const float cb = contrast[b], bb = bright[b];
+  float* o = pre + (size_t)b * n;
+#pragma unroll
+  for (int l = 0; l < 4; ++l) {
+    const int e = e0 + l;
+    if (e < n) {
+      const float nz = po::philox_affine(po::philox_unif(x[l]), 2.0f, -1.0f);
+      o[e] = mp[e] * cb + bb + nz * 0.1f;
+    }
+  }
+}
+}  // namespace
+
+extern "C" int po_augment_patch(const float* patch_mp, uint64_t seed, uint64_t counter, int b0, const float* contrast,
+                                const float* bright, int B, int P, float* pre, po_stream_t s) {
+  PO_REQUIRE(patch_mp && contrast && bright && pre, "po_augment_patch: null pointer");
+  PO_REQUIRE(B > 0 && P > 0 && b0 >= 0 && 3LL * P * P < (1LL << 31), "po_augment_patch: bad shape B=%d P=%d", B, P);
+  const int n = 3 * P * P;
+  WarpGeom g = make_geom(P, P, seed, counter, b0);
+  hipLaunchKernelGGL(augment_k, dim3(po::ceil_div(po::ceil_div(n, 4), 256), B), dim3(256), 0, po::stream_of(s),
+                     patch_mp, contrast, bright, g, n, pre);
+  return po::check_launch("po_augment_patch");
+}
+
+extern "C" int po_warp_fwd_pre(const float* img, const float* pre, const double* affine, int B, int S, int P, int mode, float* out,
+                               po_stream_t s) {
+  PO_REQUIRE(pre && affine && out, "po_warp_fwd_pre: null pointer");
+  PO_REQUIRE(mode == 0 || (mode == 1 && img), "po_warp_fwd_pre: mode must be 0 or 1 (1 needs img)");
+  PO_REQUIRE(B > 0 && S > 1 && P > 0 && P <= S, "po_warp_fwd_pre: bad shape B=%d S=%d P=%d", B, S, P);
+  PO_REQUIRE(3LL * P * P < (1LL << 31), "po_warp_fwd_pre: patch too large");
+  WarpGeom g = make_geom(S, P);
+  g.pre = pre;
+  return warp_fwd(img, pre, nullptr, nullptr, nullptr, affine, B, S, mode, out, g, s);
+}
+
+extern "C" int po_warp_bwd_pre(const float* d_out, const float* pre, const float* contrast, const double* affine, int B,
+                               int S, int P, int mode, float* work, float* d_patch_mp, po_stream_t s) {
+  PO_REQUIRE(d_out && pre && contrast && affine && work && d_patch_mp, "po_warp_bwd_pre: null pointer");
+  PO_REQUIRE(mode == 0 || mode == 1, "po_warp_bwd_pre: mode must be 0 or 1");
+  PO_REQUIRE(B > 0 && S > 1 && P > 0 && P <= S, "po_warp_bwd_pre: bad shape");
+  PO_REQUIRE(3LL * P * P < (1LL << 31), "po_warp_bwd_pre: patch too large");
+  WarpGeom g = make_geom(S, P);
+  g.pre = pre;
+  return warp_bwd(d_out, pre, nullptr, contrast, nullptr, affine, B, S, P, mode, work, d_patch_mp, g, s);
 }
 
 extern "C" int po_warp_composite_multi(const float* img, const float* patch_mp, const float* noise,

@@ -172,16 +172,30 @@ class _Warp(torch.autograd.Function):
     """Augment + warp + clamp*mask (mode 0) or + composite onto img (mode 1)."""
 
     @staticmethod
-    def forward(ctx, mp, noise, contrast, bright, affine, img, S, mode):
+    def forward(ctx, mp, noise, contrast, bright, affine, img, S, mode, pre_aug=True):
         """``noise``: the [B,3,P,P] tensor, or a po_draws key (seed, counter,
-        b0) — the kernels then regenerate the same values in-kernel
-        (po_warp_fwd_keyed) and no noise tensor exists."""
+        b0) — the noise is then regenerated from the key and no noise tensor
+        exists: with ``pre_aug`` (default) po_augment_patch forms the
+        augmented patches [B,3,P,P] once (one Philox call per 4 elements) and
+        the warp gathers them (po_warp_*_pre); otherwise the warp kernels
+        regenerate the noise at every corner read (po_warp_*_keyed).  All
+        three forms give the same bits."""
         mp = mp.contiguous()
         B = affine.size(0)
         P = mp.size(-1)
         out = torch.empty(B, 3, S, S, device=mp.device)
         imgp = nat.ptr(img.contiguous() if img is not None else None)
-        if isinstance(noise, tuple):
+        ctx.pre = False
+        if isinstance(noise, tuple) and pre_aug:
+            seed, counter, b0 = noise
+            pre = torch.empty(B, 3, P, P, device=mp.device)
+            nat.call("po_augment_patch", nat.ptr(mp), int(seed) & 0xFFFFFFFFFFFFFFFF, int(counter) & 0xFFFFFFFFFFFFFFFF,
+                     int(b0), nat.ptr(contrast), nat.ptr(bright), B, P, nat.ptr(pre), nat.stream())
+            nat.call("po_warp_fwd_pre", imgp, nat.ptr(pre), nat.ptr(affine, torch.float64), B, S, P, mode,
+                     nat.ptr(out), nat.stream())
+            ctx.key, ctx.pre = noise, True
+            ctx.save_for_backward(mp, contrast, bright, affine, pre)
+        elif isinstance(noise, tuple):
             seed, counter, b0 = noise
             nat.call("po_warp_fwd_keyed", imgp, nat.ptr(mp), int(seed) & 0xFFFFFFFFFFFFFFFF,
                      int(counter) & 0xFFFFFFFFFFFFFFFF, int(b0), nat.ptr(contrast), nat.ptr(bright),
@@ -203,7 +217,11 @@ class _Warp(torch.autograd.Function):
         work = torch.empty_like(d_out)
         d_mp = torch.empty_like(mp)
         B, P = affine.size(0), mp.size(-1)
-        if ctx.key is not None:
+        if ctx.pre:
+            pre = ctx.saved_tensors[4]
+            nat.call("po_warp_bwd_pre", nat.ptr(d_out), nat.ptr(pre), nat.ptr(contrast), nat.ptr(affine, torch.float64),
+                     B, ctx.S, P, ctx.mode, nat.ptr(work), nat.ptr(d_mp), nat.stream())
+        elif ctx.key is not None:
             seed, counter, b0 = ctx.key
             nat.call("po_warp_bwd_keyed", nat.ptr(d_out), nat.ptr(mp), int(seed) & 0xFFFFFFFFFFFFFFFF,
                      int(counter) & 0xFFFFFFFFFFFFFFFF, int(b0), nat.ptr(contrast), nat.ptr(bright),
@@ -214,7 +232,7 @@ class _Warp(torch.autograd.Function):
             nat.call("po_warp_bwd", nat.ptr(d_out), nat.ptr(mp), nat.ptr(noise), nat.ptr(contrast),
                      nat.ptr(bright), nat.ptr(affine, torch.float64), B, ctx.S, P, ctx.mode,
                      nat.ptr(work), nat.ptr(d_mp), nat.stream())
-        return d_mp, None, None, None, None, None, None, None
+        return d_mp, None, None, None, None, None, None, None, None
 
 
 class PatchTransformer(nn.Module):
@@ -240,6 +258,9 @@ class PatchTransformer(nn.Module):
         self.draw_step = 0
         self.draw_b0 = 0
         self.keyed_noise = os.environ.get("ADVPATCH_NOISE_KEYED", "1") != "0"
+        # keyed noise through the pre-augmented patches (po_augment_patch +
+        # po_warp_*_pre); ADVPATCH_WARP_PRE=0: regenerate it at every corner read
+        self.pre_aug = os.environ.get("ADVPATCH_WARP_PRE", "1") != "0"
         self.last_roi = None     # [B,4] int32 footprint boxes of the last placement
 
     def lab_transform(self, lab_batch_origin):
@@ -286,7 +307,7 @@ class PatchTransformer(nn.Module):
         """-> (adv_batch_t [B,1,3,S,S], patch_center [B,2] = (x*S, y*S))."""
         mp, d, affine, center = self._prep(adv_patch, lab_batch, img_size, do_rotate, draws)
         out = _Warp.apply(mp, self._noise(d), d["contrast"].contiguous(),
-                          d["bright"].contiguous(), affine, None, int(img_size), 0)
+                          d["bright"].contiguous(), affine, None, int(img_size), 0, self.pre_aug)
         return out.unsqueeze(1), center
 
     def forward_composite(self, adv_patch, lab_batch, img_batch, img_size, do_rotate=True, draws=None):
@@ -295,7 +316,7 @@ class PatchTransformer(nn.Module):
         adv_batch_t."""
         mp, d, affine, center = self._prep(adv_patch, lab_batch, img_size, do_rotate, draws)
         out = _Warp.apply(mp, self._noise(d), d["contrast"].contiguous(),
-                          d["bright"].contiguous(), affine, img_batch.contiguous(), int(img_size), 1)
+                          d["bright"].contiguous(), affine, img_batch.contiguous(), int(img_size), 1, self.pre_aug)
         return out, center
 
 

@@ -33,7 +33,7 @@ typedef void* po_stream_t;
 #define PO_EHIP -2     /* HIP runtime error */
 #define PO_EDEVICE -3  /* device is not gfx950 */
 
-#define PO_ABI_VERSION 17
+#define PO_ABI_VERSION 18
 #define PO_AMAX_SUB 64  /* sub-slots per max|x| slot (see po_conv_desc) */
 
 int po_abi_version(void);
@@ -119,6 +119,20 @@ int po_warp_fwd_keyed(const float* img, const float* patch_mp, uint64_t seed, ui
 int po_warp_bwd_keyed(const float* d_out, const float* patch_mp, uint64_t seed, uint64_t counter, int b0,
                       const float* contrast, const float* bright, const double* affine, int B, int S, int P,
                       int mode, float* work, float* d_patch_mp, po_stream_t s);
+/* The augmentation half of PatchTransformer (load_data.py:548-571) for the
+ * keyed draws, before the clamp: pre [B,3,P,P] = patch_mp * contrast[b] +
+ * bright[b] + 0.1 * noise, the noise being po_draws(seed, counter, b0, ...)'s
+ * value of global image b0 + b (as po_warp_*_keyed).  po_warp_fwd_pre /
+ * po_warp_bwd_pre then gather these values: the same outputs and patch
+ * gradient as po_warp_*_keyed bit for bit, with one Philox call per 4 patch
+ * elements instead of one per bilinear corner read.  po_warp_bwd_pre still
+ * takes contrast (the gradient's factor). */
+int po_augment_patch(const float* patch_mp, uint64_t seed, uint64_t counter, int b0, const float* contrast,
+                     const float* bright, int B, int P, float* pre, po_stream_t s);
+int po_warp_fwd_pre(const float* img, const float* pre, const double* affine, int B, int S, int P, int mode,
+                    float* out, po_stream_t s);
+int po_warp_bwd_pre(const float* d_out, const float* pre, const float* contrast, const double* affine, int B, int S,
+                    int P, int mode, float* work, float* d_patch_mp, po_stream_t s);
 
 /* PatchApplier for an explicit adv tensor: out = where(adv==0, img, adv)
  * (load_data.py:820); n elements. bwd: d_img = d_out*(adv==0), d_adv = d_out*(adv!=0). */

@@ -115,5 +115,11 @@ def test_evaluate_folder_matches_oracle(tmp_path):
         assert (out / "pre_patched" / (stem + ".png")).exists()
     n = sum(len(b) for b in res.values())
     assert us.txt_len_read(str(out / "yolo-labels"))[0] == n
-    m = us.creation_metrics(str(out / "yolo-labels"), str(lab_dir), str(out / "yolo-labels"), str(lab_dir))
+    # the clean frames' detections (an all-zero patch composites nothing: the reference's
+    # clean-image label folders) against the patched ones
+    clean = tmp_path / "clean"
+    ev.evaluate_folder(net, torch.zeros_like(patch).to(DEV), str(img_dir), str(lab_dir), str(clean), 0.4, 0.4,
+                       batch_size=4, seed=seed, save_images=False)
+    m = us.creation_metrics(str(out / "yolo-labels"), str(clean / "yolo-labels"), str(out / "yolo-labels"),
+                            str(clean / "yolo-labels"))
     assert "M1_04" in m and len(m["M4"]) == 15

@@ -277,9 +277,10 @@ def test_warp_bwd_tight_scan_matches_oracle(S, P, B, big):
 @pytest.mark.parametrize("B,S,P,b0", [(6, 608, 224, 0), (5, 416, 224, 37), (3, 97, 33, 2)])
 def test_keyed_noise_warp_bit_identical(B, S, P, b0):
     """po_warp_fwd_keyed / po_warp_bwd_keyed regenerate po_draws' noise in the
-    kernels: the composite, the warp-only output and the patch gradient equal
-    the tensor path fed po_draws' own noise tensor bit for bit (global image
-    index b0 + b, odd S and P included)."""
+    kernels, po_augment_patch + po_warp_*_pre form the augmented patches once
+    from the same key: the composite, the warp-only output and the patch
+    gradient of both equal the tensor path fed po_draws' own noise tensor bit
+    for bit (global image index b0 + b, odd S and P included)."""
     ld, sy = pkg_mod("load_data"), pkg_mod("synthetic")
     seed, step = 0x5EED1234ABCD, 9
     full = sy.draws_device(seed, step, b0, B, P, DEV)
@@ -290,15 +291,17 @@ def test_keyed_noise_warp_bit_identical(B, S, P, b0):
     patch = sy.patch(P, seed=5).to(DEV)
     outs = []
     g = torch.randn(B, 3, S, S, generator=torch.Generator().manual_seed(6)).to(DEV)
-    for dr in (full, keyed):
+    for dr, pre_aug in ((full, False), (keyed, False), (keyed, True)):
         pt = ld.PatchTransformer()
+        pt.pre_aug = pre_aug
         pg = patch.clone().requires_grad_(True)
         comp, _ = pt.forward_composite(pg, lab, img, S, draws=dr)
         comp.backward(g)
         adv, _ = pt(patch, lab, S, draws=dr)
         outs.append((comp.detach(), pg.grad.clone(), adv))
-    for a, b in zip(outs[0], outs[1]):
-        assert torch.equal(a, b)
+    for other in outs[1:]:
+        for a, b in zip(outs[0], other):
+            assert torch.equal(a, b)
     assert (outs[0][0] != img).any()                   # the patch landed somewhere
 
 

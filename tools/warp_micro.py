@@ -72,6 +72,27 @@ def bwd(aff, keyed):
                             nat.ptr(d_mp), st)
 
 
+pre = torch.empty(B, 3, P, P, device=dev)
+
+
+def aug():
+    nat.call("po_augment_patch", nat.ptr(mp), seed, step, 0, nat.ptr(dr["contrast"]), nat.ptr(dr["bright"]), B, P,
+             nat.ptr(pre), st)
+
+
+def fwd_pre(aff):
+    def f():
+        aug()
+        nat.call("po_warp_fwd_pre", nat.ptr(img), nat.ptr(pre), nat.ptr(aff, torch.float64), B, S, P, 1, nat.ptr(out),
+                 st)
+    return f
+
+
+def bwd_pre(aff):
+    return lambda: nat.call("po_warp_bwd_pre", nat.ptr(d_out), nat.ptr(pre), nat.ptr(dr["contrast"]),
+                            nat.ptr(aff, torch.float64), B, S, P, 1, nat.ptr(work), nat.ptr(d_mp), st)
+
+
 copy = lambda: out.copy_(img)
 t = timed(copy)
 print("torch copy_ (img -> out)      %8.1f us  %7.0f GB/s" % (t, (fwd_bytes - 3 * P * P * 4) / t / 1e3))
@@ -80,6 +101,13 @@ for name, aff in (("placed", affine), ("off-frame", off)):
         t = timed(fwd(aff, keyed))
         print("fwd %-9s %-6s            %8.1f us  %7.0f GB/s" % (name, "keyed" if keyed else "tensor", t,
                                                                fwd_bytes / t / 1e3))
+t = timed(aug)
+print("po_augment_patch              %8.1f us" % t)
+for name, aff in (("placed", affine), ("off-frame", off)):
+    t = timed(fwd_pre(aff))
+    print("fwd %-9s pre (+augment)   %8.1f us  %7.0f GB/s" % (name, t, fwd_bytes / t / 1e3))
+    t = timed(bwd_pre(aff))
+    print("bwd %-9s pre              %8.1f us  %7.0f GB/s" % (name, t, bwd_bytes / t / 1e3))
 for name, aff in (("placed", affine), ("off-frame", off)):
     for keyed in (False, True):
         t = timed(bwd(aff, keyed))
