@@ -63,9 +63,9 @@ _SIGS = {
                           c_int, c_int, c_int, c_int, c_void_p, c_void_p],
     "po_augment_patch": [c_void_p, ctypes.c_uint64, ctypes.c_uint64, c_int, c_void_p, c_void_p, c_int, c_int, c_void_p,
                          c_void_p],
-    "po_warp_fwd_pre": [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_void_p],
-    "po_warp_bwd_pre": [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_void_p,
-                        c_void_p],
+    "po_warp_fwd_pre": [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_void_p],
+    "po_warp_bwd_pre": [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_void_p,
+                        c_void_p, c_void_p],
     "po_warp_bwd_keyed": [c_void_p, c_void_p, ctypes.c_uint64, ctypes.c_uint64, c_int, c_void_p, c_void_p, c_void_p,
                           c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p],
     "po_apply_fwd": [c_void_p, c_void_p, c_int64, c_void_p, c_void_p],

@@ -846,6 +846,107 @@ __global__ __launch_bounds__(256) void augment_k(const float* __restrict__ mp, c
     }
   }
 }
+
+// ---- footprint-box form of the warp (po_warp_*_pre with the footprint boxes
+// po_patch_params writes, roi [B][4] = {x0, y0, x1, y1}: no output pixel outside
+// its image's box samples the padded patch region).  The box is widened to whole
+// pixel quads [qx0, qx1) (qx0 = x0 & ~3): warp_quad_copy_k writes the quads
+// outside it (the image in mode 1, zeros in mode 0) as 16-byte copies with no
+// per-pixel geometry, warp_box_fwd_k / warp_box_bwd_a_k run warp_pixel over the
+// box's pixels, one per thread (the footprint is a few percent of the frame:
+// spread over many waves instead of a few heavy quads).  Same per-pixel
+// arithmetic as warp_fwd4_k / warp_bwd_a4_k, so bit-identical outputs.
+struct QBox {
+  int qx0, qx1, y0, y1;
+};
+__device__ __forceinline__ QBox quad_box(const int32_t* roi, int b, int S) {
+  const int4 r = reinterpret_cast<const int4*>(roi)[b];
+  QBox q;
+  q.qx0 = r.x & ~3;
+  q.qx1 = min(S, (r.z + 3) & ~3);
+  q.y0 = r.y;
+  q.y1 = r.w;
+  if (q.qx1 <= q.qx0 || q.y1 <= q.y0) q.qx0 = q.qx1 = q.y0 = q.y1 = 0;
+  return q;
+}
+
+__global__ __launch_bounds__(256) void warp_quad_copy_k(const float* __restrict__ img, const int32_t* __restrict__ roi,
+                                                        int S, int mode, float* __restrict__ out) {
+  const int b = blockIdx.y;
+  const int sq = S >> 2;
+  const int q = blockIdx.x * 256 + threadIdx.x;
+  if (q >= S * sq) return;
+  const int i = q / sq, j0 = (q - i * sq) * 4;
+  const QBox bx = quad_box(roi, b, S);
+  if (i >= bx.y0 && i < bx.y1 && j0 >= bx.qx0 && j0 < bx.qx1) return;    // warp_box_fwd_k's quad
+  const size_t plane = (size_t)S * S;
+  const size_t o = (size_t)b * 3 * plane + (size_t)i * S + j0;
+#pragma unroll
+  for (int ch = 0; ch < 3; ++ch) {
+    const float4 v = mode == 1 ? *reinterpret_cast<const float4*>(img + o + ch * plane) : make_float4(0.f, 0.f, 0.f, 0.f);
+    *reinterpret_cast<float4*>(out + o + ch * plane) = v;
+  }
+}
+
+__global__ __launch_bounds__(256) void warp_box_fwd_k(const float* __restrict__ img, const double* __restrict__ affine,
+                                                      const int32_t* __restrict__ roi, WarpGeom g, int mode,
+                                                      float* __restrict__ out) {
+  const int b = blockIdx.y;
+  const QBox bx = quad_box(roi, b, g.S);
+  const int bw = bx.qx1 - bx.qx0, area = bw * (bx.y1 - bx.y0);
+  const size_t plane = (size_t)g.S * g.S;
+  const NoiseSrc nz = noise_src(nullptr, g, b);
+  for (int p = blockIdx.x * 256 + threadIdx.x; p < area; p += gridDim.x * 256) {
+    const int r = p / bw;
+    const int i = bx.y0 + r, j = bx.qx0 + (p - r * bw);
+    const size_t o = (size_t)b * 3 * plane + (size_t)i * g.S + j;
+    float adv[3], msk;
+    bool rng[3];
+    const bool hit = warp_pixel(affine + 6 * b, g, nullptr, nz, 1.f, 0.f, i, j, adv, msk, rng);
+#pragma unroll
+    for (int ch = 0; ch < 3; ++ch) {
+      float v = hit ? adv[ch] * msk : 0.f;                       // load_data.py:791-792
+      if (mode == 1) v = (v == 0.f) ? img[o + ch * plane] : v;   // load_data.py:820
+      out[o + ch * plane] = v;
+    }
+  }
+}
+
+// phase A of the backward over the footprint box only (phase B reads gfac at
+// footprint pixels only)
+__global__ __launch_bounds__(256) void warp_box_bwd_a_k(const float* __restrict__ d_out,
+                                                        const float* __restrict__ contrast,
+                                                        const double* __restrict__ affine,
+                                                        const int32_t* __restrict__ roi, WarpGeom g, int mode,
+                                                        float* __restrict__ gfac) {
+  const int b = blockIdx.y;
+  const QBox bx = quad_box(roi, b, g.S);
+  const int bw = bx.qx1 - bx.qx0, area = bw * (bx.y1 - bx.y0);
+  const size_t plane = (size_t)g.S * g.S;
+  const NoiseSrc nz = noise_src(nullptr, g, b);
+  const float cb = contrast[b];
+  for (int p = blockIdx.x * 256 + threadIdx.x; p < area; p += gridDim.x * 256) {
+    const int r = p / bw;
+    const int i = bx.y0 + r, j = bx.qx0 + (p - r * bw);
+    const size_t o = (size_t)b * 3 * plane + (size_t)i * g.S + j;
+    float adv[3], msk;
+    bool rng[3];
+    if (!warp_pixel(affine + 6 * b, g, nullptr, nz, cb, 0.f, i, j, adv, msk, rng)) continue;
+#pragma unroll
+    for (int ch = 0; ch < 3; ++ch) {
+      const float outv = adv[ch] * msk;
+      float gv = d_out[o + ch * plane];
+      if (mode == 1 && outv == 0.f) gv = 0.f;
+      gv = gv * msk;
+      if (!rng[ch]) gv = 0.f;
+      gfac[o + ch * plane] = gv;
+    }
+  }
+}
+
+// workgroups per image of the box kernels: enough for a box of an eighth of the
+// frame in one pass (a larger box loops)
+__host__ inline int box_blocks(int S) { return po::ceil_div(po::ceil_div((int64_t)S * S, 8), 256); }
 }  // namespace
 
 extern "C" int po_augment_patch(const float* patch_mp, uint64_t seed, uint64_t counter, int b0, const float* contrast,
@@ -859,26 +960,41 @@ extern "C" int po_augment_patch(const float* patch_mp, uint64_t seed, uint64_t c
   return po::check_launch("po_augment_patch");
 }
 
-extern "C" int po_warp_fwd_pre(const float* img, const float* pre, const double* affine, int B, int S, int P, int mode, float* out,
-                               po_stream_t s) {
-  PO_REQUIRE(pre && affine && out, "po_warp_fwd_pre: null pointer");
+extern "C" int po_warp_fwd_pre(const float* img, const float* pre, const double* affine, const int32_t* roi, int B,
+                               int S, int P, int mode, float* out, po_stream_t s) {
+  PO_REQUIRE(pre && affine && roi && out, "po_warp_fwd_pre: null pointer");
   PO_REQUIRE(mode == 0 || (mode == 1 && img), "po_warp_fwd_pre: mode must be 0 or 1 (1 needs img)");
   PO_REQUIRE(B > 0 && S > 1 && P > 0 && P <= S, "po_warp_fwd_pre: bad shape B=%d S=%d P=%d", B, S, P);
-  PO_REQUIRE(3LL * P * P < (1LL << 31), "po_warp_fwd_pre: patch too large");
+  PO_REQUIRE(3LL * P * P < (1LL << 31) && (int64_t)B * 3 * S * S < (1LL << 40), "po_warp_fwd_pre: too large");
   WarpGeom g = make_geom(S, P);
   g.pre = pre;
-  return warp_fwd(img, pre, nullptr, nullptr, nullptr, affine, B, S, mode, out, g, s);
+  if (S % 4 != 0 || ((uintptr_t)img | (uintptr_t)out) % 16 != 0)      // whole-frame one-pixel kernel
+    return warp_fwd(img, pre, nullptr, nullptr, nullptr, affine, B, S, mode, out, g, s);
+  hipStream_t st = po::stream_of(s);
+  hipLaunchKernelGGL(warp_quad_copy_k, dim3(po::ceil_div(S * (S / 4), 256), B), dim3(256), 0, st, img, roi, S, mode,
+                     out);
+  hipLaunchKernelGGL(warp_box_fwd_k, dim3(box_blocks(S), B), dim3(256), 0, st, img, affine, roi, g, mode, out);
+  return po::check_launch("po_warp_fwd_pre");
 }
 
-extern "C" int po_warp_bwd_pre(const float* d_out, const float* pre, const float* contrast, const double* affine, int B,
-                               int S, int P, int mode, float* work, float* d_patch_mp, po_stream_t s) {
-  PO_REQUIRE(d_out && pre && contrast && affine && work && d_patch_mp, "po_warp_bwd_pre: null pointer");
+extern "C" int po_warp_bwd_pre(const float* d_out, const float* pre, const float* contrast, const double* affine,
+                               const int32_t* roi, int B, int S, int P, int mode, float* work, float* d_patch_mp,
+                               po_stream_t s) {
+  PO_REQUIRE(d_out && pre && contrast && affine && roi && work && d_patch_mp, "po_warp_bwd_pre: null pointer");
   PO_REQUIRE(mode == 0 || mode == 1, "po_warp_bwd_pre: mode must be 0 or 1");
   PO_REQUIRE(B > 0 && S > 1 && P > 0 && P <= S, "po_warp_bwd_pre: bad shape");
   PO_REQUIRE(3LL * P * P < (1LL << 31), "po_warp_bwd_pre: patch too large");
+  PO_REQUIRE(work != d_out, "po_warp_bwd_pre: work may not alias d_out");
   WarpGeom g = make_geom(S, P);
   g.pre = pre;
-  return warp_bwd(d_out, pre, nullptr, contrast, nullptr, affine, B, S, P, mode, work, d_patch_mp, g, s);
+  hipStream_t st = po::stream_of(s);
+  hipLaunchKernelGGL(warp_box_bwd_a_k, dim3(box_blocks(S), B), dim3(256), 0, st, d_out, contrast, affine, roi, g, mode,
+                     work);
+  int rc = po::check_launch("po_warp_bwd_pre(a)");
+  if (rc) return rc;
+  hipLaunchKernelGGL(warp_bwd_b_k, dim3(po::ceil_div(P * P, WB_EL)), dim3(256), 0, st, work, pre, nullptr, contrast,
+                     nullptr, affine, g, B, d_patch_mp);
+  return po::check_launch("po_warp_bwd_pre(b)");
 }
 
 extern "C" int po_warp_composite_multi(const float* img, const float* patch_mp, const float* noise,

@@ -172,7 +172,7 @@ class _Warp(torch.autograd.Function):
     """Augment + warp + clamp*mask (mode 0) or + composite onto img (mode 1)."""
 
     @staticmethod
-    def forward(ctx, mp, noise, contrast, bright, affine, img, S, mode, pre_aug=True):
+    def forward(ctx, mp, noise, contrast, bright, affine, img, S, mode, pre_aug=True, roi=None):
         """``noise``: the [B,3,P,P] tensor, or a po_draws key (seed, counter,
         b0) — the noise is then regenerated from the key and no noise tensor
         exists: with ``pre_aug`` (default) po_augment_patch forms the
@@ -186,15 +186,15 @@ class _Warp(torch.autograd.Function):
         out = torch.empty(B, 3, S, S, device=mp.device)
         imgp = nat.ptr(img.contiguous() if img is not None else None)
         ctx.pre = False
-        if isinstance(noise, tuple) and pre_aug:
+        if isinstance(noise, tuple) and pre_aug and roi is not None:
             seed, counter, b0 = noise
             pre = torch.empty(B, 3, P, P, device=mp.device)
             nat.call("po_augment_patch", nat.ptr(mp), int(seed) & 0xFFFFFFFFFFFFFFFF, int(counter) & 0xFFFFFFFFFFFFFFFF,
                      int(b0), nat.ptr(contrast), nat.ptr(bright), B, P, nat.ptr(pre), nat.stream())
-            nat.call("po_warp_fwd_pre", imgp, nat.ptr(pre), nat.ptr(affine, torch.float64), B, S, P, mode,
-                     nat.ptr(out), nat.stream())
+            nat.call("po_warp_fwd_pre", imgp, nat.ptr(pre), nat.ptr(affine, torch.float64), nat.ptr(roi, torch.int32),
+                     B, S, P, mode, nat.ptr(out), nat.stream())
             ctx.key, ctx.pre = noise, True
-            ctx.save_for_backward(mp, contrast, bright, affine, pre)
+            ctx.save_for_backward(mp, contrast, bright, affine, pre, roi)
         elif isinstance(noise, tuple):
             seed, counter, b0 = noise
             nat.call("po_warp_fwd_keyed", imgp, nat.ptr(mp), int(seed) & 0xFFFFFFFFFFFFFFFF,
@@ -218,9 +218,9 @@ class _Warp(torch.autograd.Function):
         d_mp = torch.empty_like(mp)
         B, P = affine.size(0), mp.size(-1)
         if ctx.pre:
-            pre = ctx.saved_tensors[4]
+            pre, roi = ctx.saved_tensors[4:6]
             nat.call("po_warp_bwd_pre", nat.ptr(d_out), nat.ptr(pre), nat.ptr(contrast), nat.ptr(affine, torch.float64),
-                     B, ctx.S, P, ctx.mode, nat.ptr(work), nat.ptr(d_mp), nat.stream())
+                     nat.ptr(roi, torch.int32), B, ctx.S, P, ctx.mode, nat.ptr(work), nat.ptr(d_mp), nat.stream())
         elif ctx.key is not None:
             seed, counter, b0 = ctx.key
             nat.call("po_warp_bwd_keyed", nat.ptr(d_out), nat.ptr(mp), int(seed) & 0xFFFFFFFFFFFFFFFF,
@@ -232,7 +232,7 @@ class _Warp(torch.autograd.Function):
             nat.call("po_warp_bwd", nat.ptr(d_out), nat.ptr(mp), nat.ptr(noise), nat.ptr(contrast),
                      nat.ptr(bright), nat.ptr(affine, torch.float64), B, ctx.S, P, ctx.mode,
                      nat.ptr(work), nat.ptr(d_mp), nat.stream())
-        return d_mp, None, None, None, None, None, None, None, None
+        return d_mp, None, None, None, None, None, None, None, None, None
 
 
 class PatchTransformer(nn.Module):
@@ -307,7 +307,7 @@ class PatchTransformer(nn.Module):
         """-> (adv_batch_t [B,1,3,S,S], patch_center [B,2] = (x*S, y*S))."""
         mp, d, affine, center = self._prep(adv_patch, lab_batch, img_size, do_rotate, draws)
         out = _Warp.apply(mp, self._noise(d), d["contrast"].contiguous(),
-                          d["bright"].contiguous(), affine, None, int(img_size), 0, self.pre_aug)
+                          d["bright"].contiguous(), affine, None, int(img_size), 0, self.pre_aug, self.last_roi)
         return out.unsqueeze(1), center
 
     def forward_composite(self, adv_patch, lab_batch, img_batch, img_size, do_rotate=True, draws=None):
@@ -316,7 +316,8 @@ class PatchTransformer(nn.Module):
         adv_batch_t."""
         mp, d, affine, center = self._prep(adv_patch, lab_batch, img_size, do_rotate, draws)
         out = _Warp.apply(mp, self._noise(d), d["contrast"].contiguous(),
-                          d["bright"].contiguous(), affine, img_batch.contiguous(), int(img_size), 1, self.pre_aug)
+                          d["bright"].contiguous(), affine, img_batch.contiguous(), int(img_size), 1, self.pre_aug,
+                          self.last_roi)
         return out, center
 
 

@@ -126,13 +126,17 @@ int po_warp_bwd_keyed(const float* d_out, const float* patch_mp, uint64_t seed, 
  * po_warp_bwd_pre then gather these values: the same outputs and patch
  * gradient as po_warp_*_keyed bit for bit, with one Philox call per 4 patch
  * elements instead of one per bilinear corner read.  po_warp_bwd_pre still
- * takes contrast (the gradient's factor). */
+ * takes contrast (the gradient's factor).  roi [B][4] = po_patch_params' footprint
+ * boxes {x0, y0, x1, y1}: the pixels outside an image's box are written as
+ * 16-byte copies of img (mode 1) or zeros (mode 0) without per-pixel geometry,
+ * the box's pixels one per thread; the backward's per-pixel phase runs over the
+ * boxes only (`work` must not alias d_out). */
 int po_augment_patch(const float* patch_mp, uint64_t seed, uint64_t counter, int b0, const float* contrast,
                      const float* bright, int B, int P, float* pre, po_stream_t s);
-int po_warp_fwd_pre(const float* img, const float* pre, const double* affine, int B, int S, int P, int mode,
-                    float* out, po_stream_t s);
-int po_warp_bwd_pre(const float* d_out, const float* pre, const float* contrast, const double* affine, int B, int S,
-                    int P, int mode, float* work, float* d_patch_mp, po_stream_t s);
+int po_warp_fwd_pre(const float* img, const float* pre, const double* affine, const int32_t* roi, int B, int S,
+                    int P, int mode, float* out, po_stream_t s);
+int po_warp_bwd_pre(const float* d_out, const float* pre, const float* contrast, const double* affine,
+                    const int32_t* roi, int B, int S, int P, int mode, float* work, float* d_patch_mp, po_stream_t s);
 
 /* PatchApplier for an explicit adv tensor: out = where(adv==0, img, adv)
  * (load_data.py:820); n elements. bwd: d_img = d_out*(adv==0), d_adv = d_out*(adv!=0). */

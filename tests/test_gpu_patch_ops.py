@@ -274,20 +274,25 @@ def test_warp_bwd_tight_scan_matches_oracle(S, P, B, big):
     assert err <= 1e-4, err
 
 
-@pytest.mark.parametrize("B,S,P,b0", [(6, 608, 224, 0), (5, 416, 224, 37), (3, 97, 33, 2)])
-def test_keyed_noise_warp_bit_identical(B, S, P, b0):
+@pytest.mark.parametrize("B,S,P,b0,big", [(6, 608, 224, 0, False), (5, 416, 224, 37, False), (3, 97, 33, 2, False),
+                                          (4, 96, 32, 5, True)])
+def test_keyed_noise_warp_bit_identical(B, S, P, b0, big):
     """po_warp_fwd_keyed / po_warp_bwd_keyed regenerate po_draws' noise in the
     kernels, po_augment_patch + po_warp_*_pre form the augmented patches once
     from the same key: the composite, the warp-only output and the patch
     gradient of both equal the tensor path fed po_draws' own noise tensor bit
-    for bit (global image index b0 + b, odd S and P included)."""
+    for bit (global image index b0 + b, odd S and P included; ``big``: magnified
+    patches whose footprint boxes exceed the box kernels' one-pass grid)."""
     ld, sy = pkg_mod("load_data"), pkg_mod("synthetic")
     seed, step = 0x5EED1234ABCD, 9
     full = sy.draws_device(seed, step, b0, B, P, DEV)
     keyed = {k: v for k, v in full.items() if k != "noise"}
     keyed["noise_key"] = (seed, step, b0)
     img = sy.frames(B, S, seed=3).to(DEV)
-    lab = sy.labels(B, seed=4).to(DEV)
+    lab = sy.labels(B, seed=4)
+    if big:
+        lab[:, :, 3:5] = lab[:, :, 3:5].clamp(min=0.6)
+    lab = lab.to(DEV)
     patch = sy.patch(P, seed=5).to(DEV)
     outs = []
     g = torch.randn(B, 3, S, S, generator=torch.Generator().manual_seed(6)).to(DEV)

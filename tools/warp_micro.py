@@ -31,6 +31,7 @@ mp = sy.patch(P, seed=5).to(dev).contiguous()
 _, _, _, roi, affine = ld.patch_params(lab, S, P, dr, True, with_roi=True)
 off = affine.clone()
 off[:, 2] += 4 * S                      # every sample point far right of the patch: no footprint pixel
+roi_off = torch.zeros_like(roi)          # ... and an empty footprint box
 out = torch.empty(B, 3, S, S, device=dev)
 work = torch.empty(B, 3, S, S, device=dev)
 d_out = torch.randn(B, 3, S, S, device=dev)
@@ -83,14 +84,15 @@ def aug():
 def fwd_pre(aff):
     def f():
         aug()
-        nat.call("po_warp_fwd_pre", nat.ptr(img), nat.ptr(pre), nat.ptr(aff, torch.float64), B, S, P, 1, nat.ptr(out),
-                 st)
+        nat.call("po_warp_fwd_pre", nat.ptr(img), nat.ptr(pre), nat.ptr(aff, torch.float64),
+                 nat.ptr(roi if aff is affine else roi_off, torch.int32), B, S, P, 1, nat.ptr(out), st)
     return f
 
 
 def bwd_pre(aff):
     return lambda: nat.call("po_warp_bwd_pre", nat.ptr(d_out), nat.ptr(pre), nat.ptr(dr["contrast"]),
-                            nat.ptr(aff, torch.float64), B, S, P, 1, nat.ptr(work), nat.ptr(d_mp), st)
+                            nat.ptr(aff, torch.float64), nat.ptr(roi if aff is affine else roi_off, torch.int32),
+                            B, S, P, 1, nat.ptr(work), nat.ptr(d_mp), st)
 
 
 copy = lambda: out.copy_(img)
