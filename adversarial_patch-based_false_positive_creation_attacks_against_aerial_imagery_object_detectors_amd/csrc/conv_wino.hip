@@ -1092,6 +1092,15 @@ __global__ __launch_bounds__(256, 2) void conv_wino3_k(const ConvArgs a, const f
 // 8h + s) and epilogue arithmetic as tiles 65/66: bit-identical outputs.
 // Split-K (blockIdx.y = slice) and the fused pool epilogue as tile 66.
 constexpr int T4 = 64, N4 = 64;
+#ifdef PO_WINO_STAMP
+// diagnostic build only (tools/wino_phases.py): per-workgroup s_memrealtime
+// stamps of conv_wino4_k's phases (start, k-loop entry, k-loop exit, end)
+__device__ unsigned long long g_wino_stamp[1 << 16][8];
+#define PO_STAMP(k) do { if (threadIdx.x == 0 && wgid < (1 << 16) && blockIdx.y == 0) { \
+    g_wino_stamp[wgid][k] = __builtin_amdgcn_s_memrealtime(); g_wino_stamp[wgid][4 + k] = __builtin_amdgcn_s_memtime(); } } while (0)
+#else
+#define PO_STAMP(k) do { } while (0)
+#endif
 constexpr int V4_FLOATS = 16 * T4 * WK;                 // one transformed buffer: 64 KB
 __device__ __forceinline__ int v4idx(int xi, int t, int ch) { return ((xi * T4 + t) * WK) + ((ch ^ ((t >> 2) & 3)) << 2); }
 
@@ -1107,6 +1116,7 @@ __global__ __launch_bounds__(512, 1) void conv_wino4_k(const ConvArgs a, const f
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wave_u = __builtin_amdgcn_readfirstlane(wave);
   const int h = lane >> 5;
+  PO_STAMP(0);
 
   if (tid == 0) s_live = 0;
   __syncthreads();
@@ -1220,6 +1230,7 @@ __global__ __launch_bounds__(512, 1) void conv_wino4_k(const ConvArgs a, const f
     bload(1, ks0);
     __builtin_amdgcn_sched_barrier(0);
     __syncthreads();
+    PO_STAMP(1);
     int ks = ks0;
     do {
       float* Vc = smem + ((ks - ks0) & 1) * V4_FLOATS;
@@ -1246,6 +1257,7 @@ __global__ __launch_bounds__(512, 1) void conv_wino4_k(const ConvArgs a, const f
     bload(1, ks0);
     __builtin_amdgcn_sched_barrier(0);
     __syncthreads();
+    PO_STAMP(1);
     int ks = ks0;
     do {                                     // ks1 > ks0: every slice has a k-step (host check); no
       float* Vc = smem + ((ks - ks0) & 1) * V4_FLOATS;    // zero-trip test to sink the prologue loads into
@@ -1272,6 +1284,7 @@ __global__ __launch_bounds__(512, 1) void conv_wino4_k(const ConvArgs a, const f
     } while (++ks < ks1);
   }
 
+  PO_STAMP(2);
 
   // ---- epilogue, two passes of 32 tiles (pass = M-block mb): M[xi][tile - 32 pass][64 ch]
   // in the 128 KB of the V buffers; thread tid owns tile tid >> 4 of the pass, channels n4 .. n4+3
@@ -1400,6 +1413,7 @@ __global__ __launch_bounds__(512, 1) void conv_wino4_k(const ConvArgs a, const f
       }
     }
   }
+  PO_STAMP(3);
   if (a.ksplit > 1) return;                // conv_reduce_k commits the max|x| slots
   if (a.y_amax) po::amax_commit(a.y_amax, mx.y);
   if (a.sum_amax) po::amax_commit(a.sum_amax, mx.s);
@@ -1480,4 +1494,9 @@ int launch_wino4(const ConvArgs& a, const float* U, hipStream_t st, bool stagger
     hipLaunchKernelGGL(conv_wino4_k<false>, dim3(ntm * b.ntiles_n, a.ksplit), dim3(512), 0, st, b, U, Ht, Wt);
   return check_launch("po_conv (winograd 64x64)");
 }
+#ifdef PO_WINO_STAMP
+extern "C" int po_debug_wino_stamps(unsigned long long* host, int n) {
+  return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_wino_stamp), (size_t)n * 64) == hipSuccess ? 0 : -1;
+}
+#endif
 }  // namespace po

@@ -283,8 +283,11 @@ def test_windowed_plan_matches_full_maps(tmp_path, cfg, B, P):
     for k in ("loss", "no_obj_loss", "no_cls_loss"):
         assert abs(float(t0[k]) - float(t1[k])) <= 1e-5 * max(1.0, abs(float(t0[k]))), (k, float(t0[k]), float(t1[k]))
     torch.testing.assert_close(t1["obj"], t0["obj"], rtol=0, atol=1e-5)
+    # two fp32 evaluations, each held to 1e-4 of float64 by the branch-aligned
+    # tests (test_gpu_train): their difference is bounded by the sum, 2e-4
+    # (yolov3 B=3 measured 1.07e-4 with box-tuned Winograd tiles on both sides)
     rel = float((g0 - g1).abs().max() / g0.abs().max())
-    assert rel < 1e-4, rel
+    assert rel < 2e-4, rel
 
 
 @pytest.mark.parametrize("cfg,B,P", [("builtin:mini3", 4, 32), ("builtin:yolov3-dota", 2, 224)])
