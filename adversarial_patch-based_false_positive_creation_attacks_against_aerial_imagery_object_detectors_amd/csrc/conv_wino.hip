@@ -1095,9 +1095,12 @@ constexpr int T4 = 64, N4 = 64;
 #ifdef PO_WINO_STAMP
 // diagnostic build only (tools/wino_phases.py): per-workgroup s_memrealtime
 // stamps of conv_wino4_k's phases (start, k-loop entry, k-loop exit, end)
-__device__ unsigned long long g_wino_stamp[1 << 16][8];
+__device__ unsigned long long g_wino_stamp[1 << 16][16];
+// slots 0-9: s_memrealtime at start, k-loop entry, k-loop exit, epilogue pass
+// steps (3 per pass), end; slots 10/11: s_memtime at k-loop entry/exit
 #define PO_STAMP(k) do { if (threadIdx.x == 0 && wgid < (1 << 16) && blockIdx.y == 0) { \
-    g_wino_stamp[wgid][k] = __builtin_amdgcn_s_memrealtime(); g_wino_stamp[wgid][4 + k] = __builtin_amdgcn_s_memtime(); } } while (0)
+    g_wino_stamp[wgid][k] = __builtin_amdgcn_s_memrealtime(); \
+    if ((k) == 1 || (k) == 2) g_wino_stamp[wgid][9 + (k)] = __builtin_amdgcn_s_memtime(); } } while (0)
 #else
 #define PO_STAMP(k) do { } while (0)
 #endif
@@ -1323,6 +1326,7 @@ __global__ __launch_bounds__(512, 1) void conv_wino4_k(const ConvArgs a, const f
       }
     }
     __syncthreads();                       // the k-loop's (or the previous pass's) LDS reads are done
+    PO_STAMP(3 + 3 * pass);
 #pragma unroll
     for (int c = 0; c < CPW; ++c)
 #pragma unroll
@@ -1333,6 +1337,7 @@ __global__ __launch_bounds__(512, 1) void conv_wino4_k(const ConvArgs a, const f
           M[((wave * CPW + c) * TH + t) * N4 + nb * 32 + (lane & 31)] = acc[c][pass][nb][e];
         }
     __syncthreads();
+    PO_STAMP(4 + 3 * pass);
     const int t = tid >> 4;
     float4 s0[4], s1[4];
 #pragma unroll
@@ -1346,6 +1351,7 @@ __global__ __launch_bounds__(512, 1) void conv_wino4_k(const ConvArgs a, const f
     }
     const float4 yv[2][2] = {{f4add(f4add(s0[0], s0[1]), s0[2]), f4sub(f4sub(s0[1], s0[2]), s0[3])},
                              {f4add(f4add(s1[0], s1[1]), s1[2]), f4sub(f4sub(s1[1], s1[2]), s1[3])}};
+    PO_STAMP(5 + 3 * pass);
     if (a.ksplit > 1) {
       // split-K slice: the raw inverse-transformed partial sums at the GEMM rows
       // conv_reduce_k enumerates (grid_point: row-major over the map, or over
@@ -1413,7 +1419,7 @@ __global__ __launch_bounds__(512, 1) void conv_wino4_k(const ConvArgs a, const f
       }
     }
   }
-  PO_STAMP(3);
+  PO_STAMP(9);
   if (a.ksplit > 1) return;                // conv_reduce_k commits the max|x| slots
   if (a.y_amax) po::amax_commit(a.y_amax, mx.y);
   if (a.sum_amax) po::amax_commit(a.sum_amax, mx.s);
@@ -1496,7 +1502,7 @@ int launch_wino4(const ConvArgs& a, const float* U, hipStream_t st, bool stagger
 }
 #ifdef PO_WINO_STAMP
 extern "C" int po_debug_wino_stamps(unsigned long long* host, int n) {
-  return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_wino_stamp), (size_t)n * 64) == hipSuccess ? 0 : -1;
+  return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_wino_stamp), (size_t)n * 128) == hipSuccess ? 0 : -1;
 }
 #endif
 }  // namespace po

@@ -36,11 +36,12 @@ for _ in range(5):
 torch.cuda.synchronize()
 Ht = (H + 1) // 2
 nwg = -(-(B * Ht * Ht) // 64) * (Cout // 64)
-buf = np.zeros((nwg, 8), dtype=np.uint64)
+buf = np.zeros((nwg, 16), dtype=np.uint64)
 lib = ctypes.CDLL(nat.LIB_PATH)
 assert lib.po_debug_wino_stamps(buf.ctypes.data_as(ctypes.c_void_p), nwg) == 0
-cyc = buf[:, 4:].astype(np.float64)
-buf = buf[:, :4]
+cyc = buf[:, 10:12].astype(np.float64)
+sub = (buf[:, :10].astype(np.float64) - buf[:, :1].astype(np.float64)) / 100.0
+buf = buf[:, [0, 1, 2, 9]]
 t = (buf.astype(np.float64) - float(buf[:, 0].min())) / 100.0      # 100 MHz -> us
 pro, kl, epi = t[:, 1] - t[:, 0], t[:, 2] - t[:, 1], t[:, 3] - t[:, 2]
 span = t[:, 3].max()
@@ -52,6 +53,10 @@ print("  per workgroup: prologue %.2f us, k-loop %.2f us (%.3f us/k-step), epilo
 print("  p10/p90 total %.2f / %.2f us; concurrent workgroups mean %.0f max %d; last start %.1f us" % (
     np.percentile(t[:, 3] - t[:, 0], 10), np.percentile(t[:, 3] - t[:, 0], 90), np.mean(conc), max(conc),
     t[:, 0].max()))
-ghz = (cyc[:, 2] - cyc[:, 1]) / (t[:, 2] - t[:, 1]) / 1e3
+ghz = (cyc[:, 1] - cyc[:, 0]) / (t[:, 2] - t[:, 1]) / 1e3
 print("  shader clock in the k-loop %.2f GHz (p10 %.2f, p90 %.2f): %.0f cycles per k-step per SIMD (MFMA floor 8192)" % (
     np.median(ghz), np.percentile(ghz, 10), np.percentile(ghz, 90), np.median(ghz) * 1e3 * kl.mean() / (Cin // 16)))
+names = ["loop exit", "p0 loads+sync", "p0 LDS dump+sync", "p0 inverse", "p1 sync", "p1 LDS dump+sync", "p1 inverse",
+         "stores+end"]
+d = np.diff(sub[:, 2:10], axis=1).mean(axis=0)
+print("  epilogue steps (us): " + ", ".join("%s %.2f" % (n, v) for n, v in zip(names[1:], d)))
