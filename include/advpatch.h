@@ -33,7 +33,7 @@ typedef void* po_stream_t;
 #define PO_EHIP -2     /* HIP runtime error */
 #define PO_EDEVICE -3  /* device is not gfx950 */
 
-#define PO_ABI_VERSION 18
+#define PO_ABI_VERSION 19
 #define PO_AMAX_SUB 64  /* sub-slots per max|x| slot (see po_conv_desc) */
 
 int po_abi_version(void);
@@ -415,7 +415,7 @@ typedef struct po_conv_desc {
   int8_t* pool_argmax;
 } po_conv_desc;
 
-#define PO_CONV_NTILES 68
+#define PO_CONV_NTILES 69
 /* Tile `t` (1-based): block rows BM (output pixels), block columns BN (output
  * channels), k-step BK (input channels).  Tiles 1..10 stage operands through
  * registers, 11..20 are the same shapes staged by LDS-DMA, 27 a 128x256
@@ -433,6 +433,11 @@ typedef struct po_conv_desc {
  * 65/66; 68: 67 with the two waves of every SIMD staggered; 16 input channels
  * per k-step) for stride-1 3x3 convs and their input gradients on full maps,
  * without split-K except on 66/67/68 (needs Wwino; 65..68 need N % 64 == 0).
+ * 69 (exact fp32, ABI 19) is a persistent direct kernel for a stride-1 3x3
+ * conv with Cin_p = 16, N = 32 and pool_y set (full even maps, no split-K, no
+ * boxes, only the pooled outputs): 8 x 16-pixel tiles whose input patch is
+ * staged once, weights held in registers, pool in registers; bit-identical
+ * to the generic tiles.
  * Retired tiles (21..26, 28, 62..64: never selected by a tuner run) keep their
  * numbers; po_conv_tile_info reports them with *prec = -1 and po_conv refuses
  * them.  A tile that does not apply to a launch makes po_conv return

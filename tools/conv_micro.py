@@ -48,7 +48,12 @@ if os.environ.get("MICRO_RES") == "1":                 # fused shortcut epilogue
     sm = torch.empty_like(res)
     bits = torch.empty(B * Ho * Ho * (Cout // 32), dtype=torch.int32, device=dev)
     d.ybits = bits.data_ptr()
-args = (ctypes.byref(d), nat.ptr(x), nat.ptr(w, w.dtype), nat.ptr(b), nat.ptr(y), nat.ptr(res), nat.ptr(sm), None,
+yp = y
+if os.environ.get("MICRO_POOL") == "1":                # fused 2x2/2 max pool: only the pooled outputs
+    pool = torch.empty(B, Ho // 2, Ho // 2, Cout, device=dev)
+    pam = torch.empty(B, Ho // 2, Ho // 2, Cout, dtype=torch.int8, device=dev)
+    d.pool_y, d.pool_argmax, yp = pool.data_ptr(), pam.data_ptr(), None
+args = (ctypes.byref(d), nat.ptr(x), nat.ptr(w, w.dtype), nat.ptr(b), nat.ptr(yp), nat.ptr(res), nat.ptr(sm), None,
         None, None)
 st = nat.stream()
 for _ in range(3):
