@@ -9,7 +9,8 @@ import os
 import torch
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libadvpatch_hip.so")
+# ADVPATCH_LIB: an ablation build (tools/build_variant.sh) for A/B measurements only
+LIB_PATH = os.environ.get("ADVPATCH_LIB") or os.path.join(_HERE, "libadvpatch_hip.so")
 
 c_int, c_float, c_int64, c_void_p = ctypes.c_int, ctypes.c_float, ctypes.c_int64, ctypes.c_void_p
 
