@@ -26,7 +26,7 @@ inline int ceil_div(int64_t a, int64_t b) { return (int)((a + b - 1) / b); }
 // leaky'(y) for LeakyReLU(0.1): PyTorch leaky_relu_backward uses x > 0
 // (y and x share sign), slope 0.1 otherwise.
 __device__ __forceinline__ float leaky_grad(float y) { return y > 0.f ? 1.f : 0.1f; }
-__device__ __forceinline__ float leaky(float v) { return v > 0.f ? v : v * 0.1f; }
+__device__ __forceinline__ float leaky(float v) { return fmaxf(v, v * 0.1f); }   // = (v > 0 ? v : 0.1 v), NaN and signed zeros included
 
 // torch.div(a, b, rounding_mode='floor') for float32 (ATen div_floor)
 __device__ __forceinline__ float div_floor(float a, float b) {

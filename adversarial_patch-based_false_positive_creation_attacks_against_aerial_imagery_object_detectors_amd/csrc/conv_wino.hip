@@ -74,9 +74,9 @@ __device__ __forceinline__ int vidx(int xi, int t, int ch) { return ((xi * WT + 
 struct EpiMax {
   float y = 0.f, s = 0.f, y2 = 0.f;
 };
-__device__ __forceinline__ float epi_store(const ConvArgs& a, size_t pix, int n, float v, EpiMax& mx) {
-  const size_t o = pix * (size_t)a.Cout_p + n;
-  const size_t wo = pix * (size_t)(a.Cout_p >> 5) + (n >> 5);
+__device__ __forceinline__ float epi_store(const ConvArgs& a, uint32_t pix, int n, float v, EpiMax& mx) {
+  const uint32_t o = pix * (uint32_t)a.Cout_p + n;
+  const uint32_t wo = pix * (uint32_t)(a.Cout_p >> 5) + (n >> 5);
   float x = v + (a.bias ? a.bias[n] : 0.f);
   if (a.act) x = po::leaky(x);
   if (a.accumulate) x += a.y[o];
@@ -110,9 +110,9 @@ struct EpiIn {
 // epi_store with the inputs loaded ahead (same arithmetic, same order)
 // (bias_n = the channel's bias, loaded once per thread: a load here would be
 // re-issued after every store, which may alias it)
-__device__ __forceinline__ float epi_store_in(const ConvArgs& a, size_t pix, int n, float v, float bias_n,
+__device__ __forceinline__ float epi_store_in(const ConvArgs& a, uint32_t pix, int n, float v, float bias_n,
                                               const EpiIn& e, EpiMax& mx) {
-  const size_t o = pix * (size_t)a.Cout_p + n;
+  const uint32_t o = pix * (uint32_t)a.Cout_p + n;
   float x = v + bias_n;
   if (a.act) x = po::leaky(x);
   if (a.accumulate) x += e.yold;
@@ -142,9 +142,9 @@ struct EpiIn4 {
   uint32_t m = 0u, m2 = 0u;
 };
 
-__device__ __forceinline__ float4 epi_store4(const ConvArgs& a, size_t pix, int n, float4 v, float4 bias_n,
+__device__ __forceinline__ float4 epi_store4(const ConvArgs& a, uint32_t pix, int n, float4 v, float4 bias_n,
                                              const EpiIn4& e, EpiMax& mx) {
-  const size_t o = pix * (size_t)a.Cout_p + n;
+  const uint32_t o = pix * (uint32_t)a.Cout_p + n;
   float x[4] = {v.x + bias_n.x, v.y + bias_n.y, v.z + bias_n.z, v.w + bias_n.w};
   if (a.act) {
 #pragma unroll
@@ -349,7 +349,7 @@ __global__ __launch_bounds__(256) void conv_wino_k(const ConvArgs a, const float
         }
         if (a.act) arg |= 8u | (pv > 0.f ? 0u : 4u);
         mx.y = fmaxf(mx.y, fabsf(pv));
-        const size_t po = (((size_t)bb * (a.Hout >> 1) + tti) * (a.Wout >> 1) + ttj) * a.Cout_p + n;
+        const uint32_t po = (((uint32_t)bb * (a.Hout >> 1) + tti) * (a.Wout >> 1) + ttj) * a.Cout_p + n;
         a.pool_y[po] = pv;
         a.pool_am[po] = (int8_t)arg;
       }
@@ -363,7 +363,7 @@ __global__ __launch_bounds__(256) void conv_wino_k(const ConvArgs a, const float
       for (int dj = 0; dj < 2; ++dj) {
         const int i = 2 * tti + di, j = 2 * ttj + dj;
         const bool ok = tl && n < a.N && i >= 0 && j >= 0 && i < a.Hout && j < a.Wout && i >= bx.x && i < bx.z && j >= bx.y && j < bx.w;
-        const size_t pix = ((size_t)bb * a.Hout + i) * a.Wout + j;
+        const uint32_t pix = ((uint32_t)bb * a.Hout + i) * a.Wout + j;
         float out = 0.f;
         if (ok) out = epi_store(a, pix, n, yv[di][dj], mx);
         if (a.ybits) {
@@ -548,9 +548,9 @@ __global__ __launch_bounds__(64 * NW) void conv_wino2_k(const ConvArgs a, const 
       for (int p = 0; p < 4; ++p) {
         const int i = 2 * tti_[it] + (p >> 1), j = 2 * ttj_[it] + (p & 1);
         if (!((okm[it] >> p) & 1u)) continue;
-        const size_t pix = ((size_t)tb[it] * a.Hout + i) * a.Wout + j;
-        const size_t o = pix * (size_t)a.Cout_p + n;
-        const size_t wo = pix * (size_t)(a.Cout_p >> 5) + (n >> 5);
+        const uint32_t pix = ((uint32_t)tb[it] * a.Hout + i) * a.Wout + j;
+        const uint32_t o = pix * (uint32_t)a.Cout_p + n;
+        const uint32_t wo = pix * (uint32_t)(a.Cout_p >> 5) + (n >> 5);
         EpiIn& e = pre[it][p];
         if (early == (PRE == 1) && a.res) e.res = a.res[o];
         if (early == (PRE == 2)) {
@@ -582,9 +582,9 @@ __global__ __launch_bounds__(64 * NW) void conv_wino2_k(const ConvArgs a, const 
 #pragma unroll
     for (int p = 0; p < 4; ++p) {
       if (!((vok >> p) & 1u)) continue;
-      const size_t pix = ((size_t)vb * a.Hout + 2 * vti + (p >> 1)) * a.Wout + 2 * vtj + (p & 1);
-      const size_t o = pix * (size_t)a.Cout_p + n4;
-      const size_t wo = pix * (size_t)(a.Cout_p >> 5) + (n4 >> 5);
+      const uint32_t pix = ((uint32_t)vb * a.Hout + 2 * vti + (p >> 1)) * a.Wout + 2 * vtj + (p & 1);
+      const uint32_t o = pix * (uint32_t)a.Cout_p + n4;
+      const uint32_t wo = pix * (uint32_t)(a.Cout_p >> 5) + (n4 >> 5);
       if (early == (PRE == 1) && a.res) pre4[p].res = *reinterpret_cast<const float4*>(a.res + o);
       if (early == (PRE == 2)) {
         if (a.accumulate) pre4[p].yold = *reinterpret_cast<const float4*>(a.y + o);
@@ -735,7 +735,7 @@ __global__ __launch_bounds__(64 * NW) void conv_wino2_k(const ConvArgs a, const 
 #pragma unroll
     for (int p = 0; p < 4; ++p) {
       const bool ok = (vok >> p) & 1u;
-      const size_t pix = ((size_t)vb * a.Hout + 2 * vti + (p >> 1)) * a.Wout + 2 * vtj + (p & 1);
+      const uint32_t pix = ((uint32_t)vb * a.Hout + 2 * vti + (p >> 1)) * a.Wout + 2 * vtj + (p & 1);
       uint32_t nib = 0u;
       if (ok) {
         const float4 out = epi_store4(a, pix, n4, yv[p >> 1][p & 1], bias4, pre4[p], mx);
@@ -779,7 +779,7 @@ __global__ __launch_bounds__(64 * NW) void conv_wino2_k(const ConvArgs a, const 
       for (int dj = 0; dj < 2; ++dj) {
         const int i = 2 * tti + di, j = 2 * ttj + dj;
         const bool ok = (okm[it] >> (2 * di + dj)) & 1u;
-        const size_t pix = ((size_t)bb * a.Hout + i) * a.Wout + j;
+        const uint32_t pix = ((uint32_t)bb * a.Hout + i) * a.Wout + j;
         float out = 0.f;
 #ifdef PO_ABLATE_WINO_NOSTORE
         out = yv[di][dj] + bias_n;             // ablation build: epilogue without global traffic
@@ -960,9 +960,9 @@ __global__ __launch_bounds__(256, 2) void conv_wino3_k(const ConvArgs a, const f
 #pragma unroll
       for (int p = 0; p < 4; ++p) {
         if (!((vok >> p) & 1u) || a.ksplit > 1) continue;
-        const size_t pix = ((size_t)vb * a.Hout + 2 * vti + (p >> 1)) * a.Wout + 2 * vtj + (p & 1);
-        const size_t o = pix * (size_t)a.Cout_p + n4;
-        const size_t wo = pix * (size_t)(a.Cout_p >> 5) + (n4 >> 5);
+        const uint32_t pix = ((uint32_t)vb * a.Hout + 2 * vti + (p >> 1)) * a.Wout + 2 * vtj + (p & 1);
+        const uint32_t o = pix * (uint32_t)a.Cout_p + n4;
+        const uint32_t wo = pix * (uint32_t)(a.Cout_p >> 5) + (n4 >> 5);
         if (a.res) pre4[p].res = *reinterpret_cast<const float4*>(a.res + o);
         if (a.accumulate) pre4[p].yold = *reinterpret_cast<const float4*>(a.y + o);
         if (a.mbits) pre4[p].m = a.mbits[wo];
@@ -1036,7 +1036,7 @@ __global__ __launch_bounds__(256, 2) void conv_wino3_k(const ConvArgs a, const f
           code |= arg[c] << (8 * c);
           mx.y = fmaxf(mx.y, fabsf(pv[c]));
         }
-        const size_t po = (((size_t)vb * (a.Hout >> 1) + vti) * (a.Wout >> 1) + vtj) * a.Cout_p + n4;
+        const uint32_t po = (((uint32_t)vb * (a.Hout >> 1) + vti) * (a.Wout >> 1) + vtj) * a.Cout_p + n4;
         *reinterpret_cast<float4*>(a.pool_y + po) = make_float4(pv[0], pv[1], pv[2], pv[3]);
         *reinterpret_cast<uint32_t*>(a.pool_am + po) = code;
       }
@@ -1044,7 +1044,7 @@ __global__ __launch_bounds__(256, 2) void conv_wino3_k(const ConvArgs a, const f
 #pragma unroll
       for (int p = 0; p < 4; ++p) {
         const bool ok = (vok >> p) & 1u;
-        const size_t pix = ((size_t)vb * a.Hout + 2 * vti + (p >> 1)) * a.Wout + 2 * vtj + (p & 1);
+        const uint32_t pix = ((uint32_t)vb * a.Hout + 2 * vti + (p >> 1)) * a.Wout + 2 * vtj + (p & 1);
         uint32_t nib = 0u;
         if (ok) {
           const float4 out = epi_store4(a, pix, n4, yv[p >> 1][p & 1], bias4, pre4[p], mx);
@@ -1316,9 +1316,9 @@ __global__ __launch_bounds__(512, 1) void conv_wino4_k(const ConvArgs a, const f
 #pragma unroll
       for (int p = 0; p < 4; ++p) {
         if (!((vok >> p) & 1u) || a.ksplit > 1) continue;
-        const size_t pix = ((size_t)vb * a.Hout + 2 * vti + (p >> 1)) * a.Wout + 2 * vtj + (p & 1);
-        const size_t o = pix * (size_t)a.Cout_p + n4;
-        const size_t wo = pix * (size_t)(a.Cout_p >> 5) + (n4 >> 5);
+        const uint32_t pix = ((uint32_t)vb * a.Hout + 2 * vti + (p >> 1)) * a.Wout + 2 * vtj + (p & 1);
+        const uint32_t o = pix * (uint32_t)a.Cout_p + n4;
+        const uint32_t wo = pix * (uint32_t)(a.Cout_p >> 5) + (n4 >> 5);
         if (a.res) pre4[p].res = *reinterpret_cast<const float4*>(a.res + o);
         if (a.accumulate) pre4[p].yold = *reinterpret_cast<const float4*>(a.y + o);
         if (a.mbits) pre4[p].m = a.mbits[wo];
@@ -1394,7 +1394,7 @@ __global__ __launch_bounds__(512, 1) void conv_wino4_k(const ConvArgs a, const f
           code |= arg[c] << (8 * c);
           mx.y = fmaxf(mx.y, fabsf(pv[c]));
         }
-        const size_t po = (((size_t)vb * (a.Hout >> 1) + vti) * (a.Wout >> 1) + vtj) * a.Cout_p + n4;
+        const uint32_t po = (((uint32_t)vb * (a.Hout >> 1) + vti) * (a.Wout >> 1) + vtj) * a.Cout_p + n4;
         *reinterpret_cast<float4*>(a.pool_y + po) = make_float4(pv[0], pv[1], pv[2], pv[3]);
         *reinterpret_cast<uint32_t*>(a.pool_am + po) = code;
       }
@@ -1402,7 +1402,7 @@ __global__ __launch_bounds__(512, 1) void conv_wino4_k(const ConvArgs a, const f
 #pragma unroll
       for (int p = 0; p < 4; ++p) {
         const bool ok = (vok >> p) & 1u;
-        const size_t pix = ((size_t)vb * a.Hout + 2 * vti + (p >> 1)) * a.Wout + 2 * vtj + (p & 1);
+        const uint32_t pix = ((uint32_t)vb * a.Hout + 2 * vti + (p >> 1)) * a.Wout + 2 * vtj + (p & 1);
         uint32_t nib = 0u;
         if (ok) {
           const float4 out = epi_store4(a, pix, n4, yv[p >> 1][p & 1], bias4, pre4[p], mx);
@@ -1450,6 +1450,8 @@ int launch_wino(const ConvArgs& a, const float* U, hipStream_t st, int bm, int w
              "po_conv: a fused pool runs on Winograd tiles 61 and 66 only (even map, no boxes)");
   const int Ht = (a.Hout + 1) / 2, Wt = (a.Wout + 1) / 2;
   PO_REQUIRE((int64_t)a.B * Ht * Wt < (1LL << 31), "po_conv: too many tiles");
+  PO_REQUIRE((int64_t)a.B * a.Hout * a.Wout * a.Cout_p < (1LL << 31),
+             "po_conv: Winograd tiles index the destination with 32-bit element offsets (< 2^31 elements)");
   if (bm == T2) {
     PO_REQUIRE(a.N % N2 == 0, "po_conv: Winograd tiles 62/63 need N %% 64 == 0");
     ConvArgs b = a;
@@ -1491,6 +1493,8 @@ int launch_wino4(const ConvArgs& a, const float* U, hipStream_t st, bool stagger
              "po_conv: a fused pool needs an even map and no boxes");
   const int Ht = (a.Hout + 1) / 2, Wt = (a.Wout + 1) / 2;
   PO_REQUIRE((int64_t)a.B * Ht * Wt < (1LL << 31), "po_conv: too many tiles");
+  PO_REQUIRE((int64_t)a.B * a.Hout * a.Wout * a.Cout_p < (1LL << 31),
+             "po_conv: Winograd tiles index the destination with 32-bit element offsets (< 2^31 elements)");
   ConvArgs b = a;
   b.ntiles_n = a.N / N4;
   const int ntm = ceil_div((int64_t)a.B * Ht * Wt, T4);
