@@ -19,7 +19,7 @@
 #include "common.h"
 
 namespace {
-constexpr int BOXF = 8;      // floats per box record: x y w h det cls_conf cls_id pad
+constexpr int BOXF = 8;      // floats per box record: x y w h det cls_conf cls_id, source index (int bits)
 
 __device__ __forceinline__ float sigm(float x) { return 1.f / (1.f + expf(-x)); }
 
@@ -44,8 +44,10 @@ __global__ __launch_bounds__(256) void region_boxes_k(const RegionArgs a, const 
     const int k = k0 + tid;
     bool keep = false;
     float rec[7];
+    int src = 0;
     if (k < n) {
       const int i = k % a.A, cell = k / a.A;
+      src = i * hw + cell;                             // the head element (anchor, cy, cx) of the record
       const int cy = cell / a.w, cx = cell - cy * a.w;
       const float* f = hb + (size_t)i * F * hw + cell;
       const float det = sigm(f[4 * hw]);
@@ -80,7 +82,7 @@ __global__ __launch_bounds__(256) void region_boxes_k(const RegionArgs a, const 
         float* o = boxes + ((size_t)b * a.cap + pos) * BOXF;
 #pragma unroll
         for (int q = 0; q < 7; ++q) o[q] = rec[q];
-        o[7] = 0.f;
+        o[7] = __int_as_float(src);
       } else {
         atomicOr(overflow, 1);
       }

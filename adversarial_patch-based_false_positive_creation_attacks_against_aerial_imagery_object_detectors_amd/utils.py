@@ -153,13 +153,35 @@ def get_region_boxes(output, conf_thresh, num_classes, anchors, num_anchors, img
                      validation=False):
     """utils.py:125-245 on the device: per image, the boxes [cx, cy, w, h,
     det_conf, cls_max_conf, cls_max_id] (input pixels) whose confidence
-    exceeds conf_thresh, in the reference's order (cy, cx, anchor)."""
-    if validation:
-        raise NotImplementedError("get_region_boxes(validation=True) is not on the device path")
+    exceeds conf_thresh, in the reference's order (cy, cx, anchor).
+    validation=True (and not only_objectness, utils.py:221-226): each box also
+    lists (cls_conf, c) for every other class c with det_conf * cls_conf >
+    conf_thresh, in class order -- read at the record's head element
+    (po_region_boxes' src field), fp32 products and comparison as torch's."""
     det = region_boxes_device(output, conf_thresh, num_classes, anchors, num_anchors, img_size, only_objectness)
     if int(det.overflow.item()):
         raise RuntimeError("po_region_boxes: buffer overflow")
-    return _box_lists(det.boxes.cpu().numpy(), det.counts.cpu().numpy())
+    boxes_cpu, counts = det.boxes.cpu().numpy(), det.counts.cpu().numpy()
+    lists = _box_lists(boxes_cpu, counts)
+    if validation and not only_objectness:
+        out = output.unsqueeze(0) if output.dim() == 3 else output
+        B, _, h, w = out.shape
+        cls = torch.sigmoid(out.contiguous().float().view(B, num_anchors, 5 + num_classes, h * w)[:, :, 5:])
+        for b in range(B):
+            n = int(counts[b])
+            if n == 0:
+                continue
+            src = torch.from_numpy(boxes_cpu[b, :n, 7].copy()).view(torch.int32).long().to(out.device)
+            a_i, cell = src // (h * w), src % (h * w)
+            cc = cls[b][a_i, :, cell]                                    # [n, C] class probabilities
+            detc = det.boxes[b, :n, 4].view(n, 1)
+            over = (detc * cc) > conf_thresh                             # utils.py:224 (fp32)
+            over[torch.arange(n, device=out.device), det.boxes[b, :n, 6].long()] = False
+            cc, over = cc.cpu(), over.cpu()
+            for r in range(n):
+                for c in torch.nonzero(over[r]).view(-1).tolist():
+                    lists[b][r] += [float(cc[r, c]), c]
+    return lists
 
 
 def nms(boxes, nms_thresh):

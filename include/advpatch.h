@@ -33,7 +33,7 @@ typedef void* po_stream_t;
 #define PO_EHIP -2     /* HIP runtime error */
 #define PO_EDEVICE -3  /* device is not gfx950 */
 
-#define PO_ABI_VERSION 19
+#define PO_ABI_VERSION 20
 #define PO_AMAX_SUB 64  /* sub-slots per max|x| slot (see po_conv_desc) */
 
 int po_abi_version(void);
@@ -238,7 +238,9 @@ int po_grad_boxes(const int32_t* roi, int B, int S, const int32_t* prog, int npr
  * candidates enumerated per image in the reference's loop order (cy, cx,
  * anchor i); a candidate is kept when conf = sigmoid(obj) * max_c sigmoid(cls_c)
  * (only_objectness: sigmoid(obj)) > conf_thresh, as the 8-float record
- *   {cx, cy, w, h, det_conf, cls_max_conf, cls_max_id, 0}
+ *   {cx, cy, w, h, det_conf, cls_max_conf, cls_max_id, src}
+ * (src: the int32 bits of i*h*w + cy*w + cx, the record's head element --
+ * get_region_boxes(validation=True) reads the other classes there; ABI 20)
  * with cx = (sigmoid(tx) + x) * stride_w, w = (exp(tw) * anchor_w) * stride_w
  * (anchors_scaled = HOST [A][2] fp32 anchor / stride), divided by norm_w /
  * norm_h unless 1 (do_detect's normalisation, utils.py:511-515).  Records are

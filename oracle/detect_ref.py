@@ -95,9 +95,12 @@ def nms(boxes, nms_thresh):                                              # utils
     return out_boxes
 
 
-def get_region_boxes(output, conf_thresh, num_classes, anchors, num_anchors, img_size, only_objectness=0):
-    """utils.py:125-245 without validation mode: boxes [cx, cy, w, h, det_conf,
-    cls_max_conf, cls_max_id] in input pixels, per image."""
+def get_region_boxes(output, conf_thresh, num_classes, anchors, num_anchors, img_size, only_objectness=0,
+                     validation=False):
+    """utils.py:125-245: boxes [cx, cy, w, h, det_conf, cls_max_conf,
+    cls_max_id] in input pixels, per image; validation (utils.py:221-226):
+    after the test-side 8th element, (cls_conf, c) for every other class with
+    det_conf * cls_conf > conf_thresh."""
     all_boxes = []
     if output.dim() == 3:
         output = output.unsqueeze(0)
@@ -143,8 +146,15 @@ def get_region_boxes(output, conf_thresh, num_classes, anchors, num_anchors, img
                         # 1e-6 relative of the max -- the device's and the CPU's sigmoid may
                         # order such near-ties differently by an ulp
                         near = set(torch.nonzero(cls_confs[ind] >= cls_max_confs[ind] * (1 - 1e-6)).view(-1).tolist())
-                        boxes.append([xs[ind], ys[ind], ws[ind], hs[ind], det_conf, cls_max_confs[ind],
-                                      cls_max_ids[ind], near])
+                        box = [xs[ind], ys[ind], ws[ind], hs[ind], det_conf, cls_max_confs[ind],
+                               cls_max_ids[ind], near]
+                        if (not only_objectness) and validation:                     # utils.py:221-226
+                            for c in range(num_classes):
+                                tmp_conf = cls_confs[ind][c]
+                                if c != cls_max_ids[ind] and det_confs[ind] * tmp_conf > conf_thresh:
+                                    box.append(tmp_conf)
+                                    box.append(c)
+                        boxes.append(box)
         all_boxes.append(boxes)
     return all_boxes
 

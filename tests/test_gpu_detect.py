@@ -58,6 +58,37 @@ def test_region_boxes_match_oracle(h, thresh, only_obj):
         _assert_boxes_equal(got[b], want[b])
 
 
+@pytest.mark.parametrize("h,thresh", [(13, 0.05), (19, 0.02)])
+def test_region_boxes_validation_matches_oracle(h, thresh):
+    """get_region_boxes(validation=True) (utils.py:221-226): after the seven
+    box fields, (cls_conf, c) for every other class whose det_conf * cls_conf
+    clears the threshold, in class order; every product kept clear of the
+    threshold so the comparison cannot flip by an ulp."""
+    ut = pkg_mod("utils")
+    out = _heads(2, [h], seed=100 + h)[0]
+    anchors = ut.get_anchors(None)[0]
+    o = out.view(2, 3, 20, h * h)
+    for _ in range(4):                         # push every det * p and det * max p away from the threshold
+        det = torch.sigmoid(o[:, :, 4:5])
+        p = torch.sigmoid(o[:, :, 5:])
+        near = (~_away_from(det * p, thresh, 1e-4)).any(2, keepdim=True)
+        o[:, :, 4:5] = torch.where(near, o[:, :, 4:5] - 0.37, o[:, :, 4:5])
+    want = ref.get_region_boxes(out, thresh, 15, anchors, 3, (608, 608), validation=True)
+    got = ut.get_region_boxes(out.to(DEV), thresh, 15, anchors, 3, (608, 608), validation=True)
+    extras = 0
+    for b in range(2):
+        assert len(got[b]) == len(want[b]) > 0
+        _assert_boxes_equal([g[:7] for g in got[b]], [w_[:8] for w_ in want[b]])
+        for g, w_ in zip(got[b], want[b]):
+            ge, we = g[7:], w_[8:]
+            assert len(ge) == len(we), (ge, we)
+            assert [int(c) for c in ge[1::2]] == [int(c) for c in we[1::2]]
+            for a_, r_ in zip(ge[0::2], we[0::2]):
+                assert abs(a_ - float(r_)) <= 1e-6
+            extras += len(ge) // 2
+    assert extras > 0
+
+
 @pytest.mark.parametrize("n,thresh", [(1, 0.4), (300, 0.4), (1000, 0.45)])
 def test_nms_matches_oracle(n, thresh):
     """Random boxes in clusters (many overlaps), with duplicate confidences
