@@ -436,14 +436,16 @@ __global__ __launch_bounds__(64 * NW) void conv_wino2_k(const ConvArgs a, const 
   const int wave_u = __builtin_amdgcn_readfirstlane(wave);
   const int h = lane >> 5;
 
-  if (tid == 0) s_live = 0;
-  __syncthreads();
-  if (tid < T2) {
-    int b, ti, tj;
-    if (tile_point(a, Ht, Wt, m0 + tid, b, ti, tj)) s_live = 1;
+  if (a.gbox) {                          // without boxes every workgroup of the grid holds a live tile
+    if (tid == 0) s_live = 0;
+    __syncthreads();
+    if (tid < T2) {
+      int b, ti, tj;
+      if (tile_point(a, Ht, Wt, m0 + tid, b, ti, tj)) s_live = 1;
+    }
+    __syncthreads();
+    if (!s_live) return;
   }
-  __syncthreads();
-  if (!s_live) return;
 
   // ---- DMA source offsets: instruction j of wave w loads pixel p of one
   // 16-tile half: (p, half) = ((w*DPW + j) >> 1, (w*DPW + j) & 1); lane L ->
@@ -828,14 +830,16 @@ __global__ __launch_bounds__(256, 2) void conv_wino3_k(const ConvArgs a, const f
   const int wave_u = __builtin_amdgcn_readfirstlane(wave);
   const int h = lane >> 5;
 
-  if (tid == 0) s_live = 0;
-  __syncthreads();
-  if (tid < T2) {
-    int b, ti, tj;
-    if (tile_point(a, Ht, Wt, m0 + tid, b, ti, tj)) s_live = 1;
+  if (a.gbox) {                          // without boxes every workgroup of the grid holds a live tile
+    if (tid == 0) s_live = 0;
+    __syncthreads();
+    if (tid < T2) {
+      int b, ti, tj;
+      if (tile_point(a, Ht, Wt, m0 + tid, b, ti, tj)) s_live = 1;
+    }
+    __syncthreads();
+    if (!s_live) return;
   }
-  __syncthreads();
-  if (!s_live) return;
 
   const uint32_t in_bytes = (uint32_t)__builtin_amdgcn_readfirstlane(a.in_bytes);
   const __amdgpu_buffer_rsrc_t in_rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(a.in), 0, in_bytes, 0x00020000);
@@ -1121,14 +1125,16 @@ __global__ __launch_bounds__(512, 1) void conv_wino4_k(const ConvArgs a, const f
   const int h = lane >> 5;
   PO_STAMP(0);
 
-  if (tid == 0) s_live = 0;
-  __syncthreads();
-  if (tid < T4) {
-    int b, ti, tj;
-    if (tile_point(a, Ht, Wt, m0 + tid, b, ti, tj)) s_live = 1;
+  if (a.gbox) {                          // without boxes every workgroup of the grid holds a live tile
+    if (tid == 0) s_live = 0;
+    __syncthreads();
+    if (tid < T4) {
+      int b, ti, tj;
+      if (tile_point(a, Ht, Wt, m0 + tid, b, ti, tj)) s_live = 1;
+    }
+    __syncthreads();
+    if (!s_live) return;
   }
-  __syncthreads();
-  if (!s_live) return;
 
   // ---- input staging: thread (tile r, channel pair tc) loads its 4x4 patch, 2 channels
   const uint32_t in_bytes = (uint32_t)__builtin_amdgcn_readfirstlane(a.in_bytes);
