@@ -240,6 +240,69 @@ __global__ __launch_bounds__(256) void maxpool2_bwd_box_k(const float* __restric
   if (amax) po::amax_commit(amax, vmax);
 }
 
+// Stride-2 form on even maps (H = 2 Ho, W = 2 Wo): every source pixel lies in
+// exactly one window, so one thread per (pooled pixel, 4 channels) reads that
+// output's gradient and argmax bytes once and writes its window's (up to) four
+// source pixels inside the box -- instead of four gathering threads re-reading
+// them.  Per pixel the arithmetic is mp_bwd_px's (0 + g at the argmax, channel
+// mask, accumulate, slope): bit-identical, same pixels written.
+__global__ __launch_bounds__(256) void maxpool2_bwd_box_s2_k(const float* __restrict__ dd,
+                                                             const int8_t* __restrict__ am, int H, int W,
+                                                             int C, int Cp, int Ho, int Wo,
+                                                             float* __restrict__ ds, int acc,
+                                                             const float* __restrict__ my,
+                                                             const int32_t* __restrict__ boxes,
+                                                             uint32_t* __restrict__ amax) {
+  const int b = blockIdx.x;
+  const int4 bx = reinterpret_cast<const int4*>(boxes)[b];
+  const int r0 = max(bx.x, 0), c0 = max(bx.y, 0), r1 = min(bx.z, H), c1 = min(bx.w, W);
+  const int c4n = Cp >> 2;
+  float vmax = 0.f;
+  if (c1 > c0 && r1 > r0) {
+    const int oy0 = r0 >> 1, oy1 = (r1 + 1) >> 1;       // pooled rows / columns whose windows meet the box
+    const int ox0 = c0 >> 1, ox1 = (c1 + 1) >> 1;
+    const int nq = (ox1 - ox0) * c4n;
+    for (int oy = oy0 + (int)blockIdx.y; oy < oy1; oy += (int)gridDim.y)
+      for (int q = threadIdx.x; q < nq; q += 256) {
+        const int oxr = q / c4n, c = (q - oxr * c4n) * 4, ox = ox0 + oxr;
+        const uint32_t o = ((uint32_t)(b * Ho + oy) * Wo + ox) * Cp + c;     // < 2^31 (host check)
+        const char4 a = *reinterpret_cast<const char4*>(am + o);
+        const float4 g = *reinterpret_cast<const float4*>(dd + o);
+        const int ak[4] = {a.x, a.y, a.z, a.w};
+        const float gk[4] = {g.x, g.y, g.z, g.w};
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          const int y = 2 * oy + (k >> 1), x = 2 * ox + (k & 1);
+          if (y < r0 || y >= r1 || x < c0 || x >= c1) continue;
+          float v[4], lg[4];
+#pragma unroll
+          for (int u = 0; u < 4; ++u) {
+            const bool sel = (ak[u] & 3) == k;
+            v[u] = sel ? 0.f + gk[u] : 0.f;
+            lg[u] = (sel && (ak[u] & 8)) ? ((ak[u] & 4) ? 0.1f : 1.f) : 1.f;
+            if (c + u >= C) v[u] = 0.f;
+          }
+          const uint32_t t = ((uint32_t)(b * H + y) * W + x) * Cp + c;
+          if (acc) {
+            const float4 p = *reinterpret_cast<const float4*>(ds + t);
+            v[0] += p.x; v[1] += p.y; v[2] += p.z; v[3] += p.w;
+          }
+          if (my) {
+            const float4 m = *reinterpret_cast<const float4*>(my + t);
+            v[0] *= po::leaky_grad(m.x); v[1] *= po::leaky_grad(m.y);
+            v[2] *= po::leaky_grad(m.z); v[3] *= po::leaky_grad(m.w);
+          } else {
+#pragma unroll
+            for (int u = 0; u < 4; ++u) v[u] *= lg[u];
+          }
+          *reinterpret_cast<float4*>(ds + t) = make_float4(v[0], v[1], v[2], v[3]);
+          vmax = fmaxf(vmax, fmaxf(fmaxf(fabsf(v[0]), fabsf(v[1])), fmaxf(fabsf(v[2]), fabsf(v[3]))));
+        }
+      }
+  }
+  if (amax) po::amax_commit(amax, vmax);
+}
+
 __global__ __launch_bounds__(256) void nhwc2nchw_k(const float* __restrict__ s, int B, int H, int W, int C,
                                                    int Cp, float* __restrict__ d) {
   const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
@@ -420,6 +483,12 @@ extern "C" int po_maxpool2_bwd_box(const float* d_dst, const int8_t* argmax, int
   PO_REQUIRE(Cp % 4 == 0 && B < 65536 && (int64_t)W * Cp < (1LL << 30),
              "po_maxpool2_bwd_box: Cp %d must be a multiple of 4 (sizes within 32-bit grids)", Cp);
   if ((int64_t)B * H * W == 0) return PO_OK;
+  if (stride == 2 && H == 2 * Ho && W == 2 * Wo && (int64_t)B * H * W * Cp < (1LL << 31)) {
+    const int prow = Ho < 32 ? Ho : 32;
+    hipLaunchKernelGGL(maxpool2_bwd_box_s2_k, dim3(B, prow), dim3(256), 0, po::stream_of(s), d_dst, argmax, H, W, C,
+                       Cp, Ho, Wo, d_src, accumulate, mask_y, boxes, amax);
+    return po::check_launch("po_maxpool2_bwd_box");
+  }
   const int rows = H < 32 ? H : 32;
   hipLaunchKernelGGL(maxpool2_bwd_box_k, dim3(B, rows), dim3(256), 0, po::stream_of(s), d_dst, argmax, B, H, W, C,
                      Cp, stride, Ho, Wo, d_src, accumulate, mask_y, boxes, amax);

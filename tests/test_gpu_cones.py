@@ -166,6 +166,40 @@ def test_boxed_maxpool_bwd_matches_full(stride, H, W):
     assert torch.equal(boxed[~inside], prev[~inside])
 
 
+@pytest.mark.parametrize("H,W", [(22, 18), (21, 17), (416, 416)])
+def test_boxed_maxpool_bwd_slope_bytes(H, W):
+    """The first pool's form (argmax bytes carrying the LeakyReLU slope, no
+    mask, no accumulate) on even maps (the one-thread-per-window stride-2
+    kernel) and odd maps (the gathering kernel): inside the box bit-identical
+    to the full po_maxpool2_bwd, the max|x| slot = max |d_src| over the box."""
+    nat = pkg_mod("_native")
+    B, C, Cp = 3, 13, 16
+    Ho, Wo = H // 2, W // 2
+    gen = torch.Generator().manual_seed(H + W)
+    g = torch.randn(B, Ho, Wo, Cp, generator=gen)
+    g[0, 0, 0, :4] = -0.0                                         # signed zeros go through 0 + g
+    am = (torch.randint(0, 4, (B, Ho, Wo, Cp), generator=gen) | 8
+          | (torch.randint(0, 2, (B, Ho, Wo, Cp), generator=gen) * 4)).to(torch.int8)
+    g, am = g.to(DEV), am.to(DEV)
+    prev = torch.randn(B, H, W, Cp, generator=gen).to(DEV)
+    boxes = torch.tensor([[1, 3, H - 2, W - 1], [0, 0, H, W], [H // 2, W // 3, H // 2 + 3, W // 3 + 5]],
+                         dtype=torch.int32, device=DEV)
+    full, boxed = prev.clone(), prev.clone()
+    slot = torch.zeros(64, dtype=torch.int32, device=DEV)
+    nat.call("po_maxpool2_bwd", nat.ptr(g), nat.ptr(am, torch.int8), B, H, W, C, Cp, 2, nat.ptr(full), 0, None,
+             None, nat.stream())
+    nat.call("po_maxpool2_bwd_box", nat.ptr(g), nat.ptr(am, torch.int8), B, H, W, C, Cp, 2, nat.ptr(boxed), 0,
+             None, nat.ptr(boxes, torch.int32), nat.ptr(slot, torch.int32), nat.stream())
+    torch.cuda.synchronize()
+    inside = torch.zeros(B, H, W, dtype=torch.bool)
+    for b, (r0, c0, r1, c1) in enumerate(boxes.cpu().tolist()):
+        inside[b, max(r0, 0):min(r1, H), max(c0, 0):min(c1, W)] = True
+    inside = inside.to(DEV)
+    assert torch.equal(boxed[inside].view(torch.int32), full[inside].view(torch.int32))
+    assert torch.equal(boxed[~inside], prev[~inside])
+    assert float(slot.max().reshape(1).view(torch.float32)[0]) == float(full[inside].abs().max())
+
+
 def test_halo_tiles_refuse_boxes():
     """The halo kernel maps tile rows to contiguous pixels: a boxed launch
     must be refused (the autotuner then skips it), not computed wrongly."""
