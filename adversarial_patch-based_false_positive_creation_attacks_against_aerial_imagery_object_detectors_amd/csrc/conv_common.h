@@ -226,7 +226,7 @@ __device__ __forceinline__ void conv_pool_epilogue(const ConvArgs& a, const floa
           const int Wo = a.Wout, Ho = a.Hout;
           const int bimg = pix / (Ho * Wo), rem = pix - bimg * Ho * Wo;
           const int pi = rem / Wo, pj = rem - pi * Wo;
-          const size_t po = (((size_t)bimg * (Ho >> 1) + (pi >> 1)) * (Wo >> 1) + (pj >> 1)) * a.Cout_p + n;
+          const uint32_t po = (((uint32_t)bimg * (Ho >> 1) + (pi >> 1)) * (Wo >> 1) + (pj >> 1)) * a.Cout_p + n;
           *reinterpret_cast<float4*>(a.pool_y + po) = make_float4(pv[0], pv[1], pv[2], pv[3]);
           *reinterpret_cast<uint32_t*>(a.pool_am + po) = code;
         }
@@ -289,8 +289,8 @@ __device__ __forceinline__ void conv_epilogue(const ConvArgs& a, const floatx16 
         pres[q] = pold[q] = make_float4(0.f, 0.f, 0.f, 0.f);
         pmw[q] = pm2w[q] = 0u;
         if (pixq[q] >= 0 && n < a.N) {
-          const size_t o = (size_t)pixq[q] * a.Cout_p + n;
-          const size_t wo = (size_t)pixq[q] * wpp + (n >> 5);
+          const uint32_t o = (uint32_t)pixq[q] * (uint32_t)a.Cout_p + n;      // < 2^31 (po_conv host check)
+          const uint32_t wo = (uint32_t)pixq[q] * wpp + (n >> 5);
           if (a.res) pres[q] = *reinterpret_cast<const float4*>(a.res + o);
           if (a.accumulate) pold[q] = *reinterpret_cast<const float4*>(a.y + o);
           if (a.mbits) pmw[q] = a.mbits[wo];
@@ -305,7 +305,7 @@ __device__ __forceinline__ void conv_epilogue(const ConvArgs& a, const floatx16 
         const bool live = pix >= 0 && n < a.N;
         uint32_t nib = 0;
         if (live) {
-          const size_t o = (size_t)pix * a.Cout_p + n;
+          const uint32_t o = (uint32_t)pix * (uint32_t)a.Cout_p + n;
           float x[4] = {__builtin_ldexpf(v.x, -sh) + bv.x, __builtin_ldexpf(v.y, -sh) + bv.y,
                         __builtin_ldexpf(v.z, -sh) + bv.z, __builtin_ldexpf(v.w, -sh) + bv.w};
           if (a.act) {
@@ -353,7 +353,7 @@ __device__ __forceinline__ void conv_epilogue(const ConvArgs& a, const floatx16 
           w |= (uint32_t)__shfl_xor((int)w, 1);
           w |= (uint32_t)__shfl_xor((int)w, 2);
           w |= (uint32_t)__shfl_xor((int)w, 4);
-          if (live && (lane & 7) == 0) a.ybits[(size_t)pix * wpp + (n >> 5)] = w;
+          if (live && (lane & 7) == 0) a.ybits[(uint32_t)pix * wpp + (n >> 5)] = w;
         }
       }
       __builtin_amdgcn_wave_barrier();

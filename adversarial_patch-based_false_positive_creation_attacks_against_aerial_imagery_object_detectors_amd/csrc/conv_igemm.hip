@@ -461,6 +461,8 @@ extern "C" int po_conv(const po_conv_desc* d, const float* in, const float* W, c
   a.y2 = y2_out; a.mask2 = mask2;
   a.in_org = d->in_org; a.out_org = d->out_org; a.gbox = d->gbox;
   PO_REQUIRE(!d->gbox || !d->out_org, "po_conv: gbox needs a full-map destination (out_org NULL)");
+  PO_REQUIRE((int64_t)d->B * d->Hout * d->Wout * d->Cout_p < (1LL << 31),
+             "po_conv: the destination needs < 2^31 elements (32-bit epilogue offsets)");
   a.prec = d->prec;
   a.w_shift = d->w_shift;
   a.in_amax = d->in_amax;
