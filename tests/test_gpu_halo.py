@@ -90,3 +90,16 @@ def test_halo_refuses_what_it_cannot_run():
     d.ksplit, d.workspace = 2, xd.data_ptr()                 # split-K
     assert call(d) != 0
     torch.cuda.synchronize()
+
+
+def test_conv_refuses_destinations_past_2_31_elements():
+    """The po_conv epilogues index the destination in 32 bits: a launch whose
+    destination holds 2^31 or more elements is refused before anything runs."""
+    nat = pkg_mod("_native")
+    lib = nat.load()
+    xd = torch.zeros(16, device=DEV)
+    d = _desc(nat, 1 << 11, 208, 208, 9, False, 1)           # 2^11 x 208 x 208 pixels x 32 channels > 2^31
+    rc = lib.po_conv(ctypes.byref(d), nat.ptr(xd), nat.ptr(xd), nat.ptr(xd), nat.ptr(xd), None, None, None, None,
+                     None, nat.stream())
+    assert rc != 0
+    assert "2^31" in nat.last_error()
