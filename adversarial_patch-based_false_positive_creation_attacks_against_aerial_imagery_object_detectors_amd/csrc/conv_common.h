@@ -49,7 +49,22 @@ struct ConvArgs {
   uint32_t in_bytes, w_bytes;   // buffer-resource extents (< 2^31)
   // taps form a rectangular grid: tap t = th*tkw + tw -> (dh0 + th*sdh, dw0 + tw*sdw)
   int tkw, dh0, dw0, sdh, sdw;
+  // exact division by mrows and Wg for 0 <= n < 2^31 (host: po::div_magic):
+  // n / d = (n * mg) >> sh, no runtime integer-division sequence on the device
+  uint32_t mg_rows, mg_wg;
+  int sh_rows, sh_wg;
 };
+
+// d >= 1: mg = ceil(2^(31+l) / d) < 2^32, sh = 31 + l, l = ceil(log2 d)
+inline void div_magic(int d, uint32_t& mg, int& sh) {
+  int l = 0;
+  while ((1LL << l) < d) ++l;
+  mg = (uint32_t)(((1ULL << (31 + l)) + (uint64_t)d - 1) / (uint64_t)d);
+  sh = 31 + l;
+}
+__device__ __forceinline__ int div_by(int n, uint32_t mg, int sh) {
+  return (int)(((uint64_t)(uint32_t)n * mg) >> sh);
+}
 
 // Input scale exponent of a prec-1 launch: the input is multiplied by 2^e
 // (exact) so that its largest magnitude lies in [2^13, 2^14) — inside fp16's
@@ -93,7 +108,7 @@ __device__ __forceinline__ bool grid_point(const ConvArgs& a, int m, int& b, int
     b = i = j = 0;
     return false;
   }
-  b = m / HgWg;
+  b = div_by(m, a.mg_rows, a.sh_rows);
   const int l = m - b * HgWg;
   if (a.pool_y) {          // pool order: rows 4w .. 4w+3 are the 2x2 window w (row-major windows)
     const int w = l >> 2, k = l & 3, wp = a.Wg >> 1;
@@ -103,7 +118,7 @@ __device__ __forceinline__ bool grid_point(const ConvArgs& a, int m, int& b, int
     return true;
   }
   if (!a.gbox) {
-    i = l / a.Wg;
+    i = div_by(l, a.mg_wg, a.sh_wg);
     j = l - i * a.Wg;
     return true;
   }

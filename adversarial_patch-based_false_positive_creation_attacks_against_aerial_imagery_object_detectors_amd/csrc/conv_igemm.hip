@@ -492,6 +492,8 @@ extern "C" int po_conv(const po_conv_desc* d, const float* in, const float* W, c
   PO_REQUIRE(a.mrows <= d->Hg * d->Wg && (a.mrows == d->Hg * d->Wg || d->gbox),
              "po_conv: mrows %d needs gbox and at most Hg*Wg = %d rows", a.mrows, d->Hg * d->Wg);
   a.M = d->B * a.mrows;
+  po::div_magic(a.mrows, a.mg_rows, a.sh_rows);
+  po::div_magic(a.Wg, a.mg_wg, a.sh_wg);
   a.ntiles_n = 1;
   const int64_t in_bytes = (int64_t)d->B * d->Hin * d->Win * d->Cin_p * 4;
   // prec 1: w_bytes is one fp16 plane (the lo plane follows it)
