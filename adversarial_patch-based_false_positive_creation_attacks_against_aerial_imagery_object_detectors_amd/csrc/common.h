@@ -23,6 +23,18 @@ inline int check_launch(const char* what) {
 
 inline int ceil_div(int64_t a, int64_t b) { return (int)((a + b - 1) / b); }
 
+// Workgroups of `kernel` the current device holds at once: its compute units
+// times the resident workgroups per CU the occupancy calculator gives for this
+// build (VGPRs, LDS, block size) -- the grid of a persistent kernel.
+inline int resident_groups(const void* kernel, int block_threads, size_t dyn_lds = 0) {
+  int dev = 0, cus = 0, occ = 0;
+  if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) !=
+                                               hipSuccess)
+    cus = 256;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, kernel, block_threads, dyn_lds) != hipSuccess) occ = 1;
+  return (cus > 0 ? cus : 1) * (occ > 0 ? occ : 1);
+}
+
 // leaky'(y) for LeakyReLU(0.1): PyTorch leaky_relu_backward uses x > 0
 // (y and x share sign), slope 0.1 otherwise.
 __device__ __forceinline__ float leaky_grad(float y) { return y > 0.f ? 1.f : 0.1f; }

@@ -566,6 +566,7 @@ class NetPlan:
 
     # Winograd tiles of po_conv: (tiles = GEMM rows, output channels) per workgroup
     WINO_TILES = {61: (64, 32), 65: (32, 64), 66: (32, 64), 67: (64, 64), 68: (64, 64)}   # 62-64 retired
+    HALO_TILE = 69               # conv_halo_pool_k (conv_halo.hip)
     _tile_shapes = {}
 
     @classmethod
@@ -599,6 +600,10 @@ class NetPlan:
         if t in cls.WINO_TILES:
             WT = cls.WINO_TILES[t][0]
             return 2.0 * 16 * cls._live_tiles(desc, t, WT, cones) * WT * desc.Cin_p * desc.N
+        if t == cls.HALO_TILE:
+            # conv_halo_pool_k: 8 x 16-pixel output tiles (ragged ones padded), 32
+            # channels, K = 9 taps x 16 channels (full maps only: no boxes)
+            return 2.0 * desc.B * (-(-desc.Hg // 8)) * (-(-desc.Wg // 16)) * 128 * 32 * desc.ntaps * desc.Cin_p
         BM, BN, BK = cls.tile_shape(t)
         return 2.0 * cls._live_tiles(desc, t, BM, cones) * BM * (-(-desc.N // BN) * BN) * desc.ntaps * desc.Cin_p
 

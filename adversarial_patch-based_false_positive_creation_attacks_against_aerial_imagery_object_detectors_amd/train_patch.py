@@ -249,6 +249,9 @@ class PatchTrainer(object):
         self.darknet_model.load_darknet_weights(wf)
         self.darknet_model = self.darknet_model.eval()
         self.darknet_model_1 = self.darknet_model
+        # classes per anchor of the YOLO heads; po_cell_loss reads 5 + 15 channels per
+        # anchor, as the reference's loss head does (train_patch.py:459)
+        self.num_classes = int(next(b["classes"] for b in self.darknet_model.blocks if b["type"] == "yolo"))
         self.patch_applier = PatchApplier()
         self.patch_transformer = PatchTransformer()
         self.nps_calculator = NPSCalculator(self.config.printfile, self.config.patch_size).to(self.device)
@@ -322,15 +325,25 @@ class PatchTrainer(object):
         z = torch.zeros((), device=dev)
         loss, terms = combine_terms(z, z, reg[0], reg[1], reg[2], objective, weights, self._tv_floor)
         terms.update({"patch_center": torch.empty(0, 2, device=dev), "obj": torch.empty(0, 0, device=dev),
-                      "cls": torch.empty(0, 0, 15, device=dev), "cells": torch.empty(0, 0, dtype=torch.int32,
+                      "cls": torch.empty(0, 0, self.num_classes, device=dev), "cells": torch.empty(0, 0, dtype=torch.int32,
                                                                                    device=dev),
                       "flags": self.flags})
         return loss, terms
 
     def allreduce_grad(self, adv_patch, terms):
-        """One all-reduce(SUM) of [patch grad | weighted loss scalars] over all ranks."""
+        """One all-reduce(SUM) of [patch grad | weighted loss scalars] over all ranks.
+        With ``self.ar_timer`` a list (bench.py's instrumented pass), a pair of
+        device events brackets the reduction on the current stream."""
         if self.dist:
-            allreduce_patch_grad(adv_patch.grad, terms)
+            timer = getattr(self, "ar_timer", None)
+            if timer is not None and adv_patch.grad.is_cuda:
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record()
+                allreduce_patch_grad(adv_patch.grad, terms)
+                e1.record()
+                timer.append((e0, e1))
+            else:
+                allreduce_patch_grad(adv_patch.grad, terms)
 
     def step(self, adv_patch, optimizer, img_batch, lab_batch, draws=None, weights=None):
         """One full iteration: forward, backward, [all-reduce], Adam, clamp (train_patch.py:164-330)."""

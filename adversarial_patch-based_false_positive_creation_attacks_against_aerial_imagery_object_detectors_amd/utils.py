@@ -166,21 +166,24 @@ def get_region_boxes(output, conf_thresh, num_classes, anchors, num_anchors, img
     if validation and not only_objectness:
         out = output.unsqueeze(0) if output.dim() == 3 else output
         B, _, h, w = out.shape
-        cls = torch.sigmoid(out.contiguous().float().view(B, num_anchors, 5 + num_classes, h * w)[:, :, 5:])
+        raw = out.contiguous().float().view(B, num_anchors, 5 + num_classes, h * w)
         for b in range(B):
             n = int(counts[b])
             if n == 0:
                 continue
             src = torch.from_numpy(boxes_cpu[b, :n, 7].copy()).view(torch.int32).long().to(out.device)
             a_i, cell = src // (h * w), src % (h * w)
-            cc = cls[b][a_i, :, cell]                                    # [n, C] class probabilities
-            detc = det.boxes[b, :n, 4].view(n, 1)
+            # det_conf and the class probabilities with torch.sigmoid on the device
+            # tensor, as the reference computes both (utils.py:180-187), so the
+            # product and its comparison are the reference's bit for bit
+            detc = torch.sigmoid(raw[b][a_i, 4, cell]).view(n, 1)
+            cc = torch.sigmoid(raw[b][a_i, 5:, cell])                    # [n, C]
             over = (detc * cc) > conf_thresh                             # utils.py:224 (fp32)
             over[torch.arange(n, device=out.device), det.boxes[b, :n, 6].long()] = False
-            cc, over = cc.cpu(), over.cpu()
-            for r in range(n):
-                for c in torch.nonzero(over[r]).view(-1).tolist():
-                    lists[b][r] += [float(cc[r, c]), c]
+            rc = torch.nonzero(over).cpu().tolist()                      # (box, class) in row-major order
+            vals = cc[over].cpu().tolist()
+            for (r, c), v in zip(rc, vals):
+                lists[b][r] += [v, c]
     return lists
 
 

@@ -6,20 +6,27 @@ YOLOv3-DOTA forward -> cell loss + NPS/TV/colour -> backward (dgrad) ->
 [all-reduce of the patch gradient over RCCL when N > 1] -> Adam(amsgrad) + clamp.
 Inputs (frames, labels, patch) are resident in HBM before the timed region.
 
-    python bench.py [--gpus N --steps K --warmup W --batch B --config yolov3|tiny --prec both|fp32|fp16x3]
+    python bench.py [--gpus N --steps K --warmup W --batch B --config yolov3|tiny --prec fp32|both|fp16x3]
 
 ``value`` is measured with exact fp32 convolutions (v_mfma_f32_32x32x2_f32,
-the reference's arithmetic); the fp16x3 split-precision path is timed in the
-same run and reported beside it (``value_fp16x3``, ``roofline_fp16x3``).
-N > 1 is launched by torchrun (one process per GPU, RCCL over xGMI); the
-global batch is N*B (weak scaling), each rank runs its contiguous shard of one
-seeded global batch with draws keyed by global image index, and one
-all-reduce(SUM) of the weighted patch gradient per step.
+the reference's arithmetic); ``--prec both`` also times the opt-in fp16x3
+split-precision path and reports it beside (``value_fp16x3``).
+N > 1: one process per GPU (RCCL over xGMI).  ``bench.py --gpus N`` started
+without a torchrun environment launches the N ranks itself (torch.distributed.run
+as a child process, before anything touches the GPU) — the replacement for the
+reference's in-process ``nn.DataParallel`` (train_patch.py:63-71); under
+torchrun (WORLD_SIZE set) it is one rank.  The global batch is N*B (weak
+scaling), each rank runs its contiguous shard of one seeded global batch with
+draws keyed by global image index, and one all-reduce(SUM) of the weighted
+patch gradient per step.  ``--dry-run`` exercises only the
+launch, the sharding and the fused all-reduce (no GPU, no HIP step; CPU tests).
 """
 import argparse
 import json
 import os
 import platform
+import socket
+import subprocess
 import sys
 import time
 
@@ -35,6 +42,10 @@ PEAK_HBM_GBS = 8000.0
 # fp32-equivalent peak of each conv operand precision: exact fp32 MFMA, or
 # fp16x3 (three fp16 MFMA products per fp32 product)
 PEAK_CONV = {"fp32": PEAK_FP32_MFMA_TFLOPS, "fp16x3": PEAK_FP16_MFMA_TFLOPS / 3.0}
+
+# kernel of each specialised po_conv tile (others: the generic conv_k<BM,BN,WM,BK>)
+TILE_KERNELS = {61: "conv_wino_k", 65: "conv_wino2_k", 66: "conv_wino3_k", 67: "conv_wino4_k",
+                68: "conv_wino4_k<stagger>", 69: "conv_halo_pool_k"}
 
 CONFIGS = {
     # name: (cfg, S, P, default per-GPU batch)
@@ -122,9 +133,9 @@ def cpu_baseline(cfg, S, P, B=16, warmup=1, iters=3):
         oracle.train_step(patch, img, lab, dr, net, colors)
     el = time.time() - t0
     return {"value": iters * B / el, "unit": "images/s", "cores": cores, "kind": "port",
-            "sample": "oracle train_step (PyTorch-CPU fp32, weight grads on, no detect_anomaly), batch %d @%d, "
+            "sample": "oracle train_step (PyTorch-CPU fp32, weight grads on, no detect_anomaly), %s batch %d @%d, "
                       "%d timed steps after %d warm-up, %.1fs, %d threads (cgroup quota; os.cpu_count()=%d) of %s"
-                      % (B, S, iters, warmup, el, cores, os.cpu_count() or 0, _cpu_model())}
+                      % (cfg, B, S, iters, warmup, el, cores, os.cpu_count() or 0, _cpu_model())}
 
 
 WARP_ENTRIES = ("po_warp_fwd", "po_warp_bwd", "po_warp_fwd_keyed", "po_warp_bwd_keyed", "po_augment_patch",
@@ -169,6 +180,7 @@ def measure(tr, prec, patch, img, lab, B, world, rank, steps, warmup, weights):
         elapsed = float(t)
     plan.conv_timer = []
     nat.TIMERS = {k: [] for k in WARP_ENTRIES}
+    tr.ar_timer = [] if world > 1 else None
     torch.cuda.synchronize()
     t1 = time.perf_counter()
     for _ in range(steps):
@@ -177,13 +189,17 @@ def measure(tr, prec, patch, img, lab, B, world, rank, steps, warmup, weights):
     instrumented_ms = (time.perf_counter() - t1) * 1000.0 / steps
     timer, plan.conv_timer = plan.conv_timer, None
     warp, nat.TIMERS = nat.TIMERS, None
+    ar, tr.ar_timer = tr.ar_timer, None
+    # the fused [patch grad | 6 loss scalars] all-reduce, per step (this rank's view;
+    # it includes the wait for the slowest rank to arrive)
+    allreduce_ms = sum(e0.elapsed_time(e1) for e0, e1 in ar) / steps if ar else None
     conv_ms = sum(e0.elapsed_time(e1) for e0, e1, _, _ in timer) / steps
     # MACs actually computed: a boxed dgrad (gradient cones) counts its boxes only
     conv_flops = 2.0 * sum(plan.launch_macs(d, c) for _, _, d, c in timer) / steps
     # per tile family: time, dense-equivalent FLOPs and the FLOPs the matrix cores execute
     fam = {}
     for e0, e1, d, c in timer:
-        key = "winograd" if d.tile in plan.WINO_TILES else "direct"
+        key = "winograd" if d.tile in plan.WINO_TILES else ("halo" if d.tile == plan.HALO_TILE else "direct")
         f = fam.setdefault(key, {"ms": 0.0, "flops": 0.0, "mfma_flops": 0.0, "launches": 0, "tiles": {}})
         ms = e0.elapsed_time(e1)
         mf = plan.launch_mfma_flops(d, c)
@@ -220,7 +236,7 @@ def measure(tr, prec, patch, img, lab, B, world, rank, steps, warmup, weights):
     return {"elapsed": elapsed, "ms_per_step": elapsed * 1000.0 / steps, "value": world * B * steps / elapsed,
             "conv_ms": conv_ms, "conv_flops": conv_flops, "launches": len(timer) // steps, "families": fam,
             "warp_ms": warp_ms, "instrumented_ms": instrumented_ms, "loss": float(terms["loss"].detach()),
-            "plan": plan}
+            "allreduce_ms": allreduce_ms, "plan": plan}
 
 
 def roofline(cfg_name, B, prec, m, ref_flops_step):
@@ -229,15 +245,17 @@ def roofline(cfg_name, B, prec, m, ref_flops_step):
     if os.path.exists(tfile):
         with open(tfile) as f:
             traffic = json.load(f).get("conv_hbm_bytes_per_step")
-    achieved = m["conv_flops"] / (m["conv_ms"] * 1e-3) / 1e12
+    dense = m["conv_flops"] / (m["conv_ms"] * 1e-3) / 1e12
     peak = PEAK_CONV[prec]
     r = {"bound": "mfma",
          "kernel": "po_conv implicit GEMM (%s): every Darknet fwd + dgrad launch of a step" % (
              "conv_h3*_k, fp16x3 split operands" if prec == "fp16x3" else
              "conv_k + Winograd conv_wino*_k, exact fp32 v_mfma_f32_32x32x2_f32"),
-         "achieved": achieved, "peak": peak, "unit": "TFLOP/s", "frac": achieved / peak, "traffic": traffic,
-         "achieved_is": "dense-equivalent: 2 x the direct-conv MACs of every launch (Winograd launches counted at "
-                        "their direct-conv FLOPs) / conv time; the matrix-core utilisation is frac_mfma",
+         # fp32: replaced below by the FLOPs the matrix cores execute (a utilisation)
+         "achieved": dense, "peak": peak, "unit": "TFLOP/s", "frac": dense / peak, "traffic": traffic,
+         "achieved_dense_equiv": dense, "frac_dense_equiv": dense / peak,
+         "dense_equiv_is": "2 x the direct-conv MACs of every launch (Winograd launches counted at their direct-conv "
+                           "FLOPs) / conv time: NOT a utilisation (Winograd executes 4/9 of it)",
          "traffic_per": "step: HBM bytes of all conv launches + split-K reduces (rocprofv3 FETCH_SIZE/WRITE_SIZE "
                         "passes, profiles/traffic_*.json)",
          "peak_note": "fp32-equivalent: fp16 dense 2500 / 3 products" if prec == "fp16x3" else "fp32 dense MFMA",
@@ -260,9 +278,11 @@ def roofline(cfg_name, B, prec, m, ref_flops_step):
         r["mfma_flops_per_step"] = mf
         r["achieved_mfma"] = mf / (m["conv_ms"] * 1e-3) / 1e12
         r["frac_mfma"] = r["achieved_mfma"] / peak
-        r["frac_mfma_is"] = ("FLOPs the matrix cores execute (v_mfma_f32_32x32x2_f32: padded tiles, Winograd at "
-                             "16 GEMMs per 2x2 tile = 4/9 of the direct work; NetPlan.launch_mfma_flops) / conv time "
-                             "/ the 157.3 TFLOP/s peak at 2.4 GHz")
+        r["achieved"], r["frac"] = r["achieved_mfma"], r["frac_mfma"]
+        r["achieved_is"] = r["frac_mfma_is"] = (
+            "FLOPs the matrix cores execute (v_mfma_f32_32x32x2_f32: padded tiles, Winograd at 16 GEMMs per 2x2 "
+            "tile = 4/9 of the direct work; NetPlan.launch_mfma_flops) / conv time / the 157.3 TFLOP/s peak at "
+            "2.4 GHz: the MFMA utilisation of the conv launches")
         r["families"] = {k: {"ms_per_step": f["ms"], "launches_per_step": f["launches"],
                              "mfma_tflops": f["mfma_flops"] / (f["ms"] * 1e-3) / 1e12 if f["ms"] else None,
                              "frac_mfma": f["mfma_flops"] / (f["ms"] * 1e-3) / 1e12 / peak if f["ms"] else None,
@@ -271,8 +291,7 @@ def roofline(cfg_name, B, prec, m, ref_flops_step):
         # the dominant kernel: the tile with the most time per step
         best = max(((t, tt, k) for k, f in fam.items() for t, tt in f["tiles"].items()), key=lambda x: x[1]["ms"])
         t, tt, k = best
-        name = {68: "conv_wino4_k<stagger>", 67: "conv_wino4_k", 66: "conv_wino3_k", 65: "conv_wino2_k", 64: "conv_wino2_k", 63: "conv_wino2_k", 62: "conv_wino2_k",
-                61: "conv_wino_k"}.get(t, "conv_k")
+        name = TILE_KERNELS.get(t, "conv_k")
         r["dominant_kernel"] = {"kernel": "%s (po_conv tile %d, %s)" % (name, t, k), "ms_per_step": tt["ms"],
                                 "launches_per_step": tt["launches"],
                                 "avg_launch_us": 1000.0 * tt["ms"] / max(tt["launches"], 1e-9),
@@ -351,24 +370,101 @@ def measure_tiny(args, dev):
             "loss_tiny": m["loss"]}
 
 
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def launch_ranks(args):
+    """``bench.py --gpus N`` outside torchrun: start the N ranks as children
+    (python -m torch.distributed.run, one process per GPU, rendezvous on
+    127.0.0.1) and exit with their status.  Nothing here touches the GPU
+    (torch.cuda.device_count() does not initialise HIP), so the children own
+    the devices.  Every rank inherits stdout; only rank 0 prints the JSON line."""
+    n = args.gpus
+    if args.dist_backend == "nccl" and not args.dry_run:
+        ndev = torch.cuda.device_count()
+        if n > ndev:
+            raise SystemExit("bench.py --gpus %d: only %d GPU(s) visible; RCCL needs one GPU per rank "
+                             "(use --dist-backend gloo to rehearse ranks sharing a GPU)" % (n, ndev))
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(n),
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ)
+    env.setdefault("OMP_NUM_THREADS", "1")
+    return subprocess.call(cmd, env=env)
+
+
+def dry_run(args, world, rank):
+    """--dry-run: the multi-rank plumbing without a GPU — the process group,
+    this rank's shard of the global batch (GlobalBatchSampler.shard_of, as
+    train() and the synthetic bench slice it), and the fused all-reduce of
+    [patch grad | 6 loss scalars] (train_patch.allreduce_patch_grad), checked
+    against its known sum.  Prints a line with value null: nothing is measured."""
+    tp = ge._pkg("train_patch")
+    cfg, S, P, Bdef = CONFIGS[args.config]
+    B = args.batch or Bdef
+    G = B * world
+    lo, hi, ng = tp.GlobalBatchSampler(G, G, rank, world, shuffle=False).shard_of(0)
+    grad = torch.full((3, P, P), float(rank + 1))
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        g = grad.clone()
+        terms = {k: torch.tensor(float(hi - lo)) for k in tp.LOSS_KEYS}
+        if world > 1:
+            tp.allreduce_patch_grad(g, terms)
+    el = time.perf_counter() - t0
+    want = world * (world + 1) / 2.0
+    assert float(g.min()) == float(g.max()) == want, (float(g.min()), want)
+    assert all(float(terms[k]) == G for k in tp.LOSS_KEYS)
+    shards = [(lo, hi)] * world
+    if world > 1:
+        torch.distributed.all_gather_object(shards, (lo, hi))
+    if rank == 0:
+        print(json.dumps({"metric": "patch-opt images/sec (dry run: launch, sharding and all-reduce only)",
+                          "value": None, "unit": "images/s", "n_gpus": world, "steps": args.steps,
+                          "warmup": args.warmup, "dry_run": True,
+                          "dist_backend": torch.distributed.get_backend() if world > 1 else None,
+                          "config": {"workload": "%s S=%d P=%d batch=%d per GPU, global %d" % (cfg, S, P, B, G),
+                                     "global_batch": G, "per_gpu_batch": B, "parallelism": "dp%d" % world},
+                          "shards": shards, "allreduce_ms_per_step": el * 1000.0 / args.steps,
+                          "allreduce_bytes": 4 * (3 * P * P + len(tp.LOSS_KEYS))}))
+
+
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=1, help="ranks, one per GPU (launched here unless under torchrun)")
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--batch", type=int, default=None, help="per-GPU batch")
     ap.add_argument("--config", default="yolov3", choices=sorted(CONFIGS))
-    ap.add_argument("--prec", default="both", choices=("both", "fp32", "fp16x3"),
-                    help="conv operand precision(s) timed: value is exact fp32; fp16x3 is reported beside it")
+    ap.add_argument("--prec", default="fp32", choices=("fp32", "both", "fp16x3"),
+                    help="conv operand precision(s) timed: value is exact fp32; 'both' adds the opt-in fp16x3 "
+                         "split-precision path beside it")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-tiny", action="store_true", help="skip config 5 (timed beside the yolov3 line at N=1)")
     ap.add_argument("--dist-backend", default="nccl", help="nccl (= RCCL); gloo only to rehearse ranks on one GPU")
     ap.add_argument("--tile-cache", default=None, help="conv tile cache (default: the committed tiles/ file)")
+    ap.add_argument("--dry-run", action="store_true", help="launch + sharding + all-reduce only (no GPU)")
     args = ap.parse_args()
 
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(launch_ranks(args))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus and rank == 0:
+        print("bench.py: --gpus %d but WORLD_SIZE=%d; measuring %d ranks" % (args.gpus, world, world),
+              file=sys.stderr)
+    if args.dry_run:
+        if world > 1:
+            torch.distributed.init_process_group("gloo" if args.dist_backend == "nccl" else args.dist_backend)
+        dry_run(args, world, rank)
+        if world > 1:
+            torch.distributed.destroy_process_group()
+        return
     ndev = torch.cuda.device_count()
     if world > 1:
         torch.cuda.set_device(local % ndev)
@@ -420,6 +516,10 @@ def main():
             "warp_roofline": warp_roofline(m, B, S, P),
             "loss": m["loss"],
         }
+        if world > 1:
+            line["dist_backend"] = args.dist_backend
+            line["allreduce_ms_per_step"] = m["allreduce_ms"]
+            line["allreduce_bytes"] = 4 * (3 * P * P + len(tp.LOSS_KEYS))
         if "fp16x3" in res and head != "fp16x3":
             f = res["fp16x3"]
             line["value_fp16x3"] = f["value"]
@@ -432,6 +532,10 @@ def main():
             line.update(measure_tiny(args, dev))
         if world == 1 and not args.no_cpu_baseline:
             line["cpu_baseline"] = cpu_baseline(cfg, S, P, B=16)
+            if "value_tiny" in line:
+                # BASELINE.md's CPU sample for config 5: the oracle tiny-15 step, B=16 @416
+                tcfg, tS, tP, _ = CONFIGS["tiny"]
+                line["cpu_baseline_tiny"] = cpu_baseline(tcfg, tS, tP, B=16)
         print(json.dumps(line))
     if world > 1:
         torch.distributed.destroy_process_group()

@@ -170,20 +170,20 @@ def test_step_yolov3_targeted(tmp_path):
 
 
 def assert_tiny_parity(errs, tag):
-    """The tiny-15@416 bound.  Its patch covers fewer pixels (target size
-    scales with S), so the reference's fp32 affine_grid is noisier than at
-    608: the fp32 oracle alone sits up to ~1.5e-4 from the float64 evaluation
-    (all of it the placement geometry: with that geometry in float64 the
-    fp32 oracle is within ~3e-5).  Asserted: the HIP gradient within 1e-4 of
-    the float64 evaluation and of the fp32 oracle with float64 geometry, and
-    within 1e-4 + the fp32 oracle's own geometry error of the literal fp32
-    oracle (north_star's comparison, bounded by the triangle inequality)."""
+    """The tiny-15@416 bound: north_star's literal criterion, the HIP gradient
+    within 1e-4 of the fp32 oracle (the reference's own fp32 placement
+    geometry), and within 1e-4 of the float64 evaluation and of the fp32
+    oracle with float64 geometry.  The fp32 oracle's own distance to float64
+    is printed beside: its fp32 affine_grid is noisier at 416 than at 608
+    (target size scales with S), up to ~1.5e-4 on some draws,
+    so a draw where the reference's fp32 geometry alone exceeds 1e-4 would
+    fail here — none of the seeds below does."""
     print("%s patch grad: hip vs fp32 oracle %.3g (fp32 oracle vs float64 %.3g), hip vs fp32 oracle with f64 "
           "geometry %.3g, hip vs float64 %.3g" % (tag, errs["hip_o32"], errs["o32_f64"], errs["hip_o32g"],
                                                  errs["hip_f64"]))
     assert errs["hip_f64"] <= 1e-4, errs
     assert errs["hip_o32g"] <= 1e-4, errs
-    assert errs["hip_o32"] <= 1e-4 + errs["o32_f64"], errs
+    assert errs["hip_o32"] <= 1e-4, errs
 
 
 @pytest.mark.parametrize("objective", ["ce", "targeted"])
@@ -254,40 +254,67 @@ def test_two_adam_steps_yolov3(tmp_path):
     assert bool((diff <= bound).all()), float((diff - bound).max())
 
 
+@pytest.mark.timeout(900)
 @pytest.mark.parametrize("cfg,B,P", [("builtin:mini3", 5, 32), ("builtin:yolov3-tiny-dota", 3, 96),
                                      ("builtin:yolov3-dota", 3, 224)])
 def test_windowed_plan_matches_full_maps(tmp_path, cfg, B, P):
     """Receptive-field windows (NetPlan._plan_windows) change which pixels are
-    computed, not how: the loss terms, cells and the patch gradient equal the
-    full-map plan's."""
-    sy = pkg_mod("synthetic")
-    tr, ref_net = _trainer(cfg, tmp_path)
+    computed, not how: cells bit-exact, the loss terms of the two plans
+    within fp32 reassociation, and each plan's patch gradient within
+    north_star's 1e-4 of the fp32 oracle run on THAT plan's LeakyReLU /
+    max-pool branches (ties asserted).  The two HIP plans are two fp32
+    evaluations whose LeakyReLU ties may fall differently (the r03 1.07e-4
+    gap between them was one); where their branch decisions agree the oracle
+    is the same and the plans must also agree with each other within 1e-4."""
+    sy, ld = pkg_mod("synthetic"), pkg_mod("load_data")
+    tr, ref_net = _trainer(cfg, tmp_path, prec="fp32")
     S = ref_net.height
-    img, lab = sy.frames(B, S, seed=70).to(DEV), sy.labels(B, seed=71).to(DEV)
-    patch, dr = sy.patch(P, seed=72), {k: v.to(DEV) for k, v in sy.draws(B, P, seed=73).items()}
+    img, lab = sy.frames(B, S, seed=70), sy.labels(B, seed=71)
+    patch, dr = sy.patch(P, seed=72), sy.draws(B, P, seed=73)
+    colors = ld.load_printability_colors("builtin:30values")
     out = []
     for windows in (False, True):
         tr.darknet_model.window_heads = windows
         pg = patch.to(DEV).requires_grad_(True)
-        loss, terms = tr.losses(pg, img, lab, dr)
+        loss, terms = tr.losses(pg, img.to(DEV), lab.to(DEV), {k: v.to(DEV) for k, v in dr.items()})
+        br = plan_branches(tr.last_plan)
         loss.backward()
         assert tr.last_plan.windowed == windows
         if windows:
             assert int(tr.last_plan.win_flags.item()) == 0
-        out.append((terms, pg.grad.detach().clone()))
-    (t0, g0), (t1, g1) = out
+        out.append((terms, pg.grad.detach().cpu().clone(), br))
+    (t0, g0, br0), (t1, g1, br1) = out
     assert int(t1["flags"].item()) == 0
     assert t0["cells"].tolist() == t1["cells"].tolist()
-    # the window launches may split K differently (autotuned), so the sums
-    # agree to fp32 reassociation, not bitwise
     for k in ("loss", "no_obj_loss", "no_cls_loss"):
         assert abs(float(t0[k]) - float(t1[k])) <= 1e-5 * max(1.0, abs(float(t0[k]))), (k, float(t0[k]), float(t1[k]))
     torch.testing.assert_close(t1["obj"], t0["obj"], rtol=0, atol=1e-5)
-    # two fp32 evaluations, each held to 1e-4 of float64 by the branch-aligned
-    # tests (test_gpu_train): their difference is bounded by the sum, 2e-4
-    # (yolov3 B=3 measured 1.07e-4 with box-tuned Winograd tiles on both sides)
-    rel = float((g0 - g1).abs().max() / g0.abs().max())
-    assert rel < 2e-4, rel
+
+    def same_branches(a, b):
+        """b's decisions (windowed: -1 = outside the window, not computed) equal a's where b has one."""
+        for i, (kind, v) in b.items():
+            u = a[i][1]
+            if kind == "leaky" and v.dtype != torch.bool:
+                known = v >= 0
+                if not torch.equal((u[known] > 0) if u.dtype == torch.bool else (u[known] > 0), v[known] > 0):
+                    return False
+            elif not torch.equal(u, v):
+                return False
+        return True
+
+    rel = lambda a, b: float((a.double() - b.double()).abs().max() / b.double().abs().max())
+    g32 = {}
+    for tag, g, br in (("full", g0, br0), ("windowed", g1, br1)):
+        if tag == "windowed" and same_branches(br0, br1):
+            g32[tag] = g32["full"]              # same branches: the same oracle evaluation
+        else:
+            rec = {}
+            g32[tag] = oracle.train_step(patch, img, lab, dr, ref_net, colors, branch=br, record=rec)["grad"]
+            assert_branch_ties_only(br, rec, TIE_TOL["fp32"])
+        print("%s %s plan: hip vs fp32 oracle %.3g" % (cfg, tag, rel(g, g32[tag])))
+        assert rel(g, g32[tag]) <= 1e-4, (tag, rel(g, g32[tag]))
+    if g32["windowed"] is g32["full"]:
+        assert rel(g1, g0) <= 1e-4, rel(g1, g0)
 
 
 @pytest.mark.parametrize("cfg,B,P", [("builtin:mini3", 4, 32), ("builtin:yolov3-dota", 2, 224)])
