@@ -108,7 +108,8 @@ def _cpu_model():
 def cpu_baseline(cfg, S, P, B=16, warmup=1, iters=3):
     """the oracle (PyTorch-CPU fp32 restatement of the
     reference step, weight gradients ON as in the reference, no
-    detect_anomaly) on the host cores, batch B, 1 warm-up + 3 timed steps.
+    detect_anomaly) on the host cores, batch B, 1 warm-up + ``iters`` timed
+    steps (3 for yolov3 @608, ~30 s; 10 for tiny @416, a few seconds).
     Threads: every CPU the process may use (the cgroup quota; on the GPU
     box os.cpu_count() shows the whole 256-CPU machine while the job's quota
     is 16, and oversubscribing a quota only slows torch down)."""
@@ -535,7 +536,7 @@ def main():
             if "value_tiny" in line:
                 # BASELINE.md's CPU sample for config 5: the oracle tiny-15 step, B=16 @416
                 tcfg, tS, tP, _ = CONFIGS["tiny"]
-                line["cpu_baseline_tiny"] = cpu_baseline(tcfg, tS, tP, B=16)
+                line["cpu_baseline_tiny"] = cpu_baseline(tcfg, tS, tP, B=16, iters=10)
         print(json.dumps(line))
     if world > 1:
         torch.distributed.destroy_process_group()
