@@ -14,8 +14,8 @@ LIB_PATH = os.environ.get("ADVPATCH_LIB") or os.path.join(_HERE, "libadvpatch_hi
 
 c_int, c_float, c_int64, c_void_p = ctypes.c_int, ctypes.c_float, ctypes.c_int64, ctypes.c_void_p
 
-PO_ABI_VERSION = 20   # include/advpatch.h
-PO_CONV_NTILES = 69   # include/advpatch.h
+PO_ABI_VERSION = 21   # include/advpatch.h
+PO_CONV_NTILES = 70   # include/advpatch.h
 PO_AMAX_SUB = 64      # sub-slots per max|x| slot
 
 

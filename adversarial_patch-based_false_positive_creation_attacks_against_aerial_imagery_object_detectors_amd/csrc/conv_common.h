@@ -393,6 +393,7 @@ int launch_wino(const ConvArgs& a, const float* U, hipStream_t st, int bm, int w
 // tiles 67/68: 64 tiles x 64 channels per 512-thread workgroup, pipelined k-loop
 // (68: the two waves of a SIMD staggered)
 int launch_wino4(const ConvArgs& a, const float* U, hipStream_t st, bool stagger);
+int launch_wino5(const ConvArgs& a, const float* U, hipStream_t st);
 // tile 69 (conv_halo.hip): persistent 3x3 conv 16 -> 32 channels with the 2x2
 // max pool fused, input patches staged once per 8 x 16-pixel tile
 int launch_halo(const ConvArgs& a, hipStream_t st);

@@ -32,40 +32,14 @@
 // as floats or sign bits, fused shortcut, dual output, sign bits, max|x|).
 #pragma clang fp contract(off)
 #include "conv_common.h"
+#include "wino_common.h"
 
 namespace {
 using po::ConvArgs;
 
 constexpr int WT = 64;   // tiles (GEMM rows) per workgroup
 constexpr int WN = 32;   // output channels per workgroup
-constexpr int WK = 16;   // input channels per k-step
-constexpr uint32_t kOOB = 0x80000000u;
 
-// tile-grid enumeration: GEMM row m -> image b, tile (ti, tj); with a.gbox
-// only the tiles of the image's box (destination pixels [r0,r1) x [c0,c1))
-__device__ __forceinline__ bool tile_point(const ConvArgs& a, int Ht, int Wt, int m, int& b, int& ti, int& tj) {
-  const int per = Ht * Wt;
-  b = ti = tj = 0;
-  if (m >= a.B * per) return false;
-  b = m / per;
-  const int l = m - b * per;
-  if (!a.gbox) {
-    ti = l / Wt;
-    tj = l - ti * Wt;
-    return true;
-  }
-  const int4 bx = reinterpret_cast<const int4*>(a.gbox)[b];
-  const int t0 = bx.x >> 1, t1 = (bx.z + 1) >> 1, u0 = bx.y >> 1, u1 = (bx.w + 1) >> 1;
-  const int h = max(t1 - t0, 0), w = max(u1 - u0, 0);
-  if (l >= h * w) return false;
-  const int q = l / w;
-  ti = t0 + q;
-  tj = u0 + (l - q * w);
-  return true;
-}
-
-__device__ __forceinline__ float4 f4add(float4 x, float4 y) { return make_float4(x.x + y.x, x.y + y.y, x.z + y.z, x.w + y.w); }
-__device__ __forceinline__ float4 f4sub(float4 x, float4 y) { return make_float4(x.x - y.x, x.y - y.y, x.z - y.z, x.w - y.w); }
 
 // LDS V/M element (component xi, tile t, 16-byte chunk ch) — chunk swizzled by tile
 __device__ __forceinline__ int vidx(int xi, int t, int ch) { return ((xi * WT + t) * WK) + ((ch ^ ((t >> 2) & 3)) << 2); }
@@ -401,7 +375,6 @@ constexpr int M2_ROW = N2 + 8;                          // epilogue rows padded:
 __device__ __forceinline__ void lds_dma16(__amdgpu_buffer_rsrc_t rs, float* lds, uint32_t voff, uint32_t soff) {
   __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (__attribute__((address_space(3))) void*)lds, 16, voff, soff, 0, 0);
 }
-typedef float f2v __attribute__((ext_vector_type(2)));       // packed pairs: v_pk_add_f32
 __device__ __forceinline__ int v2idx(int xi, int t, int ch) { return ((xi * T2 + t) * WK) + ((ch ^ ((t >> 2) & 3)) << 2); }
 
 // NW = 4 waves (wave w owns components 4w..4w+3, a thread transforms a
@@ -1095,7 +1068,6 @@ __global__ __launch_bounds__(256, 2) void conv_wino3_k(const ConvArgs a, const f
 // Same transforms, per-accumulator MFMA order (k-steps, then channels
 // 8h + s) and epilogue arithmetic as tiles 65/66: bit-identical outputs.
 // Split-K (blockIdx.y = slice) and the fused pool epilogue as tile 66.
-constexpr int T4 = 64, N4 = 64;
 #ifdef PO_WINO_STAMP
 // diagnostic build only (tools/wino_phases.py): per-workgroup s_memrealtime
 // stamps of conv_wino4_k's phases (start, k-loop entry, k-loop exit, end)
@@ -1108,8 +1080,6 @@ __device__ unsigned long long g_wino_stamp[1 << 16][16];
 #else
 #define PO_STAMP(k) do { } while (0)
 #endif
-constexpr int V4_FLOATS = 16 * T4 * WK;                 // one transformed buffer: 64 KB
-__device__ __forceinline__ int v4idx(int xi, int t, int ch) { return ((xi * T4 + t) * WK) + ((ch ^ ((t >> 2) & 3)) << 2); }
 
 template <bool STAG>
 __global__ __launch_bounds__(512, 1) void conv_wino4_k(const ConvArgs a, const float* __restrict__ U, int Ht, int Wt) {
@@ -1431,6 +1401,7 @@ __global__ __launch_bounds__(512, 1) void conv_wino4_k(const ConvArgs a, const f
   if (a.sum_amax) po::amax_commit(a.sum_amax, mx.s);
   if (a.y2_amax) po::amax_commit(a.y2_amax, mx.y2);
 }
+
 }  // namespace
 
 namespace po {

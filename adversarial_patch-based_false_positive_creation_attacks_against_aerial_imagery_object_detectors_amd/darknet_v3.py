@@ -565,7 +565,7 @@ class NetPlan:
         return desc.macs * pts / (desc.B * desc.Hg * desc.Wg)
 
     # Winograd tiles of po_conv: (tiles = GEMM rows, output channels) per workgroup
-    WINO_TILES = {61: (64, 32), 65: (32, 64), 66: (32, 64), 67: (64, 64), 68: (64, 64)}   # 62-64 retired
+    WINO_TILES = {61: (64, 32), 65: (32, 64), 66: (32, 64), 67: (64, 64), 68: (64, 64), 70: (64, 64)}   # 62-64 retired
     HALO_TILE = 69               # conv_halo_pool_k (conv_halo.hip)
     _tile_shapes = {}
 
@@ -1199,7 +1199,7 @@ class NetPlan:
     # ---------------- autotuning ----------------
     SPLITS = (2, 4, 8, 16, 32)
     WS_FLOATS = 64 << 20          # split-K workspace cap (256 MB)
-    WINO_SPLIT_TILES = (66, 67, 68)   # Winograd tiles with split-K (conv_wino3_k, conv_wino4_k)
+    WINO_SPLIT_TILES = (66, 67, 68, 70)   # Winograd tiles with split-K (conv_wino3_k, conv_wino4_k, conv_wino5_k)
 
     def _ensure_ws(self, floats):
         if self.ws is None or self.ws.numel() < floats:
@@ -1336,6 +1336,9 @@ class NetPlan:
 
     def _set_tile(self, desc, choice):
         t, ks = (choice, 1) if isinstance(choice, int) else choice
+        remap = os.environ.get("ADVPATCH_TILE_MAP")          # diagnostic A/B: "68:70,66:70" on unboxed launches
+        if remap and not desc.gbox:
+            t = dict(tuple(int(v) for v in kv.split(":")) for kv in remap.split(",")).get(t, t)
         desc.tile, desc.ksplit = t, ks
         if ks > 1:
             desc.workspace = self._ensure_ws(ks * desc.B * desc.Hg * desc.Wg * desc.N).data_ptr()

@@ -45,7 +45,8 @@ PEAK_CONV = {"fp32": PEAK_FP32_MFMA_TFLOPS, "fp16x3": PEAK_FP16_MFMA_TFLOPS / 3.
 
 # kernel of each specialised po_conv tile (others: the generic conv_k<BM,BN,WM,BK>)
 TILE_KERNELS = {61: "conv_wino_k", 65: "conv_wino2_k", 66: "conv_wino3_k", 67: "conv_wino4_k",
-                68: "conv_wino4_k<stagger>", 69: "conv_halo_pool_k"}
+                68: "conv_wino4_k<stagger>", 69: "conv_halo_pool_k",
+                70: "conv_wino5_k (persistent)"}
 
 CONFIGS = {
     # name: (cfg, S, P, default per-GPU batch)

@@ -33,7 +33,7 @@ typedef void* po_stream_t;
 #define PO_EHIP -2     /* HIP runtime error */
 #define PO_EDEVICE -3  /* device is not gfx950 */
 
-#define PO_ABI_VERSION 20
+#define PO_ABI_VERSION 21
 #define PO_AMAX_SUB 64  /* sub-slots per max|x| slot (see po_conv_desc) */
 
 int po_abi_version(void);
@@ -417,7 +417,7 @@ typedef struct po_conv_desc {
   int8_t* pool_argmax;
 } po_conv_desc;
 
-#define PO_CONV_NTILES 69
+#define PO_CONV_NTILES 70
 /* Tile `t` (1-based): block rows BM (output pixels), block columns BN (output
  * channels), k-step BK (input channels).  Tiles 1..10 stage operands through
  * registers, 11..20 are the same shapes staged by LDS-DMA, 27 a 128x256
@@ -440,6 +440,12 @@ typedef struct po_conv_desc {
  * boxes, only the pooled outputs): 8 x 16-pixel tiles whose input patch is
  * staged once, weights held in registers, pool in registers; bit-identical
  * to the generic tiles.
+ * 70 (exact fp32, ABI 21) is tile 68 as a persistent kernel: one 512-thread
+ * workgroup per CU walks the launch's (64 tiles x 64 channels x split-K
+ * slice) units and issues each unit's stores after the next unit's first
+ * input rows, so they drain under its k-loop; full maps without boxes, at
+ * least two k-steps per slice, leaky masks as sign bits, no max|x| slots;
+ * bit-identical to 68.
  * Retired tiles (21..26, 28, 62..64: never selected by a tuner run) keep their
  * numbers; po_conv_tile_info reports them with *prec = -1 and po_conv refuses
  * them.  A tile that does not apply to a launch makes po_conv return
