@@ -44,6 +44,10 @@ _SIGS = {
     "po_draws": [ctypes.c_uint64, ctypes.c_uint64, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p,
                  c_void_p, c_void_p, c_void_p],
     "po_check_finite": [c_void_p, c_int64, c_int, c_void_p, c_void_p],
+    "po_check_finite_inf": [c_void_p, c_int64, c_int, c_void_p, c_void_p, c_void_p],
+    "po_loss_combine": [c_void_p, c_void_p, c_float, c_float, c_float, c_int, c_int, c_void_p, c_void_p, c_void_p],
+    "po_loss_combine_bwd": [c_void_p, c_void_p, c_float, c_float, c_float, c_int, c_int, c_void_p, c_void_p,
+                            c_void_p],
     "po_region_boxes": [c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p, c_float, c_float, c_float, c_float,
                         c_float, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p],
     "po_nms": [c_void_p, c_void_p, c_int, c_int, c_int, c_float, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p],

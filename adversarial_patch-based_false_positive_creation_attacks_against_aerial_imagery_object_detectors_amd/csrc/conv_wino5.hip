@@ -350,14 +350,22 @@ __global__ __launch_bounds__(512, 1) void conv_wino5_k(const ConvArgs a, const f
       mfma_c(1, Vc);
       __builtin_amdgcn_sched_barrier(0);
     }
+    const int cur_m0 = m0, cur_tn = tn, cur_s = s;
+    // ---- the next unit's first input rows, requested under the last MFMAs so
+    // they arrive during the staging (the last unit re-reads its own: branch-free)
+    const int nu = u + G;
+    const bool more = nu < units;
+    unit(more ? nu : u, m0, tn, s, ks0, ks1);
+    offsets(m0);
+    gload(ks0);
 
     // ---- this unit's epilogue positions (tile 68's per pass: tile tid >> 4, channels n4 .. n4+3)
-    const int n4 = tn * N4 + 4 * (lane & 15);
+    const int n4 = cur_tn * N4 + 4 * (lane & 15);
     uint32_t cpix[2], cok[2];
 #pragma unroll
     for (int ps = 0; ps < 2; ++ps) {
       int vb = 0, vti = 0, vtj = 0;
-      const bool tl = tile_point_full(a, Ht, Wt, m0 + TH * ps + (tid >> 4), vb, vti, vtj);
+      const bool tl = tile_point_full(a, Ht, Wt, cur_m0 + TH * ps + (tid >> 4), vb, vti, vtj);
       uint32_t ok4 = 0u;
 #pragma unroll
       for (int p = 0; p < 4; ++p) {
@@ -426,14 +434,7 @@ __global__ __launch_bounds__(512, 1) void conv_wino5_k(const ConvArgs a, const f
     vok[0] = cok[0];
     vok[1] = cok[1];
     vn4 = n4;
-    vslice = (uint32_t)s;
-
-    // ---- the next unit's first input rows (the last unit re-reads its own: branch-free)
-    const int nu = u + G;
-    const bool more = nu < units;
-    unit(more ? nu : u, m0, tn, s, ks0, ks1);
-    offsets(m0);
-    gload(ks0);
+    vslice = (uint32_t)cur_s;
     if (!more) break;
     u = nu;
   }

@@ -60,11 +60,14 @@ __global__ __launch_bounds__(256) void draws_k(uint32_t k0, uint32_t k1, uint32_
 
 // flags[0] |= bit if any of x[0..n) is NaN or +-Inf
 __global__ __launch_bounds__(256) void check_finite_k(const float* __restrict__ x, int64_t n, int32_t bit,
-                                                      int32_t* __restrict__ flags) {
+                                                      int32_t* __restrict__ flags, float* __restrict__ found_inf) {
   bool bad = false;
   for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256)
     bad |= !isfinite(x[i]);
-  if (__any(bad) && (threadIdx.x & 63) == 0) atomicOr(flags, bit);
+  if (__any(bad) && (threadIdx.x & 63) == 0) {
+    atomicOr(flags, bit);
+    if (found_inf) *found_inf = 1.f;          // sticky, as the flag bit
+  }
 }
 
 }  // namespace
@@ -82,10 +85,15 @@ extern "C" int po_draws(uint64_t seed, uint64_t counter, int b0, int B, int P, f
   return po::check_launch("po_draws");
 }
 
-extern "C" int po_check_finite(const float* x, int64_t n, int32_t bit, int32_t* flags, po_stream_t s) {
+extern "C" int po_check_finite_inf(const float* x, int64_t n, int32_t bit, int32_t* flags, float* found_inf,
+                                  po_stream_t s) {
   PO_REQUIRE(x && flags && n >= 0, "po_check_finite: null pointer");
   if (n == 0) return PO_OK;
   const int grid = (int)std::min<int64_t>(po::ceil_div(n, 256), 1024);
-  hipLaunchKernelGGL(check_finite_k, dim3(grid), dim3(256), 0, po::stream_of(s), x, n, bit, flags);
+  hipLaunchKernelGGL(check_finite_k, dim3(grid), dim3(256), 0, po::stream_of(s), x, n, bit, flags, found_inf);
   return po::check_launch("po_check_finite");
+}
+
+extern "C" int po_check_finite(const float* x, int64_t n, int32_t bit, int32_t* flags, po_stream_t s) {
+  return po_check_finite_inf(x, n, bit, flags, nullptr, s);
 }

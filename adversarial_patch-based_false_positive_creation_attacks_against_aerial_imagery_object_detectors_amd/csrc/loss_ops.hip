@@ -220,6 +220,73 @@ extern "C" int po_cell_loss(const float* const* heads, const int* hw, const int*
 }
 
 // ---------------------------------------------------------------------------
+// The loss of one iteration from the cell-loss pair and the regularisers
+// (train_patch.py:230-314, train_patch.combine_terms), and its gradient: the
+// same fp32 operations in the same order as the PyTorch expression and its
+// autograd (maximum's backward splits a tie in half), one thread.
+namespace {
+constexpr float NPS_F = 0.01f, TV_F = 2.5f, TV_FLOOR = 0.1f;
+__global__ void loss_combine_k(const float* __restrict__ out2, const float* __restrict__ reg, float w_img,
+                               float w_cls, float w_patch, int weighted, int with_cls, float* __restrict__ terms,
+                               float* __restrict__ loss_out) {
+  float no_obj = out2[0], no_cls = out2[1];
+  float nps_loss = reg[0] * NPS_F, tv_loss = reg[1] * TV_F, colorful = reg[2];
+  float tv_term = fmaxf(tv_loss, TV_FLOOR);
+  if (isnan(tv_loss)) tv_term = tv_loss;                    // torch.maximum propagates NaN
+  if (weighted) {
+    no_obj *= w_img;
+    no_cls *= w_cls;
+    nps_loss *= w_patch;
+    tv_loss *= w_patch;
+    tv_term *= w_patch;
+    colorful *= w_patch;
+  }
+  float loss = nps_loss + tv_term;
+  loss = loss + no_obj;
+  loss = loss + colorful;
+  if (with_cls) loss = loss + no_cls;
+  terms[0] = loss;
+  terms[1] = nps_loss;
+  terms[2] = tv_loss;
+  terms[3] = no_obj;
+  terms[4] = no_cls;
+  terms[5] = colorful;
+  if (loss_out) *loss_out = loss;
+}
+
+__global__ void loss_combine_bwd_k(const float* __restrict__ reg, const float* __restrict__ g_loss, float w_img,
+                                   float w_cls, float w_patch, int weighted, int with_cls, float* __restrict__ d_out2,
+                                   float* __restrict__ d_reg) {
+  const float g = g_loss[0];
+  const float tv_loss = reg[1] * TV_F;
+  // tv_term = maximum(tv_loss, 0.1): grad where tv_loss > 0.1, grad / 2 on a tie, 0 below
+  const float gt = weighted ? g * w_patch : g;
+  const float gtv = tv_loss == TV_FLOOR ? gt / 2.f : (tv_loss < TV_FLOOR ? 0.f : gt);
+  d_out2[0] = weighted ? g * w_img : g;
+  d_out2[1] = with_cls ? (weighted ? g * w_cls : g) : 0.f;
+  d_reg[0] = (weighted ? g * w_patch : g) * NPS_F;
+  d_reg[1] = gtv * TV_F;
+  d_reg[2] = weighted ? g * w_patch : g;
+}
+}  // namespace
+
+extern "C" int po_loss_combine(const float* out2, const float* reg, float w_img, float w_cls, float w_patch,
+                               int weighted, int with_cls, float* terms, float* loss_out, po_stream_t s) {
+  PO_REQUIRE(out2 && reg && terms, "po_loss_combine: null pointer");
+  hipLaunchKernelGGL(loss_combine_k, dim3(1), dim3(1), 0, po::stream_of(s), out2, reg, w_img, w_cls, w_patch,
+                     weighted, with_cls, terms, loss_out);
+  return po::check_launch("po_loss_combine");
+}
+
+extern "C" int po_loss_combine_bwd(const float* reg, const float* g_loss, float w_img, float w_cls, float w_patch,
+                                   int weighted, int with_cls, float* d_out2, float* d_reg, po_stream_t s) {
+  PO_REQUIRE(reg && g_loss && d_out2 && d_reg, "po_loss_combine_bwd: null pointer");
+  hipLaunchKernelGGL(loss_combine_bwd_k, dim3(1), dim3(1), 0, po::stream_of(s), reg, g_loss, w_img, w_cls, w_patch,
+                     weighted, with_cls, d_out2, d_reg);
+  return po::check_launch("po_loss_combine_bwd");
+}
+
+// ---------------------------------------------------------------------------
 // Receptive-field windows: one thread per (window, image).
 namespace {
 struct WinArgs {

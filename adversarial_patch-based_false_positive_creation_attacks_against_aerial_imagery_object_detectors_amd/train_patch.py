@@ -98,7 +98,11 @@ class _CellLoss(torch.autograd.Function):
     def backward(ctx, g2, *unused):
         center, *heads = ctx.saved_tensors
         S, target, objective, hw, Cp, views = ctx.meta
-        d_heads = [torch.zeros_like(h) for h in heads]
+        arena = torch.zeros(sum(h.numel() for h in heads), device=center.device)     # one fill for all heads
+        d_heads, o = [], 0
+        for h in heads:
+            d_heads.append(arena[o:o + h.numel()].view_as(h))
+            o += h.numel()
         out2 = torch.empty(2, device=center.device)
         hwa, wina, orga = _head_args(hw, views)
         scratch = torch.empty(2 * center.size(0), device=center.device)
@@ -170,6 +174,46 @@ def combine_terms(no_obj_loss, no_cls_loss, nps, tv, colorful, objective="ce", w
         loss = loss + no_cls_loss
     return loss, {"loss": loss, "nps_loss": nps_loss, "tv_loss": tv_loss, "no_obj_loss": no_obj_loss,
                   "no_cls_loss": no_cls_loss, "colorful_loss": colorful}
+
+
+class _LossCombine(torch.autograd.Function):
+    """combine_terms on the device in one launch each way (po_loss_combine /
+    po_loss_combine_bwd): the same fp32 values as the PyTorch expression and
+    its autograd, without its ~25 elementwise, select and fill kernels.
+    out2 = {no_obj, no_cls} (po_cell_loss), reg = {nps, tv, colour}
+    (po_regularisers).  Returns (loss, terms [6]) with terms = LOSS_KEYS'
+    values; only the loss is differentiable."""
+
+    @staticmethod
+    def forward(ctx, out2, reg, weights, with_cls):
+        dev = out2.device
+        w = weights if weights is not None else (1.0, 1.0, 1.0)
+        loss = torch.empty((), device=dev)
+        terms = torch.empty(6, device=dev)
+        nat.call("po_loss_combine", nat.ptr(out2), nat.ptr(reg), float(w[0]), float(w[1]), float(w[2]),
+                 int(weights is not None), int(with_cls), nat.ptr(terms), nat.ptr(loss), nat.stream())
+        ctx.save_for_backward(reg)
+        ctx.meta = (w, weights is not None, with_cls)
+        ctx.mark_non_differentiable(terms)
+        return loss, terms
+
+    @staticmethod
+    def backward(ctx, g_loss, _):
+        reg, = ctx.saved_tensors
+        w, weighted, with_cls = ctx.meta
+        d_out2 = torch.empty(2, device=reg.device)
+        d_reg = torch.empty(3, device=reg.device)
+        nat.call("po_loss_combine_bwd", nat.ptr(reg), nat.ptr(g_loss.contiguous().float()), float(w[0]), float(w[1]),
+                 float(w[2]), int(weighted), int(with_cls), nat.ptr(d_out2), nat.ptr(d_reg), nat.stream())
+        return d_out2, d_reg, None, None
+
+
+def combine_terms_device(out2, reg, objective="ce", weights=None):
+    """combine_terms(out2[0], out2[1], reg[0], reg[1], reg[2], objective,
+    weights) as one device launch (and one for its gradient)."""
+    loss, t = _LossCombine.apply(out2, reg, weights, objective != "untargeted")
+    return loss, {"loss": loss, "nps_loss": t[1], "tv_loss": t[2], "no_obj_loss": t[3], "no_cls_loss": t[4],
+                  "colorful_loss": t[5]}
 
 
 def allreduce_patch_grad(grad, terms, group=None):
@@ -267,6 +311,7 @@ class PatchTrainer(object):
         # NaN/Inf guard on the patch gradient (replaces detect_anomaly, train_patch.py:158)
         self.check_finite = os.environ.get("ADVPATCH_CHECK_FINITE", "1") != "0"
         self._found_inf = None
+        self._seed = None
 
     # ------------------------------------------------------------------
     def generate_patch(self, type):
@@ -307,9 +352,7 @@ class PatchTrainer(object):
         out2, obj, cls, cells, flags = cell_loss(heads, plan, img_size, center, TARGET_ID, objective,
                                                  flags=self.flags)
         reg = regularisers(adv_patch, self.nps_calculator.colors)
-        if self._tv_floor is None or self._tv_floor.device != adv_patch.device:
-            self._tv_floor = torch.tensor(0.1, device=adv_patch.device)
-        loss, terms = combine_terms(out2[0], out2[1], reg[0], reg[1], reg[2], objective, weights, self._tv_floor)
+        loss, terms = combine_terms_device(out2, reg, objective, weights)
         terms.update({"patch_center": center, "obj": obj, "cls": cls, "cells": cells, "flags": flags})
         return loss, terms
 
@@ -348,21 +391,26 @@ class PatchTrainer(object):
     def step(self, adv_patch, optimizer, img_batch, lab_batch, draws=None, weights=None):
         """One full iteration: forward, backward, [all-reduce], Adam, clamp (train_patch.py:164-330)."""
         loss, terms = self.losses(adv_patch, img_batch, lab_batch, draws, weights=weights)
-        loss.backward()
+        if self._seed is None or self._seed.device != loss.device:
+            self._seed = torch.ones((), device=loss.device)                 # dL/dL, allocated once
+        loss.backward(self._seed)
         self.allreduce_grad(adv_patch, terms)
         if self.check_finite:
             # after the all-reduce: a NaN/Inf on any rank reaches every rank's reduced
             # gradient, so all ranks raise the same bit and skip the same updates
             g = adv_patch.grad
-            nat.call("po_check_finite", nat.ptr(g), g.numel(), FLAG_NONFINITE, nat.ptr(self.flags, torch.int32),
-                     nat.stream())
-            if optimizer.defaults.get("fused"):
+            fused = bool(optimizer.defaults.get("fused"))
+            if fused and (self._found_inf is None or self._found_inf.device != g.device):
+                # sticky like the flag bit: po_check_finite_inf sets it to 1 with the bit, never clears it
+                self._found_inf = torch.zeros((), device=g.device)         # 0-dim, as Adam's step counters
+                if int(self.flags.item()) & FLAG_NONFINITE:
+                    self._found_inf.fill_(1.0)
+            nat.call("po_check_finite_inf", nat.ptr(g), g.numel(), FLAG_NONFINITE, nat.ptr(self.flags, torch.int32),
+                     nat.ptr(self._found_inf) if fused else None, nat.stream())
+            if fused:
                 # once the bit is up the fused Adam skips its update (found_inf, as under
                 # GradScaler): the patch stays at its last finite value until check_flags
                 # raises at the end of the epoch, instead of being corrupted by the NaN
-                if self._found_inf is None or self._found_inf.device != g.device:
-                    self._found_inf = torch.zeros((), device=g.device)     # 0-dim, as Adam's step counters
-                self._found_inf.copy_(self.flags[0] & FLAG_NONFINITE).clamp_(max=1.0)
                 optimizer.found_inf = self._found_inf
         optimizer.step()
         optimizer.zero_grad()

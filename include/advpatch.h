@@ -89,6 +89,11 @@ int po_draws(uint64_t seed, uint64_t counter, int b0, int B, int P, float* contr
  * flags[0] |= bit if any of x[0..n) is not finite.  No host synchronisation. */
 int po_check_finite(const float* x, int64_t n, int32_t bit, int32_t* flags, po_stream_t s);
 
+/* po_check_finite that also sets *found_inf = 1.0f when it raises the bit
+ * (never clears it): the found_inf operand of PyTorch's fused Adam, so a
+ * non-finite step is skipped without host code or extra launches (ABI 21). */
+int po_check_finite_inf(const float* x, int64_t n, int32_t bit, int32_t* flags, float* found_inf, po_stream_t s);
+
 /* Augment (contrast/brightness/noise/clamp, load_data.py:548-574) + affine
  * bilinear warp of patch and mask (affine_grid + grid_sample, align_corners
  * False, zeros, load_data.py:745-749) + clamp*mask (791-792).
@@ -182,6 +187,23 @@ int po_cell_loss(const float* const* heads, const int* hw, const int* win, const
                  int nheads, int Cp, int B, int S, const float* center, int target, int objective,
                  const float* g2, float* const* d_heads, float* out2, float* obj_out, float* cls_out,
                  int32_t* cells, int32_t* flags, float* scratch /* >= 2*B floats, or NULL */, po_stream_t s);
+
+/* The iteration's loss (train_patch.py:230-314) from out2 = {no_obj_loss,
+ * no_cls_loss} (po_cell_loss) and reg = {nps, tv, colour} (po_regularisers):
+ *   loss = 0.01 nps + max(2.5 tv, 0.1) + no_obj + colour [+ no_cls if with_cls]
+ * with, when `weighted` (a data-parallel rank, train_patch.shard_weights),
+ * no_obj * w_img, no_cls * w_cls and the three patch terms * w_patch.
+ * terms[0..5] = {loss, nps_loss, tv_loss, no_obj_loss, no_cls_loss,
+ * colorful_loss} as train_patch.combine_terms returns them (same fp32
+ * operations, same order); *loss_out (optional) = the loss.  One thread. */
+int po_loss_combine(const float* out2, const float* reg, float w_img, float w_cls, float w_patch, int weighted,
+                    int with_cls, float* terms, float* loss_out, po_stream_t s);
+
+/* Its gradient for dL = g_loss[0]: d_out2[2] and d_reg[3], the values and
+ * rounding of PyTorch's autograd of combine_terms (maximum's backward gives a
+ * tie half the gradient). */
+int po_loss_combine_bwd(const float* reg, const float* g_loss, float w_img, float w_cls, float w_patch, int weighted,
+                        int with_cls, float* d_out2, float* d_reg, po_stream_t s);
 
 /* MaxProbExtractor.forward (load_data.py:125-311; bbox_decode 63-122 rewrites
  * only the box fields, so it is not run): per image b, the max over every head

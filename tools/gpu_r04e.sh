@@ -1,0 +1,28 @@
+#!/bin/bash
+# Round 4: the new GPU tests, then a Winograd retune (tile 70 eligible) of both tile caches, then A/B of the
+# retuned caches against the committed ones.
+set -o pipefail
+cd "$GRAFT_REPO_ROOT" || exit 1
+OUT=gpurun_out/${TAGOUT:-r04e}
+PKG=adversarial_patch-based_false_positive_creation_attacks_against_aerial_imagery_object_detectors_amd
+mkdir -p $OUT
+(while sleep 45; do echo "tick $(date +%T)"; done) & HB=$!
+trap "kill $HB" EXIT
+timeout -k 10 900 python -u -m pytest tests/test_gpu_loss_combine.py tests/test_gpu_train.py tests/test_gpu_wino5.py -x -q --timeout 600 --timeout-method thread > $OUT/tests.log 2>&1
+rc=$?; tail -5 $OUT/tests.log; [ $rc -eq 0 ] || exit $rc
+python tools/retune_wino.py $PKG/tiles/conv_tiles_yolov3_b16.json $OUT/yolov3_b16.json
+python tools/retune_wino.py $PKG/tiles/conv_tiles_tiny_b256.json $OUT/tiny_b256.json
+timeout -k 10 900 python -u bench.py --tile-cache $OUT/yolov3_b16.json --no-cpu-baseline --no-tiny > $OUT/tune_y.json 2> $OUT/tune_y.err || exit 1
+timeout -k 10 900 python -u bench.py --config tiny --tile-cache $OUT/tiny_b256.json --no-cpu-baseline > $OUT/tune_t.json 2> $OUT/tune_t.err || exit 1
+for rnd in 1 2; do
+  for which in committed new; do
+    if [ $which = committed ]; then YC=$PKG/tiles/conv_tiles_yolov3_b16.json; TC=$PKG/tiles/conv_tiles_tiny_b256.json
+    else YC=$OUT/yolov3_b16.json; TC=$OUT/tiny_b256.json; fi
+    timeout -k 10 300 python -u bench.py --tile-cache $YC --no-cpu-baseline --no-tiny > $OUT/y_${which}_$rnd.json 2>> $OUT/err.log || exit 1
+    timeout -k 10 300 python -u bench.py --config tiny --tile-cache $TC --no-cpu-baseline > $OUT/t_${which}_$rnd.json 2>> $OUT/err.log || exit 1
+    python3 -c "
+import json
+y=json.loads(open('$OUT/y_${which}_$rnd.json').read().strip().splitlines()[-1]); t=json.loads(open('$OUT/t_${which}_$rnd.json').read().strip().splitlines()[-1])
+print('r$rnd $which yolov3', round(y['value'],1), round(y['ms_per_step'],3), 'frac', round(y['roofline']['frac'],3), '| tiny', round(t['value'],1), round(t['ms_per_step'],3))" | tee -a $OUT/summary.txt
+  done
+done
