@@ -60,14 +60,16 @@ __global__ __launch_bounds__(256) void draws_k(uint32_t k0, uint32_t k1, uint32_
 
 // flags[0] |= bit if any of x[0..n) is NaN or +-Inf
 __global__ __launch_bounds__(256) void check_finite_k(const float* __restrict__ x, int64_t n, int32_t bit,
-                                                      int32_t* __restrict__ flags, float* __restrict__ found_inf) {
+                                                      int32_t* __restrict__ flags) {
   bool bad = false;
   for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256)
     bad |= !isfinite(x[i]);
-  if (__any(bad) && (threadIdx.x & 63) == 0) {
-    atomicOr(flags, bit);
-    if (found_inf) *found_inf = 1.f;          // sticky, as the flag bit
-  }
+  if (__any(bad) && (threadIdx.x & 63) == 0) atomicOr(flags, bit);
+}
+
+// found_inf = 1.0f while the bit is up (after check_finite_k on the same stream)
+__global__ void found_inf_k(const int32_t* __restrict__ flags, int32_t bit, float* __restrict__ found_inf) {
+  *found_inf = (*flags & bit) ? 1.f : 0.f;
 }
 
 }  // namespace
@@ -88,9 +90,13 @@ extern "C" int po_draws(uint64_t seed, uint64_t counter, int b0, int B, int P, f
 extern "C" int po_check_finite_inf(const float* x, int64_t n, int32_t bit, int32_t* flags, float* found_inf,
                                   po_stream_t s) {
   PO_REQUIRE(x && flags && n >= 0, "po_check_finite: null pointer");
-  if (n == 0) return PO_OK;
+  if (n == 0) {
+    if (found_inf) hipLaunchKernelGGL(found_inf_k, dim3(1), dim3(1), 0, po::stream_of(s), flags, bit, found_inf);
+    return po::check_launch("po_check_finite");
+  }
   const int grid = (int)std::min<int64_t>(po::ceil_div(n, 256), 1024);
-  hipLaunchKernelGGL(check_finite_k, dim3(grid), dim3(256), 0, po::stream_of(s), x, n, bit, flags, found_inf);
+  hipLaunchKernelGGL(check_finite_k, dim3(grid), dim3(256), 0, po::stream_of(s), x, n, bit, flags);
+  if (found_inf) hipLaunchKernelGGL(found_inf_k, dim3(1), dim3(1), 0, po::stream_of(s), flags, bit, found_inf);
   return po::check_launch("po_check_finite");
 }
 

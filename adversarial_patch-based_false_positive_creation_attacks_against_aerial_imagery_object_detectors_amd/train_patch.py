@@ -401,10 +401,8 @@ class PatchTrainer(object):
             g = adv_patch.grad
             fused = bool(optimizer.defaults.get("fused"))
             if fused and (self._found_inf is None or self._found_inf.device != g.device):
-                # sticky like the flag bit: po_check_finite_inf sets it to 1 with the bit, never clears it
+                # po_check_finite_inf writes it from the flag word after the check
                 self._found_inf = torch.zeros((), device=g.device)         # 0-dim, as Adam's step counters
-                if int(self.flags.item()) & FLAG_NONFINITE:
-                    self._found_inf.fill_(1.0)
             nat.call("po_check_finite_inf", nat.ptr(g), g.numel(), FLAG_NONFINITE, nat.ptr(self.flags, torch.int32),
                      nat.ptr(self._found_inf) if fused else None, nat.stream())
             if fused:

@@ -89,9 +89,10 @@ int po_draws(uint64_t seed, uint64_t counter, int b0, int B, int P, float* contr
  * flags[0] |= bit if any of x[0..n) is not finite.  No host synchronisation. */
 int po_check_finite(const float* x, int64_t n, int32_t bit, int32_t* flags, po_stream_t s);
 
-/* po_check_finite that also sets *found_inf = 1.0f when it raises the bit
- * (never clears it): the found_inf operand of PyTorch's fused Adam, so a
- * non-finite step is skipped without host code or extra launches (ABI 21). */
+/* po_check_finite, then *found_inf = (flags[0] & bit) ? 1.0f : 0.0f: the
+ * found_inf operand of PyTorch's fused Adam follows the flag word (set by
+ * this or an earlier check, cleared only when the caller clears the flags),
+ * so a non-finite step is skipped with no host code (ABI 21). */
 int po_check_finite_inf(const float* x, int64_t n, int32_t bit, int32_t* flags, float* found_inf, po_stream_t s);
 
 /* Augment (contrast/brightness/noise/clamp, load_data.py:548-574) + affine
