@@ -277,6 +277,7 @@ class NetPlan:
         self.support = []             # compact dgrad grids over window supports (_support_grid)
         self._build_ops()
         self._drop_mask_only_outputs()
+        self._plan_tails()
 
     # ---------------- receptive-field windows ----------------
     def _cone(self, seed):
@@ -840,7 +841,12 @@ class NetPlan:
         net, blocks, B = self.net, self.net.blocks, self.B
         lib = self.lib
         P = lambda t: nat.c_void_p(t.data_ptr()) if t is not None else None
-        fwd = []
+        fwd, fblk = [], []
+
+        def fa(op):
+            fwd.append(op)
+            fblk.append(i)
+
         for i, d in enumerate(blocks):
             t = d["type"]
             if t == "convolutional":
@@ -853,13 +859,13 @@ class NetPlan:
                 if i == 0 and self.first_pool:
                     args = (None, B, self.H, self.W, P(wts["w27"]), P(wts["bias"]), m["cout"], self.cp[i],
                             1 if m["act"] == "leaky" else 0, P(self.act[1]), P(self.argmax[1]), self.slot(self.act[1]))
-                    fwd.append(("po_conv_first_pool_fwd", args, "img0"))
+                    fa(("po_conv_first_pool_fwd", args, "img0"))
                     assert not fuse_next
                     continue
                 if i == 0 and self.first_direct:
                     args = (None, B, self.H, self.W, m["stride"], P(wts["w27"]), P(wts["bias"]), m["cout"],
                             self.cp[i], 1 if m["act"] == "leaky" else 0, P(y_out), self.slot(y_out))
-                    fwd.append(("po_conv_first_fwd", args, "img0"))
+                    fa(("po_conv_first_fwd", args, "img0"))
                     assert not fuse_next
                     continue
                 Hin, Win = (self.H, self.W) if src == INPUT else self.dims[src]
@@ -902,16 +908,16 @@ class NetPlan:
                         P(sum_out), None, None, None)
                 desc.macs = B * desc.Hg * desc.Wg * m["cout"] * m["cin"] * k * k      # logical channels
                 desc.block, desc.kind = i, "fwd"
-                fwd.append(("po_conv", args, desc))
+                fa(("po_conv", args, desc))
             elif t == "shortcut":
                 if i in self.fused:
                     continue
                 a, b = self.srcs[i]
                 M = B * self.dims[i][0] * self.dims[i][1]
                 C = self.shp[i][2]
-                fwd.append(("po_slice_accum", (P(self.act[a]), self.cp[a], 0, P(self.act[i]), self.cp[i], 0, M, C, 0,
+                fa(("po_slice_accum", (P(self.act[a]), self.cp[a], 0, P(self.act[i]), self.cp[i], 0, M, C, 0,
                                                None, 0, self.slot(self.act[i])), None))
-                fwd.append(("po_slice_accum", (P(self.act[b]), self.cp[b], 0, P(self.act[i]), self.cp[i], 0, M, C, 1,
+                fa(("po_slice_accum", (P(self.act[b]), self.cp[b], 0, P(self.act[i]), self.cp[i], 0, M, C, 1,
                                                None, 0, self.slot(self.act[i])), None))
             elif t == "route":
                 if len(self.srcs[i]) == 1:
@@ -921,32 +927,37 @@ class NetPlan:
                 for s in self.srcs[i]:
                     C = self.shp[s][2]
                     if self._same_view(s, i):
-                        fwd.append(("po_slice_accum", (P(self.act[s]), self.cp[s], 0, P(self.act[i]), self.cp[i], off,
+                        fa(("po_slice_accum", (P(self.act[s]), self.cp[s], 0, P(self.act[i]), self.cp[i], off,
                                                        M, C, 0, None, 0, self.slot(self.act[i])), None))
                     else:
-                        fwd.append(("po_view_move", self._move(self.act[s], s, 0, self.act[i], i, off, C, 0, 0, None),
+                        fa(("po_view_move", self._move(self.act[s], s, 0, self.act[i], i, off, C, 0, 0, None),
                                     None))
                     off += C
             elif t == "upsample":
                 s = self.srcs[i][0]
                 hs, ws_, cs = self.shp[s]
                 if self.win[i] is None and self.win[s] is None:
-                    fwd.append(("po_upsample2_fwd", (P(self.act[s]), B, hs, ws_, cs, self.cp[s], P(self.act[i]),
+                    fa(("po_upsample2_fwd", (P(self.act[s]), B, hs, ws_, cs, self.cp[s], P(self.act[i]),
                                                      self.cp[i], 0, self.slot(self.act[i])), None))
                 else:
-                    fwd.append(("po_view_move", self._move(self.act[s], s, 0, self.act[i], i, 0, cs, 1, 0, None),
+                    fa(("po_view_move", self._move(self.act[s], s, 0, self.act[i], i, 0, cs, 1, 0, None),
                                 None))
             elif t == "maxpool":
                 if (i == 1 and self.first_pool) or (i - 1) in self.conv_pool:
                     continue                    # fused into the producing conv
                 s = self.srcs[i][0]
                 hs, ws_, cs = self.shp[s]
-                fwd.append(("po_maxpool2_fwd", (P(self.act[s]), B, hs, ws_, cs, self.cp[s], int(d["stride"]),
+                fa(("po_maxpool2_fwd", (P(self.act[s]), B, hs, ws_, cs, self.cp[s], int(d["stride"]),
                                                 P(self.act[i]), P(self.argmax[i]), self.slot(self.act[i])), None))
-        self.fwd_ops = fwd
+        self.fwd_ops, self.fwd_blk = fwd, fblk
 
         # backward
-        bwd = []
+        bwd, bblk = [], []
+
+        def ba(op):
+            bwd.append(op)
+            bblk.append(j)
+
         done = [0] * self.n
         root = self.root
         for r in range(self.n):
@@ -977,7 +988,7 @@ class NetPlan:
                 b, _ = self.sc_alias[r]
                 _, mask_b, _ = contrib(b)
                 M = self.B * self.dims[r][0] * self.dims[r][1]
-                bwd.append(("po_slice_accum", (P(self.grad[r]), self.cp[r], 0, P(self.grad[b]), self.cp[b], 0, M,
+                ba(("po_slice_accum", (P(self.grad[r]), self.cp[r], 0, P(self.grad[b]), self.cp[b], 0, M,
                                                self.shp[r][2], 0, P(mask_b), self.cp[b], self.slot(self.grad[b])),
                             None))
 
@@ -993,20 +1004,20 @@ class NetPlan:
                 src = self.srcs[j][0]
                 if src == INPUT:
                     if self.first_direct:
-                        bwd.append(("po_conv_first_dgrad", (P(G), B, self.H, self.W, m["stride"], P(wts["w27"]),
+                        ba(("po_conv_first_dgrad", (P(G), B, self.H, self.W, m["stride"], P(wts["w27"]),
                                                             m["cout"], self.cp[j], "roi", "dimg"), None))
                     else:
                         for desc, wd, b0 in self._dgrad_descs(j, INPUT, 0, G, self.in_nhwc):
-                            bwd.append(("po_conv", (nat.ctypes.byref(desc), self._img_ptr(G, b0), P(wd), None,
+                            ba(("po_conv", (nat.ctypes.byref(desc), self._img_ptr(G, b0), P(wd), None,
                                                     self._img_ptr(self.in_nhwc, b0), None,
                                                     None, None, None, None), desc))
-                        bwd.append(("po_nhwc_to_nchw", (P(self.in_nhwc), B, self.H, self.W, 3, 16, "dimg"), None))
+                        ba(("po_nhwc_to_nchw", (P(self.in_nhwc), B, self.H, self.W, 3, 16, "dimg"), None))
                     continue
                 acc, mask, final = contrib(src)
                 y2, m2 = dual_of(src, final)
                 for desc, wd, b0 in self._dgrad_descs(j, src, acc, G, self.grad[src], y2):
                     if desc.mrows:
-                        bwd.append(("zero", (self.grad[src],), None))
+                        ba(("zero", (self.grad[src],), None))
                     Pb = lambda t: self._img_ptr(t, b0)
                     if not desc.mrows:
                         desc.gbox = self._cone_ptr(src, b0)
@@ -1014,7 +1025,7 @@ class NetPlan:
                     mb, m2b = self._img_ptr(self.bits_of(mask), b0), self._img_ptr(self.bits_of(m2), b0)
                     desc.mbits = mb.value if mb is not None else None
                     desc.m2bits = m2b.value if m2b is not None else None
-                    bwd.append(("po_conv", (nat.ctypes.byref(desc), Pb(G), P(wd), None, Pb(self.grad[src]), None, None,
+                    ba(("po_conv", (nat.ctypes.byref(desc), Pb(G), P(wd), None, Pb(self.grad[src]), None, None,
                                             None if desc.mbits else Pb(mask), Pb(y2),
                                             None if desc.m2bits else Pb(m2)), desc))
             elif t == "shortcut":
@@ -1024,7 +1035,7 @@ class NetPlan:
                     assert acc == 0
                     if mask is not None:               # f has no later contributor: apply its mask in place
                         M = self.B * self.dims[f][0] * self.dims[f][1]
-                        bwd.append(("po_slice_accum", (P(G), self.cp[j], 0, P(self.grad[f]), self.cp[f], 0, M,
+                        ba(("po_slice_accum", (P(G), self.cp[j], 0, P(self.grad[f]), self.cp[f], 0, M,
                                                        self.shp[f][2], 0, P(mask), self.cp[f], self.slot(self.grad[f])),
                                     None))
                     continue
@@ -1032,7 +1043,7 @@ class NetPlan:
                 C = self.shp[j][2]
                 for s_ in self.srcs[j]:
                     acc, mask, final = contrib(s_)
-                    bwd.append(("po_slice_accum", (P(G), self.cp[j], 0, P(self.grad[s_]), self.cp[s_], 0, M, C, acc,
+                    ba(("po_slice_accum", (P(G), self.cp[j], 0, P(self.grad[s_]), self.cp[s_], 0, M, C, acc,
                                                    P(mask), self.cp[s_], self.slot(self.grad[s_])), None))
                     fallback_dual(s_, final)
             elif t == "route":
@@ -1042,10 +1053,10 @@ class NetPlan:
                     C = self.shp[s_][2]
                     acc, mask, final = contrib(s_)
                     if self._same_view(s_, j):
-                        bwd.append(("po_slice_accum", (P(G), self.cp[j], off, P(self.grad[s_]), self.cp[s_], 0, M, C,
+                        ba(("po_slice_accum", (P(G), self.cp[j], off, P(self.grad[s_]), self.cp[s_], 0, M, C,
                                                        acc, P(mask), self.cp[s_], self.slot(self.grad[s_])), None))
                     else:
-                        bwd.append(("po_view_move", self._move(G, j, off, self.grad[s_], s_, 0, C, 0, acc, mask),
+                        ba(("po_view_move", self._move(G, j, off, self.grad[s_], s_, 0, C, 0, acc, mask),
                                     None))
                     fallback_dual(s_, final)
                     off += C
@@ -1054,11 +1065,11 @@ class NetPlan:
                 acc, mask, final = contrib(s_)
                 hs, ws_, cs = self.shp[s_]
                 if self.win[j] is None and self.win[s_] is None:
-                    bwd.append(("po_upsample2_bwd", (P(G), self.cp[j], 0, B, hs, ws_, cs, P(self.grad[s_]),
+                    ba(("po_upsample2_bwd", (P(G), self.cp[j], 0, B, hs, ws_, cs, P(self.grad[s_]),
                                                      self.cp[s_], acc, P(mask), self.cp[s_], self.slot(self.grad[s_])),
                                 None))
                 else:
-                    bwd.append(("po_view_move", self._move(G, j, 0, self.grad[s_], s_, 0, cs, 2, acc, mask), None))
+                    ba(("po_view_move", self._move(G, j, 0, self.grad[s_], s_, 0, cs, 2, acc, mask), None))
                 fallback_dual(s_, final)
             elif t == "maxpool":
                 s_ = self.srcs[j][0]
@@ -1070,12 +1081,97 @@ class NetPlan:
                 hs, ws_, cs = self.shp[s_]
                 # on a gradient-cone source only its per-image boxes are written
                 cone = self._cone_ptr(s_, 0)
-                bwd.append(("po_maxpool2_bwd_box", (P(G), P(self.argmax[j]), B, hs, ws_, cs, self.cp[s_],
+                ba(("po_maxpool2_bwd_box", (P(G), P(self.argmax[j]), B, hs, ws_, cs, self.cp[s_],
                                                     int(d["stride"]), P(self.grad[s_]), acc, P(mask),
                                                     nat.c_void_p(cone) if cone else None,
                                                     self.slot(self.grad[s_])), None))
                 fallback_dual(s_, final)
-        self.bwd_ops = bwd
+        self.bwd_ops, self.bwd_blk = bwd, bblk
+
+    # ---------------- head tails on a second stream ----------------
+    def _plan_tails(self):
+        """Head tails: the chain of convs that feeds a YOLO head and nothing
+        else (yolov3: blocks 80-81 and 92-93; yolov3-tiny: 14-15), after the
+        branch point b whose other consumer carries on to the next head.
+        Their launches (receptive-field windows: small, latency-bound) run on
+        a second stream concurrently with the main chain: in the forward from
+        the end of block b on, joined before the heads are returned; in the
+        backward from the head-gradient copy on, except the group that
+        accumulates into grad[b], which runs in its place of the original
+        order (the accumulation order, hence the bits, are unchanged) with the
+        main stream waiting on it.  The last head's tail has nothing after it
+        to overlap and stays on the main stream.  ADVPATCH_STREAMS=0: off."""
+        self.tails = []
+        self.side = None
+        self.ws_side = None
+        if os.environ.get("ADVPATCH_STREAMS", "1") == "0" or torch.device(self.device).type != "cuda":
+            return
+        for chain, src in self.tail_chains():
+            tail = set(chain)
+            f_ops = [k for k, b in enumerate(self.fwd_blk) if b in tail]
+            trigger = max(k for k, b in enumerate(self.fwd_blk) if b <= src)
+            b_early = [k for k, b in enumerate(self.bwd_blk) if b in tail and b != chain[0]]
+            b_final = [k for k, b in enumerate(self.bwd_blk) if b == chain[0]]
+            if not f_ops or not b_final or trigger >= f_ops[0]:
+                continue
+            self.tails.append({"blocks": chain, "branch": src, "fwd": f_ops, "trigger": trigger,
+                               "bwd_early": b_early, "bwd_final": b_final})
+        if self.tails:
+            self.side = torch.cuda.Stream(device=self.device)
+            self._side_f = {k for t in self.tails for k in t["fwd"]}
+            self._trig_f = {}
+            for t in self.tails:
+                self._trig_f.setdefault(t["trigger"], []).append(t)
+            self._side_b = {k for t in self.tails for k in t["bwd_early"] + t["bwd_final"]}
+            self._final_b = {t["bwd_final"][0]: t for t in self.tails}
+            self.bind_side_workspace()
+
+    def tail_chains(self):
+        """[(tail blocks in forward order, branch point b)] of every head but
+        the last: the convs from b's consumer up to the YOLO layer, each the
+        only consumer of the one before."""
+        blocks, n = self.net.blocks, self.n
+        cons = [set() for _ in range(n)]
+        for i in range(n):
+            for src in self.srcs[i]:
+                if src != INPUT:
+                    cons[src].add(i)
+        out = []
+        for y in self.heads:
+            chain, nxt, src = [], y, self.srcs[y][0]
+            while (src != INPUT and blocks[src]["type"] == "convolutional" and self.root[src] == src
+                   and cons[src] == {nxt} and src not in self.fused and (src + 1) not in self.fused
+                   and src not in self.conv_pool):
+                chain.append(src)
+                nxt, src = src, self.srcs[src][0]
+            if not chain or src == INPUT or src in self.sc_alias or any(src in v for v in self.sc_alias.values()):
+                continue
+            chain.reverse()                       # forward order: chain[0] reads act[b]
+            if not any(i > chain[-1] and blocks[i]["type"] != "yolo" and i not in chain for i in range(n)):
+                continue                          # the last head: nothing after it to overlap
+            out.append((chain, src))
+        return out
+
+    def _side_descs(self):
+        for t in self.tails:
+            for k in t["fwd"]:
+                if self.fwd_ops[k][0] == "po_conv":
+                    yield self.fwd_ops[k][2]
+            for k in t["bwd_early"] + t["bwd_final"]:
+                if self.bwd_ops[k][0] == "po_conv":
+                    yield self.bwd_ops[k][2]
+
+    def bind_side_workspace(self):
+        """Split-K launches on the second stream get their own workspace (the
+        main one is stream-ordered on the main stream only)."""
+        if not self.tails:
+            return
+        need = max([d.ksplit * d.B * d.Hg * d.Wg * d.N for d in self._side_descs() if d.ksplit > 1] + [0])
+        if need and (self.ws_side is None or self.ws_side.numel() < need):
+            self.ws_side = torch.empty(need, device=self.device)
+        for d in self._side_descs():
+            if d.ksplit > 1:
+                d.workspace = self.ws_side.data_ptr()
 
     def _orgp(self, i):
         o = self.org_of(i)
@@ -1224,6 +1320,7 @@ class NetPlan:
                 key = self._tune_key(args, desc)
                 if key in cache:
                     self._set_tile(desc, cache[key])
+            self.bind_side_workspace()
             return
         if all(self._tune_key(args, desc) in cache for args, desc in convs):
             for args, desc in convs:                 # every shape already tuned: no launches
@@ -1231,6 +1328,7 @@ class NetPlan:
             for args, desc in convs:
                 if desc.ksplit > 1:
                     desc.workspace = self.ws.data_ptr()
+            self.bind_side_workspace()
             return
         bufs = {id(t): t for t in self.act + self.grad if t is not None}
         if self.in_nhwc is not None:
@@ -1319,6 +1417,7 @@ class NetPlan:
         for name, _, desc in self.fwd_ops + self.bwd_ops:     # the workspace may have grown
             if name == "po_conv" and desc.ksplit > 1:
                 desc.workspace = self.ws.data_ptr()
+        self.bind_side_workspace()
         with torch.no_grad():
             for t in bufs.values():
                 t.zero_()
@@ -1355,10 +1454,24 @@ class NetPlan:
         xp = nat.c_void_p(x.data_ptr())
         if not self.first_direct:
             nat.call("po_nchw_to_nhwc", xp, self.B, self.H, self.W, 3, 16, nat.c_void_p(self.in_nhwc.data_ptr()), st)
-        for name, args, desc in self.fwd_ops:
+        side = self.side if self.tails else None
+        for k, (name, args, desc) in enumerate(self.fwd_ops):
+            if side is not None and k in self._side_f:
+                continue                                  # a head tail: launched on the side stream
             if name in ("po_conv_first_fwd", "po_conv_first_pool_fwd"):
                 args = (xp,) + args[1:]
             self._launch(lib, name, args, desc, st)
+            if side is not None and k in self._trig_f:
+                # block b is done: its tail runs beside the rest of the network
+                side.wait_stream(torch.cuda.current_stream())
+                with torch.cuda.stream(side):
+                    sst = nat.stream()
+                    for t in self._trig_f[k]:
+                        for kk in t["fwd"]:
+                            n_, a_, d_ = self.fwd_ops[kk]
+                            self._launch(lib, n_, a_, d_, sst)
+        if side is not None:
+            torch.cuda.current_stream().wait_stream(side)
         return [self.act[h] for h in self.heads]
 
     def _launch(self, lib, name, args, desc, st):
@@ -1395,16 +1508,41 @@ class NetPlan:
         self.set_support_boxes()
         if self.conv_timer is not None and self.cone_boxes is not None:
             self._cone_snap = self.cone_boxes.clone()        # this step's cones, for launch_macs
-        for name, args, desc in self.bwd_ops:
+        side = self.side if self.tails else None
+
+        def run(k, sst):
+            name, args, desc = self.bwd_ops[k]
             if name == "zero":
                 args[0].zero_()
-                continue
+                return
             if args and args[-1] == "dimg":
                 if name == "po_conv_first_dgrad":
                     args = args[:-2] + (roip, dxp)
                 else:
                     args = args[:-1] + (dxp,)
-            self._launch(lib, name, args, desc, st)
+            self._launch(lib, name, args, desc, sst)
+
+        if side is not None:
+            # the head gradients, cones and support boxes are in place: the tails'
+            # inner dgrads start beside the main chain
+            side.wait_stream(torch.cuda.current_stream())
+            with torch.cuda.stream(side):
+                sst = nat.stream()
+                for t in self.tails:
+                    for k in t["bwd_early"]:
+                        run(k, sst)
+        for k in range(len(self.bwd_ops)):
+            if side is not None and k in self._side_b:
+                if k in self._final_b:
+                    # the group accumulating into grad[b], in its place of the order
+                    side.wait_stream(torch.cuda.current_stream())
+                    with torch.cuda.stream(side):
+                        sst = nat.stream()
+                        for kk in self._final_b[k]["bwd_final"]:
+                            run(kk, sst)
+                    torch.cuda.current_stream().wait_stream(side)
+                continue
+            run(k, st)
 
 
 

@@ -158,3 +158,22 @@ def test_graft_entry_build_runs():
     __graft_entry__.build()
     nat = pkg_mod("_native")
     assert nat.load().po_abi_version() == nat.PO_ABI_VERSION
+
+
+@pytest.mark.parametrize("cfg,H,want", [("builtin:yolov3-dota", 128, [([80, 81], 79), ([92, 93], 91)]),
+                                        ("builtin:yolov3-tiny-dota", 128, [([14, 15], 13)]),
+                                        ("builtin:mini3", 64, [([15, 16], 14), ([23, 24], 22)])])
+def test_head_tails(cfg, H, want):
+    """NetPlan.tail_chains: the convs that feed a YOLO head and nothing else,
+    after the branch point whose other consumer leads on to the next head
+    (run on the second stream); the last head's tail is not one of them."""
+    W, dk = pkg_mod("weights"), pkg_mod("darknet_v3")
+    net = dk.Darknet(cfg)
+    import tempfile
+    with tempfile.TemporaryDirectory() as td:
+        p = os.path.join(td, "m.weights")
+        W.write_weights(p, W.synthesize(cfg))
+        net.load_darknet_weights(p)
+    plan = net.plan(1, H, H, torch.device("cpu"))
+    assert plan.tail_chains() == want
+    assert plan.tails == []                   # no second stream off the GPU

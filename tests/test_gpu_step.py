@@ -344,3 +344,29 @@ def test_sign_bit_masks_match_fp32_masks(tmp_path, cfg, B, P, monkeypatch):
             assert plan.leaky_signs(i).shape == (B,) + plan.dims[i] + (plan.shp[i][2],)
         out.append(pg.grad.detach().clone())
     assert torch.equal(out[0], out[1]) and torch.equal(out[0], out[2])
+
+
+@pytest.mark.parametrize("cfg,B,P", [("builtin:mini3", 4, 32), ("builtin:yolov3-tiny-dota", 3, 96),
+                                     ("builtin:yolov3-dota", 2, 224)])
+def test_head_tails_on_a_second_stream_change_nothing(tmp_path, cfg, B, P, monkeypatch):
+    """The head tails' launches on the second stream (NetPlan._plan_tails)
+    keep every accumulation in its order: loss terms, cells and the patch
+    gradient bit-identical to the one-stream run."""
+    sy = pkg_mod("synthetic")
+    out = []
+    for streams in ("1", "0"):
+        monkeypatch.setenv("ADVPATCH_STREAMS", streams)
+        tr, ref_net = _trainer(cfg, tmp_path, prec="fp32")
+        S = ref_net.height
+        img, lab = sy.frames(B, S, seed=60).to(DEV), sy.labels(B, seed=61).to(DEV)
+        dr = {k: v.to(DEV) for k, v in sy.draws(B, P, seed=63).items()}
+        pg = sy.patch(P, seed=62).to(DEV).requires_grad_(True)
+        loss, terms = tr.losses(pg, img, lab, dr)
+        loss.backward()
+        assert bool(tr.last_plan.tails) == (streams == "1")
+        out.append((terms, pg.grad.detach().clone()))
+    (t1, g1), (t0, g0) = out
+    assert torch.equal(g1, g0)
+    assert t1["cells"].tolist() == t0["cells"].tolist()
+    for k in ("loss", "no_obj_loss", "no_cls_loss", "nps_loss", "tv_loss", "colorful_loss"):
+        assert float(t1[k]) == float(t0[k]), k
