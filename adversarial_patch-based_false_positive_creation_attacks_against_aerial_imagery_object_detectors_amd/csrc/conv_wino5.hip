@@ -258,10 +258,13 @@ __global__ __launch_bounds__(512, 1) void conv_wino5_k(const ConvArgs a, const f
             // sign bits: 8 lanes hold the 32 channels of one word
             const uint32_t nib = ok ? ((out.x > 0.f ? 1u : 0u) | (out.y > 0.f ? 2u : 0u) | (out.z > 0.f ? 4u : 0u) |
                                        (out.w > 0.f ? 8u : 0u)) : 0u;
+            // (OR of lanes i..i+7 into lane i by DPP row shifts, dst[i] = src[i + n] within
+            // a 16-lane row: VALU-rate, where __shfl_xor's three dependent LDS crossbar
+            // round trips per pixel were ~1 us of every unit's emit)
             uint32_t w = nib << (4 * (lane & 7));
-            w |= (uint32_t)__shfl_xor((int)w, 1);
-            w |= (uint32_t)__shfl_xor((int)w, 2);
-            w |= (uint32_t)__shfl_xor((int)w, 4);
+            w |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)w, 0x101, 0xF, 0xF, false);   // row_shl:1
+            w |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)w, 0x102, 0xF, 0xF, false);   // row_shl:2
+            w |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)w, 0x104, 0xF, 0xF, false);   // row_shl:4
             bst1(w, rsrc(a.ybits, bits_bytes),
                  (ok && (lane & 7) == 0) ? (pix * (uint32_t)wpp + (uint32_t)(vn4 >> 5)) * 4u : kOOB);
           }
