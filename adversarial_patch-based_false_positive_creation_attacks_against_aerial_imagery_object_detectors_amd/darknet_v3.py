@@ -1100,11 +1100,15 @@ class NetPlan:
         accumulates into grad[b], which runs in its place of the original
         order (the accumulation order, hence the bits, are unchanged) with the
         main stream waiting on it.  The last head's tail has nothing after it
-        to overlap and stays on the main stream.  ADVPATCH_STREAMS=0: off."""
+        to overlap and stays on the main stream.  Opt-in (ADVPATCH_STREAMS=1):
+        measured not to pay on the bench plans (interleaved A/B, yolov3 B=16:
+        887/889 img/s with the second stream against 903/889 without;
+        profiles/r04/streams_ab.txt), the tails' windows being too small to
+        fill what the main chain leaves idle."""
         self.tails = []
         self.side = None
         self.ws_side = None
-        if os.environ.get("ADVPATCH_STREAMS", "1") == "0" or torch.device(self.device).type != "cuda":
+        if os.environ.get("ADVPATCH_STREAMS", "0") != "1" or torch.device(self.device).type != "cuda":
             return
         for chain, src in self.tail_chains():
             tail = set(chain)
