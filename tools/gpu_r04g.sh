@@ -7,7 +7,7 @@ OUT=gpurun_out/${TAGOUT:-r04g}
 mkdir -p $OUT
 (while sleep 45; do echo "tick $(date +%T)"; done) & HB=$!
 trap "kill $HB" EXIT
-timeout -k 10 1000 python -u -m pytest tests -m gpu -q --timeout 900 --timeout-method thread > $OUT/tests.log 2>&1
+timeout -k 10 1000 python -u -m pytest tests -m gpu -q --timeout 900 --timeout-method thread ${TESTSEL:-} > $OUT/tests.log 2>&1
 rc=$?; tail -3 $OUT/tests.log; [ $rc -eq 0 ] || exit $rc
 timeout -k 10 600 python -u bench.py > $OUT/bench.json 2> $OUT/bench.err || { echo "bench failed"; tail -20 $OUT/bench.err; exit 1; }
 cut -c1-300 $OUT/bench.json
