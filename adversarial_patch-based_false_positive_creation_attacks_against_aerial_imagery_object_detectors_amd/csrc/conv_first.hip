@@ -2,6 +2,7 @@
 // as VALU direct convolution (K = 27 is too short for a matrix-core GEMM), and
 // its input gradient, restricted to the patch footprint on the training path.
 #include "common.h"
+#include "warp_geom.h"
 
 namespace {
 // ------------------------------------------------------------------------
@@ -73,13 +74,22 @@ __global__ __launch_bounds__(256) void first_fwd_k(const float* __restrict__ img
 // the hardware range check instead of branching.  The two 256-pixel halves
 // are staged through LDS and stored as two contiguous 16-byte-per-lane streams.
 typedef float f2_t __attribute__((ext_vector_type(2)));
+//
+// Composite source (pimg != NULL, po_conv_first_fwd_cmp): the input is the
+// patch composite, of which only the quad box of each image's footprint
+// (po::quad_box, what po_warp_box_fwd_keyed writes) is in pimg; everywhere
+// else it equals img.  A wave whose taps all miss the boxes runs the plain
+// loads; a wave with a tap inside a box reads each tap from the tensor that
+// holds it (the same values, so the same bits as on the materialised composite).
 template <int CO>
 __global__ __launch_bounds__(256) void first_fwd2_k(const float* __restrict__ img, int B, int H, int W,
                                                     int stride, int Ho, int Wo,
                                                     const float* __restrict__ Wt,
                                                     const float* __restrict__ bias, int Cout,
                                                     int act, float* __restrict__ y,
-                                                    uint32_t* __restrict__ amax) {
+                                                    uint32_t* __restrict__ amax,
+                                                    const float* __restrict__ pimg,
+                                                    const int32_t* __restrict__ roi) {
   constexpr int LS = CO + 1;
   __shared__ float ys[256 * LS];
   const int64_t npix = (int64_t)B * Ho * Wo;
@@ -99,18 +109,39 @@ __global__ __launch_bounds__(256) void first_fwd2_k(const float* __restrict__ im
     const int rem = p - b * Ho * Wo;
     const int i = rem / Wo, j = rem - i * Wo;
     const uint32_t ib = (uint32_t)b * 3u * plane;
+    po::QBox bx = {0, 0, 0, 0};
+    bool touch = false;
+    if (pimg) {
+      bx = po::quad_box(roi, b, W);
+      touch = live && i * stride + 1 >= bx.y0 && i * stride - 1 < bx.y1 && j * stride + 1 >= bx.qx0 &&
+              j * stride - 1 < bx.qx1;
+    }
+    if (!__any(touch)) {
 #pragma unroll
-    for (int kh = 0; kh < 3; ++kh)
+      for (int kh = 0; kh < 3; ++kh)
 #pragma unroll
-      for (int kw = 0; kw < 3; ++kw) {
-        const int hi = i * stride - 1 + kh, wi = j * stride - 1 + kw;
-        const bool ok = live && (unsigned)hi < (unsigned)H && (unsigned)wi < (unsigned)W;
-        const uint32_t o = ok ? ib + ((uint32_t)hi * W + wi) * 4u : kOOB;
+        for (int kw = 0; kw < 3; ++kw) {
+          const int hi = i * stride - 1 + kh, wi = j * stride - 1 + kw;
+          const bool ok = live && (unsigned)hi < (unsigned)H && (unsigned)wi < (unsigned)W;
+          const uint32_t o = ok ? ib + ((uint32_t)hi * W + wi) * 4u : kOOB;
 #pragma unroll
-        for (int c = 0; c < 3; ++c)
-          x[c * 9 + kh * 3 + kw][q] = __builtin_bit_cast(
-              float, __builtin_amdgcn_raw_buffer_load_b32(rs, ok ? o + c * plane : kOOB, 0, 0));
-      }
+          for (int c = 0; c < 3; ++c)
+            x[c * 9 + kh * 3 + kw][q] = __builtin_bit_cast(
+                float, __builtin_amdgcn_raw_buffer_load_b32(rs, ok ? o + c * plane : kOOB, 0, 0));
+        }
+    } else {
+#pragma unroll
+      for (int kh = 0; kh < 3; ++kh)
+#pragma unroll
+        for (int kw = 0; kw < 3; ++kw) {
+          const int hi = i * stride - 1 + kh, wi = j * stride - 1 + kw;
+          const bool ok = live && (unsigned)hi < (unsigned)H && (unsigned)wi < (unsigned)W;
+          const bool in = hi >= bx.y0 && hi < bx.y1 && wi >= bx.qx0 && wi < bx.qx1;
+          const float* src = (in ? pimg : img) + (size_t)b * 3 * H * W + (size_t)hi * W + wi;
+#pragma unroll
+          for (int c = 0; c < 3; ++c) x[c * 9 + kh * 3 + kw][q] = ok ? src[(size_t)c * H * W] : 0.f;
+        }
+    }
   }
   f2_t out[CO];
   f2_t vmax = {0.f, 0.f};
@@ -170,7 +201,9 @@ __global__ __launch_bounds__(256) void first_pool_fwd_k(const float* __restrict_
                                                         int Hp, int Wp, const float* __restrict__ Wt,
                                                         const float* __restrict__ bias, int Cout, int act,
                                                         float* __restrict__ y, int8_t* __restrict__ am,
-                                                        uint32_t* __restrict__ amax) {
+                                                        uint32_t* __restrict__ amax,
+                                                        const float* __restrict__ pimg,
+                                                        const int32_t* __restrict__ roi) {
   constexpr int LS = CO + 1;
   __shared__ float ys[256 * LS];
   const int npix = B * Hp * Wp;                     // < 2^31 (host check)
@@ -190,24 +223,45 @@ __global__ __launch_bounds__(256) void first_pool_fwd_k(const float* __restrict_
   // xp[c][r][q] = {x(row 2py-1+r, col 2px-1+q), x(row, col + 1)}: the operand
   // pair of the two outputs (dx = 0, 1) of one output row at tap column q
   f2_t xp[3][4][3];
-#pragma unroll
-  for (int r = 0; r < 4; ++r) {
-    const int hi = 2 * py - 1 + r;
-    float xr[3][4];
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const int wi = 2 * px - 1 + q;
-      const bool ok = live && (unsigned)hi < (unsigned)H && (unsigned)wi < (unsigned)W;
-      const uint32_t o = ib + ((uint32_t)hi * W + wi) * 4u;
-#pragma unroll
-      for (int c = 0; c < 3; ++c)
-        xr[c][q] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rs, ok ? o + c * plane : kOOB, 0, 0));
-    }
-#pragma unroll
-    for (int c = 0; c < 3; ++c)
-#pragma unroll
-      for (int q = 0; q < 3; ++q) xp[c][r][q] = (f2_t){xr[c][q], xr[c][q + 1]};
+  // composite source: as first_fwd2_k (the 4x4 input window of the pooled pixel)
+  po::QBox bx = {0, 0, 0, 0};
+  bool touch = false;
+  if (pimg) {
+    bx = po::quad_box(roi, b, W);
+    touch = live && 2 * py + 2 >= bx.y0 && 2 * py - 1 < bx.y1 && 2 * px + 2 >= bx.qx0 && 2 * px - 1 < bx.qx1;
   }
+  float xa[3][4][4];
+  if (!__any(touch)) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int hi = 2 * py - 1 + r, wi = 2 * px - 1 + q;
+        const bool ok = live && (unsigned)hi < (unsigned)H && (unsigned)wi < (unsigned)W;
+        const uint32_t o = ib + ((uint32_t)hi * W + wi) * 4u;
+#pragma unroll
+        for (int c = 0; c < 3; ++c)
+          xa[c][r][q] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rs, ok ? o + c * plane : kOOB, 0, 0));
+      }
+  } else {
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int hi = 2 * py - 1 + r, wi = 2 * px - 1 + q;
+        const bool ok = live && (unsigned)hi < (unsigned)H && (unsigned)wi < (unsigned)W;
+        const bool in = hi >= bx.y0 && hi < bx.y1 && wi >= bx.qx0 && wi < bx.qx1;
+        const float* src = (in ? pimg : img) + (size_t)b * 3 * H * W + (size_t)hi * W + wi;
+#pragma unroll
+        for (int c = 0; c < 3; ++c) xa[c][r][q] = ok ? src[(size_t)c * H * W] : 0.f;
+      }
+  }
+#pragma unroll
+  for (int c = 0; c < 3; ++c)
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+#pragma unroll
+      for (int q = 0; q < 3; ++q) xp[c][r][q] = (f2_t){xa[c][r][q], xa[c][r][q + 1]};
   float vmax = 0.f;
   uint32_t aw[CO / 4];
 #pragma unroll
@@ -331,9 +385,9 @@ __global__ __launch_bounds__(256) void first_dgrad_k(const float* __restrict__ D
 }
 }  // namespace
 
-extern "C" int po_conv_first_fwd(const float* img, int B, int H, int W, int stride, const float* Wt,
-                                 const float* bias, int Cout, int Cout_p, int act, float* y,
-                                 uint32_t* amax, po_stream_t s) {
+namespace {
+int first_fwd(const float* img, const float* pimg, const int32_t* roi, int B, int H, int W, int stride, const float* Wt,
+              const float* bias, int Cout, int Cout_p, int act, float* y, uint32_t* amax, po_stream_t s) {
   PO_REQUIRE(img && Wt && y, "po_conv_first_fwd: null pointer");
   PO_REQUIRE(stride == 1 || stride == 2, "po_conv_first_fwd: stride %d", stride);
   PO_REQUIRE(Cout > 0 && Cout <= 64 && Cout_p % 4 == 0 && Cout_p >= Cout, "po_conv_first_fwd: Cout=%d Cout_p=%d", Cout, Cout_p);
@@ -345,23 +399,27 @@ extern "C" int po_conv_first_fwd(const float* img, int B, int H, int W, int stri
   PO_REQUIRE(Cout_p == CO, "po_conv_first_fwd: Cout_p must be 16, 32 or 64 (got %d)", Cout_p);
   PO_REQUIRE((int64_t)B * 3 * H * W * 4 < (1LL << 31) && n + 512 < (1LL << 31),
              "po_conv_first_fwd: image batch must be < 2 GiB");
+  PO_REQUIRE(!pimg || (roi && CO <= 32 && H == W), "po_conv_first_fwd_cmp: needs roi, a square image and Cout_p <= 32");
   dim3 grid2(po::ceil_div(n, 512));
   if (CO == 16)
-    hipLaunchKernelGGL(first_fwd2_k<16>, grid2, dim3(256), 0, st, img, B, H, W, stride, Ho, Wo, Wt, bias, Cout, act, y, amax);
+    hipLaunchKernelGGL(first_fwd2_k<16>, grid2, dim3(256), 0, st, img, B, H, W, stride, Ho, Wo, Wt, bias, Cout, act, y, amax,
+                       pimg, roi);
   else if (CO == 32)
-    hipLaunchKernelGGL(first_fwd2_k<32>, grid2, dim3(256), 0, st, img, B, H, W, stride, Ho, Wo, Wt, bias, Cout, act, y, amax);
+    hipLaunchKernelGGL(first_fwd2_k<32>, grid2, dim3(256), 0, st, img, B, H, W, stride, Ho, Wo, Wt, bias, Cout, act, y, amax,
+                       pimg, roi);
   else
     hipLaunchKernelGGL(first_fwd_k<64>, grid, dim3(256), 0, st, img, B, H, W, stride, Ho, Wo, Wt, bias, Cout, Cout_p, act, y, amax);
   return po::check_launch("po_conv_first_fwd");
 }
 
-extern "C" int po_conv_first_pool_fwd(const float* img, int B, int H, int W, const float* Wt, const float* bias,
-                                      int Cout, int Cout_p, int act, float* y, int8_t* argmax, uint32_t* amax,
-                                      po_stream_t s) {
+int first_pool_fwd(const float* img, const float* pimg, const int32_t* roi, int B, int H, int W, const float* Wt,
+                   const float* bias, int Cout, int Cout_p, int act, float* y, int8_t* argmax, uint32_t* amax,
+                   po_stream_t s) {
   PO_REQUIRE(img && Wt && y && argmax, "po_conv_first_pool_fwd: null pointer");
   PO_REQUIRE((Cout_p == 16 || Cout_p == 32) && Cout > 0 && Cout <= Cout_p,
              "po_conv_first_pool_fwd: Cout_p must be 16 or 32 (got %d, Cout %d)", Cout_p, Cout);
   PO_REQUIRE(B > 0 && H >= 2 && W >= 2, "po_conv_first_pool_fwd: bad size B=%d H=%d W=%d", B, H, W);
+  PO_REQUIRE(!pimg || (roi && H == W), "po_conv_first_pool_fwd_cmp: needs roi and a square image");
   const int Hp = H / 2, Wp = W / 2;
   const int64_t n = (int64_t)B * Hp * Wp;
   PO_REQUIRE((int64_t)B * 3 * H * W * 4 < (1LL << 31) && n + 256 < (1LL << 31),
@@ -370,11 +428,38 @@ extern "C" int po_conv_first_pool_fwd(const float* img, int B, int H, int W, con
   dim3 grid(po::ceil_div(n, 256));
   if (Cout_p == 16)
     hipLaunchKernelGGL(first_pool_fwd_k<16>, grid, dim3(256), 0, st, img, B, H, W, Hp, Wp, Wt, bias, Cout, act, y,
-                       argmax, amax);
+                       argmax, amax, pimg, roi);
   else
     hipLaunchKernelGGL(first_pool_fwd_k<32>, grid, dim3(256), 0, st, img, B, H, W, Hp, Wp, Wt, bias, Cout, act, y,
-                       argmax, amax);
+                       argmax, amax, pimg, roi);
   return po::check_launch("po_conv_first_pool_fwd");
+}
+}  // namespace
+
+extern "C" int po_conv_first_fwd(const float* img, int B, int H, int W, int stride, const float* Wt,
+                                 const float* bias, int Cout, int Cout_p, int act, float* y,
+                                 uint32_t* amax, po_stream_t s) {
+  return first_fwd(img, nullptr, nullptr, B, H, W, stride, Wt, bias, Cout, Cout_p, act, y, amax, s);
+}
+
+extern "C" int po_conv_first_fwd_cmp(const float* img, const float* pimg, const int32_t* roi, int B, int H, int W,
+                                     int stride, const float* Wt, const float* bias, int Cout, int Cout_p, int act,
+                                     float* y, uint32_t* amax, po_stream_t s) {
+  PO_REQUIRE(pimg, "po_conv_first_fwd_cmp: null composite");
+  return first_fwd(img, pimg, roi, B, H, W, stride, Wt, bias, Cout, Cout_p, act, y, amax, s);
+}
+
+extern "C" int po_conv_first_pool_fwd(const float* img, int B, int H, int W, const float* Wt, const float* bias,
+                                      int Cout, int Cout_p, int act, float* y, int8_t* argmax, uint32_t* amax,
+                                      po_stream_t s) {
+  return first_pool_fwd(img, nullptr, nullptr, B, H, W, Wt, bias, Cout, Cout_p, act, y, argmax, amax, s);
+}
+
+extern "C" int po_conv_first_pool_fwd_cmp(const float* img, const float* pimg, const int32_t* roi, int B, int H, int W,
+                                          const float* Wt, const float* bias, int Cout, int Cout_p, int act, float* y,
+                                          int8_t* argmax, uint32_t* amax, po_stream_t s) {
+  PO_REQUIRE(pimg, "po_conv_first_pool_fwd_cmp: null composite");
+  return first_pool_fwd(img, pimg, roi, B, H, W, Wt, bias, Cout, Cout_p, act, y, argmax, amax, s);
 }
 
 extern "C" int po_conv_first_dgrad(const float* D, int B, int H, int W, int stride, const float* Wt,

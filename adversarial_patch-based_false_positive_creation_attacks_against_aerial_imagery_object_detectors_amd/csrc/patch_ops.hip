@@ -638,6 +638,7 @@ __global__ __launch_bounds__(256) void warp_bwd_b_k(const float* __restrict__ gf
     const float cb = contrast[b], bb = g.pre ? 0.f : bright[b];
     const NoiseSrc nz = noise_src(noise, g, b);
     float a0 = 0.f, a1 = 0.f, a2 = 0.f;
+    bool cand = false;
     const float* gb = gfac + (size_t)b * 3 * plane;
     for (int i = i0; i <= i1; ++i)
       for (int j = j0; j <= j1; ++j) {
@@ -654,7 +655,13 @@ __global__ __launch_bounds__(256) void warp_bwd_b_k(const float* __restrict__ gf
         a0 += w * gv[0];
         a1 += w * gv[1];
         a2 += w * gv[2];
+        cand = true;
       }
+    // no output pixel of this image has (r, c) as a corner: its term is +0
+    // (a = +0, contrast > 0), and adding +0 never changes d (which starts at +0
+    // and so is never -0), so the image is skipped exactly -- and with it the
+    // pre-augmented value (keyed: a Philox call) the clamp test below needs
+    if (!cand) continue;
     // through clamp(adv*contrast + bright + noise) and * contrast, summed over images
     const float av[3] = {a0, a1, a2};
     float dd[3];
@@ -856,19 +863,8 @@ __global__ __launch_bounds__(256) void augment_k(const float* __restrict__ mp, c
 // box's pixels, one per thread (the footprint is a few percent of the frame:
 // spread over many waves instead of a few heavy quads).  Same per-pixel
 // arithmetic as warp_fwd4_k / warp_bwd_a4_k, so bit-identical outputs.
-struct QBox {
-  int qx0, qx1, y0, y1;
-};
-__device__ __forceinline__ QBox quad_box(const int32_t* roi, int b, int S) {
-  const int4 r = reinterpret_cast<const int4*>(roi)[b];
-  QBox q;
-  q.qx0 = r.x & ~3;
-  q.qx1 = min(S, (r.z + 3) & ~3);
-  q.y0 = r.y;
-  q.y1 = r.w;
-  if (q.qx1 <= q.qx0 || q.y1 <= q.y0) q.qx0 = q.qx1 = q.y0 = q.y1 = 0;
-  return q;
-}
+using po::QBox;
+using po::quad_box;
 
 __global__ __launch_bounds__(256) void warp_quad_copy_k(const float* __restrict__ img, const int32_t* __restrict__ roi,
                                                         int S, int mode, float* __restrict__ out) {
@@ -888,7 +884,10 @@ __global__ __launch_bounds__(256) void warp_quad_copy_k(const float* __restrict_
   }
 }
 
-__global__ __launch_bounds__(256) void warp_box_fwd_k(const float* __restrict__ img, const double* __restrict__ affine,
+__global__ __launch_bounds__(256) void warp_box_fwd_k(const float* __restrict__ img, const float* __restrict__ mp,
+                                                      const float* __restrict__ contrast,
+                                                      const float* __restrict__ bright,
+                                                      const double* __restrict__ affine,
                                                       const int32_t* __restrict__ roi, WarpGeom g, int mode,
                                                       float* __restrict__ out) {
   const int b = blockIdx.y;
@@ -896,13 +895,15 @@ __global__ __launch_bounds__(256) void warp_box_fwd_k(const float* __restrict__ 
   const int bw = bx.qx1 - bx.qx0, area = bw * (bx.y1 - bx.y0);
   const size_t plane = (size_t)g.S * g.S;
   const NoiseSrc nz = noise_src(nullptr, g, b);
+  // pre-augmented values (g.pre) or mp + the draws + the keyed noise at each corner
+  const float cb = g.pre ? 1.f : contrast[b], bb = g.pre ? 0.f : bright[b];
   for (int p = blockIdx.x * 256 + threadIdx.x; p < area; p += gridDim.x * 256) {
     const int r = p / bw;
     const int i = bx.y0 + r, j = bx.qx0 + (p - r * bw);
     const size_t o = (size_t)b * 3 * plane + (size_t)i * g.S + j;
     float adv[3], msk;
     bool rng[3];
-    const bool hit = warp_pixel(affine + 6 * b, g, nullptr, nz, 1.f, 0.f, i, j, adv, msk, rng);
+    const bool hit = warp_pixel(affine + 6 * b, g, mp, nz, cb, bb, i, j, adv, msk, rng);
 #pragma unroll
     for (int ch = 0; ch < 3; ++ch) {
       float v = hit ? adv[ch] * msk : 0.f;                       // load_data.py:791-792
@@ -915,7 +916,9 @@ __global__ __launch_bounds__(256) void warp_box_fwd_k(const float* __restrict__ 
 // phase A of the backward over the footprint box only (phase B reads gfac at
 // footprint pixels only)
 __global__ __launch_bounds__(256) void warp_box_bwd_a_k(const float* __restrict__ d_out,
+                                                        const float* __restrict__ mp,
                                                         const float* __restrict__ contrast,
+                                                        const float* __restrict__ bright,
                                                         const double* __restrict__ affine,
                                                         const int32_t* __restrict__ roi, WarpGeom g, int mode,
                                                         float* __restrict__ gfac) {
@@ -924,14 +927,14 @@ __global__ __launch_bounds__(256) void warp_box_bwd_a_k(const float* __restrict_
   const int bw = bx.qx1 - bx.qx0, area = bw * (bx.y1 - bx.y0);
   const size_t plane = (size_t)g.S * g.S;
   const NoiseSrc nz = noise_src(nullptr, g, b);
-  const float cb = contrast[b];
+  const float cb = contrast[b], bb = g.pre ? 0.f : bright[b];
   for (int p = blockIdx.x * 256 + threadIdx.x; p < area; p += gridDim.x * 256) {
     const int r = p / bw;
     const int i = bx.y0 + r, j = bx.qx0 + (p - r * bw);
     const size_t o = (size_t)b * 3 * plane + (size_t)i * g.S + j;
     float adv[3], msk;
     bool rng[3];
-    if (!warp_pixel(affine + 6 * b, g, nullptr, nz, cb, 0.f, i, j, adv, msk, rng)) continue;
+    if (!warp_pixel(affine + 6 * b, g, mp, nz, cb, bb, i, j, adv, msk, rng)) continue;
 #pragma unroll
     for (int ch = 0; ch < 3; ++ch) {
       const float outv = adv[ch] * msk;
@@ -973,8 +976,29 @@ extern "C" int po_warp_fwd_pre(const float* img, const float* pre, const double*
   hipStream_t st = po::stream_of(s);
   hipLaunchKernelGGL(warp_quad_copy_k, dim3(po::ceil_div(S * (S / 4), 256), B), dim3(256), 0, st, img, roi, S, mode,
                      out);
-  hipLaunchKernelGGL(warp_box_fwd_k, dim3(box_blocks(S), B), dim3(256), 0, st, img, affine, roi, g, mode, out);
+  hipLaunchKernelGGL(warp_box_fwd_k, dim3(box_blocks(S), B), dim3(256), 0, st, img, nullptr, nullptr, nullptr, affine,
+                     roi, g, mode, out);
   return po::check_launch("po_warp_fwd_pre");
+}
+
+extern "C" int po_warp_box_fwd_keyed(const float* img, const float* patch_mp, uint64_t seed, uint64_t counter, int b0,
+                                     const float* contrast, const float* bright, const double* affine,
+                                     const int32_t* roi, int B, int S, int P, int mode, int fill, float* out,
+                                     po_stream_t s) {
+  PO_REQUIRE(patch_mp && contrast && bright && affine && roi && out, "po_warp_box_fwd_keyed: null pointer");
+  PO_REQUIRE(mode == 0 || (mode == 1 && img), "po_warp_box_fwd_keyed: mode must be 0 or 1 (1 needs img)");
+  PO_REQUIRE(B > 0 && S > 1 && P > 0 && P <= S && b0 >= 0 && S % 4 == 0,
+             "po_warp_box_fwd_keyed: bad shape B=%d S=%d P=%d (S %% 4 == 0)", B, S, P);
+  PO_REQUIRE(3LL * P * P < (1LL << 31) && (int64_t)B * 3 * S * S < (1LL << 40), "po_warp_box_fwd_keyed: too large");
+  PO_REQUIRE(!fill || ((uintptr_t)img | (uintptr_t)out) % 16 == 0, "po_warp_box_fwd_keyed: fill needs 16-byte alignment");
+  const WarpGeom g = make_geom(S, P, seed, counter, b0);
+  hipStream_t st = po::stream_of(s);
+  if (fill)
+    hipLaunchKernelGGL(warp_quad_copy_k, dim3(po::ceil_div(S * (S / 4), 256), B), dim3(256), 0, st, img, roi, S, mode,
+                       out);
+  hipLaunchKernelGGL(warp_box_fwd_k, dim3(box_blocks(S), B), dim3(256), 0, st, img, patch_mp, contrast, bright, affine,
+                     roi, g, mode, out);
+  return po::check_launch("po_warp_box_fwd_keyed");
 }
 
 extern "C" int po_warp_bwd_pre(const float* d_out, const float* pre, const float* contrast, const double* affine,
@@ -988,13 +1012,34 @@ extern "C" int po_warp_bwd_pre(const float* d_out, const float* pre, const float
   WarpGeom g = make_geom(S, P);
   g.pre = pre;
   hipStream_t st = po::stream_of(s);
-  hipLaunchKernelGGL(warp_box_bwd_a_k, dim3(box_blocks(S), B), dim3(256), 0, st, d_out, contrast, affine, roi, g, mode,
-                     work);
+  hipLaunchKernelGGL(warp_box_bwd_a_k, dim3(box_blocks(S), B), dim3(256), 0, st, d_out, nullptr, contrast, nullptr,
+                     affine, roi, g, mode, work);
   int rc = po::check_launch("po_warp_bwd_pre(a)");
   if (rc) return rc;
   hipLaunchKernelGGL(warp_bwd_b_k, dim3(po::ceil_div(P * P, WB_EL)), dim3(256), 0, st, work, pre, nullptr, contrast,
                      nullptr, affine, g, B, d_patch_mp);
   return po::check_launch("po_warp_bwd_pre(b)");
+}
+
+extern "C" int po_warp_box_bwd_keyed(const float* d_out, const float* patch_mp, uint64_t seed, uint64_t counter, int b0,
+                                     const float* contrast, const float* bright, const double* affine,
+                                     const int32_t* roi, int B, int S, int P, int mode, float* work, float* d_patch_mp,
+                                     po_stream_t s) {
+  PO_REQUIRE(d_out && patch_mp && contrast && bright && affine && roi && work && d_patch_mp,
+             "po_warp_box_bwd_keyed: null pointer");
+  PO_REQUIRE(mode == 0 || mode == 1, "po_warp_box_bwd_keyed: mode must be 0 or 1");
+  PO_REQUIRE(B > 0 && S > 1 && P > 0 && P <= S && b0 >= 0, "po_warp_box_bwd_keyed: bad shape");
+  PO_REQUIRE(3LL * P * P < (1LL << 31), "po_warp_box_bwd_keyed: patch too large");
+  PO_REQUIRE(work != d_out, "po_warp_box_bwd_keyed: work may not alias d_out");
+  const WarpGeom g = make_geom(S, P, seed, counter, b0);
+  hipStream_t st = po::stream_of(s);
+  hipLaunchKernelGGL(warp_box_bwd_a_k, dim3(box_blocks(S), B), dim3(256), 0, st, d_out, patch_mp, contrast, bright,
+                     affine, roi, g, mode, work);
+  int rc = po::check_launch("po_warp_box_bwd_keyed(a)");
+  if (rc) return rc;
+  hipLaunchKernelGGL(warp_bwd_b_k, dim3(po::ceil_div(P * P, WB_EL)), dim3(256), 0, st, work, patch_mp, nullptr,
+                     contrast, bright, affine, g, B, d_patch_mp);
+  return po::check_launch("po_warp_box_bwd_keyed(b)");
 }
 
 extern "C" int po_warp_composite_multi(const float* img, const float* patch_mp, const float* noise,

@@ -63,4 +63,23 @@ __device__ __forceinline__ void footprint_roi(const double af[6], int S, int P, 
   roi[3] = min(S, (int)ceil(ihi) + 3);
 }
 
+// The composite's written box of image b (po_warp_fwd_pre, po_warp_box_fwd_keyed):
+// the footprint box widened to whole 4-pixel quads, [qx0, qx1) x [y0, y1) (all
+// zero when empty).  Outside it the composite equals the image (mode 1), so a
+// consumer given both tensors (po_conv_first_fwd_cmp) reads the composite only
+// inside this box.
+struct QBox {
+  int qx0, qx1, y0, y1;
+};
+__device__ __forceinline__ QBox quad_box(const int32_t* roi, int b, int S) {
+  const int4 r = reinterpret_cast<const int4*>(roi)[b];
+  QBox q;
+  q.qx0 = r.x & ~3;
+  q.qx1 = min(S, (r.z + 3) & ~3);
+  q.y0 = r.y;
+  q.y1 = r.w;
+  if (q.qx1 <= q.qx0 || q.y1 <= q.y0) q.qx0 = q.qx1 = q.y0 = q.y1 = 0;
+  return q;
+}
+
 }  // namespace po

@@ -165,6 +165,7 @@ class NetPlan:
         self.net, self.B, self.H, self.W, self.device = net, B, H, W, device
         self.gen = 0
         self.conv_timer = None        # list: (start, end, desc, cones) of every po_conv launch (launch_macs)
+        self.first_timer = []         # (start, end, entry) of the first layer's forward while conv_timer is set
         self._cone_snap = None
         self.ws = None                # split-K workspace (shared by every launch; stream-ordered)
         blocks = net.blocks
@@ -244,6 +245,9 @@ class NetPlan:
         self.first_direct = (first["type"] == "convolutional" and net._conv_meta[0]["k"] == 3
                              and net._conv_meta[0]["cin"] == 3 and net._conv_meta[0]["cout"] <= 64)
         self.in_nhwc = None if self.first_direct else torch.zeros(B, H, W, 16, device=dev)
+        # the first layer can read the training step's sparse composite (the patch
+        # footprint boxes in one tensor, the frames in another: po_conv_first_*_cmp)
+        self.sparse_input = self.first_direct and H == W and H % 4 == 0 and self.cp[0] <= 32
         # first conv (stride 1) whose only consumer is a k=2 stride-2 max pool
         # (yolov3-tiny): one fused launch writes the pool output and its argmax
         # (with the LeakyReLU slope encoded); the conv output is never stored
@@ -1449,13 +1453,21 @@ class NetPlan:
             desc.workspace = None
 
     # ---------------- execution ----------------
-    def run_forward(self, x):
-        """x: [B,3,H,W] contiguous CUDA float32 (NCHW).  Returns NHWC head buffers."""
+    def run_forward(self, x, base=None, roi=None):
+        """x: [B,3,H,W] contiguous CUDA float32 (NCHW).  Returns NHWC head buffers.
+        ``base`` (with ``roi`` [B,4] int32): x is the sparse patch composite --
+        valid only inside each image's quad-widened footprint box of roi
+        (po_warp_box_fwd_keyed, fill = 0) -- and the input equals ``base``
+        elsewhere; the first layer reads the two (po_conv_first_*_cmp)."""
         self.gen += 1
         st = nat.stream()
         lib = self.lib
         self.amax.zero_()
         xp = nat.c_void_p(x.data_ptr())
+        if base is not None:
+            if not self.sparse_input or roi is None:
+                raise ValueError("NetPlan.run_forward: this plan's first layer cannot read a sparse composite")
+            cmp = (nat.c_void_p(base.data_ptr()), xp, nat.c_void_p(roi.data_ptr()))
         if not self.first_direct:
             nat.call("po_nchw_to_nhwc", xp, self.B, self.H, self.W, 3, 16, nat.c_void_p(self.in_nhwc.data_ptr()), st)
         side = self.side if self.tails else None
@@ -1463,7 +1475,10 @@ class NetPlan:
             if side is not None and k in self._side_f:
                 continue                                  # a head tail: launched on the side stream
             if name in ("po_conv_first_fwd", "po_conv_first_pool_fwd"):
-                args = (xp,) + args[1:]
+                if base is not None:
+                    name, args = name + "_cmp", cmp + args[1:]
+                else:
+                    args = (xp,) + args[1:]
             self._launch(lib, name, args, desc, st)
             if side is not None and k in self._trig_f:
                 # block b is done: its tail runs beside the rest of the network
@@ -1486,6 +1501,13 @@ class NetPlan:
             rc = lib.po_conv(*args, st)
             e1.record()
             timer.append((e0, e1, desc, self._cone_snap if desc.gbox else None))
+        elif timer is not None and name.startswith("po_conv_first_") and "dgrad" not in name:
+            # the first layer's forward (bench.py's HBM roofline of the frame read)
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            rc = getattr(lib, name)(*args, st)
+            e1.record()
+            self.first_timer.append((e0, e1, name))
         else:
             rc = getattr(lib, name)(*args, st)
         if rc:
@@ -1573,8 +1595,8 @@ def wino_transform(w, offs):
 
 class _DarknetFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, plan, nchw, roi=None):
-        heads = plan.run_forward(x.contiguous())
+    def forward(ctx, x, plan, nchw, roi=None, base=None):
+        heads = plan.run_forward(x.contiguous(), base, roi)
         ctx.plan, ctx.gen, ctx.nchw, ctx.roi = plan, plan.gen, nchw, roi
         if not nchw:
             return tuple(h.clone() if plan.net.clone_heads else h.detach() for h in heads)
@@ -1606,7 +1628,7 @@ class _DarknetFn(torch.autograd.Function):
             d_heads.append(g.contiguous())
         d_x = torch.empty(plan.B, 3, plan.H, plan.W, device=plan.device)
         plan.run_backward(d_heads, d_x, ctx.roi)
-        return d_x, None, None, None
+        return d_x, None, None, None, None
 
 
 class Darknet(nn.Module):
@@ -1843,7 +1865,7 @@ class Darknet(nn.Module):
         p = self.plan(x.size(0), x.size(2), x.size(3), x.device)
         return list(_DarknetFn.apply(x, p, True))
 
-    def forward_nhwc(self, x, input_roi=None, center=None):
+    def forward_nhwc(self, x, input_roi=None, center=None, base=None):
         """Training-path forward: returns (head buffers, plan).  Head buffers
         are NHWC [B, h, w, Cp] (Cp = padded channel stride, channel =
         anchor*(5+C) + field).
@@ -1853,10 +1875,19 @@ class Darknet(nn.Module):
         at the cells of these centres (train_patch.py:449-483); the plan then
         computes the blocks after the last full-map dependency on windows
         around them, and the heads come back as windows
-        (``plan.head_views()``)."""
+        (``plan.head_views()``).
+        ``base``: x is the sparse composite of PatchTransformer.
+        forward_composite(sparse=True) -- valid inside the quad-widened boxes
+        of input_roi only, ``base`` (the frames) elsewhere (NetPlan.run_forward)."""
         nat.ensure_device(x)
         windowed = center is not None and self.window_heads
         p = self.plan(x.size(0), x.size(2), x.size(3), x.device, windowed=windowed)
         if p.windowed:
             p.set_windows(center)
-        return list(_DarknetFn.apply(x, p, False, input_roi)), p
+        return list(_DarknetFn.apply(x, p, False, input_roi, base)), p
+
+    def sparse_input_ok(self, B, H, W, device, center=None):
+        """Whether forward_nhwc(x, roi, center, base=frames) can run (the plan's
+        first layer reads a sparse composite: po_conv_first_*_cmp)."""
+        windowed = center is not None and self.window_heads
+        return self.plan(B, H, W, device, windowed=windowed).sparse_input

@@ -168,39 +168,57 @@ def patch_params(lab_batch, img_size, P, draws, do_rotate=True, with_roi=False):
     return theta, center, tsize
 
 
+WARP_FORMS = ("box", "pre", "frame")
+
+
 class _Warp(torch.autograd.Function):
     """Augment + warp + clamp*mask (mode 0) or + composite onto img (mode 1)."""
 
     @staticmethod
-    def forward(ctx, mp, noise, contrast, bright, affine, img, S, mode, pre_aug=True, roi=None):
+    def forward(ctx, mp, noise, contrast, bright, affine, img, S, mode, form="box", roi=None, sparse=False):
         """``noise``: the [B,3,P,P] tensor, or a po_draws key (seed, counter,
-        b0) — the noise is then regenerated from the key and no noise tensor
-        exists: with ``pre_aug`` (default) po_augment_patch forms the
-        augmented patches [B,3,P,P] once (one Philox call per 4 elements) and
-        the warp gathers them (po_warp_*_pre); otherwise the warp kernels
-        regenerate the noise at every corner read (po_warp_*_keyed).  All
-        three forms give the same bits."""
+        b0) -- the noise is then regenerated from the key and no noise tensor
+        exists.  With a key and the footprint boxes ``roi``, ``form`` picks the
+        kernels: "box" (default) forms mp * contrast + bright + 0.1 * noise at
+        each bilinear corner of the box pixels (po_warp_box_*_keyed); "pre"
+        first writes the augmented patches [B,3,P,P] (po_augment_patch, one
+        Philox call per 4 elements) and gathers them (po_warp_*_pre); "frame"
+        runs the per-pixel kernels over whole frames (po_warp_*_keyed).  All
+        forms give the same bits.  ``sparse`` (form "box", mode 1): only the
+        quad-widened boxes of ``out`` are written -- the rest of the composite
+        is ``img``, and the consumer reads the two (po_conv_first_*_cmp)."""
         mp = mp.contiguous()
         B = affine.size(0)
         P = mp.size(-1)
         out = torch.empty(B, 3, S, S, device=mp.device)
         imgp = nat.ptr(img.contiguous() if img is not None else None)
-        ctx.pre = False
-        if isinstance(noise, tuple) and pre_aug and roi is not None:
+        ctx.form = "tensor"
+        keyed = isinstance(noise, tuple)
+        if keyed and roi is not None and form == "box" and S % 4 == 0:
+            seed, counter, b0 = noise
+            nat.call("po_warp_box_fwd_keyed", imgp, nat.ptr(mp), int(seed) & 0xFFFFFFFFFFFFFFFF,
+                     int(counter) & 0xFFFFFFFFFFFFFFFF, int(b0), nat.ptr(contrast), nat.ptr(bright),
+                     nat.ptr(affine, torch.float64), nat.ptr(roi, torch.int32), B, S, P, mode,
+                     0 if (sparse and mode == 1) else 1, nat.ptr(out), nat.stream())
+            ctx.key, ctx.form = noise, "box"
+            ctx.save_for_backward(mp, contrast, bright, affine, roi)
+        elif sparse:
+            raise ValueError("_Warp: a sparse composite needs keyed noise, footprint boxes, form 'box' and S % 4 == 0")
+        elif keyed and roi is not None and form == "pre":
             seed, counter, b0 = noise
             pre = torch.empty(B, 3, P, P, device=mp.device)
             nat.call("po_augment_patch", nat.ptr(mp), int(seed) & 0xFFFFFFFFFFFFFFFF, int(counter) & 0xFFFFFFFFFFFFFFFF,
                      int(b0), nat.ptr(contrast), nat.ptr(bright), B, P, nat.ptr(pre), nat.stream())
             nat.call("po_warp_fwd_pre", imgp, nat.ptr(pre), nat.ptr(affine, torch.float64), nat.ptr(roi, torch.int32),
                      B, S, P, mode, nat.ptr(out), nat.stream())
-            ctx.key, ctx.pre = noise, True
+            ctx.key, ctx.form = noise, "pre"
             ctx.save_for_backward(mp, contrast, bright, affine, pre, roi)
-        elif isinstance(noise, tuple):
+        elif keyed:
             seed, counter, b0 = noise
             nat.call("po_warp_fwd_keyed", imgp, nat.ptr(mp), int(seed) & 0xFFFFFFFFFFFFFFFF,
                      int(counter) & 0xFFFFFFFFFFFFFFFF, int(b0), nat.ptr(contrast), nat.ptr(bright),
                      nat.ptr(affine, torch.float64), B, S, P, mode, nat.ptr(out), nat.stream())
-            ctx.key = noise
+            ctx.key, ctx.form = noise, "frame"
             ctx.save_for_backward(mp, contrast, bright, affine)
         else:
             nat.call("po_warp_fwd", imgp, nat.ptr(mp), nat.ptr(noise), nat.ptr(contrast), nat.ptr(bright),
@@ -217,14 +235,18 @@ class _Warp(torch.autograd.Function):
         work = torch.empty_like(d_out)
         d_mp = torch.empty_like(mp)
         B, P = affine.size(0), mp.size(-1)
-        if ctx.pre:
+        key = tuple(int(v) & 0xFFFFFFFFFFFFFFFF for v in ctx.key[:2]) + (int(ctx.key[2]),) if ctx.key else None
+        if ctx.form == "box":
+            roi = ctx.saved_tensors[4]
+            nat.call("po_warp_box_bwd_keyed", nat.ptr(d_out), nat.ptr(mp), *key, nat.ptr(contrast), nat.ptr(bright),
+                     nat.ptr(affine, torch.float64), nat.ptr(roi, torch.int32), B, ctx.S, P, ctx.mode, nat.ptr(work),
+                     nat.ptr(d_mp), nat.stream())
+        elif ctx.form == "pre":
             pre, roi = ctx.saved_tensors[4:6]
             nat.call("po_warp_bwd_pre", nat.ptr(d_out), nat.ptr(pre), nat.ptr(contrast), nat.ptr(affine, torch.float64),
                      nat.ptr(roi, torch.int32), B, ctx.S, P, ctx.mode, nat.ptr(work), nat.ptr(d_mp), nat.stream())
-        elif ctx.key is not None:
-            seed, counter, b0 = ctx.key
-            nat.call("po_warp_bwd_keyed", nat.ptr(d_out), nat.ptr(mp), int(seed) & 0xFFFFFFFFFFFFFFFF,
-                     int(counter) & 0xFFFFFFFFFFFFFFFF, int(b0), nat.ptr(contrast), nat.ptr(bright),
+        elif ctx.form == "frame":
+            nat.call("po_warp_bwd_keyed", nat.ptr(d_out), nat.ptr(mp), *key, nat.ptr(contrast), nat.ptr(bright),
                      nat.ptr(affine, torch.float64), B, ctx.S, P, ctx.mode, nat.ptr(work), nat.ptr(d_mp),
                      nat.stream())
         else:
@@ -232,7 +254,7 @@ class _Warp(torch.autograd.Function):
             nat.call("po_warp_bwd", nat.ptr(d_out), nat.ptr(mp), nat.ptr(noise), nat.ptr(contrast),
                      nat.ptr(bright), nat.ptr(affine, torch.float64), B, ctx.S, P, ctx.mode,
                      nat.ptr(work), nat.ptr(d_mp), nat.stream())
-        return d_mp, None, None, None, None, None, None, None, None, None
+        return d_mp, None, None, None, None, None, None, None, None, None, None
 
 
 class PatchTransformer(nn.Module):
@@ -258,9 +280,10 @@ class PatchTransformer(nn.Module):
         self.draw_step = 0
         self.draw_b0 = 0
         self.keyed_noise = os.environ.get("ADVPATCH_NOISE_KEYED", "1") != "0"
-        # keyed noise through the pre-augmented patches (po_augment_patch +
-        # po_warp_*_pre); ADVPATCH_WARP_PRE=0: regenerate it at every corner read
-        self.pre_aug = os.environ.get("ADVPATCH_WARP_PRE", "1") != "0"
+        # warp kernels for keyed noise (_Warp.forward): "box" (default), "pre", "frame"
+        self.warp_form = os.environ.get("ADVPATCH_WARP", "box")
+        if self.warp_form not in WARP_FORMS:
+            raise ValueError("ADVPATCH_WARP must be one of %s" % (WARP_FORMS,))
         self.last_roi = None     # [B,4] int32 footprint boxes of the last placement
 
     def lab_transform(self, lab_batch_origin):
@@ -307,18 +330,27 @@ class PatchTransformer(nn.Module):
         """-> (adv_batch_t [B,1,3,S,S], patch_center [B,2] = (x*S, y*S))."""
         mp, d, affine, center = self._prep(adv_patch, lab_batch, img_size, do_rotate, draws)
         out = _Warp.apply(mp, self._noise(d), d["contrast"].contiguous(),
-                          d["bright"].contiguous(), affine, None, int(img_size), 0, self.pre_aug, self.last_roi)
+                          d["bright"].contiguous(), affine, None, int(img_size), 0, self.warp_form, self.last_roi)
         return out.unsqueeze(1), center
 
-    def forward_composite(self, adv_patch, lab_batch, img_batch, img_size, do_rotate=True, draws=None):
+    def forward_composite(self, adv_patch, lab_batch, img_batch, img_size, do_rotate=True, draws=None,
+                          sparse=False):
         """Fused PatchTransformer + PatchApplier (the training step's path):
         -> (p_img_batch [B,3,S,S], patch_center [B,2]) without materialising
-        adv_batch_t."""
+        adv_batch_t.  ``sparse`` (keyed draws, form "box", S % 4 == 0): only
+        the quad-widened footprint boxes of p_img_batch (``last_roi``) are
+        written; the composite equals img_batch elsewhere, and Darknet.
+        forward_nhwc(p_img, roi, center, base=img_batch) reads it that way."""
         mp, d, affine, center = self._prep(adv_patch, lab_batch, img_size, do_rotate, draws)
         out = _Warp.apply(mp, self._noise(d), d["contrast"].contiguous(),
-                          d["bright"].contiguous(), affine, img_batch.contiguous(), int(img_size), 1, self.pre_aug,
-                          self.last_roi)
+                          d["bright"].contiguous(), affine, img_batch.contiguous(), int(img_size), 1, self.warp_form,
+                          self.last_roi, sparse)
         return out, center
+
+    def sparse_ok(self, img_size, draws=None):
+        """Whether forward_composite(..., sparse=True) is available."""
+        keyed = (draws is None and self.keyed_noise) or (draws is not None and "noise" not in draws)
+        return keyed and self.warp_form == "box" and int(img_size) % 4 == 0
 
 
 class _Apply(torch.autograd.Function):

@@ -339,15 +339,23 @@ class PatchTrainer(object):
         img_size = self.darknet_model.height
         if img_batch.size(0) == 0:
             return self._patch_terms_only(adv_patch, objective, weights)
+        net = self.darknet_model
+        B, S = img_batch.size(0), img_batch.size(-1)
+        # the composite is written only inside the patch footprints when the first
+        # layer can read it beside the frames (po_conv_first_*_cmp): no B*3*S*S copy
+        sparse = (img_batch.size(-2) == S == net.height == net.width and self.patch_transformer.sparse_ok(S, draws)
+                  and net.sparse_input_ok(B, S, S, img_batch.device, center=True)
+                  and os.environ.get("ADVPATCH_SPARSE_COMPOSITE", "1") != "0")
         p_img, center = self.patch_transformer.forward_composite(adv_patch, lab_batch, img_batch, img_size,
-                                                                 do_rotate=True, draws=draws)
+                                                                 do_rotate=True, draws=draws, sparse=sparse)
         roi = self.patch_transformer.last_roi
-        if p_img.size(-1) != self.darknet_model.width or p_img.size(-2) != self.darknet_model.height:
-            p_img = F.interpolate(p_img, (self.darknet_model.height, self.darknet_model.width))
+        if p_img.size(-1) != net.width or p_img.size(-2) != net.height:
+            p_img = F.interpolate(p_img, (net.height, net.width))
             roi = None
         # the warp backward reads dL/dp_img only inside the patch footprint:
         # the first conv's input gradient is computed there only
-        heads, plan = self.darknet_model.forward_nhwc(p_img, input_roi=roi, center=center)
+        heads, plan = net.forward_nhwc(p_img, input_roi=roi, center=center,
+                                       base=img_batch.contiguous() if sparse else None)
         self.last_plan = plan
         out2, obj, cls, cells, flags = cell_loss(heads, plan, img_size, center, TARGET_ID, objective,
                                                  flags=self.flags)
@@ -435,7 +443,7 @@ class PatchTrainer(object):
 
     # ------------------------------------------------------------------
     def train(self, max_n_epochs=401, save_dir="training_patches_saves/trained_patches", num_workers=10,
-              data=None, seed=0, cache_frames=None):
+              data=None, seed=0, cache_frames=None, save_state=False, resume=None):
         """Optimise a patch on the configured dataset (train_patch.py:85-389).
         ``config.batch_size`` is the GLOBAL batch, as in the reference; under
         torchrun every rank loads its contiguous shard of each global batch
@@ -443,13 +451,22 @@ class PatchTrainer(object):
         lab_batch) replacing the DataLoader (under torchrun: this rank's
         equal shards).  ``cache_frames``: decode the dataset once into device
         memory (FrameCache) instead of every epoch; None = when the uint8
-        frames take at most a quarter of the free device memory."""
+        frames take at most a quarter of the free device memory.
+        ``save_state``: beside every saved PNG also write ``<epoch>_state.pt``
+        (fp32 patch, Adam(amsgrad) moments, LR-scheduler state, epoch and step
+        counters; save_train_state).  ``resume``: such a file; training
+        continues at the epoch after it with the same patch, optimizer and
+        scheduler state, and since the loader order (seed + epoch) and the
+        transformer draws (global step) are keyed, not streamed, the resumed
+        run ends where the uninterrupted one does.  The reference resumes
+        only from a PNG (read_image, train_patch.py:119-121)."""
         img_size = self.darknet_model.height
         batch_size = self.config.batch_size
         max_lab = 252
         rank0 = self.rank == 0
         torch.manual_seed(seed)
         adv_patch = self.generate_patch("random").to(self.device).requires_grad_(True)
+        state = load_train_state(resume) if resume else None
         sampler = None
         if data is None:
             n_images = len(fnmatch.filter(os.listdir(self.config.img_dir), "*.png")) + \
@@ -475,8 +492,16 @@ class PatchTrainer(object):
         ep_loss_list = []
         keys = LOSS_KEYS
         step = 0
+        first_epoch = 0
+        if state is not None:
+            with torch.no_grad():
+                adv_patch.copy_(state["patch"])
+            optimizer.load_state_dict(state["optimizer"])
+            scheduler.load_state_dict(state["scheduler"])
+            first_epoch, step = int(state["epoch"]) + 1, int(state["step"])
+            ep_loss_list = [float(v) for v in state["ep_losses"]]
         self.patch_transformer.draw_seed = seed + 3
-        for epoch in range(max_n_epochs):
+        for epoch in range(first_epoch, max_n_epochs):
             if sampler is not None:
                 sampler.set_epoch(epoch)
             sums = {k: torch.zeros((), device=self.device) for k in keys}
@@ -517,6 +542,9 @@ class PatchTrainer(object):
             if epoch % 20 == 0 and save_dir and rank0:
                 path = os.path.join(save_dir, "%d_patch.png" % epoch)
                 save_patch_png(adv_patch.detach(), path)
+                if save_state:
+                    save_train_state(os.path.join(save_dir, "%d_state.pt" % epoch), adv_patch, optimizer, scheduler,
+                                     epoch, step, ep_loss_list)
                 if self.verbose:
                     print("saved patch dir : ", save_dir)
                 if epoch > 0 and self.verbose:
@@ -561,6 +589,35 @@ class PatchTrainer(object):
         t = no_cls_reshape[:, :, cls_ID]
         mx, _ = torch.max(no_cls_reshape, dim=2)
         return (mx - t).mean(1).sum()
+
+
+def _to_cpu(obj):
+    if torch.is_tensor(obj):
+        return obj.detach().cpu()
+    if isinstance(obj, dict):
+        return {k: _to_cpu(v) for k, v in obj.items()}
+    if isinstance(obj, (list, tuple)):
+        return type(obj)(_to_cpu(v) for v in obj)
+    return obj
+
+
+def save_train_state(path, adv_patch, optimizer, scheduler, epoch, step, ep_losses):
+    """Training state after ``epoch`` (SURVEY §5's optional fp32 checkpoint
+    beside the PNG): the exact fp32 patch (the PNG holds trunc(255*x)), Adam's
+    state_dict (step counters, exp_avg, exp_avg_sq, max_exp_avg_sq), the
+    scheduler's and the counters.  Tensors only, no pickled objects, so
+    load_train_state reads it with torch.load(weights_only=True)."""
+    os.makedirs(os.path.dirname(os.path.abspath(path)), exist_ok=True)
+    torch.save({"format": "advpatch-train-state-1", "patch": adv_patch.detach().float().cpu(),
+                "optimizer": _to_cpu(optimizer.state_dict()), "scheduler": _to_cpu(scheduler.state_dict()),
+                "epoch": int(epoch), "step": int(step), "ep_losses": [float(v) for v in ep_losses]}, path)
+
+
+def load_train_state(path):
+    st = torch.load(path, map_location="cpu", weights_only=True)
+    if not isinstance(st, dict) or st.get("format") != "advpatch-train-state-1":
+        raise ValueError("%s is not an advpatch training state (save_train_state)" % path)
+    return st
 
 
 def save_patch_png(patch, path):

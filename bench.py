@@ -141,7 +141,7 @@ def cpu_baseline(cfg, S, P, B=16, warmup=1, iters=3):
 
 
 WARP_ENTRIES = ("po_warp_fwd", "po_warp_bwd", "po_warp_fwd_keyed", "po_warp_bwd_keyed", "po_augment_patch",
-                "po_warp_fwd_pre", "po_warp_bwd_pre")
+                "po_warp_fwd_pre", "po_warp_bwd_pre", "po_warp_box_fwd_keyed", "po_warp_box_bwd_keyed")
 
 
 def measure(tr, prec, patch, img, lab, B, world, rank, steps, warmup, weights):
@@ -180,7 +180,7 @@ def measure(tr, prec, patch, img, lab, B, world, rank, steps, warmup, weights):
         t = torch.tensor([elapsed], device=img.device)
         torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
         elapsed = float(t)
-    plan.conv_timer = []
+    plan.conv_timer, plan.first_timer = [], []
     nat.TIMERS = {k: [] for k in WARP_ENTRIES}
     tr.ar_timer = [] if world > 1 else None
     torch.cuda.synchronize()
@@ -220,6 +220,15 @@ def measure(tr, prec, patch, img, lab, B, world, rank, steps, warmup, weights):
             for key in ("ms", "mfma_flops", "launches"):
                 tt[key] /= steps
     warp_ms = {k: sum(e0.elapsed_time(e1) for e0, e1 in v) / steps for k, v in warp.items()}
+    first = {}
+    for e0, e1, name in plan.first_timer:
+        first[name] = first.get(name, 0.0) + e0.elapsed_time(e1) / steps
+    plan.first_timer = []
+    # pixels of the quad-widened footprint boxes (the sparse composite's written
+    # region, po::quad_box) of the last step: the box warp kernels' unit count
+    roi = pt.last_roi.cpu().tolist() if pt.last_roi is not None else []
+    box_px = sum(max(0, y1 - y0) * max(0, min(img.size(-1), (x1 + 3) & ~3) - (x0 & ~3)) for x0, y0, x1, y1 in roi
+                 if min(img.size(-1), (x1 + 3) & ~3) > (x0 & ~3) and y1 > y0)
     dump = os.environ.get("ADVPATCH_LAUNCH_DUMP")
     if dump:
         # per-launch table (launch order of one step, averaged over the K steps)
@@ -237,7 +246,8 @@ def measure(tr, prec, patch, img, lab, B, world, rank, steps, warmup, weights):
     tr.check_flags()
     return {"elapsed": elapsed, "ms_per_step": elapsed * 1000.0 / steps, "value": world * B * steps / elapsed,
             "conv_ms": conv_ms, "conv_flops": conv_flops, "launches": len(timer) // steps, "families": fam,
-            "warp_ms": warp_ms, "instrumented_ms": instrumented_ms, "loss": float(terms["loss"].detach()),
+            "warp_ms": warp_ms, "first_ms": first, "box_px": box_px, "instrumented_ms": instrumented_ms,
+            "loss": float(terms["loss"].detach()),
             "allreduce_ms": allreduce_ms, "plan": plan}
 
 
@@ -302,30 +312,59 @@ def roofline(cfg_name, B, prec, m, ref_flops_step):
     return r
 
 
-def warp_roofline(m, B, S, P):
-    """HBM fractions of the fused augment/warp/composite kernels (SURVEY §8d
-    algorithmic bytes: forward reads the frame and writes the composite,
-    2*3*S^2*4 B per image, plus the 3*P^2*4 B patch once; backward reads
-    dL/dp_img, 3*S^2*4 B per image), per call, HIP events on the launch stream."""
+def warp_roofline(m, B, S, P, cp0=None):
+    """HBM fractions of the fused augment/warp/composite kernels, per call,
+    HIP events on the launch stream.  Algorithmic bytes: the
+    whole-frame forms (po_warp_*_pre, _keyed) read the frame and write the
+    composite, 2*3*S^2*4 B per image, plus the 3*P^2*4 B patch; their
+    backward reads dL/dp_img, 3*S^2*4 B per image.  The training step's box
+    form (po_warp_box_*_keyed on the sparse composite) touches only the
+    quad-widened footprint boxes: forward 3*4 B read (frame) + 3*4 B written
+    per box pixel plus the patch, backward 3*4 B of dL/dp_img read + 3*4 B of
+    gfac written and read again per box pixel plus the 3*P^2*4 B patch
+    gradient written; the frame itself is then read by the first layer
+    (po_conv_first_*_cmp: 3*S^2*4 B per image in, its NHWC output out),
+    reported as ``first_layer``."""
     out = {}
     wm = m["warp_ms"]
-    for base, per_img, extra in (("po_warp_fwd", 2 * 3 * S * S * 4, 3 * P * P * 4),
-                                 ("po_warp_bwd", 3 * S * S * 4, 0)):
-        # the entries the trainer ran: pre-augmented (the forward's time includes
-        # po_augment_patch), keyed, or the tensor-noise ones
-        if wm.get(base + "_pre"):
-            name = base + "_pre" + (" + po_augment_patch" if base == "po_warp_fwd" else "")
-            ms = wm[base + "_pre"] + (wm.get("po_augment_patch", 0.0) if base == "po_warp_fwd" else 0.0)
-        else:
-            name = base + "_keyed" if wm.get(base + "_keyed") else base
-            ms = wm.get(name)
+    box_px = m.get("box_px") or 0
+    if wm.get("po_warp_box_fwd_keyed"):
+        forms = (("po_warp_fwd", "po_warp_box_fwd_keyed", box_px * 24 + 3 * P * P * 4),
+                 ("po_warp_bwd", "po_warp_box_bwd_keyed", box_px * 36 + 3 * P * P * 4))
+    else:
+        forms = []
+        for base, per_img, extra in (("po_warp_fwd", 2 * 3 * S * S * 4, 3 * P * P * 4),
+                                     ("po_warp_bwd", 3 * S * S * 4, 0)):
+            if wm.get(base + "_pre"):
+                forms.append((base, base + "_pre", B * per_img + extra))
+            else:
+                forms.append((base, base + "_keyed" if wm.get(base + "_keyed") else base, B * per_img + extra))
+    for base, name, byts in forms:
+        ms = wm.get(name)
+        if name == "po_warp_fwd_pre" and ms:
+            ms += wm.get("po_augment_patch", 0.0)
+            name += " + po_augment_patch"
         if not ms:
             continue
-        byts = B * per_img + extra
         gbs = byts / (ms * 1e-3) / 1e9
-        out[base] = {"entries": name, "bound": "hbm", "algorithmic_bytes": byts, "us_per_call": ms * 1000.0,
-                     "achieved": gbs,
-                     "peak": PEAK_HBM_GBS, "unit": "GB/s", "frac": gbs / PEAK_HBM_GBS}
+        r = {"entries": name, "bound": "hbm", "algorithmic_bytes": byts, "us_per_call": ms * 1000.0,
+             "achieved": gbs, "peak": PEAK_HBM_GBS, "unit": "GB/s", "frac": gbs / PEAK_HBM_GBS}
+        if "box" in name:
+            r["box_pixels"] = box_px
+            r["note"] = ("sparse composite: only the footprint boxes (%.2f%% of the frames) are warped and written; "
+                         "the %d-byte frame copy of the whole-frame forms no longer exists (first_layer reads the "
+                         "frames)" % (100.0 * box_px / (B * S * S), 2 * 3 * S * S * 4 * B))
+        out[base] = r
+    first = m.get("first_ms") or {}
+    if first and cp0:
+        name, ms = max(first.items(), key=lambda kv: kv[1])
+        ho = S // 2 if "pool" in name else S        # the configs' first layers: stride 1 (+ fused 2x2 pool)
+        byts = B * 3 * S * S * 4 + B * ho * ho * cp0 * (5 if "pool" in name else 4)
+        gbs = byts / (ms * 1e-3) / 1e9
+        out["first_layer"] = {"entries": name, "bound": "hbm", "algorithmic_bytes": byts, "us_per_call": ms * 1000.0,
+                              "achieved": gbs, "peak": PEAK_HBM_GBS, "unit": "GB/s", "frac": gbs / PEAK_HBM_GBS,
+                              "bytes_are": "frames in (3*S^2*4 B per image) + NHWC output out (pool: floats + "
+                                           "argmax bytes)"}
     return out
 
 
@@ -368,7 +407,7 @@ def measure_tiny(args, dev):
             "config_tiny": {"workload": "%s S=%d P=%d batch=%d (BASELINE config 5)" % (cfg, S, P, B),
                             "global_batch": B, "image_size": S, "patch_size": P, "parallelism": "dp1",
                             "conv_precision": "fp32"},
-            "roofline_tiny": roofline("tiny", B, "fp32", m, ref), "warp_roofline_tiny": warp_roofline(m, B, S, P),
+            "roofline_tiny": roofline("tiny", B, "fp32", m, ref), "warp_roofline_tiny": warp_roofline(m, B, S, P, m["plan"].cp[0]),
             "loss_tiny": m["loss"]}
 
 
@@ -515,7 +554,7 @@ def main():
                        "global_batch": B * world, "per_gpu_batch": B, "image_size": S, "patch_size": P,
                        "parallelism": "dp%d" % world, "conv_precision": head},
             "roofline": roofline(args.config, B, head, m, ref_flops_step),
-            "warp_roofline": warp_roofline(m, B, S, P),
+            "warp_roofline": warp_roofline(m, B, S, P, m["plan"].cp[0]),
             "loss": m["loss"],
         }
         if world > 1:

@@ -33,7 +33,7 @@ typedef void* po_stream_t;
 #define PO_EHIP -2     /* HIP runtime error */
 #define PO_EDEVICE -3  /* device is not gfx950 */
 
-#define PO_ABI_VERSION 21
+#define PO_ABI_VERSION 22
 #define PO_AMAX_SUB 64  /* sub-slots per max|x| slot (see po_conv_desc) */
 
 int po_abi_version(void);
@@ -143,6 +143,24 @@ int po_warp_fwd_pre(const float* img, const float* pre, const double* affine, co
                     int P, int mode, float* out, po_stream_t s);
 int po_warp_bwd_pre(const float* d_out, const float* pre, const float* contrast, const double* affine,
                     const int32_t* roi, int B, int S, int P, int mode, float* work, float* d_patch_mp, po_stream_t s);
+/* The footprint-box warp with the keyed noise formed at each bilinear corner
+ * (mp * contrast + bright + 0.1 * Philox noise, as po_warp_*_keyed) instead of
+ * gathered from po_augment_patch's [B,3,P,P] buffer: no augment pass and no
+ * pre-augmented patches in HBM (a down-scaled patch is sampled at ~4 corners
+ * per footprint pixel, far fewer than its 3*P*P elements).  Same values and
+ * gradient as po_warp_*_pre / _keyed bit for bit.  fill = 1: `out` is the whole
+ * composite (outside the boxes 16-byte copies of img / zeros, as
+ * po_warp_fwd_pre); fill = 0: only the quad-widened boxes {x0 & ~3, y0,
+ * (x1 + 3) & ~3, y1} are written -- the training step's form, consumed by
+ * po_conv_first_fwd_cmp / po_conv_first_pool_fwd_cmp, which read img outside
+ * them (S % 4 == 0).  The backward gathers only images with a bilinear
+ * candidate per patch element. */
+int po_warp_box_fwd_keyed(const float* img, const float* patch_mp, uint64_t seed, uint64_t counter, int b0,
+                          const float* contrast, const float* bright, const double* affine, const int32_t* roi,
+                          int B, int S, int P, int mode, int fill, float* out, po_stream_t s);
+int po_warp_box_bwd_keyed(const float* d_out, const float* patch_mp, uint64_t seed, uint64_t counter, int b0,
+                          const float* contrast, const float* bright, const double* affine, const int32_t* roi,
+                          int B, int S, int P, int mode, float* work, float* d_patch_mp, po_stream_t s);
 
 /* PatchApplier for an explicit adv tensor: out = where(adv==0, img, adv)
  * (load_data.py:820); n elements. bwd: d_img = d_out*(adv==0), d_adv = d_out*(adv!=0). */
@@ -507,6 +525,18 @@ int po_conv_first_fwd(const float* img, int B, int H, int W, int stride, const f
  * consumer).  Cout_p 16 or 32. */
 int po_conv_first_pool_fwd(const float* img, int B, int H, int W, const float* Wt, const float* bias, int Cout,
                            int Cout_p, int act, float* y, int8_t* argmax, uint32_t* amax, po_stream_t s);
+/* The two first-layer forwards on the training step's sparse composite: the
+ * input is img except inside each image's quad-widened footprint box of roi
+ * (po_warp_box_fwd_keyed, fill = 0), where it is pimg.  A wave whose taps all
+ * miss the boxes runs the plain loads; results equal po_conv_first_fwd /
+ * _pool_fwd on the materialised composite bit for bit, without the B*3*S*S
+ * composite copy.  Square images; po_conv_first_fwd_cmp needs Cout_p <= 32. */
+int po_conv_first_fwd_cmp(const float* img, const float* pimg, const int32_t* roi, int B, int H, int W, int stride,
+                          const float* Wt, const float* bias, int Cout, int Cout_p, int act, float* y, uint32_t* amax,
+                          po_stream_t s);
+int po_conv_first_pool_fwd_cmp(const float* img, const float* pimg, const int32_t* roi, int B, int H, int W,
+                               const float* Wt, const float* bias, int Cout, int Cout_p, int act, float* y,
+                               int8_t* argmax, uint32_t* amax, po_stream_t s);
 /* Its input gradient: d_img[b,c,h,w] (NCHW) from D [B,Ho,Wo,Cout_p] (already
  * multiplied by leaky'), W [Cout][27].  roi (may be NULL) [B,4] int32
  * {x0,y0,x1,y1}: only pixels x0<=w<x1, y0<=h<y1 of image b are computed (the

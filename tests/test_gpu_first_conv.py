@@ -156,3 +156,92 @@ def test_first_pool_fused_matches_conv_then_pool(B, H, W, cout):
                  None, None, nat.stream())
         torch.cuda.synchronize()
         assert torch.equal(d_fus, d_ref)
+
+
+def _sparse_case(B, S, P, seed, big=False):
+    """(frames, full composite, sparse composite (NaN outside the boxes), roi)."""
+    ld, sy = pkg_mod("load_data"), pkg_mod("synthetic")
+    dev = torch.device("cuda", 0)
+    keyed = {k: v for k, v in sy.draws_device(seed, 2, 0, B, P, dev).items() if k != "noise"}
+    keyed["noise_key"] = (seed, 2, 0)
+    img = sy.frames(B, S, seed=seed).to(dev)
+    lab = sy.labels(B, seed=seed + 1)
+    if big:
+        lab[:, :, 3:5] = lab[:, :, 3:5].clamp(min=0.6)
+    lab = lab.to(dev)
+    patch = sy.patch(P, seed=seed + 2).to(dev)
+    pt = ld.PatchTransformer()
+    full, _ = pt.forward_composite(patch, lab, img, S, draws=keyed)
+    roi = pt.last_roi.clone()
+    sp, _ = pt.forward_composite(patch, lab, img, S, draws=keyed, sparse=True)
+    m = torch.zeros(B, 1, S, S, dtype=torch.bool)
+    for b, (x0, y0, x1, y1) in enumerate(roi.cpu().tolist()):
+        qx0, qx1 = x0 & ~3, min(S, (x1 + 3) & ~3)
+        if qx1 > qx0 and y1 > y0:
+            m[b, :, y0:y1, qx0:qx1] = True
+    sp = torch.where(m.to(dev), sp, torch.full_like(sp, float("nan")))      # outside the boxes: never read
+    return img, full.detach(), sp.detach(), roi
+
+
+@pytest.mark.parametrize("B,S,stride,cout,big", [(4, 608, 1, 32, False), (3, 416, 2, 16, False),
+                                                 (2, 96, 1, 32, True), (3, 64, 2, 32, True)])
+def test_first_fwd_on_sparse_composite_bit_identical(B, S, stride, cout, big):
+    """po_conv_first_fwd_cmp(frames, sparse composite, roi) equals
+    po_conv_first_fwd on the materialised composite bit for bit (waves whose
+    taps miss every box take the plain loads, the others read each tap from
+    the tensor that holds it; ``big``: boxes covering most of the frame)."""
+    nat = pkg_mod("_native")
+    dev = torch.device("cuda", 0)
+    img, full, sp, roi = _sparse_case(B, S, min(224, S // 2), seed=S + stride, big=big)
+    g = torch.Generator().manual_seed(7)
+    w = (torch.randn(cout, 27, generator=g) * 0.3).to(dev)
+    b = (torch.randn(cout, generator=g) * 0.1).to(dev)
+    cp = 16 if cout <= 16 else 32
+    for act in (0, 1):
+        want, m_want = _run(full, w, b, stride, cp, act)
+        Ho = (S - 1) // stride + 1
+        y = torch.full((B, Ho, Ho, cp), float("nan"), device=dev)
+        amax = torch.zeros(nat.PO_AMAX_SUB, dtype=torch.int32, device=dev)
+        nat.call("po_conv_first_fwd_cmp", nat.ptr(img), nat.ptr(sp), nat.ptr(roi, torch.int32), B, S, S, stride,
+                 nat.ptr(w), nat.ptr(b), cout, cp, act, nat.ptr(y), nat.ptr(amax, torch.int32), nat.stream())
+        torch.cuda.synchronize()
+        assert torch.equal(y, want)
+        assert amax.view(torch.float32).max().item() == m_want
+
+
+@pytest.mark.parametrize("B,S,cout,big", [(4, 416, 16, False), (2, 96, 16, True), (2, 64, 32, True)])
+def test_first_pool_on_sparse_composite_bit_identical(B, S, cout, big):
+    nat = pkg_mod("_native")
+    dev = torch.device("cuda", 0)
+    img, full, sp, roi = _sparse_case(B, S, min(224, S // 2), seed=S + 11, big=big)
+    g = torch.Generator().manual_seed(8)
+    w = (torch.randn(cout, 27, generator=g) * 0.3).to(dev)
+    b = (torch.randn(cout, generator=g) * 0.1).to(dev)
+    h = S // 2
+    outs = []
+    for name, pre in (("po_conv_first_pool_fwd", ()), ("po_conv_first_pool_fwd_cmp", None)):
+        y = torch.full((B, h, h, cout), float("nan"), device=dev)
+        am = torch.full((B, h, h, cout), -1, dtype=torch.int8, device=dev)
+        amax = torch.zeros(nat.PO_AMAX_SUB, dtype=torch.int32, device=dev)
+        head = (nat.ptr(full),) if pre == () else (nat.ptr(img), nat.ptr(sp), nat.ptr(roi, torch.int32))
+        nat.call(name, *head, B, S, S, nat.ptr(w), nat.ptr(b), cout, cout, 1, nat.ptr(y), nat.ptr(am),
+                 nat.ptr(amax, torch.int32), nat.stream())
+        torch.cuda.synchronize()
+        outs.append((y, am, amax))
+    for u, v in zip(outs[0], outs[1]):
+        assert torch.equal(u, v)
+
+
+def test_cmp_entries_refuse_bad_arguments():
+    nat = pkg_mod("_native")
+    dev = torch.device("cuda", 0)
+    img = torch.zeros(1, 3, 16, 16, device=dev)
+    roi = torch.zeros(1, 4, dtype=torch.int32, device=dev)
+    w = torch.zeros(64, 27, device=dev)
+    y = torch.zeros(1, 16, 16, 64, device=dev)
+    lib = nat.load()
+    assert lib.po_conv_first_fwd_cmp(nat.ptr(img), None, nat.ptr(roi, torch.int32), 1, 16, 16, 1, nat.ptr(w), None,
+                                     16, 16, 0, nat.ptr(y), None, nat.stream()) != 0
+    assert lib.po_conv_first_fwd_cmp(nat.ptr(img), nat.ptr(img), nat.ptr(roi, torch.int32), 1, 16, 16, 1, nat.ptr(w),
+                                     None, 64, 64, 0, nat.ptr(y), None, nat.stream()) != 0      # Cout_p 64
+    assert "Cout_p <= 32" in nat.last_error()

@@ -279,7 +279,8 @@ def test_warp_bwd_tight_scan_matches_oracle(S, P, B, big):
 def test_keyed_noise_warp_bit_identical(B, S, P, b0, big):
     """po_warp_fwd_keyed / po_warp_bwd_keyed regenerate po_draws' noise in the
     kernels, po_augment_patch + po_warp_*_pre form the augmented patches once
-    from the same key: the composite, the warp-only output and the patch
+    from the same key, po_warp_box_*_keyed form them at the corners of the box
+    pixels only (S % 4 == 0; else the frame kernels): the composite, the warp-only output and the patch
     gradient of both equal the tensor path fed po_draws' own noise tensor bit
     for bit (global image index b0 + b, odd S and P included; ``big``: magnified
     patches whose footprint boxes exceed the box kernels' one-pass grid)."""
@@ -296,9 +297,9 @@ def test_keyed_noise_warp_bit_identical(B, S, P, b0, big):
     patch = sy.patch(P, seed=5).to(DEV)
     outs = []
     g = torch.randn(B, 3, S, S, generator=torch.Generator().manual_seed(6)).to(DEV)
-    for dr, pre_aug in ((full, False), (keyed, False), (keyed, True)):
+    for dr, form in ((full, "frame"), (keyed, "frame"), (keyed, "pre"), (keyed, "box")):
         pt = ld.PatchTransformer()
-        pt.pre_aug = pre_aug
+        pt.warp_form = form
         pg = patch.clone().requires_grad_(True)
         comp, _ = pt.forward_composite(pg, lab, img, S, draws=dr)
         comp.backward(g)
@@ -317,3 +318,47 @@ def test_trainer_draws_are_keyed():
     pt = ld.PatchTransformer()
     d = pt.make_draws(4, 32, DEV)
     assert "noise" not in d and d["noise_key"] == (pt.draw_seed, 0, 0)
+
+
+def _quad_box_mask(roi, B, S):
+    """[B,1,S,S] bool: the quad-widened footprint boxes (po::quad_box)."""
+    m = torch.zeros(B, 1, S, S, dtype=torch.bool)
+    for b, (x0, y0, x1, y1) in enumerate(roi.cpu().tolist()):
+        qx0, qx1 = x0 & ~3, min(S, (x1 + 3) & ~3)
+        if qx1 > qx0 and y1 > y0:
+            m[b, :, y0:y1, qx0:qx1] = True
+    return m
+
+
+@pytest.mark.parametrize("B,S,P,big", [(6, 608, 224, False), (5, 416, 224, False), (3, 96, 32, True)])
+def test_sparse_composite_box_pixels_and_gradient(B, S, P, big):
+    """forward_composite(sparse=True) writes only the quad-widened footprint
+    boxes (po_warp_box_fwd_keyed, fill = 0): there the values equal the full
+    composite's, outside them the full composite equals the frames, and the
+    patch gradient is the full composite's, bit for bit."""
+    ld, sy = pkg_mod("load_data"), pkg_mod("synthetic")
+    seed, step, b0 = 0x1234, 4, 3
+    keyed = {k: v for k, v in sy.draws_device(seed, step, b0, B, P, DEV).items() if k != "noise"}
+    keyed["noise_key"] = (seed, step, b0)
+    img = sy.frames(B, S, seed=13).to(DEV)
+    lab = sy.labels(B, seed=14)
+    if big:
+        lab[:, :, 3:5] = lab[:, :, 3:5].clamp(min=0.6)
+    lab = lab.to(DEV)
+    patch = sy.patch(P, seed=15).to(DEV)
+    g = torch.randn(B, 3, S, S, generator=torch.Generator().manual_seed(16)).to(DEV)
+    outs = []
+    for sparse in (False, True):
+        pt = ld.PatchTransformer()
+        assert pt.warp_form == "box" and pt.sparse_ok(S, keyed)
+        pg = patch.clone().requires_grad_(True)
+        comp, _ = pt.forward_composite(pg, lab, img, S, draws=keyed, sparse=sparse)
+        comp.backward(g)
+        outs.append((comp.detach(), pg.grad.clone(), pt.last_roi.clone()))
+    (full, g_full, roi), (sp, g_sp, roi2) = outs
+    assert torch.equal(roi, roi2)
+    m = _quad_box_mask(roi, B, S).to(DEV).expand(B, 3, S, S)
+    assert torch.equal(full[m], sp[m])
+    assert torch.equal(full[~m], img[~m])
+    assert torch.equal(g_full, g_sp)
+    assert bool(m.any()) and bool((full[m] != img[m]).any())

@@ -364,3 +364,36 @@ def test_train_on_disk_loader_matches_data_iterable(tmp_path, yolo_weights, monk
     # compare the first epoch's loss and run the disk loaders against each other over both
     assert runs[0][1] == runs[1][1] and torch.equal(runs[0][0], runs[1][0])
     assert runs[0][1][0] == runs[2][1][0]
+
+
+def test_resume_from_train_state_matches_uninterrupted(tmp_path, yolo_weights, monkeypatch):
+    """train(save_state=True) writes <epoch>_state.pt beside the PNG; a new
+    trainer resumed from 0_state.pt for the second epoch ends at the patch,
+    Adam state and epoch losses of the uninterrupted two-epoch run, bit for
+    bit (loader order and transformer draws are keyed by epoch and global
+    step, so nothing streamed is lost across the restart)."""
+    from PIL import Image
+    monkeypatch.setenv("ADVPATCH_TUNE", "0")
+    tp = pkg_mod("train_patch")
+    img_dir, lab_dir = tmp_path / "images", tmp_path / "labels"
+    img_dir.mkdir()
+    lab_dir.mkdir()
+    rng = np.random.default_rng(5)
+    for k in range(9):
+        h, w = int(rng.integers(40, 90)), int(rng.integers(40, 90))
+        Image.fromarray(rng.integers(0, 256, (h, w, 3), dtype=np.uint8), "RGB").save(str(img_dir / ("f%d.png" % k)))
+        (lab_dir / ("f%d.txt" % k)).write_text("2 0.4 0.5 0.3 0.2\n" if k % 3 else "")
+
+    def run(save_dir, epochs, resume=None):
+        tr = _trainer("builtin:mini3", yolo_weights + ".mini3", batch=4)
+        tr.config.img_dir, tr.config.lab_dir = str(img_dir), str(lab_dir)
+        tr.config.patch_size = 32
+        return tr.train(max_n_epochs=epochs, data=None, save_dir=save_dir, num_workers=0, cache_frames=True,
+                        save_state=True, resume=resume)
+
+    full_patch, full_losses = run(str(tmp_path / "full"), 2)
+    st = tmp_path / "full" / "0_state.pt"
+    assert st.exists()
+    part_patch, part_losses = run(str(tmp_path / "part"), 2, resume=str(st))
+    assert part_losses == full_losses and len(full_losses) == 2
+    assert torch.equal(part_patch, full_patch)
