@@ -86,6 +86,7 @@ _SIGS = {
                      c_void_p],
     "po_cell_windows": [c_void_p, c_int, c_int, c_int, c_void_p, c_int, c_void_p, c_int, c_void_p, c_void_p,
                         c_void_p, c_void_p],
+    "po_support_boxes": [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_void_p],
     "po_grad_boxes": [c_void_p, c_int, c_int, c_void_p, c_int, c_int, c_void_p, c_void_p],
     "po_max_prob": [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p, c_void_p,
                     c_void_p],

@@ -577,3 +577,42 @@ extern "C" int po_grad_boxes(const int32_t* roi, int B, int S, const int32_t* pr
   hipLaunchKernelGGL(grad_boxes_k, dim3(B), dim3(64), lds, po::stream_of(s), roi, B, S, prog, nprog, nbox, boxes);
   return po::check_launch("po_grad_boxes");
 }
+
+namespace {
+// Support boxes of the compact dgrad grids (NetPlan._support / set_support_boxes):
+// per entry e and image i < nb, the window of block `win` at org[win][b0 + i]
+// dilated by the launch's taps, clipped to the H x W source map, intersected
+// with the source block's gradient cone when it has one, written as
+// {r0, c0, r1, c1} to the entry's box array dst[e][i].
+__global__ __launch_bounds__(64) void support_boxes_k(const int32_t* __restrict__ org, const int32_t* __restrict__ cones,
+                                                      const int32_t* __restrict__ prog,
+                                                      const unsigned long long* __restrict__ dst, int B) {
+  const int e = blockIdx.y;
+  const int i = blockIdx.x * 64 + threadIdx.x;
+  const int32_t* p = prog + 12 * e;
+  const int win = p[0], b0 = p[1], nb = p[2];
+  if (i >= nb) return;
+  const int dh1 = p[3], dh0 = p[4], dw1 = p[5], dw0 = p[6], H = p[7], W = p[8], w = p[9], cone = p[10];
+  const int b = b0 + i;
+  const int oy = org[((size_t)win * B + b) * 2], ox = org[((size_t)win * B + b) * 2 + 1];
+  int r0 = min(max(oy - dh1, 0), H), c0 = min(max(ox - dw1, 0), W);
+  int r1 = min(max(oy + w - dh0, 0), H), c1 = min(max(ox + w - dw0, 0), W);
+  if (cone >= 0) {
+    const int4 cb = reinterpret_cast<const int4*>(cones)[(size_t)cone * B + b];
+    r0 = max(r0, cb.x);
+    c0 = max(c0, cb.y);
+    r1 = min(r1, cb.z);
+    c1 = min(c1, cb.w);
+  }
+  reinterpret_cast<int4*>(dst[e])[i] = make_int4(r0, c0, r1, c1);
+}
+}  // namespace
+
+extern "C" int po_support_boxes(const int32_t* org, const int32_t* cones, const int32_t* prog,
+                                const unsigned long long* dst, int E, int B, po_stream_t s) {
+  PO_REQUIRE(org && prog && dst, "po_support_boxes: null pointer");
+  PO_REQUIRE(E >= 1 && B >= 1, "po_support_boxes: bad sizes E=%d B=%d", E, B);
+  hipLaunchKernelGGL(support_boxes_k, dim3(po::ceil_div(B, 64), E), dim3(64), 0, po::stream_of(s), org, cones, prog,
+                     dst, B);
+  return po::check_launch("po_support_boxes");
+}

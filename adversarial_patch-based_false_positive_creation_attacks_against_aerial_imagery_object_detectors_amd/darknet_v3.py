@@ -1280,7 +1280,27 @@ class NetPlan:
 
     def set_support_boxes(self):
         """Per-step support boxes of the compact dgrad grids (after set_cones):
-        the window dilated by the taps, clipped to the map, ∩ the cone box."""
+        the window dilated by the taps, clipped to the map, ∩ the cone box --
+        every entry in one po_support_boxes launch."""
+        if not self.support:
+            return
+        key = tuple(e[0].data_ptr() for e in self.support) + (self.cone_boxes is not None,)
+        if getattr(self, "_support_key", None) != key:          # (re)built with the op list
+            rows, ptrs = [], []
+            for box, j, src, b0, nb, (dh1, dh0, dw1, dw0), _ in self.support:
+                H, W = self.shp[src][:2]
+                cone = src if (self.cone_boxes is not None and src in self.cone_blocks) else -1
+                rows.append([self.win_idx[self.root[j]], b0, nb, dh1, dh0, dw1, dw0, H, W, self.win[j], cone, 0])
+                ptrs.append(box.data_ptr())
+            self._support_prog = torch.tensor(rows, dtype=torch.int32, device=self.device)
+            self._support_dst = torch.tensor(ptrs, dtype=torch.int64, device=self.device)
+            self._support_key = key
+        nat.call("po_support_boxes", nat.ptr(self.org, torch.int32), nat.ptr(self.cone_boxes, torch.int32),
+                 nat.ptr(self._support_prog, torch.int32), nat.ptr(self._support_dst, torch.int64),
+                 len(self.support), self.B, nat.stream())
+
+    def set_support_boxes_torch(self):
+        """The torch-op restatement of set_support_boxes (tests)."""
         for box, j, src, b0, nb, (dh1, dh0, dw1, dw0), _ in self.support:
             org = self.org_of(j)[b0:b0 + nb]
             H, W = self.shp[src][:2]
@@ -1462,12 +1482,24 @@ class NetPlan:
         self.gen += 1
         st = nat.stream()
         lib = self.lib
-        self.amax.zero_()
+        if self.prec == 1:
+            self.amax.zero_()                 # the fp16x3 max|x| slots (exact fp32 plans have none)
         xp = nat.c_void_p(x.data_ptr())
         if base is not None:
             if not self.sparse_input or roi is None:
                 raise ValueError("NetPlan.run_forward: this plan's first layer cannot read a sparse composite")
             cmp = (nat.c_void_p(base.data_ptr()), xp, nat.c_void_p(roi.data_ptr()))
+        self._cones_for = None
+        if roi is not None and self.cone_boxes is not None and os.environ.get("ADVPATCH_EARLY_CONES", "1") != "0":
+            # the gradient cones depend on the footprint boxes only: evaluate them
+            # (a serial walk of the block graph, one small workgroup per image)
+            # beside the forward instead of at the head of the backward
+            if getattr(self, "_cone_stream", None) is None:
+                self._cone_stream = torch.cuda.Stream(device=self.device)
+            self._cone_stream.wait_stream(torch.cuda.current_stream())
+            with torch.cuda.stream(self._cone_stream):
+                self.set_cones(roi)
+            self._cones_for = roi
         if not self.first_direct:
             nat.call("po_nchw_to_nhwc", xp, self.B, self.H, self.W, 3, 16, nat.c_void_p(self.in_nhwc.data_ptr()), st)
         side = self.side if self.tails else None
@@ -1530,7 +1562,11 @@ class NetPlan:
                      self.slot(self.grad[r]), st)
         dxp = nat.c_void_p(d_x.data_ptr())
         roip = nat.c_void_p(roi.data_ptr()) if roi is not None else None
-        self.set_cones(roi)
+        if roi is not None and getattr(self, "_cones_for", None) is roi:
+            torch.cuda.current_stream().wait_stream(self._cone_stream)     # evaluated beside the forward
+        else:
+            self.set_cones(roi)
+        self._cones_for = None
         self.set_support_boxes()
         if self.conv_timer is not None and self.cone_boxes is not None:
             self._cone_snap = self.cone_boxes.clone()        # this step's cones, for launch_macs

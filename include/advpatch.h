@@ -272,6 +272,16 @@ int po_cell_windows(const float* center, int B, int S, int nheads, const int* hw
  * cone is {0,0,0,0}.  Boxes of blocks no row writes are left untouched. */
 int po_grad_boxes(const int32_t* roi, int B, int S, const int32_t* prog, int nprog, int nbox, int32_t* boxes,
                   po_stream_t s);
+/* Support boxes of the windowed dgrad launches' compact grids, all entries in
+ * one launch.  org [nwin][B][2] window origins (po_cell_windows), cones
+ * [nblk][B][4] po_grad_boxes output (NULL when no entry uses a cone), prog
+ * [E][12] int32 rows {win, b0, nb, dh1, dh0, dw1, dw0, H, W, w, cone or -1, 0},
+ * dst [E] device addresses of the entries' int32 [nb][4] box arrays: box i =
+ * {clamp(oy - dh1), clamp(ox - dw1), clamp(oy + w - dh0), clamp(ox + w - dw0)}
+ * (rows to [0, H], columns to [0, W]; (oy, ox) = org[win][b0 + i]), then
+ * intersected with cones[cone][b0 + i]. */
+int po_support_boxes(const int32_t* org, const int32_t* cones, const int32_t* prog, const unsigned long long* dst,
+                     int E, int B, po_stream_t s);
 
 /* ---------------- patch evaluation (reference utils.py:93-245, 450-519) ---------------- */
 

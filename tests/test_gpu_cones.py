@@ -285,3 +285,32 @@ def test_conv_pool_fusion_leaves_the_step_unchanged(tmp_path, monkeypatch, prec)
     else:
         rel = float((g1 - g0).abs().max() / g0.abs().max())
         assert rel < 1e-5, rel
+
+
+@pytest.mark.parametrize("cfg,S,B", [("builtin:yolov3-dota", 608, 5), ("builtin:yolov3-tiny-dota", 416, 7)])
+def test_support_boxes_kernel_matches_torch_restatement(tmp_path, monkeypatch, cfg, S, B):
+    """po_support_boxes (every compact dgrad grid's boxes in one launch) equals
+    the torch-op restatement NetPlan.set_support_boxes_torch after a training
+    forward + backward (windows placed, cones evaluated)."""
+    from test_gpu_step import _trainer
+    sy = pkg_mod("synthetic")
+    P = 224
+    monkeypatch.setenv("ADVPATCH_TUNE", "0")
+    tr, _ = _trainer(cfg, tmp_path)
+    img, lab = sy.frames(B, S, seed=40).to(DEV), sy.labels(B, seed=41).to(DEV)
+    dr = {k: v.to(DEV) for k, v in sy.draws(B, P, seed=43).items()}
+    pg = sy.patch(P, seed=42).to(DEV).requires_grad_(True)
+    loss, _ = tr.losses(pg, img, lab, dr)
+    loss.backward()
+    plan = tr.last_plan
+    if not plan.support:
+        pytest.skip("no compact dgrad grid in this plan")
+    for box, *_ in plan.support:
+        box.fill_(-7)
+    plan.set_support_boxes()
+    got = [e[0].clone() for e in plan.support]
+    for box, *_ in plan.support:
+        box.fill_(-7)
+    plan.set_support_boxes_torch()
+    for g, (box, *_) in zip(got, plan.support):
+        assert torch.equal(g, box)

@@ -6,7 +6,7 @@ cd "$GRAFT_REPO_ROOT" || exit 1
 OUT=gpurun_out/r04h
 mkdir -p "$OUT"
 timeout -k 10 900 python -u -m pytest -x -v --timeout 600 --timeout-method thread \
-    tests/test_gpu_first_conv.py tests/test_gpu_patch_ops.py tests/test_gpu_train.py::test_resume_from_train_state_matches_uninterrupted \
+    tests/test_gpu_first_conv.py tests/test_gpu_patch_ops.py tests/test_gpu_train.py::test_resume_from_train_state_matches_uninterrupted tests/test_gpu_cones.py \
     > "$OUT/tests.log" 2>&1
 rc=$?
 grep -E "PASSED|FAILED|passed|failed|Error" "$OUT/tests.log" | tail -40
