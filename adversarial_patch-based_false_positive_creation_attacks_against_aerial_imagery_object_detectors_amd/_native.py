@@ -81,6 +81,7 @@ _SIGS = {
     "po_apply_bwd": [c_void_p, c_void_p, c_int64, c_void_p, c_void_p, c_void_p],
     "po_regularisers": [c_void_p, c_int, c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_void_p,
                         c_void_p],
+    "po_regularisers_grad": [c_void_p, c_int, c_void_p, c_int, c_void_p, c_void_p, c_int, c_void_p, c_void_p],
     "po_cell_loss": [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_int,
                      c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
                      c_void_p],

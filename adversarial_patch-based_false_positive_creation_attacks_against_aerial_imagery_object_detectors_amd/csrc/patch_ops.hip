@@ -1202,9 +1202,15 @@ __global__ __launch_bounds__(RB) void reg_final_k(const double* __restrict__ par
 
 __device__ __forceinline__ float sgnf(float x) { return x > 0.f ? 1.f : (x < 0.f ? -1.f : 0.f); }
 
+// g3 != NULL: the upstream gradients are read here (coef[0..2] formed as
+// reg_final_k forms them, from the statistics coef[3..7] of a forward
+// po_regularisers call), so the backward is this one launch; acc: d += the
+// gradient (one fp32 add of the complete value, as autograd sums two
+// gradient contributions to the patch)
 __global__ __launch_bounds__(RB) void reg_grad_k(const float* __restrict__ p, int P,
                                                  const float* __restrict__ col, int ncol,
                                                  const float* __restrict__ coef,
+                                                 const float* __restrict__ g3, int acc,
                                                  float* __restrict__ d) {
   const int n = P * P;
   const int e = blockIdx.x * RB + threadIdx.x;
@@ -1215,7 +1221,9 @@ __global__ __launch_bounds__(RB) void reg_grad_k(const float* __restrict__ p, in
   float dmin;
   int k;
   nps_pixel(col, ncol, r, g, b, dmin, k);
-  const float cn = coef[0], ct = coef[1], wc = coef[2];
+  const double numel = 3.0 * P * P;
+  const float cn = g3 ? g3[0] / (float)numel : coef[0], ct = g3 ? g3[1] / (float)numel : coef[1],
+              wc = g3 ? g3[2] : coef[2];
   const float rg = r - g, yb = 0.5f * (r + g) - b;
   const float drg = coef[5] * (rg - coef[3]) + coef[6];
   const float dyb = coef[5] * (yb - coef[4]) + coef[7];
@@ -1229,7 +1237,8 @@ __global__ __launch_bounds__(RB) void reg_grad_k(const float* __restrict__ p, in
     if (q > 0) tvs += sgnf(pc[e] - pc[e - 1] + 0.000001f);
     if (i + 1 < P) tvs -= sgnf(pc[e + P] - pc[e] + 0.000001f);
     if (i > 0) tvs += sgnf(pc[e] - pc[e - P] + 0.000001f);
-    d[e + ch * pp] = gn + ct * tvs + dcol[ch];
+    const float v = gn + ct * tvs + dcol[ch];
+    d[e + ch * pp] = acc ? d[e + ch * pp] + v : v;
   }
 }
 }  // namespace
@@ -1251,6 +1260,16 @@ extern "C" int po_regularisers(const float* patch, int P, const float* colors, i
   rc = po::check_launch("po_regularisers(final)");
   if (rc || !d_patch) return rc;
   hipLaunchKernelGGL(reg_grad_k, dim3(po::ceil_div(n, RB)), dim3(RB), 0, st, patch, P, colors, ncol,
-                     coef, d_patch);
+                     coef, nullptr, 0, d_patch);
   return po::check_launch("po_regularisers(grad)");
+}
+
+extern "C" int po_regularisers_grad(const float* patch, int P, const float* colors, int ncol, const float* g3,
+                                    const float* workspace, int accumulate, float* d_patch, po_stream_t s) {
+  PO_REQUIRE(patch && colors && g3 && workspace && d_patch, "po_regularisers_grad: null pointer");
+  PO_REQUIRE(P > 1 && ncol > 0, "po_regularisers_grad: bad shape");
+  const float* coef = workspace + 2 * NPART * RMAXB;      // the forward's statistics (coef[3..7])
+  hipLaunchKernelGGL(reg_grad_k, dim3(po::ceil_div(P * P, RB)), dim3(RB), 0, po::stream_of(s), patch, P, colors,
+                     ncol, coef, g3, accumulate ? 1 : 0, d_patch);
+  return po::check_launch("po_regularisers_grad");
 }

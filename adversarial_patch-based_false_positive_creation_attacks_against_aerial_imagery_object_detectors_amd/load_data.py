@@ -99,6 +99,55 @@ def regularisers(patch, colors):
     return _Regularisers.apply(patch, colors)
 
 
+class _PatchFront(torch.autograd.Function):
+    """The two functions of the raw patch a training step takes: its 7x7
+    'same' median pool (MedianPool2d(7, same=True), median_pool.py:46-52) and
+    its regularisers (NPS, TV, colour).  One autograd node: the backward runs
+    po_median7_bwd and adds the regularisers' gradient into the same buffer
+    (po_regularisers_grad, accumulate, from the forward's statistics) -- the
+    value autograd forms by summing the two contributions, bit for bit,
+    without the separate sum and the regularisers' recomputed reduction."""
+
+    @staticmethod
+    def forward(ctx, patch, colors):
+        nat.ensure_device(patch)
+        patch = patch.contiguous()
+        C, H, W = patch.shape
+        mp = torch.empty_like(patch)
+        arg = torch.empty(patch.shape, dtype=torch.int32, device=patch.device)
+        nat.call("po_median7_fwd", nat.ptr(patch), C, H, W, nat.ptr(mp), nat.ptr(arg, torch.int32), nat.stream())
+        out3 = torch.empty(3, device=patch.device)
+        ws = torch.empty(16384, device=patch.device)
+        nat.call("po_regularisers", nat.ptr(patch), W, nat.ptr(colors), colors.size(0), None, nat.ptr(out3), None,
+                 nat.ptr(ws), nat.stream())
+        ctx.save_for_backward(patch, colors, arg, ws)
+        ctx.set_materialize_grads(False)
+        return mp, out3
+
+    @staticmethod
+    def backward(ctx, d_mp, g3):
+        patch, colors, arg, ws = ctx.saved_tensors
+        if d_mp is None and g3 is None:
+            return None, None
+        C, H, W = patch.shape
+        d = torch.empty_like(patch)
+        if d_mp is not None:
+            nat.call("po_median7_bwd", nat.ptr(d_mp.contiguous()), nat.ptr(arg, torch.int32), C, H, W, nat.ptr(d),
+                     nat.stream())
+        if g3 is not None:
+            nat.call("po_regularisers_grad", nat.ptr(patch), W, nat.ptr(colors), colors.size(0),
+                     nat.ptr(g3.contiguous().float()), nat.ptr(ws), int(d_mp is not None), nat.ptr(d), nat.stream())
+        return d, None
+
+
+def patch_front(patch, colors):
+    """(median-pooled patch [3,P,P], regularisers [3]) of the raw patch
+    (PatchTransformer's median pool + NPS/TV/colour) in one autograd node."""
+    if patch.size(-1) != patch.size(-2):
+        raise ValueError("patch_front: square patches only")
+    return _PatchFront.apply(patch, colors)
+
+
 class NPSCalculator(nn.Module):
     """Non-printability score (load_data.py:340-389)."""
 
@@ -316,9 +365,11 @@ class PatchTransformer(nn.Module):
     def _noise(d):
         return d["noise"].contiguous() if "noise" in d else d["noise_key"]
 
-    def _prep(self, adv_patch, lab_batch, img_size, do_rotate, draws):
+    def _prep(self, adv_patch, lab_batch, img_size, do_rotate, draws, mp=None):
         nat.ensure_device(adv_patch)
-        mp = self.medianpooler(adv_patch.unsqueeze(0))[0]               # load_data.py:531-532
+        if mp is None:
+            # load_data.py:531-532 (squeeze: a view, so its backward is no kernel)
+            mp = self.medianpooler(adv_patch.unsqueeze(0)).squeeze(0)
         B, P = lab_batch.size(0), mp.size(-1)
         if draws is None:
             draws = self.make_draws(B, P, adv_patch.device)
@@ -334,14 +385,16 @@ class PatchTransformer(nn.Module):
         return out.unsqueeze(1), center
 
     def forward_composite(self, adv_patch, lab_batch, img_batch, img_size, do_rotate=True, draws=None,
-                          sparse=False):
+                          sparse=False, mp=None):
         """Fused PatchTransformer + PatchApplier (the training step's path):
         -> (p_img_batch [B,3,S,S], patch_center [B,2]) without materialising
         adv_batch_t.  ``sparse`` (keyed draws, form "box", S % 4 == 0): only
         the quad-widened footprint boxes of p_img_batch (``last_roi``) are
         written; the composite equals img_batch elsewhere, and Darknet.
-        forward_nhwc(p_img, roi, center, base=img_batch) reads it that way."""
-        mp, d, affine, center = self._prep(adv_patch, lab_batch, img_size, do_rotate, draws)
+        forward_nhwc(p_img, roi, center, base=img_batch) reads it that way.
+        ``mp``: the median-pooled patch when the caller already has it
+        (patch_front)."""
+        mp, d, affine, center = self._prep(adv_patch, lab_batch, img_size, do_rotate, draws, mp)
         out = _Warp.apply(mp, self._noise(d), d["contrast"].contiguous(),
                           d["bright"].contiguous(), affine, img_batch.contiguous(), int(img_size), 1, self.warp_form,
                           self.last_roi, sparse)

@@ -50,7 +50,7 @@ from . import synthetic
 from . import weights as synth_weights
 from .darknet_v3 import Darknet
 from .load_data import (DevicePrefetcher, DotaCollate, DotaDataset, FrameCache, HasSusRGB, NPSCalculator, PatchApplier,
-                        PatchTransformer, TotalVariation, read_image as _read_image, regularisers)
+                        PatchTransformer, TotalVariation, patch_front, read_image as _read_image, regularisers)
 
 TV_FACTOR = 2.5      # train_patch.py:25
 NPS_FACTOR = 0.01    # train_patch.py:26
@@ -92,6 +92,7 @@ class _CellLoss(torch.autograd.Function):
         ctx.save_for_backward(center, *heads)
         ctx.meta = (S, target, objective, tuple(hw), Cp, views)
         ctx.mark_non_differentiable(obj, cls, cells, flags)
+        ctx.set_materialize_grads(False)          # no zero tensors for the non-differentiable outputs
         return out2, obj, cls, cells, flags
 
     @staticmethod
@@ -195,6 +196,7 @@ class _LossCombine(torch.autograd.Function):
         ctx.save_for_backward(reg)
         ctx.meta = (w, weights is not None, with_cls)
         ctx.mark_non_differentiable(terms)
+        ctx.set_materialize_grads(False)
         return loss, terms
 
     @staticmethod
@@ -346,8 +348,10 @@ class PatchTrainer(object):
         sparse = (img_batch.size(-2) == S == net.height == net.width and self.patch_transformer.sparse_ok(S, draws)
                   and net.sparse_input_ok(B, S, S, img_batch.device, center=True)
                   and os.environ.get("ADVPATCH_SPARSE_COMPOSITE", "1") != "0")
+        # the median pool and the regularisers of the patch: one autograd node
+        mp, reg = patch_front(adv_patch, self.nps_calculator.colors)
         p_img, center = self.patch_transformer.forward_composite(adv_patch, lab_batch, img_batch, img_size,
-                                                                 do_rotate=True, draws=draws, sparse=sparse)
+                                                                 do_rotate=True, draws=draws, sparse=sparse, mp=mp)
         roi = self.patch_transformer.last_roi
         if p_img.size(-1) != net.width or p_img.size(-2) != net.height:
             p_img = F.interpolate(p_img, (net.height, net.width))
@@ -359,7 +363,6 @@ class PatchTrainer(object):
         self.last_plan = plan
         out2, obj, cls, cells, flags = cell_loss(heads, plan, img_size, center, TARGET_ID, objective,
                                                  flags=self.flags)
-        reg = regularisers(adv_patch, self.nps_calculator.colors)
         loss, terms = combine_terms_device(out2, reg, objective, weights)
         terms.update({"patch_center": center, "obj": obj, "cls": cls, "cells": cells, "flags": flags})
         return loss, terms

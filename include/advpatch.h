@@ -179,6 +179,13 @@ int po_apply_bwd(const float* d_out, const float* adv, int64_t n, float* d_img, 
 int po_regularisers(const float* patch, int P, const float* colors, int ncol, const float* g3,
                     float* out3, float* d_patch,
                     float* workspace /* >= 16384 floats */, po_stream_t s);
+/* Its gradient in one launch: d_patch = g3[0] dNPS/dp + g3[1] dTV/dp + g3[2]
+ * dCOL/dp from the statistics a po_regularisers call left in `workspace`
+ * (that call's patch and colours; any g3), the same values bit for bit as
+ * po_regularisers with d_patch.  accumulate = 1: d_patch += the gradient
+ * (one fp32 add of the complete value: autograd's sum of two contributions). */
+int po_regularisers_grad(const float* patch, int P, const float* colors, int ncol, const float* g3,
+                         const float* workspace, int accumulate, float* d_patch, po_stream_t s);
 
 /* Loss head (train_patch.py:428-548 + 230-253):
  * for each head h (map side hw_h, NHWC, Cp>=60, channel a*20+f), each image b:

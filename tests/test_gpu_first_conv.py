@@ -224,7 +224,7 @@ def test_first_pool_on_sparse_composite_bit_identical(B, S, cout, big):
         am = torch.full((B, h, h, cout), -1, dtype=torch.int8, device=dev)
         amax = torch.zeros(nat.PO_AMAX_SUB, dtype=torch.int32, device=dev)
         head = (nat.ptr(full),) if pre == () else (nat.ptr(img), nat.ptr(sp), nat.ptr(roi, torch.int32))
-        nat.call(name, *head, B, S, S, nat.ptr(w), nat.ptr(b), cout, cout, 1, nat.ptr(y), nat.ptr(am),
+        nat.call(name, *head, B, S, S, nat.ptr(w), nat.ptr(b), cout, cout, 1, nat.ptr(y), nat.ptr(am, torch.int8),
                  nat.ptr(amax, torch.int32), nat.stream())
         torch.cuda.synchronize()
         outs.append((y, am, amax))

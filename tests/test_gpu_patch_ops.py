@@ -362,3 +362,33 @@ def test_sparse_composite_box_pixels_and_gradient(B, S, P, big):
     assert torch.equal(full[~m], img[~m])
     assert torch.equal(g_full, g_sp)
     assert bool(m.any()) and bool((full[m] != img[m]).any())
+
+
+@pytest.mark.parametrize("P", [224, 37])
+def test_patch_front_matches_separate_nodes(P):
+    """patch_front (median pool + regularisers in one autograd node, the
+    regularisers' gradient added into the median pool's by
+    po_regularisers_grad) equals MedianPool2d(7, same) and regularisers() as
+    two nodes whose gradients autograd sums: outputs and patch gradient bit
+    for bit, also with only one of the two outputs used."""
+    ld, mpm, sy = pkg_mod("load_data"), pkg_mod("median_pool"), pkg_mod("synthetic")
+    patch = sy.patch(P, seed=21).to(DEV)
+    colors = ld.NPSCalculator(pkg_mod("patch_config").patch_configs["paper_obj"]().printfile, P).colors.to(DEV)
+    gen = torch.Generator().manual_seed(22)
+    g_mp = torch.randn(3, P, P, generator=gen).to(DEV)
+    g3 = torch.tensor([0.37, -1.25, 0.81]).to(DEV)
+    pool = mpm.MedianPool2d(7, same=True)
+    for use in ("both", "mp", "reg"):
+        a = patch.clone().requires_grad_(True)
+        mp_a, reg_a = ld.patch_front(a, colors)
+        b = patch.clone().requires_grad_(True)
+        mp_b, reg_b = pool(b.unsqueeze(0)).squeeze(0), ld.regularisers(b, colors)
+        assert torch.equal(mp_a, mp_b) and torch.equal(reg_a, reg_b)
+        la = (mp_a * g_mp).sum() if use != "reg" else 0
+        lb = (mp_b * g_mp).sum() if use != "reg" else 0
+        if use != "mp":
+            la = la + (reg_a * g3).sum()
+            lb = lb + (reg_b * g3).sum()
+        la.backward()
+        lb.backward()
+        assert torch.equal(a.grad, b.grad), use
