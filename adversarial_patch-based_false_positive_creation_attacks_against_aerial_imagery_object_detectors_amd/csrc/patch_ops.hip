@@ -71,20 +71,54 @@ __global__ __launch_bounds__(256) void median7_fwd_k(const float* __restrict__ x
   const int i = i0 + ty, j = j0 + tx;
   if (i >= H || j >= W) return;
   float v[49];
+  bool nan = false;
 #pragma unroll
-  for (int a = 0; a < 49; ++a) v[a] = tile[ty + a / 7][tx + a % 7];
-  // rank selection: the 25th smallest (index 24) of 49; first window
-  // position (row-major) holding the median value is the argument.
+  for (int a = 0; a < 49; ++a) {
+    v[a] = tile[ty + a / 7][tx + a % 7];
+    nan |= v[a] != v[a];
+  }
+  // the 25th smallest (index 24) of 49; the argument is the first window
+  // position (row-major) holding the median value.
   int found = 48;
+  if (!nan) {
+    // a bitonic sort of the 49 values padded to 64 with +inf (672 min/max
+    // pairs in registers) gives the value; the first position holding it is
+    // the rank-counting rule's argument (any position whose value equals the
+    // 25th smallest has < 25 smaller and >= 25 not-larger values; -0 and +0
+    // compare equal, as in the counting)
+    float srt[64];
 #pragma unroll
-  for (int a = 48; a >= 0; --a) {
-    int less = 0, leq = 0;
+    for (int a = 0; a < 64; ++a) srt[a] = a < 49 ? v[a] : INFINITY;
 #pragma unroll
-    for (int b = 0; b < 49; ++b) {
-      less += v[b] < v[a];
-      leq += v[b] <= v[a];
+    for (int k = 2; k <= 64; k <<= 1)
+#pragma unroll
+      for (int jj = k >> 1; jj > 0; jj >>= 1)
+#pragma unroll
+        for (int a = 0; a < 64; ++a) {
+          const int l = a ^ jj;
+          if (l > a) {
+            const float lo = fminf(srt[a], srt[l]), hi = fmaxf(srt[a], srt[l]);
+            const bool up = (a & k) == 0;
+            srt[a] = up ? lo : hi;
+            srt[l] = up ? hi : lo;
+          }
+        }
+    const float m24 = srt[24];
+#pragma unroll
+    for (int a = 48; a >= 0; --a)
+      if (v[a] == m24) found = a;
+  } else {
+    // rank selection by counting (NaN compares false, as in the reference's sort)
+#pragma unroll 1
+    for (int a = 48; a >= 0; --a) {
+      int less = 0, leq = 0;
+#pragma unroll
+      for (int b = 0; b < 49; ++b) {
+        less += v[b] < v[a];
+        leq += v[b] <= v[a];
+      }
+      if (less <= 24 && leq > 24) found = a;
     }
-    if (less <= 24 && leq > 24) found = a;
   }
   float med = v[0];
 #pragma unroll

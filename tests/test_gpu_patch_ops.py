@@ -392,3 +392,39 @@ def test_patch_front_matches_separate_nodes(P):
         la.backward()
         lb.backward()
         assert torch.equal(a.grad, b.grad), use
+
+
+@pytest.mark.parametrize("kind", ["uniform", "ties", "zeros", "nan"])
+def test_median7_network_matches_counting_kernel(kind):
+    """po_median7_fwd (bitonic network + first-position scan; the counting
+    rule only in windows holding a NaN) equals the general kernel
+    po_median_fwd (rank by counting) with the same 7x7 reflect-3 geometry,
+    values and arguments, on windows full of ties, of signed zeros and with
+    NaNs."""
+    nat = pkg_mod("_native")
+    gen = torch.Generator().manual_seed(31)
+    C, H, W = 3, 61, 45
+    x = torch.rand(C, H, W, generator=gen)
+    if kind == "ties":
+        x = (x * 4).floor() / 4
+    elif kind == "zeros":
+        x = torch.where(x < 0.5, torch.zeros_like(x), -torch.zeros_like(x))
+        x[0, 5, 5] = 1.0
+    elif kind == "nan":
+        x[x < 0.01] = float("nan")
+    x = x.to(DEV)
+    outs = []
+    for name in ("po_median7_fwd", "po_median_fwd"):
+        y = torch.full((C, H, W), 7.0, device=DEV)
+        arg = torch.full((C, H, W), -1, dtype=torch.int32, device=DEV)
+        if name == "po_median7_fwd":
+            nat.call(name, nat.ptr(x), C, H, W, nat.ptr(y), nat.ptr(arg, torch.int32), nat.stream())
+        else:
+            nat.call(name, nat.ptr(x), C, H, W, 7, 7, 1, 1, 3, 3, 3, 3, nat.ptr(y), nat.ptr(arg, torch.int32),
+                     nat.stream())
+        torch.cuda.synchronize()
+        outs.append((y, arg))
+    (y7, a7), (yg, ag) = outs
+    assert torch.equal(a7, ag)
+    assert torch.equal(y7.nan_to_num(5.0), yg.nan_to_num(5.0))
+    assert torch.equal(torch.signbit(y7), torch.signbit(yg))
