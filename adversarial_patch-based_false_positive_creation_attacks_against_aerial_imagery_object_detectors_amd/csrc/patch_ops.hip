@@ -429,31 +429,6 @@ __device__ __forceinline__ float aug_value(const float* __restrict__ mp, const N
   return fminf(fmaxf(v, 0.f), 1.f);                      // load_data.py:574
 }
 
-// aug_value with the keyed noise value already formed (noise_pair)
-__device__ __forceinline__ float aug_value_nz(const float* __restrict__ mp, float nzval, float contrast, float bright,
-                                              int ch, int pr, int pc, int P) {
-  const size_t o = ((size_t)ch * P + pr) * P + pc;
-  const float v = mp[o] * contrast + bright + nzval * 0.1f;                            // load_data.py:566-571
-  return fminf(fmaxf(v, 0.f), 1.f);                      // load_data.py:574
-}
-
-// Keyed noise of elements e and e + 1 (need0 / need1: which are wanted): one
-// Philox call when both lie in one group of 4, else one per element
-__device__ __forceinline__ void noise_pair(const NoiseSrc& ns, uint32_t e, bool need0, bool need1, float& n0,
-                                           float& n1) {
-  if (need0 && need1 && (e & 3u) != 3u) {
-    const po::u4 r = po::philox4x32_10(po::u4{e >> 2, ns.gb, ns.c_lo, ns.c_hi}, ns.k0, ns.k1);
-    const uint32_t l = e & 3u;
-    const uint32_t x0 = l == 0 ? r.x : (l == 1 ? r.y : r.z);
-    const uint32_t x1 = l == 0 ? r.y : (l == 1 ? r.z : r.w);
-    n0 = po::philox_affine(po::philox_unif(x0), 2.0f, -1.0f);
-    n1 = po::philox_affine(po::philox_unif(x1), 2.0f, -1.0f);
-  } else {
-    n0 = need0 ? ns.at(e) : 0.f;
-    n1 = need1 ? ns.at(e + 1) : 0.f;
-  }
-}
-
 // Forward of one output pixel: adv_t[3] (clamped) and msk_t.  Returns false
 // if no neighbour lies inside the padded patch region (output exactly 0).
 template <bool AUG = true>
@@ -472,33 +447,11 @@ __device__ __forceinline__ bool warp_pixel(const double* af, const WarpGeom& g, 
   const int cx[4] = {x0, x0 + 1, x0, x0 + 1};
   const int cy[4] = {y0, y0, y0 + 1, y0 + 1};
   float a0 = 0.f, a1 = 0.f, a2 = 0.f, m = 0.f;
-  // keyed noise: the two corners of a row are consecutive elements, usually of
-  // one Philox group, so a group's call serves both (the same values as one
-  // call per corner; the sums below keep their order)
-  float nzv[4][3];
-  const bool keyed = AUG && !nz.nz && !nz.pre;
-  if (keyed) {
-#pragma unroll
-    for (int rr = 0; rr < 2; ++rr) {
-      const int pr = cy[2 * rr] - g.padT, pc = cx[2 * rr] - g.padL;
-      const bool rin = pr >= 0 && pr < g.P;
-      const bool n0 = rin && pc >= 0 && pc < g.P, n1 = rin && pc + 1 >= 0 && pc + 1 < g.P;
-#pragma unroll
-      for (int ch = 0; ch < 3; ++ch) {
-        const uint32_t e = (uint32_t)(((ch * g.P) + pr) * g.P + pc);
-        noise_pair(nz, e, n0, n1, nzv[2 * rr][ch], nzv[2 * rr + 1][ch]);
-      }
-    }
-  }
 #pragma unroll
   for (int k = 0; k < 4; ++k) {
     const int pr = cy[k] - g.padT, pc = cx[k] - g.padL;
     if (pr >= 0 && pr < g.P && pc >= 0 && pc < g.P) {
-      if (keyed) {
-        a0 += aug_value_nz(mp, nzv[k][0], contrast, bright, 0, pr, pc, g.P) * w[k];
-        a1 += aug_value_nz(mp, nzv[k][1], contrast, bright, 1, pr, pc, g.P) * w[k];
-        a2 += aug_value_nz(mp, nzv[k][2], contrast, bright, 2, pr, pc, g.P) * w[k];
-      } else if (AUG) {
+      if (AUG) {
         a0 += aug_value(mp, nz, contrast, bright, 0, pr, pc, g.P) * w[k];
         a1 += aug_value(mp, nz, contrast, bright, 1, pr, pc, g.P) * w[k];
         a2 += aug_value(mp, nz, contrast, bright, 2, pr, pc, g.P) * w[k];
