@@ -635,7 +635,16 @@ __global__ __launch_bounds__(256) void warp_bwd_a4_k(const float* __restrict__ d
 // single pass that recomputes phase A at each candidate instead of reading
 // gfac measured 477 us against 165 + 159 us on tiny B=256: each footprint
 // pixel is the candidate of 4 corners, and warp_pixel's 24 gathers dominate.)
-constexpr int WB_EL = 32, WB_G = 8;
+// Per-image terms (the pixel-space map, its inverse, contrast, brightness)
+// are formed once per workgroup into LDS, WB_CH images at a time, instead of
+// once per (element, image) pair (the same double values, so the same bits).
+// 32 image groups x 8 elements per workgroup: 4x the threads of an
+// element-major split, to hide the candidates' dependent gfac loads.
+constexpr int WB_EL = 8, WB_G = 32, WB_CH = 256;
+struct WarpInv {
+  double a[6], m[4];
+  float cb, bb;
+};
 __global__ __launch_bounds__(256) void warp_bwd_b_k(const float* __restrict__ gfac,
                                                     const float* __restrict__ mp,
                                                     const float* __restrict__ noise,
@@ -644,6 +653,7 @@ __global__ __launch_bounds__(256) void warp_bwd_b_k(const float* __restrict__ gf
                                                     const double* __restrict__ affine, WarpGeom g,
                                                     int B, float* __restrict__ d_mp) {
   __shared__ float part[3][WB_G][WB_EL];
+  __shared__ WarpInv tab[WB_CH];
   const int el = threadIdx.x % WB_EL, q = threadIdx.x / WB_EL;
   const int e0 = blockIdx.x * WB_EL + el;
   const bool live = e0 < g.P * g.P;
@@ -652,77 +662,97 @@ __global__ __launch_bounds__(256) void warp_bwd_b_k(const float* __restrict__ gf
   const int r = pr + g.padT, c = pc + g.padL;
   const size_t plane = (size_t)g.S * g.S;
   float d0 = 0.f, d1 = 0.f, d2 = 0.f;
-  for (int b = q; b < (live ? B : 0); b += WB_G) {
-    const double* af = affine + 6 * b;
-    // output pixels whose sample point can have (r, c) as a bilinear corner:
-    // the preimage of (c-1, c+1) x (r-1, r+1) under the pixel-space affine
-    const double A00 = af[0], A01 = af[1], A02 = af[2], A10 = af[3], A11 = af[4], A12 = af[5];
-    const double det = A00 * A11 - A01 * A10;
-    const double inv = 1.0 / det;
-    const double m00 = A11 * inv, m01 = -A01 * inv, m10 = -A10 * inv, m11 = A00 * inv;
-    const double X = (double)c - A02, Y = (double)r - A12;
-    const double jc = m00 * X + m01 * Y, ic = m10 * X + m11 * Y;
-    const double hj = fabs(m00) + fabs(m01), hi_ = fabs(m10) + fabs(m11);
-    const double jlo = jc - hj, jhi = jc + hj, ilo = ic - hi_, ihi = ic + hi_;
-    if (!(jhi >= -1.0 && jlo <= (double)g.S && ihi >= -1.0 && ilo <= (double)g.S)) continue;
-    constexpr double eps = 1e-6;
-    const double hiS = (double)(g.S - 1);
-    const int j0 = (int)fmax(0.0, ceil(jlo - eps)), j1 = (int)fmin(hiS, floor(jhi + eps));
-    const int i0 = (int)fmax(0.0, ceil(ilo - eps)), i1 = (int)fmin(hiS, floor(ihi + eps));
-    const float cb = contrast[b], bb = g.pre ? 0.f : bright[b];
-    const NoiseSrc nz = noise_src(noise, g, b);
-    float a0 = 0.f, a1 = 0.f, a2 = 0.f;
-    bool cand = false;
-    const float* gb = gfac + (size_t)b * 3 * plane;
-    for (int i = i0; i <= i1; ++i)
-      for (int j = j0; j <= j1; ++j) {
-        double ix, iy;
-        sample_coord(af, i, j, ix, iy);
-        int x0, y0;
-        float wb[4];
-        bilinear(ix, iy, x0, y0, wb);
-        const int dx = c - x0, dy = r - y0;
-        if (dx < 0 || dx > 1 || dy < 0 || dy > 1) continue;
-        const float w = wb[2 * dy + dx];
-        const size_t o = (size_t)i * g.S + j;
-        const float gv[3] = {gb[o], gb[o + plane], gb[o + 2 * plane]};
-        a0 += w * gv[0];
-        a1 += w * gv[1];
-        a2 += w * gv[2];
-        cand = true;
-      }
-    // no output pixel of this image has (r, c) as a corner: its term is +0
-    // (a = +0, contrast > 0), and adding +0 never changes d (which starts at +0
-    // and so is never -0), so the image is skipped exactly -- and with it the
-    // pre-augmented value (keyed: a Philox call) the clamp test below needs
-    if (!cand) continue;
-    // through clamp(adv*contrast + bright + noise) and * contrast, summed over images
-    const float av[3] = {a0, a1, a2};
-    float dd[3];
+  for (int bc = 0; bc < B; bc += WB_CH) {
+    const int nb = min(WB_CH, B - bc);
+    if (bc) __syncthreads();                  // the previous chunk's readers are done
+    for (int t = threadIdx.x; t < nb; t += 256) {
+      const double* af = affine + 6 * (bc + t);
+      WarpInv w;
 #pragma unroll
-    for (int ch = 0; ch < 3; ++ch) {
-      const size_t po_ = ((size_t)ch * g.P + pr) * g.P + pc;
-      bool in;
-      if (nz.pre) {
-        const float pre = nz.pre[po_];
-        in = pre >= 0.f && pre <= 1.f;
-      } else {
-        // pre = fl(t + fl(0.1 nz)), t = fl(fl(mp cb) + bb), |fl(0.1 nz)| <= 0.1f
-        // (nz in [-1, 1)): rounding is monotonic, so pre lies in [fl(t - 0.1f),
-        // fl(t + 0.1f)], and when that interval is inside [0, 1] the clamp
-        // test passes whatever the noise -- its Philox call is skipped
-        const float t = mp[po_] * cb + bb;
-        if (t - 0.1f >= 0.f && t + 0.1f <= 1.f) {
-          in = true;
-        } else {
-          const float pre = t + nz.at(po_) * 0.1f;
-          in = pre >= 0.f && pre <= 1.f;
-        }
-      }
-      dd[ch] = in ? av[ch] * cb : 0.f;
+      for (int k = 0; k < 6; ++k) w.a[k] = af[k];
+      const double det = w.a[0] * w.a[4] - w.a[1] * w.a[3];
+      const double inv = 1.0 / det;
+      w.m[0] = w.a[4] * inv;
+      w.m[1] = -w.a[1] * inv;
+      w.m[2] = -w.a[3] * inv;
+      w.m[3] = w.a[0] * inv;
+      w.cb = contrast[bc + t];
+      w.bb = g.pre ? 0.f : bright[bc + t];
+      tab[t] = w;
     }
-    d0 += dd[0]; d1 += dd[1]; d2 += dd[2];
+    __syncthreads();
+    for (int bl = q; bl < (live ? nb : 0); bl += WB_G) {
+      const int b = bc + bl;
+      const double* af = tab[bl].a;
+      // output pixels whose sample point can have (r, c) as a bilinear corner:
+      // the preimage of (c-1, c+1) x (r-1, r+1) under the pixel-space affine
+      const double A02 = af[2], A12 = af[5];
+      const double m00 = tab[bl].m[0], m01 = tab[bl].m[1], m10 = tab[bl].m[2], m11 = tab[bl].m[3];
+      const double X = (double)c - A02, Y = (double)r - A12;
+      const double jc = m00 * X + m01 * Y, ic = m10 * X + m11 * Y;
+      const double hj = fabs(m00) + fabs(m01), hi_ = fabs(m10) + fabs(m11);
+      const double jlo = jc - hj, jhi = jc + hj, ilo = ic - hi_, ihi = ic + hi_;
+      if (!(jhi >= -1.0 && jlo <= (double)g.S && ihi >= -1.0 && ilo <= (double)g.S)) continue;
+      constexpr double eps = 1e-6;
+      const double hiS = (double)(g.S - 1);
+      const int j0 = (int)fmax(0.0, ceil(jlo - eps)), j1 = (int)fmin(hiS, floor(jhi + eps));
+      const int i0 = (int)fmax(0.0, ceil(ilo - eps)), i1 = (int)fmin(hiS, floor(ihi + eps));
+      const float cb = tab[bl].cb, bb = tab[bl].bb;
+      const NoiseSrc nz = noise_src(noise, g, b);
+      float a0 = 0.f, a1 = 0.f, a2 = 0.f;
+      bool cand = false;
+      const float* gb = gfac + (size_t)b * 3 * plane;
+      for (int i = i0; i <= i1; ++i)
+        for (int j = j0; j <= j1; ++j) {
+          double ix, iy;
+          sample_coord(af, i, j, ix, iy);
+          int x0, y0;
+          float wb[4];
+          bilinear(ix, iy, x0, y0, wb);
+          const int dx = c - x0, dy = r - y0;
+          if (dx < 0 || dx > 1 || dy < 0 || dy > 1) continue;
+          const float w = wb[2 * dy + dx];
+          const size_t o = (size_t)i * g.S + j;
+          const float gv[3] = {gb[o], gb[o + plane], gb[o + 2 * plane]};
+          a0 += w * gv[0];
+          a1 += w * gv[1];
+          a2 += w * gv[2];
+          cand = true;
+        }
+      // no output pixel of this image has (r, c) as a corner: its term is +0
+      // (a = +0, contrast > 0), and adding +0 never changes d (which starts at
+      // +0 and so is never -0), so the image is skipped exactly -- and with it
+      // the pre-augmented value (keyed: a Philox call) the clamp test needs
+      if (!cand) continue;
+      // through clamp(adv*contrast + bright + noise) and * contrast, summed over images
+      const float av[3] = {a0, a1, a2};
+      float dd[3];
+#pragma unroll
+      for (int ch = 0; ch < 3; ++ch) {
+        const size_t po_ = ((size_t)ch * g.P + pr) * g.P + pc;
+        bool in;
+        if (nz.pre) {
+          const float pre = nz.pre[po_];
+          in = pre >= 0.f && pre <= 1.f;
+        } else {
+          // pre = fl(t + fl(0.1 nz)), t = fl(fl(mp cb) + bb), |fl(0.1 nz)| <= 0.1f
+          // (nz in [-1, 1)): rounding is monotonic, so pre lies in [fl(t - 0.1f),
+          // fl(t + 0.1f)], and when that interval is inside [0, 1] the clamp
+          // test passes whatever the noise -- its Philox call is skipped
+          const float t = mp[po_] * cb + bb;
+          if (t - 0.1f >= 0.f && t + 0.1f <= 1.f) {
+            in = true;
+          } else {
+            const float pre = t + nz.at(po_) * 0.1f;
+            in = pre >= 0.f && pre <= 1.f;
+          }
+        }
+        dd[ch] = in ? av[ch] * cb : 0.f;
+      }
+      d0 += dd[0]; d1 += dd[1]; d2 += dd[2];
+    }
   }
+  __syncthreads();
   part[0][q][el] = d0;
   part[1][q][el] = d1;
   part[2][q][el] = d2;

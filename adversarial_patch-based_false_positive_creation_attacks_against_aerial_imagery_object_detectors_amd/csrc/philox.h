@@ -18,8 +18,11 @@ __device__ __forceinline__ u4 philox4x32_10(u4 c, uint32_t k0, uint32_t k1) {
   constexpr uint32_t M0 = 0xD2511F53u, M1 = 0xCD9E8D57u, W0 = 0x9E3779B9u, W1 = 0xBB67AE85u;
 #pragma unroll
   for (int r = 0; r < 10; ++r) {
-    const uint32_t lo0 = M0 * c.x, hi0 = __umulhi(M0, c.x);
-    const uint32_t lo1 = M1 * c.z, hi1 = __umulhi(M1, c.z);
+    // one 32x32 -> 64-bit product per word (v_mad_u64_u32) instead of a
+    // separate low and high multiply (both quarter-rate)
+    const uint64_t p0 = (uint64_t)M0 * c.x, p1 = (uint64_t)M1 * c.z;
+    const uint32_t lo0 = (uint32_t)p0, hi0 = (uint32_t)(p0 >> 32);
+    const uint32_t lo1 = (uint32_t)p1, hi1 = (uint32_t)(p1 >> 32);
     c = u4{hi1 ^ c.y ^ k0, lo1, hi0 ^ c.w ^ k1, lo0};
     k0 += W0;
     k1 += W1;
