@@ -639,12 +639,15 @@ __global__ __launch_bounds__(256) void warp_bwd_a4_k(const float* __restrict__ d
 // are formed once per workgroup into LDS, WB_CH images at a time, instead of
 // once per (element, image) pair (the same double values, so the same bits).
 // 32 image groups x 8 elements per workgroup: 4x the threads of an
-// element-major split, to hide the candidates' dependent gfac loads.
-constexpr int WB_EL = 8, WB_G = 32, WB_CH = 256;
+// element-major split, to hide the candidates' dependent gfac loads (batches
+// of more than 32 images; smaller ones keep 8 groups x 32 elements, whose
+// groups all hold images).
+constexpr int WB_CH = 256;
 struct WarpInv {
   double a[6], m[4];
   float cb, bb;
 };
+template <int WB_EL, int WB_G>
 __global__ __launch_bounds__(256) void warp_bwd_b_k(const float* __restrict__ gfac,
                                                     const float* __restrict__ mp,
                                                     const float* __restrict__ noise,
@@ -765,6 +768,16 @@ __global__ __launch_bounds__(256) void warp_bwd_b_k(const float* __restrict__ gf
   }
 }
 
+void launch_bwd_b(const float* gfac, const float* mp, const float* noise, const float* contrast, const float* bright,
+                  const double* affine, const WarpGeom& g, int B, int P, float* d_mp, hipStream_t st) {
+  if (B > 32)
+    hipLaunchKernelGGL((warp_bwd_b_k<8, 32>), dim3(po::ceil_div(P * P, 8)), dim3(256), 0, st, gfac, mp, noise,
+                       contrast, bright, affine, g, B, d_mp);
+  else
+    hipLaunchKernelGGL((warp_bwd_b_k<32, 8>), dim3(po::ceil_div(P * P, 32)), dim3(256), 0, st, gfac, mp, noise,
+                       contrast, bright, affine, g, B, d_mp);
+}
+
 // L patches per image composited in slot order (PatchApplier, load_data.py:
 // 808-833, over the [B,L,3,S,S] output of PatchTransformer_vanishing): per
 // element the value of the last slot whose clamp(adv)*msk is non-zero, else
@@ -875,9 +888,7 @@ int warp_bwd(const float* d_out, const float* patch_mp, const float* noise, cons
   }
   int rc = po::check_launch("po_warp_bwd(a)");
   if (rc) return rc;
-  dim3 gridb(po::ceil_div(P * P, WB_EL));
-  hipLaunchKernelGGL(warp_bwd_b_k, gridb, dim3(256), 0, po::stream_of(s), work, patch_mp, noise, contrast, bright,
-                     affine, g, B, d_patch_mp);
+  launch_bwd_b(work, patch_mp, noise, contrast, bright, affine, g, B, P, d_patch_mp, po::stream_of(s));
   return po::check_launch("po_warp_bwd(b)");
 }
 }  // namespace
@@ -1096,8 +1107,7 @@ extern "C" int po_warp_bwd_pre(const float* d_out, const float* pre, const float
                      affine, roi, g, mode, work);
   int rc = po::check_launch("po_warp_bwd_pre(a)");
   if (rc) return rc;
-  hipLaunchKernelGGL(warp_bwd_b_k, dim3(po::ceil_div(P * P, WB_EL)), dim3(256), 0, st, work, pre, nullptr, contrast,
-                     nullptr, affine, g, B, d_patch_mp);
+  launch_bwd_b(work, pre, nullptr, contrast, nullptr, affine, g, B, P, d_patch_mp, st);
   return po::check_launch("po_warp_bwd_pre(b)");
 }
 
@@ -1117,8 +1127,7 @@ extern "C" int po_warp_box_bwd_keyed(const float* d_out, const float* patch_mp, 
                      affine, roi, g, mode, work);
   int rc = po::check_launch("po_warp_box_bwd_keyed(a)");
   if (rc) return rc;
-  hipLaunchKernelGGL(warp_bwd_b_k, dim3(po::ceil_div(P * P, WB_EL)), dim3(256), 0, st, work, patch_mp, nullptr,
-                     contrast, bright, affine, g, B, d_patch_mp);
+  launch_bwd_b(work, patch_mp, nullptr, contrast, bright, affine, g, B, P, d_patch_mp, st);
   return po::check_launch("po_warp_box_bwd_keyed(b)");
 }
 
