@@ -553,7 +553,7 @@ class NetPlan:
         boxed launch (cones = the step's po_grad_boxes output) only its
         per-image boxes' grid points, counted as the kernels enumerate them."""
         if getattr(desc, "support", None) is not None:
-            bx = desc.support.cpu().tolist()
+            bx = desc.support.tolist()
             pts = sum(max(r1 - r0, 0) * max(c1 - c0, 0) for r0, c0, r1, c1 in bx)
             return desc.macs * pts / (desc.B * desc.mrows)
         if cones is None or not desc.gbox:
@@ -564,7 +564,7 @@ class NetPlan:
             b = 0 if hi - 1 - off < 0 else min(n, (hi - 1 - off) // step + 1)
             return max(b - a, 0)
 
-        bx = cones[desc.cone_block, desc.cone_b0:desc.cone_b0 + desc.B].cpu().tolist()
+        bx = cones[desc.cone_block, desc.cone_b0:desc.cone_b0 + desc.B].tolist()       # host or device tensor
         pts = sum(span(r0, r1, desc.out_oy, desc.out_step, desc.Hg) * span(c0, c1, desc.out_ox, desc.out_step, desc.Wg)
                   for r0, c0, r1, c1 in bx)
         return desc.macs * pts / (desc.B * desc.Hg * desc.Wg)

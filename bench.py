@@ -190,6 +190,9 @@ def measure(tr, prec, patch, img, lab, B, world, rank, steps, warmup, weights):
     torch.cuda.synchronize()
     instrumented_ms = (time.perf_counter() - t1) * 1000.0 / steps
     timer, plan.conv_timer = plan.conv_timer, None
+    # each step's cone snapshot to the host once (launch_macs reads per-image boxes)
+    snaps = {}
+    timer = [(e0, e1, d, None if c is None else snaps.setdefault(id(c), c.cpu())) for e0, e1, d, c in timer]
     warp, nat.TIMERS = nat.TIMERS, None
     ar, tr.ar_timer = tr.ar_timer, None
     # the fused [patch grad | 6 loss scalars] all-reduce, per step (this rank's view;
