@@ -342,12 +342,13 @@ __device__ __forceinline__ void conv_epilogue(const ConvArgs& a, const floatx16 
           }
           if (a.y) *reinterpret_cast<float4*>(a.y + o) = out;     // NULL: only signs/sum wanted
           nib = (out.x > 0.f ? 1u : 0u) | (out.y > 0.f ? 2u : 0u) | (out.z > 0.f ? 4u : 0u) | (out.w > 0.f ? 8u : 0u);
-          my = fmaxf(my, fmaxf(fmaxf(fabsf(out.x), fabsf(out.y)), fmaxf(fabsf(out.z), fabsf(out.w))));
+          if (a.y_amax)        // max|x| slots: fp16x3 plans only (no VALU spent on them otherwise)
+            my = fmaxf(my, fmaxf(fmaxf(fabsf(out.x), fabsf(out.y)), fmaxf(fabsf(out.z), fabsf(out.w))));
           if (a.res) {
             const float4 r = pres[q];
             const float4 sm = make_float4(x[0] + r.x, x[1] + r.y, x[2] + r.z, x[3] + r.w);
             *reinterpret_cast<float4*>(a.sum + o) = sm;
-            ms = fmaxf(ms, fmaxf(fmaxf(fabsf(sm.x), fabsf(sm.y)), fmaxf(fabsf(sm.z), fabsf(sm.w))));
+            if (a.sum_amax) ms = fmaxf(ms, fmaxf(fmaxf(fabsf(sm.x), fabsf(sm.y)), fmaxf(fabsf(sm.z), fabsf(sm.w))));
           }
           if (a.y2) {
             float4 g;
@@ -359,7 +360,7 @@ __device__ __forceinline__ void conv_epilogue(const ConvArgs& a, const floatx16 
             }
             const float4 o2 = make_float4(x[0] * g.x, x[1] * g.y, x[2] * g.z, x[3] * g.w);
             *reinterpret_cast<float4*>(a.y2 + o) = o2;
-            my2 = fmaxf(my2, fmaxf(fmaxf(fabsf(o2.x), fabsf(o2.y)), fmaxf(fabsf(o2.z), fabsf(o2.w))));
+            if (a.y2_amax) my2 = fmaxf(my2, fmaxf(fmaxf(fabsf(o2.x), fabsf(o2.y)), fmaxf(fabsf(o2.z), fabsf(o2.w))));
           }
         }
         if (a.ybits) {
