@@ -53,6 +53,13 @@ if os.environ.get("MICRO_POOL") == "1":                # fused 2x2/2 max pool: o
     pool = torch.empty(B, Ho // 2, Ho // 2, Cout, device=dev)
     pam = torch.empty(B, Ho // 2, Ho // 2, Cout, dtype=torch.int8, device=dev)
     d.pool_y, d.pool_argmax, yp = pool.data_ptr(), pam.data_ptr(), None
+box = None
+if os.environ.get("MICRO_BOX"):                       # gradient-cone boxes: a centred square of side frac * Ho per image
+    f = float(os.environ["MICRO_BOX"])
+    a0 = int(Ho * (1 - f) / 2)
+    a1 = a0 + int(Ho * f)
+    box = torch.tensor([[a0, a0, a1, a1]] * B, dtype=torch.int32, device=dev)
+    d.gbox = box.data_ptr()
 args = (ctypes.byref(d), nat.ptr(x), nat.ptr(w, w.dtype), nat.ptr(b), nat.ptr(yp), nat.ptr(res), nat.ptr(sm), None,
         None, None)
 st = nat.stream()
