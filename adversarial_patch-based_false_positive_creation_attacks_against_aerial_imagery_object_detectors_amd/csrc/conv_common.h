@@ -154,7 +154,7 @@ __device__ __forceinline__ int xcd_remap() {
 // Raw partial sums of one split-K slice (the reduction applies the epilogue)
 template <int TM, int TN>
 __device__ __forceinline__ void store_partials(const ConvArgs& a, const floatx16 (&acc)[TM][TN], int m0, int n0,
-                                               int wm, int wn, int lane, int m_end = 0x7fffffff) {
+                                               int wm, int wn, int lane) {
   float* ws = a.ws + (size_t)blockIdx.y * a.M * a.N;
 #pragma unroll
   for (int i = 0; i < TM; ++i)
@@ -165,7 +165,7 @@ __device__ __forceinline__ void store_partials(const ConvArgs& a, const floatx16
 #pragma unroll
       for (int e = 0; e < 16; ++e) {
         const int m = m0 + wm * TM * 32 + i * 32 + (e & 3) + 8 * (e >> 2) + 4 * (lane >> 5);
-        if (m < a.M && m < m_end) ws[(size_t)m * a.N + n] = acc[i][j][e];
+        if (m < a.M) ws[(size_t)m * a.N + n] = acc[i][j][e];
       }
     }
 }

@@ -19,7 +19,6 @@
 #include "conv_common.h"
 #include <stdlib.h>
 #include <string.h>
-#include <algorithm>
 
 namespace {
 using po::ConvArgs;
@@ -29,14 +28,7 @@ __device__ __forceinline__ void lds_dma16(__amdgpu_buffer_rsrc_t rs, float* lds,
   __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (__attribute__((address_space(3))) void*)lds, 16, voff, 0, 0, 0);
 }
 
-// WALK (boxed launches, a.gbox set, no fused pool): the grid is the chip's
-// resident workgroups, and each walks the launch's LIVE tiles -- per image
-// ceil(box points / BM) row tiles x the N tiles, images in order -- instead
-// of one workgroup per grid tile, most of which would hold only dead rows
-// past their image's box (dispatching such a workgroup costs ~1.4 ns; a
-// 304^2 boxed launch has ~11k of them).  Rows past the tile's image's box
-// compute nothing in either mode, so the outputs are the same bits.
-template <int BM, int BN, int WM, int BK, bool GL, bool WALK = false>
+template <int BM, int BN, int WM, int BK, bool GL>
 __global__ __launch_bounds__(256) void conv_k(const ConvArgs a) {
   constexpr int WN = 4 / WM;
   constexpr int TM = BM / WM / 32;
@@ -48,9 +40,13 @@ __global__ __launch_bounds__(256) void conv_k(const ConvArgs a) {
   constexpr int BL = (BN + RPP - 1) / RPP;     // B float4 loads per thread per k-step
   constexpr int SW = (BK == 16) ? 2 : 1;       // rows sharing a 256-byte bank line: 1 << SW
   __shared__ __attribute__((aligned(16))) float smem[2 * (BM + BN) * BK];
-  __shared__ int dst_pix[BM];
   float* As = smem;                            // [2][BM][BK]
   float* Bs = smem + 2 * BM * BK;              // [2][BN][BK]
+
+  const int wgid = po::xcd_remap();
+  const int tn = wgid % a.ntiles_n, tm = wgid / a.ntiles_n;
+  const int m0 = tm * BM, n0 = tn * BN;
+  if (!po::tile_live(a, m0, BM)) return;      // every row of the tile is outside its image's box
 
   const int tid = threadIdx.x & 255, lane = tid & 63, wave = tid >> 6;   // mask: lets the compiler bound rows
   const int wm = wave / WN, wn = wave % WN;
@@ -66,9 +62,6 @@ __global__ __launch_bounds__(256) void conv_k(const ConvArgs a) {
   constexpr uint32_t kOOB = 0x80000000u;
   const uint32_t pix_bytes = (uint32_t)a.Cin_p * 4u;
 
-  // one output tile: GEMM rows [m0, m0 + BM) (rows at or past m_end compute
-  // nothing), channels [n0, n0 + BN)
-  auto run_tile = [&](const int m0, const int n0, const int m_end) {
   // ---- A loader state.  Register staging (GL = false): thread (rth, cth)
   // loads chunk cth of rows rth + RPP*r.  LDS-DMA staging (GL = true): the
   // tile is cut into 1 KB pieces (RPI rows); lane L of the wave that owns
@@ -88,7 +81,7 @@ __global__ __launch_bounds__(256) void conv_k(const ConvArgs a) {
     const int row = a_row(r);
     const int m = m0 + row;
     int b = 0, i = 0, j = 0;
-    const bool ok = (row < BM) && m < m_end && po::grid_point(a, m, b, i, j);
+    const bool ok = (row < BM) && po::grid_point(a, m, b, i, j);
     if (!ok) b = 0;
     a_off[r] = ((uint32_t)b * a.Hin * a.Win) * pix_bytes + a_chunk(row) * 16u;
     // window buffers: shift from output-buffer to input-buffer coordinates
@@ -241,51 +234,11 @@ __global__ __launch_bounds__(256) void conv_k(const ConvArgs a) {
   }
 
   if (a.ksplit > 1) {
-    po::store_partials<TM, TN>(a, acc, m0, n0, wm, wn, lane, m_end);
+    po::store_partials<TM, TN>(a, acc, m0, n0, wm, wn, lane);
     return;
   }
-  if constexpr (WALK) {
-    if (tid < BM) {
-      int b, i, j;
-      const int m = m0 + tid;
-      dst_pix[tid] = (m < m_end && po::grid_point(a, m, b, i, j))
-                         ? (b * a.Hout + i * a.out_step + a.out_oy) * a.Wout + j * a.out_step + a.out_ox
-                         : -1;
-    }
-  }
-  po::conv_epilogue<BM, TM, TN>(a, acc, smem, dst_pix, m0, n0, wm, wn, 0, true, !WALK);
-  };   // run_tile
-
-  if constexpr (!WALK) {
-    const int wgid = po::xcd_remap();
-    const int tn = wgid % a.ntiles_n, tm = wgid / a.ntiles_n;
-    const int m0 = tm * BM;
-    if (!po::tile_live(a, m0, BM)) return;      // every row of the tile is outside its image's box
-    run_tile(m0, tn * BN, a.M);
-  } else {
-    // live tiles of image b: ceil(box points / BM) row tiles x ntiles_n
-    auto live_rows = [&](int b) {
-      const po::GridBox g = po::grid_box(a, b);
-      return min(g.h * g.w, a.mrows);
-    };
-    int cb = 0, cbase = 0, crows = live_rows(0);
-    int ccnt = (crows + BM - 1) / BM * a.ntiles_n;
-    for (int L = blockIdx.x;; L += gridDim.x) {
-      while (cb < a.B && L >= cbase + ccnt) {
-        cbase += ccnt;
-        if (++cb < a.B) {
-          crows = live_rows(cb);
-          ccnt = (crows + BM - 1) / BM * a.ntiles_n;
-        }
-      }
-      if (cb >= a.B) break;
-      const int r = L - cbase;
-      const int tm = r / a.ntiles_n, tn = r - tm * a.ntiles_n;
-      const int m0 = cb * a.mrows + tm * BM;
-      run_tile(m0, tn * BN, min(cb * a.mrows + crows, a.M));
-      __syncthreads();                          // smem and dst_pix are reused by the next tile
-    }
-  }
+  __shared__ int dst_pix[BM];
+  po::conv_epilogue<BM, TM, TN>(a, acc, smem, dst_pix, m0, n0, wm, wn, 0);
 }
 
 // Split-K reduction + epilogue: one thread per 8 output channels of a row.
@@ -390,15 +343,7 @@ int launch(const ConvArgs& a, hipStream_t st) {
   ConvArgs b = a;
   b.ntiles_n = po::ceil_div(a.N, BN);
   const int ntiles = po::ceil_div(a.M, BM) * b.ntiles_n;
-  if (a.gbox && !a.pool_y && !getenv("ADVPATCH_NO_WALK")) {
-    // boxed: the resident workgroups walk the live tiles (conv_k WALK)
-    static int res = 0;
-    if (!res) res = po::resident_groups(reinterpret_cast<const void*>(&conv_k<BM, BN, WM, BK, GL, true>), 256, 0);
-    const int grid = std::max(1, std::min(ntiles, res));
-    hipLaunchKernelGGL((conv_k<BM, BN, WM, BK, GL, true>), dim3(grid, a.ksplit), dim3(256), 0, st, b);
-  } else {
-    hipLaunchKernelGGL((conv_k<BM, BN, WM, BK, GL>), dim3(ntiles, a.ksplit), dim3(256), 0, st, b);
-  }
+  hipLaunchKernelGGL((conv_k<BM, BN, WM, BK, GL>), dim3(ntiles, a.ksplit), dim3(256), 0, st, b);
   if (a.ksplit > 1) {
     PO_REQUIRE((int64_t)a.M * a.N < (1LL << 31), "po_conv: split-K output too large");
     int rc = po::check_launch("po_conv");

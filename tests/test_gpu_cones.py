@@ -44,8 +44,7 @@ def _conv(nat, x, wt, shift, slot, bias, dst, box, prec, tile, ks, geo):
 @pytest.mark.parametrize("ks", [1, 3])
 @pytest.mark.parametrize("geo", [(21, 21, 21, 1, 0, 0), (11, 22, 11, 2, 1, 0)])
 def test_boxed_conv_matches_full_launch(prec, tile, ks, geo):
-    """Exact-fp32 boxed launches walk their live tiles (conv_k WALK: the
-    resident workgroups loop over each image's box tiles); image 1's box is
+    """Boxed launches of every tile family the plans use; image 1's box is
     the whole 21x21 map, whose 441 rows end inside a 128-row tile."""
     from test_gpu_darknet import _conv_operands
     nat = pkg_mod("_native")
@@ -319,37 +318,3 @@ def test_support_boxes_kernel_matches_torch_restatement(tmp_path, monkeypatch, c
     for g, (box, *_) in zip(got, plan.support):
         assert torch.equal(g, box)
 
-
-@pytest.mark.parametrize("tile", [1, 9, 11, 13, 19])
-@pytest.mark.parametrize("ks", [1, 4])
-def test_boxed_walk_bit_identical_to_grid_launch(tile, ks, monkeypatch):
-    """conv_k WALK (the default for boxed launches) against the one-workgroup-
-    per-tile grid (ADVPATCH_NO_WALK=1): the same bits everywhere the grid
-    writes, on boxes of every size, at B = 16 (more live tiles than resident
-    workgroups on some images, none on others)."""
-    from test_gpu_darknet import _conv_operands
-    nat = pkg_mod("_native")
-    B, Cin, Cout, H = 16, 64, 64, 38
-    geo = (H, H, H, 1, 0, 0)
-    gen = torch.Generator().manual_seed(9)
-    x = torch.randn(B, H, H, Cin, generator=gen)
-    w = torch.randn(Cout, 9, Cin, generator=gen) * (2.0 / (9 * Cin)) ** 0.5
-    bias = (torch.randn(Cout, generator=gen) * 0.1).to(DEV)
-    wt, shift, slot = _conv_operands(nat, w.to(DEV), x.permute(0, 3, 1, 2), 0)
-    xd = x.to(DEV)
-    rows = []
-    for b in range(B):
-        r0 = int(torch.randint(0, H, (1,), generator=gen))
-        c0 = int(torch.randint(0, H, (1,), generator=gen))
-        rows.append([r0, c0, min(H, r0 + int(torch.randint(0, H, (1,), generator=gen))),
-                     min(H, c0 + int(torch.randint(0, H, (1,), generator=gen)))])
-    rows[0], rows[1] = [0, 0, H, H], [5, 5, 5, 20]
-    boxes = torch.tensor(rows, dtype=torch.int32, device=DEV)
-    out = []
-    for walk in ("1", "0"):
-        if walk == "0":
-            monkeypatch.setenv("ADVPATCH_NO_WALK", "1")
-        y = torch.full((B, H, H, Cout), float("nan"), device=DEV)
-        _conv(nat, xd, wt, shift, slot, bias, y, boxes, 0, tile, ks, geo)
-        out.append(y.cpu())
-    assert torch.equal(out[0].nan_to_num(7.0), out[1].nan_to_num(7.0))
