@@ -177,3 +177,38 @@ def test_head_tails(cfg, H, want):
     plan = net.plan(1, H, H, torch.device("cpu"))
     assert plan.tail_chains() == want
     assert plan.tails == []                   # no second stream off the GPU
+
+
+def test_sparse_input_plan_flag_on_cpu_buffers():
+    """NetPlan.sparse_input: the first layer can read the step's sparse
+    composite (po_conv_first_*_cmp) -- a direct 3-channel first conv of at
+    most 32 padded channels on a square input whose side is a multiple of 4."""
+    W, dk = pkg_mod("weights"), pkg_mod("darknet_v3")
+    net = dk.Darknet("builtin:mini3")
+    import tempfile
+    with tempfile.TemporaryDirectory() as td:
+        p = os.path.join(td, "m.weights")
+        W.write_weights(p, W.synthesize("builtin:mini3"))
+        net.load_darknet_weights(p)
+    sq = net.plan(2, 64, 64, torch.device("cpu"))
+    assert sq.first_direct and sq.cp[0] <= 32 and sq.sparse_input
+    assert not net.plan(2, 64, 96, torch.device("cpu")).sparse_input          # not square
+
+
+def test_warp_form_selection_and_sparse_ok(monkeypatch):
+    """PatchTransformer.warp_form (ADVPATCH_WARP: box / pre / frame, anything
+    else refused) and sparse_ok: the sparse composite needs keyed noise, the
+    box form and a side that is a multiple of 4."""
+    ld = pkg_mod("load_data")
+    pt = ld.PatchTransformer()
+    assert pt.warp_form == "box" and pt.keyed_noise
+    assert pt.sparse_ok(608) and pt.sparse_ok(416) and not pt.sparse_ok(97)
+    assert not pt.sparse_ok(608, {"noise": torch.zeros(1)})                   # a noise tensor: not keyed
+    assert pt.sparse_ok(608, {"noise_key": (1, 2, 3)})
+    pt.warp_form = "pre"
+    assert not pt.sparse_ok(608)
+    monkeypatch.setenv("ADVPATCH_WARP", "frame")
+    assert ld.PatchTransformer().warp_form == "frame"
+    monkeypatch.setenv("ADVPATCH_WARP", "sideways")
+    with pytest.raises(ValueError):
+        ld.PatchTransformer()
