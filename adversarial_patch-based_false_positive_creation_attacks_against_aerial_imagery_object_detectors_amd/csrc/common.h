@@ -38,7 +38,11 @@ inline int resident_groups(const void* kernel, int block_threads, size_t dyn_lds
 // leaky'(y) for LeakyReLU(0.1): PyTorch leaky_relu_backward uses x > 0
 // (y and x share sign), slope 0.1 otherwise.
 __device__ __forceinline__ float leaky_grad(float y) { return y > 0.f ? 1.f : 0.1f; }
-__device__ __forceinline__ float leaky(float v) { return fmaxf(v, v * 0.1f); }   // = (v > 0 ? v : 0.1 v), NaN and signed zeros included
+// = (v > 0 ? v : 0.1 v), NaN and signed zeros included.  IEEE maximum (NaN-propagating,
+// v_maximum3_f32 on gfx950): the same value as fmaxf for these operands (both NaN or
+// neither, zeros of one sign) without the canonicalize fmaxf needs on a value the
+// compiler cannot prove canonical (one VALU per element in the epilogues)
+__device__ __forceinline__ float leaky(float v) { return __builtin_elementwise_maximum(v, v * 0.1f); }
 
 // torch.div(a, b, rounding_mode='floor') for float32 (ATen div_floor)
 __device__ __forceinline__ float div_floor(float a, float b) {
