@@ -43,6 +43,11 @@ __device__ __forceinline__ float leaky_grad(float y) { return y > 0.f ? 1.f : 0.
 // neither, zeros of one sign) without the canonicalize fmaxf needs on a value the
 // compiler cannot prove canonical (one VALU per element in the epilogues)
 __device__ __forceinline__ float leaky(float v) { return __builtin_elementwise_maximum(v, v * 0.1f); }
+// The activation of a conv epilogue without a branch on ConvArgs.act: slope 0.1
+// is leaky() exactly, slope 1 the identity (maximum(v, v * 1) = v, NaN, signed
+// zeros and infinities included) -- no per-element moves between the two paths.
+__device__ __forceinline__ float act_slope(int act) { return act ? 0.1f : 1.0f; }
+__device__ __forceinline__ float leaky_or_id(float v, float slope) { return __builtin_elementwise_maximum(v, v * slope); }
 
 // torch.div(a, b, rounding_mode='floor') for float32 (ATen div_floor)
 __device__ __forceinline__ float div_floor(float a, float b) {

@@ -225,7 +225,7 @@ __device__ __forceinline__ void conv_pool_epilogue(const ConvArgs& a, const floa
                           __builtin_ldexpf(vk.z, -sh) + bv.z, __builtin_ldexpf(vk.w, -sh) + bv.w};
 #pragma unroll
             for (int c = 0; c < 4; ++c) {
-              if (a.act) x[c] = leaky(x[c]);
+              x[c] = leaky_or_id(x[c], act_slope(a.act));
               if (k == 0 || x[c] > pv[c] || isnan(x[c])) { pv[c] = x[c]; arg[c] = (uint32_t)k; }
             }
           }
@@ -323,10 +323,8 @@ __device__ __forceinline__ void conv_epilogue(const ConvArgs& a, const floatx16 
           const uint32_t o = (uint32_t)pix * (uint32_t)a.Cout_p + n;
           float x[4] = {__builtin_ldexpf(v.x, -sh) + bv.x, __builtin_ldexpf(v.y, -sh) + bv.y,
                         __builtin_ldexpf(v.z, -sh) + bv.z, __builtin_ldexpf(v.w, -sh) + bv.w};
-          if (a.act) {
 #pragma unroll
-            for (int c = 0; c < 4; ++c) x[c] = leaky(x[c]);
-          }
+          for (int c = 0; c < 4; ++c) x[c] = leaky_or_id(x[c], act_slope(a.act));
           if (a.accumulate) {
             const float4 p = pold[q];
             x[0] += p.x; x[1] += p.y; x[2] += p.z; x[3] += p.w;

@@ -129,7 +129,7 @@ __global__ __launch_bounds__(256, PO_HALO_OCC) void conv_halo_pool_k(const ConvA
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
           float x = v[k] + bias_n;
-          if (a.act) x = po::leaky(x);
+          x = po::leaky_or_id(x, po::act_slope(a.act));
           if (k == 0 || x > pv || isnan(x)) { pv = x; arg = (uint32_t)k; }
         }
         if (a.act) arg |= 8u | (pv > 0.f ? 0u : 4u);

@@ -310,7 +310,7 @@ __global__ __launch_bounds__(256) void conv_reduce_k(const ConvArgs a) {
 #pragma unroll
       for (int c = 0; c < 4; ++c) {
         float x = __builtin_ldexpf(r[c], -sh) + bsv[c];
-        if (a.act) x = po::leaky(x);
+        x = po::leaky_or_id(x, po::act_slope(a.act));
         if (a.accumulate) x += yiv[c];
         const float yv = a.mbits ? x * g1v[c] : (a.mask ? x * po::leaky_grad(mkv[c]) : x);
         yo[c] = yv;

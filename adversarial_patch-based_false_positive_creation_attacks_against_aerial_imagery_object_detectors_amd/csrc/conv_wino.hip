@@ -52,7 +52,7 @@ __device__ __forceinline__ float epi_store(const ConvArgs& a, uint32_t pix, int 
   const uint32_t o = pix * (uint32_t)a.Cout_p + n;
   const uint32_t wo = pix * (uint32_t)(a.Cout_p >> 5) + (n >> 5);
   float x = v + (a.bias ? a.bias[n] : 0.f);
-  if (a.act) x = po::leaky(x);
+  x = po::leaky_or_id(x, po::act_slope(a.act));
   if (a.accumulate) x += a.y[o];
   float out = x;
   if (a.mbits) out = x * (((a.mbits[wo] >> (n & 31)) & 1u) ? 1.f : 0.1f);
@@ -88,7 +88,7 @@ __device__ __forceinline__ float epi_store_in(const ConvArgs& a, uint32_t pix, i
                                               const EpiIn& e, EpiMax& mx) {
   const uint32_t o = pix * (uint32_t)a.Cout_p + n;
   float x = v + bias_n;
-  if (a.act) x = po::leaky(x);
+  x = po::leaky_or_id(x, po::act_slope(a.act));
   if (a.accumulate) x += e.yold;
   float out = x;
   if (a.mbits) out = x * (((e.m >> (n & 31)) & 1u) ? 1.f : 0.1f);
@@ -120,10 +120,8 @@ __device__ __forceinline__ float4 epi_store4(const ConvArgs& a, uint32_t pix, in
                                              const EpiIn4& e, EpiMax& mx) {
   const uint32_t o = pix * (uint32_t)a.Cout_p + n;
   float x[4] = {v.x + bias_n.x, v.y + bias_n.y, v.z + bias_n.z, v.w + bias_n.w};
-  if (a.act) {
 #pragma unroll
-    for (int c = 0; c < 4; ++c) x[c] = po::leaky(x[c]);
-  }
+  for (int c = 0; c < 4; ++c) x[c] = po::leaky_or_id(x[c], po::act_slope(a.act));
   if (a.accumulate) { x[0] += e.yold.x; x[1] += e.yold.y; x[2] += e.yold.z; x[3] += e.yold.w; }
   float4 out = make_float4(x[0], x[1], x[2], x[3]);
   if (a.mbits) {
@@ -318,7 +316,7 @@ __global__ __launch_bounds__(256) void conv_wino_k(const ConvArgs a, const float
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
           float x = yv[k >> 1][k & 1] + (a.bias ? a.bias[n] : 0.f);
-          if (a.act) x = po::leaky(x);
+          x = po::leaky_or_id(x, po::act_slope(a.act));
           if (k == 0 || x > pv || isnan(x)) { pv = x; arg = (uint32_t)k; }
         }
         if (a.act) arg |= 8u | (pv > 0.f ? 0u : 4u);
@@ -1002,7 +1000,7 @@ __global__ __launch_bounds__(256, 2) void conv_wino3_k(const ConvArgs a, const f
           float x[4] = {v.x + bias4.x, v.y + bias4.y, v.z + bias4.z, v.w + bias4.w};
 #pragma unroll
           for (int c = 0; c < 4; ++c) {
-            if (a.act) x[c] = po::leaky(x[c]);
+            x[c] = po::leaky_or_id(x[c], po::act_slope(a.act));
             if (k == 0 || x[c] > pv[c] || isnan(x[c])) { pv[c] = x[c]; arg[c] = (uint32_t)k; }
           }
         }
@@ -1359,7 +1357,7 @@ __global__ __launch_bounds__(512, 1) void conv_wino4_k(const ConvArgs a, const f
           float x[4] = {v.x + bias4.x, v.y + bias4.y, v.z + bias4.z, v.w + bias4.w};
 #pragma unroll
           for (int c = 0; c < 4; ++c) {
-            if (a.act) x[c] = po::leaky(x[c]);
+            x[c] = po::leaky_or_id(x[c], po::act_slope(a.act));
             if (k == 0 || x[c] > pv[c] || isnan(x[c])) { pv[c] = x[c]; arg[c] = (uint32_t)k; }
           }
         }

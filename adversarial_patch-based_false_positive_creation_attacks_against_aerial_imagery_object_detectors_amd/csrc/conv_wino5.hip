@@ -211,7 +211,7 @@ __global__ __launch_bounds__(512, 1) void conv_wino5_k(const ConvArgs a, const f
           float x[4] = {v.x + bias4.x, v.y + bias4.y, v.z + bias4.z, v.w + bias4.w};
 #pragma unroll
           for (int c = 0; c < 4; ++c) {
-            if (a.act) x[c] = po::leaky(x[c]);
+            x[c] = po::leaky_or_id(x[c], po::act_slope(a.act));
             if (k == 0 || x[c] > pv[c] || isnan(x[c])) { pv[c] = x[c]; arg[c] = (uint32_t)k; }
           }
         }
@@ -233,10 +233,8 @@ __global__ __launch_bounds__(512, 1) void conv_wino5_k(const ConvArgs a, const f
           const uint32_t o = (pix * (uint32_t)a.Cout_p + vn4) * 4u;
           const float4 v = yv[ps][p >> 1][p & 1];
           float x[4] = {v.x + bias4.x, v.y + bias4.y, v.z + bias4.z, v.w + bias4.w};
-          if (a.act) {
 #pragma unroll
-            for (int c = 0; c < 4; ++c) x[c] = po::leaky(x[c]);
-          }
+          for (int c = 0; c < 4; ++c) x[c] = po::leaky_or_id(x[c], po::act_slope(a.act));
           if constexpr (ACC) {
             x[0] += pin[ps][p].x; x[1] += pin[ps][p].y; x[2] += pin[ps][p].z; x[3] += pin[ps][p].w;
           }
@@ -256,8 +254,9 @@ __global__ __launch_bounds__(512, 1) void conv_wino5_k(const ConvArgs a, const f
           }
           if constexpr ((EF & EF_YB) != 0) {
             // sign bits: 8 lanes hold the 32 channels of one word
-            const uint32_t nib = ok ? ((out.x > 0.f ? 1u : 0u) | (out.y > 0.f ? 2u : 0u) | (out.z > 0.f ? 4u : 0u) |
-                                       (out.w > 0.f ? 8u : 0u)) : 0u;
+            // (masked, not branched: a divergent branch here costs an exec save/restore per pixel)
+            const uint32_t nib = ((out.x > 0.f ? 1u : 0u) | (out.y > 0.f ? 2u : 0u) | (out.z > 0.f ? 4u : 0u) |
+                                  (out.w > 0.f ? 8u : 0u)) & (0u - (uint32_t)ok);
             // (OR of lanes i..i+7 into lane i by DPP row shifts, dst[i] = src[i + n] within
             // a 16-lane row: VALU-rate, where __shfl_xor's three dependent LDS crossbar
             // round trips per pixel were ~1 us of every unit's emit)
