@@ -53,6 +53,12 @@ struct ConvArgs {
   // n / d = (n * mg) >> sh, no runtime integer-division sequence on the device
   uint32_t mg_rows, mg_wg;
   int sh_rows, sh_wg;
+  // the same for the Winograd 2x2-tile grid of tile 70 (Ht*Wt tiles per image, Wt per row)
+  uint32_t mg_tiles, mg_wt;
+  int sh_tiles, sh_wt;
+  // and its unit decomposition (units per split-K slice, n-blocks, slices)
+  uint32_t mg_mn, mg_ntn, mg_ks;
+  int sh_mn, sh_ntn, sh_ks;
 };
 
 // d >= 1: mg = ceil(2^(31+l) / d) < 2^32, sh = 31 + l, l = ceil(log2 d)

@@ -30,6 +30,18 @@ namespace {
 // Per unit the arithmetic is tile 68's (same transforms, MFMA order, inverse
 // transform and epilogue operations, in the same order): bit-identical outputs.
 typedef unsigned int u32x4v __attribute__((ext_vector_type(4)));
+// tile_point_full with the two divisions by host magic numbers (ConvArgs
+// mg_tiles / mg_wt): exact, and a multiply-high instead of a division sequence
+// three times per unit
+__device__ __forceinline__ bool tile_point_magic(const ConvArgs& a, int Ht, int Wt, int m, int& b, int& ti, int& tj) {
+  const int per = Ht * Wt;
+  const bool ok = m < a.B * per;
+  b = ok ? po::div_by(m, a.mg_tiles, a.sh_tiles) : 0;
+  const int l = ok ? m - b * per : 0;
+  ti = po::div_by(l, a.mg_wt, a.sh_wt);
+  tj = l - ti * Wt;
+  return ok;
+}
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const void* p, uint32_t bytes) {
   return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), 0, (int)bytes, 0x00020000);
 }
@@ -84,14 +96,15 @@ __global__ __launch_bounds__(512, 1) void conv_wino5_k(const ConvArgs a, const f
   if constexpr (MODE != 1) rs_bias = rsrc(a.bias, a.bias ? (uint32_t)a.N * 4u : 0u);
 
   // ---- unit u -> (first tile row m0, n-block tn, split-K slice s and its k-steps [ks0, ks1)), wave-uniform
+  // (divisions by host magic numbers: ConvArgs mg_mn / mg_ntn / mg_ks)
   auto unit = [&](int u, int& m0, int& tn, int& s, int& ks0, int& ks1) {
-    s = u / mn;
+    s = po::div_by(u, a.mg_mn, a.sh_mn);
     const int rem = u - s * mn;
-    const int tm = rem / a.ntiles_n;
+    const int tm = po::div_by(rem, a.mg_ntn, a.sh_ntn);
     tn = rem - tm * a.ntiles_n;
     m0 = tm * T4;
-    ks0 = s * kc_n / a.ksplit;
-    ks1 = (s + 1) * kc_n / a.ksplit;
+    ks0 = po::div_by(s * kc_n, a.mg_ks, a.sh_ks);
+    ks1 = po::div_by((s + 1) * kc_n, a.mg_ks, a.sh_ks);
   };
 
   // ---- input staging: thread (tile r, channel pair tc) loads its 4x4 patch, 2 channels
@@ -99,13 +112,21 @@ __global__ __launch_bounds__(512, 1) void conv_wino5_k(const ConvArgs a, const f
   uint32_t off[16];
   auto offsets = [&](int m0) {
     int b, ti, tj;
-    const bool ok_t = tile_point_full(a, Ht, Wt, m0 + r, b, ti, tj);
+    const bool ok_t = tile_point_magic(a, Ht, Wt, m0 + r, b, ti, tj);
     const uint32_t pix_bytes = (uint32_t)a.Cin_p * 4u;
+    // (one row product per patch row, the columns as uniform steps: the same
+    // offsets modulo 2^32 with 4 instead of 16 pairs of quarter-rate multiplies)
+    const int y0 = 2 * ti - 1, x0 = 2 * tj - 1;
 #pragma unroll
-    for (int p = 0; p < 16; ++p) {
-      const int y = 2 * ti - 1 + (p >> 2), x = 2 * tj - 1 + (p & 3);
-      const bool ok = ok_t && (unsigned)y < (unsigned)a.Hin && (unsigned)x < (unsigned)a.Win;
-      off[p] = ok ? (((uint32_t)b * a.Hin + y) * a.Win + x) * pix_bytes + 8u * tc : kOOB;
+    for (int i = 0; i < 4; ++i) {
+      const int y = y0 + i;
+      const bool rok = ok_t && (unsigned)y < (unsigned)a.Hin;
+      const uint32_t rb = (((uint32_t)b * a.Hin + y) * a.Win + x0) * pix_bytes + 8u * tc;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const bool ok = rok && (unsigned)(x0 + j) < (unsigned)a.Win;
+        off[4 * i + j] = ok ? rb + (uint32_t)j * pix_bytes : kOOB;
+      }
     }
   };
   f2v d[16];
@@ -367,7 +388,7 @@ __global__ __launch_bounds__(512, 1) void conv_wino5_k(const ConvArgs a, const f
 #pragma unroll
     for (int ps = 0; ps < 2; ++ps) {
       int vb = 0, vti = 0, vtj = 0;
-      const bool tl = tile_point_full(a, Ht, Wt, cur_m0 + TH * ps + (tid >> 4), vb, vti, vtj);
+      const bool tl = tile_point_magic(a, Ht, Wt, cur_m0 + TH * ps + (tid >> 4), vb, vti, vtj);
       uint32_t ok4 = 0u;
 #pragma unroll
       for (int p = 0; p < 4; ++p) {
@@ -468,8 +489,13 @@ int launch_wino5(const ConvArgs& a, const float* U, hipStream_t st) {
   const int Ht = (a.Hout + 1) / 2, Wt = (a.Wout + 1) / 2;
   ConvArgs b = a;
   b.ntiles_n = a.N / N4;
+  div_magic(Ht * Wt, b.mg_tiles, b.sh_tiles);
+  div_magic(Wt, b.mg_wt, b.sh_wt);
   const int ntm = ceil_div((int64_t)a.B * Ht * Wt, T4);
   const int mn = ntm * b.ntiles_n;
+  div_magic(mn, b.mg_mn, b.sh_mn);
+  div_magic(b.ntiles_n, b.mg_ntn, b.sh_ntn);
+  div_magic(a.ksplit, b.mg_ks, b.sh_ks);
   PO_REQUIRE((int64_t)mn * a.ksplit < (1LL << 31), "po_conv: too many tiles");
   const int units = mn * a.ksplit;
   PO_REQUIRE(!(a.res && a.accumulate), "po_conv: tile 70 does not accumulate a shortcut launch");
