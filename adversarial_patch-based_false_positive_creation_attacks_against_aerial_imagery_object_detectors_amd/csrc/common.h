@@ -47,6 +47,20 @@ __device__ __forceinline__ float leaky(float v) { return __builtin_elementwise_m
 // is leaky() exactly, slope 1 the identity (maximum(v, v * 1) = v, NaN, signed
 // zeros and infinities included) -- no per-element moves between the two paths.
 __device__ __forceinline__ float act_slope(int act) { return act ? 0.1f : 1.0f; }
+
+// OR of w over lanes i .. i+n-1 into lane i (n = 4 or 8, groups aligned inside
+// a 16-lane DPP row; other lanes get partial ORs) by DPP row shifts
+// (dst[i] = src[i + k], 0 past the row's end): VALU-rate, where __shfl_xor's
+// dependent ds_bpermute round trips stall the epilogue.  Every lane of the
+// wave must be active.
+template <int n>
+__device__ __forceinline__ uint32_t or_group_down(uint32_t w) {
+  static_assert(n == 4 || n == 8, "groups of 4 or 8 lanes");
+  w |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)w, 0x101, 0xF, 0xF, false);   // row_shl:1
+  w |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)w, 0x102, 0xF, 0xF, false);   // row_shl:2
+  if constexpr (n == 8) w |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)w, 0x104, 0xF, 0xF, false);   // row_shl:4
+  return w;
+}
 __device__ __forceinline__ float leaky_or_id(float v, float slope) { return __builtin_elementwise_maximum(v, v * slope); }
 
 // torch.div(a, b, rounding_mode='floor') for float32 (ATen div_floor)

@@ -370,9 +370,7 @@ __device__ __forceinline__ void conv_epilogue(const ConvArgs& a, const floatx16 
         if (a.ybits) {
           // the 8 lanes of a row hold channels n0' .. n0' + 31 of one word: OR their nibbles
           uint32_t w = nib << (4 * (lane & 7));
-          w |= (uint32_t)__shfl_xor((int)w, 1);
-          w |= (uint32_t)__shfl_xor((int)w, 2);
-          w |= (uint32_t)__shfl_xor((int)w, 4);
+          w = or_group_down<8>(w);
           if (live && (lane & 7) == 0) a.ybits[(uint32_t)pix * wpp + (n >> 5)] = w;
         }
       }

@@ -329,8 +329,7 @@ __global__ __launch_bounds__(256) void conv_reduce_k(const ConvArgs a) {
   if (a.ybits) {
     // threads 4k .. 4k+3 hold the 32 channels of one sign-bit word (N % 32 == 0)
     uint32_t w = nib << (4 * RQ * (threadIdx.x & 3));
-    w |= (uint32_t)__shfl_xor((int)w, 1);
-    w |= (uint32_t)__shfl_xor((int)w, 2);
+    w = po::or_group_down<4>(w);
     if (live && (threadIdx.x & 3) == 0) a.ybits[pix * (a.Cout_p >> 5) + (n0 >> 5)] = w;
   }
   if (a.y_amax) po::amax_commit(a.y_amax, my);

@@ -717,9 +717,7 @@ __global__ __launch_bounds__(64 * NW) void conv_wino2_k(const ConvArgs a, const 
       if (a.ybits) {
         // 8 lanes hold the 32 channels of one sign-bit word: OR their nibbles
         uint32_t w = nib << (4 * (lane & 7));
-        w |= (uint32_t)__shfl_xor((int)w, 1);
-        w |= (uint32_t)__shfl_xor((int)w, 2);
-        w |= (uint32_t)__shfl_xor((int)w, 4);
+        w = po::or_group_down<8>(w);
         if (ok && (lane & 7) == 0) a.ybits[pix * wpp + (n4 >> 5)] = w;
       }
     }
@@ -1028,9 +1026,7 @@ __global__ __launch_bounds__(256, 2) void conv_wino3_k(const ConvArgs a, const f
         if (a.ybits) {
           // 8 lanes hold the 32 channels of one sign-bit word: OR their nibbles
           uint32_t w = nib << (4 * (lane & 7));
-          w |= (uint32_t)__shfl_xor((int)w, 1);
-          w |= (uint32_t)__shfl_xor((int)w, 2);
-          w |= (uint32_t)__shfl_xor((int)w, 4);
+          w = po::or_group_down<8>(w);
           if (ok && (lane & 7) == 0) a.ybits[pix * wpp + (n4 >> 5)] = w;
         }
       }
@@ -1385,9 +1381,7 @@ __global__ __launch_bounds__(512, 1) void conv_wino4_k(const ConvArgs a, const f
         if (a.ybits) {
           // 8 lanes hold the 32 channels of one sign-bit word: OR their nibbles
           uint32_t w = nib << (4 * (lane & 7));
-          w |= (uint32_t)__shfl_xor((int)w, 1);
-          w |= (uint32_t)__shfl_xor((int)w, 2);
-          w |= (uint32_t)__shfl_xor((int)w, 4);
+          w = po::or_group_down<8>(w);
           if (ok && (lane & 7) == 0) a.ybits[pix * wpp + (n4 >> 5)] = w;
         }
       }
