@@ -4,6 +4,9 @@
 #include <stdint.h>
 #include <stdio.h>
 #include <stdarg.h>
+#include <map>
+#include <mutex>
+#include <utility>
 #include "../../include/advpatch.h"
 
 namespace po {
@@ -33,6 +36,23 @@ inline int resident_groups(const void* kernel, int block_threads, size_t dyn_lds
     cus = 256;
   if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, kernel, block_threads, dyn_lds) != hipSuccess) occ = 1;
   return (cus > 0 ? cus : 1) * (occ > 0 ? occ : 1);
+}
+
+// resident_groups, remembered per (current device, kernel): a persistent
+// launch queries the occupancy calculator once per device it runs on, so a
+// process driving devices with different CU counts or partition modes sizes
+// each device's grid from that device.
+inline int resident_groups_cached(const void* kernel, int block_threads) {
+  static std::mutex mu;
+  static std::map<std::pair<int, const void*>, int> table;
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) dev = -1;
+  std::lock_guard<std::mutex> lock(mu);
+  auto it = table.find({dev, kernel});
+  if (it != table.end()) return it->second;
+  const int n = resident_groups(kernel, block_threads);
+  table[{dev, kernel}] = n;
+  return n;
 }
 
 // leaky'(y) for LeakyReLU(0.1): PyTorch leaky_relu_backward uses x > 0

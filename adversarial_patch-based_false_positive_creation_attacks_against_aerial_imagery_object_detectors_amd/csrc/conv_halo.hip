@@ -160,8 +160,8 @@ int launch_halo(const ConvArgs& a, hipStream_t st) {
   const int tiles_r = ceil_div(a.Hout, HR), tiles_c = ceil_div(a.Wout, HC);
   const int64_t ntiles = (int64_t)a.B * tiles_r * tiles_c;
   PO_REQUIRE(ntiles < (1LL << 31), "po_conv: tile 69: too many tiles");
-  // persistent: as many workgroups as the device holds at once (queried once per process)
-  static const int resident = resident_groups(reinterpret_cast<const void*>(conv_halo_pool_k), 256);
+  // persistent: as many workgroups as the device holds at once (queried once per device)
+  const int resident = resident_groups_cached(reinterpret_cast<const void*>(conv_halo_pool_k), 256);
   const int grid = (int)(ntiles < resident ? ntiles : resident);
   hipLaunchKernelGGL(conv_halo_pool_k, dim3(grid), dim3(256), 0, st, a, tiles_r, tiles_c, (int)ntiles);
   return check_launch("po_conv (halo pool tile)");

@@ -530,9 +530,8 @@ int launch_wino5(const ConvArgs& a, const float* U, hipStream_t st) {
 #undef PO_W5
   PO_REQUIRE(k, "po_conv: tile 70 has no kernel for epilogue fields 0x%x", which);
   // one workgroup per CU (the occupancy of this build), at most one per unit
-  static int resident[192] = {0};
-  if (!resident[which]) resident[which] = resident_groups(k, 512);
-  const int grid = units < resident[which] ? units : resident[which];
+  const int resident = resident_groups_cached(k, 512);
+  const int grid = units < resident ? units : resident;
   void* args[] = {&b, const_cast<float**>(&U), const_cast<int*>(&Ht), const_cast<int*>(&Wt),
                   const_cast<int*>(&units), const_cast<int*>(&mn)};
   PO_REQUIRE(hipLaunchKernel(k, dim3(grid), dim3(512), args, 0, st) == hipSuccess, "po_conv: tile 70 launch failed");

@@ -1365,6 +1365,7 @@ class NetPlan:
             for t in bufs.values():
                 t.uniform_(-1.0, 1.0)           # time on random data, not zeros (clock)
         self.amax.fill_(0x3F800000)             # max|x| = 1.0 for the U(-1,1) buffers
+        self.join_cone_stream()                 # no early cone evaluation still writing cone_boxes
         if self.cone_boxes is not None:         # boxed dgrads: time them on training-like footprints
             self.set_cones(self.tuning_rois())
         self.set_support_boxes()                # compact dgrad grids: boxes at the current window origins
@@ -1461,12 +1462,50 @@ class NetPlan:
             key = key + ("pool", 1)
         return key + ("mrows", desc.mrows) if desc.mrows else key
 
+    _tile_map = None
+
+    @classmethod
+    def tile_map(cls):
+        """ADVPATCH_TILE_MAP ("68:70,66:70"), parsed once per value: a diagnostic
+        A/B remap of cached / tuned tiles on unboxed launches."""
+        remap = os.environ.get("ADVPATCH_TILE_MAP", "")
+        if cls._tile_map is None or cls._tile_map[0] != remap:
+            m = dict(tuple(int(v) for v in kv.split(":")) for kv in remap.split(",") if kv.strip())
+            cls._tile_map = (remap, m)
+        return cls._tile_map[1]
+
     def _set_tile(self, desc, choice):
         t, ks = (choice, 1) if isinstance(choice, int) else choice
-        remap = os.environ.get("ADVPATCH_TILE_MAP")          # diagnostic A/B: "68:70,66:70" on unboxed launches
-        if remap and not desc.gbox:
-            t = dict(tuple(int(v) for v in kv.split(":")) for kv in remap.split(",")).get(t, t)
         desc.tile, desc.ksplit = t, ks
+        self._apply_ws(desc)
+        remap = self.tile_map()
+        if remap and not desc.gbox and t in remap:
+            # only where the target tile takes the launch: po_conv is called under
+            # a stream capture that is discarded (its argument checks run, its
+            # kernels never do); a refused remap keeps the chosen tile
+            desc.tile = remap[t]
+            self._apply_ws(desc)
+            if not self._probe_conv(desc):
+                desc.tile = t
+                self._apply_ws(desc)
+
+    def _probe_conv(self, desc):
+        args = next((a for n, a, d in self.fwd_ops + self.bwd_ops if d is desc), None)
+        if args is None or any(isinstance(a, str) for a in args):
+            return False
+        side = torch.cuda.Stream(device=self.device)
+        graph = torch.cuda.CUDAGraph()
+        ok = False
+        try:
+            with torch.cuda.graph(graph, stream=side, capture_error_mode="relaxed"):
+                ok = self.lib.po_conv(*args, nat.stream()) == 0
+        except RuntimeError:
+            ok = False
+        del graph
+        return ok
+
+    def _apply_ws(self, desc):
+        ks = desc.ksplit
         if ks > 1:
             desc.workspace = self._ensure_ws(ks * desc.B * desc.Hg * desc.Wg * desc.N).data_ptr()
         else:
@@ -1489,7 +1528,9 @@ class NetPlan:
             if not self.sparse_input or roi is None:
                 raise ValueError("NetPlan.run_forward: this plan's first layer cannot read a sparse composite")
             cmp = (nat.c_void_p(base.data_ptr()), xp, nat.c_void_p(roi.data_ptr()))
+        self.join_cone_stream()               # a previous forward's cone write is ordered before this one
         self._cones_for = None
+        self.last_first_op = None
         if roi is not None and self.cone_boxes is not None and os.environ.get("ADVPATCH_EARLY_CONES", "1") != "0":
             # the gradient cones depend on the footprint boxes only: evaluate them
             # (a serial walk of the block graph, one small workgroup per image)
@@ -1497,6 +1538,7 @@ class NetPlan:
             if getattr(self, "_cone_stream", None) is None:
                 self._cone_stream = torch.cuda.Stream(device=self.device)
             self._cone_stream.wait_stream(torch.cuda.current_stream())
+            roi.record_stream(self._cone_stream)          # read there: not reused before that read ends
             with torch.cuda.stream(self._cone_stream):
                 self.set_cones(roi)
             self._cones_for = roi
@@ -1511,6 +1553,7 @@ class NetPlan:
                     name, args = name + "_cmp", cmp + args[1:]
                 else:
                     args = (xp,) + args[1:]
+                self.last_first_op = name
             self._launch(lib, name, args, desc, st)
             if side is not None and k in self._trig_f:
                 # block b is done: its tail runs beside the rest of the network
@@ -1524,6 +1567,15 @@ class NetPlan:
         if side is not None:
             torch.cuda.current_stream().wait_stream(side)
         return [self.act[h] for h in self.heads]
+
+    def join_cone_stream(self):
+        """Order the current stream after any cone evaluation still pending on
+        the side stream (run_forward with roi evaluates the cones there; a
+        forward whose backward never runs would otherwise leave that write
+        unordered with the next set_cones or a host read of cone_boxes)."""
+        cs = getattr(self, "_cone_stream", None)
+        if cs is not None:
+            torch.cuda.current_stream().wait_stream(cs)
 
     def _launch(self, lib, name, args, desc, st):
         timer = self.conv_timer
@@ -1565,6 +1617,7 @@ class NetPlan:
         if roi is not None and getattr(self, "_cones_for", None) is roi:
             torch.cuda.current_stream().wait_stream(self._cone_stream)     # evaluated beside the forward
         else:
+            self.join_cone_stream()           # an unconsumed early evaluation must land before this one
             self.set_cones(roi)
         self._cones_for = None
         self.set_support_boxes()

@@ -56,6 +56,10 @@ TV_FACTOR = 2.5      # train_patch.py:25
 NPS_FACTOR = 0.01    # train_patch.py:26
 TARGET_ID = 14       # train_patch.py:28 (helicopter)
 OBJECTIVES = {"ce": 0, "targeted": 1, "untargeted": 2}
+# classes per anchor that po_cell_loss reads: 5 + 15 channels per anchor, the
+# layout the reference's loss head hard-codes (train_patch.py:459; NCLS in
+# csrc/loss_ops.hip).  PatchTrainer refuses a network with another count.
+CELL_CLASSES = 15
 
 
 def _head_args(hw, views):
@@ -79,7 +83,7 @@ class _CellLoss(torch.autograd.Function):
         A = 3 * len(heads)
         out2 = torch.empty(2, device=dev)
         obj = torch.empty(B, A, device=dev)
-        cls = torch.empty(B, A, 15, device=dev)
+        cls = torch.empty(B, A, CELL_CLASSES, device=dev)
         cells = torch.empty(len(heads), B, dtype=torch.int32, device=dev)
         if flags is None:
             flags = torch.zeros(1, dtype=torch.int32, device=dev)
@@ -298,6 +302,9 @@ class PatchTrainer(object):
         # classes per anchor of the YOLO heads; po_cell_loss reads 5 + 15 channels per
         # anchor, as the reference's loss head does (train_patch.py:459)
         self.num_classes = int(next(b["classes"] for b in self.darknet_model.blocks if b["type"] == "yolo"))
+        if self.num_classes != CELL_CLASSES:
+            raise ValueError("%s: YOLO heads with %d classes; the loss head (po_cell_loss, train_patch.py:459) "
+                             "reads 5 + %d channels per anchor" % (self.config.cfgfile, self.num_classes, CELL_CLASSES))
         self.patch_applier = PatchApplier()
         self.patch_transformer = PatchTransformer()
         self.nps_calculator = NPSCalculator(self.config.printfile, self.config.patch_size).to(self.device)
@@ -348,6 +355,7 @@ class PatchTrainer(object):
         sparse = (img_batch.size(-2) == S == net.height == net.width and self.patch_transformer.sparse_ok(S, draws)
                   and net.sparse_input_ok(B, S, S, img_batch.device, center=True)
                   and os.environ.get("ADVPATCH_SPARSE_COMPOSITE", "1") != "0")
+        self.last_sparse = sparse
         # the median pool and the regularisers of the patch: one autograd node
         mp, reg = patch_front(adv_patch, self.nps_calculator.colors)
         p_img, center = self.patch_transformer.forward_composite(adv_patch, lab_batch, img_batch, img_size,

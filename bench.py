@@ -422,16 +422,44 @@ def _free_port():
     return port
 
 
+def visible_gpu_count():
+    """GPUs this process could use, counted without any HIP call (the parent
+    of the ranks must leave the devices untouched): the KFD topology's GPU
+    nodes (simd_count > 0), narrowed by the visible-device variables the ROCm
+    runtime honours.  None when neither source is readable (the ranks then
+    find out themselves)."""
+    n = None
+    try:
+        root = "/sys/class/kfd/kfd/topology/nodes"
+        n = 0
+        for d in os.listdir(root):
+            try:
+                with open(os.path.join(root, d, "properties")) as f:
+                    props = dict(line.split()[:2] for line in f if len(line.split()) >= 2)
+            except OSError:
+                continue
+            if int(props.get("simd_count", "0")) > 0:
+                n += 1
+    except (OSError, ValueError):
+        n = None
+    for var in ("ROCR_VISIBLE_DEVICES", "HIP_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES"):
+        v = os.environ.get(var)
+        if v is not None:
+            k = len([x for x in v.split(",") if x.strip() != ""])
+            n = k if n is None else min(n, k)
+    return n
+
+
 def launch_ranks(args):
     """``bench.py --gpus N`` outside torchrun: start the N ranks as children
     (python -m torch.distributed.run, one process per GPU, rendezvous on
     127.0.0.1) and exit with their status.  Nothing here touches the GPU
-    (torch.cuda.device_count() does not initialise HIP), so the children own
-    the devices.  Every rank inherits stdout; only rank 0 prints the JSON line."""
+    (visible_gpu_count reads the KFD topology and the environment), so the
+    children own the devices.  Every rank inherits stdout; only rank 0 prints the JSON line."""
     n = args.gpus
     if args.dist_backend == "nccl" and not args.dry_run:
-        ndev = torch.cuda.device_count()
-        if n > ndev:
+        ndev = visible_gpu_count()
+        if ndev is not None and n > ndev:
             raise SystemExit("bench.py --gpus %d: only %d GPU(s) visible; RCCL needs one GPU per rank "
                              "(use --dist-backend gloo to rehearse ranks sharing a GPU)" % (n, ndev))
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(n),

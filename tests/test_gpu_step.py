@@ -91,13 +91,37 @@ TIE_TOL = {"fp32": 5e-5, "fp16x3": 1e-4}
 OBJ_TOL_608 = 5e-5
 
 
-def branch_aligned(tr, ref_net, img, lab, patch, dr, objective="ce", geometry32=False):
+def keyed_draws(seed, step, b0, B, P):
+    """(hip draws, oracle draws) of one step exactly as the trainer makes them
+    (PatchTransformer.make_draws, the path bench.py times): the HIP side gets
+    the six scalars per image and the po_draws key -- no noise tensor, so the
+    warp kernels regenerate the noise at each corner they read and the step
+    takes the sparse box composite -- and the oracle gets the same scalars
+    plus the noise tensor po_draws materialises from that key."""
+    sy = pkg_mod("synthetic")
+    full = {k: v.cpu() for k, v in sy.draws_device(seed, step, b0, B, P, DEV).items()}
+    hip = {k: v for k, v in full.items() if k != "noise"}
+    hip["noise_key"] = (seed, step, b0)
+    return hip, full
+
+
+def assert_timed_path(tr):
+    """The step just run took the path bench.py times: the sparse box-only
+    composite (po_warp_box_fwd_keyed / _bwd_keyed) with the first layer reading
+    frames + boxes (po_conv_first_*_cmp)."""
+    plan = tr.last_plan
+    assert tr.last_sparse and plan.sparse_input, "sparse composite not taken"
+    assert plan.last_first_op in ("po_conv_first_fwd_cmp", "po_conv_first_pool_fwd_cmp"), plan.last_first_op
+
+
+def branch_aligned(tr, ref_net, img, lab, patch, dr, objective="ce", geometry32=False, hip_dr=None):
     """One HIP step and the oracle on the branch decisions it took: the fp32
     oracle (with the tie check), the float64 yardstick and, with
     ``geometry32``, the fp32 oracle with its placement geometry in float64
     (the HIP path's deliberate deviation).  Inputs on the CPU,
-    draws as CPU tensors.  Returns (terms, hip grad, fp32 oracle result, errs)
-    with errs = {"hip_f64": |g_hip - g64|/max|g64|, "o32_f64": the fp32
+    draws as CPU tensors (``hip_dr``: the HIP side's draws when they differ
+    in form, e.g. keyed_draws).  Returns (terms, hip grad, fp32 oracle result,
+    errs) with errs = {"hip_f64": |g_hip - g64|/max|g64|, "o32_f64": the fp32
     oracle's own distance, "hip_o32": north_star's |g_hip - g32|/max|g32|,
     "hip_o32g": the same against the float64-geometry fp32 oracle}."""
     import time
@@ -106,7 +130,9 @@ def branch_aligned(tr, ref_net, img, lab, patch, dr, objective="ce", geometry32=
     t0 = time.time()
     say = lambda what: print("  [branch_aligned B=%d] %s (%.1fs)" % (img.size(0), what, time.time() - t0), flush=True)
     pg = patch.to(DEV).requires_grad_(True)
-    loss, terms = tr.losses(pg, img.to(DEV), lab.to(DEV), {k: v.to(DEV) for k, v in dr.items()}, objective=objective)
+    hd = dr if hip_dr is None else hip_dr
+    hd = {k: (v.to(DEV) if torch.is_tensor(v) else v) for k, v in hd.items()}
+    loss, terms = tr.losses(pg, img.to(DEV), lab.to(DEV), hd, objective=objective)
     br = plan_branches(tr.last_plan)
     loss.backward()
     g = pg.grad.cpu()
@@ -148,6 +174,18 @@ def assert_north_star(errs, tag):
     assert errs["hip_o32"] <= 1e-4, errs
 
 
+# The HIP path's own accuracy: its patch gradient against the float64
+# evaluation on the same branches.  The 1e-4 legs are dominated by the fp32
+# oracle's own error (its fp32 placement geometry); this bound is what a
+# regression of the HIP arithmetic itself would have to get past.
+HIP_F64_TOL = 1e-5
+
+
+def assert_hip_accuracy(errs, tag):
+    print("%s: hip vs float64 %.3g (bound %.0e)" % (tag, errs["hip_f64"], HIP_F64_TOL))
+    assert errs["hip_f64"] <= HIP_F64_TOL, errs
+
+
 @pytest.mark.parametrize("prec", ["fp16x3", "fp32"])
 def test_step_yolov3_dota_608(tmp_path, prec):
     """yolov3-dota, two 608x608 frames, 224x224 patch: patch gradient within
@@ -157,16 +195,24 @@ def test_step_yolov3_dota_608(tmp_path, prec):
     terms, g, ref32, errs = branch_aligned_608(tr, ref_net, 2, 40)
     _compare(ref32, terms, g, grad_check=False, obj_tol=OBJ_TOL_608)
     assert_north_star(errs, "yolov3 (%s)" % prec)
+    assert_hip_accuracy(errs, "yolov3 (%s)" % prec)
 
 
 def test_step_yolov3_targeted(tmp_path):
     """BASELINE config 4's per-rank workload: the targeted class objective
     (noCLS_loss_targeted, a batch SUM, train_patch.py:550-577) + NPS + TV on
-    yolov3-dota@608, exact fp32 convolutions."""
+    yolov3-dota@608, exact fp32 convolutions, with the trainer's keyed draws
+    (the sparse box composite the bench times, asserted)."""
     tr, ref_net = _trainer("builtin:yolov3-dota", tmp_path, objective="targeted", prec="fp32")
-    terms, g, ref32, errs = branch_aligned_608(tr, ref_net, 3, 140, objective="targeted")
+    sy = pkg_mod("synthetic")
+    B, P, S = 3, 224, 608
+    img, lab, patch = sy.frames(B, S, seed=140), sy.labels(B, seed=141), sy.patch(P, seed=142)
+    hip_dr, dr = keyed_draws(143, 0, 0, B, P)             # the trainer's keyed draws: the timed path
+    terms, g, ref32, errs = branch_aligned(tr, ref_net, img, lab, patch, dr, "targeted", hip_dr=hip_dr)
+    assert_timed_path(tr)
     _compare(ref32, terms, g, grad_check=False, obj_tol=OBJ_TOL_608)
     assert_north_star(errs, "yolov3 targeted")
+    assert_hip_accuracy(errs, "yolov3 targeted")
 
 
 def assert_tiny_parity(errs, tag):
@@ -202,6 +248,7 @@ def test_step_tiny_416(tmp_path, objective):
     assert terms["obj"].shape == (B, 6) and terms["cls"].shape == (B, 6, 15)
     _compare(ref32, terms, g, grad_check=False, obj_tol=OBJ_TOL_608)
     assert_tiny_parity(errs, "tiny B=4 %s" % objective)
+    assert_hip_accuracy(errs, "tiny B=4 %s" % objective)
 
 
 def test_two_adam_steps_yolov3(tmp_path):

@@ -12,7 +12,8 @@ import torch
 
 import oracle
 from conftest import ROOT, pkg_mod
-from test_gpu_step import assert_north_star, assert_tiny_parity, branch_aligned
+from test_gpu_step import (assert_hip_accuracy, assert_north_star, assert_timed_path, assert_tiny_parity,
+                           branch_aligned, keyed_draws)
 
 pytestmark = pytest.mark.gpu
 DEV = torch.device("cuda", 0)
@@ -175,10 +176,14 @@ def test_empty_shard_adds_only_its_patch_terms(yolo_weights, objective):
 def test_headline_plan_b16_608(yolo_weights, monkeypatch, prec):
     """The exact plan bench.py times: yolov3-dota, B=16, S=608, P=224,
     receptive-field windows and gradient cones on, conv tiles and split-K
-    factors from the committed cache the bench uses.  Cells bit-exact, loss
-    terms, objectness/class at the cells, and the patch gradient against the
-    branch-aligned oracle (ties asserted): within 1e-4 of the fp32 oracle
-    (north_star) and of the float64 evaluation."""
+    factors from the committed cache the bench uses, and the trainer's keyed
+    draws, so the composite is the sparse box-only one and the first layer
+    reads frames + boxes (asserted).  Cells bit-exact, loss terms,
+    objectness/class at the cells, and the patch gradient against the
+    branch-aligned oracle (ties asserted; the oracle gets the noise tensor
+    po_draws materialises from the same key): within 1e-4 of the fp32 oracle
+    (north_star) and of the float64 evaluation, and the HIP gradient within
+    1e-5 of the float64 evaluation."""
     monkeypatch.setenv("ADVPATCH_TUNE_CACHE", TILES)
     monkeypatch.setenv("ADVPATCH_TUNE", "cache")          # the committed tiles, nothing timed
     sy, G = pkg_mod("synthetic"), pkg_mod("cfg_gen")
@@ -187,9 +192,10 @@ def test_headline_plan_b16_608(yolo_weights, monkeypatch, prec):
     B, S, P = 16, 608, 224
     img, lab = sy.frames_slice(0, B, S, seed=1000), sy.labels_slice(0, B, seed=2000)
     patch = sy.patch(P, seed=2)
-    dr = {k: v.cpu() for k, v in sy.draws_device(3, 0, 0, B, P, DEV).items()}      # the bench's step-0 draws
+    hip_dr, dr = keyed_draws(3, 0, 0, B, P)               # the bench's step-0 draws, keyed as it takes them
     ref_net = oracle.OracleDarknet(G.cfg_text("builtin:yolov3-dota"), yolo_weights)
-    terms, g, ref32, errs = branch_aligned(tr, ref_net, img, lab, patch, dr)
+    terms, g, ref32, errs = branch_aligned(tr, ref_net, img, lab, patch, dr, hip_dr=hip_dr)
+    assert_timed_path(tr)                                  # sparse box composite + first layer on frames + boxes
     plan = tr.last_plan
     assert plan.windowed and plan.cone_blocks
     tuned = [d for name, _, d in plan.fwd_ops + plan.bwd_ops if name == "po_conv"]
@@ -201,6 +207,7 @@ def test_headline_plan_b16_608(yolo_weights, monkeypatch, prec):
         a, b = float(terms[k]), float(ref32[k])
         assert abs(a - b) <= 2e-5 * max(1.0, abs(b)), (k, a, b)
     assert_north_star(errs, "headline plan (%s) B=16" % prec)
+    assert_hip_accuracy(errs, "headline plan (%s) B=16" % prec)
     tr.check_flags()
 
 
@@ -208,10 +215,11 @@ def test_headline_plan_b16_608(yolo_weights, monkeypatch, prec):
 def test_tiny_bench_plan_b256_416(tmp_path_factory, monkeypatch):
     """Config 5 as bench.py times it: yolov3-tiny-15 @416, B=256, P=224, the
     committed tiny tile cache in ADVPATCH_TUNE=cache (nothing timed), with
-    every plan feature the tiny number depends on asserted on: the first conv
-    fused with its max pool, the conv + pool epilogues (Winograd pool on tile
-    66 where the cache picks it), the support grid of the head-window dgrad,
-    receptive-field windows and gradient cones.  Against the oracle's
+    every plan feature the tiny number depends on asserted on: the keyed
+    draws' sparse box composite read by the first conv fused with its max pool
+    (po_conv_first_pool_fwd_cmp), the conv + pool epilogues (Winograd pool on
+    tile 66 where the cache picks it), the support grid of the head-window
+    dgrad, receptive-field windows and gradient cones.  Against the oracle's
     generalised two-head loss, branch-aligned (LeakyReLU signs,
     max-pool argmaxes; ties asserted): cells bit-exact, loss terms within
     2e-5, objectness/class within 5e-5, the gradient per assert_tiny_parity."""
@@ -224,9 +232,10 @@ def test_tiny_bench_plan_b256_416(tmp_path_factory, monkeypatch):
     B, S, P = 256, 416, 224
     img, lab = sy.frames_slice(0, B, S, seed=1000), sy.labels_slice(0, B, seed=2000)
     patch = sy.patch(P, seed=2)
-    dr = {k: v.cpu() for k, v in sy.draws_device(3, 0, 0, B, P, DEV).items()}      # the bench's step-0 draws
+    hip_dr, dr = keyed_draws(3, 0, 0, B, P)               # the bench's step-0 draws, keyed as it takes them
     ref_net = oracle.OracleDarknet(G.cfg_text(cfg), wpath)
-    terms, g, ref32, errs = branch_aligned(tr, ref_net, img, lab, patch, dr, geometry32=True)
+    terms, g, ref32, errs = branch_aligned(tr, ref_net, img, lab, patch, dr, geometry32=True, hip_dr=hip_dr)
+    assert_timed_path(tr)
     plan = tr.last_plan
     assert plan.first_pool and plan.conv_pool and plan.support and plan.windowed and plan.cone_blocks
     convs = [d for name, _, d in plan.fwd_ops + plan.bwd_ops if name == "po_conv"]
@@ -240,6 +249,7 @@ def test_tiny_bench_plan_b256_416(tmp_path_factory, monkeypatch):
         a, b = float(terms[k]), float(ref32[k])
         assert abs(a - b) <= 2e-5 * max(1.0, abs(b)), (k, a, b)
     assert_tiny_parity(errs, "tiny bench plan B=256")
+    assert_hip_accuracy(errs, "tiny bench plan B=256")
     tr.check_flags()
 
 

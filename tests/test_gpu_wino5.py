@@ -103,11 +103,14 @@ def test_tile70_sum_only_forward():
     assert torch.equal(runs[0][0], prev)             # y untouched
 
 
-@pytest.mark.parametrize("ks", [2, 4])
+@pytest.mark.parametrize("Cin,ks", [(512, 2), (512, 4), (512, 3), (512, 6), (256, 3)])
 @pytest.mark.parametrize("mode", ["fwd_bits", "dgrad_acc_bits", "dgrad_dual"])
-def test_tile70_split_k_bit_identical_to_68(mode, ks):
+def test_tile70_split_k_bit_identical_to_68(mode, Cin, ks):
+    """Even slices (32 k-steps over 2 or 4) and the uneven ones the tuner also
+    offers (ks 3 and 6: slice bounds by the host's magic-number division;
+    32 k-steps -> 10/11/11 and 5/5/5/5/6/6, 16 -> 5/5/6)."""
     nat = pkg_mod("_native")
-    B, H, Cin, Cout = 4, 19, 512, 256
+    B, H, Cout = 4, 19, 256
     flip = mode.startswith("dgrad")
     xd, wd, bias, U, prev, res, mbits, m2bits = _inputs(B, H, Cin, Cout, flip, seed=17)
     runs = []
