@@ -1,0 +1,475 @@
+// Winograd F(4x4,3x3) po_conv tile 71 (staging 16): conv_wino6_k, a
+// persistent kernel on tile 70's pipeline (conv_wino5.hip) with 4x4 output
+// tiles.
+#pragma clang fp contract(off)
+#include "conv_common.h"
+#include "wino_common.h"
+
+namespace {
+
+// ---------------------------------------------------------------------------
+// Tile 71 (staging 16): conv_wino6_k.
+//
+// F(2x2,3x3) executes 16 products per 4 outputs and input channel (4 per
+// output); F(4x4,3x3) executes 36 per 16 (2.25 per output): 44 % fewer matrix
+// cycles for the same convolution, and on gfx950 the fp32 MFMA shares its
+// issue with the VALU, so the cycles saved are cycles saved.  The price is a
+// 6x6 input transform (12 operations per 6-point transform, Lavin's B^T with
+// the points 0, +-1, +-2, inf, products by powers of two folded into fmas),
+// a larger inverse transform, and 2.25x the transformed weights per input
+// channel (U = G g G^T, float64 on the host, rounded once).
+//
+// Unit = 32 4x4-tiles (512 output pixels) x 64 output channels x one split-K
+// slice; one 512-thread workgroup per CU walks the units (tile 70's order and
+// pipelining: the next unit's first input rows and B fragments are requested
+// under this unit's last MFMAs).
+//   * input: thread (tile tid >> 4, channel tid & 15) loads its 6x6 patch of
+//     one channel (36 dword loads; rows by per-thread offsets, columns as
+//     uniform steps in the scalar offset), transforms it in registers and
+//     writes the 36 components to V[xi][tile][16 channels] (73,728 B, double
+//     buffered: 144 KiB of LDS);
+//   * GEMMs: wave w owns 32 output channels (w >> 2) and 9 of the 36
+//     components (9 (w & 3) ..): one 32x32 accumulator per component (144
+//     accumulator registers), 8 v_mfma_f32_32x32x2_f32 per component and
+//     k-step; B fragments ride a three-deep register ring, each requested
+//     three components before its use;
+//   * epilogue: four passes of 8 tiles.  Each stages its 8 accumulator rows of
+//     every component in LDS (M[xi][tile][64], the two 32-lane halves of a
+//     wave XOR-swizzled apart), inverse-transforms one (tile, channel) per
+//     thread (Y = A^T M A) into LDS, and applies tile 70's epilogue with
+//     16-byte lanes (thread: one pixel of one tile x 4 channels per store).
+//     Every epilogue memory operation is an unconditional buffer op, and a
+//     pass's inputs are requested before the previous pass's stores (vmcnt
+//     counts loads and stores in one queue), so no wait covers a store.
+// Numerics: each output sums 36 transformed products per input channel; the
+// transforms' coefficients (up to 5 in B^T, 8 in A^T) cost accuracy against
+// F(2x2) (DESIGN.md §4 tabulates the per-layer error against float64), and
+// the plan may keep any layer on tile 70.
+constexpr int T6 = 32;                      // 4x4 output tiles per unit
+constexpr int N6 = 64;                      // output channels per unit
+constexpr int NX6 = 36;                     // transform components
+constexpr int CPW6 = 9;                     // components per wave
+constexpr int V6_FLOATS = NX6 * T6 * WK;    // one transformed-input buffer (73,728 B)
+constexpr int TP6 = 8;                      // tiles per epilogue pass
+constexpr int Y6_OFF = NX6 * TP6 * N6;      // LDS floats of one pass's staged accumulators; its outputs follow
+
+// V[xi][tile][16 channels]: 16-byte chunk `chunk` of tile t, swizzled by tile
+__device__ __forceinline__ int v6idx(int xi, int t, int chunk) {
+  return (xi * T6 + t) * WK + ((chunk ^ ((t >> 2) & 3)) << 2);
+}
+
+// 1-D F(4,3) input transform r = B^T d (Lavin: rows 4 0 -5 0 1 0 / 0 -4 -4 1 1 0 /
+// 0 4 -4 -1 1 0 / 0 -2 -1 2 1 0 / 0 2 -1 -2 1 0 / 0 4 0 -5 0 1)
+__device__ __forceinline__ void bt6(float d0, float d1, float d2, float d3, float d4, float d5, float* r) {
+  const float a = __builtin_fmaf(-4.f, d2, d4), b = __builtin_fmaf(-4.f, d1, d3);
+  const float c = d4 - d2, e = d3 - d1;
+  r[0] = __builtin_fmaf(4.f, d0, __builtin_fmaf(-5.f, d2, d4));
+  r[1] = a + b;
+  r[2] = a - b;
+  r[3] = __builtin_fmaf(2.f, e, c);
+  r[4] = __builtin_fmaf(-2.f, e, c);
+  r[5] = __builtin_fmaf(4.f, d1, __builtin_fmaf(-5.f, d3, d5));
+}
+// 1-D inverse y = A^T m (rows 1 1 1 1 1 0 / 0 1 -1 2 -2 0 / 0 1 1 4 4 0 / 0 1 -1 8 -8 1)
+__device__ __forceinline__ void at6(float m0, float m1, float m2, float m3, float m4, float m5, float* y) {
+  const float p = m1 + m2, q = m1 - m2, r = m3 + m4, s = m3 - m4;
+  y[0] = (m0 + p) + r;
+  y[1] = __builtin_fmaf(2.f, s, q);
+  y[2] = __builtin_fmaf(4.f, r, p);
+  y[3] = __builtin_fmaf(8.f, s, q) + m5;
+}
+
+template <int MODE, int EF>   // MODE 0: po_conv epilogue (fields EF), 1: raw split-K partials
+__global__ __launch_bounds__(512, 1) void conv_wino6_k(const ConvArgs a, const float* __restrict__ U, int Ht, int Wt,
+                                                       int units, int mn) {
+  __shared__ __attribute__((aligned(16))) float smem[2 * V6_FLOATS];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave_u = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int h = lane >> 5;
+  const int nbw = wave_u >> 2;                 // the wave's 32-channel half of the unit
+  const int xq = (wave_u & 3) * CPW6;          // its first component
+  const int G = gridDim.x;
+  const int kc_n = a.Cin_p / WK;
+  const int wpp = a.Cout_p >> 5;
+
+  // ---- buffer resources (host: every extent < 2^31 bytes, the input < 2^30)
+  const uint32_t npix = (uint32_t)a.B * (uint32_t)a.Hout * (uint32_t)a.Wout;
+  const uint32_t dst_bytes = npix * (uint32_t)a.Cout_p * 4u;
+  const uint32_t bits_bytes = npix * (uint32_t)wpp * 4u;
+  const uint32_t in_bytes = (uint32_t)__builtin_amdgcn_readfirstlane(a.in_bytes);
+  const __amdgpu_buffer_rsrc_t in_rs = rsrc(a.in, in_bytes);
+  __amdgpu_buffer_rsrc_t rs_out = in_rs, rs_bias = in_rs;
+  if constexpr (MODE == 0) rs_out = rsrc(a.y, (EF & (EF_Y | EF_ACC)) ? dst_bytes : 0u);
+  if constexpr (MODE == 1) rs_out = rsrc(a.ws, (uint32_t)a.ksplit * (uint32_t)a.M * (uint32_t)a.N * 4u);
+  if constexpr (MODE == 0) rs_bias = rsrc(a.bias, a.bias ? (uint32_t)a.N * 4u : 0u);
+
+  // ---- unit u -> (first tile row m0, n-block tn, split-K slice s, its k-steps [ks0, ks1)), wave-uniform
+  auto unit = [&](int u, int& m0, int& tn, int& s, int& ks0, int& ks1) {
+    s = po::div_by(u, a.mg_mn, a.sh_mn);
+    const int rem = u - s * mn;
+    const int tm = po::div_by(rem, a.mg_ntn, a.sh_ntn);
+    tn = rem - tm * a.ntiles_n;
+    m0 = tm * T6;
+    ks0 = po::div_by(s * kc_n, a.mg_ks, a.sh_ks);
+    ks1 = po::div_by((s + 1) * kc_n, a.mg_ks, a.sh_ks);
+  };
+
+  // ---- input staging: thread (tile r, channel c) loads its 6x6 patch of one channel.
+  // Two registers per thread across the k-loop: rbase = byte offset of the
+  // patch's pixel (row 1, column 1), i.e. (4 ti, 4 tj): never negative; okm =
+  // row (bits 0-5) and column (bits 8-13) validity.  Row i >= 1, column j >= 1
+  // read rbase + (i-1)*row_bytes + (j-1)*pix_bytes with the steps in the scalar
+  // offset; row 0 / column 0 subtract row_bytes / pix_bytes in the vector
+  // offset, taken only when that row / column is inside the map (so the vector
+  // offset is the true, non-negative one: no reliance on 32-bit wrap-around)
+  const int r = tid >> 4, c = tid & 15;
+  const uint32_t pix_bytes = (uint32_t)a.Cin_p * 4u;
+  const uint32_t row_bytes = (uint32_t)a.Win * pix_bytes;
+  uint32_t rbase = 0u, okm = 0u;
+  auto offsets = [&](int m0) {
+    int b, ti, tj;
+    const bool ok_t = tile_point_magic(a, Ht, Wt, m0 + r, b, ti, tj);
+    const int y0 = 4 * ti - 1, x0 = 4 * tj - 1;
+    rbase = (((uint32_t)b * a.Hin + (uint32_t)(4 * ti)) * a.Win + (uint32_t)(4 * tj)) * pix_bytes + 4u * c;
+    okm = 0u;
+#pragma unroll
+    for (int i = 0; i < 6; ++i) okm |= (ok_t && (unsigned)(y0 + i) < (unsigned)a.Hin ? 1u : 0u) << i;
+#pragma unroll
+    for (int j = 0; j < 6; ++j) okm |= ((unsigned)(x0 + j) < (unsigned)a.Win ? 1u : 0u) << (8 + j);
+  };
+  float d[36];
+  auto gload = [&](int ks) {
+    const uint32_t cb = (uint32_t)__builtin_amdgcn_readfirstlane(ks * (WK * 4));
+    // opaque per call: hoisted out of the k-loop, the per-load selects would hold
+    // 36 registers across it
+    uint32_t rb = rbase, om = okm;
+    asm volatile("" : "+v"(rb), "+v"(om));
+    const bool c0 = (om >> 8) & 1u;
+#pragma unroll
+    for (int i = 0; i < 6; ++i) {
+      const bool rok = (om >> i) & 1u;
+      const uint32_t rr = i == 0 ? rb - row_bytes : rb;
+      const uint32_t rv = rok ? rr : kOOB;                            // columns 1..5
+      const uint32_t rv0 = (rok && c0) ? rr - pix_bytes : kOOB;       // column 0
+#pragma unroll
+      for (int j = 0; j < 6; ++j) {
+        const uint32_t vo = j == 0 ? rv0 : (((om >> (8 + j)) & 1u) ? rv : kOOB);
+        const uint32_t so = cb + (i == 0 ? 0u : (uint32_t)(i - 1) * row_bytes) + (j == 0 ? 0u : (uint32_t)(j - 1) * pix_bytes);
+        d[6 * i + j] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(in_rs, vo, so, 0));
+      }
+    }
+  };
+  // V = B^T d B: the columns, then the rows; component xi = 6 i + j
+  auto transform = [&](float* Vb) {
+    float t[6][6];
+#pragma unroll
+    for (int j = 0; j < 6; ++j) {
+      float col[6];
+      bt6(d[j], d[6 + j], d[12 + j], d[18 + j], d[24 + j], d[30 + j], col);
+#pragma unroll
+      for (int i = 0; i < 6; ++i) t[i][j] = col[i];
+      __builtin_amdgcn_sched_barrier(0);     // one column at a time: d's registers turn into t's
+    }
+    float* dst = Vb + v6idx(0, r, c >> 2) + (c & 3);
+#pragma unroll
+    for (int i = 0; i < 6; ++i) {
+      float e[6];
+      bt6(t[i][0], t[i][1], t[i][2], t[i][3], t[i][4], t[i][5], e);
+#pragma unroll
+      for (int j = 0; j < 6; ++j) dst[(6 * i + j) * T6 * WK] = e[j];     // v6idx(xi, r, .) = v6idx(0, r, .) + xi*T6*WK
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  };
+
+  // ---- B operand: fragment-ordered U [N/32][Cin_p/16][36][2][64][4] through a buffer
+  // resource (per-lane 16-byte offset, block offset in a scalar register)
+  const __amdgpu_buffer_rsrc_t u_rs = rsrc(U, (uint32_t)a.N * (uint32_t)NX6 * (uint32_t)a.Cin_p * 4u);
+  const uint32_t u_lane = (uint32_t)lane * 16u;
+  float4 bq[3][2];
+  auto bload = [&](int slot, int cc, int ks, int tnn) {
+    const uint32_t blk = (uint32_t)__builtin_amdgcn_readfirstlane(
+        ((((2 * tnn + nbw) * kc_n + ks) * NX6 + xq + cc) * 512) * 4);
+    bq[slot][0] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(u_rs, u_lane, blk, 0));
+    bq[slot][1] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(u_rs, u_lane + 1024u, blk, 0));
+  };
+  floatx16 acc[CPW6];
+  auto mfma_c = [&](int cc, const float* Vb) {
+    // chunks 2h and 2h + 1 of tile lane & 31: their swizzled positions differ in bit 0
+    const int o0 = v6idx(xq, lane & 31, 2 * h), o1 = o0 ^ 4;
+    const float4 a0 = *reinterpret_cast<const float4*>(Vb + o0 + cc * T6 * WK);
+    const float4 a1 = *reinterpret_cast<const float4*>(Vb + o1 + cc * T6 * WK);
+    const float av[8] = {a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w};
+    const float4 b0 = bq[cc % 3][0], b1 = bq[cc % 3][1];
+    const float bv[8] = {b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, b1.z, b1.w};
+#pragma unroll
+    for (int s8 = 0; s8 < 8; ++s8)             // MFMA step s, half h <-> channel 8h + s
+      acc[cc] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[s8], bv[s8], acc[cc], 0, 0, 0);
+  };
+  // component cc's MFMAs, then the ring slot it freed gets component cc + 3 (this
+  // k-step) or cc - 6 (the next one)
+  auto comp = [&](int cc, const float* Vb, int ks, int tnn) {
+    mfma_c(cc, Vb);
+    __builtin_amdgcn_sched_barrier(0);
+    if (cc + 3 < CPW6) bload(cc % 3, cc + 3, ks, tnn);
+    else bload(cc % 3, cc - 6, ks + 1, tnn);
+    __builtin_amdgcn_sched_barrier(0);
+  };
+
+  // ---- the unit loop
+  int u = po::xcd_remap();                     // host: gridDim.x <= units
+  int m0, tn, s, ks0, ks1;
+  unit(u, m0, tn, s, ks0, ks1);
+  offsets(m0);
+  gload(ks0);
+#pragma unroll
+  for (int cc = 0; cc < 3; ++cc) bload(cc, cc, ks0, tn);
+  float* const M = smem;
+  float* const Yl = smem + Y6_OFF;
+  for (;;) {
+    __syncthreads();                           // the previous unit's epilogue LDS reads are done
+    transform(smem);                           // step ks0 into V0
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int cc = 0; cc < CPW6; ++cc)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) acc[cc][e] = 0.f;
+    gload(ks0 + 1);                            // host: ks1 - ks0 >= 2
+    __syncthreads();
+    int ks = ks0;
+    // every wave: this step's MFMAs, then the next step's transform and the
+    // request of the one after.  (The fp32 MFMA does not co-issue with the VALU,
+    // so a SIMD's time is the sum in any order.  One order of loads on entry and
+    // around the loop keeps the compiler's vmcnt waits partial: the transform
+    // waits for its rows only, not for the B fragments requested after them.)
+    do {                                       // steps ks0 .. ks1-2
+      const float* Vc = smem + ((ks - ks0) & 1) * V6_FLOATS;
+      float* Vn = smem + (((ks - ks0) & 1) ^ 1) * V6_FLOATS;
+      const int k2 = min(ks + 2, ks1 - 1);
+#pragma unroll
+      for (int cc = 0; cc < CPW6; ++cc) comp(cc, Vc, ks, tn);
+      transform(Vn);
+      __builtin_amdgcn_sched_barrier(0);
+      gload(k2);
+      __syncthreads();
+    } while (++ks < ks1 - 1);
+    // ---- the last step, peeled (no prefetch past the unit)
+    const float* Vl = smem + ((ks - ks0) & 1) * V6_FLOATS;
+    const int cur_m0 = m0, cur_tn = tn, cur_s = s;
+    const int nu = u + G;
+    const bool more = nu < units;
+    unit(more ? nu : u, m0, tn, s, ks0, ks1);
+#pragma unroll
+    for (int cc = 0; cc < CPW6; ++cc) {
+      mfma_c(cc, Vl);
+      __builtin_amdgcn_sched_barrier(0);
+      if (cc + 3 < CPW6) bload(cc % 3, cc + 3, ks, cur_tn);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+
+    // ---- epilogue: four passes of 8 tiles
+    const int n_loc = 4 * (tid & 15);          // the epilogue thread's 4 channels in the unit
+    const int n4 = cur_tn * N6 + n_loc;
+    const int epx = (tid >> 4) & 15;           // its pixel of the tile: row epx >> 2, column epx & 3
+    const int et = tid >> 8;                   // its tiles in a pass: et, et + 2, et + 4, et + 6
+    constexpr bool RES = MODE == 0 && (EF & EF_RES), ACC = MODE == 0 && (EF & EF_ACC);
+    constexpr bool MB = MODE == 0 && (EF & EF_MB), Y2 = MODE == 0 && (EF & EF_Y2);
+    float4 bias4 = make_float4(0.f, 0.f, 0.f, 0.f);
+    if constexpr (MODE == 0) bias4 = bld4(rs_bias, (uint32_t)n4 * 4u);
+    // per pass parity: the pixels (MODE 1: workspace rows) of the thread's four
+    // tiles, their output mask, and the epilogue inputs
+    uint32_t epix[2][4], eok[2];
+    float4 pin[2][4];
+    uint32_t pm[2][4], pm2[2][4];
+    auto inputs = [&](int p) {
+      const int q = p & 1;
+      eok[q] = 0u;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        int b, ti, tj;
+        const bool tl = tile_point_magic(a, Ht, Wt, cur_m0 + TP6 * p + et + 2 * k, b, ti, tj);
+        const int i = 4 * ti + (epx >> 2), j = 4 * tj + (epx & 3);
+        const bool ok = tl && i < a.Hout && j < a.Wout;
+        eok[q] |= (ok ? 1u : 0u) << k;
+        epix[q][k] = MODE == 1 ? (uint32_t)b * a.mrows + (uint32_t)i * a.Wg + j
+                               : ((uint32_t)b * a.Hout + i) * a.Wout + j;
+        const uint32_t o = (epix[q][k] * (uint32_t)a.Cout_p + n4) * 4u;
+        const uint32_t wo = (epix[q][k] * (uint32_t)wpp + (uint32_t)(n4 >> 5)) * 4u;
+        if constexpr (RES) pin[q][k] = bld4(rsrc(a.res, dst_bytes), ok ? o : kOOB);
+        if constexpr (ACC) pin[q][k] = bld4(rs_out, ok ? o : kOOB);
+        if constexpr (MB) pm[q][k] = bld1(rsrc(a.mbits, bits_bytes), ok ? wo : kOOB);
+        if constexpr (Y2) pm2[q][k] = bld1(rsrc(a.m2bits, bits_bytes), ok ? wo : kOOB);
+      }
+    };
+    inputs(0);
+#pragma unroll
+    for (int p = 0; p < 4; ++p) {
+      const int q = p & 1;
+      __syncthreads();                         // the k-loop's / previous pass's LDS reads are done
+      {
+        // stage rows e = 4p .. 4p+3 of the wave's accumulators: row (e & 3) + 4h of the pass
+        // (column n of the unit's 64, the wave halves XOR-swizzled by 32 apart)
+        int wrow = 4 * h * N6 + ((32 * nbw + (lane & 31)) ^ (32 * h));
+        asm volatile("" : "+v"(wrow));
+#pragma unroll
+        for (int cc = 0; cc < CPW6; ++cc)
+#pragma unroll
+          for (int e4 = 0; e4 < 4; ++e4) M[((xq + cc) * TP6 + e4) * N6 + wrow] = acc[cc][4 * p + e4];
+      }
+      __syncthreads();
+      {
+        // inverse transform: thread (tile wave, channel lane) of the pass
+        int rd = wave_u * N6 + (lane ^ (32 * ((wave_u >> 2) & 1)));
+        asm volatile("" : "+v"(rd));
+        float z[6][4];
+#pragma unroll
+        for (int i = 0; i < 6; ++i) {
+          float m[6];
+#pragma unroll
+          for (int j = 0; j < 6; ++j) m[j] = M[(6 * i + j) * TP6 * N6 + rd];
+          at6(m[0], m[1], m[2], m[3], m[4], m[5], z[i]);
+        }
+        int wr = wave_u * 16 * N6 + lane;
+        asm volatile("" : "+v"(wr));
+#pragma unroll
+        for (int jj = 0; jj < 4; ++jj) {
+          float y[4];
+          at6(z[0][jj], z[1][jj], z[2][jj], z[3][jj], z[4][jj], z[5][jj], y);
+#pragma unroll
+          for (int ii = 0; ii < 4; ++ii) Yl[wr + (4 * ii + jj) * N6] = y[ii];
+        }
+      }
+      if (p < 3) inputs(p + 1);                // requested before this pass's stores
+      __syncthreads();
+      int rrow = (et * 16 + epx) * N6 + n_loc;
+      asm volatile("" : "+v"(rrow));
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const float4 v = *reinterpret_cast<const float4*>(Yl + rrow + 2 * k * 16 * N6);
+        const bool ok = (eok[q] >> k) & 1u;
+        const uint32_t pix = epix[q][k];
+        if constexpr (MODE == 1) {
+          const uint32_t o = (((uint32_t)cur_s * (uint32_t)a.M + pix) * (uint32_t)a.N + n4) * 4u;
+          bst4(v, rs_out, ok ? o : kOOB);
+        } else {
+          const uint32_t o = (pix * (uint32_t)a.Cout_p + n4) * 4u;
+          float x[4] = {v.x + bias4.x, v.y + bias4.y, v.z + bias4.z, v.w + bias4.w};
+#pragma unroll
+          for (int cch = 0; cch < 4; ++cch) x[cch] = po::leaky_or_id(x[cch], po::act_slope(a.act));
+          if constexpr (ACC) {
+            x[0] += pin[q][k].x; x[1] += pin[q][k].y; x[2] += pin[q][k].z; x[3] += pin[q][k].w;
+          }
+          float4 out = make_float4(x[0], x[1], x[2], x[3]);
+          if constexpr (MB) {
+            const float4 g = po::leaky_grad_bits(pm[q][k], n4);
+            out = make_float4(x[0] * g.x, x[1] * g.y, x[2] * g.z, x[3] * g.w);
+          }
+          if constexpr ((EF & EF_Y) != 0) bst4(out, rs_out, ok ? o : kOOB);
+          if constexpr (RES) {
+            const float4 rr = pin[q][k];
+            bst4(make_float4(x[0] + rr.x, x[1] + rr.y, x[2] + rr.z, x[3] + rr.w), rsrc(a.sum, dst_bytes), ok ? o : kOOB);
+          }
+          if constexpr (Y2) {
+            const float4 g2 = po::leaky_grad_bits(pm2[q][k], n4);
+            bst4(make_float4(x[0] * g2.x, x[1] * g2.y, x[2] * g2.z, x[3] * g2.w), rsrc(a.y2, dst_bytes), ok ? o : kOOB);
+          }
+          if constexpr ((EF & EF_YB) != 0) {
+            // sign bits: 8 lanes hold the 32 channels of one word (DPP row shifts, tile 70)
+            const uint32_t nib = ((out.x > 0.f ? 1u : 0u) | (out.y > 0.f ? 2u : 0u) | (out.z > 0.f ? 4u : 0u) |
+                                  (out.w > 0.f ? 8u : 0u)) & (0u - (uint32_t)ok);
+            uint32_t w = nib << (4 * (lane & 7));
+            w |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)w, 0x101, 0xF, 0xF, false);   // row_shl:1
+            w |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)w, 0x102, 0xF, 0xF, false);   // row_shl:2
+            w |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)w, 0x104, 0xF, 0xF, false);   // row_shl:4
+            bst1(w, rsrc(a.ybits, bits_bytes),
+                 (ok && (lane & 7) == 0) ? (pix * (uint32_t)wpp + (uint32_t)(n4 >> 5)) * 4u : kOOB);
+          }
+        }
+      }
+      if (p == 1) {
+        // the next unit's first input rows and B fragments (the last unit re-reads
+        // its own: branch-free), requested halfway through the epilogue: earlier,
+        // their 60 registers would sit beside the accumulators of passes 1-3
+        offsets(m0);
+        gload(ks0);
+#pragma unroll
+        for (int cc = 0; cc < 3; ++cc) bload(cc, cc, ks0, tn);
+      }
+    }
+    if (!more) break;
+    u = nu;
+  }
+}
+}  // namespace
+
+namespace po {
+// po_conv tile staging 16 (tile 71): conv_wino6_k, Winograd F(4x4,3x3) as a
+// persistent kernel (see above).
+int launch_wino6(const ConvArgs& a, const float* U6, hipStream_t st) {
+  PO_REQUIRE(U6, "po_conv: tile 71 needs the F(4x4,3x3) weights (Wwino6)");
+  PO_REQUIRE(a.prec == 0 && a.ntaps == 9 && a.tkw == 3 && (a.sdh == 1 || a.sdh == -1) && (a.sdw == 1 || a.sdw == -1) &&
+                 a.dh0 == -a.sdh && a.dw0 == -a.sdw,
+             "po_conv: Winograd tile needs a full 3x3 neighbourhood of taps");
+  PO_REQUIRE(a.in_step == 1 && a.out_step == 1 && a.out_oy == 0 && a.out_ox == 0 && !a.in_org && !a.out_org && !a.gbox,
+             "po_conv: tile 71 needs stride 1 on full maps without boxes");
+  PO_REQUIRE(a.Hg == a.Hout && a.Wg == a.Wout && a.Hin == a.Hout && a.Win == a.Wout,
+             "po_conv: Winograd tile needs source, grid and destination of one size");
+  PO_REQUIRE(!a.pool_y, "po_conv: tile 71 has no fused pool");
+  PO_REQUIRE(a.N % N6 == 0 && a.Cin_p % WK == 0, "po_conv: tile 71 needs N %% 64 == 0 and Cin_p %% 16 == 0");
+  PO_REQUIRE(a.Cin_p / WK >= 2 * a.ksplit, "po_conv: tile 71 needs at least two k-steps per slice");
+  PO_REQUIRE(a.ksplit == 1 || (a.ws && (int64_t)a.ksplit * a.M * a.N * 4 < (1LL << 31)),
+             "po_conv: tile 71 split-K needs a workspace of < 2^31 bytes");
+  PO_REQUIRE(!a.mask && !a.mask2 && !a.y_amax && !a.sum_amax && !a.y2_amax,
+             "po_conv: tile 71 takes leaky masks as sign bits and no max|x| slots");
+  PO_REQUIRE(!(a.res && a.accumulate), "po_conv: tile 71 does not accumulate a shortcut launch");
+  PO_REQUIRE(a.in_bytes < (1u << 30), "po_conv: tile 71 needs an input of < 2^30 bytes");
+  PO_REQUIRE((int64_t)a.N * NX6 * a.Cin_p * 4 < (1LL << 31), "po_conv: tile 71 weights too large");
+  PO_REQUIRE((int64_t)a.B * a.Hout * a.Wout * a.Cout_p * 4 < (1LL << 31),
+             "po_conv: tile 71 addresses the destination with 32-bit byte offsets (< 2^31 bytes)");
+  const int Ht = (a.Hout + 3) / 4, Wt = (a.Wout + 3) / 4;
+  ConvArgs b = a;
+  b.ntiles_n = a.N / N6;
+  div_magic(Ht * Wt, b.mg_tiles, b.sh_tiles);
+  div_magic(Wt, b.mg_wt, b.sh_wt);
+  const int ntm = ceil_div((int64_t)a.B * Ht * Wt, T6);
+  const int mn = ntm * b.ntiles_n;
+  div_magic(mn, b.mg_mn, b.sh_mn);
+  div_magic(b.ntiles_n, b.mg_ntn, b.sh_ntn);
+  div_magic(a.ksplit, b.mg_ks, b.sh_ks);
+  PO_REQUIRE((int64_t)mn * a.ksplit < (1LL << 31), "po_conv: too many tiles");
+  const int units = mn * a.ksplit;
+  const int ef = (a.y ? EF_Y : 0) | (a.res ? EF_RES : 0) | (a.accumulate ? EF_ACC : 0) | (a.mbits ? EF_MB : 0) |
+                 (a.y2 ? EF_Y2 : 0) | (a.ybits ? EF_YB : 0);
+  const void* k = nullptr;
+  // the epilogue-field combinations po_conv launches on full-map Winograd tiles
+#define PO_W6(MODE, EF)                                             \
+  case (MODE) * 64 + (EF):                                          \
+    k = reinterpret_cast<const void*>(conv_wino6_k<MODE, EF>);      \
+    break;
+  const int which = a.ksplit > 1 ? 64 : ef;
+  switch (which) {
+    PO_W6(1, 0)
+    PO_W6(0, EF_Y)
+    PO_W6(0, EF_Y | EF_YB)
+    PO_W6(0, EF_RES | EF_YB)
+    PO_W6(0, EF_Y | EF_RES)
+    PO_W6(0, EF_Y | EF_RES | EF_YB)
+    PO_W6(0, EF_Y | EF_ACC)
+    PO_W6(0, EF_Y | EF_MB)
+    PO_W6(0, EF_Y | EF_ACC | EF_MB)
+    PO_W6(0, EF_Y | EF_Y2)
+    PO_W6(0, EF_Y | EF_ACC | EF_Y2)
+    PO_W6(0, EF_Y | EF_MB | EF_Y2)
+    PO_W6(0, EF_Y | EF_ACC | EF_MB | EF_Y2)
+    default:
+      break;
+  }
+#undef PO_W6
+  PO_REQUIRE(k, "po_conv: tile 71 has no kernel for epilogue fields 0x%x", which);
+  const int resident = resident_groups_cached(k, 512);
+  const int grid = units < resident ? units : resident;
+  void* args[] = {&b, const_cast<float**>(&U6), const_cast<int*>(&Ht), const_cast<int*>(&Wt),
+                  const_cast<int*>(&units), const_cast<int*>(&mn)};
+  PO_REQUIRE(hipLaunchKernel(k, dim3(grid), dim3(512), args, 0, st) == hipSuccess, "po_conv: tile 71 launch failed");
+  return check_launch("po_conv (winograd F(4x4) persistent)");
+}
+}  // namespace po

@@ -570,7 +570,12 @@ class NetPlan:
         return desc.macs * pts / (desc.B * desc.Hg * desc.Wg)
 
     # Winograd tiles of po_conv: (tiles = GEMM rows, output channels) per workgroup
-    WINO_TILES = {61: (64, 32), 65: (32, 64), 66: (32, 64), 67: (64, 64), 68: (64, 64), 70: (64, 64)}   # 62-64 retired
+    WINO_TILES = {61: (64, 32), 65: (32, 64), 66: (32, 64), 67: (64, 64), 68: (64, 64), 70: (64, 64),
+                  71: (32, 64)}   # 62-64 retired
+    # output-tile side and transform components of each Winograd tile: F(2x2,3x3)
+    # (16), except tile 71, F(4x4,3x3) (36)
+    WINO_SIDE = {71: 4}
+    WINO_COMPS = {71: 36}
     HALO_TILE = 69               # conv_halo_pool_k (conv_halo.hip)
     _tile_shapes = {}
 
@@ -594,9 +599,11 @@ class NetPlan:
         are all dead exits before its first MFMA).
 
         * direct tiles: 2 * live M-tiles * BM * ceil(N/BN)*BN * ntaps * Cin_p;
-        * Winograd F(2x2,3x3) tiles (61-66): 2 * 16 * live workgroups * WT
+        * Winograd F(2x2,3x3) tiles (61-70): 2 * 16 * live workgroups * WT
           * Cin_p * N — 16 transform-domain GEMMs over the 2x2 output tiles,
-          4/9 of the direct-conv MFMA work of the same launch.
+          4/9 of the direct-conv MFMA work of the same launch; F(4x4,3x3)
+          (tile 71): 2 * 36 * live units * 32 4x4-tiles * Cin_p * N, 1/4 of
+          the direct work (9/16 of F(2x2)'s).
         Boxed launches (gbox) count the live rows of this step's boxes
         (conv_common.h grid_point / conv_wino.hip tile_point)."""
         if desc.prec != 0:
@@ -604,7 +611,7 @@ class NetPlan:
         t = desc.tile
         if t in cls.WINO_TILES:
             WT = cls.WINO_TILES[t][0]
-            return 2.0 * 16 * cls._live_tiles(desc, t, WT, cones) * WT * desc.Cin_p * desc.N
+            return 2.0 * cls.WINO_COMPS.get(t, 16) * cls._live_tiles(desc, t, WT, cones) * WT * desc.Cin_p * desc.N
         if t == cls.HALO_TILE:
             # conv_halo_pool_k: 8 x 16-pixel output tiles (ragged ones padded), 32
             # channels, K = 9 taps x 16 channels (full maps only: no boxes)
@@ -623,10 +630,11 @@ class NetPlan:
             boxes = cones[desc.cone_block, desc.cone_b0:desc.cone_b0 + desc.B].tolist()
         if t in cls.WINO_TILES:
             WT = cls.WINO_TILES[t][0]
-            Ht, Wt = (desc.Hg + 1) // 2, (desc.Wg + 1) // 2
+            q = cls.WINO_SIDE.get(t, 2)
+            Ht, Wt = -(-desc.Hg // q), -(-desc.Wg // q)
             per = Ht * Wt
             live = [per] * desc.B if boxes is None else [
-                min(max(((r1 + 1) >> 1) - (r0 >> 1), 0) * max(((c1 + 1) >> 1) - (c0 >> 1), 0), per)
+                min(max(-(-r1 // q) - r0 // q, 0) * max(-(-c1 // q) - c0 // q, 0), per)
                 for r0, c0, r1, c1 in boxes]
             return cls._live_groups(live, per, WT, desc.B)
         mrows = desc.mrows or desc.Hg * desc.Wg
@@ -828,9 +836,12 @@ class NetPlan:
         return self.net._dgrad_weight(wts_or_j, taps, cin_p, self.device)
 
     def _attach_wino(self, desc, w):
-        """Winograd F(2x2,3x3) weights (po_conv tile 61) of an exact-fp32
-        launch that is a stride-1 3x3 correlation on full maps."""
+        """Winograd weights of an exact-fp32 launch that is a stride-1 3x3
+        correlation on full maps: F(2x2,3x3) (po_conv_desc.Wwino, tiles
+        61-70) and, where N % 64 == 0, F(4x4,3x3) (Wwino6, tile 71;
+        ADVPATCH_WINO4X4=0: not built, so the tuner never picks tile 71)."""
         desc.Wwino = None
+        desc.Wwino6 = None
         if (desc.prec != 0 or desc.ntaps != 9 or desc.in_step != 1 or desc.out_step != 1 or desc.in_org
                 or desc.out_org or w.dim() != 3 or w.size(0) % 32 or w.size(2) % 16
                 or os.environ.get("ADVPATCH_WINOGRAD", "1") == "0"):
@@ -839,6 +850,8 @@ class NetPlan:
         if sorted(offs) != [(a, b) for a in (-1, 0, 1) for b in (-1, 0, 1)]:
             return
         desc.Wwino = self.net._wino(w, offs)
+        if w.size(0) % 64 == 0 and os.environ.get("ADVPATCH_WINO4X4", "1") != "0":
+            desc.Wwino6 = self.net._wino(w, offs, f4=True)
 
     # ---------------- launch lists ----------------
     def _build_ops(self):
@@ -1323,7 +1336,7 @@ class NetPlan:
     # ---------------- autotuning ----------------
     SPLITS = (2, 4, 8, 16, 32)
     WS_FLOATS = 64 << 20          # split-K workspace cap (256 MB)
-    WINO_SPLIT_TILES = (66, 67, 68, 70)   # Winograd tiles with split-K (conv_wino3_k, conv_wino4_k, conv_wino5_k)
+    WINO_SPLIT_TILES = (66, 67, 68, 70, 71)   # Winograd tiles with split-K (conv_wino3_k .. conv_wino6_k)
 
     def _ensure_ws(self, floats):
         if self.ws is None or self.ws.numel() < floats:
@@ -1682,6 +1695,31 @@ def wino_transform(w, offs):
     return U.view(16, C // 16, 2, 2, 4, N // 32, 32).permute(5, 1, 0, 3, 2, 6, 4).contiguous()
 
 
+# Winograd F(4x4,3x3) (Lavin; points 0, +-1, +-2, inf): U = G g G^T with this G,
+# the input transform B^T and inverse A^T as csrc/conv_wino6.hip's bt6 / at6
+_WINO6_G = ((1 / 4, 0.0, 0.0), (-1 / 6, -1 / 6, -1 / 6), (-1 / 6, 1 / 6, -1 / 6), (1 / 24, 1 / 12, 1 / 6),
+            (1 / 24, -1 / 12, 1 / 6), (0.0, 0.0, 1.0))
+WINO6_BT = ((4, 0, -5, 0, 1, 0), (0, -4, -4, 1, 1, 0), (0, 4, -4, -1, 1, 0), (0, -2, -1, 2, 1, 0),
+            (0, 2, -1, -2, 1, 0), (0, 4, 0, -5, 0, 1))
+WINO6_AT = ((1, 1, 1, 1, 1, 0), (0, 1, -1, 2, -2, 0), (0, 1, 1, 4, 4, 0), (0, 1, -1, 8, -8, 1))
+
+
+def wino6_transform(w, offs):
+    """po_conv_desc.Wwino6 of launch weights w [N][9][Cin_p] (fp32) whose tap
+    t reads source offset offs[t]: U = G g G^T (F(4x4,3x3), component xi =
+    6 i + j) in float64, rounded once to fp32, in MFMA fragment order
+    [N/32][Cin_p/16][36][2][64 lanes][4] (wino_transform's order with 36
+    components)."""
+    N, T, C = w.shape
+    assert T == 9 and N % 32 == 0 and C % 16 == 0
+    g = torch.zeros(N, C, 3, 3, dtype=torch.float64, device=w.device)
+    for t, (dh, dw) in enumerate(offs):
+        g[:, :, dh + 1, dw + 1] = w[:, t, :].double()
+    G = torch.tensor(_WINO6_G, dtype=torch.float64, device=w.device)
+    U = torch.einsum("xa,ncab,yb->xycn", G, g, G).reshape(36, C, N).float()        # [xi][c][n]
+    return U.view(36, C // 16, 2, 2, 4, N // 32, 32).permute(5, 1, 0, 3, 2, 6, 4).contiguous()
+
+
 class _DarknetFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, plan, nchw, roi=None, base=None):
@@ -1884,12 +1922,13 @@ class Darknet(nn.Module):
             self._frag[key] = (w16, f)          # keep w16 alive with its key
         return nat.c_void_p(self._frag[key][1].data_ptr())
 
-    def _wino(self, w, offs):
+    def _wino(self, w, offs, f4=False):
         """Device address of the Winograd weights of launch weights w with tap
-        offsets offs (wino_transform), built once per (weights, tap order)."""
-        key = (w.data_ptr(), tuple(offs))
+        offsets offs (wino_transform; f4: F(4x4,3x3), wino6_transform), built
+        once per (weights, tap order, form)."""
+        key = (w.data_ptr(), tuple(offs), bool(f4))
         if key not in self._frag:
-            self._frag[key] = (w, wino_transform(w, offs))      # keep w alive with its key
+            self._frag[key] = (w, (wino6_transform if f4 else wino_transform)(w, offs))   # keep w alive with its key
         return nat.c_void_p(self._frag[key][1].data_ptr())
 
     def _dev16(self, i):

@@ -33,7 +33,7 @@ typedef void* po_stream_t;
 #define PO_EHIP -2     /* HIP runtime error */
 #define PO_EDEVICE -3  /* device is not gfx950 */
 
-#define PO_ABI_VERSION 22
+#define PO_ABI_VERSION 23
 #define PO_AMAX_SUB 64  /* sub-slots per max|x| slot (see po_conv_desc) */
 
 int po_abi_version(void);
@@ -473,9 +473,15 @@ typedef struct po_conv_desc {
    * itself is not stored (darknet_v3.py:61-69 conv + maxpool pairs). */
   float* pool_y;
   int8_t* pool_argmax;
+  /* Optional (prec 0, tile 71, ABI 23): Winograd F(4x4,3x3) weights of this
+   * launch, U = G g G^T (Lavin's G for the points 0, +-1, +-2, inf) in
+   * float64 rounded to fp32, in MFMA fragment order [N/32][Cin_p/16][36
+   * components][2][64 lanes][4] (Wwino's order with 36 components).  NULL:
+   * tile 71 does not apply. */
+  const float* Wwino6;
 } po_conv_desc;
 
-#define PO_CONV_NTILES 70
+#define PO_CONV_NTILES 71
 /* Tile `t` (1-based): block rows BM (output pixels), block columns BN (output
  * channels), k-step BK (input channels).  Tiles 1..10 stage operands through
  * registers, 11..20 are the same shapes staged by LDS-DMA, 27 a 128x256
@@ -504,6 +510,11 @@ typedef struct po_conv_desc {
  * input rows, so they drain under its k-loop; full maps without boxes, at
  * least two k-steps per slice, leaky masks as sign bits, no max|x| slots;
  * bit-identical to 68.
+ * 71 (exact fp32, ABI 23) is the Winograd F(4x4,3x3) form of tile 70 (needs
+ * Wwino6): 32 4x4-tiles x 64 channels per unit, one 512-thread workgroup per
+ * CU walking the units; the same requirements as tile 70 and no fused pool.
+ * Not bit-identical to the F(2x2) tiles (a different exact-arithmetic
+ * factorisation); its error against float64 is tested per layer.
  * Retired tiles (21..26, 28, 62..64: never selected by a tuner run) keep their
  * numbers; po_conv_tile_info reports them with *prec = -1 and po_conv refuses
  * them.  A tile that does not apply to a launch makes po_conv return

@@ -31,7 +31,7 @@ def test_library_exports_every_header_symbol():
     for name in sorted(declared):
         assert hasattr(lib, name), "libadvpatch_hip.so does not export %s" % name
     assert declared == set(nat.symbols()), declared ^ set(nat.symbols())
-    assert lib.po_abi_version() == nat.PO_ABI_VERSION == 22
+    assert lib.po_abi_version() == nat.PO_ABI_VERSION == 23
 
 
 def test_conv_desc_struct_matches_header():
@@ -212,3 +212,32 @@ def test_warp_form_selection_and_sparse_ok(monkeypatch):
     monkeypatch.setenv("ADVPATCH_WARP", "sideways")
     with pytest.raises(ValueError):
         ld.PatchTransformer()
+
+
+def test_wino6_matrices_and_fragment_order():
+    """F(4x4,3x3) (tile 71): A^T [(G g G^T) * (B^T d B)] A is the 3x3
+    correlation of the 6x6 patch (float64), with G = darknet_v3._WINO6_G and
+    the B^T / A^T the kernel's bt6 / at6 implement; wino6_transform stores
+    U[xi][16 kc + 8 (l >> 5) + s][32 nb + (l & 31)] at [nb][kc][xi][s >> 2][l][s & 3]."""
+    import torch
+    dk = pkg_mod("darknet_v3")
+    G = torch.tensor(dk._WINO6_G, dtype=torch.float64)
+    BT = torch.tensor(dk.WINO6_BT, dtype=torch.float64)
+    AT = torch.tensor(dk.WINO6_AT, dtype=torch.float64)
+    gen = torch.Generator().manual_seed(0)
+    for _ in range(5):
+        d = torch.randn(6, 6, generator=gen, dtype=torch.float64)
+        g = torch.randn(3, 3, generator=gen, dtype=torch.float64)
+        ref = torch.stack([torch.stack([(d[i:i + 3, j:j + 3] * g).sum() for j in range(4)]) for i in range(4)])
+        out = AT @ ((G @ g @ G.T) * (BT @ d @ BT.T)) @ AT.T
+        assert float((out - ref).abs().max()) < 1e-12
+    N, C = 64, 32
+    w = torch.randn(N, 9, C, generator=gen)
+    offs = [(kh - 1, kw - 1) for kh in range(3) for kw in range(3)]
+    frag = dk.wino6_transform(w, offs).reshape(N // 32, C // 16, 36, 2, 64, 4)
+    g = torch.zeros(N, C, 3, 3, dtype=torch.float64)
+    for t, (dh, dw) in enumerate(offs):
+        g[:, :, dh + 1, dw + 1] = w[:, t, :].double()
+    U = torch.einsum("xa,ncab,yb->xycn", G, g, G).reshape(36, C, N).float()
+    for nb, kc, xi, l, s in ((1, 0, 35, 63, 7), (0, 1, 7, 5, 0), (1, 1, 20, 40, 5)):
+        assert frag[nb, kc, xi, s >> 2, l, s & 3] == U[xi, 16 * kc + 8 * (l >> 5) + s, 32 * nb + (l & 31)]

@@ -1,0 +1,172 @@
+"""po_conv tile 71 (conv_wino6_k, csrc/conv_wino6.hip): Winograd F(4x4,3x3)
+as a persistent kernel.  It is a different exact-arithmetic factorisation of
+the same convolution, so it is compared with float64 torch conv2d (and with
+the direct fp32 kernel's own error beside it), and its epilogues with tile
+70's on the same descriptor: both tap orientations, ragged 4x4 tiles on odd
+and non-multiple-of-4 map sides, every epilogue-field combination the plan
+launches, split-K slices (even and uneven), and the launches it refuses."""
+import ctypes
+
+import pytest
+import torch
+import torch.nn.functional as F
+
+from conftest import pkg_mod
+from test_gpu_wino import _desc, _rel, _setup
+from test_gpu_wino5 import MODES, _inputs
+
+pytestmark = pytest.mark.gpu
+DEV = torch.device("cuda", 0)
+# max-abs error relative to max|float64 output| of one F(4x4,3x3) layer (fp32
+# transforms and products; a numpy model of the same arithmetic gives ~8e-6 at
+# worst, ~8e-7 rms, against ~5e-7 / 1e-7 for the direct fp32 conv)
+TOL71 = 2e-5
+
+
+def _u6(wd, flip):
+    dk = pkg_mod("darknet_v3")
+    s = -1 if flip else 1
+    offs = [(s * (kh - 1), s * (kw - 1)) for kh in range(3) for kw in range(3)]
+    return dk.wino6_transform(wd, offs)
+
+
+def _conv(nat, tile, B, H, Cin, Cout, flip, xd, wd, bias, U, U6, ksplit=1):
+    y = torch.full((B, H, H, Cout), float("nan"), device=DEV)
+    d = _desc(nat, B, H, Cin, Cout, tile, flip)
+    d.Wwino, d.Wwino6 = U.data_ptr(), U6.data_ptr()
+    ws = None
+    if ksplit > 1:
+        ws = torch.full((ksplit * B * H * H * Cout,), float("nan"), device=DEV)
+        d.ksplit, d.workspace = ksplit, ws.data_ptr()
+    nat.call("po_conv", ctypes.byref(d), nat.ptr(xd), nat.ptr(wd), nat.ptr(bias), nat.ptr(y), None, None,
+             None, None, None, nat.stream())
+    torch.cuda.synchronize()
+    return y.permute(0, 3, 1, 2).cpu()
+
+
+@pytest.mark.parametrize("B,H,Cin,Cout,flip", [(3, 7, 96, 128, False), (3, 7, 96, 128, True), (2, 38, 256, 512, False),
+                                               (4, 19, 512, 256, True), (1, 76, 128, 64, False),
+                                               (2, 9, 32, 64, False), (2, 10, 64, 64, True), (16, 76, 128, 256, False),
+                                               (2, 13, 48, 192, False)])
+def test_tile71_matches_float64_conv(B, H, Cin, Cout, flip):
+    nat = pkg_mod("_native")
+    x, w, bias, wd, U = _setup(B, H, Cin, Cout, flip, seed=H * Cin + flip)
+    U6 = _u6(wd, flip)
+    ref = F.conv2d(x.double(), w.double(), bias.double(), padding=1)
+    xd = x.permute(0, 2, 3, 1).contiguous().to(DEV)
+    bd = bias.to(DEV)
+    outs = {t: _conv(nat, t, B, H, Cin, Cout, flip, xd, wd, bd, U, U6) for t in (71, 70, 1)}
+    assert not torch.isnan(outs[71]).any()
+    e = {t: _rel(o.double(), ref) for t, o in outs.items()}
+    print("F(4x4) %.3g  F(2x2) %.3g  direct %.3g (max-abs relative to float64)" % (e[71], e[70], e[1]))
+    assert e[71] < TOL71, e
+
+
+@pytest.mark.parametrize("mode", MODES)
+@pytest.mark.parametrize("B,H,Cin,Cout", [(2, 11, 64, 128), (3, 38, 256, 512), (2, 7, 32, 64), (16, 76, 128, 256)])
+def test_tile71_epilogues_match_tile70(mode, B, H, Cin, Cout):
+    """Each epilogue-field combination writes what tile 70 writes, up to the
+    two factorisations' rounding: values within TOL71 of the layer's max,
+    sign bits equal wherever the value is not within that rounding of zero,
+    untouched outputs untouched."""
+    from test_gpu_wino5 import _run
+    nat = pkg_mod("_native")
+    flip = mode.startswith("dgrad")
+    xd, wd, bias, U, prev, res, mbits, m2bits = _inputs(B, H, Cin, Cout, flip, seed=H + Cin)
+    U6 = _u6(wd, flip)
+    runs = {}
+    for t in (71, 70):
+        d_runs = _run_with(nat, t, mode, B, H, Cin, Cout, flip, U, U6, xd, wd, bias, prev, res, mbits, m2bits)
+        runs[t] = d_runs
+    (y1, s1, z1, b1), (y0, s0, z0, b0) = runs[71], runs[70]
+    for a, b in ((y1, y0), (s1, s0), (z1, z0)):
+        fin = torch.isfinite(b)
+        assert torch.equal(fin, torch.isfinite(a))
+        if fin.any():
+            scale = float(b[fin].abs().max())
+            assert float((a[fin] - b[fin]).abs().max()) <= TOL71 * max(scale, 1e-30), mode
+    if mode in ("fwd_bits", "fwd_shortcut"):
+        # sign bits: equal except at values within rounding of zero
+        ref = y0 if mode == "fwd_bits" else None
+        if ref is not None:
+            bits = lambda bt: ((bt.unsqueeze(-1) >> torch.arange(32, device=bt.device, dtype=torch.int32)) & 1)
+            bb1, bb0 = bits(b1).reshape(ref.shape), bits(b0).reshape(ref.shape)
+            tie = ref.abs() <= TOL71 * float(ref.abs().max())
+            assert torch.equal(bb1[~tie], bb0[~tie])
+
+
+def _run_with(nat, tile, mode, B, H, Cin, Cout, flip, U, U6, xd, wd, bias, prev, res, mbits, m2bits, ksplit=1):
+    from test_gpu_wino5 import _run
+    # tile 70's harness, with the F(4x4) weights attached for tile 71
+    orig = _desc
+    import test_gpu_wino5 as w5
+
+    def desc6(nat_, B_, H_, Cin_, Cout_, tile_, flip_=False):
+        d = orig(nat_, B_, H_, Cin_, Cout_, tile_, flip_)
+        d.Wwino6 = U6.data_ptr()
+        return d
+    w5._desc = desc6
+    try:
+        ws = torch.full((ksplit * B * H * H * Cout,), float("nan"), device=DEV) if ksplit > 1 else None
+        return _run(nat, tile, mode, B, H, Cin, Cout, flip, U, xd, wd, bias, prev, res, mbits, m2bits,
+                    ksplit=ksplit, ws=ws)
+    finally:
+        w5._desc = orig
+
+
+@pytest.mark.parametrize("Cin,ks", [(512, 2), (512, 3), (512, 4), (512, 6), (256, 3)])
+@pytest.mark.parametrize("mode", ["fwd_bits", "dgrad_acc_bits", "dgrad_dual"])
+def test_tile71_split_k(mode, Cin, ks):
+    """Split-K slices (raw partials, conv_reduce_k applies the epilogue) give
+    the one-slice result up to summation order: two evaluations each within
+    TOL71 of the exact value, so within 2 TOL71 of each other."""
+    nat = pkg_mod("_native")
+    B, H, Cout = 4, 19, 256
+    flip = mode.startswith("dgrad")
+    xd, wd, bias, U, prev, res, mbits, m2bits = _inputs(B, H, Cin, Cout, flip, seed=17)
+    U6 = _u6(wd, flip)
+    one = _run_with(nat, 71, mode, B, H, Cin, Cout, flip, U, U6, xd, wd, bias, prev, res, mbits, m2bits)
+    spl = _run_with(nat, 71, mode, B, H, Cin, Cout, flip, U, U6, xd, wd, bias, prev, res, mbits, m2bits, ksplit=ks)
+    for a, b in zip(spl[:3], one[:3]):
+        fin = torch.isfinite(b)
+        assert torch.equal(fin, torch.isfinite(a))
+        if fin.any():
+            assert float((a[fin] - b[fin]).abs().max()) <= 2 * TOL71 * float(b[fin].abs().max())
+
+
+def test_tile71_refuses_what_it_cannot_run():
+    nat = pkg_mod("_native")
+    B, H, Cin, Cout = 2, 16, 32, 64
+    xd, wd, bias, U, prev, res, mbits, m2bits = _inputs(B, H, Cin, Cout, False, seed=9)
+    U6 = _u6(wd, False)
+    y = torch.zeros(B, H, H, Cout, device=DEV)
+
+    def call(d, mask=None):
+        return nat.load().po_conv(ctypes.byref(d), nat.ptr(xd), nat.ptr(wd), None, nat.ptr(y), None, None,
+                                  nat.ptr(mask), None, None, nat.stream())
+
+    d = _desc(nat, B, H, Cin, Cout, 71)
+    assert call(d) != 0 and "Wwino6" in nat.last_error()
+    d.Wwino6 = U6.data_ptr()
+    assert call(d) == 0
+    box = torch.tensor([[0, 0, 8, 8]] * B, dtype=torch.int32, device=DEV)
+    d.gbox = box.data_ptr()
+    assert call(d) != 0 and "boxes" in nat.last_error()
+    d.gbox = None
+    slot = torch.zeros(64, dtype=torch.int32, device=DEV)
+    d.y_amax = slot.data_ptr()
+    assert call(d) != 0
+    d.y_amax = None
+    assert call(d, mask=prev) != 0
+    ws = torch.empty(4 * B * H * H * Cout, device=DEV)
+    d.ksplit, d.workspace = 2, ws.data_ptr()
+    assert call(d) != 0 and "two k-steps" in nat.last_error()
+    d.ksplit, d.workspace = 1, None
+    py = torch.zeros(B, H // 2, H // 2, Cout, device=DEV)
+    pam = torch.zeros(B, H // 2, H // 2, Cout, dtype=torch.int8, device=DEV)
+    d.pool_y, d.pool_argmax = py.data_ptr(), pam.data_ptr()
+    assert nat.load().po_conv(ctypes.byref(d), nat.ptr(xd), nat.ptr(wd), None, None, None, None, None, None, None,
+                              nat.stream()) != 0
+    d = _desc(nat, 2, 16, 32, 32, 71)                      # N = 32: not a multiple of 64
+    d.Wwino6 = U6.data_ptr()
+    assert call(d) != 0
