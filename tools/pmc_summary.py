@@ -1,17 +1,22 @@
-"""Summarise a tools/profile_round.sh output directory into profiles/.
+"""Summarise a tools/profile_round.sh output directory into profiles/, in
+steady state.
 
-Inputs: rocprofv3 csv output (kernel trace + stats, and the FETCH_SIZE and
-WRITE_SIZE counter passes) of `bench.py` with D = steps + warmup identical
-steps and no tuning launches.  Per kernel family (template arguments
-stripped) it writes calls per step, mean duration, time per step and HBM
-bytes per step.
+Inputs: rocprofv3 csv output of the same bench command at K=5 and K=25 timed
+steps (kernel trace + stats, and the FETCH_SIZE and WRITE_SIZE counter
+passes).  Every quantity is the K=25 run minus the K=5 run, divided by the
+2*20 steps between them (bench.py runs each timed step twice: plain and
+instrumented), so the one-time work of a run -- weight transforms, the
+float64 Winograd weights' hipBLASLt GEMMs, plan build, warm-up -- cancels and
+the per-step totals are those of the step itself.  Per kernel family
+(template arguments stripped): launches per step, mean duration, time per
+step and HBM bytes per step.
 
 HBM bytes follow MI355X_MICROARCH.md §HBM: FETCH_SIZE and WRITE_SIZE are in
 KiB; on gfx950 FETCH_SIZE reports half the bytes of wide (16 B/lane)
 coalesced reads, which is what every hot kernel here issues, so
     hbm_bytes = (2 * FETCH_SIZE + WRITE_SIZE) * 1024.
 
-usage: python tools/pmc_summary.py OUTDIR ROUND CONFIG BATCH NSTEPS [PREC]
+usage: python tools/pmc_summary.py OUTDIR ROUND CONFIG BATCH [PREC]
 """
 import csv
 import glob
@@ -23,6 +28,7 @@ import sys
 from collections import defaultdict
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+NSTEPS = 2 * (25 - 5)
 
 
 def family(name):
@@ -39,67 +45,83 @@ def rows(pattern, d):
     return out
 
 
+def bench_line(path):
+    if not os.path.exists(path):
+        return None
+    txt = [l for l in open(path).read().splitlines() if l.startswith("{")]
+    return json.loads(txt[-1]) if txt else None
+
+
 def main():
-    outdir, rnd, cfg, batch, nsteps = sys.argv[1], sys.argv[2], sys.argv[3], int(sys.argv[4]), int(sys.argv[5])
-    prec = sys.argv[6] if len(sys.argv) > 6 else "fp16x3"
-    trace = rows("*kernel_trace.csv", os.path.join(outdir, "trace"))
-    if not trace:
-        raise SystemExit("no kernel trace under %s" % outdir)
-    dur = defaultdict(list)
-    for r in trace:
-        dur[family(r["Kernel_Name"])].append(int(r["End_Timestamp"]) - int(r["Start_Timestamp"]))
+    outdir, rnd, cfg, batch = sys.argv[1], sys.argv[2], sys.argv[3], int(sys.argv[4])
+    prec = sys.argv[5] if len(sys.argv) > 5 else "fp32"
+    calls, ns = defaultdict(float), defaultdict(float)
+    for sign, k in ((-1, 5), (1, 25)):
+        tr = rows("*kernel_trace.csv", os.path.join(outdir, "trace_k%d" % k))
+        if not tr:
+            raise SystemExit("no kernel trace under %s/trace_k%d" % (outdir, k))
+        for r in tr:
+            f = family(r["Kernel_Name"])
+            calls[f] += sign
+            ns[f] += sign * (int(r["End_Timestamp"]) - int(r["Start_Timestamp"]))
     pmc = defaultdict(float)
-    for sub, ctr in (("pmc_fetch", "FETCH_SIZE"), ("pmc_write", "WRITE_SIZE")):
-        for r in rows("*counter_collection.csv", os.path.join(outdir, sub)):
-            if r.get("Counter_Name") == ctr:
-                pmc[(family(r["Kernel_Name"]), ctr)] += float(r["Counter_Value"])
-    fams = sorted(dur, key=lambda k: -sum(dur[k]))
+    have = {}
+    for sub, ctr in (("fetch", "FETCH_SIZE"), ("write", "WRITE_SIZE")):
+        for sign, k in ((-1, 5), (1, 25)):
+            rr = rows("*counter_collection.csv", os.path.join(outdir, "%s_k%d" % (sub, k)))
+            have[(sub, k)] = bool(rr)
+            for r in rr:
+                if r.get("Counter_Name") == ctr:
+                    pmc[(family(r["Kernel_Name"]), ctr)] += sign * float(r["Counter_Value"])
+    counters = all(have.values())
+    fams = sorted((f for f in calls if calls[f] > 0.5 or ns[f] > 0), key=lambda f: -ns[f])
     table = {}
-    for k in fams:
-        calls = len(dur[k])
-        fetch = pmc.get((k, "FETCH_SIZE"))
-        write = pmc.get((k, "WRITE_SIZE"))
-        hbm = None if fetch is None or write is None else (2.0 * fetch + write) * 1024.0 / nsteps
-        ms = sum(dur[k]) / 1e6 / nsteps
-        table[k] = {"calls_per_step": calls / nsteps, "mean_us": sum(dur[k]) / calls / 1e3, "ms_per_step": ms,
-                    "hbm_bytes_per_step": hbm,
-                    "fetch_size_kib_per_step": None if fetch is None else fetch / nsteps,
-                    "write_size_kib_per_step": None if write is None else write / nsteps,
-                    "hbm_GBps": None if hbm is None or ms == 0 else hbm / (ms * 1e-3) / 1e9}
+    for f in fams:
+        c = calls[f] / NSTEPS
+        ms = ns[f] / 1e6 / NSTEPS
+        fetch, write = pmc.get((f, "FETCH_SIZE")), pmc.get((f, "WRITE_SIZE"))
+        hbm = (2.0 * fetch + write) * 1024.0 / NSTEPS if counters and fetch is not None and write is not None else None
+        table[f] = {"calls_per_step": c, "mean_us": (ns[f] / calls[f] / 1e3) if calls[f] > 0 else None,
+                    "ms_per_step": ms, "hbm_bytes_per_step": hbm,
+                    "fetch_size_kib_per_step": None if fetch is None else fetch / NSTEPS,
+                    "write_size_kib_per_step": None if write is None else write / NSTEPS,
+                    "hbm_GBps": None if hbm is None or ms <= 0 else hbm / (ms * 1e-3) / 1e9}
     pdir = os.path.join(ROOT, "profiles", rnd)
     os.makedirs(pdir, exist_ok=True)
     tag = "%s_b%d_%s" % (cfg, batch, prec)
-    for f in glob.glob(os.path.join(outdir, "trace", "**", "*kernel_stats.csv"), recursive=True):
-        shutil.copy(f, os.path.join(pdir, "kernel_stats_%s.csv" % tag))
-    lines = ["# rocprofv3 summary, %s, bench.py --config %s --batch %d (%d identical steps incl. warm-up)" %
-             (rnd, cfg, batch, nsteps), "",
-             "Commands: `tools/profile_round.sh %s %s %d` (kernel trace + stats; FETCH_SIZE and WRITE_SIZE passes)."
-             % (rnd, cfg, batch),
+    for f in glob.glob(os.path.join(outdir, "trace_k25", "**", "*kernel_stats.csv"), recursive=True):
+        shutil.copy(f, os.path.join(pdir, "kernel_stats_%s_k25.csv" % tag))
+    wall = bench_line(os.path.join(outdir, "bench_trace_k25.json"))
+    lines = ["# rocprofv3 summary, %s, bench.py --config %s --batch %d --prec %s: steady state" % (rnd, cfg, batch, prec),
+             "",
+             "Commands: `tools/profile_round.sh %s %s %d %s` (kernel trace + stats, FETCH_SIZE and WRITE_SIZE passes, "
+             "each at K=5 and K=25 timed steps); per step = (K=25 run - K=5 run) / %d steps, so one-time launches "
+             "(weight transforms, plan build, warm-up) cancel." % (rnd, cfg, batch, prec, NSTEPS),
              "HBM bytes = (2*FETCH_SIZE + WRITE_SIZE) * 1024 (gfx950 FETCH_SIZE half-count correction, "
              "MI355X_MICROARCH.md §HBM).", "",
-             "| kernel family | calls/step | mean us | ms/step | HBM MB/step | HBM GB/s |", "|---|---|---|---|---|---|"]
-    for k in fams:
-        t = table[k]
+             "| kernel family | launches/step | mean us | ms/step | HBM MB/step | HBM GB/s |", "|---|---|---|---|---|---|"]
+    for f in fams:
+        t = table[f]
         mb = "-" if t["hbm_bytes_per_step"] is None else "%.1f" % (t["hbm_bytes_per_step"] / 1e6)
         gb = "-" if t["hbm_GBps"] is None else "%.0f" % t["hbm_GBps"]
-        lines.append("| %s | %.2f | %.1f | %.3f | %s | %s |" % (k, t["calls_per_step"], t["mean_us"], t["ms_per_step"],
-                                                               mb, gb))
+        mu = "-" if t["mean_us"] is None else "%.1f" % t["mean_us"]
+        lines.append("| %s | %.2f | %s | %.3f | %s | %s |" % (f, t["calls_per_step"], mu, t["ms_per_step"], mb, gb))
     tot = sum(t["ms_per_step"] for t in table.values())
-    lines += ["", "GPU kernel time per step: %.3f ms" % tot]
-    for f in ("bench_plain.json", "bench_trace.json"):
-        p = os.path.join(outdir, f)
-        if os.path.exists(p):
-            txt = [l for l in open(p).read().splitlines() if l.startswith("{")]
-            if txt:
-                lines += ["", "%s:" % f, "```", txt[-1], "```"]
+    lines += ["", "GPU kernel time per step (steady state): %.3f ms" % tot]
+    if wall is not None:
+        lines += ["Wall time per step of the same run (bench.py `ms_per_step`, profiler attached): %.3f ms"
+                  % wall["ms_per_step"]]
+        if tot > wall["ms_per_step"] * 1.005:
+            lines += ["WARNING: the kernel total exceeds the wall step (the difference did not cancel the setup)."]
+        lines += ["", "bench_trace_k25.json:", "```", json.dumps(wall), "```"]
     with open(os.path.join(pdir, "summary_%s.md" % tag), "w") as fh:
         fh.write("\n".join(lines) + "\n")
     conv = [table[k] for k in table if k.startswith("conv_") and k.endswith("_k")]
     hb = [t["hbm_bytes_per_step"] for t in conv]
     with open(os.path.join(ROOT, "profiles", "traffic_%s.json" % tag), "w") as fh:
-        json.dump({"round": rnd, "prec": prec,
-                   "kernel": "po_conv launches of one step (conv_k / conv_h3*_k tile families + split-K reduce)",
-                   "conv_hbm_bytes_per_step": None if None in hb else sum(hb),
+        json.dump({"round": rnd, "prec": prec, "steady_state": True,
+                   "kernel": "po_conv launches of one step (conv_* tile families + split-K reduce)",
+                   "conv_hbm_bytes_per_step": None if (not hb or None in hb) else sum(hb),
                    "conv_ms_per_step": sum(t["ms_per_step"] for t in conv),
                    "conv_calls_per_step": sum(t["calls_per_step"] for t in conv),
                    "families": table}, fh, indent=1)
