@@ -51,7 +51,6 @@ constexpr int NX6 = 36;                     // transform components
 constexpr int CPW6 = 9;                     // components per wave
 constexpr int V6_FLOATS = NX6 * T6 * WK;    // one transformed-input buffer (73,728 B)
 constexpr int TP6 = 8;                      // tiles per epilogue pass
-constexpr int Y6_OFF = NX6 * TP6 * N6;      // LDS floats of one pass's staged accumulators; its outputs follow
 
 // V[xi][tile][16 channels]: 16-byte chunk `chunk` of tile t, swizzled by tile
 __device__ __forceinline__ int v6idx(int xi, int t, int chunk) {
@@ -70,6 +69,18 @@ __device__ __forceinline__ void bt6(float d0, float d1, float d2, float d3, floa
   r[4] = __builtin_fmaf(-2.f, e, c);
   r[5] = __builtin_fmaf(4.f, d1, __builtin_fmaf(-5.f, d3, d5));
 }
+// bt6 on pairs (v_pk_fma_f32 / v_pk_add_f32): the same operations per element
+__device__ __forceinline__ void bt6v(f2v d0, f2v d1, f2v d2, f2v d3, f2v d4, f2v d5, f2v* r) {
+  const f2v m4 = {-4.f, -4.f}, p4 = {4.f, 4.f}, m5 = {-5.f, -5.f}, p2 = {2.f, 2.f}, m2 = {-2.f, -2.f};
+  const f2v a = __builtin_elementwise_fma(m4, d2, d4), b = __builtin_elementwise_fma(m4, d1, d3);
+  const f2v c = d4 - d2, e = d3 - d1;
+  r[0] = __builtin_elementwise_fma(p4, d0, __builtin_elementwise_fma(m5, d2, d4));
+  r[1] = a + b;
+  r[2] = a - b;
+  r[3] = __builtin_elementwise_fma(p2, e, c);
+  r[4] = __builtin_elementwise_fma(m2, e, c);
+  r[5] = __builtin_elementwise_fma(p4, d1, __builtin_elementwise_fma(m5, d3, d5));
+}
 // 1-D inverse y = A^T m (rows 1 1 1 1 1 0 / 0 1 -1 2 -2 0 / 0 1 1 4 4 0 / 0 1 -1 8 -8 1)
 __device__ __forceinline__ void at6(float m0, float m1, float m2, float m3, float m4, float m5, float* y) {
   const float p = m1 + m2, q = m1 - m2, r = m3 + m4, s = m3 - m4;
@@ -78,6 +89,24 @@ __device__ __forceinline__ void at6(float m0, float m1, float m2, float m3, floa
   y[2] = __builtin_fmaf(4.f, r, p);
   y[3] = __builtin_fmaf(8.f, s, q) + m5;
 }
+
+#ifdef PO_W6_STAMP
+// diagnostic build only (tools/w6_phases.py): per workgroup, shader cycles
+// (s_memtime) summed over its units per phase -- [0] unit top through the
+// k-loop, [1] the peeled last step, [2] the epilogue passes -- [3] units,
+// [4]/[5] s_memrealtime at start / end
+__device__ unsigned long long g_w6_stamp[1 << 12][8];
+#define PO_W6_T(v) v = __builtin_amdgcn_s_memtime()
+#else
+#define PO_W6_T(v) do { } while (0)
+#endif
+
+#ifdef PO_W6_NOSTORE
+// diagnostic build only: the epilogue's global stores removed (what the stores cost)
+#define W6ST(x) do { } while (0)
+#else
+#define W6ST(x) x
+#endif
 
 template <int MODE, int EF>   // MODE 0: po_conv epilogue (fields EF), 1: raw split-K partials
 __global__ __launch_bounds__(512, 1) void conv_wino6_k(const ConvArgs a, const float* __restrict__ U, int Ht, int Wt,
@@ -137,46 +166,72 @@ __global__ __launch_bounds__(512, 1) void conv_wino6_k(const ConvArgs a, const f
 #pragma unroll
     for (int j = 0; j < 6; ++j) okm |= ((unsigned)(x0 + j) < (unsigned)a.Win ? 1u : 0u) << (8 + j);
   };
-  float d[36];
+  f2v d[18];                                   // d[3 i + jp] = patch row i, columns 2jp, 2jp+1
   auto gload = [&](int ks) {
     const uint32_t cb = (uint32_t)__builtin_amdgcn_readfirstlane(ks * (WK * 4));
     // opaque per call: hoisted out of the k-loop, the per-load selects would hold
     // 36 registers across it
     uint32_t rb = rbase, om = okm;
     asm volatile("" : "+v"(rb), "+v"(om));
-    const bool c0 = (om >> 8) & 1u;
+    auto rows = [&](bool cols_all) {
+      const bool c0 = cols_all || ((om >> 8) & 1u);
 #pragma unroll
-    for (int i = 0; i < 6; ++i) {
-      const bool rok = (om >> i) & 1u;
-      const uint32_t rr = i == 0 ? rb - row_bytes : rb;
-      const uint32_t rv = rok ? rr : kOOB;                            // columns 1..5
-      const uint32_t rv0 = (rok && c0) ? rr - pix_bytes : kOOB;       // column 0
+      for (int i = 0; i < 6; ++i) {
+        const bool rok = (om >> i) & 1u;
+        const uint32_t rr = i == 0 ? rb - row_bytes : rb;
+        const uint32_t rv = rok ? rr : kOOB;                            // columns 1..5
+        const uint32_t rv0 = (rok && c0) ? rr - pix_bytes : kOOB;       // column 0
 #pragma unroll
-      for (int j = 0; j < 6; ++j) {
-        const uint32_t vo = j == 0 ? rv0 : (((om >> (8 + j)) & 1u) ? rv : kOOB);
-        const uint32_t so = cb + (i == 0 ? 0u : (uint32_t)(i - 1) * row_bytes) + (j == 0 ? 0u : (uint32_t)(j - 1) * pix_bytes);
-        d[6 * i + j] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(in_rs, vo, so, 0));
+        for (int j = 0; j < 6; ++j) {
+          const uint32_t vo = j == 0 ? rv0 : ((cols_all || ((om >> (8 + j)) & 1u)) ? rv : kOOB);
+          const uint32_t so = cb + (i == 0 ? 0u : (uint32_t)(i - 1) * row_bytes) + (j == 0 ? 0u : (uint32_t)(j - 1) * pix_bytes);
+          d[3 * i + (j >> 1)][j & 1] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(in_rs, vo, so, 0));
+        }
       }
-    }
+    };
+    // a wave whose 4 tiles all lie inside the map's columns (most of them) skips
+    // the per-load column selects (the same 36 loads either way)
+    if (__all(((om >> 8) & 0x3Fu) == 0x3Fu)) rows(true);
+    else rows(false);
   };
-  // V = B^T d B: the columns, then the rows; component xi = 6 i + j
+  // V = B^T d B on column pairs / row pairs (packed f32): the columns (pairs of
+  // columns), a 2x2 transposition of every block, then the rows (pairs of rows);
+  // component xi = 6 i + j.  The same operations as bt6 lane by lane.
   auto transform = [&](float* Vb) {
-    float t[6][6];
+#ifdef PO_W6_ABL_NOVWRITE
+    return;                                    // diagnostic only (wrong results): no transform, no V writes
+#endif
+#ifdef PO_W6_ABL_NOTRANS
+    // diagnostic only (wrong results): the raw rows written as they are, no transform VALU
+    {
+      float* dst = Vb + v6idx(0, r, c >> 2) + (c & 3);
 #pragma unroll
-    for (int j = 0; j < 6; ++j) {
-      float col[6];
-      bt6(d[j], d[6 + j], d[12 + j], d[18 + j], d[24 + j], d[30 + j], col);
+      for (int xi = 0; xi < 36; ++xi) dst[xi * T6 * WK] = d[xi >> 1][xi & 1];
+      return;
+    }
+#endif
+    f2v t[6][3];                               // t[i][jp]: (B^T d)[i][2jp], [i][2jp+1]
 #pragma unroll
-      for (int i = 0; i < 6; ++i) t[i][j] = col[i];
-      __builtin_amdgcn_sched_barrier(0);     // one column at a time: d's registers turn into t's
+    for (int jp = 0; jp < 3; ++jp) {
+      f2v col[6];
+      bt6v(d[jp], d[3 + jp], d[6 + jp], d[9 + jp], d[12 + jp], d[15 + jp], col);
+#pragma unroll
+      for (int i = 0; i < 6; ++i) t[i][jp] = col[i];
+      __builtin_amdgcn_sched_barrier(0);     // one column pair at a time: d's registers turn into t's
     }
     float* dst = Vb + v6idx(0, r, c >> 2) + (c & 3);
 #pragma unroll
-    for (int i = 0; i < 6; ++i) {
-      float e[6];
-      bt6(t[i][0], t[i][1], t[i][2], t[i][3], t[i][4], t[i][5], e);
+    for (int ip = 0; ip < 3; ++ip) {
+      f2v rw[6];                               // (t[2ip][j], t[2ip+1][j])
 #pragma unroll
-      for (int j = 0; j < 6; ++j) dst[(6 * i + j) * T6 * WK] = e[j];     // v6idx(xi, r, .) = v6idx(0, r, .) + xi*T6*WK
+      for (int j = 0; j < 6; ++j) rw[j] = f2v{t[2 * ip][j >> 1][j & 1], t[2 * ip + 1][j >> 1][j & 1]};
+      f2v e[6];
+      bt6v(rw[0], rw[1], rw[2], rw[3], rw[4], rw[5], e);
+#pragma unroll
+      for (int j = 0; j < 6; ++j) {
+        dst[(6 * (2 * ip) + j) * T6 * WK] = e[j][0];     // v6idx(xi, r, .) = v6idx(0, r, .) + xi*T6*WK
+        dst[(6 * (2 * ip + 1) + j) * T6 * WK] = e[j][1];
+      }
       __builtin_amdgcn_sched_barrier(0);
     }
   };
@@ -187,32 +242,45 @@ __global__ __launch_bounds__(512, 1) void conv_wino6_k(const ConvArgs a, const f
   const uint32_t u_lane = (uint32_t)lane * 16u;
   float4 bq[3][2];
   auto bload = [&](int slot, int cc, int ks, int tnn) {
+#ifdef PO_W6_ABL_UHOT
+    // diagnostic only (wrong results): every B fragment from one block, always cache-hot
+    const uint32_t blk = (uint32_t)__builtin_amdgcn_readfirstlane((nbw * NX6 + xq + cc) * 512 * 4) * 0u;
+#else
     const uint32_t blk = (uint32_t)__builtin_amdgcn_readfirstlane(
         ((((2 * tnn + nbw) * kc_n + ks) * NX6 + xq + cc) * 512) * 4);
+#endif
     bq[slot][0] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(u_rs, u_lane, blk, 0));
     bq[slot][1] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(u_rs, u_lane + 1024u, blk, 0));
   };
   floatx16 acc[CPW6];
-  auto mfma_c = [&](int cc, const float* Vb) {
-    // chunks 2h and 2h + 1 of tile lane & 31: their swizzled positions differ in bit 0
-    const int o0 = v6idx(xq, lane & 31, 2 * h), o1 = o0 ^ 4;
-    const float4 a0 = *reinterpret_cast<const float4*>(Vb + o0 + cc * T6 * WK);
-    const float4 a1 = *reinterpret_cast<const float4*>(Vb + o1 + cc * T6 * WK);
-    const float av[8] = {a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w};
-    const float4 b0 = bq[cc % 3][0], b1 = bq[cc % 3][1];
-    const float bv[8] = {b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, b1.z, b1.w};
+  // the wave's 9 components of one k-step: component cc's MFMAs, each half's A
+  // fragment of component cc + 1 read from LDS as soon as its registers are
+  // free (after the 4 MFMAs that use them), and the ring slot cc frees refilled
+  // with component cc + 3 (this k-step) or cc - 6 (the next; not on the last step)
+  auto comps = [&](const float* Vb, int ks, int tnn, bool last) {
+    const int o0 = v6idx(xq, lane & 31, 2 * h), o1 = o0 ^ 4;     // chunks 2h, 2h + 1: swizzled apart in bit 0
+    float4 a0 = *reinterpret_cast<const float4*>(Vb + o0);
+    float4 a1 = *reinterpret_cast<const float4*>(Vb + o1);
 #pragma unroll
-    for (int s8 = 0; s8 < 8; ++s8)             // MFMA step s, half h <-> channel 8h + s
-      acc[cc] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[s8], bv[s8], acc[cc], 0, 0, 0);
-  };
-  // component cc's MFMAs, then the ring slot it freed gets component cc + 3 (this
-  // k-step) or cc - 6 (the next one)
-  auto comp = [&](int cc, const float* Vb, int ks, int tnn) {
-    mfma_c(cc, Vb);
-    __builtin_amdgcn_sched_barrier(0);
-    if (cc + 3 < CPW6) bload(cc % 3, cc + 3, ks, tnn);
-    else bload(cc % 3, cc - 6, ks + 1, tnn);
-    __builtin_amdgcn_sched_barrier(0);
+    for (int cc = 0; cc < CPW6; ++cc) {
+      const float4 b0 = bq[cc % 3][0], b1 = bq[cc % 3][1];
+      acc[cc] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0.x, b0.x, acc[cc], 0, 0, 0);   // step s <-> channel 8h + s
+      acc[cc] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0.y, b0.y, acc[cc], 0, 0, 0);
+      acc[cc] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0.z, b0.z, acc[cc], 0, 0, 0);
+      acc[cc] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0.w, b0.w, acc[cc], 0, 0, 0);
+      __builtin_amdgcn_sched_barrier(0);
+      if (cc + 1 < CPW6) a0 = *reinterpret_cast<const float4*>(Vb + o0 + (cc + 1) * T6 * WK);
+      __builtin_amdgcn_sched_barrier(0);
+      acc[cc] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1.x, b1.x, acc[cc], 0, 0, 0);
+      acc[cc] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1.y, b1.y, acc[cc], 0, 0, 0);
+      acc[cc] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1.z, b1.z, acc[cc], 0, 0, 0);
+      acc[cc] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1.w, b1.w, acc[cc], 0, 0, 0);
+      __builtin_amdgcn_sched_barrier(0);
+      if (cc + 1 < CPW6) a1 = *reinterpret_cast<const float4*>(Vb + o1 + (cc + 1) * T6 * WK);
+      if (cc + 3 < CPW6) bload(cc % 3, cc + 3, ks, tnn);
+      else if (!last) bload(cc % 3, cc - 6, ks + 1, tnn);
+      __builtin_amdgcn_sched_barrier(0);
+    }
   };
 
   // ---- the unit loop
@@ -224,10 +292,111 @@ __global__ __launch_bounds__(512, 1) void conv_wino6_k(const ConvArgs a, const f
 #pragma unroll
   for (int cc = 0; cc < 3; ++cc) bload(cc, cc, ks0, tn);
   float* const M = smem;
-  float* const Yl = smem + Y6_OFF;
+  // ---- epilogue state.  The epilogue runs in four passes of 8 tiles; passes 0
+  // and 1 emit at once, passes 2 and 3 leave their outputs in LDS (the V1 buffer,
+  // free until the next unit's first k-step ends) and emit after the next
+  // unit's first transform, so their stores drain under its first MFMAs.
+  const int n_loc = 4 * (tid & 15);            // the emitting thread's 4 channels in the unit
+  const int epx = (tid >> 4) & 15;             // its pixel of a tile: row epx >> 2, column epx & 3
+  const int et = tid >> 8;                     // its tiles of a pass: et, et + 2, et + 4, et + 6
+  constexpr bool RES = MODE == 0 && (EF & EF_RES), ACC = MODE == 0 && (EF & EF_ACC);
+  constexpr bool MB = MODE == 0 && (EF & EF_MB), Y2 = MODE == 0 && (EF & EF_Y2);
+  int n4 = 0, es = 0;                          // the staged unit's channel base and split-K slice
+  float4 bias4 = make_float4(0.f, 0.f, 0.f, 0.f);
+  // per pass parity: pixels (MODE 1: workspace rows) of the thread's four tiles,
+  // their output mask (0: nothing staged yet), and the epilogue inputs
+  uint32_t epix[2][4], eok[2] = {0u, 0u};
+  float4 pin[2][4];
+  uint32_t pm[2][4], pm2[2][4];
+#pragma unroll
+  for (int q = 0; q < 2; ++q)
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      epix[q][k] = pm[q][k] = pm2[q][k] = 0u;
+      pin[q][k] = make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+  int cur_m0 = 0;
+  auto inputs = [&](int p) {
+    const int q = p & 1;
+    eok[q] = 0u;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      int b, ti, tj;
+      const bool tl = tile_point_magic(a, Ht, Wt, cur_m0 + TP6 * p + et + 2 * k, b, ti, tj);
+      const int i = 4 * ti + (epx >> 2), j = 4 * tj + (epx & 3);
+      const bool ok = tl && i < a.Hout && j < a.Wout;
+      eok[q] |= (ok ? 1u : 0u) << k;
+      epix[q][k] = MODE == 1 ? (uint32_t)b * a.mrows + (uint32_t)i * a.Wg + j
+                             : ((uint32_t)b * a.Hout + i) * a.Wout + j;
+      const uint32_t o = (epix[q][k] * (uint32_t)a.Cout_p + n4) * 4u;
+      const uint32_t wo = (epix[q][k] * (uint32_t)wpp + (uint32_t)(n4 >> 5)) * 4u;
+      if constexpr (RES) pin[q][k] = bld4(rsrc(a.res, dst_bytes), ok ? o : kOOB);
+      if constexpr (ACC) pin[q][k] = bld4(rs_out, ok ? o : kOOB);
+      if constexpr (MB) pm[q][k] = bld1(rsrc(a.mbits, bits_bytes), ok ? wo : kOOB);
+      if constexpr (Y2) pm2[q][k] = bld1(rsrc(a.m2bits, bits_bytes), ok ? wo : kOOB);
+    }
+  };
+  // outputs of pass p of the staged unit from its LDS slot (every store
+  // unconditional: a masked one goes out of range)
+  auto emit = [&](int p) {
+    const int q = p & 1;
+    int rrow = V6_FLOATS + q * (TP6 * 16 * N6) + (et * 16 + epx) * N6 + n_loc;
+    asm volatile("" : "+v"(rrow));
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const float4 v = *reinterpret_cast<const float4*>(smem + rrow + 2 * k * 16 * N6);
+      const bool ok = (eok[q] >> k) & 1u;
+      const uint32_t pix = epix[q][k];
+      if constexpr (MODE == 1) {
+        const uint32_t o = (((uint32_t)es * (uint32_t)a.M + pix) * (uint32_t)a.N + n4) * 4u;
+        W6ST(bst4(v, rs_out, ok ? o : kOOB));
+      } else {
+        const uint32_t o = (pix * (uint32_t)a.Cout_p + n4) * 4u;
+        float x[4] = {v.x + bias4.x, v.y + bias4.y, v.z + bias4.z, v.w + bias4.w};
+#pragma unroll
+        for (int cch = 0; cch < 4; ++cch) x[cch] = po::leaky_or_id(x[cch], po::act_slope(a.act));
+        if constexpr (ACC) {
+          x[0] += pin[q][k].x; x[1] += pin[q][k].y; x[2] += pin[q][k].z; x[3] += pin[q][k].w;
+        }
+        float4 out = make_float4(x[0], x[1], x[2], x[3]);
+        if constexpr (MB) {
+          const float4 g = po::leaky_grad_bits(pm[q][k], n4);
+          out = make_float4(x[0] * g.x, x[1] * g.y, x[2] * g.z, x[3] * g.w);
+        }
+        if constexpr ((EF & EF_Y) != 0) W6ST(bst4(out, rs_out, ok ? o : kOOB));
+        if constexpr (RES) {
+          const float4 rr = pin[q][k];
+          W6ST(bst4(make_float4(x[0] + rr.x, x[1] + rr.y, x[2] + rr.z, x[3] + rr.w), rsrc(a.sum, dst_bytes), ok ? o : kOOB));
+        }
+        if constexpr (Y2) {
+          const float4 g2 = po::leaky_grad_bits(pm2[q][k], n4);
+          W6ST(bst4(make_float4(x[0] * g2.x, x[1] * g2.y, x[2] * g2.z, x[3] * g2.w), rsrc(a.y2, dst_bytes), ok ? o : kOOB));
+        }
+        if constexpr ((EF & EF_YB) != 0) {
+          // sign bits: 8 lanes hold the 32 channels of one word (DPP row shifts, tile 70)
+          const uint32_t nib = ((out.x > 0.f ? 1u : 0u) | (out.y > 0.f ? 2u : 0u) | (out.z > 0.f ? 4u : 0u) |
+                                (out.w > 0.f ? 8u : 0u)) & (0u - (uint32_t)ok);
+          uint32_t w = nib << (4 * (lane & 7));
+          w |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)w, 0x101, 0xF, 0xF, false);   // row_shl:1
+          w |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)w, 0x102, 0xF, 0xF, false);   // row_shl:2
+          w |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)w, 0x104, 0xF, 0xF, false);   // row_shl:4
+          W6ST(bst1(w, rsrc(a.ybits, bits_bytes),
+                    (ok && (lane & 7) == 0) ? (pix * (uint32_t)wpp + (uint32_t)(n4 >> 5)) * 4u : kOOB));
+        }
+      }
+    }
+  };
+#ifdef PO_W6_STAMP
+  unsigned long long ph[3] = {0, 0, 0}, t0 = 0, t1 = 0, t2 = 0, t3 = 0, nunits = 0;
+  const unsigned long long rt0 = __builtin_amdgcn_s_memrealtime();
+#endif
   for (;;) {
-    __syncthreads();                           // the previous unit's epilogue LDS reads are done
+    PO_W6_T(t0);
+    __syncthreads();                           // the previous unit's LDS traffic is done
     transform(smem);                           // step ks0 into V0
+    __builtin_amdgcn_sched_barrier(0);
+    emit(2);                                   // the previous unit's last two passes (masked on the first)
+    emit(3);
     __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
     for (int cc = 0; cc < CPW6; ++cc)
@@ -240,70 +409,44 @@ __global__ __launch_bounds__(512, 1) void conv_wino6_k(const ConvArgs a, const f
     // request of the one after.  (The fp32 MFMA does not co-issue with the VALU,
     // so a SIMD's time is the sum in any order.  One order of loads on entry and
     // around the loop keeps the compiler's vmcnt waits partial: the transform
-    // waits for its rows only, not for the B fragments requested after them.)
+    // waits for its rows only, not for the B fragments requested after them.
+    // Staggering the two waves of a SIMD as tile 70 does -- waves 4-7
+    // transforming before their MFMAs -- measured 7 % slower per k-step here.)
+    // Per k-step at 19^2 512->1024 (tools/w6_phases.py): 13.3k shader
+    // cycles against the 9.2k MFMA floor; the row loads ~1.9k, the transform's
+    // VALU ~0.9k, the V writes ~1k, the workgroup barrier the rest.
     do {                                       // steps ks0 .. ks1-2
       const float* Vc = smem + ((ks - ks0) & 1) * V6_FLOATS;
       float* Vn = smem + (((ks - ks0) & 1) ^ 1) * V6_FLOATS;
       const int k2 = min(ks + 2, ks1 - 1);
-#pragma unroll
-      for (int cc = 0; cc < CPW6; ++cc) comp(cc, Vc, ks, tn);
+      comps(Vc, ks, tn, false);
       transform(Vn);
       __builtin_amdgcn_sched_barrier(0);
-      gload(k2);
+#ifndef PO_W6_ABL_NOGLOAD
+      gload(k2);                               // (diagnostic builds: optionally not)
+#endif
+#ifndef PO_W6_ABL_NOBAR
       __syncthreads();
+#endif
     } while (++ks < ks1 - 1);
     // ---- the last step, peeled (no prefetch past the unit)
+    PO_W6_T(t1);
     const float* Vl = smem + ((ks - ks0) & 1) * V6_FLOATS;
-    const int cur_m0 = m0, cur_tn = tn, cur_s = s;
+    cur_m0 = m0;
+    const int cur_tn = tn, cur_s = s;
     const int nu = u + G;
     const bool more = nu < units;
     unit(more ? nu : u, m0, tn, s, ks0, ks1);
-#pragma unroll
-    for (int cc = 0; cc < CPW6; ++cc) {
-      mfma_c(cc, Vl);
-      __builtin_amdgcn_sched_barrier(0);
-      if (cc + 3 < CPW6) bload(cc % 3, cc + 3, ks, cur_tn);
-      __builtin_amdgcn_sched_barrier(0);
-    }
+    comps(Vl, ks, cur_tn, true);
 
     // ---- epilogue: four passes of 8 tiles
-    const int n_loc = 4 * (tid & 15);          // the epilogue thread's 4 channels in the unit
-    const int n4 = cur_tn * N6 + n_loc;
-    const int epx = (tid >> 4) & 15;           // its pixel of the tile: row epx >> 2, column epx & 3
-    const int et = tid >> 8;                   // its tiles in a pass: et, et + 2, et + 4, et + 6
-    constexpr bool RES = MODE == 0 && (EF & EF_RES), ACC = MODE == 0 && (EF & EF_ACC);
-    constexpr bool MB = MODE == 0 && (EF & EF_MB), Y2 = MODE == 0 && (EF & EF_Y2);
-    float4 bias4 = make_float4(0.f, 0.f, 0.f, 0.f);
+    PO_W6_T(t2);
+    n4 = cur_tn * N6 + n_loc;
+    es = cur_s;
     if constexpr (MODE == 0) bias4 = bld4(rs_bias, (uint32_t)n4 * 4u);
-    // per pass parity: the pixels (MODE 1: workspace rows) of the thread's four
-    // tiles, their output mask, and the epilogue inputs
-    uint32_t epix[2][4], eok[2];
-    float4 pin[2][4];
-    uint32_t pm[2][4], pm2[2][4];
-    auto inputs = [&](int p) {
-      const int q = p & 1;
-      eok[q] = 0u;
-#pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        int b, ti, tj;
-        const bool tl = tile_point_magic(a, Ht, Wt, cur_m0 + TP6 * p + et + 2 * k, b, ti, tj);
-        const int i = 4 * ti + (epx >> 2), j = 4 * tj + (epx & 3);
-        const bool ok = tl && i < a.Hout && j < a.Wout;
-        eok[q] |= (ok ? 1u : 0u) << k;
-        epix[q][k] = MODE == 1 ? (uint32_t)b * a.mrows + (uint32_t)i * a.Wg + j
-                               : ((uint32_t)b * a.Hout + i) * a.Wout + j;
-        const uint32_t o = (epix[q][k] * (uint32_t)a.Cout_p + n4) * 4u;
-        const uint32_t wo = (epix[q][k] * (uint32_t)wpp + (uint32_t)(n4 >> 5)) * 4u;
-        if constexpr (RES) pin[q][k] = bld4(rsrc(a.res, dst_bytes), ok ? o : kOOB);
-        if constexpr (ACC) pin[q][k] = bld4(rs_out, ok ? o : kOOB);
-        if constexpr (MB) pm[q][k] = bld1(rsrc(a.mbits, bits_bytes), ok ? wo : kOOB);
-        if constexpr (Y2) pm2[q][k] = bld1(rsrc(a.m2bits, bits_bytes), ok ? wo : kOOB);
-      }
-    };
     inputs(0);
 #pragma unroll
     for (int p = 0; p < 4; ++p) {
-      const int q = p & 1;
       __syncthreads();                         // the k-loop's / previous pass's LDS reads are done
       {
         // stage rows e = 4p .. 4p+3 of the wave's accumulators: row (e & 3) + 4h of the pass
@@ -317,7 +460,7 @@ __global__ __launch_bounds__(512, 1) void conv_wino6_k(const ConvArgs a, const f
       }
       __syncthreads();
       {
-        // inverse transform: thread (tile wave, channel lane) of the pass
+        // inverse transform: thread (tile wave, channel lane) of the pass, into LDS slot p & 1
         int rd = wave_u * N6 + (lane ^ (32 * ((wave_u >> 2) & 1)));
         asm volatile("" : "+v"(rd));
         float z[6][4];
@@ -328,62 +471,20 @@ __global__ __launch_bounds__(512, 1) void conv_wino6_k(const ConvArgs a, const f
           for (int j = 0; j < 6; ++j) m[j] = M[(6 * i + j) * TP6 * N6 + rd];
           at6(m[0], m[1], m[2], m[3], m[4], m[5], z[i]);
         }
-        int wr = wave_u * 16 * N6 + lane;
+        int wr = V6_FLOATS + (p & 1) * (TP6 * 16 * N6) + wave_u * 16 * N6 + lane;
         asm volatile("" : "+v"(wr));
 #pragma unroll
         for (int jj = 0; jj < 4; ++jj) {
           float y[4];
           at6(z[0][jj], z[1][jj], z[2][jj], z[3][jj], z[4][jj], z[5][jj], y);
 #pragma unroll
-          for (int ii = 0; ii < 4; ++ii) Yl[wr + (4 * ii + jj) * N6] = y[ii];
+          for (int ii = 0; ii < 4; ++ii) smem[wr + (4 * ii + jj) * N6] = y[ii];
         }
       }
       if (p < 3) inputs(p + 1);                // requested before this pass's stores
-      __syncthreads();
-      int rrow = (et * 16 + epx) * N6 + n_loc;
-      asm volatile("" : "+v"(rrow));
-#pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        const float4 v = *reinterpret_cast<const float4*>(Yl + rrow + 2 * k * 16 * N6);
-        const bool ok = (eok[q] >> k) & 1u;
-        const uint32_t pix = epix[q][k];
-        if constexpr (MODE == 1) {
-          const uint32_t o = (((uint32_t)cur_s * (uint32_t)a.M + pix) * (uint32_t)a.N + n4) * 4u;
-          bst4(v, rs_out, ok ? o : kOOB);
-        } else {
-          const uint32_t o = (pix * (uint32_t)a.Cout_p + n4) * 4u;
-          float x[4] = {v.x + bias4.x, v.y + bias4.y, v.z + bias4.z, v.w + bias4.w};
-#pragma unroll
-          for (int cch = 0; cch < 4; ++cch) x[cch] = po::leaky_or_id(x[cch], po::act_slope(a.act));
-          if constexpr (ACC) {
-            x[0] += pin[q][k].x; x[1] += pin[q][k].y; x[2] += pin[q][k].z; x[3] += pin[q][k].w;
-          }
-          float4 out = make_float4(x[0], x[1], x[2], x[3]);
-          if constexpr (MB) {
-            const float4 g = po::leaky_grad_bits(pm[q][k], n4);
-            out = make_float4(x[0] * g.x, x[1] * g.y, x[2] * g.z, x[3] * g.w);
-          }
-          if constexpr ((EF & EF_Y) != 0) bst4(out, rs_out, ok ? o : kOOB);
-          if constexpr (RES) {
-            const float4 rr = pin[q][k];
-            bst4(make_float4(x[0] + rr.x, x[1] + rr.y, x[2] + rr.z, x[3] + rr.w), rsrc(a.sum, dst_bytes), ok ? o : kOOB);
-          }
-          if constexpr (Y2) {
-            const float4 g2 = po::leaky_grad_bits(pm2[q][k], n4);
-            bst4(make_float4(x[0] * g2.x, x[1] * g2.y, x[2] * g2.z, x[3] * g2.w), rsrc(a.y2, dst_bytes), ok ? o : kOOB);
-          }
-          if constexpr ((EF & EF_YB) != 0) {
-            // sign bits: 8 lanes hold the 32 channels of one word (DPP row shifts, tile 70)
-            const uint32_t nib = ((out.x > 0.f ? 1u : 0u) | (out.y > 0.f ? 2u : 0u) | (out.z > 0.f ? 4u : 0u) |
-                                  (out.w > 0.f ? 8u : 0u)) & (0u - (uint32_t)ok);
-            uint32_t w = nib << (4 * (lane & 7));
-            w |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)w, 0x101, 0xF, 0xF, false);   // row_shl:1
-            w |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)w, 0x102, 0xF, 0xF, false);   // row_shl:2
-            w |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)w, 0x104, 0xF, 0xF, false);   // row_shl:4
-            bst1(w, rsrc(a.ybits, bits_bytes),
-                 (ok && (lane & 7) == 0) ? (pix * (uint32_t)wpp + (uint32_t)(n4 >> 5)) * 4u : kOOB);
-          }
-        }
+      if (p < 2) {
+        __syncthreads();
+        emit(p);
       }
       if (p == 1) {
         // the next unit's first input rows and B fragments (the last unit re-reads
@@ -395,9 +496,27 @@ __global__ __launch_bounds__(512, 1) void conv_wino6_k(const ConvArgs a, const f
         for (int cc = 0; cc < 3; ++cc) bload(cc, cc, ks0, tn);
       }
     }
+    PO_W6_T(t3);
+#ifdef PO_W6_STAMP
+    ph[0] += t1 - t0;
+    ph[1] += t2 - t1;
+    ph[2] += t3 - t2;
+    ++nunits;
+#endif
     if (!more) break;
     u = nu;
   }
+  __syncthreads();                             // the last unit's passes 2 and 3
+  emit(2);
+  emit(3);
+#ifdef PO_W6_STAMP
+  if (tid == 0 && blockIdx.x < (1 << 12)) {
+    for (int i = 0; i < 3; ++i) g_w6_stamp[blockIdx.x][i] = ph[i];
+    g_w6_stamp[blockIdx.x][3] = nunits;
+    g_w6_stamp[blockIdx.x][4] = rt0;
+    g_w6_stamp[blockIdx.x][5] = __builtin_amdgcn_s_memrealtime();
+  }
+#endif
 }
 }  // namespace
 
@@ -472,4 +591,9 @@ int launch_wino6(const ConvArgs& a, const float* U6, hipStream_t st) {
   PO_REQUIRE(hipLaunchKernel(k, dim3(grid), dim3(512), args, 0, st) == hipSuccess, "po_conv: tile 71 launch failed");
   return check_launch("po_conv (winograd F(4x4) persistent)");
 }
+#ifdef PO_W6_STAMP
+extern "C" int po_debug_w6_stamps(unsigned long long* host, int n) {
+  return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_w6_stamp), (size_t)n * 64) == hipSuccess ? 0 : -1;
+}
+#endif
 }  // namespace po

@@ -5,7 +5,7 @@ set -e
 TAG=$1; shift
 ROOT=$(cd "$(dirname "$0")/.." && pwd)
 SRC=$ROOT/adversarial_patch-based_false_positive_creation_attacks_against_aerial_imagery_object_detectors_amd/csrc
-OUT=$ROOT/tools/abl
+OUT=${OUT:-$ROOT/tools/abl}; case $OUT in /*) ;; *) OUT=$ROOT/$OUT;; esac
 TMP=$(mktemp -d)
 mkdir -p "$OUT"
 for f in "$SRC"/*.hip; do
