@@ -1,7 +1,7 @@
-"""Drop the unboxed Winograd choices (tiles 65-68) of a committed tile cache
-so the next bench run re-times those launch shapes against every tile,
-persistent tile 70 included; boxed launches (gradient cones) keep their
-choice (tile 70 runs full maps only).
+"""Drop the unboxed Winograd choices (tiles 65-68, 70) of a committed tile
+cache so the next bench run re-times those launch shapes against every tile,
+the persistent tiles 70 (F(2x2,3x3)) and 71 (F(4x4,3x3)) included; boxed
+launches (gradient cones) keep their choice (tiles 70/71 run full maps only).
 Usage: python tools/retune_wino.py IN.json OUT.json"""
 import json
 import sys
@@ -13,7 +13,7 @@ for k, v in cache.items():
     key = json.loads(k)
     tile = v[0] if isinstance(v, list) else v
     boxed = bool(key[15])
-    if tile in (65, 66, 67, 68) and not boxed:
+    if tile in (65, 66, 67, 68, 70) and not boxed:
         continue
     keep[k] = v
 json.dump(keep, open(dst, "w"))
