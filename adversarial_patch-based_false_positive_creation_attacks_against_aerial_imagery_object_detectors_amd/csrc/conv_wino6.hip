@@ -90,6 +90,49 @@ __device__ __forceinline__ void at6(float m0, float m1, float m2, float m3, floa
   y[3] = __builtin_fmaf(8.f, s, q) + m5;
 }
 
+// Gradient-cone boxes (ConvArgs.gbox, destination pixels [r0,r1) x [c0,c1) of
+// image b): the image's GEMM rows l < h*w enumerate the 4x4 tiles meeting its
+// box row-major, the rest are dead (conv_wino.hip tile_point with 4x4 tiles)
+struct Box6 {
+  int t0, u0, h, w;
+};
+__device__ __forceinline__ Box6 box6(const ConvArgs& a, int b) {
+  const int4 bx = reinterpret_cast<const int4*>(a.gbox)[b];
+  const int t0 = bx.x >> 2, t1 = (bx.z + 3) >> 2, u0 = bx.y >> 2, u1 = (bx.w + 3) >> 2;
+  return {t0, u0, max(t1 - t0, 0), max(u1 - u0, 0)};
+}
+// GEMM row m -> image b, tile (ti, tj); false: the row computes nothing
+__device__ __forceinline__ bool tile_pt6(const ConvArgs& a, int Ht, int Wt, int m, int& b, int& ti, int& tj) {
+  if (!a.gbox) return tile_point_magic(a, Ht, Wt, m, b, ti, tj);
+  const int per = Ht * Wt;
+  const bool in = m < a.B * per;
+  b = in ? po::div_by(m, a.mg_tiles, a.sh_tiles) : 0;
+  const int l = in ? m - b * per : 0;
+  const Box6 x = box6(a, b);
+  const bool ok = in && l < x.h * x.w;
+  const int q = ok ? l / x.w : 0;
+  ti = x.t0 + q;
+  tj = x.u0 + (ok ? l - q * x.w : 0);
+  return ok;
+}
+// whether unit u (its 32 GEMM rows; wave-uniform) holds a live tile: always on
+// a full map, with boxes when one of the (at most a few) images it spans has
+// one of its first h*w rows in it
+__device__ __forceinline__ bool unit_live6(const ConvArgs& a, int Ht, int Wt, int u, int mn) {
+  if (!a.gbox) return true;
+  const int per = Ht * Wt;
+  const int s = po::div_by(u, a.mg_mn, a.sh_mn);
+  const int tm = po::div_by(u - s * mn, a.mg_ntn, a.sh_ntn);
+  const int m0 = tm * 32;
+  const int b0 = po::div_by(m0, a.mg_tiles, a.sh_tiles);
+  const int b1 = min(po::div_by(m0 + 31, a.mg_tiles, a.sh_tiles), a.B - 1);
+  for (int b = b0; b <= b1; ++b) {
+    const Box6 x = box6(a, b);
+    if (max(m0 - b * per, 0) < x.h * x.w) return true;
+  }
+  return false;
+}
+
 #ifdef PO_W6_STAMP
 // diagnostic build only (tools/w6_phases.py): per workgroup, shader cycles
 // (s_memtime) summed over its units per phase -- [0] unit top through the
@@ -157,7 +200,7 @@ __global__ __launch_bounds__(512, 1) void conv_wino6_k(const ConvArgs a, const f
   uint32_t rbase = 0u, okm = 0u;
   auto offsets = [&](int m0) {
     int b, ti, tj;
-    const bool ok_t = tile_point_magic(a, Ht, Wt, m0 + r, b, ti, tj);
+    const bool ok_t = tile_pt6(a, Ht, Wt, m0 + r, b, ti, tj);
     const int y0 = 4 * ti - 1, x0 = 4 * tj - 1;
     rbase = (((uint32_t)b * a.Hin + (uint32_t)(4 * ti)) * a.Win + (uint32_t)(4 * tj)) * pix_bytes + 4u * c;
     okm = 0u;
@@ -285,6 +328,8 @@ __global__ __launch_bounds__(512, 1) void conv_wino6_k(const ConvArgs a, const f
 
   // ---- the unit loop
   int u = po::xcd_remap();                     // host: gridDim.x <= units
+  while (u < units && !unit_live6(a, Ht, Wt, u, mn)) u += G;       // boxed: skip units with no live tile
+  if (u >= units) return;                      // (uniform: every wave of the workgroup leaves)
   int m0, tn, s, ks0, ks1;
   unit(u, m0, tn, s, ks0, ks1);
   offsets(m0);
@@ -322,12 +367,22 @@ __global__ __launch_bounds__(512, 1) void conv_wino6_k(const ConvArgs a, const f
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
       int b, ti, tj;
-      const bool tl = tile_point_magic(a, Ht, Wt, cur_m0 + TP6 * p + et + 2 * k, b, ti, tj);
+      const bool tl = tile_pt6(a, Ht, Wt, cur_m0 + TP6 * p + et + 2 * k, b, ti, tj);
       const int i = 4 * ti + (epx >> 2), j = 4 * tj + (epx & 3);
-      const bool ok = tl && i < a.Hout && j < a.Wout;
+      bool ok = tl && i < a.Hout && j < a.Wout;
+      // split-K partials at conv_reduce_k's GEMM rows: row-major over the map,
+      // or over the image's box (conv_common.h grid_point)
+      int wl = i * a.Wg + j;
+      if (a.gbox) {                                // only the box's pixels are written
+        const int4 bx = reinterpret_cast<const int4*>(a.gbox)[b];
+        ok = ok && i >= bx.x && i < bx.z && j >= bx.y && j < bx.w;
+        if constexpr (MODE == 1) {
+          const int i0 = max(bx.x, 0), j0 = max(bx.y, 0);
+          wl = (i - i0) * (min(bx.w, a.Wg) - j0) + j - j0;
+        }
+      }
       eok[q] |= (ok ? 1u : 0u) << k;
-      epix[q][k] = MODE == 1 ? (uint32_t)b * a.mrows + (uint32_t)i * a.Wg + j
-                             : ((uint32_t)b * a.Hout + i) * a.Wout + j;
+      epix[q][k] = MODE == 1 ? (uint32_t)b * a.mrows + (uint32_t)wl : ((uint32_t)b * a.Hout + i) * a.Wout + j;
       const uint32_t o = (epix[q][k] * (uint32_t)a.Cout_p + n4) * 4u;
       const uint32_t wo = (epix[q][k] * (uint32_t)wpp + (uint32_t)(n4 >> 5)) * 4u;
       if constexpr (RES) pin[q][k] = bld4(rsrc(a.res, dst_bytes), ok ? o : kOOB);
@@ -434,7 +489,8 @@ __global__ __launch_bounds__(512, 1) void conv_wino6_k(const ConvArgs a, const f
     const float* Vl = smem + ((ks - ks0) & 1) * V6_FLOATS;
     cur_m0 = m0;
     const int cur_tn = tn, cur_s = s;
-    const int nu = u + G;
+    int nu = u + G;
+    while (nu < units && !unit_live6(a, Ht, Wt, nu, mn)) nu += G;
     const bool more = nu < units;
     unit(more ? nu : u, m0, tn, s, ks0, ks1);
     comps(Vl, ks, cur_tn, true);
@@ -528,8 +584,9 @@ int launch_wino6(const ConvArgs& a, const float* U6, hipStream_t st) {
   PO_REQUIRE(a.prec == 0 && a.ntaps == 9 && a.tkw == 3 && (a.sdh == 1 || a.sdh == -1) && (a.sdw == 1 || a.sdw == -1) &&
                  a.dh0 == -a.sdh && a.dw0 == -a.sdw,
              "po_conv: Winograd tile needs a full 3x3 neighbourhood of taps");
-  PO_REQUIRE(a.in_step == 1 && a.out_step == 1 && a.out_oy == 0 && a.out_ox == 0 && !a.in_org && !a.out_org && !a.gbox,
-             "po_conv: tile 71 needs stride 1 on full maps without boxes");
+  PO_REQUIRE(a.in_step == 1 && a.out_step == 1 && a.out_oy == 0 && a.out_ox == 0 && !a.in_org && !a.out_org,
+             "po_conv: tile 71 needs stride 1 on full maps");
+  PO_REQUIRE(!a.gbox || a.mrows == a.Hg * a.Wg, "po_conv: tile 71 takes gradient-cone boxes on the full grid only");
   PO_REQUIRE(a.Hg == a.Hout && a.Wg == a.Wout && a.Hin == a.Hout && a.Win == a.Wout,
              "po_conv: Winograd tile needs source, grid and destination of one size");
   PO_REQUIRE(!a.pool_y, "po_conv: tile 71 has no fused pool");

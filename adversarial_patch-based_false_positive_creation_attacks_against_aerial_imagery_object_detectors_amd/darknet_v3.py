@@ -1480,7 +1480,7 @@ class NetPlan:
     @classmethod
     def tile_map(cls):
         """ADVPATCH_TILE_MAP ("68:70,66:70"), parsed once per value: a diagnostic
-        A/B remap of cached / tuned tiles on unboxed launches."""
+        A/B remap of cached / tuned tiles (kept only where the target tile takes the launch)."""
         remap = os.environ.get("ADVPATCH_TILE_MAP", "")
         if cls._tile_map is None or cls._tile_map[0] != remap:
             m = dict(tuple(int(v) for v in kv.split(":")) for kv in remap.split(",") if kv.strip())
@@ -1492,7 +1492,7 @@ class NetPlan:
         desc.tile, desc.ksplit = t, ks
         self._apply_ws(desc)
         remap = self.tile_map()
-        if remap and not desc.gbox and t in remap:
+        if remap and t in remap:
             # only where the target tile takes the launch: po_conv is called under
             # a stream capture that is discarded (its argument checks run, its
             # kernels never do); a refused remap keeps the chosen tile

@@ -4,7 +4,8 @@ the same convolution, so it is compared with float64 torch conv2d (and with
 the direct fp32 kernel's own error beside it), and its epilogues with tile
 70's on the same descriptor: both tap orientations, ragged 4x4 tiles on odd
 and non-multiple-of-4 map sides, every epilogue-field combination the plan
-launches, split-K slices (even and uneven), and the launches it refuses."""
+launches, split-K slices (even and uneven), gradient-cone boxes, and the
+launches it refuses."""
 import ctypes
 
 import pytest
@@ -95,15 +96,18 @@ def test_tile71_epilogues_match_tile70(mode, B, H, Cin, Cout):
             assert torch.equal(bb1[~tie], bb0[~tie])
 
 
-def _run_with(nat, tile, mode, B, H, Cin, Cout, flip, U, U6, xd, wd, bias, prev, res, mbits, m2bits, ksplit=1):
+def _run_with(nat, tile, mode, B, H, Cin, Cout, flip, U, U6, xd, wd, bias, prev, res, mbits, m2bits, ksplit=1,
+              box=None):
     from test_gpu_wino5 import _run
-    # tile 70's harness, with the F(4x4) weights attached for tile 71
+    # tile 70's harness, with the F(4x4) weights (and a gradient-cone box) attached
     orig = _desc
     import test_gpu_wino5 as w5
 
     def desc6(nat_, B_, H_, Cin_, Cout_, tile_, flip_=False):
         d = orig(nat_, B_, H_, Cin_, Cout_, tile_, flip_)
         d.Wwino6 = U6.data_ptr()
+        if box is not None:
+            d.gbox = box.data_ptr()
         return d
     w5._desc = desc6
     try:
@@ -134,6 +138,48 @@ def test_tile71_split_k(mode, Cin, ks):
             assert float((a[fin] - b[fin]).abs().max()) <= 2 * TOL71 * float(b[fin].abs().max())
 
 
+BOXES = {
+    # per image (r0, c0, r1, c1): unaligned to the 4x4 tiles, on the ragged
+    # edge, a single pixel, an empty box, the whole map
+    "mixed": lambda H: [[3, 5, 14, 11], [H - 6, H - 9, H, H], [7, 7, 8, 8], [5, 5, 5, 9]],
+    "full": lambda H: [[0, 0, H, H]] * 4,
+    "row": lambda H: [[0, 1, 2, H], [H - 1, 0, H, H], [4, 4, 9, 6], [0, 0, H, 3]],
+}
+
+
+@pytest.mark.parametrize("boxes", sorted(BOXES))
+@pytest.mark.parametrize("mode", ["dgrad_mask", "dgrad_acc_bits", "dgrad_dual", "dgrad_acc_dual", "fwd_plain"])
+@pytest.mark.parametrize("B,H,Cin,Cout,ks", [(4, 19, 256, 128, 1), (4, 38, 128, 64, 1), (4, 17, 64, 128, 1),
+                                             (4, 19, 256, 128, 3), (4, 38, 128, 64, 2)])
+def test_tile71_gradient_cone_boxes(boxes, mode, B, H, Cin, Cout, ks):
+    """A boxed launch (gbox, the patch-gradient cones of the dgrads) writes
+    exactly each image's box, within TOL71 of tile 68 (F(2x2), boxed) there
+    (2 TOL71 with split-K: partials at the box's compact rows, conv_reduce_k),
+    and leaves every other pixel as it was; units with no live tile are skipped
+    (the empty box), the rest see their images' boxes."""
+    nat = pkg_mod("_native")
+    flip = mode.startswith("dgrad")
+    xd, wd, bias, U, prev, res, mbits, m2bits = _inputs(B, H, Cin, Cout, flip, seed=H + Cout + len(boxes))
+    U6 = _u6(wd, flip)
+    box = torch.tensor(BOXES[boxes](H), dtype=torch.int32, device=DEV)
+    runs = {t: _run_with(nat, t, mode, B, H, Cin, Cout, flip, U, U6, xd, wd, bias, prev, res, mbits, m2bits, box=box,
+                         ksplit=ks if t == 71 else 1)
+            for t in (71, 68)}
+    tol = TOL71 * (2 if ks > 1 else 1)
+    inside = torch.zeros(B, H, H, 1, dtype=torch.bool, device=DEV)
+    for b, (r0, c0, r1, c1) in enumerate(box.tolist()):
+        inside[b, r0:r1, c0:c1] = True
+    for a, b in zip(runs[71][:3], runs[68][:3]):
+        assert torch.equal(a.nan_to_num(7.0), torch.where(inside, a, b).nan_to_num(7.0))   # outside: as tile 68 left it
+        fin = torch.isfinite(b) & inside
+        assert torch.equal(fin, torch.isfinite(a) & inside)
+        if fin.any():
+            scale = float(b[fin].abs().max())
+            assert float((a[fin] - b[fin]).abs().max()) <= tol * max(scale, 1e-30), mode
+    y0 = runs[68][0]
+    assert torch.equal(torch.where(inside, prev, y0), prev)           # tile 68 itself kept the outside
+
+
 def test_tile71_refuses_what_it_cannot_run():
     nat = pkg_mod("_native")
     B, H, Cin, Cout = 2, 16, 32, 64
@@ -151,8 +197,10 @@ def test_tile71_refuses_what_it_cannot_run():
     assert call(d) == 0
     box = torch.tensor([[0, 0, 8, 8]] * B, dtype=torch.int32, device=DEV)
     d.gbox = box.data_ptr()
-    assert call(d) != 0 and "boxes" in nat.last_error()
-    d.gbox = None
+    assert call(d) == 0                                              # gradient-cone boxes
+    d.mrows = 8 * 8
+    assert call(d) != 0                                              # ... on the full grid only
+    d.gbox, d.mrows = None, 0
     slot = torch.zeros(64, dtype=torch.int32, device=DEV)
     d.y_amax = slot.data_ptr()
     assert call(d) != 0
