@@ -398,7 +398,7 @@ int launch_wino(const ConvArgs& a, const float* U, hipStream_t st, int bm, int w
 int launch_wino4(const ConvArgs& a, const float* U, hipStream_t st, bool stagger);
 int launch_wino5(const ConvArgs& a, const float* U, hipStream_t st);
 // tile 71 (conv_wino6.hip): Winograd F(4x4,3x3), persistent; U6 = po_conv_desc.Wwino6
-int launch_wino6(const ConvArgs& a, const float* U6, hipStream_t st);
+int launch_wino6(const ConvArgs& a, const float* U6, hipStream_t st, float* VG = nullptr, int64_t vg_floats = 0);
 // tile 69 (conv_halo.hip): persistent 3x3 conv 16 -> 32 channels with the 2x2
 // max pool fused, input patches staged once per 8 x 16-pixel tile
 int launch_halo(const ConvArgs& a, hipStream_t st);

@@ -151,9 +151,12 @@ __device__ unsigned long long g_w6_stamp[1 << 12][8];
 #define W6ST(x) x
 #endif
 
-template <int MODE, int EF>   // MODE 0: po_conv epilogue (fields EF), 1: raw split-K partials
+// MODE 0: po_conv epilogue (fields EF), 1: raw split-K partials.  PT (tile 72):
+// the transformed input comes from VG (wino6_pre_k) straight into registers
+template <int MODE, int EF, bool PT = false>
 __global__ __launch_bounds__(512, 1) void conv_wino6_k(const ConvArgs a, const float* __restrict__ U, int Ht, int Wt,
-                                                       int units, int mn) {
+                                                       int units, int mn, const float* __restrict__ VG,
+                                                       uint32_t vg_bytes) {
   __shared__ __attribute__((aligned(16))) float smem[2 * V6_FLOATS];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave_u = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -210,32 +213,28 @@ __global__ __launch_bounds__(512, 1) void conv_wino6_k(const ConvArgs a, const f
     for (int j = 0; j < 6; ++j) okm |= ((unsigned)(x0 + j) < (unsigned)a.Win ? 1u : 0u) << (8 + j);
   };
   f2v d[18];                                   // d[3 i + jp] = patch row i, columns 2jp, 2jp+1
-  auto gload = [&](int ks) {
+  // row i of step ks's patches into d (6 loads; opaque per call: hoisted out of
+  // the k-loop, the per-load selects would hold 36 registers across it).
+  // Branch-free: a wave-uniform fast path for tiles inside the map's columns
+  // made the compiler's vmcnt waits after the merge count every row load.
+  auto grow = [&](int ks, int i) {
     const uint32_t cb = (uint32_t)__builtin_amdgcn_readfirstlane(ks * (WK * 4));
-    // opaque per call: hoisted out of the k-loop, the per-load selects would hold
-    // 36 registers across it
     uint32_t rb = rbase, om = okm;
     asm volatile("" : "+v"(rb), "+v"(om));
-    auto rows = [&](bool cols_all) {
-      const bool c0 = cols_all || ((om >> 8) & 1u);
+    const bool rok = (om >> i) & 1u;
+    const uint32_t rr = i == 0 ? rb - row_bytes : rb;
+    const uint32_t rv = rok ? rr : kOOB;                                  // columns 1..5
+    const uint32_t rv0 = (rok && ((om >> 8) & 1u)) ? rr - pix_bytes : kOOB;  // column 0
 #pragma unroll
-      for (int i = 0; i < 6; ++i) {
-        const bool rok = (om >> i) & 1u;
-        const uint32_t rr = i == 0 ? rb - row_bytes : rb;
-        const uint32_t rv = rok ? rr : kOOB;                            // columns 1..5
-        const uint32_t rv0 = (rok && c0) ? rr - pix_bytes : kOOB;       // column 0
+    for (int j = 0; j < 6; ++j) {
+      const uint32_t vo = j == 0 ? rv0 : (((om >> (8 + j)) & 1u) ? rv : kOOB);
+      const uint32_t so = cb + (i == 0 ? 0u : (uint32_t)(i - 1) * row_bytes) + (j == 0 ? 0u : (uint32_t)(j - 1) * pix_bytes);
+      d[3 * i + (j >> 1)][j & 1] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(in_rs, vo, so, 0));
+    }
+  };
+  auto gload = [&](int ks) {
 #pragma unroll
-        for (int j = 0; j < 6; ++j) {
-          const uint32_t vo = j == 0 ? rv0 : ((cols_all || ((om >> (8 + j)) & 1u)) ? rv : kOOB);
-          const uint32_t so = cb + (i == 0 ? 0u : (uint32_t)(i - 1) * row_bytes) + (j == 0 ? 0u : (uint32_t)(j - 1) * pix_bytes);
-          d[3 * i + (j >> 1)][j & 1] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(in_rs, vo, so, 0));
-        }
-      }
-    };
-    // a wave whose 4 tiles all lie inside the map's columns (most of them) skips
-    // the per-load column selects (the same 36 loads either way)
-    if (__all(((om >> 8) & 0x3Fu) == 0x3Fu)) rows(true);
-    else rows(false);
+    for (int i = 0; i < 6; ++i) grow(ks, i);
   };
   // V = B^T d B on column pairs / row pairs (packed f32): the columns (pairs of
   // columns), a 2x2 transposition of every block, then the rows (pairs of rows);
@@ -295,33 +294,60 @@ __global__ __launch_bounds__(512, 1) void conv_wino6_k(const ConvArgs a, const f
     bq[slot][0] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(u_rs, u_lane, blk, 0));
     bq[slot][1] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(u_rs, u_lane + 1024u, blk, 0));
   };
+  // ---- A operand (tile 72): VG [m-block][k-step][36][32 tiles][16 channels]; lane
+  // (tile lane & 31, half h) takes channels 8h .. 8h+7 of its tile (two 16-byte
+  // loads, a wave's 2 KB contiguous), on a ring beside the B fragments'
+  const __amdgpu_buffer_rsrc_t v_rs = rsrc(VG, PT ? vg_bytes : 0u);
+  const uint32_t a_lane = ((uint32_t)(lane & 31) * WK + 8u * (uint32_t)h) * 4u;
+  float4 aq[3][2];
+  auto aload = [&](int slot, int cc, int ks, int tmm) {
+    const uint32_t blk = (uint32_t)__builtin_amdgcn_readfirstlane(((tmm * kc_n + ks) * NX6 + xq + cc) * (T6 * WK * 4));
+    aq[slot][0] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(v_rs, a_lane, blk, 0));
+    aq[slot][1] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(v_rs, a_lane + 16u, blk, 0));
+  };
   floatx16 acc[CPW6];
   // the wave's 9 components of one k-step: component cc's MFMAs, each half's A
   // fragment of component cc + 1 read from LDS as soon as its registers are
   // free (after the 4 MFMAs that use them), and the ring slot cc frees refilled
   // with component cc + 3 (this k-step) or cc - 6 (the next; not on the last step)
-  auto comps = [&](const float* Vb, int ks, int tnn, bool last) {
+  // !last: row cc of step kg's input patches requested after component cc's
+  // MFMAs (cc < 6), so the row loads issue beside the matrix work
+  auto comps = [&](const float* Vb, int ks, int tnn, int tmm, auto last_c, int kg) {
+    constexpr bool last = decltype(last_c)::value;
     const int o0 = v6idx(xq, lane & 31, 2 * h), o1 = o0 ^ 4;     // chunks 2h, 2h + 1: swizzled apart in bit 0
-    float4 a0 = *reinterpret_cast<const float4*>(Vb + o0);
-    float4 a1 = *reinterpret_cast<const float4*>(Vb + o1);
+    float4 a0, a1;
+    if constexpr (!PT) {
+      a0 = *reinterpret_cast<const float4*>(Vb + o0);
+      a1 = *reinterpret_cast<const float4*>(Vb + o1);
+    }
 #pragma unroll
     for (int cc = 0; cc < CPW6; ++cc) {
+      if constexpr (PT) {
+        a0 = aq[cc % 3][0];
+        a1 = aq[cc % 3][1];
+      }
       const float4 b0 = bq[cc % 3][0], b1 = bq[cc % 3][1];
       acc[cc] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0.x, b0.x, acc[cc], 0, 0, 0);   // step s <-> channel 8h + s
       acc[cc] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0.y, b0.y, acc[cc], 0, 0, 0);
       acc[cc] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0.z, b0.z, acc[cc], 0, 0, 0);
       acc[cc] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0.w, b0.w, acc[cc], 0, 0, 0);
       __builtin_amdgcn_sched_barrier(0);
-      if (cc + 1 < CPW6) a0 = *reinterpret_cast<const float4*>(Vb + o0 + (cc + 1) * T6 * WK);
+      if (!PT && cc + 1 < CPW6) a0 = *reinterpret_cast<const float4*>(Vb + o0 + (cc + 1) * T6 * WK);
       __builtin_amdgcn_sched_barrier(0);
       acc[cc] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1.x, b1.x, acc[cc], 0, 0, 0);
       acc[cc] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1.y, b1.y, acc[cc], 0, 0, 0);
       acc[cc] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1.z, b1.z, acc[cc], 0, 0, 0);
       acc[cc] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1.w, b1.w, acc[cc], 0, 0, 0);
       __builtin_amdgcn_sched_barrier(0);
-      if (cc + 1 < CPW6) a1 = *reinterpret_cast<const float4*>(Vb + o1 + (cc + 1) * T6 * WK);
-      if (cc + 3 < CPW6) bload(cc % 3, cc + 3, ks, tnn);
-      else if (!last) bload(cc % 3, cc - 6, ks + 1, tnn);
+      if (!PT && cc + 1 < CPW6) a1 = *reinterpret_cast<const float4*>(Vb + o1 + (cc + 1) * T6 * WK);
+      if (cc + 3 < CPW6) {
+        bload(cc % 3, cc + 3, ks, tnn);
+        if constexpr (PT) aload(cc % 3, cc + 3, ks, tmm);
+      } else if (!last) {
+        bload(cc % 3, cc - 6, ks + 1, tnn);
+        if constexpr (PT) aload(cc % 3, cc - 6, ks + 1, tmm);
+      }
+      if (!PT && cc < 6 && !last) grow(kg, cc);
       __builtin_amdgcn_sched_barrier(0);
     }
   };
@@ -332,10 +358,10 @@ __global__ __launch_bounds__(512, 1) void conv_wino6_k(const ConvArgs a, const f
   if (u >= units) return;                      // (uniform: every wave of the workgroup leaves)
   int m0, tn, s, ks0, ks1;
   unit(u, m0, tn, s, ks0, ks1);
-  offsets(m0);
-  gload(ks0);
-#pragma unroll
-  for (int cc = 0; cc < 3; ++cc) bload(cc, cc, ks0, tn);
+  if constexpr (!PT) {
+    offsets(m0);
+    gload(ks0);
+  }
   float* const M = smem;
   // ---- epilogue state.  The epilogue runs in four passes of 8 tiles; passes 0
   // and 1 emit at once, passes 2 and 3 leave their outputs in LDS (the V1 buffer,
@@ -448,42 +474,63 @@ __global__ __launch_bounds__(512, 1) void conv_wino6_k(const ConvArgs a, const f
   for (;;) {
     PO_W6_T(t0);
     __syncthreads();                           // the previous unit's LDS traffic is done
-    transform(smem);                           // step ks0 into V0
-    __builtin_amdgcn_sched_barrier(0);
-    emit(2);                                   // the previous unit's last two passes (masked on the first)
-    emit(3);
-    __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-    for (int cc = 0; cc < CPW6; ++cc)
-#pragma unroll
-      for (int e = 0; e < 16; ++e) acc[cc][e] = 0.f;
-    gload(ks0 + 1);                            // host: ks1 - ks0 >= 2
-    __syncthreads();
     int ks = ks0;
-    // every wave: this step's MFMAs, then the next step's transform and the
-    // request of the one after.  (The fp32 MFMA does not co-issue with the VALU,
-    // so a SIMD's time is the sum in any order.  One order of loads on entry and
-    // around the loop keeps the compiler's vmcnt waits partial: the transform
-    // waits for its rows only, not for the B fragments requested after them.
-    // Staggering the two waves of a SIMD as tile 70 does -- waves 4-7
-    // transforming before their MFMAs -- measured 7 % slower per k-step here.)
-    // Per k-step at 19^2 512->1024 (tools/w6_phases.py): 13.3k shader
-    // cycles against the 9.2k MFMA floor; the row loads ~1.9k, the transform's
-    // VALU ~0.9k, the V writes ~1k, the workgroup barrier the rest.
-    do {                                       // steps ks0 .. ks1-2
-      const float* Vc = smem + ((ks - ks0) & 1) * V6_FLOATS;
-      float* Vn = smem + (((ks - ks0) & 1) ^ 1) * V6_FLOATS;
-      const int k2 = min(ks + 2, ks1 - 1);
-      comps(Vc, ks, tn, false);
-      transform(Vn);
+    if constexpr (PT) {
+      // tile 72: the unit's first A and B fragments, then the previous unit's
+      // last two passes (their stores behind the loads), then the k-steps --
+      // each wave on its own: no LDS and no barrier until the epilogue
+#pragma unroll
+      for (int cc = 0; cc < 3; ++cc) {
+        aload(cc, cc, ks0, m0 / T6);
+        bload(cc, cc, ks0, tn);
+      }
       __builtin_amdgcn_sched_barrier(0);
-#ifndef PO_W6_ABL_NOGLOAD
-      gload(k2);                               // (diagnostic builds: optionally not)
-#endif
-#ifndef PO_W6_ABL_NOBAR
+      emit(2);
+      emit(3);
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int cc = 0; cc < CPW6; ++cc)
+#pragma unroll
+        for (int e = 0; e < 16; ++e) acc[cc][e] = 0.f;
+      do {                                     // steps ks0 .. ks1-2
+        comps(smem, ks, tn, m0 / T6, std::false_type{}, 0);
+      } while (++ks < ks1 - 1);
+    } else {
+      transform(smem);                         // step ks0 into V0
+      __builtin_amdgcn_sched_barrier(0);
+      emit(2);                                 // the previous unit's last two passes (masked on the first)
+      emit(3);
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int cc = 0; cc < CPW6; ++cc)
+#pragma unroll
+        for (int e = 0; e < 16; ++e) acc[cc][e] = 0.f;
+      gload(ks0 + 1);                          // host: ks1 - ks0 >= 2
+      // the first B fragments after the rows, as around the loop (the compiler's
+      // vmcnt waits at the loop head then count the fragments as later than the rows)
+#pragma unroll
+      for (int cc = 0; cc < 3; ++cc) bload(cc, cc, ks0, tn);
       __syncthreads();
+      // every wave: the next step's transform (its rows requested during this
+      // unit's previous step, or above), then this step's MFMAs with the rows of
+      // the step after requested between them -- the 36 row loads of a k-step
+      // issued beside the matrix work rather than in a burst that the whole
+      // workgroup waits for at the barrier.  (The fp32 MFMA does not co-issue
+      // with the VALU, so a SIMD's time is the sum in any order.  Staggering the
+      // two waves of a SIMD as tile 70 does -- waves 4-7 transforming before their
+      // MFMAs -- measured 7 % slower per k-step here.)
+      do {                                     // steps ks0 .. ks1-2
+        const float* Vc = smem + ((ks - ks0) & 1) * V6_FLOATS;
+        float* Vn = smem + (((ks - ks0) & 1) ^ 1) * V6_FLOATS;
+        const int k2 = min(ks + 2, ks1 - 1);
+        transform(Vn);
+        __builtin_amdgcn_sched_barrier(0);
+        comps(Vc, ks, tn, 0, std::false_type{}, k2);
+#ifndef PO_W6_ABL_NOBAR
+        __syncthreads();
 #endif
-    } while (++ks < ks1 - 1);
+      } while (++ks < ks1 - 1);
+    }
     // ---- the last step, peeled (no prefetch past the unit)
     PO_W6_T(t1);
     const float* Vl = smem + ((ks - ks0) & 1) * V6_FLOATS;
@@ -493,7 +540,7 @@ __global__ __launch_bounds__(512, 1) void conv_wino6_k(const ConvArgs a, const f
     while (nu < units && !unit_live6(a, Ht, Wt, nu, mn)) nu += G;
     const bool more = nu < units;
     unit(more ? nu : u, m0, tn, s, ks0, ks1);
-    comps(Vl, ks, cur_tn, true);
+    comps(Vl, ks, cur_tn, cur_m0 / T6, std::true_type{}, 0);
 
     // ---- epilogue: four passes of 8 tiles
     PO_W6_T(t2);
@@ -542,14 +589,12 @@ __global__ __launch_bounds__(512, 1) void conv_wino6_k(const ConvArgs a, const f
         __syncthreads();
         emit(p);
       }
-      if (p == 1) {
+      if (!PT && p == 1) {
         // the next unit's first input rows and B fragments (the last unit re-reads
         // its own: branch-free), requested halfway through the epilogue: earlier,
         // their 60 registers would sit beside the accumulators of passes 1-3
         offsets(m0);
         gload(ks0);
-#pragma unroll
-        for (int cc = 0; cc < 3; ++cc) bload(cc, cc, ks0, tn);
       }
     }
     PO_W6_T(t3);
@@ -574,12 +619,89 @@ __global__ __launch_bounds__(512, 1) void conv_wino6_k(const ConvArgs a, const f
   }
 #endif
 }
+
+// ---------------------------------------------------------------------------
+// Tile 72 (staging 17): the input transform as its own pass.  wino6_pre_k writes
+// V = B^T d B of every 32-tile m-block and 16-channel k-step once,
+// VG[m-block][k-step][xi][tile][channel] (73,728 B per block and step, the
+// order conv_wino6_k<.., PT> reads A fragments in), and the GEMM kernel then
+// streams its A fragments from it like its B fragments: its k-loop is MFMAs and
+// 16-byte loads, with no gathers, no transform VALU, no LDS and no barrier.
+// The price is VG's round trip through HBM (2.25 x the input for interior
+// 4x4 tiles): the plan's tuner weighs it per launch against tile 71.
+// Block (m-block, 4 k-steps), thread (tile r, channel quad q): tile 71's
+// gather (16-byte loads: a tile's 64 channels are 256 contiguous bytes) and
+// transform on 4 channels at once, the components stored as 16-byte runs.
+// Channels past Cin_p (Cin_p % 64 != 0) are neither read nor written.  An
+// m-block without a live tile (boxes) is skipped: no unit reads it.
+constexpr int PRE_KS = 4;                      // k-steps per wino6_pre_k block
+__global__ __launch_bounds__(512) void wino6_pre_k(const ConvArgs a, float* __restrict__ VG, int Ht, int Wt) {
+  const int tm = blockIdx.x, kc_n = a.Cin_p / WK;
+  const int tid = threadIdx.x, r = tid >> 4, q = tid & 15;
+  const int ks = blockIdx.y * PRE_KS + (q >> 2);
+  if (a.gbox) {
+    const int per = Ht * Wt, m0 = tm * T6;
+    const int b0 = po::div_by(m0, a.mg_tiles, a.sh_tiles);
+    const int b1 = min(po::div_by(m0 + T6 - 1, a.mg_tiles, a.sh_tiles), a.B - 1);
+    bool live = false;
+    for (int b = b0; b <= b1; ++b) {
+      const Box6 x = box6(a, b);
+      live = live || max(m0 - b * per, 0) < x.h * x.w;
+    }
+    if (!live) return;
+  }
+  int b, ti, tj;
+  const bool ok_t = tile_pt6(a, Ht, Wt, tm * T6 + r, b, ti, tj) && ks < kc_n;
+  const __amdgpu_buffer_rsrc_t in_rs = rsrc(a.in, a.in_bytes);
+  const uint32_t pix_bytes = (uint32_t)a.Cin_p * 4u;
+  const uint32_t base = (((uint32_t)b * a.Hin) * a.Win) * pix_bytes + (uint32_t)(ks * WK + 4 * (q & 3)) * 4u;
+  float4 d[6][6];
+#pragma unroll
+  for (int i = 0; i < 6; ++i) {
+    const int y = 4 * ti - 1 + i;
+#pragma unroll
+    for (int j = 0; j < 6; ++j) {
+      const int x = 4 * tj - 1 + j;
+      const bool ok = ok_t && (unsigned)y < (unsigned)a.Hin && (unsigned)x < (unsigned)a.Win;
+      const uint32_t vo = ok ? base + ((uint32_t)y * a.Win + (uint32_t)x) * pix_bytes : kOOB;
+      d[i][j] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(in_rs, vo, 0, 0));
+    }
+  }
+  if (!(ks < kc_n)) return;
+  // per channel: the columns, then the rows -- bt6 in tile 71's order (its
+  // packed pairs compute each element with the same operations)
+  float* dst = VG + ((size_t)tm * kc_n + ks) * (NX6 * T6 * WK) + r * WK + 4 * (q & 3);
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    float t[6][6];
+#pragma unroll
+    for (int j = 0; j < 6; ++j) {
+      float col[6];
+      bt6(d[0][j][e], d[1][j][e], d[2][j][e], d[3][j][e], d[4][j][e], d[5][j][e], col);
+#pragma unroll
+      for (int i = 0; i < 6; ++i) t[i][j] = col[i];
+    }
+#pragma unroll
+    for (int i = 0; i < 6; ++i) {
+      float row[6];
+      bt6(t[i][0], t[i][1], t[i][2], t[i][3], t[i][4], t[i][5], row);
+#pragma unroll
+      for (int j = 0; j < 6; ++j) d[i][j][e] = row[j];       // d now holds V[6i + j] for channel e
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < 6; ++i)
+#pragma unroll
+    for (int j = 0; j < 6; ++j) *reinterpret_cast<float4*>(dst + (6 * i + j) * T6 * WK) = d[i][j];
+}
 }  // namespace
 
 namespace po {
 // po_conv tile staging 16 (tile 71): conv_wino6_k, Winograd F(4x4,3x3) as a
 // persistent kernel (see above).
-int launch_wino6(const ConvArgs& a, const float* U6, hipStream_t st) {
+// staging 17 (tile 72, VG != nullptr): the same GEMM and epilogues on the
+// input transformed beforehand by wino6_pre_k into VG (vg_floats floats).
+int launch_wino6(const ConvArgs& a, const float* U6, hipStream_t st, float* VG, int64_t vg_floats) {
   PO_REQUIRE(U6, "po_conv: tile 71 needs the F(4x4,3x3) weights (Wwino6)");
   PO_REQUIRE(a.prec == 0 && a.ntaps == 9 && a.tkw == 3 && (a.sdh == 1 || a.sdh == -1) && (a.sdw == 1 || a.sdw == -1) &&
                  a.dh0 == -a.sdh && a.dw0 == -a.sdw,
@@ -613,13 +735,22 @@ int launch_wino6(const ConvArgs& a, const float* U6, hipStream_t st) {
   div_magic(a.ksplit, b.mg_ks, b.sh_ks);
   PO_REQUIRE((int64_t)mn * a.ksplit < (1LL << 31), "po_conv: too many tiles");
   const int units = mn * a.ksplit;
+  const int kc_n = a.Cin_p / WK;
+  const int64_t vg_need = (int64_t)ntm * kc_n * NX6 * T6 * WK;
+  if (VG) {
+    PO_REQUIRE(vg_floats >= vg_need, "po_conv: tile 72 needs a transformed-input workspace of %lld floats (have %lld)",
+               (long long)vg_need, (long long)vg_floats);
+    PO_REQUIRE(vg_need * 4 < (1LL << 31), "po_conv: tile 72 transformed input must be < 2^31 bytes");
+  }
+  const uint32_t vg_bytes = VG ? (uint32_t)(vg_need * 4) : 0u;
   const int ef = (a.y ? EF_Y : 0) | (a.res ? EF_RES : 0) | (a.accumulate ? EF_ACC : 0) | (a.mbits ? EF_MB : 0) |
                  (a.y2 ? EF_Y2 : 0) | (a.ybits ? EF_YB : 0);
   const void* k = nullptr;
   // the epilogue-field combinations po_conv launches on full-map Winograd tiles
-#define PO_W6(MODE, EF)                                             \
-  case (MODE) * 64 + (EF):                                          \
-    k = reinterpret_cast<const void*>(conv_wino6_k<MODE, EF>);      \
+#define PO_W6(MODE, EF)                                                                              \
+  case (MODE) * 64 + (EF):                                                                           \
+    k = VG ? reinterpret_cast<const void*>(conv_wino6_k<MODE, EF, true>)                            \
+           : reinterpret_cast<const void*>(conv_wino6_k<MODE, EF, false>);                          \
     break;
   const int which = a.ksplit > 1 ? 64 : ef;
   switch (which) {
@@ -641,10 +772,17 @@ int launch_wino6(const ConvArgs& a, const float* U6, hipStream_t st) {
   }
 #undef PO_W6
   PO_REQUIRE(k, "po_conv: tile 71 has no kernel for epilogue fields 0x%x", which);
+  if (VG) {
+    hipLaunchKernelGGL(wino6_pre_k, dim3(ntm, ceil_div(kc_n, PRE_KS)), dim3(512), 0, st, b, VG, Ht, Wt);
+    const int rc = check_launch("po_conv (tile 72 input transform)");
+    if (rc) return rc;
+  }
   const int resident = resident_groups_cached(k, 512);
   const int grid = units < resident ? units : resident;
+  const float* vgc = VG;
   void* args[] = {&b, const_cast<float**>(&U6), const_cast<int*>(&Ht), const_cast<int*>(&Wt),
-                  const_cast<int*>(&units), const_cast<int*>(&mn)};
+                  const_cast<int*>(&units), const_cast<int*>(&mn), const_cast<float**>(&vgc),
+                  const_cast<uint32_t*>(&vg_bytes)};
   PO_REQUIRE(hipLaunchKernel(k, dim3(grid), dim3(512), args, 0, st) == hipSuccess, "po_conv: tile 71 launch failed");
   return check_launch("po_conv (winograd F(4x4) persistent)");
 }

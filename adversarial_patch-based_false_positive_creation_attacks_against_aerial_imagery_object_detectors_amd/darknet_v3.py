@@ -571,11 +571,11 @@ class NetPlan:
 
     # Winograd tiles of po_conv: (tiles = GEMM rows, output channels) per workgroup
     WINO_TILES = {61: (64, 32), 65: (32, 64), 66: (32, 64), 67: (64, 64), 68: (64, 64), 70: (64, 64),
-                  71: (32, 64)}   # 62-64 retired
+                  71: (32, 64), 72: (32, 64)}   # 62-64 retired
     # output-tile side and transform components of each Winograd tile: F(2x2,3x3)
-    # (16), except tile 71, F(4x4,3x3) (36)
-    WINO_SIDE = {71: 4}
-    WINO_COMPS = {71: 36}
+    # (16), except tiles 71/72, F(4x4,3x3) (36)
+    WINO_SIDE = {71: 4, 72: 4}
+    WINO_COMPS = {71: 36, 72: 36}
     HALO_TILE = 69               # conv_halo_pool_k (conv_halo.hip)
     _tile_shapes = {}
 
@@ -1193,6 +1193,13 @@ class NetPlan:
         for d in self._side_descs():
             if d.ksplit > 1:
                 d.workspace = self.ws_side.data_ptr()
+        need = max([self.winov_floats(d) for d in self._side_descs() if d.tile == self.WINOV_TILE] + [0])
+        if need:
+            if getattr(self, "winov_side", None) is None or self.winov_side.numel() < need:
+                self.winov_side = torch.empty(need, device=self.device)
+            for d in self._side_descs():
+                if d.tile == self.WINOV_TILE:
+                    d.winov, d.winov_floats = self.winov_side.data_ptr(), self.winov_floats(d)
 
     def _orgp(self, i):
         o = self.org_of(i)
@@ -1336,7 +1343,8 @@ class NetPlan:
     # ---------------- autotuning ----------------
     SPLITS = (2, 4, 8, 16, 32)
     WS_FLOATS = 64 << 20          # split-K workspace cap (256 MB)
-    WINO_SPLIT_TILES = (66, 67, 68, 70, 71)   # Winograd tiles with split-K (conv_wino3_k .. conv_wino6_k)
+    WINO_SPLIT_TILES = (66, 67, 68, 70, 71, 72)   # Winograd tiles with split-K (conv_wino3_k .. conv_wino6_k)
+    WINOV_TILE = 72               # F(4x4,3x3) on an input transformed beforehand (po_conv_desc.winov)
 
     def _ensure_ws(self, floats):
         if self.ws is None or self.ws.numel() < floats:
@@ -1361,6 +1369,11 @@ class NetPlan:
                 key = self._tune_key(args, desc)
                 if key in cache:
                     self._set_tile(desc, cache[key])
+            for args, desc in convs:                 # the workspaces may have grown
+                if desc.ksplit > 1:
+                    desc.workspace = self.ws.data_ptr()
+                if desc.tile == self.WINOV_TILE:
+                    desc.winov = self.winov.data_ptr()
             self.bind_side_workspace()
             return
         if all(self._tune_key(args, desc) in cache for args, desc in convs):
@@ -1369,6 +1382,8 @@ class NetPlan:
             for args, desc in convs:
                 if desc.ksplit > 1:
                     desc.workspace = self.ws.data_ptr()
+                if desc.tile == self.WINOV_TILE:
+                    desc.winov = self.winov.data_ptr()
             self.bind_side_workspace()
             return
         bufs = {id(t): t for t in self.act + self.grad if t is not None}
@@ -1456,9 +1471,11 @@ class NetPlan:
                 best = min((v, c) for c, v in score.items())
             self._set_tile(desc, best[1])
             cache[key] = list(best[1])
-        for name, _, desc in self.fwd_ops + self.bwd_ops:     # the workspace may have grown
+        for name, _, desc in self.fwd_ops + self.bwd_ops:     # the workspaces may have grown
             if name == "po_conv" and desc.ksplit > 1:
                 desc.workspace = self.ws.data_ptr()
+            if name == "po_conv" and desc.tile == self.WINOV_TILE:
+                desc.winov = self.winov.data_ptr()
         self.bind_side_workspace()
         with torch.no_grad():
             for t in bufs.values():
@@ -1517,12 +1534,29 @@ class NetPlan:
         del graph
         return ok
 
+    @staticmethod
+    def winov_floats(desc):
+        """Floats of tile 72's transformed-input workspace for launch desc
+        (include/advpatch.h po_conv_desc.winov)."""
+        tiles = desc.B * (-(-desc.Hg // 4)) * (-(-desc.Wg // 4))
+        return -(-tiles // 32) * (desc.Cin_p // 16) * 18432
+
+    def _ensure_winov(self, floats):
+        if getattr(self, "winov", None) is None or self.winov.numel() < floats:
+            self.winov = torch.empty(floats, device=self.device)
+        return self.winov
+
     def _apply_ws(self, desc):
         ks = desc.ksplit
         if ks > 1:
             desc.workspace = self._ensure_ws(ks * desc.B * desc.Hg * desc.Wg * desc.N).data_ptr()
         else:
             desc.workspace = None
+        if desc.tile == self.WINOV_TILE:
+            n = self.winov_floats(desc)
+            desc.winov, desc.winov_floats = self._ensure_winov(n).data_ptr(), n
+        else:
+            desc.winov, desc.winov_floats = None, 0
 
     # ---------------- execution ----------------
     def run_forward(self, x, base=None, roi=None):

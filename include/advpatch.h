@@ -33,7 +33,7 @@ typedef void* po_stream_t;
 #define PO_EHIP -2     /* HIP runtime error */
 #define PO_EDEVICE -3  /* device is not gfx950 */
 
-#define PO_ABI_VERSION 23
+#define PO_ABI_VERSION 24
 #define PO_AMAX_SUB 64  /* sub-slots per max|x| slot (see po_conv_desc) */
 
 int po_abi_version(void);
@@ -479,9 +479,15 @@ typedef struct po_conv_desc {
    * components][2][64 lanes][4] (Wwino's order with 36 components).  NULL:
    * tile 71 does not apply. */
   const float* Wwino6;
+  /* Optional (tile 72, ABI 24): DEVICE workspace of winov_floats floats for the
+   * transformed input V = B^T d B the tile writes before its GEMM:
+   * ceil(B*ceil(Hout/4)*ceil(Wout/4)/32) * (Cin_p/16) * 18432 floats.  NULL:
+   * tile 72 does not apply. */
+  float* winov;
+  int64_t winov_floats;
 } po_conv_desc;
 
-#define PO_CONV_NTILES 71
+#define PO_CONV_NTILES 72
 /* Tile `t` (1-based): block rows BM (output pixels), block columns BN (output
  * channels), k-step BK (input channels).  Tiles 1..10 stage operands through
  * registers, 11..20 are the same shapes staged by LDS-DMA, 27 a 128x256
@@ -515,6 +521,10 @@ typedef struct po_conv_desc {
  * CU walking the units; the same requirements as tile 70 and no fused pool.
  * Not bit-identical to the F(2x2) tiles (a different exact-arithmetic
  * factorisation); its error against float64 is tested per layer.
+ * 72 (exact fp32, ABI 24) is tile 71 with its input transform as a separate
+ * pass into winov: the GEMM kernel then loads its A fragments like its B
+ * fragments (no gathers, transform or LDS in its k-loop); the same
+ * requirements as tile 71 plus winov; the same results as tile 71 bit for bit.
  * Retired tiles (21..26, 28, 62..64: never selected by a tuner run) keep their
  * numbers; po_conv_tile_info reports them with *prec = -1 and po_conv refuses
  * them.  A tile that does not apply to a launch makes po_conv return

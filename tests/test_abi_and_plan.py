@@ -31,14 +31,14 @@ def test_library_exports_every_header_symbol():
     for name in sorted(declared):
         assert hasattr(lib, name), "libadvpatch_hip.so does not export %s" % name
     assert declared == set(nat.symbols()), declared ^ set(nat.symbols())
-    assert lib.po_abi_version() == nat.PO_ABI_VERSION == 23
+    assert lib.po_abi_version() == nat.PO_ABI_VERSION == 24
 
 
 def test_conv_desc_struct_matches_header():
     text = open(HEADER).read()
     body = text[text.index("typedef struct po_conv_desc"):text.index("} po_conv_desc;")]
     body = re.sub(r"/\*.*?\*/", "", body, flags=re.S)
-    fields = re.findall(r"(?:int|int8_t\*|int32_t\*|float\*|void\*)\s+([^;]+);", body)
+    fields = re.findall(r"(?:int64_t|int|int8_t\*|int32_t\*|float\*|void\*)\s+([^;]+);", body)
     names = []
     for f in fields:
         for part in f.split(","):

@@ -1,5 +1,6 @@
 """po_conv tile 71 (conv_wino6_k, csrc/conv_wino6.hip): Winograd F(4x4,3x3)
-as a persistent kernel.  It is a different exact-arithmetic factorisation of
+as a persistent kernel, and tile 72 (the same with the input transform as a
+pass of its own, bit-identical to 71).  It is a different exact-arithmetic factorisation of
 the same convolution, so it is compared with float64 torch conv2d (and with
 the direct fp32 kernel's own error beside it), and its epilogues with tile
 70's on the same descriptor: both tap orientations, ragged 4x4 tiles on odd
@@ -96,6 +97,18 @@ def test_tile71_epilogues_match_tile70(mode, B, H, Cin, Cout):
             assert torch.equal(bb1[~tie], bb0[~tie])
 
 
+_WINOV = []
+
+
+def _winov(d):
+    """Tile 72's transformed-input workspace for desc d (NaN-filled: every float
+    the GEMM reads must have been written by the transform pass)."""
+    n = (-(-(d.B * (-(-d.Hg // 4)) * (-(-d.Wg // 4))) // 32)) * (d.Cin_p // 16) * 18432
+    v = torch.full((n,), float("nan"), device=DEV)
+    _WINOV.append(v)
+    d.winov, d.winov_floats = v.data_ptr(), n
+
+
 def _run_with(nat, tile, mode, B, H, Cin, Cout, flip, U, U6, xd, wd, bias, prev, res, mbits, m2bits, ksplit=1,
               box=None):
     from test_gpu_wino5 import _run
@@ -108,6 +121,8 @@ def _run_with(nat, tile, mode, B, H, Cin, Cout, flip, U, U6, xd, wd, bias, prev,
         d.Wwino6 = U6.data_ptr()
         if box is not None:
             d.gbox = box.data_ptr()
+        if tile_ == 72:
+            _winov(d)
         return d
     w5._desc = desc6
     try:
@@ -178,6 +193,72 @@ def test_tile71_gradient_cone_boxes(boxes, mode, B, H, Cin, Cout, ks):
             assert float((a[fin] - b[fin]).abs().max()) <= tol * max(scale, 1e-30), mode
     y0 = runs[68][0]
     assert torch.equal(torch.where(inside, prev, y0), prev)           # tile 68 itself kept the outside
+
+
+def _equal(a, b):
+    for u, v in zip(a, b):
+        assert torch.equal(u.nan_to_num(7.0), v.nan_to_num(7.0))
+
+
+@pytest.mark.parametrize("mode", MODES)
+@pytest.mark.parametrize("B,H,Cin,Cout", [(2, 11, 64, 128), (3, 38, 256, 512), (2, 7, 32, 64), (16, 76, 128, 256),
+                                          (1, 19, 512, 64)])
+def test_tile72_bit_identical_to_71(mode, B, H, Cin, Cout):
+    """Tile 72 runs tile 71's transform (as a pass of its own, wino6_pre_k),
+    MFMA order and epilogues: every output bit for bit."""
+    nat = pkg_mod("_native")
+    flip = mode.startswith("dgrad")
+    xd, wd, bias, U, prev, res, mbits, m2bits = _inputs(B, H, Cin, Cout, flip, seed=H + Cin + 5)
+    U6 = _u6(wd, flip)
+    runs = [_run_with(nat, t, mode, B, H, Cin, Cout, flip, U, U6, xd, wd, bias, prev, res, mbits, m2bits)
+            for t in (72, 71)]
+    _equal(runs[0], runs[1])
+
+
+@pytest.mark.parametrize("Cin,ks", [(512, 2), (512, 3), (256, 3)])
+@pytest.mark.parametrize("mode", ["fwd_bits", "dgrad_acc_bits"])
+def test_tile72_split_k_bit_identical_to_71(mode, Cin, ks):
+    nat = pkg_mod("_native")
+    B, H, Cout = 4, 19, 256
+    flip = mode.startswith("dgrad")
+    xd, wd, bias, U, prev, res, mbits, m2bits = _inputs(B, H, Cin, Cout, flip, seed=23)
+    U6 = _u6(wd, flip)
+    runs = [_run_with(nat, t, mode, B, H, Cin, Cout, flip, U, U6, xd, wd, bias, prev, res, mbits, m2bits, ksplit=ks)
+            for t in (72, 71)]
+    _equal(runs[0], runs[1])
+
+
+@pytest.mark.parametrize("boxes", sorted(BOXES))
+@pytest.mark.parametrize("mode", ["dgrad_mask", "dgrad_dual"])
+@pytest.mark.parametrize("ks", [1, 2])
+def test_tile72_boxes_bit_identical_to_71(boxes, mode, ks):
+    nat = pkg_mod("_native")
+    B, H, Cin, Cout = 4, 38, 128, 64
+    flip = True
+    xd, wd, bias, U, prev, res, mbits, m2bits = _inputs(B, H, Cin, Cout, flip, seed=31)
+    U6 = _u6(wd, flip)
+    box = torch.tensor(BOXES[boxes](H), dtype=torch.int32, device=DEV)
+    runs = [_run_with(nat, t, mode, B, H, Cin, Cout, flip, U, U6, xd, wd, bias, prev, res, mbits, m2bits, box=box,
+                      ksplit=ks) for t in (72, 71)]
+    _equal(runs[0], runs[1])
+
+
+def test_tile72_needs_its_workspace():
+    nat = pkg_mod("_native")
+    B, H, Cin, Cout = 2, 16, 32, 64
+    xd, wd, bias, U, prev, res, mbits, m2bits = _inputs(B, H, Cin, Cout, False, seed=9)
+    U6 = _u6(wd, False)
+    y = torch.zeros(B, H, H, Cout, device=DEV)
+    d = _desc(nat, B, H, Cin, Cout, 72)
+    d.Wwino6 = U6.data_ptr()
+    call = lambda: nat.load().po_conv(ctypes.byref(d), nat.ptr(xd), nat.ptr(wd), None, nat.ptr(y), None, None, None,
+                                      None, None, nat.stream())
+    assert call() != 0 and "winov" in nat.last_error()
+    _winov(d)
+    d.winov_floats -= 1
+    assert call() != 0 and "workspace" in nat.last_error()
+    d.winov_floats += 1
+    assert call() == 0
 
 
 def test_tile71_refuses_what_it_cannot_run():

@@ -33,13 +33,17 @@ if os.environ.get("MICRO_PREC", "0") == "1":          # fp16x3 operands
     wf._frag = {}
     d.Wfrag = wf._frag16(w)                             # fragment-ordered copy (tiles 57..60)
 d.tile = int(os.environ.get("MICRO_TILE", "0"))
-if d.tile in (61, 62, 63, 64, 65, 66, 67, 68, 70, 71):                                 # Winograd: transformed weights
+if d.tile in (61, 62, 63, 64, 65, 66, 67, 68, 70, 71, 72):                             # Winograd: transformed weights
     offs = [(d.dh[t], d.dw[t]) for t in range(9)]
     U = ge._pkg("darknet_v3").wino_transform(w, offs)
     d.Wwino = U.data_ptr()
-    if d.tile == 71:                                                                     # F(4x4,3x3)
+    if d.tile in (71, 72):                                                               # F(4x4,3x3)
         U6 = ge._pkg("darknet_v3").wino6_transform(w, offs)
         d.Wwino6 = U6.data_ptr()
+    if d.tile == 72:                                                                     # its transformed input
+        nv = ge._pkg("darknet_v3").NetPlan.winov_floats(d)
+        winov = torch.empty(nv, device=dev)
+        d.winov, d.winov_floats = winov.data_ptr(), nv
 ws = None
 if int(os.environ.get("MICRO_KSPLIT", "1")) > 1:        # split-K slices + conv_reduce_k
     d.ksplit = int(os.environ["MICRO_KSPLIT"])

@@ -1,8 +1,8 @@
 """Drop the Winograd choices of a committed tile cache so the next bench run
 re-times those launch shapes against every tile: mode "unboxed" (default)
-drops the full-map ones (tiles 65-68, 70), to weigh the persistent tiles 70
-(F(2x2,3x3)) and 71 (F(4x4,3x3)); mode "boxed" the gradient-cone ones
-(tiles 65-68), to weigh tile 71's boxed launches.
+drops the full-map ones (tiles 65-68, 70-72), to weigh the persistent tiles 70
+(F(2x2,3x3)), 71 and 72 (F(4x4,3x3)); mode "boxed" the gradient-cone ones
+(tiles 65-68, 71, 72), to weigh tiles 71/72 on boxed launches.
 Usage: python tools/retune_wino.py IN.json OUT.json [unboxed|boxed]"""
 import json
 import sys
@@ -15,7 +15,7 @@ for k, v in cache.items():
     key = json.loads(k)
     tile = v[0] if isinstance(v, list) else v
     boxed = bool(key[15])
-    if tile in (65, 66, 67, 68, 70) and boxed == (mode == "boxed"):
+    if tile in (65, 66, 67, 68, 70, 71, 72) and boxed == (mode == "boxed"):
         continue
     keep[k] = v
 json.dump(keep, open(dst, "w"))

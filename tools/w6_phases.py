@@ -1,4 +1,4 @@
-"""Phase timing of tile 71 (conv_wino6_k) from a diagnostic build with
+"""Phase timing of tile 71 / 72 (W6_TILE; conv_wino6_k) from a diagnostic build with
 per-workgroup s_memtime sums (-DPO_W6_STAMP):
     OUT=tools/abl_push bash tools/build_ablate.sh w6stamp -DPO_W6_STAMP
     MICRO_LIB=tools/abl_push/libadvpatch_w6stamp.so python tools/w6_phases.py B H Cin Cout [ksplit]
@@ -30,10 +30,14 @@ d.B, d.Hin, d.Win, d.Cin_p, d.Hout, d.Wout, d.Cout_p, d.Hg, d.Wg = B, H, H, Cin,
 d.in_step, d.out_step, d.out_oy, d.out_ox, d.ntaps = 1, 1, 0, 0, 9
 for t in range(9):
     d.dh[t], d.dw[t] = t // 3 - 1, t % 3 - 1
-d.N, d.act, d.accumulate, d.tile = Cout, 1, 0, 71
+d.N, d.act, d.accumulate, d.tile = Cout, 1, 0, int(os.environ.get("W6_TILE", "71"))
 offs = [(d.dh[t], d.dw[t]) for t in range(9)]
 U6 = dk.wino6_transform(w, offs)
 d.Wwino6 = U6.data_ptr()
+if d.tile == 72:                                 # the pre-transformed input's workspace
+    nv = dk.NetPlan.winov_floats(d)
+    winov = torch.empty(nv, device=dev)
+    d.winov, d.winov_floats = winov.data_ptr(), nv
 mode = os.environ.get("W6_MODE", "resy")       # resy: y + sum + bits; res: sum + bits (the plan's); y: y only
 if mode != "y":
     d.ybits = bits.data_ptr()
