@@ -56,7 +56,7 @@ for k, (name, args, desc) in enumerate(plan.bwd_ops):
     res = {"k": k, "Hg": desc.Hg, "Cin_p": desc.Cin_p, "N": desc.N, "ntaps": desc.ntaps, "cur": cur,
            "live_wg": live, "mfma_flops": plan.launch_mfma_flops(desc, cones), "t": {}}
     if cur[0] in plan.WINO_TILES:
-        cands = [(t, ks) for t in (66, 67, 68, 71) for ks in (1, 2, 3, 4, 6, 8) if desc.Cin_p // 16 // ks >= 2]
+        cands = [(t, ks) for t in (66, 67, 68, 71, 72) for ks in (1, 2, 3, 4, 6, 8) if desc.Cin_p // 16 // ks >= 2]
     else:
         cands = [(t, ks) for t in (3, 5, 7, 9, 13, 15, 17, 19) for ks in (1, 2, 4, 8)
                  if desc.ntaps * desc.Cin_p // plan.tile_shape(t)[2] // ks >= 2]
