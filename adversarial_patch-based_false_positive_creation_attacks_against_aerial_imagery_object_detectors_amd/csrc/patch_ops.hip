@@ -647,7 +647,9 @@ struct WarpInv {
   double a[6], m[4];
   float cb, bb;
 };
-template <int WB_EL, int WB_G>
+// IL: gfac interleaved [B][S][S][4] (the footprint-box forms: one 16-byte load
+// per candidate pixel instead of one 4-byte load from each of three planes)
+template <int WB_EL, int WB_G, bool IL>
 __global__ __launch_bounds__(256) void warp_bwd_b_k(const float* __restrict__ gfac,
                                                     const float* __restrict__ mp,
                                                     const float* __restrict__ noise,
@@ -664,6 +666,13 @@ __global__ __launch_bounds__(256) void warp_bwd_b_k(const float* __restrict__ gf
   const int pr = e / g.P, pc = e % g.P;
   const int r = pr + g.padT, c = pc + g.padL;
   const size_t plane = (size_t)g.S * g.S;
+  // the element's patch values (the clamp test's t = mp * contrast + bright),
+  // requested once before the table build instead of after each image's
+  // candidate gathers (one dependent round trip less per image)
+  float mpv[3] = {0.f, 0.f, 0.f};
+  if (!g.pre)
+#pragma unroll
+    for (int ch = 0; ch < 3; ++ch) mpv[ch] = mp[((size_t)ch * g.P + pr) * g.P + pc];
   float d0 = 0.f, d1 = 0.f, d2 = 0.f;
   for (int bc = 0; bc < B; bc += WB_CH) {
     const int nb = min(WB_CH, B - bc);
@@ -704,7 +713,7 @@ __global__ __launch_bounds__(256) void warp_bwd_b_k(const float* __restrict__ gf
       const NoiseSrc nz = noise_src(noise, g, b);
       float a0 = 0.f, a1 = 0.f, a2 = 0.f;
       bool cand = false;
-      const float* gb = gfac + (size_t)b * 3 * plane;
+      const float* gb = gfac + (size_t)b * (IL ? 4 : 3) * plane;
       for (int i = i0; i <= i1; ++i)
         for (int j = j0; j <= j1; ++j) {
           double ix, iy;
@@ -716,7 +725,17 @@ __global__ __launch_bounds__(256) void warp_bwd_b_k(const float* __restrict__ gf
           if (dx < 0 || dx > 1 || dy < 0 || dy > 1) continue;
           const float w = wb[2 * dy + dx];
           const size_t o = (size_t)i * g.S + j;
-          const float gv[3] = {gb[o], gb[o + plane], gb[o + 2 * plane]};
+          float gv[3];
+          if constexpr (IL) {
+            const float4 v4 = *reinterpret_cast<const float4*>(gb + 4 * o);
+            gv[0] = v4.x;
+            gv[1] = v4.y;
+            gv[2] = v4.z;
+          } else {
+            gv[0] = gb[o];
+            gv[1] = gb[o + plane];
+            gv[2] = gb[o + 2 * plane];
+          }
           a0 += w * gv[0];
           a1 += w * gv[1];
           a2 += w * gv[2];
@@ -742,7 +761,7 @@ __global__ __launch_bounds__(256) void warp_bwd_b_k(const float* __restrict__ gf
           // (nz in [-1, 1)): rounding is monotonic, so pre lies in [fl(t - 0.1f),
           // fl(t + 0.1f)], and when that interval is inside [0, 1] the clamp
           // test passes whatever the noise -- its Philox call is skipped
-          const float t = mp[po_] * cb + bb;
+          const float t = mpv[ch] * cb + bb;
           if (t - 0.1f >= 0.f && t + 0.1f <= 1.f) {
             in = true;
           } else {
@@ -769,13 +788,23 @@ __global__ __launch_bounds__(256) void warp_bwd_b_k(const float* __restrict__ gf
 }
 
 void launch_bwd_b(const float* gfac, const float* mp, const float* noise, const float* contrast, const float* bright,
-                  const double* affine, const WarpGeom& g, int B, int P, float* d_mp, hipStream_t st) {
-  if (B > 32)
-    hipLaunchKernelGGL((warp_bwd_b_k<8, 32>), dim3(po::ceil_div(P * P, 8)), dim3(256), 0, st, gfac, mp, noise,
-                       contrast, bright, affine, g, B, d_mp);
-  else
-    hipLaunchKernelGGL((warp_bwd_b_k<32, 8>), dim3(po::ceil_div(P * P, 32)), dim3(256), 0, st, gfac, mp, noise,
-                       contrast, bright, affine, g, B, d_mp);
+                  const double* affine, const WarpGeom& g, int B, int P, float* d_mp, hipStream_t st,
+                  bool il = false) {
+  if (B > 32) {
+    if (il)
+      hipLaunchKernelGGL((warp_bwd_b_k<8, 32, true>), dim3(po::ceil_div(P * P, 8)), dim3(256), 0, st, gfac, mp, noise,
+                         contrast, bright, affine, g, B, d_mp);
+    else
+      hipLaunchKernelGGL((warp_bwd_b_k<8, 32, false>), dim3(po::ceil_div(P * P, 8)), dim3(256), 0, st, gfac, mp,
+                         noise, contrast, bright, affine, g, B, d_mp);
+  } else {
+    if (il)
+      hipLaunchKernelGGL((warp_bwd_b_k<32, 8, true>), dim3(po::ceil_div(P * P, 32)), dim3(256), 0, st, gfac, mp,
+                         noise, contrast, bright, affine, g, B, d_mp);
+    else
+      hipLaunchKernelGGL((warp_bwd_b_k<32, 8, false>), dim3(po::ceil_div(P * P, 32)), dim3(256), 0, st, gfac, mp,
+                         noise, contrast, bright, affine, g, B, d_mp);
+  }
 }
 
 // L patches per image composited in slot order (PatchApplier, load_data.py:
@@ -1005,7 +1034,8 @@ __global__ __launch_bounds__(256) void warp_box_fwd_k(const float* __restrict__ 
 }
 
 // phase A of the backward over the footprint box only (phase B reads gfac at
-// footprint pixels only)
+// footprint pixels only), gfac interleaved [B][S][S][4]: one 16-byte store
+// per pixel, read back by phase B as one 16-byte load per candidate
 __global__ __launch_bounds__(256) void warp_box_bwd_a_k(const float* __restrict__ d_out,
                                                         const float* __restrict__ mp,
                                                         const float* __restrict__ contrast,
@@ -1026,6 +1056,7 @@ __global__ __launch_bounds__(256) void warp_box_bwd_a_k(const float* __restrict_
     float adv[3], msk;
     bool rng[3];
     if (!warp_pixel(affine + 6 * b, g, mp, nz, cb, bb, i, j, adv, msk, rng)) continue;
+    float gv4[4] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int ch = 0; ch < 3; ++ch) {
       const float outv = adv[ch] * msk;
@@ -1033,8 +1064,10 @@ __global__ __launch_bounds__(256) void warp_box_bwd_a_k(const float* __restrict_
       if (mode == 1 && outv == 0.f) gv = 0.f;
       gv = gv * msk;
       if (!rng[ch]) gv = 0.f;
-      gfac[o + ch * plane] = gv;
+      gv4[ch] = gv;
     }
+    *reinterpret_cast<float4*>(gfac + ((size_t)b * plane + (size_t)i * g.S + j) * 4) =
+        make_float4(gv4[0], gv4[1], gv4[2], gv4[3]);
   }
 }
 
@@ -1100,6 +1133,7 @@ extern "C" int po_warp_bwd_pre(const float* d_out, const float* pre, const float
   PO_REQUIRE(B > 0 && S > 1 && P > 0 && P <= S, "po_warp_bwd_pre: bad shape");
   PO_REQUIRE(3LL * P * P < (1LL << 31), "po_warp_bwd_pre: patch too large");
   PO_REQUIRE(work != d_out, "po_warp_bwd_pre: work may not alias d_out");
+  PO_REQUIRE((uintptr_t)work % 16 == 0, "po_warp_bwd_pre: work must be 16-byte aligned");
   WarpGeom g = make_geom(S, P);
   g.pre = pre;
   hipStream_t st = po::stream_of(s);
@@ -1107,7 +1141,7 @@ extern "C" int po_warp_bwd_pre(const float* d_out, const float* pre, const float
                      affine, roi, g, mode, work);
   int rc = po::check_launch("po_warp_bwd_pre(a)");
   if (rc) return rc;
-  launch_bwd_b(work, pre, nullptr, contrast, nullptr, affine, g, B, P, d_patch_mp, st);
+  launch_bwd_b(work, pre, nullptr, contrast, nullptr, affine, g, B, P, d_patch_mp, st, true);
   return po::check_launch("po_warp_bwd_pre(b)");
 }
 
@@ -1121,13 +1155,14 @@ extern "C" int po_warp_box_bwd_keyed(const float* d_out, const float* patch_mp, 
   PO_REQUIRE(B > 0 && S > 1 && P > 0 && P <= S && b0 >= 0, "po_warp_box_bwd_keyed: bad shape");
   PO_REQUIRE(3LL * P * P < (1LL << 31), "po_warp_box_bwd_keyed: patch too large");
   PO_REQUIRE(work != d_out, "po_warp_box_bwd_keyed: work may not alias d_out");
+  PO_REQUIRE((uintptr_t)work % 16 == 0, "po_warp_box_bwd_keyed: work must be 16-byte aligned");
   const WarpGeom g = make_geom(S, P, seed, counter, b0);
   hipStream_t st = po::stream_of(s);
   hipLaunchKernelGGL(warp_box_bwd_a_k, dim3(box_blocks(S), B), dim3(256), 0, st, d_out, patch_mp, contrast, bright,
                      affine, roi, g, mode, work);
   int rc = po::check_launch("po_warp_box_bwd_keyed(a)");
   if (rc) return rc;
-  launch_bwd_b(work, patch_mp, nullptr, contrast, bright, affine, g, B, P, d_patch_mp, st);
+  launch_bwd_b(work, patch_mp, nullptr, contrast, bright, affine, g, B, P, d_patch_mp, st, true);
   return po::check_launch("po_warp_box_bwd_keyed(b)");
 }
 

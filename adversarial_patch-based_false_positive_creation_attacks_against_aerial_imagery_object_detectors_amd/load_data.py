@@ -281,9 +281,11 @@ class _Warp(torch.autograd.Function):
     def backward(ctx, d_out):
         mp, contrast, bright, affine = ctx.saved_tensors[:4]
         d_out = d_out.contiguous()
-        work = torch.empty_like(d_out)
-        d_mp = torch.empty_like(mp)
         B, P = affine.size(0), mp.size(-1)
+        # the footprint-box forms keep their per-pixel factors interleaved [B,S,S,4]
+        work = (torch.empty(B * ctx.S * ctx.S * 4, device=d_out.device) if ctx.form in ("box", "pre")
+                else torch.empty_like(d_out))
+        d_mp = torch.empty_like(mp)
         key = tuple(int(v) & 0xFFFFFFFFFFFFFFFF for v in ctx.key[:2]) + (int(ctx.key[2]),) if ctx.key else None
         if ctx.form == "box":
             roi = ctx.saved_tensors[4]

@@ -46,7 +46,8 @@ PEAK_CONV = {"fp32": PEAK_FP32_MFMA_TFLOPS, "fp16x3": PEAK_FP16_MFMA_TFLOPS / 3.
 # kernel of each specialised po_conv tile (others: the generic conv_k<BM,BN,WM,BK>)
 TILE_KERNELS = {61: "conv_wino_k", 65: "conv_wino2_k", 66: "conv_wino3_k", 67: "conv_wino4_k",
                 68: "conv_wino4_k<stagger>", 69: "conv_halo_pool_k",
-                70: "conv_wino5_k (persistent)"}
+                70: "conv_wino5_k (persistent)", 71: "conv_wino6_k (F(4x4), persistent)",
+                72: "wino6_pre_k + conv_wino6_k<PT> (F(4x4), pre-transformed input)"}
 
 CONFIGS = {
     # name: (cfg, S, P, default per-GPU batch)
@@ -295,9 +296,9 @@ def roofline(cfg_name, B, prec, m, ref_flops_step):
         r["frac_mfma"] = r["achieved_mfma"] / peak
         r["achieved"], r["frac"] = r["achieved_mfma"], r["frac_mfma"]
         r["achieved_is"] = r["frac_mfma_is"] = (
-            "FLOPs the matrix cores execute (v_mfma_f32_32x32x2_f32: padded tiles, Winograd at 16 GEMMs per 2x2 "
-            "tile = 4/9 of the direct work; NetPlan.launch_mfma_flops) / conv time / the 157.3 TFLOP/s peak at "
-            "2.4 GHz: the MFMA utilisation of the conv launches")
+            "FLOPs the matrix cores execute (v_mfma_f32_32x32x2_f32: padded tiles, Winograd F(2x2) at 16 GEMMs "
+            "per 2x2 tile = 4/9 of the direct work, F(4x4) at 36 per 4x4 tile = 1/4; NetPlan.launch_mfma_flops) "
+            "/ conv time / the 157.3 TFLOP/s peak at 2.4 GHz: the MFMA utilisation of the conv launches")
         r["families"] = {k: {"ms_per_step": f["ms"], "launches_per_step": f["launches"],
                              "mfma_tflops": f["mfma_flops"] / (f["ms"] * 1e-3) / 1e12 if f["ms"] else None,
                              "frac_mfma": f["mfma_flops"] / (f["ms"] * 1e-3) / 1e12 / peak if f["ms"] else None,

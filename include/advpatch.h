@@ -136,7 +136,8 @@ int po_warp_bwd_keyed(const float* d_out, const float* patch_mp, uint64_t seed, 
  * boxes {x0, y0, x1, y1}: the pixels outside an image's box are written as
  * 16-byte copies of img (mode 1) or zeros (mode 0) without per-pixel geometry,
  * the box's pixels one per thread; the backward's per-pixel phase runs over the
- * boxes only (`work` must not alias d_out). */
+ * boxes only (`work`: >= 4*B*S*S floats, 16-byte aligned, not aliasing d_out:
+ * the per-pixel factors interleaved [B][S][S][4]). */
 int po_augment_patch(const float* patch_mp, uint64_t seed, uint64_t counter, int b0, const float* contrast,
                      const float* bright, int B, int P, float* pre, po_stream_t s);
 int po_warp_fwd_pre(const float* img, const float* pre, const double* affine, const int32_t* roi, int B, int S,

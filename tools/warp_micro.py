@@ -33,7 +33,7 @@ off = affine.clone()
 off[:, 2] += 4 * S                      # every sample point far right of the patch: no footprint pixel
 roi_off = torch.zeros_like(roi)          # ... and an empty footprint box
 out = torch.empty(B, 3, S, S, device=dev)
-work = torch.empty(B, 3, S, S, device=dev)
+work = torch.empty(B * S * S * 4, device=dev)             # the box forms: [B,S,S,4] interleaved factors
 d_out = torch.randn(B, 3, S, S, device=dev)
 d_mp = torch.empty(3, P, P, device=dev)
 fwd_bytes = B * 2 * 3 * S * S * 4 + 3 * P * P * 4
