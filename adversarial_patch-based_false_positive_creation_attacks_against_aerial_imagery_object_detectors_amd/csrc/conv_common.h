@@ -285,6 +285,14 @@ __device__ __forceinline__ void conv_epilogue(const ConvArgs& a, const floatx16 
   float* scr = smem + wave * 1024;
   const int rr = lane >> 3, cc = (lane & 7) * 4;
   float my = 0.f, ms = 0.f, my2 = 0.f;
+  // the bias of every column tile, requested before the first store (a load
+  // issued after a store waits for it on the shared vmcnt)
+  float4 bvs[TN];
+#pragma unroll
+  for (int j = 0; j < TN; ++j) {
+    const int n = n0 + wn * TN * 32 + j * 32 + cc;
+    bvs[j] = (a.bias && n < a.N) ? *reinterpret_cast<const float4*>(a.bias + n) : make_float4(0.f, 0.f, 0.f, 0.f);
+  }
 #pragma unroll
   for (int i = 0; i < TM; ++i)
 #pragma unroll
@@ -295,8 +303,7 @@ __device__ __forceinline__ void conv_epilogue(const ConvArgs& a, const floatx16 
         scr[((e & 3) + 8 * (e >> 2) + 4 * (lane >> 5)) * 32 + (lane & 31)] = acc[i][j][e];
       __builtin_amdgcn_wave_barrier();
       const int n = n0 + wn * TN * 32 + j * 32 + cc;
-      float4 bv = make_float4(0.f, 0.f, 0.f, 0.f);
-      if (a.bias && n < a.N) bv = *reinterpret_cast<const float4*>(a.bias + n);
+      const float4 bv = bvs[j];
       const int wpp = a.Cout_p >> 5;            // sign-bit words per pixel (bits need Cout_p % 32 == 0)
       // load phase: the rows' shortcut operand, accumulated destination and
       // mask words, all before the first store (gfx9 counts stores and loads

@@ -6,7 +6,7 @@ OUT=gpurun_out/${TAGOUT:-ab}
 mkdir -p $OUT
 for rnd in $(seq ${ROUNDS:-2}); do
 for lib in ${LIBS:-base}; do
-  L=""; [ $lib != base ] && L=tools/abl/libadvpatch_$lib.so
+  L=""; [ $lib != base ] && L=${ABLDIR:-tools/abl}/libadvpatch_$lib.so
   ADVPATCH_LIB=$L timeout -k 10 400 python -u bench.py --prec fp32 --no-cpu-baseline > $OUT/bench_${lib}_$rnd.json 2> $OUT/bench_${lib}_$rnd.err || exit 1
   python3 -c "
 import json,sys; d=json.loads(open('$OUT/bench_${lib}_$rnd.json').read().strip().splitlines()[-1])
