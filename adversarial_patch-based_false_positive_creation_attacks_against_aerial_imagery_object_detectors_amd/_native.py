@@ -14,7 +14,7 @@ LIB_PATH = os.environ.get("ADVPATCH_LIB") or os.path.join(_HERE, "libadvpatch_hi
 
 c_int, c_float, c_int64, c_void_p = ctypes.c_int, ctypes.c_float, ctypes.c_int64, ctypes.c_void_p
 
-PO_ABI_VERSION = 24   # include/advpatch.h
+PO_ABI_VERSION = 25   # include/advpatch.h
 PO_CONV_NTILES = 72   # include/advpatch.h
 PO_AMAX_SUB = 64      # sub-slots per max|x| slot
 
@@ -106,6 +106,10 @@ _SIGS = {
                               c_int, c_int, c_void_p, c_void_p, c_void_p],
     "po_conv_first_pool_fwd_cmp": [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_void_p, c_void_p, c_int, c_int,
                                    c_int, c_void_p, c_void_p, c_void_p, c_void_p],
+    "po_conv_first_pool_wino_fwd": [c_void_p, c_int, c_int, c_int, c_void_p, c_void_p, c_int, c_int, c_int,
+                                    c_void_p, c_void_p, c_void_p, c_void_p],
+    "po_conv_first_pool_wino_fwd_cmp": [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_void_p, c_void_p, c_int,
+                                        c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p],
     "po_conv_first_dgrad": [c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_int, c_int, c_void_p,
                             c_void_p, c_void_p],
     "po_slice_accum": [c_void_p, c_int, c_int, c_void_p, c_int, c_int, c_int64, c_int, c_int,

@@ -196,7 +196,14 @@ __global__ __launch_bounds__(256) void first_fwd2_k(const float* __restrict__ im
 // (slope 0.1 in the backward).  Pooled floats are staged through LDS for
 // fully coalesced 16-byte stores; each thread's CO argmax bytes are one or two
 // contiguous 16-byte stores.
-template <int CO>
+// WINO: the conv as Winograd F(2x2,3x3) -- the pooled pixel's 2x2 conv outputs
+// are one F(2x2) output tile: V = B^T d B of the 4x4 input patch per channel
+// (adds only), 16 products per channel and output channel against Wt = U =
+// G g G^T ([CO][3][16], po_conv_first_pool_wino_fwd), Y = A^T M A -- 768
+// products per pooled pixel instead of 1728, the same pool rule and argmax
+// codes after it.  Not bit-identical to the direct form (another exact
+// factorisation of the same sums).
+template <int CO, bool WINO>
 __global__ __launch_bounds__(256) void first_pool_fwd_k(const float* __restrict__ img, int B, int H, int W,
                                                         int Hp, int Wp, const float* __restrict__ Wt,
                                                         const float* __restrict__ bias, int Cout, int act,
@@ -256,12 +263,40 @@ __global__ __launch_bounds__(256) void first_pool_fwd_k(const float* __restrict_
         for (int c = 0; c < 3; ++c) xa[c][r][q] = ok ? src[(size_t)c * H * W] : 0.f;
       }
   }
+  // WINO: vw[c][k] = {V[2k], V[2k+1]} of V = B^T d B (row-major 4x4), channel c;
+  // the row combinations of B^T run packed over column pairs
+  f2_t vw[WINO ? 3 : 1][8];
+  if constexpr (WINO) {
 #pragma unroll
-  for (int c = 0; c < 3; ++c)
+    for (int c = 0; c < 3; ++c) {
+      f2_t d[4][2], t[4][2];
 #pragma unroll
-    for (int r = 0; r < 4; ++r)
+      for (int r = 0; r < 4; ++r) {
+        d[r][0] = (f2_t){xa[c][r][0], xa[c][r][1]};
+        d[r][1] = (f2_t){xa[c][r][2], xa[c][r][3]};
+      }
 #pragma unroll
-      for (int q = 0; q < 3; ++q) xp[c][r][q] = (f2_t){xa[c][r][q], xa[c][r][q + 1]};
+      for (int h = 0; h < 2; ++h) {                  // t = B^T d
+        t[0][h] = d[0][h] - d[2][h];
+        t[1][h] = d[1][h] + d[2][h];
+        t[2][h] = d[2][h] - d[1][h];
+        t[3][h] = d[1][h] - d[3][h];
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {                  // V = t B (columns combined)
+        const float a0 = t[i][0][0], a1 = t[i][0][1], a2 = t[i][1][0], a3 = t[i][1][1];
+        vw[c][2 * i] = (f2_t){a0 - a2, a1 + a2};
+        vw[c][2 * i + 1] = (f2_t){a2 - a1, a1 - a3};
+      }
+    }
+  } else {
+#pragma unroll
+    for (int c = 0; c < 3; ++c)
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+#pragma unroll
+        for (int q = 0; q < 3; ++q) xp[c][r][q] = (f2_t){xa[c][r][q], xa[c][r][q + 1]};
+  }
   float vmax = 0.f;
   uint32_t aw[CO / 4];
 #pragma unroll
@@ -271,21 +306,51 @@ __global__ __launch_bounds__(256) void first_pool_fwd_k(const float* __restrict_
     float bv = 0.f;
     uint32_t code = 0u;
     if (co < Cout) {                                 // wave-uniform
-      f2_t s0 = {0.f, 0.f}, s1 = {0.f, 0.f};
+      float v[4];                                    // window positions k = 2 dy + dx
+      const float bco = bias ? bias[co] : 0.f;
+      if constexpr (WINO) {
+        // M = sum over channels of U * V, packed over element pairs; the bias
+        // enters through M[1][1] (element 5), which A^T M A adds to all four
+        // outputs once
+        const f2_t* U2 = reinterpret_cast<const f2_t*>(Wt) + co * 24;
+        f2_t m[8];
 #pragma unroll
-      for (int c = 0; c < 3; ++c)
+        for (int k = 0; k < 8; ++k) {
+          const f2_t init = k == 2 ? (f2_t){0.f, bco} : (f2_t){0.f, 0.f};
+          f2_t acc = __builtin_elementwise_fma(U2[k], vw[0][k], init);
+          acc = __builtin_elementwise_fma(U2[8 + k], vw[1][k], acc);
+          m[k] = __builtin_elementwise_fma(U2[16 + k], vw[2][k], acc);
+        }
+        f2_t s0[2], s1[2];                           // A^T M: rows (1 1 1 0), (0 1 -1 -1)
 #pragma unroll
-        for (int kh = 0; kh < 3; ++kh)
+        for (int h = 0; h < 2; ++h) {
+          s0[h] = (m[h] + m[2 + h]) + m[4 + h];
+          s1[h] = (m[2 + h] - m[4 + h]) - m[6 + h];
+        }
+        v[0] = (s0[0][0] + s0[0][1]) + s0[1][0];      // (A^T M) A
+        v[1] = (s0[0][1] - s0[1][0]) - s0[1][1];
+        v[2] = (s1[0][0] + s1[0][1]) + s1[1][0];
+        v[3] = (s1[0][1] - s1[1][0]) - s1[1][1];
+      } else {
+        f2_t s0 = {0.f, 0.f}, s1 = {0.f, 0.f};
 #pragma unroll
-          for (int kw = 0; kw < 3; ++kw) {
-            const f2_t w = (f2_t)(Wt[co * 27 + c * 9 + kh * 3 + kw]);
-            s0 = __builtin_elementwise_fma(w, xp[c][kh][kw], s0);
-            s1 = __builtin_elementwise_fma(w, xp[c][kh + 1][kw], s1);
-          }
-      const f2_t bb = (f2_t)(bias ? bias[co] : 0.f);
-      s0 += bb;
-      s1 += bb;
-      float v[4] = {s0[0], s0[1], s1[0], s1[1]};     // window positions k = 2 dy + dx
+        for (int c = 0; c < 3; ++c)
+#pragma unroll
+          for (int kh = 0; kh < 3; ++kh)
+#pragma unroll
+            for (int kw = 0; kw < 3; ++kw) {
+              const f2_t w = (f2_t)(Wt[co * 27 + c * 9 + kh * 3 + kw]);
+              s0 = __builtin_elementwise_fma(w, xp[c][kh][kw], s0);
+              s1 = __builtin_elementwise_fma(w, xp[c][kh + 1][kw], s1);
+            }
+        const f2_t bb = (f2_t)bco;
+        s0 += bb;
+        s1 += bb;
+        v[0] = s0[0];
+        v[1] = s0[1];
+        v[2] = s1[0];
+        v[3] = s1[1];
+      }
       if (act) {
 #pragma unroll
         for (int k = 0; k < 4; ++k) v[k] = po::leaky(v[k]);
@@ -414,7 +479,7 @@ int first_fwd(const float* img, const float* pimg, const int32_t* roi, int B, in
 
 int first_pool_fwd(const float* img, const float* pimg, const int32_t* roi, int B, int H, int W, const float* Wt,
                    const float* bias, int Cout, int Cout_p, int act, float* y, int8_t* argmax, uint32_t* amax,
-                   po_stream_t s) {
+                   po_stream_t s, bool wino = false) {
   PO_REQUIRE(img && Wt && y && argmax, "po_conv_first_pool_fwd: null pointer");
   PO_REQUIRE((Cout_p == 16 || Cout_p == 32) && Cout > 0 && Cout <= Cout_p,
              "po_conv_first_pool_fwd: Cout_p must be 16 or 32 (got %d, Cout %d)", Cout_p, Cout);
@@ -426,12 +491,20 @@ int first_pool_fwd(const float* img, const float* pimg, const int32_t* roi, int 
              "po_conv_first_pool_fwd: image batch must be < 2 GiB");
   hipStream_t st = po::stream_of(s);
   dim3 grid(po::ceil_div(n, 256));
-  if (Cout_p == 16)
-    hipLaunchKernelGGL(first_pool_fwd_k<16>, grid, dim3(256), 0, st, img, B, H, W, Hp, Wp, Wt, bias, Cout, act, y,
-                       argmax, amax, pimg, roi);
-  else
-    hipLaunchKernelGGL(first_pool_fwd_k<32>, grid, dim3(256), 0, st, img, B, H, W, Hp, Wp, Wt, bias, Cout, act, y,
-                       argmax, amax, pimg, roi);
+  if (wino) {
+    if (Cout_p == 16)
+      hipLaunchKernelGGL((first_pool_fwd_k<16, true>), grid, dim3(256), 0, st, img, B, H, W, Hp, Wp, Wt, bias, Cout, act,
+                         y, argmax, amax, pimg, roi);
+    else
+      hipLaunchKernelGGL((first_pool_fwd_k<32, true>), grid, dim3(256), 0, st, img, B, H, W, Hp, Wp, Wt, bias, Cout, act,
+                         y, argmax, amax, pimg, roi);
+  } else if (Cout_p == 16) {
+    hipLaunchKernelGGL((first_pool_fwd_k<16, false>), grid, dim3(256), 0, st, img, B, H, W, Hp, Wp, Wt, bias, Cout, act,
+                       y, argmax, amax, pimg, roi);
+  } else {
+    hipLaunchKernelGGL((first_pool_fwd_k<32, false>), grid, dim3(256), 0, st, img, B, H, W, Hp, Wp, Wt, bias, Cout, act,
+                       y, argmax, amax, pimg, roi);
+  }
   return po::check_launch("po_conv_first_pool_fwd");
 }
 }  // namespace
@@ -460,6 +533,19 @@ extern "C" int po_conv_first_pool_fwd_cmp(const float* img, const float* pimg, c
                                           int8_t* argmax, uint32_t* amax, po_stream_t s) {
   PO_REQUIRE(pimg, "po_conv_first_pool_fwd_cmp: null composite");
   return first_pool_fwd(img, pimg, roi, B, H, W, Wt, bias, Cout, Cout_p, act, y, argmax, amax, s);
+}
+
+extern "C" int po_conv_first_pool_wino_fwd(const float* img, int B, int H, int W, const float* U, const float* bias,
+                                           int Cout, int Cout_p, int act, float* y, int8_t* argmax, uint32_t* amax,
+                                           po_stream_t s) {
+  return first_pool_fwd(img, nullptr, nullptr, B, H, W, U, bias, Cout, Cout_p, act, y, argmax, amax, s, true);
+}
+
+extern "C" int po_conv_first_pool_wino_fwd_cmp(const float* img, const float* pimg, const int32_t* roi, int B, int H,
+                                               int W, const float* U, const float* bias, int Cout, int Cout_p,
+                                               int act, float* y, int8_t* argmax, uint32_t* amax, po_stream_t s) {
+  PO_REQUIRE(pimg, "po_conv_first_pool_wino_fwd_cmp: null composite");
+  return first_pool_fwd(img, pimg, roi, B, H, W, U, bias, Cout, Cout_p, act, y, argmax, amax, s, true);
 }
 
 extern "C" int po_conv_first_dgrad(const float* D, int B, int H, int W, int stride, const float* Wt,

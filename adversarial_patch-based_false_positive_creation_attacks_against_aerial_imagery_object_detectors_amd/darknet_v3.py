@@ -256,6 +256,8 @@ class NetPlan:
                            and self.cp[0] in (16, 32) and self.win[0] is None and self.win[1] is None
                            and [j for j in range(n) if 0 in srcs[j]] == [1]
                            and os.environ.get("ADVPATCH_FIRST_POOL", "1") != "0")
+        # ... computed as Winograd F(2x2,3x3) (po_conv_first_pool_wino_fwd)
+        self.first_wino = self.first_pool and os.environ.get("ADVPATCH_FIRST_WINO", "1") != "0"
         # later conv + k=2 stride-2 pool pairs (yolov3-tiny blocks 2/3, 4/5): the pool
         # runs in the conv epilogue (po_conv_desc.pool_y, pool-order grid) when the
         # conv's only consumer is the pool: with exact fp32 operands at any width
@@ -876,7 +878,9 @@ class NetPlan:
                 if i == 0 and self.first_pool:
                     args = (None, B, self.H, self.W, P(wts["w27"]), P(wts["bias"]), m["cout"], self.cp[i],
                             1 if m["act"] == "leaky" else 0, P(self.act[1]), P(self.argmax[1]), self.slot(self.act[1]))
-                    fa(("po_conv_first_pool_fwd", args, "img0"))
+                    if self.first_wino:
+                        args = args[:4] + (P(wts["u16"]),) + args[5:]
+                    fa(("po_conv_first_pool_wino_fwd" if self.first_wino else "po_conv_first_pool_fwd", args, "img0"))
                     assert not fuse_next
                     continue
                 if i == 0 and self.first_direct:
@@ -1595,7 +1599,7 @@ class NetPlan:
         for k, (name, args, desc) in enumerate(self.fwd_ops):
             if side is not None and k in self._side_f:
                 continue                                  # a head tail: launched on the side stream
-            if name in ("po_conv_first_fwd", "po_conv_first_pool_fwd"):
+            if name in ("po_conv_first_fwd", "po_conv_first_pool_fwd", "po_conv_first_pool_wino_fwd"):
                 if base is not None:
                     name, args = name + "_cmp", cmp + args[1:]
                 else:
@@ -1710,6 +1714,15 @@ class NetPlan:
 
 # Winograd F(2x2,3x3): U = G g G^T with G = [[1,0,0],[.5,.5,.5],[.5,-.5,.5],[0,0,1]]
 _WINO_G = ((1.0, 0.0, 0.0), (0.5, 0.5, 0.5), (0.5, -0.5, 0.5), (0.0, 0.0, 1.0))
+
+
+def first_wino_u(w):
+    """First-layer weights [Cout,3,3,3] (float64) -> the F(2x2,3x3) kernel
+    transforms U[co][c] = G g G^T, [Cout,3,16] row-major over the 4x4 (the
+    operand of po_conv_first_pool_wino_fwd), computed in float64."""
+    G = torch.tensor([[1.0, 0.0, 0.0], [0.5, 0.5, 0.5], [0.5, -0.5, 0.5], [0.0, 0.0, 1.0]], dtype=torch.float64)
+    w = w.double()
+    return torch.einsum("ik,ockl,jl->ocij", G, w, G).reshape(w.shape[0], 3, 16)
 
 
 def wino_transform(w, offs):
@@ -1927,6 +1940,7 @@ class Darknet(nn.Module):
             ent = {"w": Wn.float().contiguous().to(device), "bias": b.float().to(device)}
             if i == 0 and cin == 3 and k == 3:
                 ent["w27"] = W.reshape(cout, 27).float().contiguous().to(device)
+                ent["u16"] = first_wino_u(W).float().contiguous().to(device)
             self._dev[i] = ent
         self._dev_device = device
 

@@ -33,7 +33,7 @@ typedef void* po_stream_t;
 #define PO_EHIP -2     /* HIP runtime error */
 #define PO_EDEVICE -3  /* device is not gfx950 */
 
-#define PO_ABI_VERSION 24
+#define PO_ABI_VERSION 25
 #define PO_AMAX_SUB 64  /* sub-slots per max|x| slot (see po_conv_desc) */
 
 int po_abi_version(void);
@@ -576,6 +576,17 @@ int po_conv_first_fwd_cmp(const float* img, const float* pimg, const int32_t* ro
 int po_conv_first_pool_fwd_cmp(const float* img, const float* pimg, const int32_t* roi, int B, int H, int W,
                                const float* Wt, const float* bias, int Cout, int Cout_p, int act, float* y,
                                int8_t* argmax, uint32_t* amax, po_stream_t s);
+/* (ABI 25) po_conv_first_pool_fwd / _cmp with the conv as Winograd F(2x2,3x3):
+ * each pooled pixel's 2x2 conv window is one F(2x2) output tile.  U [Cout][3][16]
+ * = G g G^T of the [Cout][3][3][3] weights (row-major 4x4, G = {{1,0,0},
+ * {.5,.5,.5},{.5,-.5,.5},{0,0,1}}; darknet_v3.first_wino_u computes it in
+ * float64).  Same outputs, argmax codes and conditions as the direct form; the
+ * conv sums differ from it by fp32 rounding only (tests/test_gpu_first_conv.py). */
+int po_conv_first_pool_wino_fwd(const float* img, int B, int H, int W, const float* U, const float* bias, int Cout,
+                                int Cout_p, int act, float* y, int8_t* argmax, uint32_t* amax, po_stream_t s);
+int po_conv_first_pool_wino_fwd_cmp(const float* img, const float* pimg, const int32_t* roi, int B, int H, int W,
+                                    const float* U, const float* bias, int Cout, int Cout_p, int act, float* y,
+                                    int8_t* argmax, uint32_t* amax, po_stream_t s);
 /* Its input gradient: d_img[b,c,h,w] (NCHW) from D [B,Ho,Wo,Cout_p] (already
  * multiplied by leaky'), W [Cout][27].  roi (may be NULL) [B,4] int32
  * {x0,y0,x1,y1}: only pixels x0<=w<x1, y0<=h<y1 of image b are computed (the

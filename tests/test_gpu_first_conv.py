@@ -158,6 +158,69 @@ def test_first_pool_fused_matches_conv_then_pool(B, H, W, cout):
         assert torch.equal(d_fus, d_ref)
 
 
+def _pool_ref64(img, w27, b, act):
+    """float64 conv 3->Cout (pad 1) + LeakyReLU + 2/2 max pool on the CPU:
+    (pooled [B,Hp,Wp,Cout], window position [B,Hp,Wp,Cout], second-best gap)."""
+    B, _, H, W = img.shape
+    cout = w27.shape[0]
+    y = torch.nn.functional.conv2d(img.double().cpu(), w27.double().cpu().view(cout, 3, 3, 3),
+                                   b.double().cpu(), padding=1)
+    if act:
+        y = torch.nn.functional.leaky_relu(y, 0.1)
+    Hp, Wp = H // 2, W // 2
+    win = y[:, :, :2 * Hp, :2 * Wp].reshape(B, cout, Hp, 2, Wp, 2).permute(0, 2, 4, 1, 3, 5).reshape(B, Hp, Wp, cout, 4)
+    top = win.topk(2, dim=-1).values
+    return win.max(-1).values, win.argmax(-1), top[..., 0] - top[..., 1]
+
+
+@pytest.mark.parametrize("B,H,W,cout", [(2, 38, 54, 32), (3, 29, 31, 16), (1, 64, 64, 16), (2, 17, 20, 13),
+                                        (4, 416, 416, 16)])
+def test_first_pool_wino_matches_float64(B, H, W, cout):
+    """po_conv_first_pool_wino_fwd (the conv as Winograd F(2x2,3x3), U from
+    darknet_v3.first_wino_u) against the float64 conv + leaky + pool.
+    Tolerance (stated): |pooled - ref| <= 2e-6 * (1 + |ref|) where ref is
+    the conv output scale of these inputs (|y| <~ 4) -- the direct fused
+    kernel's own error is of the same order; window positions equal the
+    float64 argmax wherever the best two window values differ by more than
+    that tolerance; argmax bits 2-3 as po_conv_first_pool_fwd."""
+    nat, dv3 = pkg_mod("_native"), pkg_mod("darknet_v3")
+    dev = torch.device("cuda", 0)
+    g = torch.Generator().manual_seed(B * 100 + H + W + 5)
+    cp = 16 if cout <= 16 else 32
+    img = torch.rand(B, 3, H, W, generator=g)
+    w27 = torch.randn(cout, 27, generator=g, dtype=torch.float64) * 0.3
+    b = torch.randn(cout, generator=g, dtype=torch.float64) * 0.1
+    u16 = dv3.first_wino_u(w27.view(cout, 3, 3, 3)).float().contiguous().to(dev)
+    w32, b32 = w27.float().to(dev), b.float().to(dev)
+    imgd = img.to(dev)
+    Hp, Wp = H // 2, W // 2
+    for act in (0, 1):
+        ref, pos, gap = _pool_ref64(img, w32, b32, act)
+        outs = {}
+        for name, wt in (("po_conv_first_pool_wino_fwd", u16), ("po_conv_first_pool_fwd", w32)):
+            y = torch.full((B, Hp, Wp, cp), float("nan"), device=dev)
+            am = torch.full((B, Hp, Wp, cp), -1, dtype=torch.int8, device=dev)
+            amax = torch.zeros(nat.PO_AMAX_SUB, dtype=torch.int32, device=dev)
+            nat.call(name, nat.ptr(imgd), B, H, W, nat.ptr(wt), nat.ptr(b32), cout, cp, act, nat.ptr(y),
+                     nat.ptr(am, torch.int8), nat.ptr(amax, torch.int32), nat.stream())
+            torch.cuda.synchronize()
+            outs[name] = (y[..., :cout].double().cpu(), am.long().cpu()[..., :cout], amax)
+        y, code, amax = outs["po_conv_first_pool_wino_fwd"]
+        tol = 2e-6 * (1.0 + ref.abs())
+        err = (y - ref).abs()
+        assert bool((err <= tol).all()), "max err %.3g" % float(err.max())
+        d_err = (outs["po_conv_first_pool_fwd"][0] - ref).abs().max()
+        assert float(err.max()) <= 4 * float(d_err) + 1e-7      # same order as the direct form
+        clear = gap > 2 * tol
+        assert torch.equal((code & 3)[clear], pos[clear])
+        if act:
+            assert bool(((code & 8) == 8).all())
+            assert torch.equal((code & 4) == 4, y <= 0)
+        else:
+            assert bool((code < 4).all())
+        assert amax.view(torch.float32).max().item() == y.abs().max().item()
+
+
 def _sparse_case(B, S, P, seed, big=False):
     """(frames, full composite, sparse composite (NaN outside the boxes), roi)."""
     ld, sy = pkg_mod("load_data"), pkg_mod("synthetic")
@@ -209,8 +272,11 @@ def test_first_fwd_on_sparse_composite_bit_identical(B, S, stride, cout, big):
         assert amax.view(torch.float32).max().item() == m_want
 
 
+@pytest.mark.parametrize("wino", [False, True])
 @pytest.mark.parametrize("B,S,cout,big", [(4, 416, 16, False), (2, 96, 16, True), (2, 64, 32, True)])
-def test_first_pool_on_sparse_composite_bit_identical(B, S, cout, big):
+def test_first_pool_on_sparse_composite_bit_identical(B, S, cout, big, wino):
+    """po_conv_first_pool[_wino]_fwd_cmp on (frames, sparse composite, roi)
+    equals the same kernel on the materialised composite bit for bit."""
     nat = pkg_mod("_native")
     dev = torch.device("cuda", 0)
     img, full, sp, roi = _sparse_case(B, S, min(224, S // 2), seed=S + 11, big=big)
@@ -219,7 +285,10 @@ def test_first_pool_on_sparse_composite_bit_identical(B, S, cout, big):
     b = (torch.randn(cout, generator=g) * 0.1).to(dev)
     h = S // 2
     outs = []
-    for name, pre in (("po_conv_first_pool_fwd", ()), ("po_conv_first_pool_fwd_cmp", None)):
+    if wino:
+        w = pkg_mod("darknet_v3").first_wino_u(w.double().view(cout, 3, 3, 3).cpu()).float().contiguous().to(dev)
+    base = "po_conv_first_pool_wino_fwd" if wino else "po_conv_first_pool_fwd"
+    for name, pre in ((base, ()), (base + "_cmp", None)):
         y = torch.full((B, h, h, cout), float("nan"), device=dev)
         am = torch.full((B, h, h, cout), -1, dtype=torch.int8, device=dev)
         amax = torch.zeros(nat.PO_AMAX_SUB, dtype=torch.int32, device=dev)

@@ -125,7 +125,8 @@ def assert_timed_path(tr):
     frames + boxes (po_conv_first_*_cmp)."""
     plan = tr.last_plan
     assert tr.last_sparse and plan.sparse_input, "sparse composite not taken"
-    assert plan.last_first_op in ("po_conv_first_fwd_cmp", "po_conv_first_pool_fwd_cmp"), plan.last_first_op
+    assert plan.last_first_op in ("po_conv_first_fwd_cmp", "po_conv_first_pool_fwd_cmp",
+                                  "po_conv_first_pool_wino_fwd_cmp"), plan.last_first_op
 
 
 def branch_aligned(tr, ref_net, img, lab, patch, dr, objective="ce", geometry32=False, hip_dr=None):
