@@ -182,87 +182,16 @@ __global__ __launch_bounds__(256) void first_fwd2_k(const float* __restrict__ im
   }
 }
 
-// First conv (stride 1) with the k=2 stride-2 max pool that follows it fused
-// into the epilogue (yolov3-tiny: conv 3->16 @416 then maxpool,
-// darknet_v3.py:61-69).  The conv output is never stored: the pool backward
-// needs only the window argmax and leaky'(y) at the argmax, which equals
-// leaky'(pooled max) (same value).  One thread per pooled pixel: the 4x4x3
-// input patch of its 2x2 conv outputs (zero outside the image through the
-// buffer range check), the two output rows as packed pairs (v_pk_fma_f32,
-// weights from the scalar cache), per output the summation order of
-// first_fwd2_k (bit-identical conv values), and po_maxpool2_fwd's window rule
-// (first position on ties, NaN wins).  Argmax byte: bits 0-1 window position,
-// bit 3 "LeakyReLU mask encoded", bit 2 set when the max is not positive
-// (slope 0.1 in the backward).  Pooled floats are staged through LDS for
-// fully coalesced 16-byte stores; each thread's CO argmax bytes are one or two
-// contiguous 16-byte stores.
-// WINO: the conv as Winograd F(2x2,3x3) -- the pooled pixel's 2x2 conv outputs
-// are one F(2x2) output tile: V = B^T d B of the 4x4 input patch per channel
-// (adds only), 16 products per channel and output channel against Wt = U =
-// G g G^T ([CO][3][16], po_conv_first_pool_wino_fwd), Y = A^T M A -- 768
-// products per pooled pixel instead of 1728, the same pool rule and argmax
-// codes after it.  Not bit-identical to the direct form (another exact
-// factorisation of the same sums; DESIGN.md §4).
+// The conv + LeakyReLU + 2x2 window rule of one pooled pixel from its 4x4x3
+// input patch xa (rows 2py-1.., columns 2px-1..): pooled values to ys_px[co],
+// argmax codes packed 4 per word into aw, max |pooled| into vmax.
 template <int CO, bool WINO>
-__global__ __launch_bounds__(256) void first_pool_fwd_k(const float* __restrict__ img, int B, int H, int W,
-                                                        int Hp, int Wp, const float* __restrict__ Wt,
-                                                        const float* __restrict__ bias, int Cout, int act,
-                                                        float* __restrict__ y, int8_t* __restrict__ am,
-                                                        uint32_t* __restrict__ amax,
-                                                        const float* __restrict__ pimg,
-                                                        const int32_t* __restrict__ roi) {
-  constexpr int LS = CO + 1;
-  __shared__ float ys[256 * LS];
-  const int npix = B * Hp * Wp;                     // < 2^31 (host check)
-  const int pbase = (int)blockIdx.x * 256;
-  const int tid = threadIdx.x;
-  const int p0 = pbase + tid;
-  const bool live = p0 < npix;
-  const int p = live ? p0 : 0;
-  const int b = p / (Hp * Wp);
-  const int rem = p - b * Hp * Wp;
-  const int py = rem / Wp, px = rem - py * Wp;
-  const uint32_t img_bytes = (uint32_t)((int64_t)B * 3 * H * W * 4);
-  const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(img), 0, img_bytes, 0x00020000);
-  constexpr uint32_t kOOB = 0x80000000u;
-  const uint32_t plane = (uint32_t)H * W * 4u;
-  const uint32_t ib = (uint32_t)b * 3u * plane;
+__device__ __forceinline__ void pool_conv_px(const float (&xa)[3][4][4], const float* __restrict__ Wt,
+                                             const float* __restrict__ bias, int Cout, int act, float* ys_px,
+                                             uint32_t (&aw)[CO / 4], float& vmax) {
   // xp[c][r][q] = {x(row 2py-1+r, col 2px-1+q), x(row, col + 1)}: the operand
   // pair of the two outputs (dx = 0, 1) of one output row at tap column q
   f2_t xp[3][4][3];
-  // composite source: as first_fwd2_k (the 4x4 input window of the pooled pixel)
-  po::QBox bx = {0, 0, 0, 0};
-  bool touch = false;
-  if (pimg) {
-    bx = po::quad_box(roi, b, W);
-    touch = live && 2 * py + 2 >= bx.y0 && 2 * py - 1 < bx.y1 && 2 * px + 2 >= bx.qx0 && 2 * px - 1 < bx.qx1;
-  }
-  float xa[3][4][4];
-  if (!__any(touch)) {
-#pragma unroll
-    for (int r = 0; r < 4; ++r)
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const int hi = 2 * py - 1 + r, wi = 2 * px - 1 + q;
-        const bool ok = live && (unsigned)hi < (unsigned)H && (unsigned)wi < (unsigned)W;
-        const uint32_t o = ib + ((uint32_t)hi * W + wi) * 4u;
-#pragma unroll
-        for (int c = 0; c < 3; ++c)
-          xa[c][r][q] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rs, ok ? o + c * plane : kOOB, 0, 0));
-      }
-  } else {
-#pragma unroll
-    for (int r = 0; r < 4; ++r)
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const int hi = 2 * py - 1 + r, wi = 2 * px - 1 + q;
-        const bool ok = live && (unsigned)hi < (unsigned)H && (unsigned)wi < (unsigned)W;
-        const bool in = hi >= bx.y0 && hi < bx.y1 && wi >= bx.qx0 && wi < bx.qx1;
-        const float* src = (in ? pimg : img) + (size_t)b * 3 * H * W + (size_t)hi * W + wi;
-#pragma unroll
-        for (int c = 0; c < 3; ++c) xa[c][r][q] = ok ? src[(size_t)c * H * W] : 0.f;
-      }
-  }
   // WINO: vw[c][k] = {V[2k], V[2k+1]} of V = B^T d B (row-major 4x4), channel c;
   // the row combinations of B^T run packed over column pairs
   f2_t vw[WINO ? 3 : 1][8];
@@ -297,8 +226,7 @@ __global__ __launch_bounds__(256) void first_pool_fwd_k(const float* __restrict_
 #pragma unroll
         for (int q = 0; q < 3; ++q) xp[c][r][q] = (f2_t){xa[c][r][q], xa[c][r][q + 1]};
   }
-  float vmax = 0.f;
-  uint32_t aw[CO / 4];
+  vmax = 0.f;
 #pragma unroll
   for (int i = 0; i < CO / 4; ++i) aw[i] = 0u;
 #pragma unroll
@@ -362,9 +290,92 @@ __global__ __launch_bounds__(256) void first_pool_fwd_k(const float* __restrict_
       if (act) code |= 8u | (bv > 0.f ? 0u : 4u);   // linear conv: no slope to apply
     }
     vmax = fmaxf(vmax, fabsf(bv));
-    ys[tid * LS + co] = bv;
+    ys_px[co] = bv;
     aw[co >> 2] |= code << (8 * (co & 3));
   }
+}
+
+// First conv (stride 1) with the k=2 stride-2 max pool that follows it fused
+// into the epilogue (yolov3-tiny: conv 3->16 @416 then maxpool,
+// darknet_v3.py:61-69).  The conv output is never stored: the pool backward
+// needs only the window argmax and leaky'(y) at the argmax, which equals
+// leaky'(pooled max) (same value).  One thread per pooled pixel: the 4x4x3
+// input patch of its 2x2 conv outputs (zero outside the image through the
+// buffer range check), the two output rows as packed pairs (v_pk_fma_f32,
+// weights from the scalar cache), per output the summation order of
+// first_fwd2_k (bit-identical conv values), and po_maxpool2_fwd's window rule
+// (first position on ties, NaN wins).  Argmax byte: bits 0-1 window position,
+// bit 3 "LeakyReLU mask encoded", bit 2 set when the max is not positive
+// (slope 0.1 in the backward).  Pooled floats are staged through LDS for
+// fully coalesced 16-byte stores; each thread's CO argmax bytes are one or two
+// contiguous 16-byte stores.
+// WINO: the conv as Winograd F(2x2,3x3) -- the pooled pixel's 2x2 conv outputs
+// are one F(2x2) output tile: V = B^T d B of the 4x4 input patch per channel
+// (adds only), 16 products per channel and output channel against Wt = U =
+// G g G^T ([CO][3][16], po_conv_first_pool_wino_fwd), Y = A^T M A -- 768
+// products per pooled pixel instead of 1728, the same pool rule and argmax
+// codes after it.  Not bit-identical to the direct form (another exact
+// factorisation of the same sums; DESIGN.md §4).
+template <int CO, bool WINO>
+__global__ __launch_bounds__(256) void first_pool_fwd_k(const float* __restrict__ img, int B, int H, int W,
+                                                        int Hp, int Wp, const float* __restrict__ Wt,
+                                                        const float* __restrict__ bias, int Cout, int act,
+                                                        float* __restrict__ y, int8_t* __restrict__ am,
+                                                        uint32_t* __restrict__ amax,
+                                                        const float* __restrict__ pimg,
+                                                        const int32_t* __restrict__ roi) {
+  constexpr int LS = CO + 1;
+  __shared__ float ys[256 * LS];
+  const int npix = B * Hp * Wp;                     // < 2^31 (host check)
+  const int pbase = (int)blockIdx.x * 256;
+  const int tid = threadIdx.x;
+  const int p0 = pbase + tid;
+  const bool live = p0 < npix;
+  const int p = live ? p0 : 0;
+  const int b = p / (Hp * Wp);
+  const int rem = p - b * Hp * Wp;
+  const int py = rem / Wp, px = rem - py * Wp;
+  const uint32_t img_bytes = (uint32_t)((int64_t)B * 3 * H * W * 4);
+  const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(img), 0, img_bytes, 0x00020000);
+  constexpr uint32_t kOOB = 0x80000000u;
+  const uint32_t plane = (uint32_t)H * W * 4u;
+  const uint32_t ib = (uint32_t)b * 3u * plane;
+  // composite source: as first_fwd2_k (the 4x4 input window of the pooled pixel)
+  po::QBox bx = {0, 0, 0, 0};
+  bool touch = false;
+  if (pimg) {
+    bx = po::quad_box(roi, b, W);
+    touch = live && 2 * py + 2 >= bx.y0 && 2 * py - 1 < bx.y1 && 2 * px + 2 >= bx.qx0 && 2 * px - 1 < bx.qx1;
+  }
+  float xa[3][4][4];
+  if (!__any(touch)) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int hi = 2 * py - 1 + r, wi = 2 * px - 1 + q;
+        const bool ok = live && (unsigned)hi < (unsigned)H && (unsigned)wi < (unsigned)W;
+        const uint32_t o = ib + ((uint32_t)hi * W + wi) * 4u;
+#pragma unroll
+        for (int c = 0; c < 3; ++c)
+          xa[c][r][q] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rs, ok ? o + c * plane : kOOB, 0, 0));
+      }
+  } else {
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int hi = 2 * py - 1 + r, wi = 2 * px - 1 + q;
+        const bool ok = live && (unsigned)hi < (unsigned)H && (unsigned)wi < (unsigned)W;
+        const bool in = hi >= bx.y0 && hi < bx.y1 && wi >= bx.qx0 && wi < bx.qx1;
+        const float* src = (in ? pimg : img) + (size_t)b * 3 * H * W + (size_t)hi * W + wi;
+#pragma unroll
+        for (int c = 0; c < 3; ++c) xa[c][r][q] = ok ? src[(size_t)c * H * W] : 0.f;
+      }
+  }
+  float vmax;
+  uint32_t aw[CO / 4];
+  pool_conv_px<CO, WINO>(xa, Wt, bias, Cout, act, ys + tid * LS, aw, vmax);
   if (amax) po::amax_commit(amax, live ? vmax : 0.f);
   if (live) {
     uint4* ap = reinterpret_cast<uint4*>(am + (int64_t)p0 * CO);
@@ -378,6 +389,112 @@ __global__ __launch_bounds__(256) void first_pool_fwd_k(const float* __restrict_
     const int q = f / (CO / 4), ch = (f % (CO / 4)) * 4;
     const float* r = ys + q * LS + ch;
     *reinterpret_cast<float4*>(yb + (int64_t)f * 4) = make_float4(r[0], r[1], r[2], r[3]);
+  }
+}
+
+// first_pool_fwd_k over 16x16 tiles of pooled pixels: the workgroup stages
+// the tile's 34x34x3 input window in LDS with coalesced loads (14 per thread
+// instead of 48 strided gathers, each input element fetched once per tile
+// instead of four times per thread), then each thread reads its 4x4x3 patch
+// as 8-byte LDS pairs.  Same arithmetic per pixel as first_pool_fwd_k
+// (pool_conv_px), so the outputs are bit-identical to it; the LDS window
+// aliases the output staging (a barrier between).
+template <int CO, bool WINO>
+__global__ __launch_bounds__(256) void first_pool_tile_k(const float* __restrict__ img, int B, int H, int W,
+                                                         int Hp, int Wp, int tiles_x, int tiles_y,
+                                                         const float* __restrict__ Wt,
+                                                         const float* __restrict__ bias, int Cout, int act,
+                                                         float* __restrict__ y, int8_t* __restrict__ am,
+                                                         uint32_t* __restrict__ amax,
+                                                         const float* __restrict__ pimg,
+                                                         const int32_t* __restrict__ roi) {
+  constexpr int LS = CO + 1;
+  constexpr int TE = 34, TLD = 34;                  // input window rows/columns (2*16 + 2), LDS row stride (even: 8-byte pairs)
+  static_assert(3 * TE * TLD <= 256 * LS, "input window must fit the output staging");
+  __shared__ float ys[256 * LS];
+  const int tid = threadIdx.x;
+  int t = (int)blockIdx.x;
+  const int b = t / (tiles_x * tiles_y);
+  t -= b * tiles_x * tiles_y;
+  const int ty = t / tiles_x, tx = t - ty * tiles_x;
+  const int ly = tid >> 4, lx = tid & 15;
+  const int py = ty * 16 + ly, px = tx * 16 + lx;
+  const bool live = py < Hp && px < Wp;
+  const int r0 = 32 * ty - 1, c0 = 32 * tx - 1;     // image row/column of window element (0, 0)
+  const uint32_t img_bytes = (uint32_t)((int64_t)B * 3 * H * W * 4);
+  const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(img), 0, img_bytes, 0x00020000);
+  constexpr uint32_t kOOB = 0x80000000u;
+  const uint32_t plane = (uint32_t)H * W * 4u;
+  const uint32_t ib = (uint32_t)b * 3u * plane;
+  po::QBox bx = {0, 0, 0, 0};
+  bool touch = false;                               // workgroup-uniform: the window meets the composite box
+  if (pimg) {
+    bx = po::quad_box(roi, b, W);
+    touch = r0 + TE > bx.y0 && r0 < bx.y1 && c0 + TE > bx.qx0 && c0 < bx.qx1;
+  }
+  float* xs = ys;
+  if (!touch) {
+#pragma unroll
+    for (int k = 0; k < (3 * TE * TE + 255) / 256; ++k) {
+      const int e = tid + 256 * k;
+      const int cr = e / TE, col = e - cr * TE;     // cr = c * TE + r
+      const int c = cr / TE, r = cr - c * TE;
+      const int hi = r0 + r, wi = c0 + col;
+      const bool ok = e < 3 * TE * TE && (unsigned)hi < (unsigned)H && (unsigned)wi < (unsigned)W;
+      const uint32_t o = ib + c * plane + ((uint32_t)hi * W + wi) * 4u;
+      const float v = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rs, ok ? o : kOOB, 0, 0));
+      if (e < 3 * TE * TE) xs[cr * TLD + col] = v;
+    }
+  } else {
+    const uint32_t pbytes = img_bytes;
+    const __amdgpu_buffer_rsrc_t rp = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(pimg), 0, pbytes, 0x00020000);
+#pragma unroll
+    for (int k = 0; k < (3 * TE * TE + 255) / 256; ++k) {
+      const int e = tid + 256 * k;
+      const int cr = e / TE, col = e - cr * TE;
+      const int c = cr / TE, r = cr - c * TE;
+      const int hi = r0 + r, wi = c0 + col;
+      const bool ok = e < 3 * TE * TE && (unsigned)hi < (unsigned)H && (unsigned)wi < (unsigned)W;
+      const bool in = hi >= bx.y0 && hi < bx.y1 && wi >= bx.qx0 && wi < bx.qx1;
+      const uint32_t o = ib + c * plane + ((uint32_t)hi * W + wi) * 4u;
+      const float vi = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rs, ok && !in ? o : kOOB, 0, 0));
+      const float vp = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rp, ok && in ? o : kOOB, 0, 0));
+      if (e < 3 * TE * TE) xs[cr * TLD + col] = in ? vp : vi;
+    }
+  }
+  __syncthreads();
+  float xa[3][4][4];
+#pragma unroll
+  for (int c = 0; c < 3; ++c)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const f2_t* row = reinterpret_cast<const f2_t*>(xs + (c * TE + 2 * ly + r) * TLD + 2 * lx);
+      const f2_t lo = row[0], hi2 = row[1];
+      xa[c][r][0] = lo[0];
+      xa[c][r][1] = lo[1];
+      xa[c][r][2] = hi2[0];
+      xa[c][r][3] = hi2[1];
+    }
+  __syncthreads();                                  // ys aliases the window
+  float vmax;
+  uint32_t aw[CO / 4];
+  pool_conv_px<CO, WINO>(xa, Wt, bias, Cout, act, ys + tid * LS, aw, vmax);
+  if (amax) po::amax_commit(amax, live ? vmax : 0.f);
+  const int64_t row0 = ((int64_t)b * Hp + ty * 16) * Wp + tx * 16;   // pixel (ly = 0, lx = 0)
+  if (live) {
+    uint4* ap = reinterpret_cast<uint4*>(am + (row0 + (int64_t)ly * Wp + lx) * CO);
+#pragma unroll
+    for (int i = 0; i < CO / 16; ++i) ap[i] = make_uint4(aw[4 * i], aw[4 * i + 1], aw[4 * i + 2], aw[4 * i + 3]);
+  }
+  __syncthreads();
+  const int nx = min(16, Wp - tx * 16), ny = min(16, Hp - ty * 16);
+  for (int f = tid; f < 256 * (CO / 4); f += 256) {
+    const int q = f / (CO / 4), ch = (f % (CO / 4)) * 4;
+    const int qy = q >> 4, qx = q & 15;
+    if (qy < ny && qx < nx) {
+      const float* r = ys + q * LS + ch;
+      *reinterpret_cast<float4*>(y + (row0 + (int64_t)qy * Wp + qx) * CO + ch) = make_float4(r[0], r[1], r[2], r[3]);
+    }
   }
 }
 
@@ -481,6 +598,10 @@ int first_pool_fwd(const float* img, const float* pimg, const int32_t* roi, int 
                    const float* bias, int Cout, int Cout_p, int act, float* y, int8_t* argmax, uint32_t* amax,
                    po_stream_t s, bool wino = false) {
   PO_REQUIRE(img && Wt && y && argmax, "po_conv_first_pool_fwd: null pointer");
+  static const bool lt = [] {
+    const char* e = getenv("ADVPATCH_FIRST_TILE");
+    return !(e && e[0] == '0');
+  }();
   PO_REQUIRE((Cout_p == 16 || Cout_p == 32) && Cout > 0 && Cout <= Cout_p,
              "po_conv_first_pool_fwd: Cout_p must be 16 or 32 (got %d, Cout %d)", Cout_p, Cout);
   PO_REQUIRE(B > 0 && H >= 2 && W >= 2, "po_conv_first_pool_fwd: bad size B=%d H=%d W=%d", B, H, W);
@@ -490,6 +611,21 @@ int first_pool_fwd(const float* img, const float* pimg, const int32_t* roi, int 
   PO_REQUIRE((int64_t)B * 3 * H * W * 4 < (1LL << 31) && n + 256 < (1LL << 31),
              "po_conv_first_pool_fwd: image batch must be < 2 GiB");
   hipStream_t st = po::stream_of(s);
+  if (lt) {                                         // 16x16 pooled tiles, LDS-staged window
+    const int tx = (Wp + 15) / 16, ty = (Hp + 15) / 16;
+    PO_REQUIRE((int64_t)B * tx * ty < (1LL << 31), "po_conv_first_pool_fwd: too many tiles");
+    dim3 gt((unsigned)(B * tx * ty));
+#define PO_FPT(CO_, WI_)                                                                                    \
+  hipLaunchKernelGGL((first_pool_tile_k<CO_, WI_>), gt, dim3(256), 0, st, img, B, H, W, Hp, Wp, tx, ty, Wt, bias, \
+                     Cout, act, y, argmax, amax, pimg, roi)
+    if (Cout_p == 16) {
+      if (wino) PO_FPT(16, true); else PO_FPT(16, false);
+    } else {
+      if (wino) PO_FPT(32, true); else PO_FPT(32, false);
+    }
+#undef PO_FPT
+    return po::check_launch("po_conv_first_pool_fwd");
+  }
   dim3 grid(po::ceil_div(n, 256));
   if (wino) {
     if (Cout_p == 16)

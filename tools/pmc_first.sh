@@ -2,7 +2,7 @@
 # PMC passes over the first-layer pooled conv (direct and F(2x2)), B=256 @416 3->16
 cd /tmp && export TMPDIR=/tmp
 cd "$GRAFT_REPO_ROOT"
-for v in True wino; do
+for v in ${VARIANTS:-True wino}; do
 OUT=gpurun_out/pmc_first_$v
 mkdir -p $OUT
 i=0
