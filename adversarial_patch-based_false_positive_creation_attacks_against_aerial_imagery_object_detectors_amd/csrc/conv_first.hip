@@ -393,10 +393,11 @@ __global__ __launch_bounds__(256) void first_pool_fwd_k(const float* __restrict_
 }
 
 // first_pool_fwd_k over 16x16 tiles of pooled pixels: the workgroup stages
-// the tile's 34x34x3 input window in LDS with coalesced loads (14 per thread
-// instead of 48 strided gathers, each input element fetched once per tile
-// instead of four times per thread), then each thread reads its 4x4x3 patch
-// as 8-byte LDS pairs.  Same arithmetic per pixel as first_pool_fwd_k
+// the tile's 34x34x3 input window in LDS with coalesced 16-byte loads (4 per
+// thread instead of 48 strided gathers; each input element fetched once per
+// tile instead of four times per thread), then each thread reads its 4x4x3
+// patch from LDS.  W % 4 == 0 and 16-byte aligned images (host check; else
+// first_pool_fwd_k).  Same arithmetic per pixel as first_pool_fwd_k
 // (pool_conv_px), so the outputs are bit-identical to it; the LDS window
 // aliases the output staging (a barrier between).
 template <int CO, bool WINO>
@@ -409,7 +410,7 @@ __global__ __launch_bounds__(256) void first_pool_tile_k(const float* __restrict
                                                          const float* __restrict__ pimg,
                                                          const int32_t* __restrict__ roi) {
   constexpr int LS = CO + 1;
-  constexpr int TE = 34, TLD = 34;                  // input window rows/columns (2*16 + 2), LDS row stride (even: 8-byte pairs)
+  constexpr int TE = 34, TLD = 40;                  // input window rows/columns (2*16 + 2); LDS row: 10 column groups
   static_assert(3 * TE * TLD <= 256 * LS, "input window must fit the output staging");
   __shared__ float ys[256 * LS];
   const int tid = threadIdx.x;
@@ -432,49 +433,41 @@ __global__ __launch_bounds__(256) void first_pool_tile_k(const float* __restrict
     bx = po::quad_box(roi, b, W);
     touch = r0 + TE > bx.y0 && r0 < bx.y1 && c0 + TE > bx.qx0 && c0 < bx.qx1;
   }
+  // the window's image columns 32tx-1 .. 32tx+32 lie in the 16-byte column
+  // groups 8tx-1 .. 8tx+8 (W % 4 == 0, host check): 10 float4 loads per
+  // window row, 102 rows, 4 per thread; a group is entirely inside or outside
+  // the image and the quad-widened composite box (both 4-aligned in x)
   float* xs = ys;
-  if (!touch) {
+  const __amdgpu_buffer_rsrc_t rp =
+      __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(pimg ? pimg : img), 0, img_bytes, 0x00020000);
 #pragma unroll
-    for (int k = 0; k < (3 * TE * TE + 255) / 256; ++k) {
-      const int e = tid + 256 * k;
-      const int cr = e / TE, col = e - cr * TE;     // cr = c * TE + r
-      const int c = cr / TE, r = cr - c * TE;
-      const int hi = r0 + r, wi = c0 + col;
-      const bool ok = e < 3 * TE * TE && (unsigned)hi < (unsigned)H && (unsigned)wi < (unsigned)W;
-      const uint32_t o = ib + c * plane + ((uint32_t)hi * W + wi) * 4u;
-      const float v = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rs, ok ? o : kOOB, 0, 0));
-      if (e < 3 * TE * TE) xs[cr * TLD + col] = v;
+  for (int k = 0; k < (3 * TE * 10 + 255) / 256; ++k) {
+    const int e = tid + 256 * k;
+    const int R = e / 10, g = e - R * 10;           // window row R = c * TE + r, column group g
+    const int c = (R >= TE) + (R >= 2 * TE), r = R - c * TE;
+    const int hi = r0 + r, wi = 32 * tx - 4 + 4 * g;
+    const bool ok = e < 3 * TE * 10 && (unsigned)hi < (unsigned)H && (unsigned)wi < (unsigned)W;
+    const bool in = touch && hi >= bx.y0 && hi < bx.y1 && wi >= bx.qx0 && wi < bx.qx1;
+    const uint32_t o = ib + c * plane + ((uint32_t)hi * W + wi) * 4u;
+    float4 v;
+    if (!touch) {
+      v = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rs, ok ? o : kOOB, 0, 0));
+    } else {
+      const float4 vi = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rs, ok && !in ? o : kOOB, 0, 0));
+      const float4 vp = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rp, ok && in ? o : kOOB, 0, 0));
+      v = in ? vp : vi;
     }
-  } else {
-    const uint32_t pbytes = img_bytes;
-    const __amdgpu_buffer_rsrc_t rp = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(pimg), 0, pbytes, 0x00020000);
-#pragma unroll
-    for (int k = 0; k < (3 * TE * TE + 255) / 256; ++k) {
-      const int e = tid + 256 * k;
-      const int cr = e / TE, col = e - cr * TE;
-      const int c = cr / TE, r = cr - c * TE;
-      const int hi = r0 + r, wi = c0 + col;
-      const bool ok = e < 3 * TE * TE && (unsigned)hi < (unsigned)H && (unsigned)wi < (unsigned)W;
-      const bool in = hi >= bx.y0 && hi < bx.y1 && wi >= bx.qx0 && wi < bx.qx1;
-      const uint32_t o = ib + c * plane + ((uint32_t)hi * W + wi) * 4u;
-      const float vi = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rs, ok && !in ? o : kOOB, 0, 0));
-      const float vp = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rp, ok && in ? o : kOOB, 0, 0));
-      if (e < 3 * TE * TE) xs[cr * TLD + col] = in ? vp : vi;
-    }
+    // LDS column = image column - (32tx - 4): 16-byte stores
+    if (e < 3 * TE * 10) *reinterpret_cast<float4*>(xs + R * TLD + 4 * g) = v;
   }
   __syncthreads();
   float xa[3][4][4];
 #pragma unroll
   for (int c = 0; c < 3; ++c)
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const f2_t* row = reinterpret_cast<const f2_t*>(xs + (c * TE + 2 * ly + r) * TLD + 2 * lx);
-      const f2_t lo = row[0], hi2 = row[1];
-      xa[c][r][0] = lo[0];
-      xa[c][r][1] = lo[1];
-      xa[c][r][2] = hi2[0];
-      xa[c][r][3] = hi2[1];
-    }
+    for (int r = 0; r < 4; ++r)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) xa[c][r][q] = xs[(c * TE + 2 * ly + r) * TLD + 2 * lx + 3 + q];
   __syncthreads();                                  // ys aliases the window
   float vmax;
   uint32_t aw[CO / 4];
@@ -611,7 +604,7 @@ int first_pool_fwd(const float* img, const float* pimg, const int32_t* roi, int 
   PO_REQUIRE((int64_t)B * 3 * H * W * 4 < (1LL << 31) && n + 256 < (1LL << 31),
              "po_conv_first_pool_fwd: image batch must be < 2 GiB");
   hipStream_t st = po::stream_of(s);
-  if (lt) {                                         // 16x16 pooled tiles, LDS-staged window
+  if (lt && W % 4 == 0 && ((uintptr_t)img & 15) == 0 && ((uintptr_t)pimg & 15) == 0) {   // 16x16 pooled tiles
     const int tx = (Wp + 15) / 16, ty = (Hp + 15) / 16;
     PO_REQUIRE((int64_t)B * tx * ty < (1LL << 31), "po_conv_first_pool_fwd: too many tiles");
     dim3 gt((unsigned)(B * tx * ty));
