@@ -54,7 +54,12 @@ def _run(cfg, B, P, tmp_path, objective="ce", seed=0):
     return ref, terms, pg.grad.cpu()
 
 
-def _compare(ref, terms, grad, loss_tol=2e-5, grad_check=True, obj_tol=2e-5):
+def _compare(ref, terms, grad, loss_tol=2e-5, grad_check=True, obj_tol=2e-5, ref_g64=None):
+    """``ref_g64``: the fp32 oracle with its placement geometry in float64 (the
+    HIP path's deliberate deviation); when given, each loss term
+    may differ from the literal fp32 oracle by loss_tol plus that oracle's own
+    geometry error on the term (|ref - ref_g64|), the triangle inequality of
+    assert_geometry_parity, and must be within loss_tol of ref_g64."""
     assert int(terms["flags"].item()) == 0
     torch.testing.assert_close(terms["patch_center"].cpu(), ref["patch_center"], rtol=0, atol=0)
     cells = terms["cells"].cpu().tolist()
@@ -63,7 +68,12 @@ def _compare(ref, terms, grad, loss_tol=2e-5, grad_check=True, obj_tol=2e-5):
     torch.testing.assert_close(terms["cls"].cpu(), ref["cls"], rtol=0, atol=obj_tol)
     for k in ("loss", "nps_loss", "tv_loss", "no_obj_loss", "no_cls_loss", "colorful_loss"):
         a, b = float(terms[k]), float(ref[k])
-        assert abs(a - b) <= loss_tol * max(1.0, abs(b)), (k, a, b)
+        slack = 0.0
+        if ref_g64 is not None:
+            bg = float(ref_g64[k])
+            slack = abs(b - bg)
+            assert abs(a - bg) <= loss_tol * max(1.0, abs(bg)), (k, a, bg, "float64-geometry oracle")
+        assert abs(a - b) <= loss_tol * max(1.0, abs(b)) + slack, (k, a, b, slack)
     if grad_check:
         rel = float((grad - ref["grad"]).abs().max() / ref["grad"].abs().max())
         assert rel < 1e-4, rel
@@ -161,8 +171,10 @@ def branch_aligned(tr, ref_net, img, lab, patch, dr, objective="ce", geometry32=
     rel = lambda a, b: float((a.double() - b.double()).abs().max() / b.double().abs().max())
     errs = {"hip_o32": rel(g, g32)}
     if geometry32:
-        errs["hip_o32g"] = rel(g, oracle.train_step(patch, img, lab, dr, ref_net, colors, objective=objective,
-                                                     branch=br, geometry="f64")["grad"])
+        ref32g = oracle.train_step(patch, img, lab, dr, ref_net, colors, objective=objective, branch=br,
+                                   geometry="f64")
+        errs["hip_o32g"] = rel(g, ref32g["grad"])
+        errs["ref32g"] = ref32g
         say("fp32 oracle, float64 geometry")
     g64 = oracle.train_step_f64(patch, img, lab, dr, ref_net, colors, objective=objective, branch=br)["grad"]
     errs["hip_f64"], errs["o32_f64"] = rel(g, g64), rel(g32, g64)
@@ -249,7 +261,7 @@ def test_step_yolov3_targeted_po_draws(tmp_path):
     terms, g, ref32, errs = branch_aligned(tr, ref_net, img, lab, patch, dr, "targeted", geometry32=True,
                                            hip_dr=hip_dr)
     assert_timed_path(tr)
-    _compare(ref32, terms, g, grad_check=False, obj_tol=OBJ_TOL_608)
+    _compare(ref32, terms, g, grad_check=False, obj_tol=OBJ_TOL_608, ref_g64=errs.pop("ref32g"))
     assert_geometry_parity(errs, "yolov3 targeted, po_draws")
     assert_hip_accuracy(errs, "yolov3 targeted, po_draws")
 
@@ -299,6 +311,7 @@ def test_step_tiny_416(tmp_path, objective):
     img, lab = sy.frames(B, S, seed=90), sy.labels(B, seed=91)
     patch, dr = sy.patch(P, seed=92), sy.draws(B, P, seed=93)
     terms, g, ref32, errs = branch_aligned(tr, ref_net, img, lab, patch, dr, objective, geometry32=True)
+    errs.pop("ref32g")
     assert terms["obj"].shape == (B, 6) and terms["cls"].shape == (B, 6, 15)
     _compare(ref32, terms, g, grad_check=False, obj_tol=OBJ_TOL_608)
     assert_tiny_parity(errs, "tiny B=4 %s" % objective)
