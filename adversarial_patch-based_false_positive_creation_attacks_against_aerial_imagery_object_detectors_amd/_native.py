@@ -14,7 +14,7 @@ LIB_PATH = os.environ.get("ADVPATCH_LIB") or os.path.join(_HERE, "libadvpatch_hi
 
 c_int, c_float, c_int64, c_void_p = ctypes.c_int, ctypes.c_float, ctypes.c_int64, ctypes.c_void_p
 
-PO_ABI_VERSION = 25   # include/advpatch.h
+PO_ABI_VERSION = 26   # include/advpatch.h
 PO_CONV_NTILES = 72   # include/advpatch.h
 PO_AMAX_SUB = 64      # sub-slots per max|x| slot
 
@@ -76,6 +76,10 @@ _SIGS = {
                               c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p, c_void_p],
     "po_warp_box_bwd_keyed": [c_void_p, c_void_p, ctypes.c_uint64, ctypes.c_uint64, c_int, c_void_p, c_void_p,
                               c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p],
+    "po_warp_box_fwd_fac": [c_void_p, c_void_p, ctypes.c_uint64, ctypes.c_uint64, c_int, c_void_p, c_void_p,
+                            c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p],
+    "po_warp_box_bwd_fac": [c_void_p, c_void_p, ctypes.c_uint64, ctypes.c_uint64, c_int, c_void_p, c_void_p,
+                            c_void_p, c_void_p, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p],
     "po_warp_bwd_keyed": [c_void_p, c_void_p, ctypes.c_uint64, ctypes.c_uint64, c_int, c_void_p, c_void_p, c_void_p,
                           c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p],
     "po_apply_fwd": [c_void_p, c_void_p, c_int64, c_void_p, c_void_p],

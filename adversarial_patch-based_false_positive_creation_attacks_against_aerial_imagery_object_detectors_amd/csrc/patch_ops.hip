@@ -1013,7 +1013,7 @@ __global__ __launch_bounds__(256) void warp_box_fwd_k(const float* __restrict__ 
                                                       const float* __restrict__ bright,
                                                       const double* __restrict__ affine,
                                                       const int32_t* __restrict__ roi, WarpGeom g, int mode,
-                                                      float* __restrict__ out) {
+                                                      float* __restrict__ out, float* __restrict__ fac) {
   const int b = blockIdx.y;
   const QBox bx = quad_box(roi, b, g.S);
   const int bw = bx.qx1 - bx.qx0, area = bw * (bx.y1 - bx.y0);
@@ -1028,12 +1028,20 @@ __global__ __launch_bounds__(256) void warp_box_fwd_k(const float* __restrict__ 
     float adv[3], msk;
     bool rng[3];
     const bool hit = warp_pixel(affine + 6 * b, g, mp, nz, cb, bb, i, j, adv, msk, rng);
+    float f4[4] = {-1.f, -1.f, -1.f, -1.f};
 #pragma unroll
     for (int ch = 0; ch < 3; ++ch) {
       float v = hit ? adv[ch] * msk : 0.f;                       // load_data.py:791-792
+      // the backward's factor: d_out * msk where the gradient passes (clamp in
+      // range, and in mode 1 the patch value not replaced by the frame), else
+      // the sentinel -1 for an exact +0 (warp_box_bwd_a_k's rule)
+      if (hit && rng[ch] && !(mode == 1 && v == 0.f)) f4[ch] = msk;
       if (mode == 1) v = (v == 0.f) ? img[o + ch * plane] : v;   // load_data.py:820
       out[o + ch * plane] = v;
     }
+    if (fac)
+      *reinterpret_cast<float4*>(fac + ((size_t)b * plane + (size_t)i * g.S + j) * 4) =
+          make_float4(f4[0], f4[1], f4[2], f4[3]);
   }
 }
 
@@ -1075,6 +1083,31 @@ __global__ __launch_bounds__(256) void warp_box_bwd_a_k(const float* __restrict_
   }
 }
 
+// phase A from the forward's factors (po_warp_box_fwd_fac): no warp_pixel
+// recomputation -- a 16-byte factor load, the three d_out loads and the gfac
+// store in place of the factors.  The same products as warp_box_bwd_a_k
+// (d_out * msk where the gradient passes, +0 elsewhere), so the same bits.
+__global__ __launch_bounds__(256) void warp_box_bwd_fac_k(const float* __restrict__ d_out,
+                                                          const int32_t* __restrict__ roi, int S,
+                                                          float* __restrict__ fac) {
+  const int b = blockIdx.y;
+  const QBox bx = quad_box(roi, b, S);
+  const int bw = bx.qx1 - bx.qx0, area = bw * (bx.y1 - bx.y0);
+  const size_t plane = (size_t)S * S;
+  for (int p = blockIdx.x * 256 + threadIdx.x; p < area; p += gridDim.x * 256) {
+    const int r = p / bw;
+    const int i = bx.y0 + r, j = bx.qx0 + (p - r * bw);
+    const size_t o = (size_t)b * 3 * plane + (size_t)i * S + j;
+    float4* fp = reinterpret_cast<float4*>(fac + ((size_t)b * plane + (size_t)i * S + j) * 4);
+    const float4 f = *fp;
+    const float fv[3] = {f.x, f.y, f.z};
+    float gv[3];
+#pragma unroll
+    for (int ch = 0; ch < 3; ++ch) gv[ch] = fv[ch] < 0.f ? 0.f : d_out[o + ch * plane] * fv[ch];
+    *fp = make_float4(gv[0], gv[1], gv[2], 0.f);
+  }
+}
+
 // workgroups per image of the box kernels: enough for a box of an eighth of the
 // frame in one pass (a larger box loops)
 __host__ inline int box_blocks(int S) { return po::ceil_div(po::ceil_div((int64_t)S * S, 8), 256); }
@@ -1105,14 +1138,13 @@ extern "C" int po_warp_fwd_pre(const float* img, const float* pre, const double*
   hipLaunchKernelGGL(warp_quad_copy_k, dim3(po::ceil_div(S * (S / 4), 256), B), dim3(256), 0, st, img, roi, S, mode,
                      out);
   hipLaunchKernelGGL(warp_box_fwd_k, dim3(box_blocks(S), B), dim3(256), 0, st, img, nullptr, nullptr, nullptr, affine,
-                     roi, g, mode, out);
+                     roi, g, mode, out, nullptr);
   return po::check_launch("po_warp_fwd_pre");
 }
 
-extern "C" int po_warp_box_fwd_keyed(const float* img, const float* patch_mp, uint64_t seed, uint64_t counter, int b0,
-                                     const float* contrast, const float* bright, const double* affine,
-                                     const int32_t* roi, int B, int S, int P, int mode, int fill, float* out,
-                                     po_stream_t s) {
+static int box_fwd_keyed(const float* img, const float* patch_mp, uint64_t seed, uint64_t counter, int b0,
+                         const float* contrast, const float* bright, const double* affine, const int32_t* roi, int B,
+                         int S, int P, int mode, int fill, float* out, float* fac, po_stream_t s) {
   PO_REQUIRE(patch_mp && contrast && bright && affine && roi && out, "po_warp_box_fwd_keyed: null pointer");
   PO_REQUIRE(mode == 0 || (mode == 1 && img), "po_warp_box_fwd_keyed: mode must be 0 or 1 (1 needs img)");
   PO_REQUIRE(B > 0 && S > 1 && P > 0 && P <= S && b0 >= 0 && S % 4 == 0,
@@ -1125,8 +1157,25 @@ extern "C" int po_warp_box_fwd_keyed(const float* img, const float* patch_mp, ui
     hipLaunchKernelGGL(warp_quad_copy_k, dim3(po::ceil_div(S * (S / 4), 256), B), dim3(256), 0, st, img, roi, S, mode,
                        out);
   hipLaunchKernelGGL(warp_box_fwd_k, dim3(box_blocks(S), B), dim3(256), 0, st, img, patch_mp, contrast, bright, affine,
-                     roi, g, mode, out);
+                     roi, g, mode, out, fac);
   return po::check_launch("po_warp_box_fwd_keyed");
+}
+
+extern "C" int po_warp_box_fwd_keyed(const float* img, const float* patch_mp, uint64_t seed, uint64_t counter, int b0,
+                                     const float* contrast, const float* bright, const double* affine,
+                                     const int32_t* roi, int B, int S, int P, int mode, int fill, float* out,
+                                     po_stream_t s) {
+  return box_fwd_keyed(img, patch_mp, seed, counter, b0, contrast, bright, affine, roi, B, S, P, mode, fill, out,
+                       nullptr, s);
+}
+
+extern "C" int po_warp_box_fwd_fac(const float* img, const float* patch_mp, uint64_t seed, uint64_t counter, int b0,
+                                   const float* contrast, const float* bright, const double* affine,
+                                   const int32_t* roi, int B, int S, int P, int mode, int fill, float* out, float* fac,
+                                   po_stream_t s) {
+  PO_REQUIRE(fac && (uintptr_t)fac % 16 == 0, "po_warp_box_fwd_fac: fac must be non-null and 16-byte aligned");
+  return box_fwd_keyed(img, patch_mp, seed, counter, b0, contrast, bright, affine, roi, B, S, P, mode, fill, out, fac,
+                       s);
 }
 
 extern "C" int po_warp_bwd_pre(const float* d_out, const float* pre, const float* contrast, const double* affine,
@@ -1168,6 +1217,25 @@ extern "C" int po_warp_box_bwd_keyed(const float* d_out, const float* patch_mp, 
   if (rc) return rc;
   launch_bwd_b(work, patch_mp, nullptr, contrast, bright, affine, g, B, P, d_patch_mp, st, true);
   return po::check_launch("po_warp_box_bwd_keyed(b)");
+}
+
+extern "C" int po_warp_box_bwd_fac(const float* d_out, const float* patch_mp, uint64_t seed, uint64_t counter, int b0,
+                                   const float* contrast, const float* bright, const double* affine,
+                                   const int32_t* roi, int B, int S, int P, float* fac, float* d_patch_mp,
+                                   po_stream_t s) {
+  PO_REQUIRE(d_out && patch_mp && contrast && bright && affine && roi && fac && d_patch_mp,
+             "po_warp_box_bwd_fac: null pointer");
+  PO_REQUIRE(B > 0 && S > 1 && P > 0 && P <= S && b0 >= 0, "po_warp_box_bwd_fac: bad shape");
+  PO_REQUIRE(3LL * P * P < (1LL << 31), "po_warp_box_bwd_fac: patch too large");
+  PO_REQUIRE(fac != d_out, "po_warp_box_bwd_fac: fac may not alias d_out");
+  PO_REQUIRE((uintptr_t)fac % 16 == 0, "po_warp_box_bwd_fac: fac must be 16-byte aligned");
+  const WarpGeom g = make_geom(S, P, seed, counter, b0);
+  hipStream_t st = po::stream_of(s);
+  hipLaunchKernelGGL(warp_box_bwd_fac_k, dim3(box_blocks(S), B), dim3(256), 0, st, d_out, roi, S, fac);
+  int rc = po::check_launch("po_warp_box_bwd_fac(a)");
+  if (rc) return rc;
+  launch_bwd_b(fac, patch_mp, nullptr, contrast, bright, affine, g, B, P, d_patch_mp, st, true);
+  return po::check_launch("po_warp_box_bwd_fac(b)");
 }
 
 extern "C" int po_warp_composite_multi(const float* img, const float* patch_mp, const float* noise,

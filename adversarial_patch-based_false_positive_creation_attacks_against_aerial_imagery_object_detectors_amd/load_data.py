@@ -245,10 +245,18 @@ class _Warp(torch.autograd.Function):
         keyed = isinstance(noise, tuple)
         if keyed and roi is not None and form == "box" and S % 4 == 0:
             seed, counter, b0 = noise
-            nat.call("po_warp_box_fwd_keyed", imgp, nat.ptr(mp), int(seed) & 0xFFFFFFFFFFFFFFFF,
-                     int(counter) & 0xFFFFFFFFFFFFFFFF, int(b0), nat.ptr(contrast), nat.ptr(bright),
-                     nat.ptr(affine, torch.float64), nat.ptr(roi, torch.int32), B, S, P, mode,
-                     0 if (sparse and mode == 1) else 1, nat.ptr(out), nat.stream())
+            head = (imgp, nat.ptr(mp), int(seed) & 0xFFFFFFFFFFFFFFFF, int(counter) & 0xFFFFFFFFFFFFFFFF, int(b0),
+                    nat.ptr(contrast), nat.ptr(bright), nat.ptr(affine, torch.float64), nat.ptr(roi, torch.int32),
+                    B, S, P, mode, 0 if (sparse and mode == 1) else 1, nat.ptr(out))
+            # the backward's per-pixel factors, written by the forward and turned
+            # into the gradient factors in place (po_warp_box_*_fac; "0": re-evaluate
+            # the warp in the backward, po_warp_box_bwd_keyed -- the same bits)
+            ctx.fac = None
+            if os.environ.get("ADVPATCH_WARP_FAC", "1") != "0":
+                ctx.fac = torch.empty(B * S * S * 4, device=mp.device)
+                nat.call("po_warp_box_fwd_fac", *head, nat.ptr(ctx.fac), nat.stream())
+            else:
+                nat.call("po_warp_box_fwd_keyed", *head, nat.stream())
             ctx.key, ctx.form = noise, "box"
             ctx.save_for_backward(mp, contrast, bright, affine, roi)
         elif sparse:
@@ -282,11 +290,18 @@ class _Warp(torch.autograd.Function):
         mp, contrast, bright, affine = ctx.saved_tensors[:4]
         d_out = d_out.contiguous()
         B, P = affine.size(0), mp.size(-1)
+        d_mp = torch.empty_like(mp)
+        key = tuple(int(v) & 0xFFFFFFFFFFFFFFFF for v in ctx.key[:2]) + (int(ctx.key[2]),) if ctx.key else None
+        if ctx.form == "box" and ctx.fac is not None:
+            roi = ctx.saved_tensors[4]
+            fac, ctx.fac = ctx.fac, None                 # consumed in place
+            nat.call("po_warp_box_bwd_fac", nat.ptr(d_out), nat.ptr(mp), *key, nat.ptr(contrast), nat.ptr(bright),
+                     nat.ptr(affine, torch.float64), nat.ptr(roi, torch.int32), B, ctx.S, P, nat.ptr(fac),
+                     nat.ptr(d_mp), nat.stream())
+            return d_mp, None, None, None, None, None, None, None, None, None, None
         # the footprint-box forms keep their per-pixel factors interleaved [B,S,S,4]
         work = (torch.empty(B * ctx.S * ctx.S * 4, device=d_out.device) if ctx.form in ("box", "pre")
                 else torch.empty_like(d_out))
-        d_mp = torch.empty_like(mp)
-        key = tuple(int(v) & 0xFFFFFFFFFFFFFFFF for v in ctx.key[:2]) + (int(ctx.key[2]),) if ctx.key else None
         if ctx.form == "box":
             roi = ctx.saved_tensors[4]
             nat.call("po_warp_box_bwd_keyed", nat.ptr(d_out), nat.ptr(mp), *key, nat.ptr(contrast), nat.ptr(bright),

@@ -142,7 +142,8 @@ def cpu_baseline(cfg, S, P, B=16, warmup=1, iters=3):
 
 
 WARP_ENTRIES = ("po_warp_fwd", "po_warp_bwd", "po_warp_fwd_keyed", "po_warp_bwd_keyed", "po_augment_patch",
-                "po_warp_fwd_pre", "po_warp_bwd_pre", "po_warp_box_fwd_keyed", "po_warp_box_bwd_keyed")
+                "po_warp_fwd_pre", "po_warp_bwd_pre", "po_warp_box_fwd_keyed", "po_warp_box_bwd_keyed",
+                "po_warp_box_fwd_fac", "po_warp_box_bwd_fac")
 
 
 def measure(tr, prec, patch, img, lab, B, world, rank, steps, warmup, weights):
@@ -328,11 +329,17 @@ def warp_roofline(m, B, S, P, cp0=None):
     gfac written and read again per box pixel plus the 3*P^2*4 B patch
     gradient written; the frame itself is then read by the first layer
     (po_conv_first_*_cmp: 3*S^2*4 B per image in, its NHWC output out),
-    reported as ``first_layer``."""
+    reported as ``first_layer``.  With the forward-saved factors
+    (po_warp_box_*_fac, the default) the forward also writes 16 B of factors
+    per box pixel and the backward reads them (16 B) instead of re-evaluating
+    the warp: 40 B and 60 B per box pixel."""
     out = {}
     wm = m["warp_ms"]
     box_px = m.get("box_px") or 0
-    if wm.get("po_warp_box_fwd_keyed"):
+    if wm.get("po_warp_box_fwd_fac"):
+        forms = (("po_warp_fwd", "po_warp_box_fwd_fac", box_px * 40 + 3 * P * P * 4),
+                 ("po_warp_bwd", "po_warp_box_bwd_fac", box_px * 60 + 3 * P * P * 4))
+    elif wm.get("po_warp_box_fwd_keyed"):
         forms = (("po_warp_fwd", "po_warp_box_fwd_keyed", box_px * 24 + 3 * P * P * 4),
                  ("po_warp_bwd", "po_warp_box_bwd_keyed", box_px * 36 + 3 * P * P * 4))
     else:

@@ -33,7 +33,7 @@ typedef void* po_stream_t;
 #define PO_EHIP -2     /* HIP runtime error */
 #define PO_EDEVICE -3  /* device is not gfx950 */
 
-#define PO_ABI_VERSION 25
+#define PO_ABI_VERSION 26
 #define PO_AMAX_SUB 64  /* sub-slots per max|x| slot (see po_conv_desc) */
 
 int po_abi_version(void);
@@ -162,6 +162,21 @@ int po_warp_box_fwd_keyed(const float* img, const float* patch_mp, uint64_t seed
 int po_warp_box_bwd_keyed(const float* d_out, const float* patch_mp, uint64_t seed, uint64_t counter, int b0,
                           const float* contrast, const float* bright, const double* affine, const int32_t* roi,
                           int B, int S, int P, int mode, float* work, float* d_patch_mp, po_stream_t s);
+/* (ABI 26) The same pair with the backward's per-pixel factors saved by the
+ * forward: po_warp_box_fwd_fac also writes fac [B][S][S][4] (16-byte aligned;
+ * per box pixel and channel msk where the gradient passes -- clamp in range and,
+ * mode 1, the patch value not replaced by the frame -- else -1), and
+ * po_warp_box_bwd_fac turns them into the gradient factors in place (d_out *
+ * fac, +0 at -1) instead of re-evaluating the warp at every box pixel, then
+ * runs the same gather as po_warp_box_bwd_keyed.  fac must hold the forward's
+ * values (nothing may write it in between); outputs equal po_warp_box_*_keyed
+ * bit for bit. */
+int po_warp_box_fwd_fac(const float* img, const float* patch_mp, uint64_t seed, uint64_t counter, int b0,
+                        const float* contrast, const float* bright, const double* affine, const int32_t* roi, int B,
+                        int S, int P, int mode, int fill, float* out, float* fac, po_stream_t s);
+int po_warp_box_bwd_fac(const float* d_out, const float* patch_mp, uint64_t seed, uint64_t counter, int b0,
+                        const float* contrast, const float* bright, const double* affine, const int32_t* roi, int B,
+                        int S, int P, float* fac, float* d_patch_mp, po_stream_t s);
 
 /* PatchApplier for an explicit adv tensor: out = where(adv==0, img, adv)
  * (load_data.py:820); n elements. bwd: d_img = d_out*(adv==0), d_adv = d_out*(adv!=0). */

@@ -364,6 +364,50 @@ def test_sparse_composite_box_pixels_and_gradient(B, S, P, big):
     assert bool(m.any()) and bool((full[m] != img[m]).any())
 
 
+@pytest.mark.parametrize("B,S,P,big", [(4, 416, 224, False), (3, 96, 40, True)])
+def test_forward_saved_warp_factors_bit_identical(B, S, P, big, monkeypatch):
+    """po_warp_box_fwd_fac / po_warp_box_bwd_fac (the forward saves the
+    backward's per-pixel factors; ADVPATCH_WARP_FAC, default on) against
+    po_warp_box_fwd_keyed / po_warp_box_bwd_keyed (the backward re-evaluates
+    the warp): warped patches (mode 0), composites (mode 1, whole and sparse)
+    and patch gradients bit for bit."""
+    ld, sy = pkg_mod("load_data"), pkg_mod("synthetic")
+    seed, step, b0 = 0x77, 2, 1
+    keyed = {k: v for k, v in sy.draws_device(seed, step, b0, B, P, DEV).items() if k != "noise"}
+    keyed["noise_key"] = (seed, step, b0)
+    img = sy.frames(B, S, seed=23).to(DEV)
+    lab = sy.labels(B, seed=24)
+    if big:
+        lab[:, :, 3:5] = lab[:, :, 3:5].clamp(min=0.6)
+    lab = lab.to(DEV)
+    patch = sy.patch(P, seed=25).to(DEV)
+    gen = torch.Generator().manual_seed(26)
+    g4 = torch.randn(B, 1, 3, S, S, generator=gen).to(DEV)
+    g3 = torch.randn(B, 3, S, S, generator=gen).to(DEV)
+    res = {}
+    for fac in ("0", "1"):
+        monkeypatch.setenv("ADVPATCH_WARP_FAC", fac)
+        outs = []
+        for form in ("mode0", "full", "sparse"):
+            pt = ld.PatchTransformer()
+            assert pt.warp_form == "box" and pt.sparse_ok(S, keyed)
+            pg = patch.clone().requires_grad_(True)
+            if form == "mode0":
+                out, _ = pt(pg, lab, S, draws=keyed)
+                out.backward(g4)
+            else:
+                out, _ = pt.forward_composite(pg, lab, img, S, draws=keyed, sparse=form == "sparse")
+                out.backward(g3)
+            out = out.detach()
+            if form == "sparse":                      # only the quad-widened boxes are written
+                out = out[_quad_box_mask(pt.last_roi, B, S).to(DEV).expand(B, 3, S, S)]
+            outs.append((out, pg.grad.clone()))
+        res[fac] = outs
+    for (o0, g0), (o1, g1) in zip(res["0"], res["1"]):
+        assert torch.equal(o0, o1)
+        assert torch.equal(g0, g1) and bool((g0 != 0).any())
+
+
 @pytest.mark.parametrize("P", [224, 37])
 def test_patch_front_matches_separate_nodes(P):
     """patch_front (median pool + regularisers in one autograd node, the
