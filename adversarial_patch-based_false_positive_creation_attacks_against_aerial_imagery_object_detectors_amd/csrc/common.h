@@ -139,6 +139,14 @@ __device__ __forceinline__ uint32_t amax_read(const uint32_t* slot) {
   return (uint32_t)__builtin_amdgcn_readfirstlane(u);
 }
 
+// XCD-aware bijective remap: consecutive logical tiles share an XCD's L2
+// (workgroups are dispatched to the 8 XCDs round-robin: orig % 8)
+__device__ __forceinline__ int xcd_remap() {
+  const int nwg = gridDim.x, orig = blockIdx.x;
+  const int q = nwg / 8, r8 = nwg % 8, xcd = orig % 8;
+  return (xcd < r8 ? xcd * (q + 1) : r8 * (q + 1) + (xcd - r8) * q) + orig / 8;
+}
+
 }  // namespace po
 
 #define PO_REQUIRE(cond, ...)          \

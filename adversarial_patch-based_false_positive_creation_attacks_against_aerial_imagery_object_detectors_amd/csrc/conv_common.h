@@ -150,13 +150,6 @@ __device__ __forceinline__ bool tile_live(const ConvArgs& a, int m0, int rows) {
   return false;
 }
 
-// XCD-aware bijective remap: consecutive logical tiles share an XCD's L2
-__device__ __forceinline__ int xcd_remap() {
-  const int nwg = gridDim.x, orig = blockIdx.x;
-  const int q = nwg / 8, r8 = nwg % 8, xcd = orig % 8;
-  return (xcd < r8 ? xcd * (q + 1) : r8 * (q + 1) + (xcd - r8) * q) + orig / 8;
-}
-
 // Raw partial sums of one split-K slice (the reduction applies the epilogue)
 template <int TM, int TN>
 __device__ __forceinline__ void store_partials(const ConvArgs& a, const floatx16 (&acc)[TM][TN], int m0, int n0,

@@ -671,11 +671,15 @@ __global__ __launch_bounds__(256) void warp_bwd_b_k(const float* __restrict__ gf
                                                     const float* __restrict__ contrast,
                                                     const float* __restrict__ bright,
                                                     const double* __restrict__ affine, WarpGeom g,
-                                                    int B, float* __restrict__ d_mp) {
+                                                    int B, float* __restrict__ d_mp, int xr) {
   __shared__ float part[3][WB_G][WB_EL];
   __shared__ WarpInv tab[WB_CH];
   const int el = threadIdx.x % WB_EL, q = threadIdx.x / WB_EL;
-  const int e0 = blockIdx.x * WB_EL + el;
+  // xr: consecutive element blocks on one XCD (a band of patch rows per XCD):
+  // neighbouring elements share candidate pixels, whose gfac lines then stay
+  // in that XCD's L2 instead of being fetched by several
+  const int blk = xr ? po::xcd_remap() : (int)blockIdx.x;
+  const int e0 = blk * WB_EL + el;
   const bool live = e0 < g.P * g.P;
   const int e = live ? e0 : 0;
   const int pr = e / g.P, pc = e % g.P;
@@ -794,20 +798,24 @@ __global__ __launch_bounds__(256) void warp_bwd_b_k(const float* __restrict__ gf
 void launch_bwd_b(const float* gfac, const float* mp, const float* noise, const float* contrast, const float* bright,
                   const double* affine, const WarpGeom& g, int B, int P, float* d_mp, hipStream_t st,
                   bool il = false) {
+  static const int xr = [] {
+    const char* e = getenv("ADVPATCH_WARP_XCD");
+    return (e && e[0] == '0') ? 0 : 1;
+  }();
   if (B > 32) {
     if (il)
       hipLaunchKernelGGL((warp_bwd_b_k<8, 32, true>), dim3(po::ceil_div(P * P, 8)), dim3(256), 0, st, gfac, mp, noise,
-                         contrast, bright, affine, g, B, d_mp);
+                         contrast, bright, affine, g, B, d_mp, xr);
     else
       hipLaunchKernelGGL((warp_bwd_b_k<8, 32, false>), dim3(po::ceil_div(P * P, 8)), dim3(256), 0, st, gfac, mp,
-                         noise, contrast, bright, affine, g, B, d_mp);
+                         noise, contrast, bright, affine, g, B, d_mp, xr);
   } else {
     if (il)
       hipLaunchKernelGGL((warp_bwd_b_k<32, 8, true>), dim3(po::ceil_div(P * P, 32)), dim3(256), 0, st, gfac, mp,
-                         noise, contrast, bright, affine, g, B, d_mp);
+                         noise, contrast, bright, affine, g, B, d_mp, xr);
     else
       hipLaunchKernelGGL((warp_bwd_b_k<32, 8, false>), dim3(po::ceil_div(P * P, 32)), dim3(256), 0, st, gfac, mp,
-                         noise, contrast, bright, affine, g, B, d_mp);
+                         noise, contrast, bright, affine, g, B, d_mp, xr);
   }
 }
 
