@@ -89,11 +89,13 @@ __global__ __launch_bounds__(256) void first_fwd2_k(const float* __restrict__ im
                                                     int act, float* __restrict__ y,
                                                     uint32_t* __restrict__ amax,
                                                     const float* __restrict__ pimg,
-                                                    const int32_t* __restrict__ roi) {
+                                                    const int32_t* __restrict__ roi, int xr) {
   constexpr int LS = CO + 1;
   __shared__ float ys[256 * LS];
   const int64_t npix = (int64_t)B * Ho * Wo;
-  const int64_t pbase = (int64_t)blockIdx.x * 512;
+  // xr: consecutive pixel blocks on one XCD (the rows above and below a
+  // block's are its neighbours' rows: shared in that XCD's L2)
+  const int64_t pbase = (int64_t)(xr ? po::xcd_remap() : (int)blockIdx.x) * 512;
   const int tid = threadIdx.x;
   const uint32_t img_bytes = (uint32_t)((int64_t)B * 3 * H * W * 4);
   const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(img), 0, img_bytes, 0x00020000);
@@ -408,13 +410,15 @@ __global__ __launch_bounds__(256) void first_pool_tile_k(const float* __restrict
                                                          float* __restrict__ y, int8_t* __restrict__ am,
                                                          uint32_t* __restrict__ amax,
                                                          const float* __restrict__ pimg,
-                                                         const int32_t* __restrict__ roi) {
+                                                         const int32_t* __restrict__ roi, int xr) {
   constexpr int LS = CO + 1;
   constexpr int TE = 34, TLD = 40;                  // input window rows/columns (2*16 + 2); LDS row: 10 column groups
   static_assert(3 * TE * TLD <= 256 * LS, "input window must fit the output staging");
   __shared__ float ys[256 * LS];
   const int tid = threadIdx.x;
-  int t = (int)blockIdx.x;
+  // xr: consecutive tiles (row-major within an image) on one XCD, so the
+  // halo rows and columns neighbouring tiles share hit that XCD's L2
+  int t = xr ? po::xcd_remap() : (int)blockIdx.x;
   const int b = t / (tiles_x * tiles_y);
   t -= b * tiles_x * tiles_y;
   const int ty = t / tiles_x, tx = t - ty * tiles_x;
@@ -576,12 +580,19 @@ int first_fwd(const float* img, const float* pimg, const int32_t* roi, int B, in
              "po_conv_first_fwd: image batch must be < 2 GiB");
   PO_REQUIRE(!pimg || (roi && CO <= 32 && H == W), "po_conv_first_fwd_cmp: needs roi, a square image and Cout_p <= 32");
   dim3 grid2(po::ceil_div(n, 512));
+  // the XCD remap cuts this launch's fetched bytes 229 -> 68 MB (yolov3 B=16)
+  // but measured 201 -> 206 us: off unless ADVPATCH_FIRST_XCD=1
+  // (profiles/r05/first_xcd_ab.txt)
+  static const int xr = [] {
+    const char* e = getenv("ADVPATCH_FIRST_XCD");
+    return (e && e[0] == '1') ? 1 : 0;
+  }();
   if (CO == 16)
     hipLaunchKernelGGL(first_fwd2_k<16>, grid2, dim3(256), 0, st, img, B, H, W, stride, Ho, Wo, Wt, bias, Cout, act, y, amax,
-                       pimg, roi);
+                       pimg, roi, xr);
   else if (CO == 32)
     hipLaunchKernelGGL(first_fwd2_k<32>, grid2, dim3(256), 0, st, img, B, H, W, stride, Ho, Wo, Wt, bias, Cout, act, y, amax,
-                       pimg, roi);
+                       pimg, roi, xr);
   else
     hipLaunchKernelGGL(first_fwd_k<64>, grid, dim3(256), 0, st, img, B, H, W, stride, Ho, Wo, Wt, bias, Cout, Cout_p, act, y, amax);
   return po::check_launch("po_conv_first_fwd");
@@ -594,6 +605,10 @@ int first_pool_fwd(const float* img, const float* pimg, const int32_t* roi, int 
   static const bool lt = [] {
     const char* e = getenv("ADVPATCH_FIRST_TILE");
     return !(e && e[0] == '0');
+  }();
+  static const int xr = [] {
+    const char* e = getenv("ADVPATCH_FIRST_XCD");
+    return (e && e[0] == '0') ? 0 : 1;
   }();
   PO_REQUIRE((Cout_p == 16 || Cout_p == 32) && Cout > 0 && Cout <= Cout_p,
              "po_conv_first_pool_fwd: Cout_p must be 16 or 32 (got %d, Cout %d)", Cout_p, Cout);
@@ -610,7 +625,7 @@ int first_pool_fwd(const float* img, const float* pimg, const int32_t* roi, int 
     dim3 gt((unsigned)(B * tx * ty));
 #define PO_FPT(CO_, WI_)                                                                                    \
   hipLaunchKernelGGL((first_pool_tile_k<CO_, WI_>), gt, dim3(256), 0, st, img, B, H, W, Hp, Wp, tx, ty, Wt, bias, \
-                     Cout, act, y, argmax, amax, pimg, roi)
+                     Cout, act, y, argmax, amax, pimg, roi, xr)
     if (Cout_p == 16) {
       if (wino) PO_FPT(16, true); else PO_FPT(16, false);
     } else {
