@@ -37,7 +37,7 @@ constexpr uint32_t kOOB = 0x80000000u;
 #define PO_HALO_OCC 3                      // workgroups per CU (134 VGPRs: 3 waves per SIMD)
 #endif
 
-__global__ __launch_bounds__(256, PO_HALO_OCC) void conv_halo_pool_k(const ConvArgs a, int tiles_r, int tiles_c, int ntiles) {
+__global__ __launch_bounds__(256, PO_HALO_OCC) void conv_halo_pool_k(const ConvArgs a, int tiles_r, int tiles_c, int ntiles, int xr) {
   __shared__ __attribute__((aligned(16))) float smem[2 * PATCH];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int h = lane >> 5, n = lane & 31;
@@ -87,7 +87,9 @@ __global__ __launch_bounds__(256, PO_HALO_OCC) void conv_halo_pool_k(const ConvA
   };
 
   float my = 0.f;
-  int tile = blockIdx.x;
+  // xr: the workgroups of one XCD walk consecutive tiles at each step (their
+  // halos then meet in that XCD's L2); the schedule stays a bijection
+  int tile = xr ? po::xcd_remap() : (int)blockIdx.x;
   if (tile < ntiles) gload(tile);
   for (int it = 0; tile < ntiles; ++it) {
     float* P = smem + (it & 1) * PATCH;
@@ -163,7 +165,11 @@ int launch_halo(const ConvArgs& a, hipStream_t st) {
   // persistent: as many workgroups as the device holds at once (queried once per device)
   const int resident = resident_groups_cached(reinterpret_cast<const void*>(conv_halo_pool_k), 256);
   const int grid = (int)(ntiles < resident ? ntiles : resident);
-  hipLaunchKernelGGL(conv_halo_pool_k, dim3(grid), dim3(256), 0, st, a, tiles_r, tiles_c, (int)ntiles);
+  static const int xr = [] {
+    const char* e = getenv("ADVPATCH_HALO_XCD");
+    return (e && e[0] == '0') ? 0 : 1;
+  }();
+  hipLaunchKernelGGL(conv_halo_pool_k, dim3(grid), dim3(256), 0, st, a, tiles_r, tiles_c, (int)ntiles, xr);
   return check_launch("po_conv (halo pool tile)");
 }
 }  // namespace po
