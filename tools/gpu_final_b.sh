@@ -2,7 +2,7 @@
 # round-end: full -m gpu suite, default bench line, steady-state profiles of both configs
 set -e
 cd "$GRAFT_REPO_ROOT"
-OUT=gpurun_out/final2
+OUT=gpurun_out/${FINAL_OUT:-final2}
 mkdir -p $OUT
 timeout -k 10 700 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > $OUT/tests_full.txt 2>&1 || { tail -30 $OUT/tests_full.txt; exit 1; }
 tail -1 $OUT/tests_full.txt
