@@ -635,10 +635,22 @@ __global__ __launch_bounds__(512, 1) void conv_wino6_k(const ConvArgs a, const f
 // Channels past Cin_p (Cin_p % 64 != 0) are neither read nor written.  An
 // m-block without a live tile (boxes) is skipped: no unit reads it.
 constexpr int PRE_KS = 4;                      // k-steps per wino6_pre_k block
-__global__ __launch_bounds__(512) void wino6_pre_k(const ConvArgs a, float* __restrict__ VG, int Ht, int Wt) {
-  const int tm = blockIdx.x, kc_n = a.Cin_p / WK;
+__global__ __launch_bounds__(512) void wino6_pre_k(const ConvArgs a, float* __restrict__ VG, int Ht, int Wt, int xr) {
+  // xr: the (m-block, k-group) blocks in an XCD-aware order -- consecutive
+  // m-blocks of one k-group on one XCD, so the window rows that vertically
+  // neighbouring tile rows share meet in that XCD's L2 (a bijection over the
+  // grid; blocks are dispatched to the 8 XCDs round-robin in linear order)
+  int bx = blockIdx.x, by = blockIdx.y;
+  if (xr) {
+    const int gx = gridDim.x, n = gx * gridDim.y, lin = by * gx + bx;
+    const int qn = n / 8, r8 = n % 8, xcd = lin % 8;
+    const int lr = (xcd < r8 ? xcd * (qn + 1) : r8 * (qn + 1) + (xcd - r8) * qn) + lin / 8;
+    bx = lr % gx;
+    by = lr / gx;
+  }
+  const int tm = bx, kc_n = a.Cin_p / WK;
   const int tid = threadIdx.x, r = tid >> 4, q = tid & 15;
-  const int ks = blockIdx.y * PRE_KS + (q >> 2);
+  const int ks = by * PRE_KS + (q >> 2);
   if (a.gbox) {
     const int per = Ht * Wt, m0 = tm * T6;
     const int b0 = po::div_by(m0, a.mg_tiles, a.sh_tiles);
@@ -773,7 +785,11 @@ int launch_wino6(const ConvArgs& a, const float* U6, hipStream_t st, float* VG, 
 #undef PO_W6
   PO_REQUIRE(k, "po_conv: tile 71 has no kernel for epilogue fields 0x%x", which);
   if (VG) {
-    hipLaunchKernelGGL(wino6_pre_k, dim3(ntm, ceil_div(kc_n, PRE_KS)), dim3(512), 0, st, b, VG, Ht, Wt);
+    static const int xr = [] {
+      const char* e = getenv("ADVPATCH_PRE_XCD");
+      return (e && e[0] == '0') ? 0 : 1;
+    }();
+    hipLaunchKernelGGL(wino6_pre_k, dim3(ntm, ceil_div(kc_n, PRE_KS)), dim3(512), 0, st, b, VG, Ht, Wt, xr);
     const int rc = check_launch("po_conv (tile 72 input transform)");
     if (rc) return rc;
   }
