@@ -74,6 +74,14 @@ __global__ __launch_bounds__(256) void first_fwd_k(const float* __restrict__ img
 // the hardware range check instead of branching.  The two 256-pixel halves
 // are staged through LDS and stored as two contiguous 16-byte-per-lane streams.
 typedef float f2_t __attribute__((ext_vector_type(2)));
+// nt: a streaming (non-temporal) store for outputs larger than the caches
+__device__ __forceinline__ void po_store4(float* p, float4 v, int nt) {
+  typedef float f4v __attribute__((ext_vector_type(4)));
+  if (nt)
+    __builtin_nontemporal_store((f4v){v.x, v.y, v.z, v.w}, reinterpret_cast<f4v*>(p));
+  else
+    *reinterpret_cast<float4*>(p) = v;
+}
 //
 // Composite source (pimg != NULL, po_conv_first_fwd_cmp): the input is the
 // patch composite, of which only the quad box of each image's footprint
@@ -89,7 +97,7 @@ __global__ __launch_bounds__(256) void first_fwd2_k(const float* __restrict__ im
                                                     int act, float* __restrict__ y,
                                                     uint32_t* __restrict__ amax,
                                                     const float* __restrict__ pimg,
-                                                    const int32_t* __restrict__ roi, int xr) {
+                                                    const int32_t* __restrict__ roi, int xr, int nt) {
   constexpr int LS = CO + 1;
   __shared__ float ys[256 * LS];
   const int64_t npix = (int64_t)B * Ho * Wo;
@@ -179,7 +187,7 @@ __global__ __launch_bounds__(256) void first_fwd2_k(const float* __restrict__ im
     for (int f = tid; f < nlive * (CO / 4); f += 256) {
       const int px = f / (CO / 4), ch = (f % (CO / 4)) * 4;
       const float* r = ys + px * LS + ch;
-      *reinterpret_cast<float4*>(yb + (int64_t)f * 4) = make_float4(r[0], r[1], r[2], r[3]);
+      po_store4(yb + (int64_t)f * 4, make_float4(r[0], r[1], r[2], r[3]), nt);
     }
   }
 }
@@ -410,7 +418,7 @@ __global__ __launch_bounds__(256) void first_pool_tile_k(const float* __restrict
                                                          float* __restrict__ y, int8_t* __restrict__ am,
                                                          uint32_t* __restrict__ amax,
                                                          const float* __restrict__ pimg,
-                                                         const int32_t* __restrict__ roi, int xr) {
+                                                         const int32_t* __restrict__ roi, int xr, int nt) {
   constexpr int LS = CO + 1;
   constexpr int TE = 34, TLD = 40;                  // input window rows/columns (2*16 + 2); LDS row: 10 column groups
   static_assert(3 * TE * TLD <= 256 * LS, "input window must fit the output staging");
@@ -490,7 +498,7 @@ __global__ __launch_bounds__(256) void first_pool_tile_k(const float* __restrict
     const int qy = q >> 4, qx = q & 15;
     if (qy < ny && qx < nx) {
       const float* r = ys + q * LS + ch;
-      *reinterpret_cast<float4*>(y + (row0 + (int64_t)qy * Wp + qx) * CO + ch) = make_float4(r[0], r[1], r[2], r[3]);
+      po_store4(y + (row0 + (int64_t)qy * Wp + qx) * CO + ch, make_float4(r[0], r[1], r[2], r[3]), nt);
     }
   }
 }
@@ -587,12 +595,16 @@ int first_fwd(const float* img, const float* pimg, const int32_t* roi, int B, in
     const char* e = getenv("ADVPATCH_FIRST_XCD");
     return (e && e[0] == '1') ? 1 : 0;
   }();
+  static const int nt = [] {
+    const char* e = getenv("ADVPATCH_FIRST_NT");
+    return (e && e[0] == '1') ? 1 : 0;
+  }();
   if (CO == 16)
     hipLaunchKernelGGL(first_fwd2_k<16>, grid2, dim3(256), 0, st, img, B, H, W, stride, Ho, Wo, Wt, bias, Cout, act, y, amax,
-                       pimg, roi, xr);
+                       pimg, roi, xr, nt);
   else if (CO == 32)
     hipLaunchKernelGGL(first_fwd2_k<32>, grid2, dim3(256), 0, st, img, B, H, W, stride, Ho, Wo, Wt, bias, Cout, act, y, amax,
-                       pimg, roi, xr);
+                       pimg, roi, xr, nt);
   else
     hipLaunchKernelGGL(first_fwd_k<64>, grid, dim3(256), 0, st, img, B, H, W, stride, Ho, Wo, Wt, bias, Cout, Cout_p, act, y, amax);
   return po::check_launch("po_conv_first_fwd");
@@ -610,6 +622,10 @@ int first_pool_fwd(const float* img, const float* pimg, const int32_t* roi, int 
     const char* e = getenv("ADVPATCH_FIRST_XCD");
     return (e && e[0] == '0') ? 0 : 1;
   }();
+  static const int nt = [] {
+    const char* e = getenv("ADVPATCH_FIRST_NT");
+    return (e && e[0] == '1') ? 1 : 0;
+  }();
   PO_REQUIRE((Cout_p == 16 || Cout_p == 32) && Cout > 0 && Cout <= Cout_p,
              "po_conv_first_pool_fwd: Cout_p must be 16 or 32 (got %d, Cout %d)", Cout_p, Cout);
   PO_REQUIRE(B > 0 && H >= 2 && W >= 2, "po_conv_first_pool_fwd: bad size B=%d H=%d W=%d", B, H, W);
@@ -625,7 +641,7 @@ int first_pool_fwd(const float* img, const float* pimg, const int32_t* roi, int 
     dim3 gt((unsigned)(B * tx * ty));
 #define PO_FPT(CO_, WI_)                                                                                    \
   hipLaunchKernelGGL((first_pool_tile_k<CO_, WI_>), gt, dim3(256), 0, st, img, B, H, W, Hp, Wp, tx, ty, Wt, bias, \
-                     Cout, act, y, argmax, amax, pimg, roi, xr)
+                     Cout, act, y, argmax, amax, pimg, roi, xr, nt)
     if (Cout_p == 16) {
       if (wino) PO_FPT(16, true); else PO_FPT(16, false);
     } else {
