@@ -60,6 +60,11 @@ for k, (name, args, desc) in enumerate(plan.bwd_ops):
     else:
         cands = [(t, ks) for t in (3, 5, 7, 9, 13, 15, 17, 19) for ks in (1, 2, 4, 8)
                  if desc.ntaps * desc.Cin_p // plan.tile_shape(t)[2] // ks >= 2]
+        if desc.ntaps == 9 and os.environ.get("PROBE_WINO_ON_DIRECT"):
+            # a direct-tile 3x3 launch: the Winograd tiles too (refused ones time as None)
+            cands += [(t, ks) for t in (66, 67, 68, 71, 72) for ks in (1, 2, 4, 8, 16) if desc.Cin_p // 16 // ks >= 2]
+    if cur not in cands:
+        cands.append(cur)
     for c in cands:
         plan._set_tile(desc, c)
         t = timeit(args)
@@ -70,6 +75,8 @@ for k, (name, args, desc) in enumerate(plan.bwd_ops):
     print("k=%3d %3d^2 Cin%4d N%4d tap%d cur %s %.1f us  live_wg %d  best %s %.1f us" % (
         k, desc.Hg, desc.Cin_p, desc.N, desc.ntaps, "%d/%d" % cur, res["t"].get("%d/%d" % cur, -1), live,
         best[0], best[1]), flush=True)
+    if os.environ.get("PROBE_VERBOSE"):
+        print("   ", json.dumps(res["t"]), flush=True)
     rows.append(res)
 tot_cur = sum(r["t"].get("%d/%d" % r["cur"], 0) for r in rows)
 tot_best = sum(min(r["t"].values()) for r in rows)
