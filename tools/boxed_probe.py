@@ -53,7 +53,8 @@ for k, (name, args, desc) in enumerate(plan.bwd_ops):
         continue
     cur = (int(desc.tile), int(desc.ksplit))
     live = plan._live_tiles(desc, cur[0], plan.WINO_TILES.get(cur[0], plan.tile_shape(cur[0]))[0], cones)
-    res = {"k": k, "Hg": desc.Hg, "Cin_p": desc.Cin_p, "N": desc.N, "ntaps": desc.ntaps, "cur": cur,
+    res = {"key": json.dumps(list(plan._tune_key(args, desc))),
+           "k": k, "Hg": desc.Hg, "Cin_p": desc.Cin_p, "N": desc.N, "ntaps": desc.ntaps, "cur": cur,
            "live_wg": live, "mfma_flops": plan.launch_mfma_flops(desc, cones), "t": {}}
     if cur[0] in plan.WINO_TILES:
         cands = [(t, ks) for t in (66, 67, 68, 71, 72) for ks in (1, 2, 3, 4, 6, 8) if desc.Cin_p // 16 // ks >= 2]
@@ -87,3 +88,30 @@ if out:
         for r in rows:
             r["cur"] = "%d/%d" % r["cur"]
             f.write(json.dumps(r) + "\n")
+
+wr = os.environ.get("PROBE_WRITE")
+if wr:
+    # per cache key (launches of one signature share a choice): the candidate
+    # with the least summed time over those launches, kept where it beats the
+    # cached choice by >= 3 %; the updated cache goes to PROBE_WRITE
+    cache = json.load(open(os.environ["ADVPATCH_TUNE_CACHE"]))
+    by = {}
+    for r in rows:
+        by.setdefault(r["key"], []).append(r)
+    changed = 0
+    for key, rs in by.items():
+        curs = {r["cur"] if isinstance(r["cur"], str) else "%d/%d" % r["cur"] for r in rs}
+        common = set.intersection(*(set(r["t"]) for r in rs))
+        if len(curs) != 1 or not common or key not in cache:
+            continue
+        cur = next(iter(curs))
+        tot = {c: sum(r["t"][c] for r in rs) for c in common}
+        best = min(tot, key=tot.get)
+        if cur in tot and tot[best] <= 0.97 * tot[cur]:
+            t, ks = (int(v) for v in best.split("/"))
+            print("key %s: %s %.1f us -> %s %.1f us over %d launches" % (key, cur, tot[cur], best, tot[best], len(rs)))
+            cache[key] = [t, ks]
+            changed += 1
+    with open(wr, "w") as f:
+        json.dump(cache, f)
+    print("updated %d cache entries -> %s" % (changed, wr))
