@@ -252,7 +252,8 @@ class _Warp(torch.autograd.Function):
             # into the gradient factors in place (po_warp_box_*_fac; "0": re-evaluate
             # the warp in the backward, po_warp_box_bwd_keyed -- the same bits)
             ctx.fac = None
-            if os.environ.get("ADVPATCH_WARP_FAC", "1") != "0":
+            # only when a backward can follow (no factor buffer for no-grad / eval forwards)
+            if ctx.needs_input_grad[0] and os.environ.get("ADVPATCH_WARP_FAC", "1") != "0":
                 ctx.fac = torch.empty(B * S * S * 4, device=mp.device)
                 nat.call("po_warp_box_fwd_fac", *head, nat.ptr(ctx.fac), nat.stream())
             else:
