@@ -59,7 +59,7 @@ for k, (name, args, desc) in enumerate(plan.bwd_ops):
     if cur[0] in plan.WINO_TILES:
         cands = [(t, ks) for t in (66, 67, 68, 71, 72) for ks in (1, 2, 3, 4, 6, 8) if desc.Cin_p // 16 // ks >= 2]
     else:
-        cands = [(t, ks) for t in (3, 5, 7, 9, 13, 15, 17, 19) for ks in (1, 2, 4, 8)
+        cands = [(t, ks) for t in (3, 5, 7, 9, 13, 15, 17, 19) for ks in (1, 2, 4, 8, 12, 16)
                  if desc.ntaps * desc.Cin_p // plan.tile_shape(t)[2] // ks >= 2]
         if desc.ntaps == 9 and os.environ.get("PROBE_WINO_ON_DIRECT"):
             # a direct-tile 3x3 launch: the Winograd tiles too (refused ones time as None)
