@@ -14,7 +14,7 @@ LIB_PATH = os.environ.get("ADVPATCH_LIB") or os.path.join(_HERE, "libadvpatch_hi
 
 c_int, c_float, c_int64, c_void_p = ctypes.c_int, ctypes.c_float, ctypes.c_int64, ctypes.c_void_p
 
-PO_ABI_VERSION = 26   # include/advpatch.h
+PO_ABI_VERSION = 27   # include/advpatch.h
 PO_CONV_NTILES = 72   # include/advpatch.h
 PO_AMAX_SUB = 64      # sub-slots per max|x| slot
 
@@ -40,8 +40,8 @@ _SIGS = {
     "po_median7_bwd": [c_void_p, c_void_p, c_int, c_int, c_int, c_void_p, c_void_p],
     "po_median_fwd": [c_void_p] + [c_int] * 11 + [c_void_p, c_void_p, c_void_p],
     "po_median_bwd": [c_void_p, c_void_p] + [c_int] * 11 + [c_void_p, c_void_p],
-    "po_patch_params": [c_void_p, c_int, c_int, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int,
-                        c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p],
+    "po_patch_params": [c_void_p, c_int, c_int, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int,
+                        c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p],
     "po_draws": [ctypes.c_uint64, ctypes.c_uint64, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p,
                  c_void_p, c_void_p, c_void_p],
     "po_check_finite": [c_void_p, c_int64, c_int, c_void_p, c_void_p],

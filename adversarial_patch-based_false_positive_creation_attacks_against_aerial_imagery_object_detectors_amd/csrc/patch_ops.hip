@@ -11,6 +11,7 @@
 #include "warp_geom.h"
 #include <math.h>
 #include <string.h>
+#include <algorithm>
 
 namespace po {
 static thread_local char g_err[512] = {0};
@@ -287,10 +288,44 @@ extern "C" int po_median_bwd(const float* dy, const int32_t* argidx, int C, int 
 // Placement parameters (load_data.py:453-509, 654-743)
 // ------------------------------------------------------------------------
 namespace {
+constexpr float kDrawPi = 3.14159265358979323846f;   // po_draws' pi (draw_ops.hip)
+constexpr int kLatticeN = 1 << 24;
+
+// sin and cos of an angle as torch.sin / torch.cos compute them on the CPU
+// (load_data.py:731-732; MKL VML, not correctly rounded, so not restatable):
+// angles on po_draws' lattice (angle_k = fp32(k 2^-24 fp32(2 pi) - pi)) are
+// looked up in `lut` [2^24][2] (load_data.sincos_lattice_table: the CPU's own
+// values, tabulated once per process); any other angle, or no table, gets the
+// correctly rounded values (float64 evaluation rounded once), which equal
+// the CPU's in ~95 % of cases.
+__device__ __forceinline__ void ref_sincos(float a, const float* __restrict__ lut, float& sn, float& cs) {
+  if (lut) {
+    const double span = (double)(2.0f * kDrawPi), from = (double)(-kDrawPi);
+    const double kd = rint(((double)a - from) / span * 16777216.0);
+    if (kd >= -1.0 && kd <= 16777216.0) {
+      const int k0 = (int)kd;
+      for (int d = -1; d <= 1; ++d) {
+        const int k = k0 + d;
+        if (k < 0 || k >= kLatticeN) continue;
+        const float ak = (float)((double)((float)k * 0x1p-24f) * span + from);
+        if (__float_as_uint(ak) == __float_as_uint(a)) {
+          const float2 v = reinterpret_cast<const float2*>(lut)[k];
+          sn = v.x;
+          cs = v.y;
+          return;
+        }
+      }
+    }
+  }
+  sn = (float)sin((double)a);
+  cs = (float)cos((double)a);
+}
+
 // one wave per image: the label scan is a wave reduction of (area, row) pairs
 __global__ __launch_bounds__(64) void patch_params_k(const float* __restrict__ lab, int B, int L,
                                                      const float* __restrict__ angle, const float* __restrict__ ux,
                                                      const float* __restrict__ uy, int do_rotate, int S, int P,
+                                                     int geometry, const float* __restrict__ lut,
                                                      float* __restrict__ theta, float* __restrict__ center,
                                                      float* __restrict__ tsize, int32_t* __restrict__ roi,
                                                      double* __restrict__ affine) {
@@ -320,6 +355,36 @@ __global__ __launch_bounds__(64) void patch_params_k(const float* __restrict__ l
   const float ty_f = fminf(uy[b], 0.8f);     // load_data.py:706
   center[2 * b + 0] = tx_f * fS;             // load_data.py:712-715
   center[2 * b + 1] = ty_f * fS;
+  if (geometry == 1) {
+    // the reference's fp32 arithmetic, op by op (warp_geom.h): lab_transform's
+    // (max row + min row) / 2 (load_data.py:474-477), * img_size (654-660),
+    // .mul(1/2) ** 2, the sum and sqrt (667-668), / patch side (717)
+    float s2 = 0.25f, s3 = 0.25f;
+    if (!(vmax > 0.99f)) {
+      s2 = __fdiv_rn(__fadd_rn(lb[imax * 5 + 2], lb[imin * 5 + 2]), 2.0f);
+      s3 = __fdiv_rn(__fadd_rn(lb[imax * 5 + 3], lb[imin * 5 + 3]), 2.0f);
+    }
+    const float h2 = __fmul_rn(__fmul_rn(s2, fS), 0.5f), h3 = __fmul_rn(__fmul_rn(s3, fS), 0.5f);
+    const float ts = __fsqrt_rn(__fadd_rn(__fmul_rn(h2, h2), __fmul_rn(h3, h3)));
+    const float sc = __fdiv_rn(ts, (float)P);
+    const float tx = __fmul_rn(__fadd_rn(-tx_f, 0.5f), 2.0f);             // load_data.py:726
+    const float ty = __fmul_rn(__fadd_rn(-ty_f, 0.5f), 2.0f);             // load_data.py:727
+    float sn = 0.f, cs = 1.f;                                              // angle fill_(0): 614
+    if (do_rotate) ref_sincos(angle[b], lut, sn, cs);
+    float th[6];
+    po::ref_theta(sn, cs, sc, tx, ty, th);
+    float* tho = theta + 6 * b;
+    for (int k = 0; k < 6; ++k) tho[k] = th[k];
+    if (tsize) tsize[b] = ts;
+    if (affine) po::store_ref_row(th, affine + 6 * b);
+    if (roi) {
+      double thd[6], af[6];
+      for (int k = 0; k < 6; ++k) thd[k] = (double)th[k];
+      po::theta_pixel_affine(thd, (double)S, af);
+      po::footprint_roi(af, S, P, roi + 4 * b);
+    }
+    return;
+  }
   // Placement geometry in float64 (from the same fp32 labels and draws).  The
   // translation terms of theta reach |tx cos / scale| ~ 10-20 and cancel in the
   // affine grid down to the patch's ~0.4; in fp32 that cancellation leaves
@@ -354,14 +419,16 @@ __global__ __launch_bounds__(64) void patch_params_k(const float* __restrict__ l
 }  // namespace
 
 extern "C" int po_patch_params(const float* lab, int B, int L, const float* angle, const float* ux,
-                               const float* uy, int do_rotate, int S, int P, float* theta,
-                               float* center, float* target_size, int32_t* roi, double* affine,
-                               po_stream_t s) {
+                               const float* uy, int do_rotate, int S, int P, int geometry,
+                               const float* sincos_lut, float* theta, float* center, float* target_size,
+                               int32_t* roi, double* affine, po_stream_t s) {
   PO_REQUIRE(lab && ux && uy && theta && center, "po_patch_params: null pointer");
   PO_REQUIRE(!do_rotate || angle, "po_patch_params: angle required when do_rotate");
   PO_REQUIRE(B > 0 && L > 0 && S > 0 && P > 0, "po_patch_params: bad shape");
+  PO_REQUIRE(geometry == 0 || (geometry == 1 && S > 1), "po_patch_params: geometry must be 0 (float64) or 1 (reference fp32, S > 1)");
+  PO_REQUIRE(!sincos_lut || ((uintptr_t)sincos_lut % 8) == 0, "po_patch_params: sincos_lut must be 8-byte aligned");
   hipLaunchKernelGGL(patch_params_k, dim3(B), dim3(64), 0, po::stream_of(s), lab, B, L, angle, ux, uy,
-                     do_rotate, S, P, theta, center, target_size, roi, affine);
+                     do_rotate, S, P, geometry, sincos_lut, theta, center, target_size, roi, affine);
   return po::check_launch("po_patch_params");
 }
 
@@ -422,6 +489,39 @@ __device__ __forceinline__ void bilinear(double ix, double iy, int& x0, int& y0,
   w[3] = (float)(ex * ey);
 }
 
+// The bilinear corner (x0, y0) and weights {nw, ne, sw, se} of output pixel
+// (i, j) under image geometry G; false if no corner lies in the padded patch
+// region [pad - 1, pad + P) -- the output is then exactly 0.  Reference form:
+// grid_sample's fp32 arithmetic (warp_geom.h; GridSamplerKernel.cpp: w = ix -
+// floor(ix), e = 1 - w, nw = s*e, ne = s*w, sw = n*e, se = n*w).
+__device__ __forceinline__ bool sample_point(const po::Geo& G, const WarpGeom& g, int i, int j, int& x0, int& y0,
+                                             float w[4]) {
+  if (G.ref) {
+    float ix, iy;
+    po::ref_sample_coord(G.th, g.S, i, j, ix, iy);
+    if (!(ix >= (float)(g.padL - 1) && ix < (float)(g.padL + g.P) && iy >= (float)(g.padT - 1) &&
+          iy < (float)(g.padT + g.P)))
+      return false;
+    const float fx = floorf(ix), fy = floorf(iy);
+    x0 = (int)fx;
+    y0 = (int)fy;
+    const float ex = __fsub_rn(ix, fx), wx = __fsub_rn(1.0f, ex);
+    const float ny = __fsub_rn(iy, fy), sy = __fsub_rn(1.0f, ny);
+    w[0] = __fmul_rn(sy, wx);
+    w[1] = __fmul_rn(sy, ex);
+    w[2] = __fmul_rn(ny, wx);
+    w[3] = __fmul_rn(ny, ex);
+    return true;
+  }
+  double ix, iy;
+  sample_coord(G.af, i, j, ix, iy);
+  if (!(ix >= (double)(g.padL - 1) && ix < (double)(g.padL + g.P) && iy >= (double)(g.padT - 1) &&
+        iy < (double)(g.padT + g.P)))
+    return false;
+  bilinear(ix, iy, x0, y0, w);
+  return true;
+}
+
 __device__ __forceinline__ float aug_value(const float* __restrict__ mp, const NoiseSrc& ns,
                                            float contrast, float bright, int ch, int pr, int pc, int P) {
   const size_t o = ((size_t)ch * P + pr) * P + pc;
@@ -429,21 +529,22 @@ __device__ __forceinline__ float aug_value(const float* __restrict__ mp, const N
   return fminf(fmaxf(v, 0.f), 1.f);                      // load_data.py:574
 }
 
+// one bilinear term: the reference form accumulates as grid_sample's fma
+// chain (fma(v, w, acc) corner after corner), the float64 form adds products
+__device__ __forceinline__ float bterm(bool ref, float v, float w, float acc) {
+  return ref ? __fmaf_rn(v, w, acc) : acc + v * w;
+}
+
 // Forward of one output pixel: adv_t[3] (clamped) and msk_t.  Returns false
 // if no neighbour lies inside the padded patch region (output exactly 0).
 template <bool AUG = true>
-__device__ __forceinline__ bool warp_pixel(const double* af, const WarpGeom& g, const float* mp,
+__device__ __forceinline__ bool warp_pixel(const po::Geo& G, const WarpGeom& g, const float* mp,
                                            const NoiseSrc& nz, float contrast, float bright, int i, int j,
                                            float adv[3], float& msk, bool raw_in_range[3]) {
-  double ix, iy;
-  sample_coord(af, i, j, ix, iy);
-  // no corner inside the padded patch region [pad, pad+P): output exactly 0
-  if (!(ix >= (double)(g.padL - 1) && ix < (double)(g.padL + g.P) && iy >= (double)(g.padT - 1) &&
-        iy < (double)(g.padT + g.P)))
-    return false;
   int x0, y0;
   float w[4];
-  bilinear(ix, iy, x0, y0, w);
+  if (!sample_point(G, g, i, j, x0, y0, w)) return false;
+  const bool ref = G.ref != 0;
   const int cx[4] = {x0, x0 + 1, x0, x0 + 1};
   const int cy[4] = {y0, y0, y0 + 1, y0 + 1};
   float a0 = 0.f, a1 = 0.f, a2 = 0.f, m = 0.f;
@@ -452,16 +553,16 @@ __device__ __forceinline__ bool warp_pixel(const double* af, const WarpGeom& g, 
     const int pr = cy[k] - g.padT, pc = cx[k] - g.padL;
     if (pr >= 0 && pr < g.P && pc >= 0 && pc < g.P) {
       if (AUG) {
-        a0 += aug_value(mp, nz, contrast, bright, 0, pr, pc, g.P) * w[k];
-        a1 += aug_value(mp, nz, contrast, bright, 1, pr, pc, g.P) * w[k];
-        a2 += aug_value(mp, nz, contrast, bright, 2, pr, pc, g.P) * w[k];
+        a0 = bterm(ref, aug_value(mp, nz, contrast, bright, 0, pr, pc, g.P), w[k], a0);
+        a1 = bterm(ref, aug_value(mp, nz, contrast, bright, 1, pr, pc, g.P), w[k], a1);
+        a2 = bterm(ref, aug_value(mp, nz, contrast, bright, 2, pr, pc, g.P), w[k], a2);
       } else {                                // test_real: clamp(patch) only (load_data.py:1070-1076)
         const size_t o = (size_t)pr * g.P + pc, pp = (size_t)g.P * g.P;
-        a0 += fminf(fmaxf(mp[o], 0.f), 1.f) * w[k];
-        a1 += fminf(fmaxf(mp[o + pp], 0.f), 1.f) * w[k];
-        a2 += fminf(fmaxf(mp[o + 2 * pp], 0.f), 1.f) * w[k];
+        a0 = bterm(ref, fminf(fmaxf(mp[o], 0.f), 1.f), w[k], a0);
+        a1 = bterm(ref, fminf(fmaxf(mp[o + pp], 0.f), 1.f), w[k], a1);
+        a2 = bterm(ref, fminf(fmaxf(mp[o + 2 * pp], 0.f), 1.f), w[k], a2);
       }
-      m += 1.f * w[k];
+      m = bterm(ref, 1.f, w[k], m);
     }
   }
   raw_in_range[0] = a0 >= 0.f && a0 <= 1.f;
@@ -488,7 +589,8 @@ __global__ __launch_bounds__(256) void warp_fwd_k(const float* __restrict__ img,
   const size_t o = (size_t)b * 3 * plane + (size_t)i * g.S + j;
   float adv[3], msk;
   bool rng[3];
-  const bool hit = warp_pixel(affine + 6 * b, g, mp, noise_src(noise, g, b), g.pre ? 1.f : contrast[b],
+  const po::Geo G = po::load_geo(affine + 6 * b, g.S);
+  const bool hit = warp_pixel(G, g, mp, noise_src(noise, g, b), g.pre ? 1.f : contrast[b],
                               g.pre ? 0.f : bright[b], i, j, adv, msk, rng);
 #pragma unroll
   for (int ch = 0; ch < 3; ++ch) {
@@ -515,7 +617,7 @@ __global__ __launch_bounds__(256) void warp_fwd4_k(const float* __restrict__ img
   const int i = q / sq, j0 = (q - i * sq) * 4;
   const size_t plane = (size_t)g.S * g.S;
   const size_t o = (size_t)b * 3 * plane + (size_t)i * g.S + j0;
-  const double* th = affine + 6 * b;
+  const po::Geo G = po::load_geo(affine + 6 * b, g.S);
   const NoiseSrc nz = noise_src(noise, g, b);
   const float cb = g.pre ? 1.f : contrast[b], bb = g.pre ? 0.f : bright[b];
   float v[3][4];
@@ -523,7 +625,7 @@ __global__ __launch_bounds__(256) void warp_fwd4_k(const float* __restrict__ img
   for (int u = 0; u < 4; ++u) {
     float adv[3], msk;
     bool rng[3];
-    const bool hit = warp_pixel(th, g, mp, nz, cb, bb, i, j0 + u, adv, msk, rng);
+    const bool hit = warp_pixel(G, g, mp, nz, cb, bb, i, j0 + u, adv, msk, rng);
 #pragma unroll
     for (int ch = 0; ch < 3; ++ch) v[ch][u] = hit ? adv[ch] * msk : 0.f;   // load_data.py:791-792
   }
@@ -555,7 +657,8 @@ __global__ __launch_bounds__(256) void warp_bwd_a_k(const float* __restrict__ d_
   const size_t o = (size_t)b * 3 * plane + (size_t)i * g.S + j;
   float adv[3], msk;
   bool rng[3];
-  if (!warp_pixel(affine + 6 * b, g, mp, noise_src(noise, g, b), contrast[b], g.pre ? 0.f : bright[b],
+  const po::Geo G = po::load_geo(affine + 6 * b, g.S);
+  if (!warp_pixel(G, g, mp, noise_src(noise, g, b), contrast[b], g.pre ? 0.f : bright[b],
                   i, j, adv, msk, rng))
     return;   // never read by phase B
 #pragma unroll
@@ -588,7 +691,7 @@ __global__ __launch_bounds__(256) void warp_bwd_a4_k(const float* __restrict__ d
   const int i = q / sq, j0 = (q - i * sq) * 4;
   const size_t plane = (size_t)g.S * g.S;
   const size_t o = (size_t)b * 3 * plane + (size_t)i * g.S + j0;
-  const double* th = affine + 6 * b;
+  const po::Geo G = po::load_geo(affine + 6 * b, g.S);
   const NoiseSrc nz = noise_src(noise, g, b);
   const float cb = contrast[b], bb = g.pre ? 0.f : bright[b];
   float adv[4][3], msk[4];
@@ -596,7 +699,7 @@ __global__ __launch_bounds__(256) void warp_bwd_a4_k(const float* __restrict__ d
   bool any = false;
 #pragma unroll
   for (int u = 0; u < 4; ++u) {
-    hit[u] = warp_pixel(th, g, mp, nz, cb, bb, i, j0 + u, adv[u], msk[u], rng[u]);
+    hit[u] = warp_pixel(G, g, mp, nz, cb, bb, i, j0 + u, adv[u], msk[u], rng[u]);
     any |= hit[u];
   }
   if (!any) return;
@@ -644,20 +747,23 @@ __global__ __launch_bounds__(256) void warp_bwd_a4_k(const float* __restrict__ d
 // groups all hold images).
 constexpr int WB_CH = 256;
 struct WarpInv {
-  double a[6], m[4];
+  po::Geo G;
+  float m[4], a02, a12;     // the inverse's linear part and the translation, rounded to fp32
   float cb, bb;
 };
-// image b's pixel-space map, its inverse's linear part, contrast, brightness
-__device__ __forceinline__ WarpInv make_inv(const double* af, float cb, float bb) {
+// image b's geometry, its pixel-space map's inverse linear part, contrast, brightness
+__device__ __forceinline__ WarpInv make_inv(const double* row, int S, float cb, float bb) {
   WarpInv w;
-#pragma unroll
-  for (int k = 0; k < 6; ++k) w.a[k] = af[k];
-  const double det = w.a[0] * w.a[4] - w.a[1] * w.a[3];
+  w.G = po::load_geo(row, S);
+  const double* a = w.G.af;
+  const double det = a[0] * a[4] - a[1] * a[3];
   const double inv = 1.0 / det;
-  w.m[0] = w.a[4] * inv;
-  w.m[1] = -w.a[1] * inv;
-  w.m[2] = -w.a[3] * inv;
-  w.m[3] = w.a[0] * inv;
+  w.m[0] = (float)(a[4] * inv);
+  w.m[1] = (float)(-a[1] * inv);
+  w.m[2] = (float)(-a[3] * inv);
+  w.m[3] = (float)(a[0] * inv);
+  w.a02 = (float)a[2];
+  w.a12 = (float)a[5];
   w.cb = cb;
   w.bb = bb;
   return w;
@@ -699,24 +805,27 @@ __global__ __launch_bounds__(256) void warp_bwd_b_k(const float* __restrict__ gf
     // built per workgroup in LDS, measured slower: 140 -> 158 us on tiny B=256)
     if (bc) __syncthreads();                  // the previous chunk's readers are done
     for (int t = threadIdx.x; t < nb; t += 256)
-      tab[t] = make_inv(affine + 6 * (bc + t), contrast[bc + t], g.pre ? 0.f : bright[bc + t]);
+      tab[t] = make_inv(affine + 6 * (bc + t), g.S, contrast[bc + t], g.pre ? 0.f : bright[bc + t]);
     __syncthreads();
     for (int bl = q; bl < (live ? nb : 0); bl += WB_G) {
       const int b = bc + bl;
-      const double* af = tab[bl].a;
+      const po::Geo& G = tab[bl].G;
       // output pixels whose sample point can have (r, c) as a bilinear corner:
-      // the preimage of (c-1, c+1) x (r-1, r+1) under the pixel-space affine
-      const double A02 = af[2], A12 = af[5];
-      const double m00 = tab[bl].m[0], m01 = tab[bl].m[1], m10 = tab[bl].m[2], m11 = tab[bl].m[3];
-      const double X = (double)c - A02, Y = (double)r - A12;
-      const double jc = m00 * X + m01 * Y, ic = m10 * X + m11 * Y;
-      const double hj = fabs(m00) + fabs(m01), hi_ = fabs(m10) + fabs(m11);
-      const double jlo = jc - hj, jhi = jc + hj, ilo = ic - hi_, ihi = ic + hi_;
-      if (!(jhi >= -1.0 && jlo <= (double)g.S && ihi >= -1.0 && ilo <= (double)g.S)) continue;
-      constexpr double eps = 1e-6;
-      const double hiS = (double)(g.S - 1);
-      const int j0 = (int)fmax(0.0, ceil(jlo - eps)), j1 = (int)fmin(hiS, floor(jhi + eps));
-      const int i0 = (int)fmax(0.0, ceil(ilo - eps)), i1 = (int)fmin(hiS, floor(ihi + eps));
+      // the preimage of (c-1, c+1) x (r-1, r+1) under the pixel-space affine,
+      // evaluated in fp32 with a margin that covers that evaluation's rounding
+      // (|error| < 1e-4 px at these sizes) and, for the reference form, the
+      // distance of the fp32 sample points from the float64 map (well under
+      // 0.01 px): a wider scan only tests more pixels, each with the exact
+      // sample point below, so the candidates and their order are unchanged
+      const float X = (float)c - tab[bl].a02, Y = (float)r - tab[bl].a12;
+      const float m00 = tab[bl].m[0], m01 = tab[bl].m[1], m10 = tab[bl].m[2], m11 = tab[bl].m[3];
+      const float jc = m00 * X + m01 * Y, ic = m10 * X + m11 * Y;
+      const float eps = G.ref ? 0.05f : 1e-3f;
+      const float hj = fabsf(m00) + fabsf(m01) + eps, hi_ = fabsf(m10) + fabsf(m11) + eps;
+      const float jl = fmaxf(ceilf(jc - hj), 0.f), jh = fminf(floorf(jc + hj), (float)(g.S - 1));
+      const float il = fmaxf(ceilf(ic - hi_), 0.f), ih = fminf(floorf(ic + hi_), (float)(g.S - 1));
+      if (!(jl <= jh && il <= ih)) continue;                 // no pixel of the frame (or a NaN map)
+      const int j0 = (int)jl, j1 = (int)jh, i0 = (int)il, i1 = (int)ih;
       const float cb = tab[bl].cb, bb = tab[bl].bb;
       const NoiseSrc nz = noise_src(noise, g, b);
       float a0 = 0.f, a1 = 0.f, a2 = 0.f;
@@ -724,11 +833,9 @@ __global__ __launch_bounds__(256) void warp_bwd_b_k(const float* __restrict__ gf
       const float* gb = gfac + (size_t)b * (IL ? 4 : 3) * plane;
       for (int i = i0; i <= i1; ++i)
         for (int j = j0; j <= j1; ++j) {
-          double ix, iy;
-          sample_coord(af, i, j, ix, iy);
           int x0, y0;
           float wb[4];
-          bilinear(ix, iy, x0, y0, wb);
+          if (!sample_point(G, g, i, j, x0, y0, wb)) continue;
           const int dx = c - x0, dy = r - y0;
           if (dx < 0 || dx > 1 || dy < 0 || dy > 1) continue;
           const float w = wb[2 * dy + dx];
@@ -848,7 +955,8 @@ __global__ __launch_bounds__(256) void warp_multi_k(const float* __restrict__ im
     float adv[3], msk;
     bool rng[3];
     const NoiseSrc nz = noise_src(AUG ? noise : nullptr, g, t);     // !AUG: never read
-    if (!warp_pixel<AUG>(affine + 6 * t, g, mp, nz, AUG ? contrast[t] : 1.f, AUG ? bright[t] : 0.f, i, j, adv,
+    const po::Geo G = po::load_geo(affine + 6 * t, g.S);
+    if (!warp_pixel<AUG>(G, g, mp, nz, AUG ? contrast[t] : 1.f, AUG ? bright[t] : 0.f, i, j, adv,
                          msk, rng))
       continue;
 #pragma unroll
@@ -1016,6 +1124,97 @@ __global__ __launch_bounds__(256) void warp_quad_copy_k(const float* __restrict_
   }
 }
 
+// The box kernels over one flat list of the batch's box pixels: the per-image
+// grid (box_blocks(S) workgroups per image) dispatches every workgroup of an
+// image whose box is a few percent of the frame, and most of them find no
+// pixel (tiny B=256: 56 of 85 per image, ~14k empty workgroups per launch).
+// Here a fixed grid walks the concatenated boxes: each workgroup tabulates the
+// boxes' areas and their exclusive prefix in LDS (FLAT_MAXB images at most),
+// and pixel q of the list is pixel q - pre[b] of the image b with pre[b] <= q
+// < pre[b + 1] (binary search), row-major in that box as before -- the same
+// pixels with the same per-pixel arithmetic, so the same bits.
+constexpr int FLAT_MAXB = 1024;
+struct FlatBoxes {
+  int pre[FLAT_MAXB + 1];   // exclusive prefix of the box areas; pre[B] = total
+  int x0[FLAT_MAXB], bw[FLAT_MAXB], y0[FLAT_MAXB];
+  int part[256];
+};
+__device__ __forceinline__ int flat_boxes(const int32_t* __restrict__ roi, int B, int S, FlatBoxes& t) {
+  const int tid = threadIdx.x;
+  const int per = (B + 255) / 256, b0 = tid * per;
+  int sum = 0;
+  for (int k = 0; k < per; ++k) {
+    const int b = b0 + k;
+    if (b < B) {
+      const QBox q = quad_box(roi, b, S);
+      const int w = q.qx1 - q.qx0;
+      t.x0[b] = q.qx0;
+      t.bw[b] = w > 0 ? w : 1;
+      t.y0[b] = q.y0;
+      sum += w * (q.y1 - q.y0);
+    }
+  }
+  t.part[tid] = sum;
+  __syncthreads();
+  for (int o = 1; o < 256; o <<= 1) {         // inclusive scan of the 256 partial sums
+    const int v = tid >= o ? t.part[tid - o] : 0;
+    __syncthreads();
+    t.part[tid] += v;
+    __syncthreads();
+  }
+  int run = t.part[tid] - sum;                 // exclusive prefix of this thread's images
+  for (int k = 0; k < per; ++k) {
+    const int b = b0 + k;
+    if (b < B) {
+      t.pre[b] = run;
+      const QBox q = quad_box(roi, b, S);
+      run += (q.qx1 - q.qx0) * (q.y1 - q.y0);
+    }
+  }
+  if (tid == 255) t.pre[B] = t.part[255];
+  __syncthreads();
+  return t.pre[B];
+}
+// pixel q of the flat list -> image b and its pixel (i, j)
+__device__ __forceinline__ void flat_pixel(const FlatBoxes& t, int B, int q, int& b, int& i, int& j) {
+  int lo = 0, hi = B;
+  while (hi - lo > 1) {
+    const int mid = (lo + hi) >> 1;
+    if (t.pre[mid] <= q) lo = mid; else hi = mid;
+  }
+  b = lo;
+  const int p = q - t.pre[b], w = t.bw[b];
+  const int r = p / w;
+  i = t.y0[b] + r;
+  j = t.x0[b] + (p - r * w);
+}
+
+// one box pixel of the forward (warp_box_fwd_k / warp_box_flat_fwd_k)
+__device__ __forceinline__ void box_fwd_pixel(const float* __restrict__ img, const float* __restrict__ mp,
+                                              const po::Geo& G, const NoiseSrc& nz, float cb, float bb,
+                                              const WarpGeom& g, int mode, int b, int i, int j,
+                                              float* __restrict__ out, float* __restrict__ fac) {
+  const size_t plane = (size_t)g.S * g.S;
+  const size_t o = (size_t)b * 3 * plane + (size_t)i * g.S + j;
+  float adv[3], msk;
+  bool rng[3];
+  const bool hit = warp_pixel(G, g, mp, nz, cb, bb, i, j, adv, msk, rng);
+  float f4[4] = {-1.f, -1.f, -1.f, -1.f};
+#pragma unroll
+  for (int ch = 0; ch < 3; ++ch) {
+    float v = hit ? adv[ch] * msk : 0.f;                       // load_data.py:791-792
+    // the backward's factor: d_out * msk where the gradient passes (clamp in
+    // range, and in mode 1 the patch value not replaced by the frame), else
+    // the sentinel -1 for an exact +0 (warp_box_bwd_a_k's rule)
+    if (hit && rng[ch] && !(mode == 1 && v == 0.f)) f4[ch] = msk;
+    if (mode == 1) v = (v == 0.f) ? img[o + ch * plane] : v;   // load_data.py:820
+    out[o + ch * plane] = v;
+  }
+  if (fac)
+    *reinterpret_cast<float4*>(fac + ((size_t)b * plane + (size_t)i * g.S + j) * 4) =
+        make_float4(f4[0], f4[1], f4[2], f4[3]);
+}
+
 __global__ __launch_bounds__(256) void warp_box_fwd_k(const float* __restrict__ img, const float* __restrict__ mp,
                                                       const float* __restrict__ contrast,
                                                       const float* __restrict__ bright,
@@ -1025,31 +1224,30 @@ __global__ __launch_bounds__(256) void warp_box_fwd_k(const float* __restrict__ 
   const int b = blockIdx.y;
   const QBox bx = quad_box(roi, b, g.S);
   const int bw = bx.qx1 - bx.qx0, area = bw * (bx.y1 - bx.y0);
-  const size_t plane = (size_t)g.S * g.S;
   const NoiseSrc nz = noise_src(nullptr, g, b);
   // pre-augmented values (g.pre) or mp + the draws + the keyed noise at each corner
   const float cb = g.pre ? 1.f : contrast[b], bb = g.pre ? 0.f : bright[b];
+  const po::Geo G = po::load_geo(affine + 6 * b, g.S);
   for (int p = blockIdx.x * 256 + threadIdx.x; p < area; p += gridDim.x * 256) {
     const int r = p / bw;
-    const int i = bx.y0 + r, j = bx.qx0 + (p - r * bw);
-    const size_t o = (size_t)b * 3 * plane + (size_t)i * g.S + j;
-    float adv[3], msk;
-    bool rng[3];
-    const bool hit = warp_pixel(affine + 6 * b, g, mp, nz, cb, bb, i, j, adv, msk, rng);
-    float f4[4] = {-1.f, -1.f, -1.f, -1.f};
-#pragma unroll
-    for (int ch = 0; ch < 3; ++ch) {
-      float v = hit ? adv[ch] * msk : 0.f;                       // load_data.py:791-792
-      // the backward's factor: d_out * msk where the gradient passes (clamp in
-      // range, and in mode 1 the patch value not replaced by the frame), else
-      // the sentinel -1 for an exact +0 (warp_box_bwd_a_k's rule)
-      if (hit && rng[ch] && !(mode == 1 && v == 0.f)) f4[ch] = msk;
-      if (mode == 1) v = (v == 0.f) ? img[o + ch * plane] : v;   // load_data.py:820
-      out[o + ch * plane] = v;
-    }
-    if (fac)
-      *reinterpret_cast<float4*>(fac + ((size_t)b * plane + (size_t)i * g.S + j) * 4) =
-          make_float4(f4[0], f4[1], f4[2], f4[3]);
+    box_fwd_pixel(img, mp, G, nz, cb, bb, g, mode, b, bx.y0 + r, bx.qx0 + (p - r * bw), out, fac);
+  }
+}
+
+__global__ __launch_bounds__(256) void warp_box_flat_fwd_k(const float* __restrict__ img, const float* __restrict__ mp,
+                                                           const float* __restrict__ contrast,
+                                                           const float* __restrict__ bright,
+                                                           const double* __restrict__ affine,
+                                                           const int32_t* __restrict__ roi, int B, WarpGeom g,
+                                                           int mode, float* __restrict__ out, float* __restrict__ fac) {
+  __shared__ FlatBoxes t;
+  const int total = flat_boxes(roi, B, g.S, t);
+  for (int q = blockIdx.x * 256 + threadIdx.x; q < total; q += gridDim.x * 256) {
+    int b, i, j;
+    flat_pixel(t, B, q, b, i, j);
+    const po::Geo G = po::load_geo(affine + 6 * b, g.S);
+    const float cb = g.pre ? 1.f : contrast[b], bb = g.pre ? 0.f : bright[b];
+    box_fwd_pixel(img, mp, G, noise_src(nullptr, g, b), cb, bb, g, mode, b, i, j, out, fac);
   }
 }
 
@@ -1069,13 +1267,14 @@ __global__ __launch_bounds__(256) void warp_box_bwd_a_k(const float* __restrict_
   const size_t plane = (size_t)g.S * g.S;
   const NoiseSrc nz = noise_src(nullptr, g, b);
   const float cb = contrast[b], bb = g.pre ? 0.f : bright[b];
+  const po::Geo G = po::load_geo(affine + 6 * b, g.S);
   for (int p = blockIdx.x * 256 + threadIdx.x; p < area; p += gridDim.x * 256) {
     const int r = p / bw;
     const int i = bx.y0 + r, j = bx.qx0 + (p - r * bw);
     const size_t o = (size_t)b * 3 * plane + (size_t)i * g.S + j;
     float adv[3], msk;
     bool rng[3];
-    if (!warp_pixel(affine + 6 * b, g, mp, nz, cb, bb, i, j, adv, msk, rng)) continue;
+    if (!warp_pixel(G, g, mp, nz, cb, bb, i, j, adv, msk, rng)) continue;
     float gv4[4] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int ch = 0; ch < 3; ++ch) {
@@ -1095,30 +1294,56 @@ __global__ __launch_bounds__(256) void warp_box_bwd_a_k(const float* __restrict_
 // recomputation -- a 16-byte factor load, the three d_out loads and the gfac
 // store in place of the factors.  The same products as warp_box_bwd_a_k
 // (d_out * msk where the gradient passes, +0 elsewhere), so the same bits.
+__device__ __forceinline__ void box_fac_pixel(const float* __restrict__ d_out, int S, int b, int i, int j,
+                                              float* __restrict__ fac) {
+  const size_t plane = (size_t)S * S;
+  const size_t o = (size_t)b * 3 * plane + (size_t)i * S + j;
+  float4* fp = reinterpret_cast<float4*>(fac + ((size_t)b * plane + (size_t)i * S + j) * 4);
+  const float4 f = *fp;
+  const float fv[3] = {f.x, f.y, f.z};
+  float gv[3];
+#pragma unroll
+  for (int ch = 0; ch < 3; ++ch) gv[ch] = fv[ch] < 0.f ? 0.f : d_out[o + ch * plane] * fv[ch];
+  *fp = make_float4(gv[0], gv[1], gv[2], 0.f);
+}
+
 __global__ __launch_bounds__(256) void warp_box_bwd_fac_k(const float* __restrict__ d_out,
                                                           const int32_t* __restrict__ roi, int S,
                                                           float* __restrict__ fac) {
   const int b = blockIdx.y;
   const QBox bx = quad_box(roi, b, S);
   const int bw = bx.qx1 - bx.qx0, area = bw * (bx.y1 - bx.y0);
-  const size_t plane = (size_t)S * S;
   for (int p = blockIdx.x * 256 + threadIdx.x; p < area; p += gridDim.x * 256) {
     const int r = p / bw;
-    const int i = bx.y0 + r, j = bx.qx0 + (p - r * bw);
-    const size_t o = (size_t)b * 3 * plane + (size_t)i * S + j;
-    float4* fp = reinterpret_cast<float4*>(fac + ((size_t)b * plane + (size_t)i * S + j) * 4);
-    const float4 f = *fp;
-    const float fv[3] = {f.x, f.y, f.z};
-    float gv[3];
-#pragma unroll
-    for (int ch = 0; ch < 3; ++ch) gv[ch] = fv[ch] < 0.f ? 0.f : d_out[o + ch * plane] * fv[ch];
-    *fp = make_float4(gv[0], gv[1], gv[2], 0.f);
+    box_fac_pixel(d_out, S, b, bx.y0 + r, bx.qx0 + (p - r * bw), fac);
+  }
+}
+
+__global__ __launch_bounds__(256) void warp_box_flat_fac_k(const float* __restrict__ d_out,
+                                                           const int32_t* __restrict__ roi, int B, int S,
+                                                           float* __restrict__ fac) {
+  __shared__ FlatBoxes t;
+  const int total = flat_boxes(roi, B, S, t);
+  for (int q = blockIdx.x * 256 + threadIdx.x; q < total; q += gridDim.x * 256) {
+    int b, i, j;
+    flat_pixel(t, B, q, b, i, j);
+    box_fac_pixel(d_out, S, b, i, j, fac);
   }
 }
 
 // workgroups per image of the box kernels: enough for a box of an eighth of the
 // frame in one pass (a larger box loops)
 __host__ inline int box_blocks(int S) { return po::ceil_div(po::ceil_div((int64_t)S * S, 8), 256); }
+// the flat-list forms (ADVPATCH_WARP_FLAT=0: the per-image grid): batches of
+// at most FLAT_MAXB images, a fixed grid of at most 1024 workgroups
+__host__ inline int flat_blocks(int B, int S) {
+  static const bool on = [] {
+    const char* e = getenv("ADVPATCH_WARP_FLAT");
+    return !(e && e[0] == '0');
+  }();
+  if (!on || B > FLAT_MAXB) return 0;
+  return (int)std::min<int64_t>(1024, (int64_t)box_blocks(S) * B);
+}
 }  // namespace
 
 extern "C" int po_augment_patch(const float* patch_mp, uint64_t seed, uint64_t counter, int b0, const float* contrast,
@@ -1145,8 +1370,12 @@ extern "C" int po_warp_fwd_pre(const float* img, const float* pre, const double*
   hipStream_t st = po::stream_of(s);
   hipLaunchKernelGGL(warp_quad_copy_k, dim3(po::ceil_div(S * (S / 4), 256), B), dim3(256), 0, st, img, roi, S, mode,
                      out);
-  hipLaunchKernelGGL(warp_box_fwd_k, dim3(box_blocks(S), B), dim3(256), 0, st, img, nullptr, nullptr, nullptr, affine,
-                     roi, g, mode, out, nullptr);
+  if (const int nf = flat_blocks(B, S))
+    hipLaunchKernelGGL(warp_box_flat_fwd_k, dim3(nf), dim3(256), 0, st, img, nullptr, nullptr, nullptr, affine, roi, B,
+                       g, mode, out, nullptr);
+  else
+    hipLaunchKernelGGL(warp_box_fwd_k, dim3(box_blocks(S), B), dim3(256), 0, st, img, nullptr, nullptr, nullptr,
+                       affine, roi, g, mode, out, nullptr);
   return po::check_launch("po_warp_fwd_pre");
 }
 
@@ -1164,8 +1393,12 @@ static int box_fwd_keyed(const float* img, const float* patch_mp, uint64_t seed,
   if (fill)
     hipLaunchKernelGGL(warp_quad_copy_k, dim3(po::ceil_div(S * (S / 4), 256), B), dim3(256), 0, st, img, roi, S, mode,
                        out);
-  hipLaunchKernelGGL(warp_box_fwd_k, dim3(box_blocks(S), B), dim3(256), 0, st, img, patch_mp, contrast, bright, affine,
-                     roi, g, mode, out, fac);
+  if (const int nf = flat_blocks(B, S))
+    hipLaunchKernelGGL(warp_box_flat_fwd_k, dim3(nf), dim3(256), 0, st, img, patch_mp, contrast, bright, affine, roi,
+                       B, g, mode, out, fac);
+  else
+    hipLaunchKernelGGL(warp_box_fwd_k, dim3(box_blocks(S), B), dim3(256), 0, st, img, patch_mp, contrast, bright,
+                       affine, roi, g, mode, out, fac);
   return po::check_launch("po_warp_box_fwd_keyed");
 }
 
@@ -1239,7 +1472,10 @@ extern "C" int po_warp_box_bwd_fac(const float* d_out, const float* patch_mp, ui
   PO_REQUIRE((uintptr_t)fac % 16 == 0, "po_warp_box_bwd_fac: fac must be 16-byte aligned");
   const WarpGeom g = make_geom(S, P, seed, counter, b0);
   hipStream_t st = po::stream_of(s);
-  hipLaunchKernelGGL(warp_box_bwd_fac_k, dim3(box_blocks(S), B), dim3(256), 0, st, d_out, roi, S, fac);
+  if (const int nf = flat_blocks(B, S))
+    hipLaunchKernelGGL(warp_box_flat_fac_k, dim3(nf), dim3(256), 0, st, d_out, roi, B, S, fac);
+  else
+    hipLaunchKernelGGL(warp_box_bwd_fac_k, dim3(box_blocks(S), B), dim3(256), 0, st, d_out, roi, S, fac);
   int rc = po::check_launch("po_warp_box_bwd_fac(a)");
   if (rc) return rc;
   launch_bwd_b(fac, patch_mp, nullptr, contrast, bright, affine, g, B, P, d_patch_mp, st, true);

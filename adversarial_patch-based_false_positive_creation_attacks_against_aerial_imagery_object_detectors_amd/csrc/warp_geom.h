@@ -63,6 +63,96 @@ __device__ __forceinline__ void footprint_roi(const double af[6], int S, int P, 
   roi[3] = min(S, (int)ceil(ihi) + 3);
 }
 
+// ---------------------------------------------------------------------------
+// Reference geometry (po_patch_params geometry 1; ABI 27): the placement as
+// the reference computes it on PyTorch-CPU in fp32 (load_data.py:726-749),
+// every rounding restated from ATen / MKL and pinned bit for bit against the
+// installed torch by tests/test_geometry_ref.py (oracle/geometry_ref.py):
+//   theta        cos/scale, sin/scale, tx*cos/scale + ty*sin/scale, ...   738-743
+//   affine_grid  base b(k) = fl(fl(linspace_k * (S-1)) / S), linspace_k =
+//                fma(step, k, -1) (k < S/2) or fma(-step, S-1-k, 1), step =
+//                fl(2/(S-1)); x = fl(fma(by, t1, fl(bx*t0)) + t2)        745
+//   grid_sample  ix = fma(x + 1, S/2, -0.5); bilinear weights s*e, s*w, n*e,
+//                n*w; value = fma chain over the corners nw, ne, sw, se   748-749
+// An affine row [6] float64 in this form holds the six fp32 theta values as
+// float[6] in its first 24 bytes and AFFINE_REF_TAG in row[3] -- a signalling
+// NaN bit pattern, which no arithmetic produces, so a float64-form row (the
+// pixel-space map of theta_pixel_affine) never carries it.
+// ---------------------------------------------------------------------------
+constexpr unsigned long long AFFINE_REF_TAG = 0x7FF4A0F3E5F32000ull;
+
+// Per-image placement of the warp kernels: the form, the fp32 theta (reference
+// form) and a float64 pixel-space map (the map itself in the float64 form; in
+// the reference form its float64 evaluation, used only for footprint boxes and
+// candidate searches, whose margins cover the fp32 rounding).
+struct Geo {
+  double af[6];
+  float th[6];
+  int ref;
+};
+
+__device__ __forceinline__ bool affine_row_is_ref(const double* row) {
+  return (unsigned long long)__double_as_longlong(row[3]) == AFFINE_REF_TAG;
+}
+
+__device__ __forceinline__ Geo load_geo(const double* row, int S) {
+  Geo G;
+  G.ref = affine_row_is_ref(row) ? 1 : 0;
+  if (G.ref) {
+    const float* t = reinterpret_cast<const float*>(row);
+    double th[6];
+#pragma unroll
+    for (int k = 0; k < 6; ++k) {
+      G.th[k] = t[k];
+      th[k] = (double)t[k];
+    }
+    theta_pixel_affine(th, (double)S, G.af);
+  } else {
+#pragma unroll
+    for (int k = 0; k < 6; ++k) {
+      G.af[k] = row[k];
+      G.th[k] = 0.f;
+    }
+  }
+  return G;
+}
+
+__device__ __forceinline__ void store_ref_row(const float th[6], double* row) {
+  float* t = reinterpret_cast<float*>(row);
+#pragma unroll
+  for (int k = 0; k < 6; ++k) t[k] = th[k];
+  row[3] = __longlong_as_double((long long)AFFINE_REF_TAG);
+  row[4] = 0.0;
+  row[5] = 0.0;
+}
+
+// affine_grid's base coordinate k of an S-point axis (align_corners=False)
+__device__ __forceinline__ float ref_base(int k, int S) {
+  const float step = __fdiv_rn(2.0f, (float)(S - 1));
+  const float lin = k < (S >> 1) ? __fmaf_rn(step, (float)k, -1.0f) : __fmaf_rn(-step, (float)(S - 1 - k), 1.0f);
+  return __fdiv_rn(__fmul_rn(lin, (float)(S - 1)), (float)S);
+}
+
+// grid_sample's source coordinate (column ix, row iy) of output pixel (i, j)
+__device__ __forceinline__ void ref_sample_coord(const float th[6], int S, int i, int j, float& ix, float& iy) {
+  const float bx = ref_base(j, S), by = ref_base(i, S);
+  const float gx = __fadd_rn(__fmaf_rn(by, th[1], __fmul_rn(bx, th[0])), th[2]);
+  const float gy = __fadd_rn(__fmaf_rn(by, th[4], __fmul_rn(bx, th[3])), th[5]);
+  const float half = (float)S * 0.5f;
+  ix = __fmaf_rn(__fadd_rn(gx, 1.0f), half, -0.5f);
+  iy = __fmaf_rn(__fadd_rn(gy, 1.0f), half, -0.5f);
+}
+
+// the reference theta from its fp32 inputs (load_data.py:738-743)
+__device__ __forceinline__ void ref_theta(float sn, float cs, float sc, float tx, float ty, float th[6]) {
+  th[0] = __fdiv_rn(cs, sc);
+  th[1] = __fdiv_rn(sn, sc);
+  th[2] = __fadd_rn(__fdiv_rn(__fmul_rn(tx, cs), sc), __fdiv_rn(__fmul_rn(ty, sn), sc));
+  th[3] = __fdiv_rn(-sn, sc);
+  th[4] = __fdiv_rn(cs, sc);
+  th[5] = __fadd_rn(__fdiv_rn(__fmul_rn(-tx, sn), sc), __fdiv_rn(__fmul_rn(ty, cs), sc));
+}
+
 // The composite's written box of image b (po_warp_fwd_pre, po_warp_box_fwd_keyed):
 // the footprint box widened to whole 4-pixel quads, [qx0, qx1) x [y0, y1) (all
 // zero when empty).  Outside it the composite equals the image (mode 1), so a

@@ -1371,7 +1371,7 @@ class NetPlan:
         if not time_missing:
             for args, desc in convs:
                 key = self._tune_key(args, desc)
-                if key in cache:
+                if key in cache and self._cached_ok(desc, cache[key]):
                     self._set_tile(desc, cache[key])
             for args, desc in convs:                 # the workspaces may have grown
                 if desc.ksplit > 1:
@@ -1380,7 +1380,8 @@ class NetPlan:
                     desc.winov = self.winov.data_ptr()
             self.bind_side_workspace()
             return
-        if all(self._tune_key(args, desc) in cache for args, desc in convs):
+        if all(self._tune_key(args, desc) in cache and self._cached_ok(desc, cache[self._tune_key(args, desc)])
+               for args, desc in convs):
             for args, desc in convs:                 # every shape already tuned: no launches
                 self._set_tile(desc, cache[self._tune_key(args, desc)])
             for args, desc in convs:
@@ -1413,7 +1414,7 @@ class NetPlan:
             if name != "po_conv":
                 continue
             key = self._tune_key(args, desc)
-            if key in cache:
+            if key in cache and self._cached_ok(desc, cache[key]):
                 self._set_tile(desc, cache[key])
                 continue
             M = desc.B * (desc.mrows or desc.Hg * desc.Wg)
@@ -1486,6 +1487,18 @@ class NetPlan:
                 t.zero_()
         self.amax.zero_()
         torch.cuda.synchronize()
+
+    def _cached_ok(self, desc, choice):
+        """Whether a cached (tile, ksplit) can run this launch as built: a
+        Winograd tile needs its transformed weights, which ADVPATCH_WINOGRAD=0
+        / ADVPATCH_WINO4X4=0 leave unbuilt (po_conv would refuse the launch).
+        A choice that cannot run is treated as missing from the cache."""
+        t = choice if isinstance(choice, int) else choice[0]
+        if t in (71, self.WINOV_TILE):
+            return getattr(desc, "Wwino6", None) is not None
+        if t in self.WINO_TILES:
+            return getattr(desc, "Wwino", None) is not None
+        return True
 
     @staticmethod
     def _tune_key(args, desc):

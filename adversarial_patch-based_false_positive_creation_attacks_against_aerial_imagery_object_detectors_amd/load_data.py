@@ -194,11 +194,52 @@ class HasSusRGB(nn.Module):
 # ---------------------------------------------------------------------------
 # Patch placement and warp
 # ---------------------------------------------------------------------------
-def patch_params(lab_batch, img_size, P, draws, do_rotate=True, with_roi=False):
+GEOMETRIES = {"ref": 1, "f64": 0}
+
+
+def default_geometry():
+    """The placement geometry of the training path: "ref" (default) -- the
+    reference's fp32 theta / affine_grid / grid_sample arithmetic, op by op
+    (po_patch_params geometry 1); "f64" (ADVPATCH_GEOMETRY=f64) -- the same
+    formulas evaluated in float64 (closer to the exact value, not to the
+    reference)."""
+    g = os.environ.get("ADVPATCH_GEOMETRY", "ref")
+    if g not in GEOMETRIES:
+        raise ValueError("ADVPATCH_GEOMETRY must be one of %s" % (tuple(GEOMETRIES),))
+    return g
+
+
+_SINCOS_LUT = {}
+
+
+def sincos_lattice_table(device):
+    """[2^24, 2] fp32 on ``device``: (sin, cos) of every angle po_draws can
+    draw, angle_k = fp32(k * 2^-24 * fp32(2 pi) - pi) (csrc/draw_ops.hip),
+    as the reference's torch.sin / torch.cos compute them on PyTorch-CPU
+    (load_data.py:731-732).  Those run MKL VML, which is not correctly
+    rounded (~5 % of values one ulp off), so no device formula reproduces
+    them; po_patch_params looks each drawn angle up here.  Built once per
+    process and device (the CPU's own values, 128 MiB of HBM)."""
+    dev = torch.device(device)
+    key = (dev.type, dev.index)
+    lut = _SINCOS_LUT.get(key)
+    if lut is None:
+        pi = np.float32(math.pi)
+        k = np.arange(1 << 24, dtype=np.int64)
+        u = (k.astype(np.float32) * np.float32(2.0 ** -24)).astype(np.float64)
+        ang = torch.from_numpy((u * np.float64(np.float32(2.0) * pi) + np.float64(-pi)).astype(np.float32))
+        lut = torch.stack([torch.sin(ang), torch.cos(ang)], 1).contiguous().to(dev)
+        _SINCOS_LUT[key] = lut
+    return lut
+
+
+def patch_params(lab_batch, img_size, P, draws, do_rotate=True, with_roi=False, geometry=None):
     """(theta [B,6], patch_center [B,2], target_size [B][, roi [B,4] int32,
-    affine [B,6] float64]) on the device.  ``affine`` is the pixel-space
-    sampling map the warp kernels use (po_patch_params)."""
+    affine [B,6] float64]) on the device.  ``affine`` holds the per-image
+    placement rows the warp kernels read (po_patch_params); ``geometry``:
+    "ref" / "f64" (default_geometry())."""
     nat.ensure_device(lab_batch)
+    geometry = default_geometry() if geometry is None else geometry
     lab = lab_batch.contiguous().float()
     B, L = lab.size(0), lab.size(1)
     dev = lab.device
@@ -208,10 +249,11 @@ def patch_params(lab_batch, img_size, P, draws, do_rotate=True, with_roi=False):
     roi = torch.empty(B, 4, dtype=torch.int32, device=dev) if with_roi else None
     affine = torch.empty(B, 6, dtype=torch.float64, device=dev) if with_roi else None
     angle = draws["angle"].contiguous().float() if do_rotate else None
+    lut = sincos_lattice_table(dev) if (geometry == "ref" and do_rotate) else None
     nat.call("po_patch_params", nat.ptr(lab), B, L, nat.ptr(angle), nat.ptr(draws["ux"].contiguous().float()),
              nat.ptr(draws["uy"].contiguous().float()), int(bool(do_rotate)), int(img_size), int(P),
-             nat.ptr(theta), nat.ptr(center), nat.ptr(tsize), nat.ptr(roi, torch.int32),
-             nat.ptr(affine, torch.float64), nat.stream())
+             GEOMETRIES[geometry], nat.ptr(lut), nat.ptr(theta), nat.ptr(center), nat.ptr(tsize),
+             nat.ptr(roi, torch.int32), nat.ptr(affine, torch.float64), nat.stream())
     if with_roi:
         return theta, center, tsize, roi, affine
     return theta, center, tsize
@@ -224,7 +266,8 @@ class _Warp(torch.autograd.Function):
     """Augment + warp + clamp*mask (mode 0) or + composite onto img (mode 1)."""
 
     @staticmethod
-    def forward(ctx, mp, noise, contrast, bright, affine, img, S, mode, form="box", roi=None, sparse=False):
+    def forward(ctx, mp, noise, contrast, bright, affine, img, S, mode, form="box", roi=None, sparse=False,
+                grad=True):
         """``noise``: the [B,3,P,P] tensor, or a po_draws key (seed, counter,
         b0) -- the noise is then regenerated from the key and no noise tensor
         exists.  With a key and the footprint boxes ``roi``, ``form`` picks the
@@ -235,7 +278,11 @@ class _Warp(torch.autograd.Function):
         runs the per-pixel kernels over whole frames (po_warp_*_keyed).  All
         forms give the same bits.  ``sparse`` (form "box", mode 1): only the
         quad-widened boxes of ``out`` are written -- the rest of the composite
-        is ``img``, and the consumer reads the two (po_conv_first_*_cmp)."""
+        is ``img``, and the consumer reads the two (po_conv_first_*_cmp).
+        ``grad``: whether a backward can follow -- the caller's
+        torch.is_grad_enabled() and mp.requires_grad (grad mode is always off
+        inside forward, and needs_input_grad ignores no_grad / inference
+        mode), so no-grad and eval forwards skip the factor buffer."""
         mp = mp.contiguous()
         B = affine.size(0)
         P = mp.size(-1)
@@ -252,8 +299,10 @@ class _Warp(torch.autograd.Function):
             # into the gradient factors in place (po_warp_box_*_fac; "0": re-evaluate
             # the warp in the backward, po_warp_box_bwd_keyed -- the same bits)
             ctx.fac = None
-            # only when a backward can follow (no factor buffer for no-grad / eval forwards)
-            if ctx.needs_input_grad[0] and os.environ.get("ADVPATCH_WARP_FAC", "1") != "0":
+            # only when a backward can follow (no factor buffer for no-grad / eval forwards).
+            # The buffer (B*S*S*16 bytes: 0.7 GB at tiny B=256 @416, 24 MB at yolov3 B=16 @608)
+            # lives from the warp forward through the detector's forward and backward.
+            if grad and os.environ.get("ADVPATCH_WARP_FAC", "1") != "0":
                 ctx.fac = torch.empty(B * S * S * 4, device=mp.device)
                 nat.call("po_warp_box_fwd_fac", *head, nat.ptr(ctx.fac), nat.stream())
             else:
@@ -299,7 +348,7 @@ class _Warp(torch.autograd.Function):
             nat.call("po_warp_box_bwd_fac", nat.ptr(d_out), nat.ptr(mp), *key, nat.ptr(contrast), nat.ptr(bright),
                      nat.ptr(affine, torch.float64), nat.ptr(roi, torch.int32), B, ctx.S, P, nat.ptr(fac),
                      nat.ptr(d_mp), nat.stream())
-            return d_mp, None, None, None, None, None, None, None, None, None, None
+            return d_mp, None, None, None, None, None, None, None, None, None, None, None
         # the footprint-box forms keep their per-pixel factors interleaved [B,S,S,4]
         work = (torch.empty(B * ctx.S * ctx.S * 4, device=d_out.device) if ctx.form in ("box", "pre")
                 else torch.empty_like(d_out))
@@ -321,7 +370,7 @@ class _Warp(torch.autograd.Function):
             nat.call("po_warp_bwd", nat.ptr(d_out), nat.ptr(mp), nat.ptr(noise), nat.ptr(contrast),
                      nat.ptr(bright), nat.ptr(affine, torch.float64), B, ctx.S, P, ctx.mode,
                      nat.ptr(work), nat.ptr(d_mp), nat.stream())
-        return d_mp, None, None, None, None, None, None, None, None, None, None
+        return d_mp, None, None, None, None, None, None, None, None, None, None, None
 
 
 class PatchTransformer(nn.Module):
@@ -352,6 +401,8 @@ class PatchTransformer(nn.Module):
         if self.warp_form not in WARP_FORMS:
             raise ValueError("ADVPATCH_WARP must be one of %s" % (WARP_FORMS,))
         self.last_roi = None     # [B,4] int32 footprint boxes of the last placement
+        # placement arithmetic: "ref" (the reference's fp32 ops) or "f64" (ADVPATCH_GEOMETRY)
+        self.geometry = default_geometry()
 
     def lab_transform(self, lab_batch_origin):
         """[B,L,5] -> [B,1,5] (load_data.py:453-478): (max-area row + min-area row)/2,
@@ -391,7 +442,8 @@ class PatchTransformer(nn.Module):
         B, P = lab_batch.size(0), mp.size(-1)
         if draws is None:
             draws = self.make_draws(B, P, adv_patch.device)
-        theta, center, _, roi, affine = patch_params(lab_batch, img_size, P, draws, do_rotate, with_roi=True)
+        theta, center, _, roi, affine = patch_params(lab_batch, img_size, P, draws, do_rotate, with_roi=True,
+                                                     geometry=self.geometry)
         self.last_roi = roi
         return mp, draws, affine, center
 
@@ -399,7 +451,8 @@ class PatchTransformer(nn.Module):
         """-> (adv_batch_t [B,1,3,S,S], patch_center [B,2] = (x*S, y*S))."""
         mp, d, affine, center = self._prep(adv_patch, lab_batch, img_size, do_rotate, draws)
         out = _Warp.apply(mp, self._noise(d), d["contrast"].contiguous(),
-                          d["bright"].contiguous(), affine, None, int(img_size), 0, self.warp_form, self.last_roi)
+                          d["bright"].contiguous(), affine, None, int(img_size), 0, self.warp_form, self.last_roi,
+                          False, torch.is_grad_enabled() and mp.requires_grad)
         return out.unsqueeze(1), center
 
     def forward_composite(self, adv_patch, lab_batch, img_batch, img_size, do_rotate=True, draws=None,
@@ -415,7 +468,7 @@ class PatchTransformer(nn.Module):
         mp, d, affine, center = self._prep(adv_patch, lab_batch, img_size, do_rotate, draws, mp)
         out = _Warp.apply(mp, self._noise(d), d["contrast"].contiguous(),
                           d["bright"].contiguous(), affine, img_batch.contiguous(), int(img_size), 1, self.warp_form,
-                          self.last_roi, sparse)
+                          self.last_roi, sparse, torch.is_grad_enabled() and mp.requires_grad)
         return out, center
 
     def sparse_ok(self, img_size, draws=None):

@@ -9,6 +9,7 @@ benches and parity tests run on synthetic data of the DOTA loader's shapes:
   i.e. one row of ones(5) (load_data.py:918-923)                      seed 1
 * patch   [3,P,P]   U[0,1) (train_patch.py:404-406)                    seed 2
 * draws   the PatchTransformer random draws (load_data.py:548-707)      seed 3
+          (angles on po_draws' lattice, as the trainer draws them)
 
 All generators use numpy's PCG64 so the oracle and the HIP path see the
 same bytes.  ``draws_device`` is the on-device generator the training loop
@@ -59,10 +60,19 @@ def draws(B, P, seed=3):
         "contrast": torch.from_numpy(g.uniform(0.8, 1.2, B).astype(f32)),
         "bright": torch.from_numpy(g.uniform(-0.1, 0.1, B).astype(f32)),
         "noise": torch.from_numpy(g.uniform(-1.0, 1.0, (B, 3, P, P)).astype(f32)),
-        "angle": torch.from_numpy(g.uniform(-math.pi, math.pi, B).astype(f32)),
+        "angle": torch.from_numpy(lattice_angle(np.floor(g.random(B) * 2.0 ** 24))),
         "ux": torch.from_numpy(g.random(B, dtype=f32)),
         "uy": torch.from_numpy(g.random(B, dtype=f32)),
     }
+
+
+def lattice_angle(k):
+    """U(-pi, pi) on po_draws' lattice (csrc/draw_ops.hip): fp32(k 2^-24 *
+    fp32(2 pi) - pi) for integer k in [0, 2^24) -- the only angles the
+    trainer draws (load_data.sincos_lattice_table tabulates their sin/cos)."""
+    pi = np.float32(math.pi)
+    u = (np.asarray(k, dtype=np.float64).astype(np.float32) * np.float32(2.0 ** -24)).astype(np.float64)
+    return (u * np.float64(np.float32(2.0) * pi) + np.float64(-pi)).astype(np.float32)
 
 
 DRAW_KEYS = ("contrast", "bright", "noise", "angle", "ux", "uy")

@@ -33,7 +33,7 @@ typedef void* po_stream_t;
 #define PO_EHIP -2     /* HIP runtime error */
 #define PO_EDEVICE -3  /* device is not gfx950 */
 
-#define PO_ABI_VERSION 26
+#define PO_ABI_VERSION 27
 #define PO_AMAX_SUB 64  /* sub-slots per max|x| slot (see po_conv_desc) */
 
 int po_abi_version(void);
@@ -67,14 +67,27 @@ int po_median_bwd(const float* dy, const int32_t* argidx, int C, int H, int W, i
  * derived from it); target_size out [B] (may be NULL); roi out [B,4] int32
  * (may be NULL) = {x0,y0,x1,y1} bounding box (+2 px margin, clipped to the
  * image) of the output pixels the warped patch can touch; affine out [B,6]
- * float64 (may be NULL) = the pixel-space sampling map of affine_grid +
- * grid_sample (align_corners=False): output pixel (i,j) samples the padded
- * patch at column ix = a0*j + a1*i + a2, row iy = a3*j + a4*i + a5.  theta,
- * target_size, roi and affine are evaluated in float64 from the fp32 inputs
- * (theta rounded to fp32 on output); po_warp_* take `affine`. */
+ * float64 rows (may be NULL) for po_warp_*.
+ * geometry 1 (ABI 27; the trainer's default): the reference's fp32
+ * arithmetic -- theta (load_data.py:738-743), affine_grid (745) and
+ * grid_sample (748-749) as PyTorch-CPU computes them, op by op (pinned by
+ * tests/test_geometry_ref.py); theta and target_size are those fp32 values,
+ * and each affine row holds the fp32 theta as float[6] in its first 24 bytes
+ * with a tag in row[3] (warp_geom.h), so the warp kernels sample exactly
+ * where the reference samples.  sin/cos of angles on po_draws' lattice come
+ * from sincos_lut [2^24][2] fp32 (8-byte aligned; may be NULL): PyTorch-CPU's
+ * own torch.sin/torch.cos of the lattice angle k at [k] (MKL VML is not
+ * correctly rounded, so the values are tabulated, not restated); other angles
+ * get correctly rounded values.
+ * geometry 0: the same formulas in float64 from the same fp32 inputs; each
+ * affine row is the pixel-space sampling map of affine_grid + grid_sample
+ * (align_corners=False): output pixel (i,j) samples the padded patch at
+ * column ix = a0*j + a1*i + a2, row iy = a3*j + a4*i + a5 (theta rounded to
+ * fp32 on output). */
 int po_patch_params(const float* lab, int B, int L, const float* angle, const float* ux,
-                    const float* uy, int do_rotate, int S, int P, float* theta, float* center,
-                    float* target_size, int32_t* roi, double* affine, po_stream_t s);
+                    const float* uy, int do_rotate, int S, int P, int geometry, const float* sincos_lut,
+                    float* theta, float* center, float* target_size, int32_t* roi, double* affine,
+                    po_stream_t s);
 
 /* Random draws of the patch transformer for images b0 .. b0+B-1 of a global
  * batch (load_data.py:548-574 contrast U(0.8,1.2), brightness U(-0.1,0.1),

@@ -126,13 +126,15 @@ def patch_transformer(adv_patch, lab_batch, img_size, draws, do_rotate=True, geo
     (column, row) in pixels = (target_x*S, target_y*S) (load_data.py:712-715).
 
     ``geometry`` (tests only): "fp32" is the reference (theta, affine_grid and
-    grid_sample in fp32).  "f64" evaluates theta, the grid and the bilinear
-    sampling in float64 from the same fp32 inputs and rounds each sampled
-    value to fp32 once — the HIP path's deliberate deviation:
-    the fp32 affine_grid leaves ~1e-4 px in the sampling coordinates (its
-    translation terms cancel), i.e. up to ~1.5e-4 relative in the patch
-    gradient, so an fp32 comparison of two implementations at 1e-4 needs the
-    geometry taken out of the rounding noise."""
+    grid_sample in the inputs' dtype: fp32 for the reference itself).  "f64"
+    evaluates theta, the grid and the bilinear sampling in float64 from the
+    same fp32 inputs and rounds each sampled value to fp32 once (the HIP
+    path's opt-in float64 geometry, ADVPATCH_GEOMETRY=f64).  "fp32in64" (for
+    float64 runs, train_step_f64): theta and the affine grid exactly as the
+    fp32 reference computes them (from the fp32 labels and draws), the
+    sampling and everything after it in the batch's dtype -- the accuracy
+    yardstick of an implementation that reproduces the reference's fp32
+    sample points (the HIP default, po_patch_params geometry 1)."""
     adv = median_pool7(adv_patch.unsqueeze(0))                    # 531-532
     P = adv.size(-1)
     pad = (img_size - P) / 2                                     # 534
@@ -182,7 +184,13 @@ def patch_transformer(adv_patch, lab_batch, img_size, draws, do_rotate=True, geo
     theta[:, 1, 0] = -sin / scale
     theta[:, 1, 1] = cos / scale
     theta[:, 1, 2] = -tx * sin / scale + ty * cos / scale
-    grid = F.affine_grid(theta, adv_batch.shape, align_corners=False)      # 745
+    if geometry == "fp32in64":
+        # the reference's own fp32 theta and grid (same ops, fp32 inputs)
+        th32, _, _ = patch_theta(lab_batch.float(), img_size, P, {k: v.float() for k, v in draws.items()},
+                                 do_rotate)
+        grid = F.affine_grid(th32, adv_batch.shape, align_corners=False).to(adv_batch.dtype)
+    else:
+        grid = F.affine_grid(theta, adv_batch.shape, align_corners=False)  # 745
     adv_t = F.grid_sample(adv_batch, grid, align_corners=False)            # 748
     msk_t = F.grid_sample(msk_batch, grid, align_corners=False)            # 749
     adv_t = adv_t.view(s[0], s[1], s[2], s[3], s[4])
@@ -197,7 +205,7 @@ def patch_transformer(adv_patch, lab_batch, img_size, draws, do_rotate=True, geo
 def patch_theta(lab_batch, img_size, P, draws, do_rotate=True):
     """The per-image affine parameters of patch_transformer (for tests)."""
     B = lab_batch.size(0)
-    angle = draws["angle"].clone() if do_rotate else torch.zeros(B)
+    angle = draws["angle"].clone() if do_rotate else torch.zeros(B, dtype=lab_batch.dtype)
     sel = lab_transform(lab_batch)
     ls2 = sel[:, :, 2] * img_size
     ls3 = sel[:, :, 3] * img_size
@@ -208,7 +216,7 @@ def patch_theta(lab_batch, img_size, P, draws, do_rotate=True):
     tx = (-tx_ + 0.5) * 2
     ty = (-ty_ + 0.5) * 2
     sin, cos = torch.sin(angle), torch.cos(angle)
-    theta = torch.zeros(B, 2, 3)
+    theta = torch.zeros(B, 2, 3, dtype=lab_batch.dtype)
     theta[:, 0, 0] = cos / scale
     theta[:, 0, 1] = sin / scale
     theta[:, 0, 2] = tx * cos / scale + ty * sin / scale
@@ -621,8 +629,9 @@ def train_step(patch, img_batch, lab_batch, draws, net, colors, target_id=TARGET
     (recorded pre-activations keep their gradients).  ``combine`` (tests of
     the data-parallel weighting): f(no_obj_loss, no_cls_loss, nps, tv,
     colorful) -> (loss, terms) replaces the loss formula of 312-314.
-    ``geometry``: see patch_transformer ("f64": the placement geometry in
-    float64, as the HIP path evaluates it).
+    ``geometry``: see patch_transformer ("fp32" the reference; "f64" the
+    placement geometry in float64; "fp32in64" the reference's fp32 sample
+    points under a float64 evaluation).
     """
     leaf = patch.detach().clone().requires_grad_(True)
     img_size = net.height

@@ -6,8 +6,11 @@ max|g_hip - g_ref| / max|g_ref| <= 1e-4).
 On yolov3-dota@608 the comparison is branch-aligned: the oracle runs on the
 LeakyReLU/maxpool decisions the HIP forward took, and every decision where
 the two disagree must be a rounding tie (assert_branch_ties_only) — a kernel
-that flips a real branch fails.  The yardstick is the float64 evaluation of
-the same ops on those branches; the bound is a fixed 1e-4."""
+that flips a real branch fails.  The trainer's placement is the reference's
+own fp32 arithmetic (po_patch_params geometry 1), so the bound is
+north_star's, literally: the HIP gradient within 1e-4 of the fp32 oracle.
+The float64 evaluation at the same sample points is the accuracy yardstick
+(HIP within 1e-5 of it)."""
 import pytest
 import torch
 
@@ -54,12 +57,7 @@ def _run(cfg, B, P, tmp_path, objective="ce", seed=0):
     return ref, terms, pg.grad.cpu()
 
 
-def _compare(ref, terms, grad, loss_tol=2e-5, grad_check=True, obj_tol=2e-5, ref_g64=None):
-    """``ref_g64``: the fp32 oracle with its placement geometry in float64 (the
-    HIP path's deliberate deviation); when given, each loss term
-    may differ from the literal fp32 oracle by loss_tol plus that oracle's own
-    geometry error on the term (|ref - ref_g64|), the triangle inequality of
-    assert_geometry_parity, and must be within loss_tol of ref_g64."""
+def _compare(ref, terms, grad, loss_tol=2e-5, grad_check=True, obj_tol=2e-5):
     assert int(terms["flags"].item()) == 0
     torch.testing.assert_close(terms["patch_center"].cpu(), ref["patch_center"], rtol=0, atol=0)
     cells = terms["cells"].cpu().tolist()
@@ -68,12 +66,7 @@ def _compare(ref, terms, grad, loss_tol=2e-5, grad_check=True, obj_tol=2e-5, ref
     torch.testing.assert_close(terms["cls"].cpu(), ref["cls"], rtol=0, atol=obj_tol)
     for k in ("loss", "nps_loss", "tv_loss", "no_obj_loss", "no_cls_loss", "colorful_loss"):
         a, b = float(terms[k]), float(ref[k])
-        slack = 0.0
-        if ref_g64 is not None:
-            bg = float(ref_g64[k])
-            slack = abs(b - bg)
-            assert abs(a - bg) <= loss_tol * max(1.0, abs(bg)), (k, a, bg, "float64-geometry oracle")
-        assert abs(a - b) <= loss_tol * max(1.0, abs(b)) + slack, (k, a, b, slack)
+        assert abs(a - b) <= loss_tol * max(1.0, abs(b)), (k, a, b)
     if grad_check:
         rel = float((grad - ref["grad"]).abs().max() / ref["grad"].abs().max())
         assert rel < 1e-4, rel
@@ -139,16 +132,23 @@ def assert_timed_path(tr):
                                   "po_conv_first_pool_wino_fwd_cmp"), plan.last_first_op
 
 
-def branch_aligned(tr, ref_net, img, lab, patch, dr, objective="ce", geometry32=False, hip_dr=None):
+def yardstick_geometry(tr):
+    """The float64 yardstick's placement geometry for trainer ``tr``: with the
+    reference geometry (the default) the HIP path samples exactly where the
+    fp32 reference samples, so the yardstick is the float64 evaluation at
+    those sample points ("fp32in64"); with ADVPATCH_GEOMETRY=f64 it is the
+    float64 geometry itself."""
+    return "fp32in64" if tr.patch_transformer.geometry == "ref" else "fp32"
+
+
+def branch_aligned(tr, ref_net, img, lab, patch, dr, objective="ce", hip_dr=None, f64=True):
     """One HIP step and the oracle on the branch decisions it took: the fp32
-    oracle (with the tie check), the float64 yardstick and, with
-    ``geometry32``, the fp32 oracle with its placement geometry in float64
-    (the HIP path's deliberate deviation).  Inputs on the CPU,
-    draws as CPU tensors (``hip_dr``: the HIP side's draws when they differ
-    in form, e.g. keyed_draws).  Returns (terms, hip grad, fp32 oracle result,
-    errs) with errs = {"hip_f64": |g_hip - g64|/max|g64|, "o32_f64": the fp32
-    oracle's own distance, "hip_o32": north_star's |g_hip - g32|/max|g32|,
-    "hip_o32g": the same against the float64-geometry fp32 oracle}."""
+    oracle (with the tie check) and (``f64``) the float64 yardstick.  Inputs
+    on the CPU, draws as CPU tensors (``hip_dr``: the HIP side's draws when
+    they differ in form, e.g. keyed_draws).  Returns (terms, hip grad, fp32
+    oracle result, errs) with errs = {"hip_o32": north_star's |g_hip -
+    g32|/max|g32|, "hip_f64": |g_hip - g64|/max|g64|, "o32_f64": the fp32
+    oracle's own distance from the yardstick}."""
     import time
     ld = pkg_mod("load_data")
     colors = ld.load_printability_colors("builtin:30values")
@@ -170,15 +170,11 @@ def branch_aligned(tr, ref_net, img, lab, patch, dr, objective="ce", geometry32=
     g32 = ref32["grad"]
     rel = lambda a, b: float((a.double() - b.double()).abs().max() / b.double().abs().max())
     errs = {"hip_o32": rel(g, g32)}
-    if geometry32:
-        ref32g = oracle.train_step(patch, img, lab, dr, ref_net, colors, objective=objective, branch=br,
-                                   geometry="f64")
-        errs["hip_o32g"] = rel(g, ref32g["grad"])
-        errs["ref32g"] = ref32g
-        say("fp32 oracle, float64 geometry")
-    g64 = oracle.train_step_f64(patch, img, lab, dr, ref_net, colors, objective=objective, branch=br)["grad"]
-    errs["hip_f64"], errs["o32_f64"] = rel(g, g64), rel(g32, g64)
-    say("float64 oracle")
+    if f64:
+        g64 = oracle.train_step_f64(patch, img, lab, dr, ref_net, colors, objective=objective, branch=br,
+                                    geometry=yardstick_geometry(tr))["grad"]
+        errs["hip_f64"], errs["o32_f64"] = rel(g, g64), rel(g32, g64)
+        say("float64 oracle")
     return terms, g, ref32, errs
 
 
@@ -193,17 +189,19 @@ def branch_aligned_608(tr, ref_net, B, seed, objective="ce"):
 
 def assert_north_star(errs, tag):
     """north_star's criterion: the HIP patch gradient within 1e-4 (max-abs
-    relative) of the fp32 oracle on the aligned branches, and within 1e-4 of
-    the float64 evaluation (the accuracy yardstick)."""
+    relative) of the fp32 oracle on the aligned branches -- literally, with
+    no allowance for the oracle's own error -- and within 1e-4 of the float64
+    yardstick."""
     print("%s patch grad: hip vs fp32 oracle %.3g, hip vs float64 %.3g, fp32 oracle vs float64 %.3g" % (
-        tag, errs["hip_o32"], errs["hip_f64"], errs["o32_f64"]))
-    assert errs["hip_f64"] <= 1e-4, errs
+        tag, errs["hip_o32"], errs.get("hip_f64", float("nan")), errs.get("o32_f64", float("nan"))))
     assert errs["hip_o32"] <= 1e-4, errs
+    if "hip_f64" in errs:
+        assert errs["hip_f64"] <= 1e-4, errs
 
 
 # The HIP path's own accuracy: its patch gradient against the float64
-# evaluation on the same branches.  The 1e-4 legs are dominated by the fp32
-# oracle's own error (its fp32 placement geometry); this bound is what a
+# evaluation at the same sample points and on the same branches.  The fp32
+# oracle carries its own fp32 convolution rounding; this bound is what a
 # regression of the HIP arithmetic itself would have to get past.
 HIP_F64_TOL = 1e-5
 
@@ -245,57 +243,21 @@ def test_step_yolov3_targeted(tmp_path):
 
 def test_step_yolov3_targeted_po_draws(tmp_path):
     """The same workload on the trainer's own draws (po_draws, key (143, 0, 0):
-    every scalar and the noise keyed).  On these draws the reference's fp32
-    placement geometry is itself ~2.2e-4 from the float64 evaluation (measured,
-    r05), so north_star's literal criterion (|g_hip - g_o32| <= 1e-4) cannot
-    hold for ANY implementation closer to the exact value than the fp32 oracle:
-    the bound is assert_geometry_parity's -- the HIP gradient within 1e-4 of the
-    float64 evaluation and of the fp32 oracle with float64 geometry, within
-    1e-4 + the fp32 oracle's own distance of the literal fp32 oracle -- and the
-    HIP path's own accuracy, within 1e-5 of float64."""
+    every scalar and the noise keyed): north_star's literal criterion, the HIP
+    gradient within 1e-4 of the fp32 oracle, and the HIP path's own accuracy
+    within 1e-5 of the float64 evaluation at the reference's sample points.
+    (Round 5 sampled in float64 and measured 2.18e-4 here: the reference's
+    fp32 placement rounding, which the reference geometry now reproduces.)"""
     tr, ref_net = _trainer("builtin:yolov3-dota", tmp_path, objective="targeted", prec="fp32")
     sy = pkg_mod("synthetic")
     B, P, S = 3, 224, 608
     img, lab, patch = sy.frames(B, S, seed=140), sy.labels(B, seed=141), sy.patch(P, seed=142)
     hip_dr, dr = keyed_draws(143, 0, 0, B, P)
-    terms, g, ref32, errs = branch_aligned(tr, ref_net, img, lab, patch, dr, "targeted", geometry32=True,
-                                           hip_dr=hip_dr)
+    terms, g, ref32, errs = branch_aligned(tr, ref_net, img, lab, patch, dr, "targeted", hip_dr=hip_dr)
     assert_timed_path(tr)
-    _compare(ref32, terms, g, grad_check=False, obj_tol=OBJ_TOL_608, ref_g64=errs.pop("ref32g"))
-    assert_geometry_parity(errs, "yolov3 targeted, po_draws")
+    _compare(ref32, terms, g, grad_check=False, obj_tol=OBJ_TOL_608)
+    assert_north_star(errs, "yolov3 targeted, po_draws")
     assert_hip_accuracy(errs, "yolov3 targeted, po_draws")
-
-
-def assert_tiny_parity(errs, tag):
-    """The tiny-15@416 bound: north_star's literal criterion, the HIP gradient
-    within 1e-4 of the fp32 oracle (the reference's own fp32 placement
-    geometry), and within 1e-4 of the float64 evaluation and of the fp32
-    oracle with float64 geometry.  The fp32 oracle's own distance to float64
-    is printed beside: its fp32 affine_grid is noisier at 416 than at 608
-    (target size scales with S), up to ~1.5e-4 on some draws,
-    so a draw where the reference's fp32 geometry alone exceeds 1e-4 would
-    fail here — none of the seeds below does."""
-    print("%s patch grad: hip vs fp32 oracle %.3g (fp32 oracle vs float64 %.3g), hip vs fp32 oracle with f64 "
-          "geometry %.3g, hip vs float64 %.3g" % (tag, errs["hip_o32"], errs["o32_f64"], errs["hip_o32g"],
-                                                 errs["hip_f64"]))
-    assert errs["hip_f64"] <= 1e-4, errs
-    assert errs["hip_o32g"] <= 1e-4, errs
-    assert errs["hip_o32"] <= 1e-4, errs
-
-
-def assert_geometry_parity(errs, tag):
-    """For draws on which the reference's fp32 placement geometry is itself
-    more than 1e-4 from the float64 evaluation: the HIP gradient within 1e-4
-    of the float64 evaluation and of the fp32 oracle with float64 geometry,
-    and within 1e-4 + the fp32 oracle's own distance of the literal fp32
-    oracle (triangle inequality: no tighter bound can hold for an
-    implementation closer to the exact value than that oracle)."""
-    print("%s patch grad: hip vs fp32 oracle %.3g (fp32 oracle vs float64 %.3g), hip vs fp32 oracle with f64 "
-          "geometry %.3g, hip vs float64 %.3g" % (tag, errs["hip_o32"], errs["o32_f64"], errs["hip_o32g"],
-                                                 errs["hip_f64"]))
-    assert errs["hip_f64"] <= 1e-4, errs
-    assert errs["hip_o32g"] <= 1e-4, errs
-    assert errs["hip_o32"] <= 1e-4 + errs["o32_f64"], errs
 
 
 @pytest.mark.parametrize("objective", ["ce", "targeted"])
@@ -304,17 +266,17 @@ def test_step_tiny_416(tmp_path, objective):
     oracle's generalised (nheads, 5+C) loss head), B=4, exact
     fp32: cells bit-exact, loss terms within 2e-5, objectness/class within
     5e-5, the patch gradient branch-aligned (LeakyReLU signs and max-pool
-    argmaxes, ties asserted) as assert_tiny_parity states."""
+    argmaxes, ties asserted): north_star's literal 1e-4 against the fp32
+    oracle and the HIP accuracy bound against float64."""
     sy = pkg_mod("synthetic")
     tr, ref_net = _trainer("builtin:yolov3-tiny-dota", tmp_path, objective=objective, prec="fp32")
     B, P, S = 4, 224, 416
     img, lab = sy.frames(B, S, seed=90), sy.labels(B, seed=91)
     patch, dr = sy.patch(P, seed=92), sy.draws(B, P, seed=93)
-    terms, g, ref32, errs = branch_aligned(tr, ref_net, img, lab, patch, dr, objective, geometry32=True)
-    errs.pop("ref32g")
+    terms, g, ref32, errs = branch_aligned(tr, ref_net, img, lab, patch, dr, objective)
     assert terms["obj"].shape == (B, 6) and terms["cls"].shape == (B, 6, 15)
     _compare(ref32, terms, g, grad_check=False, obj_tol=OBJ_TOL_608)
-    assert_tiny_parity(errs, "tiny B=4 %s" % objective)
+    assert_north_star(errs, "tiny B=4 %s" % objective)
     assert_hip_accuracy(errs, "tiny B=4 %s" % objective)
 
 

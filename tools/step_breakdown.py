@@ -55,22 +55,35 @@ descs = [d for name, _, d in plan.fwd_ops + plan.bwd_ops if name == "po_conv"]
 assert len(descs) == n
 ms = defaultdict(float)
 macs = defaultdict(float)
+mfma = defaultdict(float)
 for k, (e0, e1, d, c) in enumerate(timer):
     ms[k % n] += e0.elapsed_time(e1) / args.steps
     macs[k % n] += plan.launch_macs(d, c) / args.steps
+    mfma[k % n] += plan.launch_mfma_flops(d, c) / args.steps
 tot = sum(ms.values())
-print("%-6s %5s %9s %5s %6s %4s %3s %9s %7s %6s" % ("kind", "block", "B*Hg*Wg", "N", "K", "tile", "ks", "us", "TF", "%"))
+PEAK = 157.3          # dense fp32 MFMA TFLOP/s (MI355X_MICROARCH.md), v_mfma_f32_32x32x2_f32
+# dense_TF: the direct convolution's FLOPs (2 x MACs of the launch's live grid) per second -- a
+# Winograd launch executes 1/4 (F(4x4)) or 4/9 (F(2x2)) of them, so this is NOT a utilisation and
+# may exceed the peak.  mfma_TF / frac: the FLOPs the matrix cores execute (NetPlan.launch_mfma_flops,
+# the bench line's roofline) per second, and their fraction of PEAK -- the utilisation.
+print("%-6s %5s %9s %5s %6s %4s %3s %9s %9s %8s %5s %6s" % ("kind", "block", "B*Hg*Wg", "N", "K", "tile", "ks", "us",
+                                                           "dense_TF", "mfma_TF", "frac", "%"))
 for k, d in enumerate(descs):
     K = d.ntaps * d.Cin_p
     M = d.B * d.Hg * d.Wg
-    print("%-6s %5d %9d %5d %6d %4d %3d %9.1f %7.1f %6.2f" % (d.kind, d.block, M, d.N, K, d.tile, d.ksplit, ms[k] * 1e3,
-                                                      2 * macs[k] / (ms[k] * 1e-3) / 1e12, 100 * ms[k] / tot))
-print("total conv ms/step %.3f, launches %d, executed TFLOP/step %.3f" % (tot, n, 2 * sum(macs.values()) / 1e12))
+    t = ms[k] * 1e-3
+    print("%-6s %5d %9d %5d %6d %4d %3d %9.1f %9.1f %8.1f %5.2f %6.2f" % (
+        d.kind, d.block, M, d.N, K, d.tile, d.ksplit, ms[k] * 1e3, 2 * macs[k] / t / 1e12, mfma[k] / t / 1e12,
+        mfma[k] / t / 1e12 / PEAK, 100 * ms[k] / tot))
+mf = sum(mfma.values())
+print("total conv ms/step %.3f, launches %d, dense-equivalent TFLOP/step %.3f (not executed work), "
+      "MFMA-executed TFLOP/step %.3f (= the bench line's mfma_flops_per_step), MFMA frac %.3f" % (
+          tot, n, 2 * sum(macs.values()) / 1e12, mf / 1e12, mf / (tot * 1e-3) / 1e12 / PEAK))
 if os.environ.get("BREAKDOWN_JSON"):
     import json
     with open(os.environ["BREAKDOWN_JSON"], "w") as f:
         json.dump({"steps": args.steps, "launches": [
             {"kind": d.kind, "block": d.block, "M": d.B * d.Hg * d.Wg, "N": d.N, "K": d.ntaps * d.Cin_p,
-             "tile": d.tile, "ksplit": d.ksplit, "macs": macs[k], "boxed": bool(d.gbox),
+             "tile": d.tile, "ksplit": d.ksplit, "macs": macs[k], "mfma_flops": mfma[k], "boxed": bool(d.gbox),
              "us_events": ms[k] * 1e3}
             for k, d in enumerate(descs)]}, f)

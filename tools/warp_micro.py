@@ -28,8 +28,8 @@ dr = sy.draws_device(seed, step, 0, B, P, dev)
 lab = sy.labels(B, seed=4).to(dev)
 img = sy.frames(B, S, seed=3).to(dev)
 mp = sy.patch(P, seed=5).to(dev).contiguous()
-_, _, _, roi, affine = ld.patch_params(lab, S, P, dr, True, with_roi=True)
-off = affine.clone()
+_, _, _, roi, affine = ld.patch_params(lab, S, P, dr, True, with_roi=True)     # the trainer's (reference) geometry
+_, _, _, _, off = ld.patch_params(lab, S, P, dr, True, with_roi=True, geometry="f64")   # pixel-space map rows
 off[:, 2] += 4 * S                      # every sample point far right of the patch: no footprint pixel
 roi_off = torch.zeros_like(roi)          # ... and an empty footprint box
 out = torch.empty(B, 3, S, S, device=dev)
