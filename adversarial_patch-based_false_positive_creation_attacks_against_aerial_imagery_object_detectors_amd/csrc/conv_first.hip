@@ -236,7 +236,7 @@ __device__ __forceinline__ void pool_conv_px(const float (&xa)[3][4][4], const f
 #pragma unroll
         for (int q = 0; q < 3; ++q) xp[c][r][q] = (f2_t){xa[c][r][q], xa[c][r][q + 1]};
   }
-  vmax = 0.f;
+  vmax = 0.f;                 // max|pooled value|: the callers read it from ys_px (fp16x3 slots only)
 #pragma unroll
   for (int i = 0; i < CO / 4; ++i) aw[i] = 0u;
 #pragma unroll
@@ -289,17 +289,31 @@ __device__ __forceinline__ void pool_conv_px(const float (&xa)[3][4][4], const f
         v[2] = s1[0];
         v[3] = s1[1];
       }
-      if (act) {
+      if (WINO) {
+        // the pool before the activation: LeakyReLU is non-decreasing, so the
+        // window's max of leaky(v) is leaky(max v), bit for bit, and one
+        // activation replaces four.  The window position is the first
+        // maximum of v; it differs from the first maximum of leaky(v) only
+        // where two negative values round to one leaky value (a tie of the
+        // pooled values either way).  Not taken in the direct
+        // form, which is bit-identical to conv + po_maxpool2_fwd.
+        bv = v[0];
 #pragma unroll
-        for (int k = 0; k < 4; ++k) v[k] = po::leaky(v[k]);
+        for (int k = 1; k < 4; ++k)
+          if (v[k] > bv || isnan(v[k])) { bv = v[k]; code = (uint32_t)k; }
+        if (act) bv = po::leaky(bv);
+      } else {
+        if (act) {
+#pragma unroll
+          for (int k = 0; k < 4; ++k) v[k] = po::leaky(v[k]);
+        }
+        bv = v[0];
+#pragma unroll
+        for (int k = 1; k < 4; ++k)
+          if (v[k] > bv || isnan(v[k])) { bv = v[k]; code = (uint32_t)k; }
       }
-      bv = v[0];
-#pragma unroll
-      for (int k = 1; k < 4; ++k)
-        if (v[k] > bv || isnan(v[k])) { bv = v[k]; code = (uint32_t)k; }
       if (act) code |= 8u | (bv > 0.f ? 0u : 4u);   // linear conv: no slope to apply
     }
-    vmax = fmaxf(vmax, fabsf(bv));
     ys_px[co] = bv;
     aw[co >> 2] |= code << (8 * (co & 3));
   }
@@ -386,7 +400,11 @@ __global__ __launch_bounds__(256) void first_pool_fwd_k(const float* __restrict_
   float vmax;
   uint32_t aw[CO / 4];
   pool_conv_px<CO, WINO>(xa, Wt, bias, Cout, act, ys + tid * LS, aw, vmax);
-  if (amax) po::amax_commit(amax, live ? vmax : 0.f);
+  if (amax) {                                       // fp16x3 plans only: no VALU spent on it otherwise
+#pragma unroll
+    for (int co = 0; co < CO; ++co) vmax = fmaxf(vmax, fabsf(ys[tid * LS + co]));
+    po::amax_commit(amax, live ? vmax : 0.f);
+  }
   if (live) {
     uint4* ap = reinterpret_cast<uint4*>(am + (int64_t)p0 * CO);
 #pragma unroll
@@ -484,7 +502,11 @@ __global__ __launch_bounds__(256) void first_pool_tile_k(const float* __restrict
   float vmax;
   uint32_t aw[CO / 4];
   pool_conv_px<CO, WINO>(xa, Wt, bias, Cout, act, ys + tid * LS, aw, vmax);
-  if (amax) po::amax_commit(amax, live ? vmax : 0.f);
+  if (amax) {                                       // fp16x3 plans only: no VALU spent on it otherwise
+#pragma unroll
+    for (int co = 0; co < CO; ++co) vmax = fmaxf(vmax, fabsf(ys[tid * LS + co]));
+    po::amax_commit(amax, live ? vmax : 0.f);
+  }
   const int64_t row0 = ((int64_t)b * Hp + ty * 16) * Wp + tx * 16;   // pixel (ly = 0, lx = 0)
   if (live) {
     uint4* ap = reinterpret_cast<uint4*>(am + (row0 + (int64_t)ly * Wp + lx) * CO);

@@ -355,7 +355,7 @@ __global__ __launch_bounds__(64) void patch_params_k(const float* __restrict__ l
   const float ty_f = fminf(uy[b], 0.8f);     // load_data.py:706
   center[2 * b + 0] = tx_f * fS;             // load_data.py:712-715
   center[2 * b + 1] = ty_f * fS;
-  if (geometry == 1) {
+  if (geometry == 1 || geometry == 2) {
     // the reference's fp32 arithmetic, op by op (warp_geom.h): lab_transform's
     // (max row + min row) / 2 (load_data.py:474-477), * img_size (654-660),
     // .mul(1/2) ** 2, the sum and sqrt (667-668), / patch side (717)
@@ -376,7 +376,7 @@ __global__ __launch_bounds__(64) void patch_params_k(const float* __restrict__ l
     float* tho = theta + 6 * b;
     for (int k = 0; k < 6; ++k) tho[k] = th[k];
     if (tsize) tsize[b] = ts;
-    if (affine) po::store_ref_row(th, affine + 6 * b);
+    if (affine) po::store_ref_row(th, geometry, affine + 6 * b);
     if (roi) {
       double thd[6], af[6];
       for (int k = 0; k < 6; ++k) thd[k] = (double)th[k];
@@ -425,7 +425,8 @@ extern "C" int po_patch_params(const float* lab, int B, int L, const float* angl
   PO_REQUIRE(lab && ux && uy && theta && center, "po_patch_params: null pointer");
   PO_REQUIRE(!do_rotate || angle, "po_patch_params: angle required when do_rotate");
   PO_REQUIRE(B > 0 && L > 0 && S > 0 && P > 0, "po_patch_params: bad shape");
-  PO_REQUIRE(geometry == 0 || (geometry == 1 && S > 1), "po_patch_params: geometry must be 0 (float64) or 1 (reference fp32, S > 1)");
+  PO_REQUIRE(geometry == 0 || ((geometry == 1 || geometry == 2) && S > 1),
+             "po_patch_params: geometry must be 0 (float64), 1 or 2 (reference fp32, S > 1)");
   PO_REQUIRE(!sincos_lut || ((uintptr_t)sincos_lut % 8) == 0, "po_patch_params: sincos_lut must be 8-byte aligned");
   hipLaunchKernelGGL(patch_params_k, dim3(B), dim3(64), 0, po::stream_of(s), lab, B, L, angle, ux, uy,
                      do_rotate, S, P, geometry, sincos_lut, theta, center, target_size, roi, affine);
@@ -498,7 +499,7 @@ __device__ __forceinline__ bool sample_point(const po::Geo& G, const WarpGeom& g
                                              float w[4]) {
   if (G.ref) {
     float ix, iy;
-    po::ref_sample_coord(G.th, g.S, i, j, ix, iy);
+    po::ref_sample_coord(G.th, G.ref, g.S, i, j, ix, iy);
     if (!(ix >= (float)(g.padL - 1) && ix < (float)(g.padL + g.P) && iy >= (float)(g.padT - 1) &&
           iy < (float)(g.padT + g.P)))
       return false;

@@ -71,13 +71,18 @@ __device__ __forceinline__ void footprint_roi(const double af[6], int S, int P, 
 //   theta        cos/scale, sin/scale, tx*cos/scale + ty*sin/scale, ...   738-743
 //   affine_grid  base b(k) = fl(fl(linspace_k * (S-1)) / S), linspace_k =
 //                fma(step, k, -1) (k < S/2) or fma(-step, S-1-k, 1), step =
-//                fl(2/(S-1)); x = fl(fma(by, t1, fl(bx*t0)) + t2)        745
+//                fl(2/(S-1)); x = bx*t0 + by*t1 + t2 through MKL's sgemm,
+//                whose code path depends on the host CPU: on AMD EPYC (the
+//                MI355X hosts) fl(fl(fl(bx*t0) + fl(by*t1)) + t2) -- geometry 1;
+//                on Intel AVX-512 fl(fma(by, t1, fl(bx*t0)) + t2) -- geometry 2
+//                (load_data.reference_bmm_form() asks the host's torch) 745
 //   grid_sample  ix = fma(x + 1, S/2, -0.5); bilinear weights s*e, s*w, n*e,
 //                n*w; value = fma chain over the corners nw, ne, sw, se   748-749
 // An affine row [6] float64 in this form holds the six fp32 theta values as
-// float[6] in its first 24 bytes and AFFINE_REF_TAG in row[3] -- a signalling
-// NaN bit pattern, which no arithmetic produces, so a float64-form row (the
-// pixel-space map of theta_pixel_affine) never carries it.
+// float[6] in its first 24 bytes and a tag in row[3] -- AFFINE_REF_TAG + 1 or
+// + 2 (the geometry), signalling-NaN bit patterns, which no arithmetic
+// produces, so a float64-form row (the pixel-space map of theta_pixel_affine)
+// never carries one.
 // ---------------------------------------------------------------------------
 constexpr unsigned long long AFFINE_REF_TAG = 0x7FF4A0F3E5F32000ull;
 
@@ -88,16 +93,18 @@ constexpr unsigned long long AFFINE_REF_TAG = 0x7FF4A0F3E5F32000ull;
 struct Geo {
   double af[6];
   float th[6];
-  int ref;
+  int ref;      // 0: float64 pixel-space map; 1 / 2: the reference's fp32 arithmetic, sgemm form 1 / 2
 };
 
-__device__ __forceinline__ bool affine_row_is_ref(const double* row) {
-  return (unsigned long long)__double_as_longlong(row[3]) == AFFINE_REF_TAG;
+// the geometry of a row: 0 (float64 form), 1 or 2 (reference forms)
+__device__ __forceinline__ int affine_row_form(const double* row) {
+  const unsigned long long t = (unsigned long long)__double_as_longlong(row[3]);
+  return (t == AFFINE_REF_TAG + 1) ? 1 : (t == AFFINE_REF_TAG + 2) ? 2 : 0;
 }
 
 __device__ __forceinline__ Geo load_geo(const double* row, int S) {
   Geo G;
-  G.ref = affine_row_is_ref(row) ? 1 : 0;
+  G.ref = affine_row_form(row);
   if (G.ref) {
     const float* t = reinterpret_cast<const float*>(row);
     double th[6];
@@ -117,11 +124,11 @@ __device__ __forceinline__ Geo load_geo(const double* row, int S) {
   return G;
 }
 
-__device__ __forceinline__ void store_ref_row(const float th[6], double* row) {
+__device__ __forceinline__ void store_ref_row(const float th[6], int form, double* row) {
   float* t = reinterpret_cast<float*>(row);
 #pragma unroll
   for (int k = 0; k < 6; ++k) t[k] = th[k];
-  row[3] = __longlong_as_double((long long)AFFINE_REF_TAG);
+  row[3] = __longlong_as_double((long long)(AFFINE_REF_TAG + (unsigned long long)form));
   row[4] = 0.0;
   row[5] = 0.0;
 }
@@ -133,11 +140,19 @@ __device__ __forceinline__ float ref_base(int k, int S) {
   return __fdiv_rn(__fmul_rn(lin, (float)(S - 1)), (float)S);
 }
 
-// grid_sample's source coordinate (column ix, row iy) of output pixel (i, j)
-__device__ __forceinline__ void ref_sample_coord(const float th[6], int S, int i, int j, float& ix, float& iy) {
+// grid_sample's source coordinate (column ix, row iy) of output pixel (i, j);
+// form: the host sgemm's order of the K = 3 dot product (see above)
+__device__ __forceinline__ void ref_sample_coord(const float th[6], int form, int S, int i, int j, float& ix,
+                                                 float& iy) {
   const float bx = ref_base(j, S), by = ref_base(i, S);
-  const float gx = __fadd_rn(__fmaf_rn(by, th[1], __fmul_rn(bx, th[0])), th[2]);
-  const float gy = __fadd_rn(__fmaf_rn(by, th[4], __fmul_rn(bx, th[3])), th[5]);
+  float gx, gy;
+  if (form == 2) {
+    gx = __fadd_rn(__fmaf_rn(by, th[1], __fmul_rn(bx, th[0])), th[2]);
+    gy = __fadd_rn(__fmaf_rn(by, th[4], __fmul_rn(bx, th[3])), th[5]);
+  } else {
+    gx = __fadd_rn(__fadd_rn(__fmul_rn(bx, th[0]), __fmul_rn(by, th[1])), th[2]);
+    gy = __fadd_rn(__fadd_rn(__fmul_rn(bx, th[3]), __fmul_rn(by, th[4])), th[5]);
+  }
   const float half = (float)S * 0.5f;
   ix = __fmaf_rn(__fadd_rn(gx, 1.0f), half, -0.5f);
   iy = __fmaf_rn(__fadd_rn(gy, 1.0f), half, -0.5f);

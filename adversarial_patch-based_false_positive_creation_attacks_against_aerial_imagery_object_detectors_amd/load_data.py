@@ -194,7 +194,47 @@ class HasSusRGB(nn.Module):
 # ---------------------------------------------------------------------------
 # Patch placement and warp
 # ---------------------------------------------------------------------------
-GEOMETRIES = {"ref": 1, "f64": 0}
+_BMM_FORM = []
+
+
+def reference_bmm_form():
+    """The order in which this host's PyTorch-CPU evaluates affine_grid's
+    K = 3 dot product x = bx*t0 + by*t1 + t2 (load_data.py:745): MKL's sgemm
+    picks its code path by CPU -- "sum" (fl(fl(bx*t0) + fl(by*t1)) + t2, the
+    AMD EPYC hosts of the MI355X boxes) or "fma" (fl(fma(by, t1, fl(bx*t0)) +
+    t2), Intel AVX-512).  Asked once per process with a small affine_grid:
+    the "sum" form reproduces it exactly or the host uses the "fma" one
+    (tests/test_geometry_ref.py pins both forms against the host's torch)."""
+    if not _BMM_FORM:
+        th = torch.randn(2, 2, 3, generator=torch.Generator().manual_seed(7)) * 3
+        g = F.affine_grid(th, (2, 1, 64, 64), align_corners=False).numpy()
+        lin = torch.linspace(-1, 1, 64).numpy()
+        base = ((lin * np.float32(63)).astype(np.float32) / np.float32(64)).astype(np.float32)
+        t = th.numpy()
+        bx, by = base[None, None, :], base[None, :, None]
+        same = True
+        for r in range(2):
+            t0, t1, t2 = (t[:, r, k][:, None, None] for k in range(3))
+            x = (((bx * t0).astype(np.float32) + (by * t1).astype(np.float32)).astype(np.float32) + t2)
+            same &= bool(np.array_equal(x.astype(np.float32), g[..., r]))
+        _BMM_FORM.append("sum" if same else "fma")
+    return _BMM_FORM[0]
+
+
+class _Geometries(dict):
+    """{"ref": 1 or 2 (po_patch_params' reference geometry for this host's
+    sgemm order, reference_bmm_form()), "f64": 0}."""
+
+    def __missing__(self, key):
+        if key != "ref":
+            raise KeyError(key)
+        return 1 if reference_bmm_form() == "sum" else 2
+
+    def __contains__(self, key):
+        return key in ("ref", "f64")
+
+
+GEOMETRIES = _Geometries(f64=0)
 
 
 def default_geometry():
@@ -205,7 +245,7 @@ def default_geometry():
     reference)."""
     g = os.environ.get("ADVPATCH_GEOMETRY", "ref")
     if g not in GEOMETRIES:
-        raise ValueError("ADVPATCH_GEOMETRY must be one of %s" % (tuple(GEOMETRIES),))
+        raise ValueError("ADVPATCH_GEOMETRY must be one of ('ref', 'f64')")
     return g
 
 

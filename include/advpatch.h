@@ -68,13 +68,16 @@ int po_median_bwd(const float* dy, const int32_t* argidx, int C, int H, int W, i
  * (may be NULL) = {x0,y0,x1,y1} bounding box (+2 px margin, clipped to the
  * image) of the output pixels the warped patch can touch; affine out [B,6]
  * float64 rows (may be NULL) for po_warp_*.
- * geometry 1 (ABI 27; the trainer's default): the reference's fp32
+ * geometry 1 or 2 (ABI 27; the trainer's default): the reference's fp32
  * arithmetic -- theta (load_data.py:738-743), affine_grid (745) and
  * grid_sample (748-749) as PyTorch-CPU computes them, op by op (pinned by
- * tests/test_geometry_ref.py); theta and target_size are those fp32 values,
- * and each affine row holds the fp32 theta as float[6] in its first 24 bytes
- * with a tag in row[3] (warp_geom.h), so the warp kernels sample exactly
- * where the reference samples.  sin/cos of angles on po_draws' lattice come
+ * tests/test_geometry_ref.py); affine_grid's K = 3 dot product in the order
+ * of the host's MKL sgemm: 1 = fl(fl(bx*t0) + fl(by*t1)) + t2 (AMD EPYC
+ * hosts), 2 = fl(fma(by, t1, fl(bx*t0))) + t2 (Intel AVX-512); theta and
+ * target_size are those fp32 values, and each affine row holds the fp32
+ * theta as float[6] in its first 24 bytes with a tag in row[3]
+ * (warp_geom.h), so the warp kernels sample exactly where the reference
+ * samples.  sin/cos of angles on po_draws' lattice come
  * from sincos_lut [2^24][2] fp32 (8-byte aligned; may be NULL): PyTorch-CPU's
  * own torch.sin/torch.cos of the lattice angle k at [k] (MKL VML is not
  * correctly rounded, so the values are tabulated, not restated); other angles

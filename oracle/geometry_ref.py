@@ -17,8 +17,12 @@ reference-geometry form (csrc/warp_geom.h ``ref_*``) is this sequence:
   affine_grid base    AffineGridGenerator.cpp linspace_from_neg_one:
                       range * (S-1) / S (two roundings).
   affine_grid bmm     base_grid [N,H*W,3] @ theta^T through MKL sgemm with
-                      K = 3: x = fl(fl(fma(by, t1, fl(bx*t0))) + t2) (the k=0
-                      product, the k=1 FMA, the k=2 term times 1 added).
+                      K = 3, whose code path MKL picks by CPU: on the MI355X
+                      boxes' AMD EPYC 9575F x = fl(fl(fl(bx*t0) + fl(by*t1)) +
+                      t2) ("sum", HIP geometry 1); on this build container's
+                      Intel AVX-512 Xeon x = fl(fma(by, t1, fl(bx*t0)) + t2)
+                      ("fma", geometry 2); tools/affine_grid_probe.py measures
+                      every evaluation order on a host.
   grid_sample         GridSamplerKernel.cpp (vectorised CPU kernel),
                       bilinear, zeros padding: ix = fma(g + 1, S/2, -0.5);
                       w = ix - floor(ix), e = 1 - w (same for rows: n, s);
@@ -77,18 +81,36 @@ def base32(S):
     return ((linspace32(S) * f32(S - 1)).astype(f32) / f32(S)).astype(f32)
 
 
-def affine_grid32(theta, H, W):
+BMM_FORMS = ("sum", "fma")          # HIP geometry 1, 2
+
+
+def affine_grid32(theta, H, W, form):
     """F.affine_grid(theta [N,2,3] fp32, (N,C,H,W), align_corners=False) ->
-    [N,H,W,2] fp32."""
+    [N,H,W,2] fp32, with the host sgemm's K = 3 order ``form`` ("sum" / "fma")."""
     th = np.asarray(theta, dtype=f32)
     bx = base32(W)[None, None, :]
     by = base32(H)[None, :, None]
     out = []
     for r in range(2):
         t0, t1, t2 = (th[:, r, k][:, None, None] for k in range(3))
-        acc = fma32(by, t1, (bx * t0).astype(f32))
+        if form == "fma":
+            acc = fma32(by, t1, (bx * t0).astype(f32))
+        else:
+            acc = ((bx * t0).astype(f32) + (by * t1).astype(f32)).astype(f32)
         out.append((acc + t2).astype(f32))
     return np.stack(out, -1)
+
+
+def host_bmm_form():
+    """The form this host's torch follows (None: neither)."""
+    import torch
+    import torch.nn.functional as F
+    th = torch.randn(2, 2, 3, generator=torch.Generator().manual_seed(7)) * 3
+    g = F.affine_grid(th, (2, 1, 64, 64), align_corners=False).numpy()
+    for form in BMM_FORMS:
+        if np.array_equal(affine_grid32(th.numpy(), 64, 64, form), g):
+            return form
+    return None
 
 
 def unnormalize32(g, size):

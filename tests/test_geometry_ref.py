@@ -72,13 +72,22 @@ def check_theta(B=64, S=608, P=224):
 
 
 def check_affine_grid():
+    """The host's sgemm follows one of the two restated K = 3 orders exactly,
+    on every shape, and the trainer's own probe (load_data.reference_bmm_form,
+    which picks the HIP geometry) names the same one."""
+    form = G.host_bmm_form()
+    print("host sgemm form:", form)
+    assert form in G.BMM_FORMS
     for S, P in ((608, 224), (416, 224), (96, 32)):
         th, _, _, _ = _placements(4, S, P, S)
         g = F.affine_grid(th, (4, 3, S, S), align_corners=False).numpy()
-        assert np.array_equal(G.affine_grid32(th.numpy(), S, S), g), S
+        assert np.array_equal(G.affine_grid32(th.numpy(), S, S, form), g), S
     th = torch.randn(3, 2, 3, generator=torch.Generator().manual_seed(1)) * 3
     g = F.affine_grid(th, (3, 1, 50, 70), align_corners=False).numpy()
-    assert np.array_equal(G.affine_grid32(th.numpy(), 50, 70), g)
+    assert np.array_equal(G.affine_grid32(th.numpy(), 50, 70, form), g)
+    ld = pkg_mod("load_data")
+    assert ld.reference_bmm_form() == form
+    assert ld.GEOMETRIES["ref"] == 1 + G.BMM_FORMS.index(form)
 
 
 def check_grid_sample():
