@@ -41,7 +41,7 @@ _SIGS = {
     "po_median_fwd": [c_void_p] + [c_int] * 11 + [c_void_p, c_void_p, c_void_p],
     "po_median_bwd": [c_void_p, c_void_p] + [c_int] * 11 + [c_void_p, c_void_p],
     "po_patch_params": [c_void_p, c_int, c_int, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int,
-                        c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p],
+                        c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p],
     "po_draws": [ctypes.c_uint64, ctypes.c_uint64, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p,
                  c_void_p, c_void_p, c_void_p],
     "po_check_finite": [c_void_p, c_int64, c_int, c_void_p, c_void_p],

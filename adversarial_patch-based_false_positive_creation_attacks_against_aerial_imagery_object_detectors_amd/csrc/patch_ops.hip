@@ -321,11 +321,32 @@ __device__ __forceinline__ void ref_sincos(float a, const float* __restrict__ lu
   cs = (float)cos((double)a);
 }
 
+// sqrt of a target size's square as torch.sqrt computes it on the CPU
+// (load_data.py:667-668; MKL VML's vsSqrt, not correctly rounded: ~0.6 % of
+// values one ulp off on Intel AVX-512, ~17 % on the AMD EPYC hosts of the
+// MI355X boxes).  Its result scales exactly with the input's powers of 4
+// (sqrt(4^k m) = 2^k sqrt(m), measured: tests/test_geometry_ref.py), so
+// `lut` holds the host's values over one period, m in [1, 4) (2^24 floats,
+// entry i = sqrt of the float with bits 0x3F800000 + i;
+// load_data.sqrt_period_table); a normal positive v = 4^k m reads entry
+// (exponent parity, mantissa) and scales by 2^k.  No table, or zero, a
+// subnormal, inf or NaN: the correctly rounded value.
+__device__ __forceinline__ float ref_sqrt(float v, const float* __restrict__ lut) {
+  const uint32_t u = __float_as_uint(v);
+  const int e = (int)((u >> 23) & 0xff);
+  if (!lut || (u >> 31) || e == 0 || e == 0xff) return sqrtf(v);      // correctly rounded (HIP default)
+  const int ue = e - 127;                                     // v = 2^ue * 1.f
+  const int k = ue >= 0 ? ue / 2 : -((1 - ue) / 2);           // floor(ue / 2)
+  const uint32_t idx = ((uint32_t)(ue - 2 * k) << 23) | (u & 0x7fffffu);   // m = 4^-k v in [1, 4)
+  return __builtin_ldexpf(lut[idx], k);
+}
+
 // one wave per image: the label scan is a wave reduction of (area, row) pairs
 __global__ __launch_bounds__(64) void patch_params_k(const float* __restrict__ lab, int B, int L,
                                                      const float* __restrict__ angle, const float* __restrict__ ux,
                                                      const float* __restrict__ uy, int do_rotate, int S, int P,
                                                      int geometry, const float* __restrict__ lut,
+                                                     const float* __restrict__ sqrt_lut,
                                                      float* __restrict__ theta, float* __restrict__ center,
                                                      float* __restrict__ tsize, int32_t* __restrict__ roi,
                                                      double* __restrict__ affine) {
@@ -361,14 +382,15 @@ __global__ __launch_bounds__(64) void patch_params_k(const float* __restrict__ l
     // .mul(1/2) ** 2, the sum and sqrt (667-668), / patch side (717)
     float s2 = 0.25f, s3 = 0.25f;
     if (!(vmax > 0.99f)) {
-      s2 = __fdiv_rn(__fadd_rn(lb[imax * 5 + 2], lb[imin * 5 + 2]), 2.0f);
-      s3 = __fdiv_rn(__fadd_rn(lb[imax * 5 + 3], lb[imin * 5 + 3]), 2.0f);
+      s2 = (lb[imax * 5 + 2] + lb[imin * 5 + 2]) / 2.0f;
+      s3 = (lb[imax * 5 + 3] + lb[imin * 5 + 3]) / 2.0f;
     }
-    const float h2 = __fmul_rn(__fmul_rn(s2, fS), 0.5f), h3 = __fmul_rn(__fmul_rn(s3, fS), 0.5f);
-    const float ts = __fsqrt_rn(__fadd_rn(__fmul_rn(h2, h2), __fmul_rn(h3, h3)));
-    const float sc = __fdiv_rn(ts, (float)P);
-    const float tx = __fmul_rn(__fadd_rn(-tx_f, 0.5f), 2.0f);             // load_data.py:726
-    const float ty = __fmul_rn(__fadd_rn(-ty_f, 0.5f), 2.0f);             // load_data.py:727
+    // (this file: fp contract(off) -- every operator below is one rounding)
+    const float h2 = (s2 * fS) * 0.5f, h3 = (s3 * fS) * 0.5f;
+    const float ts = ref_sqrt(h2 * h2 + h3 * h3, sqrt_lut);
+    const float sc = ts / (float)P;
+    const float tx = (-tx_f + 0.5f) * 2.0f;                               // load_data.py:726
+    const float ty = (-ty_f + 0.5f) * 2.0f;                               // load_data.py:727
     float sn = 0.f, cs = 1.f;                                              // angle fill_(0): 614
     if (do_rotate) ref_sincos(angle[b], lut, sn, cs);
     float th[6];
@@ -420,8 +442,8 @@ __global__ __launch_bounds__(64) void patch_params_k(const float* __restrict__ l
 
 extern "C" int po_patch_params(const float* lab, int B, int L, const float* angle, const float* ux,
                                const float* uy, int do_rotate, int S, int P, int geometry,
-                               const float* sincos_lut, float* theta, float* center, float* target_size,
-                               int32_t* roi, double* affine, po_stream_t s) {
+                               const float* sincos_lut, const float* sqrt_lut, float* theta, float* center,
+                               float* target_size, int32_t* roi, double* affine, po_stream_t s) {
   PO_REQUIRE(lab && ux && uy && theta && center, "po_patch_params: null pointer");
   PO_REQUIRE(!do_rotate || angle, "po_patch_params: angle required when do_rotate");
   PO_REQUIRE(B > 0 && L > 0 && S > 0 && P > 0, "po_patch_params: bad shape");
@@ -429,7 +451,7 @@ extern "C" int po_patch_params(const float* lab, int B, int L, const float* angl
              "po_patch_params: geometry must be 0 (float64), 1 or 2 (reference fp32, S > 1)");
   PO_REQUIRE(!sincos_lut || ((uintptr_t)sincos_lut % 8) == 0, "po_patch_params: sincos_lut must be 8-byte aligned");
   hipLaunchKernelGGL(patch_params_k, dim3(B), dim3(64), 0, po::stream_of(s), lab, B, L, angle, ux, uy,
-                     do_rotate, S, P, geometry, sincos_lut, theta, center, target_size, roi, affine);
+                     do_rotate, S, P, geometry, sincos_lut, sqrt_lut, theta, center, target_size, roi, affine);
   return po::check_launch("po_patch_params");
 }
 
@@ -506,12 +528,12 @@ __device__ __forceinline__ bool sample_point(const po::Geo& G, const WarpGeom& g
     const float fx = floorf(ix), fy = floorf(iy);
     x0 = (int)fx;
     y0 = (int)fy;
-    const float ex = __fsub_rn(ix, fx), wx = __fsub_rn(1.0f, ex);
-    const float ny = __fsub_rn(iy, fy), sy = __fsub_rn(1.0f, ny);
-    w[0] = __fmul_rn(sy, wx);
-    w[1] = __fmul_rn(sy, ex);
-    w[2] = __fmul_rn(ny, wx);
-    w[3] = __fmul_rn(ny, ex);
+    const float ex = ix - fx, wx = 1.0f - ex;          // (file-wide fp contract(off))
+    const float ny = iy - fy, sy = 1.0f - ny;
+    w[0] = sy * wx;
+    w[1] = sy * ex;
+    w[2] = ny * wx;
+    w[3] = ny * ex;
     return true;
   }
   double ix, iy;
@@ -533,7 +555,7 @@ __device__ __forceinline__ float aug_value(const float* __restrict__ mp, const N
 // one bilinear term: the reference form accumulates as grid_sample's fma
 // chain (fma(v, w, acc) corner after corner), the float64 form adds products
 __device__ __forceinline__ float bterm(bool ref, float v, float w, float acc) {
-  return ref ? __fmaf_rn(v, w, acc) : acc + v * w;
+  return ref ? __builtin_fmaf(v, w, acc) : acc + v * w;
 }
 
 // Forward of one output pixel: adv_t[3] (clamped) and msk_t.  Returns false

@@ -133,39 +133,48 @@ __device__ __forceinline__ void store_ref_row(const float th[6], int form, doubl
   row[5] = 0.0;
 }
 
+// The reference-form functions below spell out every rounding: plain fp32
+// operators under a block-scope `fp contract(off)` (HIP's __fmul_rn and
+// friends are plain operators in a header compiled with contraction allowed,
+// so an __fadd_rn(__fmul_rn(..)) pair may still fuse -- measured: it did in
+// one kernel and not in another) and __builtin_fmaf where the reference fuses.
+
 // affine_grid's base coordinate k of an S-point axis (align_corners=False)
 __device__ __forceinline__ float ref_base(int k, int S) {
-  const float step = __fdiv_rn(2.0f, (float)(S - 1));
-  const float lin = k < (S >> 1) ? __fmaf_rn(step, (float)k, -1.0f) : __fmaf_rn(-step, (float)(S - 1 - k), 1.0f);
-  return __fdiv_rn(__fmul_rn(lin, (float)(S - 1)), (float)S);
+#pragma clang fp contract(off)
+  const float step = 2.0f / (float)(S - 1);
+  const float lin = k < (S >> 1) ? __builtin_fmaf(step, (float)k, -1.0f) : __builtin_fmaf(-step, (float)(S - 1 - k), 1.0f);
+  return (lin * (float)(S - 1)) / (float)S;
 }
 
 // grid_sample's source coordinate (column ix, row iy) of output pixel (i, j);
 // form: the host sgemm's order of the K = 3 dot product (see above)
 __device__ __forceinline__ void ref_sample_coord(const float th[6], int form, int S, int i, int j, float& ix,
                                                  float& iy) {
+#pragma clang fp contract(off)
   const float bx = ref_base(j, S), by = ref_base(i, S);
   float gx, gy;
   if (form == 2) {
-    gx = __fadd_rn(__fmaf_rn(by, th[1], __fmul_rn(bx, th[0])), th[2]);
-    gy = __fadd_rn(__fmaf_rn(by, th[4], __fmul_rn(bx, th[3])), th[5]);
+    gx = __builtin_fmaf(by, th[1], bx * th[0]) + th[2];
+    gy = __builtin_fmaf(by, th[4], bx * th[3]) + th[5];
   } else {
-    gx = __fadd_rn(__fadd_rn(__fmul_rn(bx, th[0]), __fmul_rn(by, th[1])), th[2]);
-    gy = __fadd_rn(__fadd_rn(__fmul_rn(bx, th[3]), __fmul_rn(by, th[4])), th[5]);
+    gx = (bx * th[0] + by * th[1]) + th[2];
+    gy = (bx * th[3] + by * th[4]) + th[5];
   }
   const float half = (float)S * 0.5f;
-  ix = __fmaf_rn(__fadd_rn(gx, 1.0f), half, -0.5f);
-  iy = __fmaf_rn(__fadd_rn(gy, 1.0f), half, -0.5f);
+  ix = __builtin_fmaf(gx + 1.0f, half, -0.5f);
+  iy = __builtin_fmaf(gy + 1.0f, half, -0.5f);
 }
 
 // the reference theta from its fp32 inputs (load_data.py:738-743)
 __device__ __forceinline__ void ref_theta(float sn, float cs, float sc, float tx, float ty, float th[6]) {
-  th[0] = __fdiv_rn(cs, sc);
-  th[1] = __fdiv_rn(sn, sc);
-  th[2] = __fadd_rn(__fdiv_rn(__fmul_rn(tx, cs), sc), __fdiv_rn(__fmul_rn(ty, sn), sc));
-  th[3] = __fdiv_rn(-sn, sc);
-  th[4] = __fdiv_rn(cs, sc);
-  th[5] = __fadd_rn(__fdiv_rn(__fmul_rn(-tx, sn), sc), __fdiv_rn(__fmul_rn(ty, cs), sc));
+#pragma clang fp contract(off)
+  th[0] = cs / sc;
+  th[1] = sn / sc;
+  th[2] = (tx * cs) / sc + (ty * sn) / sc;
+  th[3] = (-sn) / sc;
+  th[4] = cs / sc;
+  th[5] = ((-tx) * sn) / sc + (ty * cs) / sc;
 }
 
 // The composite's written box of image b (po_warp_fwd_pre, po_warp_box_fwd_keyed):

@@ -273,6 +273,27 @@ def sincos_lattice_table(device):
     return lut
 
 
+_SQRT_LUT = {}
+
+
+def sqrt_period_table(device):
+    """[2^24] fp32 on ``device``: the host's torch.sqrt (load_data.py:667-668;
+    MKL VML, not correctly rounded: ~17 % of values one ulp off on the AMD
+    EPYC hosts of the MI355X boxes) of every float in [1, 4) -- entry i is
+    sqrt of the float with bits 0x3F800000 + i.  Its values scale exactly
+    with powers of 4 (tests/test_geometry_ref.py checks this on the host), so
+    one period reproduces the target size's sqrt for every normal input
+    (po_patch_params).  Built once per process and device (64 MiB of HBM)."""
+    dev = torch.device(device)
+    key = (dev.type, dev.index)
+    lut = _SQRT_LUT.get(key)
+    if lut is None:
+        bits = np.arange(0x3F800000, 0x3F800000 + (1 << 24), dtype=np.uint32)
+        lut = torch.sqrt(torch.from_numpy(bits.view(np.float32))).contiguous().to(dev)
+        _SQRT_LUT[key] = lut
+    return lut
+
+
 def patch_params(lab_batch, img_size, P, draws, do_rotate=True, with_roi=False, geometry=None):
     """(theta [B,6], patch_center [B,2], target_size [B][, roi [B,4] int32,
     affine [B,6] float64]) on the device.  ``affine`` holds the per-image
@@ -290,9 +311,10 @@ def patch_params(lab_batch, img_size, P, draws, do_rotate=True, with_roi=False, 
     affine = torch.empty(B, 6, dtype=torch.float64, device=dev) if with_roi else None
     angle = draws["angle"].contiguous().float() if do_rotate else None
     lut = sincos_lattice_table(dev) if (geometry == "ref" and do_rotate) else None
+    sq = sqrt_period_table(dev) if geometry == "ref" else None
     nat.call("po_patch_params", nat.ptr(lab), B, L, nat.ptr(angle), nat.ptr(draws["ux"].contiguous().float()),
              nat.ptr(draws["uy"].contiguous().float()), int(bool(do_rotate)), int(img_size), int(P),
-             GEOMETRIES[geometry], nat.ptr(lut), nat.ptr(theta), nat.ptr(center), nat.ptr(tsize),
+             GEOMETRIES[geometry], nat.ptr(lut), nat.ptr(sq), nat.ptr(theta), nat.ptr(center), nat.ptr(tsize),
              nat.ptr(roi, torch.int32), nat.ptr(affine, torch.float64), nat.stream())
     if with_roi:
         return theta, center, tsize, roi, affine

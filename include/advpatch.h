@@ -81,7 +81,10 @@ int po_median_bwd(const float* dy, const int32_t* argidx, int C, int H, int W, i
  * from sincos_lut [2^24][2] fp32 (8-byte aligned; may be NULL): PyTorch-CPU's
  * own torch.sin/torch.cos of the lattice angle k at [k] (MKL VML is not
  * correctly rounded, so the values are tabulated, not restated); other angles
- * get correctly rounded values.
+ * get correctly rounded values.  sqrt_lut [2^24] fp32 (may be NULL): the
+ * host's torch.sqrt (MKL VML, not correctly rounded either) of the floats
+ * with bits 0x3F800000 + i, i.e. one period [1, 4) of a function that scales
+ * exactly with powers of 4; the target size's sqrt reads it.
  * geometry 0: the same formulas in float64 from the same fp32 inputs; each
  * affine row is the pixel-space sampling map of affine_grid + grid_sample
  * (align_corners=False): output pixel (i,j) samples the padded patch at
@@ -89,8 +92,8 @@ int po_median_bwd(const float* dy, const int32_t* argidx, int C, int H, int W, i
  * fp32 on output). */
 int po_patch_params(const float* lab, int B, int L, const float* angle, const float* ux,
                     const float* uy, int do_rotate, int S, int P, int geometry, const float* sincos_lut,
-                    float* theta, float* center, float* target_size, int32_t* roi, double* affine,
-                    po_stream_t s);
+                    const float* sqrt_lut, float* theta, float* center, float* target_size, int32_t* roi,
+                    double* affine, po_stream_t s);
 
 /* Random draws of the patch transformer for images b0 .. b0+B-1 of a global
  * batch (load_data.py:548-574 contrast U(0.8,1.2), brightness U(-0.1,0.1),

@@ -130,11 +130,13 @@ def patch_transformer(adv_patch, lab_batch, img_size, draws, do_rotate=True, geo
     evaluates theta, the grid and the bilinear sampling in float64 from the
     same fp32 inputs and rounds each sampled value to fp32 once (the HIP
     path's opt-in float64 geometry, ADVPATCH_GEOMETRY=f64).  "fp32in64" (for
-    float64 runs, train_step_f64): theta and the affine grid exactly as the
-    fp32 reference computes them (from the fp32 labels and draws), the
-    sampling and everything after it in the batch's dtype -- the accuracy
-    yardstick of an implementation that reproduces the reference's fp32
-    sample points (the HIP default, po_patch_params geometry 1)."""
+    float64 runs, train_step_f64): the reference's fp32 sample points --
+    theta, the affine grid and grid_sample's unnormalisation exactly as the
+    fp32 reference computes them (from the fp32 labels and draws) -- with the
+    bilinear weights, the sampling and everything after it in the batch's
+    dtype: the accuracy yardstick of an implementation that reproduces the
+    reference's fp32 sample points (the HIP default, po_patch_params
+    geometry 1/2)."""
     adv = median_pool7(adv_patch.unsqueeze(0))                    # 531-532
     P = adv.size(-1)
     pad = (img_size - P) / 2                                     # 534
@@ -185,10 +187,18 @@ def patch_transformer(adv_patch, lab_batch, img_size, draws, do_rotate=True, geo
     theta[:, 1, 1] = cos / scale
     theta[:, 1, 2] = -tx * sin / scale + ty * cos / scale
     if geometry == "fp32in64":
-        # the reference's own fp32 theta and grid (same ops, fp32 inputs)
+        # the reference's own fp32 theta and grid (same ops, fp32 inputs), then the
+        # fp32 sample points grid_sample takes from it (geometry_ref.unnormalize32),
+        # handed to the float64 sampler as the float64 grid that lands on them
+        from .geometry_ref import unnormalize32
         th32, _, _ = patch_theta(lab_batch.float(), img_size, P, {k: v.float() for k, v in draws.items()},
                                  do_rotate)
-        grid = F.affine_grid(th32, adv_batch.shape, align_corners=False).to(adv_batch.dtype)
+        g32 = F.affine_grid(th32, adv_batch.shape, align_corners=False).numpy()
+        Hs, Ws = adv_batch.size(-2), adv_batch.size(-1)
+        ix = unnormalize32(g32[..., 0], Ws).astype(np.float64)
+        iy = unnormalize32(g32[..., 1], Hs).astype(np.float64)
+        grid = torch.from_numpy(np.stack([(2.0 * ix + 1.0) / Ws - 1.0, (2.0 * iy + 1.0) / Hs - 1.0], -1)).to(
+            adv_batch.dtype)
     else:
         grid = F.affine_grid(theta, adv_batch.shape, align_corners=False)  # 745
     adv_t = F.grid_sample(adv_batch, grid, align_corners=False)            # 748

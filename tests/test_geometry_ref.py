@@ -100,6 +100,29 @@ def check_grid_sample():
         assert np.array_equal(G.grid_sample32(img.numpy(), grid.numpy()), out), S
 
 
+def check_sqrt_period():
+    """torch.sqrt on this host (MKL VML) is a function of one period: for
+    every normal positive x = 4^k m (m in [1, 4)), sqrt(x) = 2^k sqrt(m) bit
+    for bit -- what load_data.sqrt_period_table and po_patch_params' lookup
+    rely on.  Checked over 2^20 random floats spread across 2^-60 .. 2^60."""
+    g = np.random.default_rng(3)
+    bits = g.integers(0, 1 << 23, 1 << 20).astype(np.uint32) | ((g.integers(67, 187, 1 << 20).astype(np.uint32)) << 23)
+    x = bits.view(np.float32)
+    got = torch.sqrt(torch.from_numpy(x)).numpy()
+    ue = ((bits >> 23) & 0xFF).astype(np.int64) - 127
+    k = np.floor_divide(ue, 2)
+    mbits = (((ue - 2 * k) << 23) | (bits & 0x7FFFFF)).astype(np.uint32) + np.uint32(0x3F800000)
+    period = torch.sqrt(torch.from_numpy(mbits.view(np.float32))).numpy()
+    want = np.ldexp(period.astype(np.float64), k).astype(np.float32)
+    assert np.array_equal(got, want), int(np.count_nonzero(got != want))
+    cr = np.sqrt(x.astype(np.float64)).astype(np.float32)
+    print("torch.sqrt vs correctly rounded: %.2f %% differ" % (100.0 * np.mean(got != cr)))
+
+
+def test_sqrt_is_periodic_in_powers_of_4():
+    check_sqrt_period()
+
+
 def test_linspace_restatement():
     check_linspace()
 
@@ -153,4 +176,5 @@ def test_geometry_restatement_on_this_host():
     check_theta()
     check_affine_grid()
     check_grid_sample()
+    check_sqrt_period()
     test_sin_cos_are_position_independent()
