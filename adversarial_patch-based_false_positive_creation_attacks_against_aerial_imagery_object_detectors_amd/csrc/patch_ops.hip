@@ -469,6 +469,7 @@ struct WarpGeom {
   // bright + 0.1*noise before the clamp (po_augment_patch); the kernels then
   // read them instead of forming them from mp, the draws and the noise
   const float* pre;
+  po::RefAxis ax;        // the reference geometry's per-axis constants (po::ref_axis(S))
 };
 
 // The transformer noise of one image: the explicit tensor [3][P][P], or (nz
@@ -517,32 +518,37 @@ __device__ __forceinline__ void bilinear(double ix, double iy, int& x0, int& y0,
 // region [pad - 1, pad + P) -- the output is then exactly 0.  Reference form:
 // grid_sample's fp32 arithmetic (warp_geom.h; GridSamplerKernel.cpp: w = ix -
 // floor(ix), e = 1 - w, nw = s*e, ne = s*w, sw = n*e, se = n*w).
-__device__ __forceinline__ bool sample_point(const po::Geo& G, const WarpGeom& g, int i, int j, int& x0, int& y0,
-                                             float w[4]) {
-  if (G.ref) {
-    float ix, iy;
-    po::ref_sample_coord(G.th, G.ref, g.S, i, j, ix, iy);
-    if (!(ix >= (float)(g.padL - 1) && ix < (float)(g.padL + g.P) && iy >= (float)(g.padT - 1) &&
-          iy < (float)(g.padT + g.P)))
-      return false;
-    const float fx = floorf(ix), fy = floorf(iy);
-    x0 = (int)fx;
-    y0 = (int)fy;
-    const float ex = ix - fx, wx = 1.0f - ex;          // (file-wide fp contract(off))
-    const float ny = iy - fy, sy = 1.0f - ny;
-    w[0] = sy * wx;
-    w[1] = sy * ex;
-    w[2] = ny * wx;
-    w[3] = ny * ex;
-    return true;
-  }
+__device__ __forceinline__ bool sample_point_ref(const float th[6], int form, const WarpGeom& g, int i, int j,
+                                                 int& x0, int& y0, float w[4]) {
+  float ix, iy;
+  po::ref_sample_coord(th, form, g.ax, i, j, ix, iy);
+  if (!(ix >= (float)(g.padL - 1) && ix < (float)(g.padL + g.P) && iy >= (float)(g.padT - 1) &&
+        iy < (float)(g.padT + g.P)))
+    return false;
+  const float fx = floorf(ix), fy = floorf(iy);
+  x0 = (int)fx;
+  y0 = (int)fy;
+  const float ex = ix - fx, wx = 1.0f - ex;          // (file-wide fp contract(off))
+  const float ny = iy - fy, sy = 1.0f - ny;
+  w[0] = sy * wx;
+  w[1] = sy * ex;
+  w[2] = ny * wx;
+  w[3] = ny * ex;
+  return true;
+}
+__device__ __forceinline__ bool sample_point_f64(const double af[6], const WarpGeom& g, int i, int j, int& x0,
+                                                 int& y0, float w[4]) {
   double ix, iy;
-  sample_coord(G.af, i, j, ix, iy);
+  sample_coord(af, i, j, ix, iy);
   if (!(ix >= (double)(g.padL - 1) && ix < (double)(g.padL + g.P) && iy >= (double)(g.padT - 1) &&
         iy < (double)(g.padT + g.P)))
     return false;
   bilinear(ix, iy, x0, y0, w);
   return true;
+}
+__device__ __forceinline__ bool sample_point(const po::Geo& G, const WarpGeom& g, int i, int j, int& x0, int& y0,
+                                             float w[4]) {
+  return G.ref ? sample_point_ref(G.th, G.ref, g, i, j, x0, y0, w) : sample_point_f64(G.af, g, i, j, x0, y0, w);
 }
 
 __device__ __forceinline__ float aug_value(const float* __restrict__ mp, const NoiseSrc& ns,
@@ -768,39 +774,82 @@ __global__ __launch_bounds__(256) void warp_bwd_a4_k(const float* __restrict__ d
 // element-major split, to hide the candidates' dependent gfac loads (batches
 // of more than 32 images; smaller ones keep 8 groups x 32 elements, whose
 // groups all hold images).
-constexpr int WB_CH = 256;
+// Per image the table holds the scan terms (the float64 map's inverse, fp32,
+// with the window margins) and the sample-point terms: the fp32 theta of a
+// reference-form row or the float64 pixel-space map.
+//
+// One candidate path serves both forms (one compiled bilinear step keeps the
+// kernel at 94 VGPRs, 5 waves per SIMD; a per-form dispatch of the whole step
+// measured 180 against 143 us on tiny B=256, factor pass included): the
+// reference form's fp32 coordinate is widened to float64 exactly and goes
+// through the float64 form's floor and weights.  That is bit-exact for every
+// coordinate >= 1 -- floor is exact, e = x - floor(x) is exact in fp32 and in
+// float64, 1 - e is exact in fp32 (e is a multiple of ulp(x) >= 2^-23), and a
+// product of two fp32 values is exact in float64, so rounding it once to fp32
+// is the fp32 product -- and phase B only meets coordinates >= pad - 1 (the
+// corner it serves lies in the padded patch region), so launches with pad >= 2
+// use it (EXACTD); others compute the reference form's weights in fp32.
+constexpr int WB_CH = 256;     // images per LDS table chunk (WB_CH x 96 B)
 struct WarpInv {
-  po::Geo G;
-  float m[4], a02, a12;     // the inverse's linear part and the translation, rounded to fp32
+  float4 m;                    // the inverse's linear part m00, m01, m10, m11
+  float4 t;                    // a02, a12, and the window half-widths hj, hi
+  union {
+    double af[6];              // form 0: the float64 pixel-space map
+    float th[6];               // forms 1, 2: the fp32 theta
+  };
   float cb, bb;
+  int form;
 };
-// image b's geometry, its pixel-space map's inverse linear part, contrast, brightness
+// image b's scan and sample-point terms, contrast, brightness
 __device__ __forceinline__ WarpInv make_inv(const double* row, int S, float cb, float bb) {
   WarpInv w;
-  w.G = po::load_geo(row, S);
-  const double* a = w.G.af;
+  const po::Geo G = po::load_geo(row, S);
+  const double* a = G.af;
   const double det = a[0] * a[4] - a[1] * a[3];
   const double inv = 1.0 / det;
-  w.m[0] = (float)(a[4] * inv);
-  w.m[1] = (float)(-a[1] * inv);
-  w.m[2] = (float)(-a[3] * inv);
-  w.m[3] = (float)(a[0] * inv);
-  w.a02 = (float)a[2];
-  w.a12 = (float)a[5];
+  const float m00 = (float)(a[4] * inv), m01 = (float)(-a[1] * inv);
+  const float m10 = (float)(-a[3] * inv), m11 = (float)(a[0] * inv);
+  // window half-widths: the preimage of the corner square, widened by the
+  // scan's own fp32 rounding (1e-3 px covers |error| < 1e-4 px at these sizes)
+  // and, for the reference forms, by the distance d of the fp32 sample points
+  // from the float64 map: a candidate's exact sample point lies within 1 + d of
+  // (c, r), d <= (S/2) u (6 (|t0| + |t1|) + 4 |t2| + 1) + u (S + 1) (u = 2^-24:
+  // the base, product, sum and fma roundings of ref_sample_coord), taken twice
+  float grow = 1.0f;
+  if (G.ref) {
+    const double u = 0x1p-24, hS = 0.5 * S;
+    double t[6];
+#pragma unroll
+    for (int k = 0; k < 6; ++k) t[k] = fabs((double)G.th[k]);
+    const double dx = hS * u * (6.0 * (t[0] + t[1]) + 4.0 * t[2] + 1.0) + u * (S + 1);
+    const double dy = hS * u * (6.0 * (t[3] + t[4]) + 4.0 * t[5] + 1.0) + u * (S + 1);
+    grow = (float)(1.0 + 2.0 * fmax(dx, dy));
+  }
+  w.m = make_float4(m00, m01, m10, m11);
+  w.t = make_float4((float)a[2], (float)a[5], (fabsf(m00) + fabsf(m01)) * grow + 1e-3f,
+                    (fabsf(m10) + fabsf(m11)) * grow + 1e-3f);
+  w.form = G.ref;
+  if (G.ref) {
+#pragma unroll
+    for (int k = 0; k < 6; ++k) w.th[k] = G.th[k];
+  } else {
+#pragma unroll
+    for (int k = 0; k < 6; ++k) w.af[k] = G.af[k];
+  }
   w.cb = cb;
   w.bb = bb;
   return w;
 }
+
 // IL: gfac interleaved [B][S][S][4] (the footprint-box forms: one 16-byte load
-// per candidate pixel instead of one 4-byte load from each of three planes)
-template <int WB_EL, int WB_G, bool IL>
-__global__ __launch_bounds__(256) void warp_bwd_b_k(const float* __restrict__ gfac,
-                                                    const float* __restrict__ mp,
+// per candidate pixel instead of one 4-byte load from each of three planes).
+template <int WB_EL, int WB_G, bool IL, bool EXACTD>
+__global__ __launch_bounds__(256) void warp_bwd_b_k(const float* __restrict__ gfac, const float* __restrict__ mp,
                                                     const float* __restrict__ noise,
                                                     const float* __restrict__ contrast,
                                                     const float* __restrict__ bright,
-                                                    const double* __restrict__ affine, WarpGeom g,
-                                                    int B, float* __restrict__ d_mp, int xr) {
+                                                    const double* __restrict__ affine, WarpGeom g, int B,
+                                                    float* __restrict__ d_mp, int xr) {
   __shared__ float part[3][WB_G][WB_EL];
   __shared__ WarpInv tab[WB_CH];
   const int el = threadIdx.x % WB_EL, q = threadIdx.x / WB_EL;
@@ -832,25 +881,20 @@ __global__ __launch_bounds__(256) void warp_bwd_b_k(const float* __restrict__ gf
     __syncthreads();
     for (int bl = q; bl < (live ? nb : 0); bl += WB_G) {
       const int b = bc + bl;
-      const po::Geo& G = tab[bl].G;
       // output pixels whose sample point can have (r, c) as a bilinear corner:
       // the preimage of (c-1, c+1) x (r-1, r+1) under the pixel-space affine,
-      // evaluated in fp32 with a margin that covers that evaluation's rounding
-      // (|error| < 1e-4 px at these sizes) and, for the reference form, the
-      // distance of the fp32 sample points from the float64 map (well under
-      // 0.01 px): a wider scan only tests more pixels, each with the exact
-      // sample point below, so the candidates and their order are unchanged
-      const float X = (float)c - tab[bl].a02, Y = (float)r - tab[bl].a12;
-      const float m00 = tab[bl].m[0], m01 = tab[bl].m[1], m10 = tab[bl].m[2], m11 = tab[bl].m[3];
-      const float jc = m00 * X + m01 * Y, ic = m10 * X + m11 * Y;
-      const float eps = G.ref ? 0.05f : 1e-3f;
-      const float hj = fabsf(m00) + fabsf(m01) + eps, hi_ = fabsf(m10) + fabsf(m11) + eps;
-      const float jl = fmaxf(ceilf(jc - hj), 0.f), jh = fminf(floorf(jc + hj), (float)(g.S - 1));
-      const float il = fmaxf(ceilf(ic - hi_), 0.f), ih = fminf(floorf(ic + hi_), (float)(g.S - 1));
+      // evaluated in fp32 with make_inv's margins: a wider scan only tests more
+      // pixels, each with its exact sample point, so the candidates and their
+      // order are unchanged
+      const float4 m = tab[bl].m, tw = tab[bl].t;
+      const float X = (float)c - tw.x, Y = (float)r - tw.y;
+      const float jc = m.x * X + m.y * Y, ic = m.z * X + m.w * Y;
+      const float jl = fmaxf(ceilf(jc - tw.z), 0.f), jh = fminf(floorf(jc + tw.z), (float)(g.S - 1));
+      const float il = fmaxf(ceilf(ic - tw.w), 0.f), ih = fminf(floorf(ic + tw.w), (float)(g.S - 1));
       if (!(jl <= jh && il <= ih)) continue;                 // no pixel of the frame (or a NaN map)
       const int j0 = (int)jl, j1 = (int)jh, i0 = (int)il, i1 = (int)ih;
-      const float cb = tab[bl].cb, bb = tab[bl].bb;
-      const NoiseSrc nz = noise_src(noise, g, b);
+      const WarpInv& w = tab[bl];
+      const int form = w.form;
       float a0 = 0.f, a1 = 0.f, a2 = 0.f;
       bool cand = false;
       const float* gb = gfac + (size_t)b * (IL ? 4 : 3) * plane;
@@ -858,10 +902,23 @@ __global__ __launch_bounds__(256) void warp_bwd_b_k(const float* __restrict__ gf
         for (int j = j0; j <= j1; ++j) {
           int x0, y0;
           float wb[4];
-          if (!sample_point(G, g, i, j, x0, y0, wb)) continue;
+          if (EXACTD || !form) {
+            double ix, iy;
+            if (form) {
+              float fx, fy;
+              po::ref_sample_coord(w.th, form, g.ax, i, j, fx, fy);
+              ix = fx;
+              iy = fy;
+            } else {
+              sample_coord(w.af, i, j, ix, iy);
+            }
+            bilinear(ix, iy, x0, y0, wb);
+          } else if (!sample_point_ref(w.th, form, g, i, j, x0, y0, wb)) {
+            continue;
+          }
           const int dx = c - x0, dy = r - y0;
           if (dx < 0 || dx > 1 || dy < 0 || dy > 1) continue;
-          const float w = wb[2 * dy + dx];
+          const float wt = wb[2 * dy + dx];
           const size_t o = (size_t)i * g.S + j;
           float gv[3];
           if constexpr (IL) {
@@ -874,9 +931,9 @@ __global__ __launch_bounds__(256) void warp_bwd_b_k(const float* __restrict__ gf
             gv[1] = gb[o + plane];
             gv[2] = gb[o + 2 * plane];
           }
-          a0 += w * gv[0];
-          a1 += w * gv[1];
-          a2 += w * gv[2];
+          a0 += wt * gv[0];
+          a1 += wt * gv[1];
+          a2 += wt * gv[2];
           cand = true;
         }
       // no output pixel of this image has (r, c) as a corner: its term is +0
@@ -884,6 +941,8 @@ __global__ __launch_bounds__(256) void warp_bwd_b_k(const float* __restrict__ gf
       // +0 and so is never -0), so the image is skipped exactly -- and with it
       // the pre-augmented value (keyed: a Philox call) the clamp test needs
       if (!cand) continue;
+      const float cb = w.cb, bb = w.bb;
+      const NoiseSrc nz = noise_src(noise, g, b);
       // through clamp(adv*contrast + bright + noise) and * contrast, summed over images
       const float av[3] = {a0, a1, a2};
       float dd[3];
@@ -925,6 +984,27 @@ __global__ __launch_bounds__(256) void warp_bwd_b_k(const float* __restrict__ gf
   }
 }
 
+template <bool EXACTD>
+void launch_bwd_b_x(const float* gfac, const float* mp, const float* noise, const float* contrast,
+                    const float* bright, const double* affine, const WarpGeom& g, int B, int P, float* d_mp,
+                    hipStream_t st, bool il, int xr) {
+  if (B > 32) {
+    if (il)
+      hipLaunchKernelGGL((warp_bwd_b_k<8, 32, true, EXACTD>), dim3(po::ceil_div(P * P, 8)), dim3(256), 0, st, gfac,
+                         mp, noise, contrast, bright, affine, g, B, d_mp, xr);
+    else
+      hipLaunchKernelGGL((warp_bwd_b_k<8, 32, false, EXACTD>), dim3(po::ceil_div(P * P, 8)), dim3(256), 0, st, gfac,
+                         mp, noise, contrast, bright, affine, g, B, d_mp, xr);
+  } else {
+    if (il)
+      hipLaunchKernelGGL((warp_bwd_b_k<32, 8, true, EXACTD>), dim3(po::ceil_div(P * P, 32)), dim3(256), 0, st, gfac,
+                         mp, noise, contrast, bright, affine, g, B, d_mp, xr);
+    else
+      hipLaunchKernelGGL((warp_bwd_b_k<32, 8, false, EXACTD>), dim3(po::ceil_div(P * P, 32)), dim3(256), 0, st,
+                         gfac, mp, noise, contrast, bright, affine, g, B, d_mp, xr);
+  }
+}
+
 void launch_bwd_b(const float* gfac, const float* mp, const float* noise, const float* contrast, const float* bright,
                   const double* affine, const WarpGeom& g, int B, int P, float* d_mp, hipStream_t st,
                   bool il = false) {
@@ -932,21 +1012,10 @@ void launch_bwd_b(const float* gfac, const float* mp, const float* noise, const 
     const char* e = getenv("ADVPATCH_WARP_XCD");
     return (e && e[0] == '0') ? 0 : 1;
   }();
-  if (B > 32) {
-    if (il)
-      hipLaunchKernelGGL((warp_bwd_b_k<8, 32, true>), dim3(po::ceil_div(P * P, 8)), dim3(256), 0, st, gfac, mp, noise,
-                         contrast, bright, affine, g, B, d_mp, xr);
-    else
-      hipLaunchKernelGGL((warp_bwd_b_k<8, 32, false>), dim3(po::ceil_div(P * P, 8)), dim3(256), 0, st, gfac, mp,
-                         noise, contrast, bright, affine, g, B, d_mp, xr);
-  } else {
-    if (il)
-      hipLaunchKernelGGL((warp_bwd_b_k<32, 8, true>), dim3(po::ceil_div(P * P, 32)), dim3(256), 0, st, gfac, mp,
-                         noise, contrast, bright, affine, g, B, d_mp, xr);
-    else
-      hipLaunchKernelGGL((warp_bwd_b_k<32, 8, false>), dim3(po::ceil_div(P * P, 32)), dim3(256), 0, st, gfac, mp,
-                         noise, contrast, bright, affine, g, B, d_mp, xr);
-  }
+  if (g.padL >= 2 && g.padT >= 2)
+    launch_bwd_b_x<true>(gfac, mp, noise, contrast, bright, affine, g, B, P, d_mp, st, il, xr);
+  else
+    launch_bwd_b_x<false>(gfac, mp, noise, contrast, bright, affine, g, B, P, d_mp, st, il, xr);
 }
 
 // L patches per image composited in slot order (PatchApplier, load_data.py:
@@ -1006,6 +1075,7 @@ WarpGeom make_geom(int S, int P, uint64_t seed = 0, uint64_t counter = 0, int b0
   const double pad = (S - P) / 2.0;      // load_data.py:534
   g.padL = (int)(pad + 0.5);            // ConstantPad2d((int(pad+.5), int(pad), int(pad+.5), int(pad)))
   g.padT = (int)(pad + 0.5);
+  g.ax = po::ref_axis(S);
   return g;
 }
 }  // namespace
@@ -1147,72 +1217,7 @@ __global__ __launch_bounds__(256) void warp_quad_copy_k(const float* __restrict_
   }
 }
 
-// The box kernels over one flat list of the batch's box pixels: the per-image
-// grid (box_blocks(S) workgroups per image) dispatches every workgroup of an
-// image whose box is a few percent of the frame, and most of them find no
-// pixel (tiny B=256: 56 of 85 per image, ~14k empty workgroups per launch).
-// Here a fixed grid walks the concatenated boxes: each workgroup tabulates the
-// boxes' areas and their exclusive prefix in LDS (FLAT_MAXB images at most),
-// and pixel q of the list is pixel q - pre[b] of the image b with pre[b] <= q
-// < pre[b + 1] (binary search), row-major in that box as before -- the same
-// pixels with the same per-pixel arithmetic, so the same bits.
-constexpr int FLAT_MAXB = 1024;
-struct FlatBoxes {
-  int pre[FLAT_MAXB + 1];   // exclusive prefix of the box areas; pre[B] = total
-  int x0[FLAT_MAXB], bw[FLAT_MAXB], y0[FLAT_MAXB];
-  int part[256];
-};
-__device__ __forceinline__ int flat_boxes(const int32_t* __restrict__ roi, int B, int S, FlatBoxes& t) {
-  const int tid = threadIdx.x;
-  const int per = (B + 255) / 256, b0 = tid * per;
-  int sum = 0;
-  for (int k = 0; k < per; ++k) {
-    const int b = b0 + k;
-    if (b < B) {
-      const QBox q = quad_box(roi, b, S);
-      const int w = q.qx1 - q.qx0;
-      t.x0[b] = q.qx0;
-      t.bw[b] = w > 0 ? w : 1;
-      t.y0[b] = q.y0;
-      sum += w * (q.y1 - q.y0);
-    }
-  }
-  t.part[tid] = sum;
-  __syncthreads();
-  for (int o = 1; o < 256; o <<= 1) {         // inclusive scan of the 256 partial sums
-    const int v = tid >= o ? t.part[tid - o] : 0;
-    __syncthreads();
-    t.part[tid] += v;
-    __syncthreads();
-  }
-  int run = t.part[tid] - sum;                 // exclusive prefix of this thread's images
-  for (int k = 0; k < per; ++k) {
-    const int b = b0 + k;
-    if (b < B) {
-      t.pre[b] = run;
-      const QBox q = quad_box(roi, b, S);
-      run += (q.qx1 - q.qx0) * (q.y1 - q.y0);
-    }
-  }
-  if (tid == 255) t.pre[B] = t.part[255];
-  __syncthreads();
-  return t.pre[B];
-}
-// pixel q of the flat list -> image b and its pixel (i, j)
-__device__ __forceinline__ void flat_pixel(const FlatBoxes& t, int B, int q, int& b, int& i, int& j) {
-  int lo = 0, hi = B;
-  while (hi - lo > 1) {
-    const int mid = (lo + hi) >> 1;
-    if (t.pre[mid] <= q) lo = mid; else hi = mid;
-  }
-  b = lo;
-  const int p = q - t.pre[b], w = t.bw[b];
-  const int r = p / w;
-  i = t.y0[b] + r;
-  j = t.x0[b] + (p - r * w);
-}
-
-// one box pixel of the forward (warp_box_fwd_k / warp_box_flat_fwd_k)
+// one box pixel of the forward
 __device__ __forceinline__ void box_fwd_pixel(const float* __restrict__ img, const float* __restrict__ mp,
                                               const po::Geo& G, const NoiseSrc& nz, float cb, float bb,
                                               const WarpGeom& g, int mode, int b, int i, int j,
@@ -1251,26 +1256,10 @@ __global__ __launch_bounds__(256) void warp_box_fwd_k(const float* __restrict__ 
   // pre-augmented values (g.pre) or mp + the draws + the keyed noise at each corner
   const float cb = g.pre ? 1.f : contrast[b], bb = g.pre ? 0.f : bright[b];
   const po::Geo G = po::load_geo(affine + 6 * b, g.S);
+  if (blockIdx.x * 256 >= area) return;                        // (uniform) no pixel of the box here
   for (int p = blockIdx.x * 256 + threadIdx.x; p < area; p += gridDim.x * 256) {
     const int r = p / bw;
     box_fwd_pixel(img, mp, G, nz, cb, bb, g, mode, b, bx.y0 + r, bx.qx0 + (p - r * bw), out, fac);
-  }
-}
-
-__global__ __launch_bounds__(256) void warp_box_flat_fwd_k(const float* __restrict__ img, const float* __restrict__ mp,
-                                                           const float* __restrict__ contrast,
-                                                           const float* __restrict__ bright,
-                                                           const double* __restrict__ affine,
-                                                           const int32_t* __restrict__ roi, int B, WarpGeom g,
-                                                           int mode, float* __restrict__ out, float* __restrict__ fac) {
-  __shared__ FlatBoxes t;
-  const int total = flat_boxes(roi, B, g.S, t);
-  for (int q = blockIdx.x * 256 + threadIdx.x; q < total; q += gridDim.x * 256) {
-    int b, i, j;
-    flat_pixel(t, B, q, b, i, j);
-    const po::Geo G = po::load_geo(affine + 6 * b, g.S);
-    const float cb = g.pre ? 1.f : contrast[b], bb = g.pre ? 0.f : bright[b];
-    box_fwd_pixel(img, mp, G, noise_src(nullptr, g, b), cb, bb, g, mode, b, i, j, out, fac);
   }
 }
 
@@ -1291,6 +1280,7 @@ __global__ __launch_bounds__(256) void warp_box_bwd_a_k(const float* __restrict_
   const NoiseSrc nz = noise_src(nullptr, g, b);
   const float cb = contrast[b], bb = g.pre ? 0.f : bright[b];
   const po::Geo G = po::load_geo(affine + 6 * b, g.S);
+  if (blockIdx.x * 256 >= area) return;                        // (uniform) no pixel of the box here
   for (int p = blockIdx.x * 256 + threadIdx.x; p < area; p += gridDim.x * 256) {
     const int r = p / bw;
     const int i = bx.y0 + r, j = bx.qx0 + (p - r * bw);
@@ -1342,31 +1332,9 @@ __global__ __launch_bounds__(256) void warp_box_bwd_fac_k(const float* __restric
   }
 }
 
-__global__ __launch_bounds__(256) void warp_box_flat_fac_k(const float* __restrict__ d_out,
-                                                           const int32_t* __restrict__ roi, int B, int S,
-                                                           float* __restrict__ fac) {
-  __shared__ FlatBoxes t;
-  const int total = flat_boxes(roi, B, S, t);
-  for (int q = blockIdx.x * 256 + threadIdx.x; q < total; q += gridDim.x * 256) {
-    int b, i, j;
-    flat_pixel(t, B, q, b, i, j);
-    box_fac_pixel(d_out, S, b, i, j, fac);
-  }
-}
-
 // workgroups per image of the box kernels: enough for a box of an eighth of the
 // frame in one pass (a larger box loops)
 __host__ inline int box_blocks(int S) { return po::ceil_div(po::ceil_div((int64_t)S * S, 8), 256); }
-// the flat-list forms (ADVPATCH_WARP_FLAT=0: the per-image grid): batches of
-// at most FLAT_MAXB images, a fixed grid of at most 1024 workgroups
-__host__ inline int flat_blocks(int B, int S) {
-  static const bool on = [] {
-    const char* e = getenv("ADVPATCH_WARP_FLAT");
-    return !(e && e[0] == '0');
-  }();
-  if (!on || B > FLAT_MAXB) return 0;
-  return (int)std::min<int64_t>(1024, (int64_t)box_blocks(S) * B);
-}
 }  // namespace
 
 extern "C" int po_augment_patch(const float* patch_mp, uint64_t seed, uint64_t counter, int b0, const float* contrast,
@@ -1393,12 +1361,8 @@ extern "C" int po_warp_fwd_pre(const float* img, const float* pre, const double*
   hipStream_t st = po::stream_of(s);
   hipLaunchKernelGGL(warp_quad_copy_k, dim3(po::ceil_div(S * (S / 4), 256), B), dim3(256), 0, st, img, roi, S, mode,
                      out);
-  if (const int nf = flat_blocks(B, S))
-    hipLaunchKernelGGL(warp_box_flat_fwd_k, dim3(nf), dim3(256), 0, st, img, nullptr, nullptr, nullptr, affine, roi, B,
-                       g, mode, out, nullptr);
-  else
-    hipLaunchKernelGGL(warp_box_fwd_k, dim3(box_blocks(S), B), dim3(256), 0, st, img, nullptr, nullptr, nullptr,
-                       affine, roi, g, mode, out, nullptr);
+  hipLaunchKernelGGL(warp_box_fwd_k, dim3(box_blocks(S), B), dim3(256), 0, st, img, nullptr, nullptr, nullptr, affine,
+                     roi, g, mode, out, nullptr);
   return po::check_launch("po_warp_fwd_pre");
 }
 
@@ -1416,12 +1380,8 @@ static int box_fwd_keyed(const float* img, const float* patch_mp, uint64_t seed,
   if (fill)
     hipLaunchKernelGGL(warp_quad_copy_k, dim3(po::ceil_div(S * (S / 4), 256), B), dim3(256), 0, st, img, roi, S, mode,
                        out);
-  if (const int nf = flat_blocks(B, S))
-    hipLaunchKernelGGL(warp_box_flat_fwd_k, dim3(nf), dim3(256), 0, st, img, patch_mp, contrast, bright, affine, roi,
-                       B, g, mode, out, fac);
-  else
-    hipLaunchKernelGGL(warp_box_fwd_k, dim3(box_blocks(S), B), dim3(256), 0, st, img, patch_mp, contrast, bright,
-                       affine, roi, g, mode, out, fac);
+  hipLaunchKernelGGL(warp_box_fwd_k, dim3(box_blocks(S), B), dim3(256), 0, st, img, patch_mp, contrast, bright, affine,
+                     roi, g, mode, out, fac);
   return po::check_launch("po_warp_box_fwd_keyed");
 }
 
@@ -1495,10 +1455,7 @@ extern "C" int po_warp_box_bwd_fac(const float* d_out, const float* patch_mp, ui
   PO_REQUIRE((uintptr_t)fac % 16 == 0, "po_warp_box_bwd_fac: fac must be 16-byte aligned");
   const WarpGeom g = make_geom(S, P, seed, counter, b0);
   hipStream_t st = po::stream_of(s);
-  if (const int nf = flat_blocks(B, S))
-    hipLaunchKernelGGL(warp_box_flat_fac_k, dim3(nf), dim3(256), 0, st, d_out, roi, B, S, fac);
-  else
-    hipLaunchKernelGGL(warp_box_bwd_fac_k, dim3(box_blocks(S), B), dim3(256), 0, st, d_out, roi, S, fac);
+  hipLaunchKernelGGL(warp_box_bwd_fac_k, dim3(box_blocks(S), B), dim3(256), 0, st, d_out, roi, S, fac);
   int rc = po::check_launch("po_warp_box_bwd_fac(a)");
   if (rc) return rc;
   launch_bwd_b(fac, patch_mp, nullptr, contrast, bright, affine, g, B, P, d_patch_mp, st, true);

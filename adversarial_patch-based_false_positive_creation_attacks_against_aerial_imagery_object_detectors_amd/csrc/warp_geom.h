@@ -139,20 +139,43 @@ __device__ __forceinline__ void store_ref_row(const float th[6], int form, doubl
 // so an __fadd_rn(__fmul_rn(..)) pair may still fuse -- measured: it did in
 // one kernel and not in another) and __builtin_fmaf where the reference fuses.
 
-// affine_grid's base coordinate k of an S-point axis (align_corners=False)
-__device__ __forceinline__ float ref_base(int k, int S) {
+// affine_grid's base coordinate k of an S-point axis (align_corners=False):
+// fl(fl(lin * (S-1)) / S), lin = fma(step, k, -1) (k < S/2) or fma(-step,
+// S-1-k, 1), step = fl(2/(S-1)).  The division is formed from the correctly
+// rounded reciprocal rcp = fl(1/S) with one Markstein step, q = fl(x rcp),
+// r = fma(-q, S, x), fma(r, rcp, q), which equals fl(x / S) for every k < S
+// of every axis S <= 32768 (checked exhaustively: tests/test_geometry_ref.py,
+// oracle/geometry_ref.py base32_markstein): five operations per coordinate
+// instead of a correctly rounded division.  step and rcp are per-launch
+// constants (RefAxis, formed once on the host).
+struct RefAxis {
+  float step, rcp;
+  int S;
+};
+__host__ __device__ inline RefAxis ref_axis(int S) {
+  RefAxis a;
+  a.S = S;
+  a.step = S > 1 ? 2.0f / (float)(S - 1) : 0.0f;
+  a.rcp = 1.0f / (float)S;
+  return a;
+}
+__device__ __forceinline__ float ref_base(int k, const RefAxis& a) {
 #pragma clang fp contract(off)
-  const float step = 2.0f / (float)(S - 1);
-  const float lin = k < (S >> 1) ? __builtin_fmaf(step, (float)k, -1.0f) : __builtin_fmaf(-step, (float)(S - 1 - k), 1.0f);
-  return (lin * (float)(S - 1)) / (float)S;
+  const int S = a.S;
+  const float fS = (float)S, fS1 = (float)(S - 1);
+  const float lin = k < (S >> 1) ? __builtin_fmaf(a.step, (float)k, -1.0f) : __builtin_fmaf(-a.step, (float)(S - 1 - k), 1.0f);
+  const float x = lin * fS1;
+  if (S > 32768) return x / fS;
+  const float q = x * a.rcp;
+  return __builtin_fmaf(__builtin_fmaf(-q, fS, x), a.rcp, q);
 }
 
 // grid_sample's source coordinate (column ix, row iy) of output pixel (i, j);
 // form: the host sgemm's order of the K = 3 dot product (see above)
-__device__ __forceinline__ void ref_sample_coord(const float th[6], int form, int S, int i, int j, float& ix,
-                                                 float& iy) {
+__device__ __forceinline__ void ref_sample_coord(const float th[6], int form, const RefAxis& a, int i, int j,
+                                                 float& ix, float& iy) {
 #pragma clang fp contract(off)
-  const float bx = ref_base(j, S), by = ref_base(i, S);
+  const float bx = ref_base(j, a), by = ref_base(i, a);
   float gx, gy;
   if (form == 2) {
     gx = __builtin_fmaf(by, th[1], bx * th[0]) + th[2];
@@ -161,7 +184,7 @@ __device__ __forceinline__ void ref_sample_coord(const float th[6], int form, in
     gx = (bx * th[0] + by * th[1]) + th[2];
     gy = (bx * th[3] + by * th[4]) + th[5];
   }
-  const float half = (float)S * 0.5f;
+  const float half = (float)a.S * 0.5f;
   ix = __builtin_fmaf(gx + 1.0f, half, -0.5f);
   iy = __builtin_fmaf(gy + 1.0f, half, -0.5f);
 }

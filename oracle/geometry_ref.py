@@ -81,6 +81,19 @@ def base32(S):
     return ((linspace32(S) * f32(S - 1)).astype(f32) / f32(S)).astype(f32)
 
 
+def base32_markstein(S):
+    """base32 as the HIP kernels form it (warp_geom.h ref_base): the division
+    by S replaced by the correctly rounded reciprocal rcp = fl(1/S) and one
+    Markstein step, q = fl(x rcp), fl(fma(fma(-q, S, x), rcp, q)).  Equal to
+    base32 bit for bit for every S <= 32768 (tests/test_geometry_ref.py)."""
+    if S <= 1:
+        return np.zeros(max(S, 1), dtype=f32)
+    x = (linspace32(S) * f32(S - 1)).astype(f32)
+    rcp = f32(f32(1.0) / f32(S))
+    q = (x * rcp).astype(f32)
+    return fma32(fma32(-q, f32(S), x), rcp, q)
+
+
 BMM_FORMS = ("sum", "fma")          # HIP geometry 1, 2
 
 

@@ -59,6 +59,16 @@ def check_linspace():
         assert np.array_equal(G.linspace32(S), torch.linspace(-1, 1, S).numpy()), S
 
 
+def test_base_division_by_reciprocal_is_exact():
+    """The HIP kernels' base coordinate (reciprocal + one Markstein step,
+    warp_geom.h ref_base) equals affine_grid's correctly rounded division on
+    every axis length up to 2048 and on a spread of lengths up to 32768 (the
+    build container's C check covered all 32767 lengths)."""
+    sizes = list(range(2, 2049)) + list(range(2049, 32769, 397)) + [4096, 8192, 16384, 32767, 32768]
+    for S in sizes:
+        assert np.array_equal(G.base32_markstein(S), G.base32(S)), S
+
+
 def check_theta(B=64, S=608, P=224):
     th, ts, d, lab = _placements(B, S, P, 5)
     sel = oracle.lab_transform(lab)

@@ -522,3 +522,76 @@ def test_median7_network_matches_counting_kernel(kind):
     assert torch.equal(a7, ag)
     assert torch.equal(y7.nan_to_num(5.0), yg.nan_to_num(5.0))
     assert torch.equal(torch.signbit(y7), torch.signbit(yg))
+
+
+def test_no_grad_forward_skips_the_factor_buffer(monkeypatch):
+    """A warp forward that no backward can follow (torch.no_grad(), or a patch
+    that does not require grad) runs po_warp_box_fwd_keyed and allocates no
+    [B,S,S,4] factor buffer; a training forward runs po_warp_box_fwd_fac
+    (needs_input_grad is True inside Function.forward even under
+    no_grad, so the caller passes torch.is_grad_enabled())."""
+    ld, sy, nat = pkg_mod("load_data"), pkg_mod("synthetic"), pkg_mod("_native")
+    B, S, P = 3, 96, 32
+    keyed = {k: v for k, v in sy.draws_device(5, 1, 0, B, P, DEV).items() if k != "noise"}
+    keyed["noise_key"] = (5, 1, 0)
+    img, lab = sy.frames(B, S, seed=1).to(DEV), sy.labels(B, seed=2).to(DEV)
+    patch = sy.patch(P, seed=3).to(DEV).requires_grad_(True)
+    seen = []
+    real = nat.call
+    monkeypatch.setattr(nat, "call", lambda name, *a: (seen.append(name), real(name, *a))[1])
+    pt = ld.PatchTransformer()
+    with torch.no_grad():
+        pt.forward_composite(patch, lab, img, S, draws=keyed, sparse=True)
+    pt.forward_composite(patch.detach(), lab, img, S, draws=keyed, sparse=True)
+    assert "po_warp_box_fwd_fac" not in seen and seen.count("po_warp_box_fwd_keyed") == 2, seen
+    seen.clear()
+    out, _ = pt.forward_composite(patch, lab, img, S, draws=keyed, sparse=True)
+    assert "po_warp_box_fwd_fac" in seen, seen
+    out.sum().backward()
+    assert "po_warp_box_bwd_fac" in seen and bool((patch.grad != 0).any())
+
+
+@pytest.mark.parametrize("B", [5, 40])
+def test_bwd_mixed_geometry_batch(B):
+    """Phase B of the warp backward reads each image's sample-point form from
+    its affine row: a batch mixing reference-form and float64-form rows gives
+    the sum of the two single-form sub-batches' gradients (to fp32 summation
+    order: 1e-5 relative), and repeated runs give the same bits."""
+    ld, sy, nat = pkg_mod("load_data"), pkg_mod("synthetic"), pkg_mod("_native")
+    S, P = 96, 32
+    dr = sy.draws_device(7, 2, 0, B, P, DEV)
+    lab = sy.labels(B, seed=3).to(DEV)
+    mp = sy.patch(P, seed=4).to(DEV).contiguous()
+    _, _, _, roi_r, aff_r = ld.patch_params(lab, S, P, dr, True, with_roi=True, geometry="ref")
+    _, _, _, roi_f, aff_f = ld.patch_params(lab, S, P, dr, True, with_roi=True, geometry="f64")
+    pick = (torch.arange(B, device=DEV) % 2 == 0)
+    aff_m = torch.where(pick[:, None], aff_r, aff_f).contiguous()
+    roi_m = torch.where(pick[:, None], roi_r, roi_f).contiguous()
+    d_out = torch.randn(B, 3, S, S, device=DEV, generator=torch.Generator(DEV).manual_seed(1))
+    st = nat.stream()
+
+    def grad(aff, roi, keep):
+        d = d_out * keep[:, None, None, None]
+        out = torch.empty(B, 3, S, S, device=DEV)
+        fac = torch.empty(B * S * S * 4, device=DEV)
+        d_mp = torch.full((3, P, P), float("nan"), device=DEV)
+        key = (7, 2, 0)
+        nat.call("po_warp_box_fwd_fac", nat.ptr(torch.zeros(B, 3, S, S, device=DEV)), nat.ptr(mp), *key,
+                 nat.ptr(dr["contrast"]), nat.ptr(dr["bright"]), nat.ptr(aff, torch.float64),
+                 nat.ptr(roi, torch.int32), B, S, P, 1, 1, nat.ptr(out), nat.ptr(fac), st)
+        nat.call("po_warp_box_bwd_fac", nat.ptr(d.contiguous()), nat.ptr(mp), *key, nat.ptr(dr["contrast"]),
+                 nat.ptr(dr["bright"]), nat.ptr(aff, torch.float64), nat.ptr(roi, torch.int32), B, S, P,
+                 nat.ptr(fac), nat.ptr(d_mp), st)
+        torch.cuda.synchronize()
+        return d_mp
+
+    ones = torch.ones(B, device=DEV)
+    g_mixed = grad(aff_m, roi_m, ones)
+    g_ref_part = grad(aff_r, roi_r, pick.float())
+    g_f64_part = grad(aff_f, roi_f, (~pick).float())
+    assert torch.isfinite(g_mixed).all()
+    want = g_ref_part + g_f64_part
+    assert torch.allclose(g_mixed, want, rtol=1e-5, atol=1e-6 * float(want.abs().max())), \
+        float((g_mixed - want).abs().max())
+    # repeatable bits
+    assert torch.equal(grad(aff_r, roi_r, ones), grad(aff_r, roi_r, ones))
