@@ -14,7 +14,7 @@ LIB_PATH = os.environ.get("ADVPATCH_LIB") or os.path.join(_HERE, "libadvpatch_hi
 
 c_int, c_float, c_int64, c_void_p = ctypes.c_int, ctypes.c_float, ctypes.c_int64, ctypes.c_void_p
 
-PO_ABI_VERSION = 27   # include/advpatch.h
+PO_ABI_VERSION = 28   # include/advpatch.h
 PO_CONV_NTILES = 72   # include/advpatch.h
 PO_AMAX_SUB = 64      # sub-slots per max|x| slot
 
@@ -30,7 +30,8 @@ class po_conv_desc(ctypes.Structure):
         ("sum_amax", c_void_p), ("y2_amax", c_void_p), ("ybits", c_void_p), ("mbits", c_void_p),
         ("m2bits", c_void_p), ("gbox", c_void_p), ("Wfrag", c_void_p), ("Wwino", c_void_p), ("mrows", c_int),
         ("pool_y", c_void_p), ("pool_argmax", c_void_p),
-        ("Wwino6", c_void_p), ("winov", c_void_p), ("winov_floats", c_int64)]
+        ("Wwino6", c_void_p), ("winov", c_void_p), ("winov_floats", c_int64),
+        ("tile_ctr", c_void_p), ("tile_ctr_n", c_int)]
 
 
 _SIGS = {

@@ -29,6 +29,8 @@ struct ConvArgs {
   const int32_t* gbox;          // optional per-image boxes [B][4] (r0, c0, r1, c1) of the destination:
                                 // only grid points whose output pixel lies in the box are computed
   float* ws;                    // split-K partials [ksplit][M][N] (ksplit > 1)
+  int32_t* tile_ctr;            // split-K arrival counters per output tile (conv_k's in-launch reduction; NULL: none)
+  int tile_ctr_n;
   const uint32_t* in_amax;      // prec 1: max|in| slot (float bits)
   uint32_t* y_amax;             // optional max|output| slots
   uint32_t* sum_amax;

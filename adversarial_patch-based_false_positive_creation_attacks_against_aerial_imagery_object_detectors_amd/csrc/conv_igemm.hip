@@ -28,6 +28,144 @@ __device__ __forceinline__ void lds_dma16(__amdgpu_buffer_rsrc_t rs, float* lds,
   __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (__attribute__((address_space(3))) void*)lds, 16, voff, 0, 0, 0);
 }
 
+// Split-K reduction + epilogue: one item = 8 output channels of a row.
+// The slices are summed in split order (deterministic); an item's loads are
+// issued two slices (four 16-byte reads) at a time instead of one dependent
+// read per slice.  Every epilogue operand is moved as one 16-byte vector (o
+// is a multiple of 4 floats).  32-bit indices: the host checks M * N < 2^31.
+// Two forms run the same item code, so their results are bit-identical:
+// conv_reduce_k (a kernel of its own, one thread per item) and the in-launch
+// reduction of conv_k (the last-arriving slice of a tile, reduce_tile).
+__device__ __forceinline__ float4 ld4(const float* p) { return *reinterpret_cast<const float4*>(p); }
+__device__ __forceinline__ void st4(float* p, float x, float y, float z, float w) {
+  *reinterpret_cast<float4*>(p) = make_float4(x, y, z, w);
+}
+__device__ __forceinline__ void add4(float4& v, const float4 p) { v.x += p.x; v.y += p.y; v.z += p.z; v.w += p.w; }
+
+// RQ channel quads (8 channels) per item: twice the slice loads in flight.
+constexpr int RQ = 2;
+
+struct RedItem {
+  uint32_t nib;     // sign bits of the item's y values (bit 4q + c)
+  size_t pix;       // destination pixel
+  bool live;
+};
+
+// Row m, channels n0 .. n0 + 4*RQ - 1 (in_range: m < M and n0 < N): sums the
+// ksplit partials in split order and applies the epilogue; max|.| of the
+// written values into my / ms / my2.
+__device__ __forceinline__ RedItem reduce_item(const ConvArgs& a, int m, int n0, bool in_range, int sh, float& my,
+                                               float& ms, float& my2) {
+  int b, i, j;
+  RedItem r{0u, 0, false};
+  r.live = in_range && po::grid_point(a, m, b, i, j);
+  if (!r.live) return r;
+  r.pix = (size_t)(b * a.Hout + i * a.out_step + a.out_oy) * a.Wout + j * a.out_step + a.out_ox;
+  const size_t slice = (size_t)a.M * a.N;
+  const float* wp = a.ws + (size_t)m * a.N + n0;
+  float4 v[RQ];
+#pragma unroll
+  for (int q = 0; q < RQ; ++q) v[q] = ld4(wp + 4 * q);
+  int s = 1;
+  for (; s + 1 < a.ksplit; s += 2) {
+    float4 p0[RQ], p1[RQ];
+#pragma unroll
+    for (int q = 0; q < RQ; ++q) {
+      p0[q] = ld4(wp + s * slice + 4 * q);
+      p1[q] = ld4(wp + (s + 1) * slice + 4 * q);
+    }
+#pragma unroll
+    for (int q = 0; q < RQ; ++q) { add4(v[q], p0[q]); add4(v[q], p1[q]); }
+  }
+  for (; s < a.ksplit; ++s)
+#pragma unroll
+    for (int q = 0; q < RQ; ++q) add4(v[q], ld4(wp + s * slice + 4 * q));
+  const size_t pix = r.pix;
+  const size_t wo = pix * (size_t)(a.Cout_p >> 5) + (n0 >> 5);
+  const uint32_t w1 = a.mbits ? a.mbits[wo] : 0u, w2 = a.m2bits ? a.m2bits[wo] : 0u;
+#pragma unroll
+  for (int q = 0; q < RQ; ++q) {
+    const int n = n0 + 4 * q;
+    const size_t o = pix * a.Cout_p + n;
+    const float rv[4] = {v[q].x, v[q].y, v[q].z, v[q].w};
+    const float4 g1 = po::leaky_grad_bits(w1, n);
+    const float4 g2 = po::leaky_grad_bits(w2, n);
+    const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
+    const float4 yin = a.accumulate ? ld4(a.y + o) : z4;
+    const float4 mk = (!a.mbits && a.mask) ? ld4(a.mask + o) : z4;
+    const float4 rs = a.res ? ld4(a.res + o) : z4;
+    const float4 mk2 = (a.y2 && !a.m2bits) ? ld4(a.mask2 + o) : z4;
+    const float4 bs = a.bias ? ld4(a.bias + n) : z4;
+    const float g1v[4] = {g1.x, g1.y, g1.z, g1.w}, g2v[4] = {g2.x, g2.y, g2.z, g2.w};
+    const float yiv[4] = {yin.x, yin.y, yin.z, yin.w}, mkv[4] = {mk.x, mk.y, mk.z, mk.w};
+    const float rsv[4] = {rs.x, rs.y, rs.z, rs.w}, mk2v[4] = {mk2.x, mk2.y, mk2.z, mk2.w};
+    const float bsv[4] = {bs.x, bs.y, bs.z, bs.w};
+    float yo[4], so[4], y2o[4];
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      float x = __builtin_ldexpf(rv[c], -sh) + bsv[c];
+      x = po::leaky_or_id(x, po::act_slope(a.act));
+      if (a.accumulate) x += yiv[c];
+      const float yv = a.mbits ? x * g1v[c] : (a.mask ? x * po::leaky_grad(mkv[c]) : x);
+      yo[c] = yv;
+      r.nib |= (yv > 0.f ? 1u : 0u) << (4 * q + c);
+      my = fmaxf(my, fabsf(yv));
+      so[c] = x + rsv[c];
+      if (a.res) ms = fmaxf(ms, fabsf(so[c]));
+      y2o[c] = x * (a.m2bits ? g2v[c] : po::leaky_grad(mk2v[c]));
+      if (a.y2) my2 = fmaxf(my2, fabsf(y2o[c]));
+    }
+    if (a.y) st4(a.y + o, yo[0], yo[1], yo[2], yo[3]);
+    if (a.res) st4(a.sum + o, so[0], so[1], so[2], so[3]);
+    if (a.y2) st4(a.y2 + o, y2o[0], y2o[1], y2o[2], y2o[3]);
+  }
+  return r;
+}
+
+// threads 4k .. 4k+3 hold the 32 channels of one sign-bit word (N % 32 == 0)
+__device__ __forceinline__ void reduce_bits(const ConvArgs& a, const RedItem& r, int n0) {
+  uint32_t w = r.nib << (4 * RQ * (threadIdx.x & 3));
+  w = po::or_group_down<4>(w);
+  if (r.live && (threadIdx.x & 3) == 0) a.ybits[r.pix * (a.Cout_p >> 5) + (n0 >> 5)] = w;
+}
+
+__global__ __launch_bounds__(256) void conv_reduce_k(const ConvArgs a) {
+  const int t0 = (int)blockIdx.x * 256 + (int)threadIdx.x;
+  const int n8 = a.N / (4 * RQ);                   // N % 16 == 0 (host check)
+  const int tot = a.M * n8;
+  const int t = t0 < tot ? t0 : 0;
+  const int sh = po::input_shift(a) + (a.prec == 1 ? a.w_shift : 0);
+  const int m = t / n8, n0 = (t - m * n8) * 4 * RQ;
+  float my = 0.f, ms = 0.f, my2 = 0.f;
+  const RedItem r = reduce_item(a, m, n0, t0 < tot, sh, my, ms, my2);
+  if (a.ybits) reduce_bits(a, r, n0);
+  if (a.y_amax) po::amax_commit(a.y_amax, my);
+  if (a.sum_amax) po::amax_commit(a.sum_amax, ms);
+  if (a.y2_amax) po::amax_commit(a.y2_amax, my2);
+}
+
+// The in-launch reduction of one BM x BN output tile (conv_k, prec 0), run by
+// the tile's last-arriving slice: items row-major over the tile, 256 threads
+// per pass (BM * BN / 8 is a multiple of 256 for every generic tile, so all
+// lanes take every pass and the sign-bit groups stay whole).
+template <int BM, int BN>
+__device__ __forceinline__ void reduce_tile(const ConvArgs& a, int m0, int n0) {
+  constexpr int C8 = BN / (4 * RQ);
+  constexpr int ITEMS = BM * C8;
+  static_assert(ITEMS % 256 == 0 && C8 % 4 == 0, "reduce_tile: whole passes and sign-bit groups");
+  float my = 0.f, ms = 0.f, my2 = 0.f;
+#pragma unroll 1
+  for (int it = (int)threadIdx.x; it < ITEMS; it += 256) {
+    const int r = it / C8, c = it - r * C8;
+    const int m = m0 + r, n = n0 + c * 4 * RQ;
+    const RedItem ri = reduce_item(a, m, n, m < a.M && n < a.N, 0, my, ms, my2);
+    if (a.ybits) reduce_bits(a, ri, n);
+  }
+  if (a.y_amax) po::amax_commit(a.y_amax, my);
+  if (a.sum_amax) po::amax_commit(a.sum_amax, ms);
+  if (a.y2_amax) po::amax_commit(a.y2_amax, my2);
+}
+
 template <int BM, int BN, int WM, int BK, bool GL>
 __global__ __launch_bounds__(256) void conv_k(const ConvArgs a) {
   constexpr int WN = 4 / WM;
@@ -235,106 +373,33 @@ __global__ __launch_bounds__(256) void conv_k(const ConvArgs a) {
 
   if (a.ksplit > 1) {
     po::store_partials<TM, TN>(a, acc, m0, n0, wm, wn, lane);
+    if (!a.tile_ctr) return;                   // the separate reduction kernel follows
+    // In-launch reduction (cdna_hip_programming.md, in-launch split-K): every
+    // wave drains its partial stores, lane 0 publishes them with an agent-scope
+    // release and counts the arrival on the tile's counter; the slice that
+    // arrives last acquires and reduces the tile.  Correct for any placement
+    // of the slices over XCDs/CUs.
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    int* flag = reinterpret_cast<int*>(smem);   // the k-loop buffers are free
+    if (tid == 0) {
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      const int old = __hip_atomic_fetch_add(a.tile_ctr + wgid, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const int last = old == a.ksplit - 1;
+      if (last) {
+        __hip_atomic_store(a.tile_ctr + wgid, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);   // for the next launch
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      }
+      flag[0] = last;
+    }
+    __syncthreads();
+    if (flag[0]) reduce_tile<BM, BN>(a, m0, n0);
     return;
   }
   __shared__ int dst_pix[BM];
   po::conv_epilogue<BM, TM, TN>(a, acc, smem, dst_pix, m0, n0, wm, wn, 0);
-}
-
-// Split-K reduction + epilogue: one thread per 8 output channels of a row.
-// The slices are summed in split order (deterministic); a thread's loads
-// are issued two slices (four 16-byte reads) at a time instead of one
-// dependent read per slice.  Every epilogue operand is moved
-// as one 16-byte vector (o is a multiple of 4 floats).  32-bit indices: the
-// host checks M * N < 2^31.
-__device__ __forceinline__ float4 ld4(const float* p) { return *reinterpret_cast<const float4*>(p); }
-__device__ __forceinline__ void st4(float* p, float x, float y, float z, float w) {
-  *reinterpret_cast<float4*>(p) = make_float4(x, y, z, w);
-}
-__device__ __forceinline__ void add4(float4& v, const float4 p) { v.x += p.x; v.y += p.y; v.z += p.z; v.w += p.w; }
-
-// RQ channel quads (8 channels) per thread: twice the slice loads in flight.
-constexpr int RQ = 2;
-__global__ __launch_bounds__(256) void conv_reduce_k(const ConvArgs a) {
-  const int t0 = (int)blockIdx.x * 256 + (int)threadIdx.x;
-  const int n8 = a.N / (4 * RQ);                   // N % 16 == 0 (host check)
-  const int tot = a.M * n8;
-  const int t = t0 < tot ? t0 : 0;
-  const int sh = po::input_shift(a) + (a.prec == 1 ? a.w_shift : 0);
-  const int m = t / n8, n0 = (t - m * n8) * 4 * RQ;
-  int b, i, j;
-  const bool live = t0 < tot && po::grid_point(a, m, b, i, j);
-  const size_t pix = live ? (size_t)(b * a.Hout + i * a.out_step + a.out_oy) * a.Wout + j * a.out_step + a.out_ox : 0;
-  float my = 0.f, ms = 0.f, my2 = 0.f;
-  uint32_t nib = 0;
-  if (live) {
-    const size_t slice = (size_t)a.M * a.N;
-    const float* wp = a.ws + (size_t)m * a.N + n0;
-    float4 v[RQ];
-#pragma unroll
-    for (int q = 0; q < RQ; ++q) v[q] = ld4(wp + 4 * q);
-    int s = 1;
-    for (; s + 1 < a.ksplit; s += 2) {
-      float4 p0[RQ], p1[RQ];
-#pragma unroll
-      for (int q = 0; q < RQ; ++q) {
-        p0[q] = ld4(wp + s * slice + 4 * q);
-        p1[q] = ld4(wp + (s + 1) * slice + 4 * q);
-      }
-#pragma unroll
-      for (int q = 0; q < RQ; ++q) { add4(v[q], p0[q]); add4(v[q], p1[q]); }
-    }
-    for (; s < a.ksplit; ++s)
-#pragma unroll
-      for (int q = 0; q < RQ; ++q) add4(v[q], ld4(wp + s * slice + 4 * q));
-    const size_t wo = pix * (size_t)(a.Cout_p >> 5) + (n0 >> 5);
-    const uint32_t w1 = a.mbits ? a.mbits[wo] : 0u, w2 = a.m2bits ? a.m2bits[wo] : 0u;
-#pragma unroll
-    for (int q = 0; q < RQ; ++q) {
-      const int n = n0 + 4 * q;
-      const size_t o = pix * a.Cout_p + n;
-      const float r[4] = {v[q].x, v[q].y, v[q].z, v[q].w};
-      const float4 g1 = po::leaky_grad_bits(w1, n);
-      const float4 g2 = po::leaky_grad_bits(w2, n);
-      const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
-      const float4 yin = a.accumulate ? ld4(a.y + o) : z4;
-      const float4 mk = (!a.mbits && a.mask) ? ld4(a.mask + o) : z4;
-      const float4 rs = a.res ? ld4(a.res + o) : z4;
-      const float4 mk2 = (a.y2 && !a.m2bits) ? ld4(a.mask2 + o) : z4;
-      const float4 bs = a.bias ? ld4(a.bias + n) : z4;
-      const float g1v[4] = {g1.x, g1.y, g1.z, g1.w}, g2v[4] = {g2.x, g2.y, g2.z, g2.w};
-      const float yiv[4] = {yin.x, yin.y, yin.z, yin.w}, mkv[4] = {mk.x, mk.y, mk.z, mk.w};
-      const float rsv[4] = {rs.x, rs.y, rs.z, rs.w}, mk2v[4] = {mk2.x, mk2.y, mk2.z, mk2.w};
-      const float bsv[4] = {bs.x, bs.y, bs.z, bs.w};
-      float yo[4], so[4], y2o[4];
-#pragma unroll
-      for (int c = 0; c < 4; ++c) {
-        float x = __builtin_ldexpf(r[c], -sh) + bsv[c];
-        x = po::leaky_or_id(x, po::act_slope(a.act));
-        if (a.accumulate) x += yiv[c];
-        const float yv = a.mbits ? x * g1v[c] : (a.mask ? x * po::leaky_grad(mkv[c]) : x);
-        yo[c] = yv;
-        nib |= (yv > 0.f ? 1u : 0u) << (4 * q + c);
-        my = fmaxf(my, fabsf(yv));
-        so[c] = x + rsv[c];
-        if (a.res) ms = fmaxf(ms, fabsf(so[c]));
-        y2o[c] = x * (a.m2bits ? g2v[c] : po::leaky_grad(mk2v[c]));
-        if (a.y2) my2 = fmaxf(my2, fabsf(y2o[c]));
-      }
-      if (a.y) st4(a.y + o, yo[0], yo[1], yo[2], yo[3]);
-      if (a.res) st4(a.sum + o, so[0], so[1], so[2], so[3]);
-      if (a.y2) st4(a.y2 + o, y2o[0], y2o[1], y2o[2], y2o[3]);
-    }
-  }
-  if (a.ybits) {
-    // threads 4k .. 4k+3 hold the 32 channels of one sign-bit word (N % 32 == 0)
-    uint32_t w = nib << (4 * RQ * (threadIdx.x & 3));
-    w = po::or_group_down<4>(w);
-    if (live && (threadIdx.x & 3) == 0) a.ybits[pix * (a.Cout_p >> 5) + (n0 >> 5)] = w;
-  }
-  if (a.y_amax) po::amax_commit(a.y_amax, my);
-  if (a.sum_amax) po::amax_commit(a.sum_amax, ms);
-  if (a.y2_amax) po::amax_commit(a.y2_amax, my2);
 }
 
 template <int BM, int BN, int WM, int BK, bool GL>
@@ -342,8 +407,11 @@ int launch(const ConvArgs& a, hipStream_t st) {
   ConvArgs b = a;
   b.ntiles_n = po::ceil_div(a.N, BN);
   const int ntiles = po::ceil_div(a.M, BM) * b.ntiles_n;
+  // the in-launch split-K reduction needs a counter per output tile
+  const bool inl = a.ksplit > 1 && a.tile_ctr && ntiles <= a.tile_ctr_n;
+  if (!inl) b.tile_ctr = nullptr;
   hipLaunchKernelGGL((conv_k<BM, BN, WM, BK, GL>), dim3(ntiles, a.ksplit), dim3(256), 0, st, b);
-  if (a.ksplit > 1) {
+  if (a.ksplit > 1 && !inl) {
     PO_REQUIRE((int64_t)a.M * a.N < (1LL << 31), "po_conv: split-K output too large");
     int rc = po::check_launch("po_conv");
     if (rc) return rc;
@@ -480,6 +548,8 @@ extern "C" int po_conv(const po_conv_desc* d, const float* in, const float* W, c
   PO_REQUIRE(!sum_out || !a.sum_amax || a.sum_amax != a.y_amax, "po_conv: y and sum share an amax slot");
   a.ksplit = d->ksplit > 1 ? d->ksplit : 1;
   a.ws = d->workspace;
+  a.tile_ctr = d->tile_ctr;
+  a.tile_ctr_n = d->tile_ctr ? d->tile_ctr_n : 0;
   PO_REQUIRE(a.ksplit <= 64 && a.ksplit <= d->ntaps * (d->Cin_p / 16), "po_conv: ksplit %d out of range", a.ksplit);
   PO_REQUIRE(a.ksplit == 1 || a.ws, "po_conv: ksplit > 1 needs a workspace");
   if (d->in_org || d->out_org)

@@ -1197,6 +1197,8 @@ class NetPlan:
         for d in self._side_descs():
             if d.ksplit > 1:
                 d.workspace = self.ws_side.data_ptr()
+                if d.tile_ctr:
+                    d.tile_ctr = self._tile_ctr(side=True).data_ptr()
         need = max([self.winov_floats(d) for d in self._side_descs() if d.tile == self.WINOV_TILE] + [0])
         if need:
             if getattr(self, "winov_side", None) is None or self.winov_side.numel() < need:
@@ -1563,12 +1565,43 @@ class NetPlan:
             self.winov = torch.empty(floats, device=self.device)
         return self.winov
 
+    TILE_CTRS = 4096              # in-launch split-K arrival counters per stream (po_conv_desc.tile_ctr)
+
+    def _tile_ctr(self, side=False):
+        """The zeroed int32 arrival counters of po_conv's in-launch split-K
+        reduction (ABI 28): one array for the main stream, one for the head-tail
+        stream (launches that may overlap need separate counters).  Every launch
+        leaves them zero."""
+        name = "_ctr_side" if side else "_ctr_main"
+        t = getattr(self, name, None)
+        if t is None:
+            t = torch.zeros(self.TILE_CTRS, dtype=torch.int32, device=self.device)
+            setattr(self, name, t)
+        return t
+
+    @staticmethod
+    def inlaunch_reduce():
+        """ADVPATCH_INLAUNCH_REDUCE=1 (opt-in): split-K launches on the generic
+        tiles reduce their slices inside the launch (the tile's last arriving
+        slice) instead of in conv_reduce_k; bit-identical.  Off by default:
+        measured slower on both bench plans (yolov3 B=16: 1000-1005 img/s
+        against 1029 with the separate reduction, tiny B=256: 41.0-41.2k
+        against 42.2-42.5k; profiles/r06/inlaunch_reduce_not_kept_ab.txt) --
+        every slice's agent-scope release writes back its XCD's L2, and one
+        workgroup reading all of a tile's slices is slower than a reduction
+        spread over the whole chip."""
+        return os.environ.get("ADVPATCH_INLAUNCH_REDUCE", "0") == "1"
+
     def _apply_ws(self, desc):
         ks = desc.ksplit
         if ks > 1:
             desc.workspace = self._ensure_ws(ks * desc.B * desc.Hg * desc.Wg * desc.N).data_ptr()
         else:
             desc.workspace = None
+        if ks > 1 and self.inlaunch_reduce():
+            desc.tile_ctr, desc.tile_ctr_n = self._tile_ctr().data_ptr(), self.TILE_CTRS
+        else:
+            desc.tile_ctr, desc.tile_ctr_n = None, 0
         if desc.tile == self.WINOV_TILE:
             n = self.winov_floats(desc)
             desc.winov, desc.winov_floats = self._ensure_winov(n).data_ptr(), n

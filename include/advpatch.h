@@ -33,7 +33,7 @@ typedef void* po_stream_t;
 #define PO_EHIP -2     /* HIP runtime error */
 #define PO_EDEVICE -3  /* device is not gfx950 */
 
-#define PO_ABI_VERSION 27
+#define PO_ABI_VERSION 28
 #define PO_AMAX_SUB 64  /* sub-slots per max|x| slot (see po_conv_desc) */
 
 int po_abi_version(void);
@@ -444,7 +444,8 @@ typedef struct po_conv_desc {
   int ksplit;                 /* <= 1: one pass over K; > 1: the k-steps are split over
                                  ksplit workgroups per tile whose partial sums (workspace,
                                  >= ksplit*M*N floats, M = B*Hg*Wg) are reduced in split
-                                 order by a second kernel that applies the epilogue */
+                                 order by a second kernel that applies the epilogue,
+                                 or inside the launch (tile_ctr below) */
   float* workspace;
   /* Operand precision.  0: exact fp32 MFMA (v_mfma_f32_32x32x2_f32); W is fp32
    * [N][ntaps][Cin_p].  1: split fp16 ("fp16x3"): every operand x is scaled by
@@ -520,6 +521,19 @@ typedef struct po_conv_desc {
    * tile 72 does not apply. */
   float* winov;
   int64_t winov_floats;
+  /* Optional (ABI 28): DEVICE int32 arrival counters, tile_ctr_n of them, all
+   * zero between launches (the caller zeroes them once; every launch leaves
+   * them zero).  With ksplit > 1 on the generic exact-fp32 tiles (1..20, 27)
+   * and at most tile_ctr_n output tiles, the split-K reduction runs inside the
+   * launch: each slice publishes its partial sums (agent-scope release, then
+   * an agent-scope arrival count on its tile's counter) and the tile's last
+   * arriving workgroup sums the slices in split order and applies the
+   * epilogue -- the same arithmetic, in the same order, as the separate
+   * reduction kernel (bit-identical), one kernel boundary fewer.  NULL (or
+   * too few counters, or other tiles): the separate reduction kernel.  Two
+   * launches that may run concurrently need separate counter arrays. */
+  int32_t* tile_ctr;
+  int tile_ctr_n;
 } po_conv_desc;
 
 #define PO_CONV_NTILES 72
