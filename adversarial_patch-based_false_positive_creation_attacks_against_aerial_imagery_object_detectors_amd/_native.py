@@ -14,8 +14,8 @@ LIB_PATH = os.environ.get("ADVPATCH_LIB") or os.path.join(_HERE, "libadvpatch_hi
 
 c_int, c_float, c_int64, c_void_p = ctypes.c_int, ctypes.c_float, ctypes.c_int64, ctypes.c_void_p
 
-PO_ABI_VERSION = 28   # include/advpatch.h
-PO_CONV_NTILES = 72   # include/advpatch.h
+PO_ABI_VERSION = 29   # include/advpatch.h
+PO_CONV_NTILES = 73   # include/advpatch.h
 PO_AMAX_SUB = 64      # sub-slots per max|x| slot
 
 

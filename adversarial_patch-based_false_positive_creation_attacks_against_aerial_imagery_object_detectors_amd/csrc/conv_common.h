@@ -404,5 +404,8 @@ int launch_wino6(const ConvArgs& a, const float* U6, hipStream_t st, float* VG =
 // tile 69 (conv_halo.hip): persistent 3x3 conv 16 -> 32 channels with the 2x2
 // max pool fused, input patches staged once per 8 x 16-pixel tile
 int launch_halo(const ConvArgs& a, hipStream_t st);
+// tile 73 (conv_wpool.hip): the Winograd F(2x2,3x3) form of tile 69 (16 -> 32 channels, 2x2 max pool
+// fused, persistent, in-register inverse transform; bit-identical to tile 61); U = po_conv_desc.Wwino
+int launch_wpool(const ConvArgs& a, const float* U, hipStream_t st);
 
 }  // namespace po

@@ -466,7 +466,9 @@ bool forced_tile(int& bm, int& bn, int& bk, int& gl) {
 // tile, BM = 128); 70, staging 15: conv_wino5_k, tile 68 as a persistent kernel
 // pipelined across its units; 71, staging 16: conv_wino6_k, Winograd F(4x4,3x3)
 // as a persistent kernel (BM counts 4x4 output tiles); 72, staging 17: tile 71
-// on an input transformed beforehand (wino6_pre_k into po_conv_desc.winov).  Retired (see retired()): 21..26, 28, 62..64.
+// on an input transformed beforehand (wino6_pre_k into po_conv_desc.winov); 73, staging 18: conv_wpool.hip,
+// tile 69's conv + pool as Winograd F(2x2,3x3) on 16x16x4 MFMAs (BM counts 2x2 tiles).  Retired (see
+// retired()): 21..26, 28, 62..64.
 constexpr int kTiles[PO_CONV_NTILES][5] = {
     {128, 128, 16, 0, 0}, {128, 128, 32, 0, 0}, {64, 128, 16, 0, 0}, {64, 128, 32, 0, 0}, {128, 64, 16, 0, 0},
     {128, 64, 32, 0, 0},  {64, 64, 16, 0, 0},   {64, 64, 32, 0, 0},  {128, 32, 16, 0, 0}, {128, 32, 32, 0, 0},
@@ -484,7 +486,7 @@ constexpr int kTiles[PO_CONV_NTILES][5] = {
     {128, 128, 16, 4, 1}, {128, 64, 16, 4, 1}, {256, 128, 16, 4, 1}, {256, 64, 16, 4, 1},
     {64, 32, 16, 5, 0}, {32, 64, 16, 5, 0}, {32, 64, 16, 6, 0}, {32, 64, 16, 7, 0}, {32, 64, 16, 8, 0},
     {32, 64, 16, 11, 0}, {64, 64, 16, 12, 0}, {64, 64, 16, 13, 0}, {128, 32, 16, 14, 0}, {64, 64, 16, 15, 0},
-    {32, 64, 16, 16, 0}, {32, 64, 16, 17, 0}};
+    {32, 64, 16, 16, 0}, {32, 64, 16, 17, 0}, {32, 32, 16, 18, 0}};
 // Tiles no tuned cache or tuner run selected over rounds 1-3 (the 256x128
 // shapes, the register-staged and BK-32 128x256 ones, the 32x64 Winograd
 // kernels before tile 65); their numbers stay reserved so cached choices keep
@@ -615,7 +617,7 @@ extern "C" int po_conv(const po_conv_desc* d, const float* in, const float* W, c
   while (bk > 16 && a.Cin_p % bk != 0) bk /= 2;
   int rc;
   PO_REQUIRE((a.mrows == a.Hg * a.Wg && !a.pool_y) || gl <= 1 ||
-                 ((gl == 5 || (gl >= 11 && gl <= 17)) && a.mrows == a.Hg * a.Wg),
+                 ((gl == 5 || (gl >= 11 && gl <= 18)) && a.mrows == a.Hg * a.Wg),
              "po_conv: a compact box grid (mrows) runs on the generic tiles only, a fused pool on those and tiles "
              "61/66/67/68/69/70");
   PO_REQUIRE(!a.pool_y || bm * bn <= 128 * 128,
@@ -632,6 +634,7 @@ extern "C" int po_conv(const po_conv_desc* d, const float* in, const float* W, c
     return rc;
   }
   if (gl == 14) return po::launch_halo(a, st);
+  if (gl == 18) return po::launch_wpool(a, d->Wwino, st);
   if (gl >= 5 && gl <= 8) return po::launch_wino(a, d->Wwino, st, bm, gl >= 6 ? 8 : 4, gl >= 7, gl == 8);
   if (gl >= 11 && gl <= 17 && gl != 14) {
     PO_REQUIRE(gl != 17 || d->winov, "po_conv: tile 72 needs the transformed-input workspace (winov)");

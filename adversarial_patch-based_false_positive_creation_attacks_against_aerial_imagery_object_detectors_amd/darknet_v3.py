@@ -579,6 +579,7 @@ class NetPlan:
     WINO_SIDE = {71: 4, 72: 4}
     WINO_COMPS = {71: 36, 72: 36}
     HALO_TILE = 69               # conv_halo_pool_k (conv_halo.hip)
+    WPOOL_TILE = 73              # conv_wpool_k (conv_wpool.hip): tile 69's launch as Winograd F(2x2,3x3)
     _tile_shapes = {}
 
     @classmethod
@@ -614,6 +615,10 @@ class NetPlan:
         if t in cls.WINO_TILES:
             WT = cls.WINO_TILES[t][0]
             return 2.0 * cls.WINO_COMPS.get(t, 16) * cls._live_tiles(desc, t, WT, cones) * WT * desc.Cin_p * desc.N
+        if t == cls.WPOOL_TILE:
+            # conv_wpool_k: 8 x 16-pixel output tiles (ragged ones padded) = 32
+            # 2x2 Winograd tiles, 16 transform-domain GEMMs over Cin_p x 32 channels
+            return 2.0 * 16 * desc.B * (-(-desc.Hg // 8)) * (-(-desc.Wg // 16)) * 32 * desc.Cin_p * 32
         if t == cls.HALO_TILE:
             # conv_halo_pool_k: 8 x 16-pixel output tiles (ragged ones padded), 32
             # channels, K = 9 taps x 16 channels (full maps only: no boxes)
@@ -1498,7 +1503,7 @@ class NetPlan:
         t = choice if isinstance(choice, int) else choice[0]
         if t in (71, self.WINOV_TILE):
             return getattr(desc, "Wwino6", None) is not None
-        if t in self.WINO_TILES:
+        if t in self.WINO_TILES or t == self.WPOOL_TILE:
             return getattr(desc, "Wwino", None) is not None
         return True
 

@@ -47,7 +47,8 @@ PEAK_CONV = {"fp32": PEAK_FP32_MFMA_TFLOPS, "fp16x3": PEAK_FP16_MFMA_TFLOPS / 3.
 TILE_KERNELS = {61: "conv_wino_k", 65: "conv_wino2_k", 66: "conv_wino3_k", 67: "conv_wino4_k",
                 68: "conv_wino4_k<stagger>", 69: "conv_halo_pool_k",
                 70: "conv_wino5_k (persistent)", 71: "conv_wino6_k (F(4x4), persistent)",
-                72: "wino6_pre_k + conv_wino6_k<PT> (F(4x4), pre-transformed input)"}
+                72: "wino6_pre_k + conv_wino6_k<PT> (F(4x4), pre-transformed input)",
+                73: "conv_wpool_k (F(2x2) + pool, persistent)"}
 
 CONFIGS = {
     # name: (cfg, S, P, default per-GPU batch)
@@ -206,7 +207,8 @@ def measure(tr, prec, patch, img, lab, B, world, rank, steps, warmup, weights):
     # per tile family: time, dense-equivalent FLOPs and the FLOPs the matrix cores execute
     fam = {}
     for e0, e1, d, c in timer:
-        key = "winograd" if d.tile in plan.WINO_TILES else ("halo" if d.tile == plan.HALO_TILE else "direct")
+        key = ("winograd" if d.tile in plan.WINO_TILES or d.tile == plan.WPOOL_TILE
+               else ("halo" if d.tile == plan.HALO_TILE else "direct"))
         f = fam.setdefault(key, {"ms": 0.0, "flops": 0.0, "mfma_flops": 0.0, "launches": 0, "tiles": {}})
         ms = e0.elapsed_time(e1)
         mf = plan.launch_mfma_flops(d, c)

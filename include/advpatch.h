@@ -33,7 +33,7 @@ typedef void* po_stream_t;
 #define PO_EHIP -2     /* HIP runtime error */
 #define PO_EDEVICE -3  /* device is not gfx950 */
 
-#define PO_ABI_VERSION 28
+#define PO_ABI_VERSION 29
 #define PO_AMAX_SUB 64  /* sub-slots per max|x| slot (see po_conv_desc) */
 
 int po_abi_version(void);
@@ -536,7 +536,7 @@ typedef struct po_conv_desc {
   int tile_ctr_n;
 } po_conv_desc;
 
-#define PO_CONV_NTILES 72
+#define PO_CONV_NTILES 73
 /* Tile `t` (1-based): block rows BM (output pixels), block columns BN (output
  * channels), k-step BK (input channels).  Tiles 1..10 stage operands through
  * registers, 11..20 are the same shapes staged by LDS-DMA, 27 a 128x256
@@ -574,6 +574,12 @@ typedef struct po_conv_desc {
  * pass into winov: the GEMM kernel then loads its A fragments like its B
  * fragments (no gathers, transform or LDS in its k-loop); the same
  * requirements as tile 71 plus winov; the same results as tile 71 bit for bit.
+ * 73 (exact fp32, ABI 29) is tile 69's launch (stride-1 3x3, Cin_p = 16, N =
+ * Cout_p = 32, pool_y, full even maps, no split-K or boxes) as Winograd
+ * F(2x2,3x3) (needs Wwino): a persistent kernel whose 2x2 output tiles are the
+ * pool windows, the component GEMMs on v_mfma_f32_16x16x4_f32 with the
+ * inverse transform, bias, LeakyReLU and pool in registers; bit-identical to
+ * tile 61 on the same launch.
  * Retired tiles (21..26, 28, 62..64: never selected by a tuner run) keep their
  * numbers; po_conv_tile_info reports them with *prec = -1 and po_conv refuses
  * them.  A tile that does not apply to a launch makes po_conv return
