@@ -328,8 +328,9 @@ def test_golden_yolov3_608_through_hip(yolo_weights):
     within the 75-layer forward bound 5e-5.  The golden cannot be
     branch-aligned to the GPU's LeakyReLU ties (a tie taken the other way
     changes a gradient path by 10x), so its gradient is compared as a whole:
-    L2 norm within 1 %, sampled elements within 5 % of the max.  Element-wise
-    gradient parity at 608 is the branch-aligned tests' job (1e-4 vs float64)."""
+    L2 norm within 0.1 %, sampled elements within 1 % of the max (round 6,
+    reference geometry: measured 0 and 3.6e-3).  Element-wise gradient parity
+    at 608 is the branch-aligned tests' job (1e-4 vs the fp32 oracle)."""
     sy = pkg_mod("synthetic")
     with np.load(os.path.join(ROOT, "tests", "golden", "golden_yolov3_608.npz"), allow_pickle=False) as z:
         want = {k: z[k] for k in z.files}
@@ -346,8 +347,11 @@ def test_golden_yolov3_608_through_hip(yolo_weights):
     np.testing.assert_allclose(t["obj"].cpu().numpy(), want["obj"], rtol=0, atol=5e-5)
     g = pg.grad.cpu().numpy().ravel()
     scale = float(want["grad_absmax"])
-    assert abs(float(np.linalg.norm(g)) - float(want["grad_l2"])) <= 1e-2 * float(want["grad_l2"])
-    assert float(np.abs(g[::37] - want["grad_sample"]).max()) <= 5e-2 * scale
+    print("golden 608: grad L2 rel diff %.3g, sampled max diff / absmax %.3g" % (
+        abs(float(np.linalg.norm(g)) - float(want["grad_l2"])) / float(want["grad_l2"]),
+        float(np.abs(g[::37] - want["grad_sample"]).max()) / scale))
+    assert abs(float(np.linalg.norm(g)) - float(want["grad_l2"])) <= 1e-3 * float(want["grad_l2"])
+    assert float(np.abs(g[::37] - want["grad_sample"]).max()) <= 1e-2 * scale
 
 
 def test_dropin_train_writes_reference_png_layout(tmp_path, capsys, monkeypatch):
