@@ -171,6 +171,7 @@ __global__ __launch_bounds__(512, 1) void conv_wino6_k(const ConvArgs a, const f
   const uint32_t npix = (uint32_t)a.B * (uint32_t)a.Hout * (uint32_t)a.Wout;
   const uint32_t dst_bytes = npix * (uint32_t)a.Cout_p * 4u;
   const uint32_t bits_bytes = npix * (uint32_t)wpp * 4u;
+  const uint32_t pool_bytes = (npix >> 2) * (uint32_t)a.Cout_p * 4u;   // EF_POOL: [B][Hout/2][Wout/2][Cout_p] floats
   const uint32_t in_bytes = (uint32_t)__builtin_amdgcn_readfirstlane(a.in_bytes);
   const __amdgpu_buffer_rsrc_t in_rs = rsrc(a.in, in_bytes);
   __amdgpu_buffer_rsrc_t rs_out = in_rs, rs_bias = in_rs;
@@ -372,6 +373,10 @@ __global__ __launch_bounds__(512, 1) void conv_wino6_k(const ConvArgs a, const f
   const int et = tid >> 8;                     // its tiles of a pass: et, et + 2, et + 4, et + 6
   constexpr bool RES = MODE == 0 && (EF & EF_RES), ACC = MODE == 0 && (EF & EF_ACC);
   constexpr bool MB = MODE == 0 && (EF & EF_MB), Y2 = MODE == 0 && (EF & EF_Y2);
+  // POOL: a 4x4 output tile holds four 2x2 pool windows; in the passes a thread
+  // owns window pw = (tid >> 4) & 3 of tile pt = tid >> 6 for the 4 channels n_loc
+  constexpr bool POOL = MODE == 0 && (EF & EF_POOL);
+  const int pw = (tid >> 4) & 3, pt = tid >> 6;
   int n4 = 0, es = 0;                          // the staged unit's channel base and split-K slice
   float4 bias4 = make_float4(0.f, 0.f, 0.f, 0.f);
   // per pass parity: pixels (MODE 1: workspace rows) of the thread's four tiles,
@@ -390,6 +395,16 @@ __global__ __launch_bounds__(512, 1) void conv_wino6_k(const ConvArgs a, const f
   auto inputs = [&](int p) {
     const int q = p & 1;
     eok[q] = 0u;
+    if constexpr (POOL) {
+      // the window's pooled pixel (full even maps, no boxes: host checks)
+      int b, ti, tj;
+      const bool tl = tile_pt6(a, Ht, Wt, cur_m0 + TP6 * p + pt, b, ti, tj);
+      const int pi = 2 * ti + (pw >> 1), pj = 2 * tj + (pw & 1);
+      const bool ok = tl && pi < (a.Hout >> 1) && pj < (a.Wout >> 1);
+      eok[q] = ok ? 1u : 0u;
+      epix[q][0] = ((uint32_t)b * (uint32_t)(a.Hout >> 1) + pi) * (uint32_t)(a.Wout >> 1) + pj;
+      return;
+    }
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
       int b, ti, tj;
@@ -421,6 +436,36 @@ __global__ __launch_bounds__(512, 1) void conv_wino6_k(const ConvArgs a, const f
   // unconditional: a masked one goes out of range)
   auto emit = [&](int p) {
     const int q = p & 1;
+    if constexpr (POOL) {
+      // window pw of tile pt: its pixels (2wy + dy, 2wx + dx), position k = 2dy + dx,
+      // bias + activation per pixel, then po_maxpool2_fwd's rule (first position on
+      // ties, NaN wins) and the slope-carrying argmax codes (conv_pool_epilogue)
+      int rrow = V6_FLOATS + q * (TP6 * 16 * N6) + (pt * 16 + 8 * (pw >> 1) + 2 * (pw & 1)) * N6 + n_loc;
+      asm volatile("" : "+v"(rrow));
+      float pv[4] = {0.f, 0.f, 0.f, 0.f};
+      uint32_t arg[4] = {0u, 0u, 0u, 0u};
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const float4 v = *reinterpret_cast<const float4*>(smem + rrow + (4 * (k >> 1) + (k & 1)) * N6);
+        const float xv[4] = {v.x + bias4.x, v.y + bias4.y, v.z + bias4.z, v.w + bias4.w};
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+          const float x = po::leaky_or_id(xv[c], po::act_slope(a.act));
+          if (k == 0 || x > pv[c] || isnan(x)) { pv[c] = x; arg[c] = (uint32_t)k; }
+        }
+      }
+      uint32_t code = 0u;
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        if (a.act) arg[c] |= 8u | (pv[c] > 0.f ? 0u : 4u);
+        code |= arg[c] << (8 * c);
+      }
+      const bool ok = eok[q] & 1u;
+      const uint32_t po = epix[q][0] * (uint32_t)a.Cout_p + n4;      // pooled element (< 2^31: host check)
+      W6ST(bst4(make_float4(pv[0], pv[1], pv[2], pv[3]), rsrc(a.pool_y, pool_bytes), ok ? po * 4u : kOOB));
+      W6ST(bst1(code, rsrc(a.pool_am, pool_bytes >> 2), ok ? po : kOOB));
+      return;
+    }
     int rrow = V6_FLOATS + q * (TP6 * 16 * N6) + (et * 16 + epx) * N6 + n_loc;
     asm volatile("" : "+v"(rrow));
 #pragma unroll
@@ -723,7 +768,10 @@ int launch_wino6(const ConvArgs& a, const float* U6, hipStream_t st, float* VG, 
   PO_REQUIRE(!a.gbox || a.mrows == a.Hg * a.Wg, "po_conv: tile 71 takes gradient-cone boxes on the full grid only");
   PO_REQUIRE(a.Hg == a.Hout && a.Wg == a.Wout && a.Hin == a.Hout && a.Win == a.Wout,
              "po_conv: Winograd tile needs source, grid and destination of one size");
-  PO_REQUIRE(!a.pool_y, "po_conv: tile 71 has no fused pool");
+  PO_REQUIRE(!a.pool_y || (a.pool_am && a.ksplit == 1 && !a.gbox && a.Hout % 2 == 0 && a.Wout % 2 == 0 && !a.y &&
+                           !a.res && !a.accumulate && !a.mbits && !a.y2 && !a.ybits),
+             "po_conv: tile 71 fuses a pool only into a plain full-map forward (even map, no split-K, only the pooled "
+             "outputs)");
   PO_REQUIRE(a.N % N6 == 0 && a.Cin_p % WK == 0, "po_conv: tile 71 needs N %% 64 == 0 and Cin_p %% 16 == 0");
   PO_REQUIRE(a.Cin_p / WK >= 2 * a.ksplit, "po_conv: tile 71 needs at least two k-steps per slice");
   PO_REQUIRE(a.ksplit == 1 || (a.ws && (int64_t)a.ksplit * a.M * a.N * 4 < (1LL << 31)),
@@ -756,15 +804,15 @@ int launch_wino6(const ConvArgs& a, const float* U6, hipStream_t st, float* VG, 
   }
   const uint32_t vg_bytes = VG ? (uint32_t)(vg_need * 4) : 0u;
   const int ef = (a.y ? EF_Y : 0) | (a.res ? EF_RES : 0) | (a.accumulate ? EF_ACC : 0) | (a.mbits ? EF_MB : 0) |
-                 (a.y2 ? EF_Y2 : 0) | (a.ybits ? EF_YB : 0);
+                 (a.y2 ? EF_Y2 : 0) | (a.ybits ? EF_YB : 0) | (a.pool_y ? EF_POOL : 0);
   const void* k = nullptr;
   // the epilogue-field combinations po_conv launches on full-map Winograd tiles
 #define PO_W6(MODE, EF)                                                                              \
-  case (MODE) * 64 + (EF):                                                                           \
+  case (MODE) * 128 + (EF):                                                                          \
     k = VG ? reinterpret_cast<const void*>(conv_wino6_k<MODE, EF, true>)                            \
            : reinterpret_cast<const void*>(conv_wino6_k<MODE, EF, false>);                          \
     break;
-  const int which = a.ksplit > 1 ? 64 : ef;
+  const int which = a.ksplit > 1 ? 128 : ef;
   switch (which) {
     PO_W6(1, 0)
     PO_W6(0, EF_Y)
@@ -779,6 +827,7 @@ int launch_wino6(const ConvArgs& a, const float* U6, hipStream_t st, float* VG, 
     PO_W6(0, EF_Y | EF_ACC | EF_Y2)
     PO_W6(0, EF_Y | EF_MB | EF_Y2)
     PO_W6(0, EF_Y | EF_ACC | EF_MB | EF_Y2)
+    PO_W6(0, EF_POOL)
     default:
       break;
   }

@@ -92,5 +92,6 @@ constexpr int EF_ACC = 4;    // load the destination, accumulate
 constexpr int EF_MB = 8;     // load the leaky-mask sign-bit word, multiply
 constexpr int EF_Y2 = 16;    // load the second mask word, store the dual output
 constexpr int EF_YB = 32;    // store the output's sign bits
+constexpr int EF_POOL = 64;  // tile 71/72: the 2x2/2 max pool fused, only the pooled values and argmax bytes stored
 
 }  // namespace

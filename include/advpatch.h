@@ -501,8 +501,8 @@ typedef struct po_conv_desc {
    * (staging 0/1). */
   int mrows;
   /* Optional fused k=2 stride-2 max pool of a plain forward conv (y_out NULL,
-   * full even grid, no split-K; generic tiles, or Winograd tiles 61/66/67/68
-   * without gbox -- their 2x2 output tiles are the windows): pool_y [B,Hout/2,Wout/2,Cout_p]
+   * full even grid, no split-K; generic tiles, or Winograd tiles 61/66/67/68/70/71/72/73
+   * without gbox -- the windows lie inside their output tiles): pool_y [B,Hout/2,Wout/2,Cout_p]
    * and pool_argmax (int8, same shape) as po_maxpool2_fwd writes them, the
    * argmax bytes of a leaky conv also carrying its LeakyReLU slope (bit 3
    * set, bit 2 = max <= 0; see po_conv_first_pool_fwd); the conv output
@@ -567,7 +567,9 @@ typedef struct po_conv_desc {
  * bit-identical to 68.
  * 71 (exact fp32, ABI 23) is the Winograd F(4x4,3x3) form of tile 70 (needs
  * Wwino6): 32 4x4-tiles x 64 channels per unit, one 512-thread workgroup per
- * CU walking the units; the same requirements as tile 70 and no fused pool.
+ * CU walking the units; the same requirements as tile 70; since round 6 (no
+ * ABI change) also the fused pool (pool_y on a plain full-map forward, even
+ * map, no split-K: each 4x4 tile's four windows pooled in the epilogue).
  * Not bit-identical to the F(2x2) tiles (a different exact-arithmetic
  * factorisation); its error against float64 is tested per layer.
  * 72 (exact fp32, ABI 24) is tile 71 with its input transform as a separate

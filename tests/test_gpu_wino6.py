@@ -299,3 +299,49 @@ def test_tile71_refuses_what_it_cannot_run():
     d = _desc(nat, 2, 16, 32, 32, 71)                      # N = 32: not a multiple of 64
     d.Wwino6 = U6.data_ptr()
     assert call(d) != 0
+
+
+@pytest.mark.parametrize("tile", [71, 72])
+@pytest.mark.parametrize("act", [0, 1])
+@pytest.mark.parametrize("B,H,Cin,Cout,flip", [(2, 104, 32, 64, False), (2, 52, 64, 128, False), (3, 18, 32, 64, True),
+                                               (2, 10, 64, 128, False)])
+def test_tile71_fused_pool(tile, act, B, H, Cin, Cout, flip):
+    """Tiles 71/72 with the 2x2/2 max pool in the epilogue (EF_POOL, round 6):
+    pooled values, window positions and slope codes bit-identical to pooling
+    tile 71's own unpooled output by po_maxpool2_fwd's rule (first position on
+    ties, NaN wins); map sides that end in half a 4x4 tile (18, 10) included."""
+    nat = pkg_mod("_native")
+    dk = pkg_mod("darknet_v3")
+    x, w, bias, wd, U = _setup(B, H, Cin, Cout, flip, seed=H + Cout + act)
+    U6 = _u6(wd, flip)
+    xd = x.permute(0, 2, 3, 1).contiguous().to(DEV)
+    bd = bias.to(DEV)
+    y = torch.full((B, H, H, Cout), float("nan"), device=DEV)
+    d = _desc(nat, B, H, Cin, Cout, 71, flip)
+    d.Wwino, d.Wwino6, d.act = U.data_ptr(), U6.data_ptr(), act
+    nat.call("po_conv", ctypes.byref(d), nat.ptr(xd), nat.ptr(wd), nat.ptr(bd), nat.ptr(y), None, None, None, None,
+             None, nat.stream())
+    h = H // 2
+    py = torch.full((B, h, h, Cout), float("nan"), device=DEV)
+    pam = torch.full((B, h, h, Cout), -1, dtype=torch.int8, device=DEV)
+    d = _desc(nat, B, H, Cin, Cout, tile, flip)
+    d.Wwino, d.Wwino6, d.act = U.data_ptr(), U6.data_ptr(), act
+    d.pool_y, d.pool_argmax = py.data_ptr(), pam.data_ptr()
+    winov = None
+    if tile == 72:
+        nv = dk.NetPlan.winov_floats(d)
+        winov = torch.empty(nv, device=DEV)
+        d.winov, d.winov_floats = winov.data_ptr(), nv
+    nat.call("po_conv", ctypes.byref(d), nat.ptr(xd), nat.ptr(wd), nat.ptr(bd), None, None, None, None, None, None,
+             nat.stream())
+    torch.cuda.synchronize()
+    win = y.view(B, h, 2, h, 2, Cout)
+    pv, arg = win[:, :, 0, :, 0], torch.zeros(B, h, h, Cout, dtype=torch.int64, device=DEV)
+    for k in range(1, 4):
+        v = win[:, :, k >> 1, :, k & 1]
+        upd = (v > pv) | torch.isnan(v)
+        pv, arg = torch.where(upd, v, pv), torch.where(upd, torch.full_like(arg, k), arg)
+    if act:
+        arg = arg | 8 | torch.where(pv > 0, 0, 4)
+    assert torch.equal(py.view(torch.int32), pv.view(torch.int32))
+    assert torch.equal(pam.long(), arg)
