@@ -960,6 +960,20 @@ class DevicePrefetcher:
 
 
 
+def loader_context(device):
+    """multiprocessing context of the DataLoader workers: "spawn" when the
+    device is a GPU (the parent has initialised HIP and runs its threads: a
+    forked worker can inherit a lock one of them held and hang -- seen once on
+    an MI355X box with two workers), else the platform default.
+    ADVPATCH_LOADER_MP=fork|spawn|forkserver overrides.  Spawned workers
+    re-import the package, not the caller's code (a script's training loop
+    belongs under ``if __name__ == "__main__":``, as with any spawn loader)."""
+    ctx = os.environ.get("ADVPATCH_LOADER_MP")
+    if ctx is None:
+        ctx = "spawn" if torch.device(device).type == "cuda" else None
+    return ctx
+
+
 class FrameCache:
     """Decoded training frames resident in device memory.  DotaDataset's
     transform (PNG decode, grey pad, bilinear resize, label padding;
@@ -980,7 +994,8 @@ class FrameCache:
         self.frames = torch.empty(n, 3, S, S, dtype=torch.uint8, device=self.device)
         self.labels = torch.empty(n, L, 5, dtype=torch.float32, device=self.device)
         dl = torch.utils.data.DataLoader(ds, batch_size=batch, shuffle=False, num_workers=num_workers,
-                                         pin_memory=self.device.type == "cuda")
+                                         pin_memory=self.device.type == "cuda",
+                                         multiprocessing_context=loader_context(self.device) if num_workers else None)
         k = 0
         for img, lab in dl:
             m = img.size(0)

@@ -50,7 +50,8 @@ from . import synthetic
 from . import weights as synth_weights
 from .darknet_v3 import Darknet
 from .load_data import (DevicePrefetcher, DotaCollate, DotaDataset, FrameCache, HasSusRGB, NPSCalculator, PatchApplier,
-                        PatchTransformer, TotalVariation, patch_front, read_image as _read_image, regularisers)
+                        PatchTransformer, TotalVariation, loader_context, patch_front, read_image as _read_image,
+                        regularisers)
 
 TV_FACTOR = 2.5      # train_patch.py:25
 NPS_FACTOR = 0.01    # train_patch.py:26
@@ -495,7 +496,8 @@ class PatchTrainer(object):
             else:
                 loader = DevicePrefetcher(torch.utils.data.DataLoader(
                     ds, batch_sampler=sampler, num_workers=num_workers, pin_memory=True,
-                    persistent_workers=num_workers > 0, collate_fn=collate), self.device)
+                    persistent_workers=num_workers > 0, collate_fn=collate,
+                    multiprocessing_context=loader_context(self.device) if num_workers else None), self.device)
         else:
             loader = DevicePrefetcher(data, self.device)
         optimizer = self.make_optimizer(adv_patch)
