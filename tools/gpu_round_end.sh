@@ -14,8 +14,13 @@ mkdir -p "$OUT"
 for stage in "$@"; do
   case $stage in
     suite)
+      # heartbeat: a test that runs for minutes writes nothing to suite.log until it ends
+      (while sleep 30; do date +%T >> "$OUT/heartbeat"; done) & HB=$!
       timeout -k 10 1080 python -u -m pytest tests -m gpu -x -v --timeout 900 --timeout-method thread \
-          > "$OUT/suite.log" 2>&1 || { echo "suite failed"; grep -E "FAILED|Error" "$OUT/suite.log" | tail -20; exit 1; }
+          > "$OUT/suite.log" 2>&1
+      rc=$?
+      kill $HB
+      [ $rc -eq 0 ] || { echo "suite failed"; grep -E "FAILED|Error" "$OUT/suite.log" | tail -20; exit 1; }
       tail -1 "$OUT/suite.log" ;;
     parity)
       timeout -k 10 600 python -u -m pytest tests/test_gpu_step.py tests/test_gpu_train.py -m gpu -x -v -s \
