@@ -294,8 +294,13 @@ def test_tile71_refuses_what_it_cannot_run():
     py = torch.zeros(B, H // 2, H // 2, Cout, device=DEV)
     pam = torch.zeros(B, H // 2, H // 2, Cout, dtype=torch.int8, device=DEV)
     d.pool_y, d.pool_argmax = py.data_ptr(), pam.data_ptr()
+    # the fused pool runs since round 6 (test_tile71_fused_pool), on full maps only
+    assert nat.load().po_conv(ctypes.byref(d), nat.ptr(xd), nat.ptr(wd), None, None, None, None, None, None, None,
+                              nat.stream()) == 0
+    d.gbox = box.data_ptr()
     assert nat.load().po_conv(ctypes.byref(d), nat.ptr(xd), nat.ptr(wd), None, None, None, None, None, None, None,
                               nat.stream()) != 0
+    d.gbox = None
     d = _desc(nat, 2, 16, 32, 32, 71)                      # N = 32: not a multiple of 64
     d.Wwino6 = U6.data_ptr()
     assert call(d) != 0
