@@ -57,6 +57,8 @@ __device__ __forceinline__ int wp_chan(int p) {
   return 2 * s + 8 * (g & 1) + (g >> 1);
 }
 
+// AMAX: the launch keeps max|pooled value| (ConvArgs.y_amax; fp16x3 consumers only)
+template <bool AMAX>
 __global__ __launch_bounds__(256, 2) void conv_wpool_k(const ConvArgs a, const float* __restrict__ U, int tiles_r,
                                                        int tiles_c, int ntiles, int xr) {
   __shared__ __attribute__((aligned(16))) float smem[QPATCH + QV];
@@ -139,6 +141,12 @@ __global__ __launch_bounds__(256, 2) void conv_wpool_k(const ConvArgs a, const f
 
   float my = 0.f;
   const float slope = po::act_slope(a.act);
+  const f2v slope2 = {slope, slope}, bias2 = {bias_n, bias_n};
+  const bool act = a.act != 0;
+  // pooled outputs [B][Hp][Wp][32] floats and argmax bytes (< 2 GiB, host check)
+  const uint32_t pool_elems = (uint32_t)(a.B * Hp * Wp) * 32u;
+  const __amdgpu_buffer_rsrc_t py_rs = rsrc(a.pool_y, 4u * pool_elems);
+  const __amdgpu_buffer_rsrc_t pa_rs = rsrc(a.pool_am, pool_elems);
   int tile = xr ? po::xcd_remap() : (int)blockIdx.x;
   if (tile < ntiles) gload(tile);
   while (tile < ntiles) {
@@ -159,43 +167,61 @@ __global__ __launch_bounds__(256, 2) void conv_wpool_k(const ConvArgs a, const f
       acc[xi] = __builtin_amdgcn_mfma_f32_16x16x4f32(av.w, u[xi][3], acc[xi], 0, 0, 0);
     }
     // epilogue in registers: lane (g, n) holds all components of Winograd tiles
-    // 16 th + 4g + e (e = 0..3) for output channel n
+    // 16 th + 4g + e (e = 0..3) for output channel n.  Tiles e = 2ep, 2ep + 1
+    // (pool windows px, px + 1 of one row) sit in adjacent accumulator
+    // registers, so A^T M A, the bias and the slope product run on the pair
+    // (v_pk_add_f32 / v_pk_mul_f32: tile 61's operations per element, in its order)
     const int tc = tile % tiles_c, rest = tile / tiles_c;
     const int tr = rest % tiles_r, b = rest / tiles_r;
+    // the lane's pooled pixels: row py, columns px0 + j (j = 2ep + hh), channel n;
+    // a dead pixel's offset lies past the buffers (the store is dropped), and
+    // the j steps ride in the stores' immediate offsets
+    const int py = 4 * tr + 2 * th + (g >> 1), px0 = 8 * tc + 4 * (g & 1);
+    const uint32_t base = (((uint32_t)b * Hp + py) * Wp + px0) * 32u + n;
+    uint32_t vo[4], vo4[4];
 #pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      const int t = 16 * th + 4 * g + e;
-      float m[16];
+    for (int j = 0; j < 4; ++j) {
+      const bool live = py < Hp && px0 + j < Wp;
+      vo[j] = live ? base : kOOB;
+      vo4[j] = live ? 4u * base : kOOB;
+    }
 #pragma unroll
-      for (int xi = 0; xi < 16; ++xi) m[xi] = acc[xi][e];
-      float s0[4], s1[4];                       // A^T m A, A^T = [[1,1,1,0],[0,1,-1,-1]] (tile 61)
+    for (int ep = 0; ep < 2; ++ep) {
+      f2v m[16];
+#pragma unroll
+      for (int xi = 0; xi < 16; ++xi) m[xi] = f2v{acc[xi][2 * ep], acc[xi][2 * ep + 1]};
+      f2v s0[4], s1[4];                         // A^T m A, A^T = [[1,1,1,0],[0,1,-1,-1]] (tile 61)
 #pragma unroll
       for (int v = 0; v < 4; ++v) {
         s0[v] = m[0 * 4 + v] + m[1 * 4 + v] + m[2 * 4 + v];
         s1[v] = m[1 * 4 + v] - m[2 * 4 + v] - m[3 * 4 + v];
       }
-      const float yv[4] = {s0[0] + s0[1] + s0[2], s0[1] - s0[2] - s0[3], s1[0] + s1[1] + s1[2],
-                           s1[1] - s1[2] - s1[3]};
-      float pv = 0.f;
-      uint32_t arg = 0u;
+      f2v x[4] = {s0[0] + s0[1] + s0[2], s0[1] - s0[2] - s0[3], s1[0] + s1[1] + s1[2], s1[1] - s1[2] - s1[3]};
+      f2v xs[4];
 #pragma unroll
       for (int k = 0; k < 4; ++k) {
-        float x = yv[k] + bias_n;
-        x = po::leaky_or_id(x, slope);
-        if (k == 0 || x > pv || isnan(x)) { pv = x; arg = (uint32_t)k; }
+        x[k] = x[k] + bias2;
+        xs[k] = x[k] * slope2;                  // leaky_or_id(x) = maximum(x, x * slope)
       }
-      if (a.act) arg |= 8u | (pv > 0.f ? 0u : 4u);
-      const int py = 4 * tr + (t >> 3), px = 8 * tc + (t & 7);
-      if (py < Hp && px < Wp && n < a.N) {
-        const size_t po = (((size_t)b * Hp + py) * Wp + px) * a.Cout_p + n;
-        a.pool_y[po] = pv;
-        a.pool_am[po] = (int8_t)arg;
-        my = fmaxf(my, fabsf(pv));
+#pragma unroll
+      for (int hh = 0; hh < 2; ++hh) {
+        const int j = 2 * ep + hh;
+        float pv = 0.f;
+        uint32_t arg = 0u;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          const float xv = __builtin_elementwise_maximum(x[k][hh], xs[k][hh]);
+          if (k == 0 || xv > pv || isnan(xv)) { pv = xv; arg = (uint32_t)k; }
+        }
+        if (act) arg |= 8u | (pv > 0.f ? 0u : 4u);
+        __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, pv), py_rs, vo4[j], 128 * j, 0);
+        __builtin_amdgcn_raw_buffer_store_b8((uint8_t)arg, pa_rs, vo[j], 32 * j, 0);
+        if constexpr (AMAX) my = fmaxf(my, vo[j] != kOOB ? fabsf(pv) : 0.f);
       }
     }
     tile = next;
   }
-  if (a.y_amax) po::amax_commit(a.y_amax, my);
+  if constexpr (AMAX) po::amax_commit(a.y_amax, my);
 }
 }  // namespace
 
@@ -214,13 +240,20 @@ int launch_wpool(const ConvArgs& a, const float* U, hipStream_t st) {
   const int tiles_r = ceil_div(a.Hout, QR), tiles_c = ceil_div(a.Wout, QC);
   const int64_t ntiles = (int64_t)a.B * tiles_r * tiles_c;
   PO_REQUIRE(ntiles < (1LL << 31), "po_conv: tile 73: too many tiles");
-  const int resident = resident_groups_cached(reinterpret_cast<const void*>(conv_wpool_k), 256);
+  PO_REQUIRE((int64_t)a.B * (a.Hout / 2) * (a.Wout / 2) * 32 * 4 < (1LL << 31),
+             "po_conv: tile 73: pooled output must be < 2 GiB");
+  const bool amax = a.y_amax != nullptr;
+  const void* fn = amax ? reinterpret_cast<const void*>(conv_wpool_k<true>) : reinterpret_cast<const void*>(conv_wpool_k<false>);
+  const int resident = resident_groups_cached(fn, 256);
   const int grid = (int)(ntiles < resident ? ntiles : resident);
   static const int xr = [] {
     const char* e = getenv("ADVPATCH_HALO_XCD");
     return (e && e[0] == '0') ? 0 : 1;
   }();
-  hipLaunchKernelGGL(conv_wpool_k, dim3(grid), dim3(256), 0, st, a, U, tiles_r, tiles_c, (int)ntiles, xr);
+  if (amax)
+    hipLaunchKernelGGL(conv_wpool_k<true>, dim3(grid), dim3(256), 0, st, a, U, tiles_r, tiles_c, (int)ntiles, xr);
+  else
+    hipLaunchKernelGGL(conv_wpool_k<false>, dim3(grid), dim3(256), 0, st, a, U, tiles_r, tiles_c, (int)ntiles, xr);
   return check_launch("po_conv (Winograd pool tile)");
 }
 }  // namespace po
