@@ -223,9 +223,14 @@ __device__ __forceinline__ void pool_conv_px(const float (&xa)[3][4][4], const f
       }
 #pragma unroll
       for (int i = 0; i < 4; ++i) {                  // V = t B (columns combined)
-        const float a0 = t[i][0][0], a1 = t[i][0][1], a2 = t[i][1][0], a3 = t[i][1][1];
-        vw[c][2 * i] = (f2_t){a0 - a2, a1 + a2};
-        vw[c][2 * i + 1] = (f2_t){a2 - a1, a1 - a3};
+        // (a0, a1) = t[i][0], (a2, a3) = t[i][1]: {a0 - a2, a1 + a2} and
+        // {a2 - a1, a1 - a3}, one v_pk_add_f32 each through its operand-select
+        // and negate modifiers (x - y is x + (-y), and IEEE addition commutes:
+        // the same values bit for bit)
+        asm("v_pk_add_f32 %0, %1, %2 op_sel:[0,0] op_sel_hi:[1,0] neg_lo:[0,1] neg_hi:[0,0]"
+            : "=v"(vw[c][2 * i]) : "v"(t[i][0]), "v"(t[i][1]));
+        asm("v_pk_add_f32 %0, %1, %2 op_sel:[1,0] op_sel_hi:[1,1] neg_lo:[1,0] neg_hi:[0,1]"
+            : "=v"(vw[c][2 * i + 1]) : "v"(t[i][0]), "v"(t[i][1]));
       }
     }
   } else {
@@ -251,10 +256,13 @@ __device__ __forceinline__ void pool_conv_px(const float (&xa)[3][4][4], const f
         // enters through M[1][1] (element 5), which A^T M A adds to all four
         // outputs once
         const f2_t* U2 = reinterpret_cast<const f2_t*>(Wt) + co * 24;
+        // {0, bias}: one v_pk_mov_b32 from the scalar bias (two moves otherwise)
+        f2_t binit;
+        asm("v_pk_mov_b32 %0, 0, %1 op_sel:[0,0]" : "=v"(binit) : "s"((uint64_t)__builtin_bit_cast(uint32_t, bco)));
         f2_t m[8];
 #pragma unroll
         for (int k = 0; k < 8; ++k) {
-          const f2_t init = k == 2 ? (f2_t){0.f, bco} : (f2_t){0.f, 0.f};
+          const f2_t init = k == 2 ? binit : (f2_t){0.f, 0.f};
           f2_t acc = __builtin_elementwise_fma(U2[k], vw[0][k], init);
           acc = __builtin_elementwise_fma(U2[8 + k], vw[1][k], acc);
           m[k] = __builtin_elementwise_fma(U2[16 + k], vw[2][k], acc);
@@ -428,7 +436,7 @@ __global__ __launch_bounds__(256) void first_pool_fwd_k(const float* __restrict_
 // first_pool_fwd_k).  Same arithmetic per pixel as first_pool_fwd_k
 // (pool_conv_px), so the outputs are bit-identical to it; the LDS window
 // aliases the output staging (a barrier between).
-template <int CO, bool WINO>
+template <int CO, bool WINO, bool ACT>
 __global__ __launch_bounds__(256) void first_pool_tile_k(const float* __restrict__ img, int B, int H, int W,
                                                          int Hp, int Wp, int tiles_x, int tiles_y,
                                                          const float* __restrict__ Wt,
@@ -501,7 +509,7 @@ __global__ __launch_bounds__(256) void first_pool_tile_k(const float* __restrict
   __syncthreads();                                  // ys aliases the window
   float vmax;
   uint32_t aw[CO / 4];
-  pool_conv_px<CO, WINO>(xa, Wt, bias, Cout, act, ys + tid * LS, aw, vmax);
+  pool_conv_px<CO, WINO>(xa, Wt, bias, Cout, ACT ? 1 : 0, ys + tid * LS, aw, vmax);   // act == ACT (host)
   if (amax) {                                       // fp16x3 plans only: no VALU spent on it otherwise
 #pragma unroll
     for (int co = 0; co < CO; ++co) vmax = fmaxf(vmax, fabsf(ys[tid * LS + co]));
@@ -661,13 +669,16 @@ int first_pool_fwd(const float* img, const float* pimg, const int32_t* roi, int 
     const int tx = (Wp + 15) / 16, ty = (Hp + 15) / 16;
     PO_REQUIRE((int64_t)B * tx * ty < (1LL << 31), "po_conv_first_pool_fwd: too many tiles");
     dim3 gt((unsigned)(B * tx * ty));
-#define PO_FPT(CO_, WI_)                                                                                    \
-  hipLaunchKernelGGL((first_pool_tile_k<CO_, WI_>), gt, dim3(256), 0, st, img, B, H, W, Hp, Wp, tx, ty, Wt, bias, \
-                     Cout, act, y, argmax, amax, pimg, roi, xr, nt)
+#define PO_FPT(CO_, WI_, AC_)                                                                                   \
+  hipLaunchKernelGGL((first_pool_tile_k<CO_, WI_, AC_>), gt, dim3(256), 0, st, img, B, H, W, Hp, Wp, tx, ty, Wt,     \
+                     bias, Cout, act, y, argmax, amax, pimg, roi, xr, nt)
+    // the activation as a template argument: no per-channel selects between the two forms
     if (Cout_p == 16) {
-      if (wino) PO_FPT(16, true); else PO_FPT(16, false);
+      if (wino) { if (act) PO_FPT(16, true, true); else PO_FPT(16, true, false); }
+      else { if (act) PO_FPT(16, false, true); else PO_FPT(16, false, false); }
     } else {
-      if (wino) PO_FPT(32, true); else PO_FPT(32, false);
+      if (wino) { if (act) PO_FPT(32, true, true); else PO_FPT(32, true, false); }
+      else { if (act) PO_FPT(32, false, true); else PO_FPT(32, false, false); }
     }
 #undef PO_FPT
     return po::check_launch("po_conv_first_pool_fwd");

@@ -1,6 +1,9 @@
 """Time the first layer (po_conv_first_fwd / po_conv_first_pool_fwd / _wino_fwd) on the
 bench shapes: yolov3 B=16 @608 3->32 and yolov3-tiny B=256 @416 3->16 + pool.
-usage: [MICRO_LIB=...] [FIRST_ONLY=False|True|wino] python tools/first_micro.py [iters]"""
+usage: [MICRO_LIB=...] [FIRST_ONLY=False|True|wino] python tools/first_micro.py [iters]
+Seeded inputs; each line ends with a hash of the outputs (pooled values and argmax bytes), so
+two libraries' lines compare bit for bit."""
+import hashlib
 import os
 import sys
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
@@ -11,6 +14,7 @@ if os.environ.get("MICRO_LIB"):
     nat.LIB_PATH = os.environ["MICRO_LIB"]
 iters = int(sys.argv[1]) if len(sys.argv) > 1 else 20
 dev = torch.device("cuda", 0)
+torch.manual_seed(0)
 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
 first_wino_u = ge._pkg("darknet_v3").first_wino_u
 for B, S, co, pool in ((16, 608, 32, False), (256, 416, 16, True), (256, 416, 16, "wino")):
@@ -42,4 +46,8 @@ for B, S, co, pool in ((16, 608, 32, False), (256, 416, 16, True), (256, 416, 16
     e1.record()
     torch.cuda.synchronize()
     us = 1000.0 * e0.elapsed_time(e1) / iters
-    print("B=%d S=%d 3->%d%s: %.1f us  %.2f TB/s" % (B, S, co, {False: "", True: " + pool"}.get(pool, " + pool (F(2x2))"), us, byts / us / 1e6))
+    h = hashlib.sha1(y.cpu().numpy().tobytes())
+    if pool:
+        h.update(am.cpu().numpy().tobytes())
+    print("B=%d S=%d 3->%d%s: %.1f us  %.2f TB/s  out %s" % (B, S, co, {False: "", True: " + pool"}.get(pool, " + pool (F(2x2))"),
+                                                      us, byts / us / 1e6, h.hexdigest()[:12]))
