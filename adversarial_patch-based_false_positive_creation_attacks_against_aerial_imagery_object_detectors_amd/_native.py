@@ -13,8 +13,9 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("ADVPATCH_LIB") or os.path.join(_HERE, "libadvpatch_hip.so")
 
 c_int, c_float, c_int64, c_void_p = ctypes.c_int, ctypes.c_float, ctypes.c_int64, ctypes.c_void_p
+c_double = ctypes.c_double
 
-PO_ABI_VERSION = 29   # include/advpatch.h
+PO_ABI_VERSION = 30   # include/advpatch.h
 PO_CONV_NTILES = 73   # include/advpatch.h
 PO_AMAX_SUB = 64      # sub-slots per max|x| slot
 
@@ -47,6 +48,8 @@ _SIGS = {
                  c_void_p, c_void_p, c_void_p],
     "po_check_finite": [c_void_p, c_int64, c_int, c_void_p, c_void_p],
     "po_check_finite_inf": [c_void_p, c_int64, c_int, c_void_p, c_void_p, c_void_p],
+    "po_adam_amsgrad": [c_void_p] * 5 + [c_int64, c_void_p, c_void_p] + [c_double] * 4 +
+                       [c_void_p, c_void_p, c_int, c_int, c_float, c_float, c_void_p],
     "po_loss_combine": [c_void_p, c_void_p, c_float, c_float, c_float, c_int, c_int, c_void_p, c_void_p, c_void_p],
     "po_loss_combine_bwd": [c_void_p, c_void_p, c_float, c_float, c_float, c_int, c_int, c_void_p, c_void_p,
                             c_void_p],

@@ -72,7 +72,65 @@ __global__ void found_inf_k(const int32_t* __restrict__ flags, int32_t bit, floa
   *found_inf = (*flags & bit) ? 1.f : 0.f;
 }
 
+// Adam(amsgrad) + clamp, one thread per element, in torch.optim.Adam's
+// single-tensor order (torch/optim/adam.py, the reference's CPU arithmetic):
+// exp_avg.lerp_(g, 1 - beta1) (ATen's vectorised lerp: fma(w, g - m, m)),
+// exp_avg_sq.mul_(beta2).addcmul_(g, g, value=1 - beta2), torch.maximum into
+// max_exp_avg_sq, denom = sqrt(max) / sqrt(1 - beta2^t) + eps, param +=
+// (-lr / (1 - beta1^t)) * exp_avg / denom, then clamp_(lo, hi) (NaN kept).
+// The scalars are formed in float64 from the step count t = step_in + 1, as
+// the Python floats of the reference; a raised found_inf / flag bit skips the
+// update and leaves the count (PyTorch's fused-Adam found_inf contract).
+// step_out != step_in (the caller alternates two counters): no block reads a
+// count another block writes.
+__global__ __launch_bounds__(256) void adam_amsgrad_k(float* __restrict__ p, const float* __restrict__ g,
+                                                      float* __restrict__ m, float* __restrict__ v,
+                                                      float* __restrict__ vmax, int64_t n,
+                                                      const float* __restrict__ step_in, float* __restrict__ step_out,
+                                                      double lr, double beta1, double beta2, float w1, float b2,
+                                                      float w2, float eps, const float* __restrict__ found_inf,
+                                                      const int32_t* __restrict__ flags, int32_t bit, int clamp,
+                                                      float lo, float hi) {
+  const bool skip = (found_inf && *found_inf != 0.f) || (flags && (*flags & bit));
+  const float s0 = *step_in;
+  if (blockIdx.x == 0 && threadIdx.x == 0) *step_out = skip ? s0 : s0 + 1.f;
+  if (skip) return;
+  const double t = (double)(s0 + 1.f);
+  const float neg_step = (float)(-(lr / (1.0 - pow(beta1, t))));
+  const float bc2s = (float)sqrt(1.0 - pow(beta2, t));
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
+    const float gi = g[i];
+    const float mi = __builtin_fmaf(w1, gi - m[i], m[i]);
+    float vi = v[i] * b2;
+    vi = vi + (w2 * gi) * gi;
+    const float vm = __builtin_elementwise_maximum(vmax[i], vi);
+    const float denom = sqrtf(vm) / bc2s + eps;
+    float pi = p[i] + (neg_step * mi) / denom;
+    if (clamp && !isnan(pi)) pi = fminf(fmaxf(pi, lo), hi);
+    m[i] = mi;
+    v[i] = vi;
+    vmax[i] = vm;
+    p[i] = pi;
+  }
+}
+
 }  // namespace
+
+extern "C" int po_adam_amsgrad(float* param, const float* grad, float* exp_avg, float* exp_avg_sq,
+                               float* max_exp_avg_sq, int64_t n, const float* step_in, float* step_out, double lr,
+                               double beta1, double beta2, double eps, const float* found_inf,
+                               const int32_t* flags, int32_t bit, int clamp, float lo, float hi, po_stream_t s) {
+  PO_REQUIRE(param && grad && exp_avg && exp_avg_sq && max_exp_avg_sq && step_in && step_out && n >= 0,
+             "po_adam_amsgrad: null pointer");
+  PO_REQUIRE(step_in != step_out, "po_adam_amsgrad: step_in and step_out must differ");
+  PO_REQUIRE(beta1 >= 0.0 && beta1 < 1.0 && beta2 >= 0.0 && beta2 < 1.0 && eps >= 0.0,
+             "po_adam_amsgrad: bad hyper-parameters");
+  const int grid = (int)std::max<int64_t>(1, std::min<int64_t>(po::ceil_div(n, 256), 2048));
+  hipLaunchKernelGGL(adam_amsgrad_k, dim3(grid), dim3(256), 0, po::stream_of(s), param, grad, exp_avg, exp_avg_sq,
+                     max_exp_avg_sq, n, step_in, step_out, lr, beta1, beta2, (float)(1.0 - beta1), (float)beta2,
+                     (float)(1.0 - beta2), (float)eps, found_inf, flags, bit, clamp, lo, hi);
+  return po::check_launch("po_adam_amsgrad");
+}
 
 extern "C" int po_draws(uint64_t seed, uint64_t counter, int b0, int B, int P, float* contrast, float* bright,
                         float* noise, float* angle, float* ux, float* uy, po_stream_t s) {

@@ -282,6 +282,75 @@ class GlobalBatchSampler(torch.utils.data.Sampler):
             yield perm[k * self.G + lo:k * self.G + hi]
 
 
+class PatchAdam(optim.Optimizer):
+    """Adam(amsgrad) + the patch clamp as one HIP launch per step
+    (po_adam_amsgrad; train_patch.py:131-136 builds the reference's
+    torch.optim.Adam(amsgrad=True), :327-330 clamps after each step).  The
+    update is torch's single-tensor Adam arithmetic (include/advpatch.h);
+    PyTorch's fused Adam instead costs three multi-tensor launches plus the
+    clamp, ~75 us per step on these 150k-element patches, for a 5 MB update.
+    The state is torch's (``step``, ``exp_avg``, ``exp_avg_sq``,
+    ``max_exp_avg_sq``; ``step`` a 0-dim float32 on the device, as under
+    fused=True), so state_dicts move between the two and ReduceLROnPlateau
+    drives ``lr`` as for torch's Adam.  ``found_inf`` (a device float) or
+    ``skip_flags`` ((flag tensor, bit)) skips the update on the device, with
+    the count unchanged.  CUDA float32 contiguous parameters only: there is no
+    CPU path (use torch.optim.Adam there)."""
+
+    clamps = True     # the trainer skips its own clamp_
+
+    def __init__(self, params, lr=1e-3, betas=(0.9, 0.999), eps=1e-8, clamp=(0.0, 1.0)):
+        defaults = dict(lr=lr, betas=betas, eps=eps, weight_decay=0, amsgrad=True, maximize=False, foreach=None,
+                        capturable=False, differentiable=False, fused=True)
+        super().__init__(params, defaults)
+        self.clamp = clamp
+        self.found_inf = None
+        self.skip_flags = None
+        self._spare = {}
+
+    def load_state_dict(self, state_dict):
+        """torch's, then every ``step`` count onto its parameter's device as a
+        0-dim float32 (a CPU Adam's state keeps it on the host)."""
+        super().load_state_dict(state_dict)
+        for p, st in self.state.items():
+            if "step" in st:
+                st["step"] = torch.as_tensor(st["step"]).to(device=p.device, dtype=torch.float32).reshape(())
+            self._spare.pop(p, None)
+
+    @torch.no_grad()
+    def step(self, closure=None):
+        loss = None
+        if closure is not None:
+            with torch.enable_grad():
+                loss = closure()
+        for group in self.param_groups:
+            beta1, beta2 = group["betas"]
+            for p in group["params"]:
+                if p.grad is None:
+                    continue
+                if not (p.is_cuda and p.dtype == torch.float32 and p.is_contiguous() and p.grad.is_contiguous()):
+                    raise RuntimeError("PatchAdam: CUDA float32 contiguous parameters and gradients only")
+                st = self.state[p]
+                if len(st) == 0:
+                    st["step"] = torch.zeros((), dtype=torch.float32, device=p.device)
+                    for k in ("exp_avg", "exp_avg_sq", "max_exp_avg_sq"):
+                        st[k] = torch.zeros_like(p, memory_format=torch.contiguous_format)
+                spare = self._spare.get(p)
+                if spare is None or spare.device != p.device or spare is st["step"]:
+                    spare = torch.empty((), dtype=torch.float32, device=p.device)
+                flags, bit = self.skip_flags if self.skip_flags is not None else (None, 0)
+                lo, hi = self.clamp if self.clamp is not None else (0.0, 0.0)
+                nat.call("po_adam_amsgrad", nat.ptr(p), nat.ptr(p.grad), nat.ptr(st["exp_avg"]),
+                         nat.ptr(st["exp_avg_sq"]), nat.ptr(st["max_exp_avg_sq"]), p.numel(), nat.ptr(st["step"]),
+                         nat.ptr(spare), float(group["lr"]), float(beta1), float(beta2), float(group["eps"]),
+                         nat.ptr(self.found_inf) if self.found_inf is not None else None,
+                         nat.ptr(flags, torch.int32) if flags is not None else None, int(bit),
+                         int(self.clamp is not None), float(lo), float(hi), nat.stream())
+                self._spare[p] = st["step"]
+                st["step"] = spare
+        return loss
+
+
 class PatchTrainer(object):
     """train_patch.py:48-577"""
 
@@ -415,7 +484,14 @@ class PatchTrainer(object):
             self._seed = torch.ones((), device=loss.device)                 # dL/dL, allocated once
         loss.backward(self._seed)
         self.allreduce_grad(adv_patch, terms)
-        if self.check_finite:
+        if self.check_finite and isinstance(optimizer, PatchAdam):
+            # after the all-reduce (every rank sees the same gradient, raises the same
+            # bit and skips the same update); PatchAdam reads the flag word itself
+            g = adv_patch.grad
+            nat.call("po_check_finite", nat.ptr(g), g.numel(), FLAG_NONFINITE, nat.ptr(self.flags, torch.int32),
+                     nat.stream())
+            optimizer.skip_flags = (self.flags, FLAG_NONFINITE)
+        elif self.check_finite:
             # after the all-reduce: a NaN/Inf on any rank reaches every rank's reduced
             # gradient, so all ranks raise the same bit and skip the same updates
             g = adv_patch.grad
@@ -432,7 +508,8 @@ class PatchTrainer(object):
                 optimizer.found_inf = self._found_inf
         optimizer.step()
         optimizer.zero_grad()
-        adv_patch.data.clamp_(0, 1)
+        if not getattr(optimizer, "clamps", False):
+            adv_patch.data.clamp_(0, 1)
         return terms
 
     def check_flags(self):
@@ -449,7 +526,12 @@ class PatchTrainer(object):
     def make_optimizer(self, adv_patch):
         """Adam(amsgrad) as the reference (train_patch.py:131-136); on the GPU
         PyTorch's fused single-kernel implementation (same update rule) instead
-        of the multi-launch foreach one."""
+        of the multi-launch foreach one.  north_star keeps the outer Adam step
+        in PyTorch-ROCm, so that is the default; ADVPATCH_HIP_ADAM=1 selects
+        PatchAdam (one po_adam_amsgrad launch, the clamp fused; measured +1 %
+        on config 5, neutral on the headline, profiles/r06/patch_adam_ab.txt)."""
+        if adv_patch.is_cuda and os.environ.get("ADVPATCH_HIP_ADAM") == "1":
+            return PatchAdam([adv_patch], lr=self.config.start_learning_rate)
         return optim.Adam([adv_patch], lr=self.config.start_learning_rate, amsgrad=True,
                           fused=bool(adv_patch.is_cuda) or None)
 

@@ -33,7 +33,7 @@ typedef void* po_stream_t;
 #define PO_EHIP -2     /* HIP runtime error */
 #define PO_EDEVICE -3  /* device is not gfx950 */
 
-#define PO_ABI_VERSION 29
+#define PO_ABI_VERSION 30
 #define PO_AMAX_SUB 64  /* sub-slots per max|x| slot (see po_conv_desc) */
 
 int po_abi_version(void);
@@ -113,6 +113,26 @@ int po_check_finite(const float* x, int64_t n, int32_t bit, int32_t* flags, po_s
  * this or an earlier check, cleared only when the caller clears the flags),
  * so a non-finite step is skipped with no host code (ABI 21). */
 int po_check_finite_inf(const float* x, int64_t n, int32_t bit, int32_t* flags, float* found_inf, po_stream_t s);
+
+/* (ABI 30) Adam(amsgrad) + clamp of one parameter tensor in one launch
+ * (replaces torch.optim.Adam(amsgrad=True).step() + adv_patch.data.clamp_(0, 1),
+ * train_patch.py:131-136, 327-330; weight decay 0, not maximize).  The
+ * arithmetic is torch's single-tensor Adam (the reference's CPU form):
+ * exp_avg = fma(1 - beta1, grad - exp_avg, exp_avg) (ATen's lerp),
+ * exp_avg_sq = exp_avg_sq * beta2 + ((1 - beta2) * grad) * grad,
+ * max_exp_avg_sq = maximum(max_exp_avg_sq, exp_avg_sq) (NaN propagating),
+ * param += (-lr / (1 - beta1^t)) * exp_avg / (sqrt(max_exp_avg_sq) /
+ * sqrt(1 - beta2^t) + eps), the scalars in float64 with t = *step_in + 1,
+ * rounded to fp32 where torch rounds them; then, if clamp, param =
+ * min(max(param, lo), hi) (NaN kept).  *step_out = t, or *step_in when the
+ * update is skipped: found_inf (if not NULL) nonzero or flags[0] & bit (if
+ * flags not NULL) -- the update, the moments and the count then stay as they
+ * were.  step_in and step_out are two different device floats (the caller
+ * alternates them).  n may be 0. */
+int po_adam_amsgrad(float* param, const float* grad, float* exp_avg, float* exp_avg_sq, float* max_exp_avg_sq,
+                    int64_t n, const float* step_in, float* step_out, double lr, double beta1, double beta2,
+                    double eps, const float* found_inf, const int32_t* flags, int32_t bit, int clamp, float lo,
+                    float hi, po_stream_t s);
 
 /* Augment (contrast/brightness/noise/clamp, load_data.py:548-574) + affine
  * bilinear warp of patch and mask (affine_grid + grid_sample, align_corners

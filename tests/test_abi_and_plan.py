@@ -31,7 +31,7 @@ def test_library_exports_every_header_symbol():
     for name in sorted(declared):
         assert hasattr(lib, name), "libadvpatch_hip.so does not export %s" % name
     assert declared == set(nat.symbols()), declared ^ set(nat.symbols())
-    assert lib.po_abi_version() == nat.PO_ABI_VERSION == 29
+    assert lib.po_abi_version() == nat.PO_ABI_VERSION == 30
 
 
 def test_conv_desc_struct_matches_header():
